@@ -1,0 +1,189 @@
+"""Benchmark: DCM-MPC QP solves/sec (batch, horizon 100) on 1..8 MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): per GPU, a batch of 4096 horizon-100 time-varying DCM MPC
+QPs (6-footstep plans, M = 8 facet slots, fp64), inputs resident in HBM.  One step = one
+blf_dcm_mpc_solve over the whole per-GPU batch (every QP solved from a cold start to
+tol_mu 1e-15).  Multi-GPU: one process per GPU (torch.distributed.run), each rank solves its own
+shard of independent problems — no data-path collective (scaling "weak"); the RCCL gather of the
+solutions to rank 0 is timed separately and reported as gather_ms.
+
+Prints ONE JSON line on rank 0 (the driver's contract), with two extra objects:
+  roofline      HBM roofline of the dominant kernel (dcm_mpc_ipm), from the algorithmic bytes
+                per QP and the kernel's average duration measured with HIP
+                events on the launch stream; plus the counted-flop fp64 fraction (the roof that
+                actually binds this latency-bound kernel).
+  cpu_baseline  the CPU oracle (same IPM, C, -O2, one problem per thread) on this host's cores,
+                rank 0 only, on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bipedal-locomotion-framework_amd"))
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6    # MI355X fp64 vector (spec)
+
+
+def algorithmic_bytes_per_qp(N, M):
+    f64 = 2 + N + 2 * (N + 1) + 2 * N + 2 * N * M + N * M + 2 * (N + 1) + 2 * N
+    i32 = N + 2
+    return 8 * f64 + 4 * i32
+
+
+def cpu_baseline(host, N, seconds, threads):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    B = host["omega"].shape[0]
+    O.dcm_mpc_solve_batch(host, threads=threads, count=min(B, 64))   # warm-up
+    solved, t0 = 0, time.perf_counter()
+    while True:
+        st, _, _, _ = O.dcm_mpc_solve_batch(host, threads=threads)
+        solved += B
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    assert (st == 0).all()
+    # single-problem latency (one thread), BASELINE.md C1-style figure at this horizon
+    t1 = time.perf_counter()
+    for i in range(20):
+        O.dcm_mpc_solve(host, index=i)
+    lat_us = (time.perf_counter() - t1) / 20 * 1e6
+    return dict(value=solved / el, unit="QP/s", cores=threads, kind="port",
+                sample=f"{solved} solves = {solved // B} passes over the same {B} horizon-{N} QPs "
+                       f"in {el:.2f} s wall on {threads} threads (oracle/blf_oracle.c, gcc -O2)",
+                single_thread_latency_us=round(lat_us, 1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="QPs per GPU")
+    ap.add_argument("--horizon", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from blf import native
+    from blf import problems as P
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    h = native.Handle(local)
+
+    B, N = args.batch, args.horizon
+    prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED, start=rank * B)
+    d = {k: torch.from_numpy(prob[k]).to(dev) for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
+    A, b, nf = h.assemble_constraints(torch.from_numpy(prob["corners"]).to(dev),
+                                      torch.from_numpy(prob["ncorners"]).to(dev))
+    d.update(A=A, b=b, nfacets=nf)
+    M = b.shape[2]
+    params = native.default_params(N, max_facets=M)
+    out = h.dcm_mpc_solve(d, params)
+    torch.cuda.synchronize()
+    assert int((out["status"] != 0).sum()) == 0, "unsolved QPs in the bench batch"
+
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        h.dcm_mpc_solve(d, params, out=out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        h.dcm_mpc_solve(d, params, out=out)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps      # one launch per step on this stream
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    iters = out["iters"].to(torch.int64)
+    active = d["nfacets"].to(torch.int64).sum(dim=1)
+    flops = sum(native.flops_per_iter(N, int(a)) * int(i)
+                for a, i in zip(active.cpu().numpy(), iters.cpu().numpy()))
+
+    # RCCL gather of every rank's solutions to rank 0 (timed separately, not in `value`)
+    gather_ms = None
+    if world > 1:
+        payload = torch.cat([out["xi"].reshape(B, -1), out["vrp"].reshape(B, -1),
+                             out["status"].to(torch.float64)[:, None]], dim=1)
+        bufs = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
+        dist.barrier(); torch.cuda.synchronize()
+        tg = time.perf_counter()
+        dist.gather(payload, bufs, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    if rank == 0:
+        total = world * B * args.steps
+        bpq = algorithmic_bytes_per_qp(N, M)
+        achieved = bpq * B / (kernel_ms * 1e-3) / 1e9
+        fp64_tf = flops / (kernel_ms * 1e-3) / 1e12
+        line = {
+            "metric": "DCM-MPC QP solves/sec (batch, horizon=100)",
+            "value": total / elapsed,
+            "unit": "QP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (6-footstep plans, SeedSequence-keyed Philox per problem)",
+            "config": {"workload": f"configs[1]: batch={B} DCM-MPC QPs per GPU, horizon={N}, "
+                                   f"M={M} facet slots, fp64, one workgroup per QP",
+                       "batch_per_gpu": B, "horizon": N, "max_facets": M,
+                       "parallelism": f"shard{world} (independent problems)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "dcm_mpc_ipm_kernel<128>", "kernel_ms": kernel_ms,
+                         "bytes_per_qp": bpq,
+                         "fp64_valu": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
+                                       "frac": fp64_tf / FP64_PEAK_TFLOPS},
+                         "mean_ipm_iters": float(iters.float().mean())},
+            "gather_ms": gather_ms,
+        }
+        if not args.no_cpu:
+            try:
+                threads = len(os.sched_getaffinity(0))
+            except AttributeError:
+                threads = os.cpu_count() or 1
+            threads = max(1, min(threads, 16))
+            host = dict(prob, A=A.cpu().numpy(), b=b.cpu().numpy(), nfacets=nf.cpu().numpy())
+            line["cpu_baseline"] = cpu_baseline(host, N, args.cpu_seconds, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,290 @@
+"""ctypes binding of the C ABI in include/blf/blf_c.h (lib/libblf.so, built for gfx950).
+
+torch is used only as device-memory and stream plumbing: every function takes torch CUDA
+tensors, checks dtype/shape/contiguity/device on the host, and passes raw device pointers plus
+torch's current HIP stream to the library.  There is no CPU fallback: if lib/libblf.so is
+missing or cannot be loaded, `lib()` raises, and every op raises with it.
+"""
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "lib", "libblf.so")
+
+BLF_OK = 0
+STATUS_NAMES = {0: "BLF_OK", 1: "BLF_ERR_INVALID_ARGUMENT", 2: "BLF_ERR_HIP",
+                3: "BLF_ERR_UNSUPPORTED", 4: "BLF_ERR_TIME_INTERVAL", 5: "BLF_ERR_EMPTY_INTERVAL"}
+QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
+
+# every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
+EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
+            "blf_lti_euler_integrate", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
+            "blf_hull2d_contains", "blf_quintic_fit", "blf_quintic_eval",
+            "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_flops_per_iter"]
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f64 = ctypes.c_double
+
+
+class BlfError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class DcmMpcParams(ctypes.Structure):
+    _fields_ = [("horizon", _i32), ("max_facets", _i32), ("max_iter", _i32), ("reserved", _i32),
+                ("dt", _f64), ("w_xi", _f64 * 2), ("w_vrp", _f64 * 2), ("w_terminal", _f64 * 2),
+                ("tol_mu", _f64), ("tol_primal", _f64), ("tol_dual", _f64)]
+
+
+class DcmMpcProblem(ctypes.Structure):
+    _fields_ = [("xi_init", _vp), ("omega", _vp), ("xi_ref", _vp), ("vrp_ref", _vp), ("A", _vp),
+                ("b", _vp), ("nfacets", _vp)]
+
+
+class DcmMpcSolution(ctypes.Structure):
+    _fields_ = [("xi", _vp), ("vrp", _vp), ("status", _vp), ("iters", _vp)]
+
+
+_LIB = None
+
+
+def lib():
+    """Load lib/libblf.so (raises if it is absent: there is no fallback path)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C "
+                              f"bipedal-locomotion-framework_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.blf_create.argtypes = [ctypes.POINTER(_vp), _i32]
+        L.blf_destroy.argtypes = [_vp]
+        L.blf_last_error.restype = ctypes.c_char_p
+        L.blf_version.restype = ctypes.c_char_p
+        L.blf_lti_euler_integrate.argtypes = [_vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _i64,
+                                              _f64, _f64, _f64, _vp]
+        L.blf_dcm_euler_rollout.argtypes = [_vp, _vp, _vp, _vp, _i32, _f64, _vp, _i64, _vp]
+        L.blf_hull2d_hrep.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
+        L.blf_hull2d_contains.argtypes = [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp]
+        L.blf_quintic_fit.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp]
+        L.blf_quintic_eval.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _i32, _vp, _vp, _vp]
+        L.blf_dcm_mpc_default_params.argtypes = [ctypes.POINTER(DcmMpcParams), _i32]
+        L.blf_dcm_mpc_default_params.restype = None
+        L.blf_dcm_mpc_solve.argtypes = [_vp, ctypes.POINTER(DcmMpcParams),
+                                        ctypes.POINTER(DcmMpcProblem), _i64,
+                                        ctypes.POINTER(DcmMpcSolution), _vp]
+        L.blf_dcm_mpc_flops_per_iter.argtypes = [_i32, _i64]
+        L.blf_dcm_mpc_flops_per_iter.restype = _f64
+        for name in EXPORTED:
+            if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
+                            "blf_dcm_mpc_default_params", "blf_dcm_mpc_flops_per_iter"):
+                getattr(L, name).restype = _i32
+        L.blf_create.restype = _i32
+        L.blf_destroy.restype = _i32
+        _LIB = L
+    return _LIB
+
+
+def _check(code):
+    if code != BLF_OK:
+        raise BlfError(code, lib().blf_last_error().decode())
+
+
+def last_error():
+    return lib().blf_last_error().decode()
+
+
+def version():
+    return lib().blf_version().decode()
+
+
+def default_params(horizon, **kw):
+    p = DcmMpcParams()
+    lib().blf_dcm_mpc_default_params(ctypes.byref(p), horizon)
+    for k, v in kw.items():
+        if k in ("w_xi", "w_vrp", "w_terminal"):
+            arr = getattr(p, k)
+            arr[0], arr[1] = (v, v) if isinstance(v, (int, float)) else (v[0], v[1])
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def flops_per_iter(horizon, active_facets):
+    return lib().blf_dcm_mpc_flops_per_iter(horizon, active_facets)
+
+
+# ---------------------------------------------------------------------------------------------
+# device-side helpers (torch as plumbing)
+# ---------------------------------------------------------------------------------------------
+def _torch():
+    import torch
+    return torch
+
+
+def _ptr(t, dtype, shape=None, name="tensor"):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a device (cuda/hip) tensor, got {t.device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+    return _vp(t.data_ptr())
+
+
+def _stream(stream=None):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return _vp(s.cuda_stream)
+
+
+class Handle:
+    """RAII wrapper of blf_handle (one per device per thread)."""
+
+    def __init__(self, device=0):
+        self._h = _vp()
+        _check(lib().blf_create(ctypes.byref(self._h), device))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().blf_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ptr(self):
+        return self._h
+
+    # --- ForwardEuler<LinearTimeInvariantSystem>::integrate, batched, in place on x ---
+    def lti_euler_integrate(self, A, Bm, u, x, t0, t1, dT, shared=False, stream=None):
+        torch = _torch()
+        n = x.shape[-1]
+        m = u.shape[-1]
+        batch = x.shape[0]
+        ashape = (n, n) if shared else (batch, n, n)
+        bshape = (n, m) if shared else (batch, n, m)
+        _check(lib().blf_lti_euler_integrate(
+            self._h, n, m, _ptr(A, torch.float64, ashape, "A"), _ptr(Bm, torch.float64, bshape, "B"),
+            1 if shared else 0, _ptr(u, torch.float64, (batch, m), "u"),
+            _ptr(x, torch.float64, (batch, n), "x"), batch, t0, t1, dT, _stream(stream)))
+        return x
+
+    def dcm_euler_rollout(self, xi0, omega, vrp, dt, out=None, stream=None):
+        torch = _torch()
+        B, N = omega.shape
+        if out is None:
+            out = torch.empty((B, N + 1, 2), dtype=torch.float64, device=omega.device)
+        _check(lib().blf_dcm_euler_rollout(
+            self._h, _ptr(xi0, torch.float64, (B, 2), "xi0"), _ptr(omega, torch.float64, (B, N), "omega"),
+            _ptr(vrp, torch.float64, (B, N, 2), "vrp"), N, dt,
+            _ptr(out, torch.float64, (B, N + 1, 2), "xi_out"), B, _stream(stream)))
+        return out
+
+    def hull2d_hrep(self, pts, npts, max_facets=8, out=None, stream=None):
+        torch = _torch()
+        B, P = pts.shape[0], pts.shape[1]
+        if out is None:
+            out = (torch.empty((B, max_facets, 2), dtype=torch.float64, device=pts.device),
+                   torch.empty((B, max_facets), dtype=torch.float64, device=pts.device),
+                   torch.empty((B,), dtype=torch.int32, device=pts.device))
+        A, b, nf = out
+        _check(lib().blf_hull2d_hrep(
+            self._h, _ptr(pts, torch.float64, (B, P, 2), "pts"), _ptr(npts, torch.int32, (B,), "npts"),
+            P, max_facets, B, _ptr(A, torch.float64, (B, max_facets, 2), "A"),
+            _ptr(b, torch.float64, (B, max_facets), "b"), _ptr(nf, torch.int32, (B,), "nfacets"),
+            _stream(stream)))
+        return A, b, nf
+
+    def hull2d_contains(self, A, b, nf, query, stream=None):
+        torch = _torch()
+        B, M = b.shape
+        inside = torch.empty((B,), dtype=torch.int32, device=A.device)
+        _check(lib().blf_hull2d_contains(
+            self._h, _ptr(A, torch.float64, (B, M, 2), "A"), _ptr(b, torch.float64, (B, M), "b"),
+            _ptr(nf, torch.int32, (B,), "nfacets"), M, _ptr(query, torch.float64, (B, 2), "query"),
+            B, _ptr(inside, torch.int32, (B,), "inside"), _stream(stream)))
+        return inside
+
+    def quintic_fit(self, knots_t, knots_pva, stream=None):
+        torch = _torch()
+        S, K1 = knots_t.shape
+        D = knots_pva.shape[-1]
+        coeffs = torch.empty((S, K1 - 1, D, 6), dtype=torch.float64, device=knots_t.device)
+        _check(lib().blf_quintic_fit(
+            self._h, _ptr(knots_t, torch.float64, (S, K1), "knots_t"),
+            _ptr(knots_pva, torch.float64, (S, K1, 3, D), "knots_pva"), K1, D, S,
+            _ptr(coeffs, torch.float64, (S, K1 - 1, D, 6), "coeffs"), _stream(stream)))
+        return coeffs
+
+    def quintic_eval(self, knots_t, coeffs, tq, stream=None):
+        torch = _torch()
+        S, K1 = knots_t.shape
+        D = coeffs.shape[2]
+        Q = tq.shape[1]
+        pva = torch.empty((S, Q, 3, D), dtype=torch.float64, device=tq.device)
+        idx = torch.empty((S, Q), dtype=torch.int32, device=tq.device)
+        _check(lib().blf_quintic_eval(
+            self._h, _ptr(knots_t, torch.float64, (S, K1), "knots_t"),
+            _ptr(coeffs, torch.float64, (S, K1 - 1, D, 6), "coeffs"), K1, D, S,
+            _ptr(tq, torch.float64, (S, Q), "tq"), Q, _ptr(pva, torch.float64, (S, Q, 3, D), "pva"),
+            _ptr(idx, torch.int32, (S, Q), "knot_idx"), _stream(stream)))
+        return pva, idx
+
+    def dcm_mpc_solve(self, prob, params=None, out=None, stream=None):
+        """prob: dict of device tensors xi_init [B,2], omega [B,N], xi_ref [B,N+1,2],
+        vrp_ref [B,N,2], A [B,N,M,2], b [B,N,M], nfacets [B,N] (int32)."""
+        torch = _torch()
+        B, N = prob["omega"].shape
+        M = prob["b"].shape[2]
+        p = params if params is not None else default_params(N, max_facets=M)
+        if p.horizon != N or p.max_facets != M:
+            raise ValueError("params.horizon / max_facets do not match the problem arrays")
+        dev = prob["omega"].device
+        if out is None:
+            out = dict(xi=torch.empty((B, N + 1, 2), dtype=torch.float64, device=dev),
+                       vrp=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+                       status=torch.empty((B,), dtype=torch.int32, device=dev),
+                       iters=torch.empty((B,), dtype=torch.int32, device=dev))
+        pb = DcmMpcProblem(
+            _ptr(prob["xi_init"], torch.float64, (B, 2), "xi_init"),
+            _ptr(prob["omega"], torch.float64, (B, N), "omega"),
+            _ptr(prob["xi_ref"], torch.float64, (B, N + 1, 2), "xi_ref"),
+            _ptr(prob["vrp_ref"], torch.float64, (B, N, 2), "vrp_ref"),
+            _ptr(prob["A"], torch.float64, (B, N, M, 2), "A"),
+            _ptr(prob["b"], torch.float64, (B, N, M), "b"),
+            _ptr(prob["nfacets"], torch.int32, (B, N), "nfacets"))
+        so = DcmMpcSolution(
+            _ptr(out["xi"], torch.float64, (B, N + 1, 2), "xi"),
+            _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
+            _ptr(out["status"], torch.int32, (B,), "status"),
+            _ptr(out["iters"], torch.int32, (B,), "iters"))
+        self._keep = (pb, so)
+        _check(lib().blf_dcm_mpc_solve(self._h, ctypes.byref(p), ctypes.byref(pb), B,
+                                       ctypes.byref(so), _stream(stream)))
+        return out
+
+    # --- C3 pipeline: corner sets -> polygons (device hull) -> QP arrays ---
+    def assemble_constraints(self, corners, ncorners, max_facets=8, stream=None):
+        """corners [B, N+1, P, 2], ncorners [B, N+1] (device) -> A [B,N,M,2], b [B,N,M],
+        nfacets [B,N] for knots 0..N-1 via blf_hull2d_hrep."""
+        torch = _torch()
+        B, N1, P, _ = corners.shape
+        N = N1 - 1
+        pts = corners[:, :N].reshape(B * N, P, 2).contiguous()
+        npts = ncorners[:, :N].reshape(B * N).contiguous()
+        A, b, nf = self.hull2d_hrep(pts, npts, max_facets, stream=stream)
+        return A.view(B, N, max_facets, 2), b.view(B, N, max_facets), nf.view(B, N)

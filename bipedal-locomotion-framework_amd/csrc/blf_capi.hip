@@ -1,0 +1,221 @@
+// blf_capi.hip — the extern "C" boundary declared in include/blf/blf_c.h: argument validation,
+// the reference's error semantics, and dispatch to the kernels' launchers.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "blf_internal.h"
+
+namespace blf {
+
+static thread_local char g_err[512] = "no error";
+
+blf_status set_error(blf_status code, const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+blf_status check_hip(hipError_t e, const char* what)
+{
+    if (e == hipSuccess) return BLF_OK;
+    return set_error(BLF_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+}  // namespace blf
+
+using namespace blf;
+
+struct blf_handle {
+    Handle h;
+};
+
+#define BLF_REQUIRE(cond, ...)                                                             \
+    do {                                                                                   \
+        if (!(cond)) return set_error(BLF_ERR_INVALID_ARGUMENT, __VA_ARGS__);              \
+    } while (0)
+
+extern "C" {
+
+blf_status blf_create(blf_handle** handle, int32_t device)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_create: null handle pointer");
+    int count = 0;
+    blf_status st = check_hip(hipGetDeviceCount(&count), "hipGetDeviceCount");
+    if (st != BLF_OK) return st;
+    if (device < 0 || device >= count)
+        return set_error(BLF_ERR_HIP, "blf_create: device %d not present (%d devices)", device, count);
+    st = check_hip(hipSetDevice(device), "hipSetDevice");
+    if (st != BLF_OK) return st;
+    blf_handle* h = new blf_handle;
+    h->h.device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) h->h.num_cus = prop.multiProcessorCount;
+    *handle = h;
+    return BLF_OK;
+}
+
+blf_status blf_destroy(blf_handle* handle)
+{
+    delete handle;
+    return BLF_OK;
+}
+
+const char* blf_last_error(void) { return g_err; }
+
+const char* blf_version(void) { return "blf-mi355x 0.1.0 (gfx950, fp64, -ffp-contract=off)"; }
+
+blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m, const double* A,
+                                   const double* Bm, int32_t shared_matrices, const double* u,
+                                   double* x, int64_t batch, double initial_time,
+                                   double final_time, double dT, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_lti_euler_integrate: null handle");
+    BLF_REQUIRE(n >= 1 && n <= 8 && m >= 1 && m <= 8,
+                "blf_lti_euler_integrate: n=%d m=%d outside [1, 8]", n, m);
+    BLF_REQUIRE(batch >= 0, "blf_lti_euler_integrate: negative batch");
+    BLF_REQUIRE(batch == 0 || (A && Bm && u && x), "blf_lti_euler_integrate: null buffer");
+    // FixedStepIntegrator.tpp:28-46
+    if (initial_time > final_time)
+        return set_error(BLF_ERR_TIME_INTERVAL,
+                         "[FixedStepIntegrator::integrate] The final time has to be greater than "
+                         "the initial one.");
+    if (!(dT > 0))
+        return set_error(BLF_ERR_TIME_INTERVAL,
+                         "[FixedStepIntegrator::integrate] The sampling time must be a strictly "
+                         "positive number.");
+    if (initial_time == final_time)
+        return set_error(BLF_ERR_EMPTY_INTERVAL,
+                         "integrate(t, t): the reference loops forever here "
+                         "(FixedStepIntegrator.tpp:96-99); refused");
+    const double q = ceil((final_time - initial_time) / dT);   // :96
+    if (!(q < 2.0e9)) return set_error(BLF_ERR_UNSUPPORTED, "too many integration steps");
+    const int iterations = (int)q;
+    double currentTime = initial_time;
+    if (iterations >= 2) currentTime = initial_time + dT * (double)(iterations - 2);   // :101
+    const double dT_last = final_time - currentTime;                                    // :112
+    return launch_lti_euler(n, m, A, Bm, shared_matrices, u, x, batch, iterations, dT, dT_last,
+                            (hipStream_t)stream);
+}
+
+blf_status blf_dcm_euler_rollout(blf_handle* handle, const double* xi0, const double* omega,
+                                 const double* vrp, int32_t horizon, double dt, double* xi_out,
+                                 int64_t batch, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_dcm_euler_rollout: null handle");
+    BLF_REQUIRE(horizon >= 1, "blf_dcm_euler_rollout: horizon %d < 1", horizon);
+    BLF_REQUIRE(batch >= 0, "blf_dcm_euler_rollout: negative batch");
+    BLF_REQUIRE(batch == 0 || (xi0 && omega && vrp && xi_out), "blf_dcm_euler_rollout: null buffer");
+    return launch_dcm_rollout(xi0, omega, vrp, horizon, dt, xi_out, batch, (hipStream_t)stream);
+}
+
+blf_status blf_hull2d_hrep(blf_handle* handle, const double* pts, const int32_t* npts,
+                           int32_t max_points, int32_t max_facets, int64_t batch, double* A,
+                           double* b, int32_t* nfacets, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_hull2d_hrep: null handle");
+    BLF_REQUIRE(max_points >= 1 && max_points <= BLF_HULL_MAX_POINTS,
+                "blf_hull2d_hrep: max_points %d outside [1, %d]", max_points, BLF_HULL_MAX_POINTS);
+    BLF_REQUIRE(max_facets >= 1 && max_facets <= 2 * BLF_HULL_MAX_POINTS,
+                "blf_hull2d_hrep: max_facets %d", max_facets);
+    BLF_REQUIRE(batch >= 0, "blf_hull2d_hrep: negative batch");
+    BLF_REQUIRE(batch == 0 || (pts && npts && A && b && nfacets), "blf_hull2d_hrep: null buffer");
+    return launch_hull2d(pts, npts, max_points, max_facets, batch, A, b, nfacets,
+                         (hipStream_t)stream);
+}
+
+blf_status blf_hull2d_contains(blf_handle* handle, const double* A, const double* b,
+                               const int32_t* nfacets, int32_t max_facets, const double* query,
+                               int64_t batch, int32_t* inside, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_hull2d_contains: null handle");
+    BLF_REQUIRE(max_facets >= 1, "blf_hull2d_contains: max_facets %d", max_facets);
+    BLF_REQUIRE(batch >= 0, "blf_hull2d_contains: negative batch");
+    BLF_REQUIRE(batch == 0 || (A && b && nfacets && query && inside),
+                "blf_hull2d_contains: null buffer");
+    return launch_hull2d_contains(A, b, nfacets, max_facets, query, batch, inside,
+                                  (hipStream_t)stream);
+}
+
+blf_status blf_quintic_fit(blf_handle* handle, const double* knots_t, const double* knots_pva,
+                           int32_t nknots, int32_t dim, int64_t nsplines, double* coeffs,
+                           void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_quintic_fit: null handle");
+    BLF_REQUIRE(nknots >= 2, "blf_quintic_fit: nknots %d < 2", nknots);
+    BLF_REQUIRE(dim >= 1 && dim <= 3, "blf_quintic_fit: dim %d outside [1, 3]", dim);
+    BLF_REQUIRE(nsplines >= 0, "blf_quintic_fit: negative nsplines");
+    BLF_REQUIRE(nsplines == 0 || (knots_t && knots_pva && coeffs), "blf_quintic_fit: null buffer");
+    return launch_quintic_fit(knots_t, knots_pva, nknots, dim, nsplines, coeffs,
+                              (hipStream_t)stream);
+}
+
+blf_status blf_quintic_eval(blf_handle* handle, const double* knots_t, const double* coeffs,
+                            int32_t nknots, int32_t dim, int64_t nsplines, const double* tq,
+                            int32_t nq, double* pva, int32_t* knot_idx, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_quintic_eval: null handle");
+    BLF_REQUIRE(nknots >= 2, "blf_quintic_eval: nknots %d < 2", nknots);
+    BLF_REQUIRE(dim >= 1 && dim <= 3, "blf_quintic_eval: dim %d outside [1, 3]", dim);
+    BLF_REQUIRE(nsplines >= 0 && nq >= 0, "blf_quintic_eval: negative size");
+    BLF_REQUIRE(nsplines == 0 || nq == 0 || (knots_t && coeffs && tq && pva && knot_idx),
+                "blf_quintic_eval: null buffer");
+    return launch_quintic_eval(knots_t, coeffs, nknots, dim, nsplines, tq, nq, pva, knot_idx,
+                               (hipStream_t)stream);
+}
+
+void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon)
+{
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->horizon = horizon;
+    p->max_facets = 8;
+    p->max_iter = 50;
+    p->dt = 0.02;
+    p->w_xi[0] = p->w_xi[1] = 1e2;
+    p->w_vrp[0] = p->w_vrp[1] = 1.0;
+    p->w_terminal[0] = p->w_terminal[1] = 1e3;
+    p->tol_mu = 1e-15;
+    p->tol_primal = 1e-10;
+    p->tol_dual = 1e-9;
+}
+
+blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
+                             const blf_dcm_mpc_problem* problem, int64_t batch,
+                             const blf_dcm_mpc_solution* solution, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve: null handle");
+    BLF_REQUIRE(params && problem && solution, "blf_dcm_mpc_solve: null argument");
+    BLF_REQUIRE(params->horizon >= 1, "blf_dcm_mpc_solve: horizon %d < 1", params->horizon);
+    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacets,
+                "blf_dcm_mpc_solve: max_facets %d outside [1, %d]", params->max_facets, kMaxFacets);
+    BLF_REQUIRE(params->max_iter >= 0, "blf_dcm_mpc_solve: max_iter < 0");
+    BLF_REQUIRE(params->reserved == 0, "blf_dcm_mpc_solve: reserved must be 0");
+    BLF_REQUIRE(params->dt > 0, "blf_dcm_mpc_solve: dt must be > 0");
+    BLF_REQUIRE(params->w_vrp[0] > 0 && params->w_vrp[1] > 0 && params->w_xi[0] >= 0 &&
+                    params->w_xi[1] >= 0 && params->w_terminal[0] >= 0 && params->w_terminal[1] >= 0,
+                "blf_dcm_mpc_solve: weights must be R > 0, Q >= 0, P >= 0");
+    BLF_REQUIRE(batch >= 0, "blf_dcm_mpc_solve: negative batch");
+    BLF_REQUIRE(batch == 0 || (problem->xi_init && problem->omega && problem->xi_ref &&
+                               problem->vrp_ref && problem->A && problem->b && problem->nfacets &&
+                               solution->xi && solution->vrp && solution->status && solution->iters),
+                "blf_dcm_mpc_solve: null buffer");
+    return launch_dcm_mpc(params, problem, batch, solution, (hipStream_t)stream);
+}
+
+double blf_dcm_mpc_flops_per_iter(int32_t horizon, int64_t active_facets)
+{
+    // Counted from dcm_mpc_ipm.hip, per IPM iteration (fp64 add/sub/mul/div = 1 flop each;
+    // negations, fabs, min/max and compares not counted):
+    //   per facet: residual 11, R' + affine rhs 17, affine step 11, mu_aff 14,
+    //              corrector rhs 10, corrector step 12, update 4                    = 79
+    //   per knot:  residual/defect/Q-terms 20, backward factor+solve 74, backward solve 32,
+    //              two forward sweeps 2 x 25, update 8                               = 184
+    return 79.0 * (double)active_facets + 184.0 * (double)horizon;
+}
+
+}  // extern "C"

@@ -1,0 +1,81 @@
+// blf_internal.h — shared declarations of the HIP kernels' launchers and device helpers.
+// Everything in csrc/ is compiled with -ffp-contract=off: every fp64 expression is evaluated
+// exactly in source order, the same order as the CPU oracle (oracle/blf_oracle.c), so that
+// device and oracle results can be compared bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "blf/blf_c.h"
+
+namespace blf {
+
+constexpr int kWave = 64;   // CDNA wavefront width
+constexpr int kMaxFacets = 8;
+
+// ---- error plumbing (blf_capi.hip) ----
+blf_status set_error(blf_status code, const char* fmt, ...);
+blf_status check_hip(hipError_t e, const char* what);
+
+struct Handle {
+    int device = 0;
+    int num_cus = 0;
+};
+
+// ---- launchers (one per kernel file) ----
+blf_status launch_lti_euler(int n, int m, const double* A, const double* Bm, int shared,
+                            const double* u, double* x, int64_t batch, int32_t nsteps,
+                            double dT, double dT_last, hipStream_t s);
+blf_status launch_dcm_rollout(const double* xi0, const double* omega, const double* vrp,
+                              int32_t N, double dt, double* xi_out, int64_t batch,
+                              hipStream_t s);
+blf_status launch_hull2d(const double* pts, const int32_t* npts, int32_t P, int32_t M,
+                         int64_t batch, double* A, double* b, int32_t* nf, hipStream_t s);
+blf_status launch_hull2d_contains(const double* A, const double* b, const int32_t* nf, int32_t M,
+                                  const double* q, int64_t batch, int32_t* inside,
+                                  hipStream_t s);
+blf_status launch_quintic_fit(const double* kt, const double* kp, int32_t K1, int32_t D,
+                              int64_t S, double* coeffs, hipStream_t s);
+blf_status launch_quintic_eval(const double* kt, const double* coeffs, int32_t K1, int32_t D,
+                               int64_t S, const double* tq, int32_t Q, double* pva,
+                               int32_t* idx, hipStream_t s);
+blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
+                          int64_t batch, const blf_dcm_mpc_solution* sol, hipStream_t s);
+
+// ---- device helpers ----
+// NaN-propagating max (matches the oracle's `if (e > m || e != e) m = e`).
+__device__ __forceinline__ double nanmax(double a, double b) { return (b > a || b != b) ? b : a; }
+// min that ignores NaN candidates (matches `if (q < m) m = q`).
+__device__ __forceinline__ double keepmin(double a, double b) { return (b < a) ? b : a; }
+
+// xor-butterfly over the 64 lanes; every lane ends with the identical value because fp addition
+// is commutative: lane l and lane l^off both compute the same two operands.
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, kWave);
+    return v;
+}
+__device__ __forceinline__ double wave_nanmax(double v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = nanmax(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+__device__ __forceinline__ double wave_keepmin(double v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = keepmin(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+__device__ __forceinline__ int wave_isum(int v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace blf

@@ -1,0 +1,173 @@
+/*
+ * blf_c.h — C ABI of the MI355X-native batched DCM-MPC planning path.
+ *
+ * This is the drop-in boundary.  Every entry point takes plain pointers and sizes (no C++ or
+ * torch types), returns a blf_status, and is stream-ordered on the hipStream_t passed in
+ * (passed as `void*` so this header needs no HIP include; NULL = the default stream).
+ * All device buffers are caller-owned and must be device-resident (hipMalloc'd or a torch CUDA
+ * tensor's data_ptr()).  Layout convention: PROBLEM-MAJOR ("[B][...]", batch outermost, each
+ * problem's arrays contiguous), innermost index = the spatial coordinate.  One workgroup (or one
+ * lane for the rollout/eval kernels) serves one problem; see DESIGN.md for why.
+ *
+ * Which reference interface each entry point replaces (paths relative to the reference root,
+ * src/...):
+ *   blf_lti_euler_integrate   System/include/BipedalLocomotion/System/FixedStepIntegrator.tpp:21-72
+ *                             + ForwardEuler.tpp:18-49 + System/src/LinearTimeInvariantSystem.cpp:40-74
+ *                             (ForwardEuler<LinearTimeInvariantSystem>::integrate(t0, T))
+ *   blf_dcm_euler_rollout     the same ForwardEuler<LTI> step applied per knot with
+ *                             A = omega_k I, B = -omega_k I (LinearTimeInvariantSystem.cpp:13-38, :71)
+ *   blf_hull2d_hrep           Planners/src/ConvexHullHelper.cpp:35-99 (buildConvexHull/getA/getB)
+ *   blf_hull2d_contains       Planners/src/ConvexHullHelper.cpp:101-117 (doesPointBelongToConvexHull)
+ *   blf_quintic_fit/_eval     ABSENT in the reference (QuinticSpline); knot rule
+ *                             of Planners/src/ContactList.cpp:190-202 (getPresentContact, `<=`)
+ *   blf_dcm_mpc_solve         ABSENT in the reference (TimeVaryingDCMPlanner QP),
+ *                             driven through System/Advanceable.h:24-46 (advance()) by the C++ host
+ *                             adapter blf::Planners::TimeVaryingDCMPlanner
+ */
+#ifndef BLF_C_H
+#define BLF_C_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------------------------- */
+typedef int32_t blf_status;
+#define BLF_OK                   0
+#define BLF_ERR_INVALID_ARGUMENT 1  /* bad size / null pointer / bad parameter                   */
+#define BLF_ERR_HIP              2  /* a HIP runtime call failed (see blf_last_error())          */
+#define BLF_ERR_UNSUPPORTED      3  /* size outside what the kernels are built for               */
+#define BLF_ERR_TIME_INTERVAL    4  /* reference rejects: initialTime > finalTime or dT <= 0     */
+#define BLF_ERR_EMPTY_INTERVAL   5  /* initialTime == finalTime: the reference loops forever
+                                       (FixedStepIntegrator.tpp:96-99, size_t vs -1); we refuse  */
+
+/* per-problem solver status written by blf_dcm_mpc_solve */
+#define BLF_QP_SOLVED        0
+#define BLF_QP_MAX_ITER      1
+#define BLF_QP_NUMERICAL     2   /* non-finite iterate or non-positive-definite KKT block        */
+#define BLF_QP_BAD_FACETS    3   /* nfacets[k] outside [0, max_facets]                            */
+
+typedef struct blf_handle blf_handle;
+
+/* Create a handle bound to HIP device `device`.  Fails with BLF_ERR_HIP if no device. */
+blf_status blf_create(blf_handle** handle, int32_t device);
+blf_status blf_destroy(blf_handle* handle);
+/* Human-readable description of the last error on this thread (never NULL). */
+const char* blf_last_error(void);
+/* Version string of the library (build id). */
+const char* blf_version(void);
+
+/* ---- 1. ForwardEuler<LinearTimeInvariantSystem>::integrate(t0, T), batched ------------------
+ * x_{i+1} = x_i + (A x_i + B u) * dT_i over the reference's step schedule:
+ *   iters = (int)ceil((T - t0) / dT); steps i = 0..iters-2 advance by dT; the final step
+ *   advances by (T - currentTime) with the stale currentTime = t0 + dT*(iters-2) (0 if iters<2).
+ * A: [B][n][n] row-major, Bm: [B][n][m] (or a single shared matrix when `shared_matrices` != 0),
+ * u: [B][m] (held constant, as setControlInput does), x: [B][n] updated in place.
+ * n, m <= 8.  Arithmetic order (no FMA contraction): dx_r = (sum_c A_rc x_c) + (sum_c B_rc u_c),
+ * each sum left to right; x_r = x_r + dx_r * dT_i.                                            */
+blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m,
+                                   const double* A, const double* Bm, int32_t shared_matrices,
+                                   const double* u, double* x, int64_t batch,
+                                   double initial_time, double final_time, double dT,
+                                   void* stream);
+
+/* ---- 2. DCM rollout: one reference Euler step per knot -------------------------------------
+ * xi_{k+1} = xi_k + ((omega_k * xi_k) + (-omega_k * r_k)) * dt,  k = 0..N-1
+ * xi0: [B][2], omega: [B][N], vrp: [B][N][2], xi_out: [B][N+1][2] (xi_out[:,0] = xi0).       */
+blf_status blf_dcm_euler_rollout(blf_handle* handle, const double* xi0, const double* omega,
+                                 const double* vrp, int32_t horizon, double dt,
+                                 double* xi_out, int64_t batch, void* stream);
+
+/* ---- 3. Support polygon H-representation (ConvexHullHelper, 2-D) ---------------------------
+ * pts: [B][P][2] (P <= BLF_HULL_MAX_POINTS), npts: [B] valid point count (<= P).
+ * Output, padded to `max_facets` rows: A: [B][max_facets][2] unit outward normals,
+ * b: [B][max_facets] offsets (inside: A x <= b), nfacets: [B] facet count (rows >= nfacets are
+ * zero rows with b = 0).  Collinear boundary points are merged (Qhull "Qt" merges them too, see
+ * ConvexHullHelper.cpp:54-58).  Facets are ordered counter-clockwise from the lowest-leftmost
+ * vertex; Qhull's order is internal, so compare as sets.  If the hull needs more than
+ * max_facets rows, or fewer than 3 distinct non-collinear points are given, nfacets = -1.     */
+#define BLF_HULL_MAX_POINTS 16
+blf_status blf_hull2d_hrep(blf_handle* handle, const double* pts, const int32_t* npts,
+                           int32_t max_points, int32_t max_facets, int64_t batch,
+                           double* A, double* b, int32_t* nfacets, void* stream);
+
+/* doesPointBelongToConvexHull: inside[q] = 1 iff for all rows i < nfacets: (A p)_i <= b_i
+ * (strict `>` rejects, no tolerance, ConvexHullHelper.cpp:110-114).  One query point per polygon:
+ * query: [B][2], inside: [B] int32.  A polygon with nfacets < 0 gives 0.                      */
+blf_status blf_hull2d_contains(blf_handle* handle, const double* A, const double* b,
+                               const int32_t* nfacets, int32_t max_facets, const double* query,
+                               int64_t batch, int32_t* inside, void* stream);
+
+/* ---- 4. Quintic spline (swing foot) -------------------------------------------------------
+ * A spline has K+1 knots t_0 < ... < t_K, and per knot and per axis (D axes, D <= 3) the
+ * position, velocity and acceleration.  Segment j spans [t_j, t_{j+1}] and is the unique
+ * quintic matching (p, v, a) at both ends.
+ * fit:  knots_t: [S][K+1], knots_pva: [S][K+1][3 (p,v,a)][D]  ->  coeffs: [S][K][D][6]
+ *       (c0..c5 of p(tau) = sum c_i tau^i, tau = t - t_j).
+ * eval: query t: [S][Q]; segment = last knot j with t_j <= t, clamped to [0, K-1] (the
+ *       getPresentContact rule, ContactList.cpp:190-202; t < t_0 -> segment 0); tau = t - t_j;
+ *       pva out: [S][Q][3][D] (position, velocity, acceleration), knot_idx out: [S][Q].     */
+blf_status blf_quintic_fit(blf_handle* handle, const double* knots_t, const double* knots_pva,
+                           int32_t nknots, int32_t dim, int64_t nsplines, double* coeffs,
+                           void* stream);
+blf_status blf_quintic_eval(blf_handle* handle, const double* knots_t, const double* coeffs,
+                            int32_t nknots, int32_t dim, int64_t nsplines, const double* tq,
+                            int32_t nq, double* pva, int32_t* knot_idx, void* stream);
+
+/* ---- 5. Time-varying DCM MPC QP (TimeVaryingDCMPlanner), batched ---------------------------
+ * Per problem, with alpha_k = 1 + dt*omega_k, beta_k = dt*omega_k:
+ *   min  sum_{k=0}^{N-1} 1/2|xi_k - xi_ref_k|^2_Q + 1/2|r_k - r_ref_k|^2_R + 1/2|xi_N - xi_ref_N|^2_P
+ *   s.t. xi_0 = xi_init,  xi_{k+1} = xi_k + dt*omega_k*(xi_k - r_k)  (reference Euler step),
+ *        A_k r_k <= b_k  (rows i < nfacets[k] of the support polygon H-rep)
+ * Solved by a Mehrotra primal-dual interior point method whose Newton systems are factored by a
+ * Riccati recursion over the knots (DESIGN.md section 4 gives the exact iteration).           */
+typedef struct blf_dcm_mpc_params {
+    int32_t horizon;       /* N >= 1                                                        */
+    int32_t max_facets;    /* M, 1..8 (padded facet slots per knot)                         */
+    int32_t max_iter;      /* IPM iteration cap (e.g. 50)                                   */
+    int32_t reserved;      /* must be 0                                                     */
+    double dt;             /* knot spacing [s]                                              */
+    double w_xi[2];        /* Q diagonal                                                    */
+    double w_vrp[2];       /* R diagonal                                                    */
+    double w_terminal[2];  /* P diagonal                                                    */
+    double tol_mu;         /* stop when mean complementarity <= tol_mu ...                   */
+    double tol_primal;     /* ... and max |primal residual|, |dynamics defect| <= tol_primal */
+    double tol_dual;       /* ... and the tracked dual residual bound <= tol_dual            */
+} blf_dcm_mpc_params;
+
+typedef struct blf_dcm_mpc_problem {
+    const double* xi_init;   /* [B][2]                                                      */
+    const double* omega;     /* [B][N]      omega_k = sqrt(g / z_k)                          */
+    const double* xi_ref;    /* [B][N+1][2]                                                 */
+    const double* vrp_ref;   /* [B][N][2]   also the IPM's initial VRP guess                 */
+    const double* A;         /* [B][N][M][2]                                                */
+    const double* b;         /* [B][N][M]                                                   */
+    const int32_t* nfacets;  /* [B][N]                                                      */
+} blf_dcm_mpc_problem;
+
+typedef struct blf_dcm_mpc_solution {
+    double* xi;              /* [B][N+1][2]                                                 */
+    double* vrp;             /* [B][N][2]                                                   */
+    int32_t* status;         /* [B]  BLF_QP_*                                               */
+    int32_t* iters;          /* [B]  IPM iterations taken                                   */
+} blf_dcm_mpc_solution;
+
+/* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-15,
+ * tol_primal 1e-10, tol_dual 1e-9, max_iter 50, max_facets 8). */
+void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);
+
+blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
+                             const blf_dcm_mpc_problem* problem, int64_t batch,
+                             const blf_dcm_mpc_solution* solution, void* stream);
+
+/* Algorithmic flop count of one IPM iteration of one problem (what the fp64 roofline field
+ * of bench.py is computed from); `active_facets` = sum_k nfacets[k]. */
+double blf_dcm_mpc_flops_per_iter(int32_t horizon, int64_t active_facets);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BLF_C_H */

@@ -1,0 +1,89 @@
+/*
+ * blf_oracle.h — TEST INFRASTRUCTURE ONLY.  CPU restatement (plain C, fp64, no FMA contraction)
+ * of the reference semantics on the DCM-MPC path.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library; the product path (the HIP library behind
+ * include/blf/blf_c.h) never links or calls it.
+ *
+ * Parity anchors (reference paths relative to src/):
+ *   orc_lti_euler_integrate  System/include/BipedalLocomotion/System/FixedStepIntegrator.tpp:21-72,
+ *                            ForwardEuler.tpp:18-49, ForwardEuler.h:35-50,
+ *                            System/src/LinearTimeInvariantSystem.cpp:40-74
+ *                            pinned by System/tests/IntegratorTest.cpp:27-75 (closed form, tol 1e-3)
+ *   orc_dcm_euler_rollout    the LTI step with A = omega I, B = -omega I (bit-exact by construction)
+ *   orc_contact_phases       Planners/src/ContactPhaseList.cpp:16-84
+ *                            pinned by Planners/tests/ContactPhaseListTest.cpp:15-153 (8 phases)
+ *   orc_present_index        Planners/src/ContactList.cpp:190-202 (getPresentContact)
+ *                            pinned by Planners/tests/ContactListTest.cpp:85-92
+ *   orc_hull2d_hrep          Planners/src/ConvexHullHelper.cpp:35-99; arithmetic of the pinned
+ *                            third-party dependency Qhull 8.0.0 ("Qt"), restated as a 2-D
+ *                            monotone chain with collinear merge; pinned against scipy's bundled
+ *                            Qhull 7.3.2 "Qt" fixtures (tests/golden/hull2d.json)
+ *   orc_hull2d_contains      Planners/src/ConvexHullHelper.cpp:101-117
+ *   orc_quintic_*            ABSENT in the reference: parity unpinned against the
+ *                            reference; pinned by boundary-condition identities + sympy fixtures
+ *   orc_dcm_mpc_solve        ABSENT in the reference: parity unpinned against the
+ *                            reference; pinned by an independent dense KKT solve (iteratively
+ *                            refined) of the same QP in tests/test_oracle_dcm_mpc.py
+ */
+#ifndef BLF_ORACLE_H
+#define BLF_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int orc_lti_euler_integrate(int n, int m, const double* A, const double* B, const double* u,
+                            double* x, double t0, double t1, double dT, int64_t* nsteps_out);
+
+void orc_dcm_euler_rollout(const double* xi0, const double* omega, const double* vrp, int N,
+                           double dt, double* xi_out);
+
+/* ContactPhaseList::createPhases over L lists of contact intervals.
+ * act/deact: [L][C] (list l has ncontacts[l] valid entries, sorted, non-overlapping).
+ * Output: up to max_phases phases: begin[p], end[p], active[p][L] = contact index of list l
+ * active in phase p or -1.  Returns the number of phases (or -1 if max_phases too small). */
+int orc_contact_phases(int L, int C, const double* act, const double* deact,
+                       const int32_t* ncontacts, int max_phases, double* begin, double* end,
+                       int32_t* active);
+
+/* getPresentContact: index of the last element with activation_time <= t, or -1 (end()). */
+int orc_present_index(const double* activation_times, int n, double t);
+
+int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);
+int orc_hull2d_contains(const double* A, const double* b, int nfacets, const double* p);
+
+void orc_quintic_fit(const double* knots_t, const double* knots_pva, int nknots, int dim,
+                     double* coeffs);
+void orc_quintic_eval(const double* knots_t, const double* coeffs, int nknots, int dim,
+                      const double* tq, int nq, double* pva, int32_t* knot_idx);
+
+typedef struct orc_dcm_params {
+    int32_t horizon, max_facets, max_iter, reserved;
+    double dt, w_xi[2], w_vrp[2], w_terminal[2], tol_mu, tol_primal, tol_dual;
+} orc_dcm_params;
+
+/* Solve one problem (arrays for this problem only, same layout as blf_dcm_mpc_problem).
+ * Returns the BLF_QP_* status; writes xi [N+1][2], vrp [N][2], *iters. */
+int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const double* omega,
+                      const double* xi_ref, const double* vrp_ref, const double* A,
+                      const double* b, const int32_t* nfacets, double* xi, double* vrp,
+                      int32_t* iters);
+
+/* Whole batch (problem-major arrays), split over `threads` POSIX threads (one problem per
+ * thread at a time).  Used as bench.py's CPU baseline. */
+void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threads,
+                             const double* xi_init, const double* omega, const double* xi_ref,
+                             const double* vrp_ref, const double* A, const double* b,
+                             const int32_t* nfacets, double* xi, double* vrp, int32_t* status,
+                             int32_t* iters);
+
+/* Tree sum with the device's reduction order: c has n entries, padded with
+ * zeros to 64*ceil(n/64); per 64-block xor-butterfly, then block sums left to right. */
+double orc_wave_tree_sum(const double* c, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

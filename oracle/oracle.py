@@ -1,0 +1,220 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU oracle (liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+The product path (bipedal-locomotion-framework_amd/blf) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [("horizon", ctypes.c_int32), ("max_facets", ctypes.c_int32),
+                ("max_iter", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("dt", ctypes.c_double), ("w_xi", ctypes.c_double * 2),
+                ("w_vrp", ctypes.c_double * 2), ("w_terminal", ctypes.c_double * 2),
+                ("tol_mu", ctypes.c_double), ("tol_primal", ctypes.c_double),
+                ("tol_dual", ctypes.c_double)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.orc_lti_euler_integrate.restype = ctypes.c_int
+        L.orc_lti_euler_integrate.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _dp,
+                                              ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                              ctypes.POINTER(ctypes.c_int64)]
+        L.orc_dcm_euler_rollout.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_double, _dp]
+        L.orc_contact_phases.restype = ctypes.c_int
+        L.orc_contact_phases.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, _ip, ctypes.c_int,
+                                         _dp, _dp, _ip]
+        L.orc_present_index.restype = ctypes.c_int
+        L.orc_present_index.argtypes = [_dp, ctypes.c_int, ctypes.c_double]
+        L.orc_hull2d_hrep.restype = ctypes.c_int
+        L.orc_hull2d_hrep.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
+        L.orc_hull2d_contains.restype = ctypes.c_int
+        L.orc_hull2d_contains.argtypes = [_dp, _dp, ctypes.c_int, _dp]
+        L.orc_quintic_fit.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_quintic_eval.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
+                                       _dp, _ip]
+        L.orc_dcm_mpc_solve.restype = ctypes.c_int
+        L.orc_dcm_mpc_solve.argtypes = [ctypes.POINTER(OrcParams), _dp, _dp, _dp, _dp, _dp, _dp,
+                                        _ip, _dp, _dp, _ip]
+        L.orc_dcm_mpc_solve_batch.argtypes = [ctypes.POINTER(OrcParams), ctypes.c_int64,
+                                              ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _ip,
+                                              _dp, _dp, _ip, _ip]
+        L.orc_wave_tree_sum.restype = ctypes.c_double
+        L.orc_wave_tree_sum.argtypes = [_dp, ctypes.c_int]
+        _LIB = L
+    return _LIB
+
+
+def _d(a):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def _i(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_ip)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def lti_euler_integrate(A, B, u, x, t0, t1, dT):
+    A, B, u = _f64(A), _f64(B), _f64(u)
+    x = _f64(x).copy()
+    n, m = A.shape[0], B.shape[1]
+    steps = ctypes.c_int64(0)
+    st = lib().orc_lti_euler_integrate(n, m, _d(A), _d(B), _d(u), _d(x), t0, t1, dT,
+                                       ctypes.byref(steps))
+    return st, x, steps.value
+
+
+def dcm_euler_rollout(xi0, omega, vrp, dt):
+    xi0, omega, vrp = _f64(xi0), _f64(omega), _f64(vrp)
+    N = omega.shape[0]
+    out = np.zeros((N + 1, 2))
+    lib().orc_dcm_euler_rollout(_d(xi0), _d(omega), _d(vrp), N, dt, _d(out))
+    return out
+
+
+def contact_phases(lists, max_phases=256):
+    """lists: sequence of [(activation, deactivation), ...] per contact list (ordered)."""
+    L = len(lists)
+    C = max(1, max(len(l) for l in lists))
+    act = np.zeros((L, C))
+    deact = np.zeros((L, C))
+    nc = np.zeros(L, dtype=np.int32)
+    for l, lst in enumerate(lists):
+        nc[l] = len(lst)
+        for c, (a, d) in enumerate(lst):
+            act[l, c], deact[l, c] = a, d
+    begin = np.zeros(max_phases)
+    end = np.zeros(max_phases)
+    active = np.zeros((max_phases, L), dtype=np.int32)
+    n = lib().orc_contact_phases(L, C, _d(act), _d(deact), _i(nc), max_phases, _d(begin),
+                                 _d(end), _i(active))
+    if n < 0:
+        raise RuntimeError("too many phases")
+    return begin[:n].copy(), end[:n].copy(), active[:n].copy()
+
+
+def present_index(times, t):
+    times = _f64(times)
+    return lib().orc_present_index(_d(times), times.shape[0], t)
+
+
+def hull2d_hrep(pts, max_facets=8):
+    pts = _f64(pts)
+    A = np.zeros((max_facets, 2))
+    b = np.zeros(max_facets)
+    m = lib().orc_hull2d_hrep(_d(pts), pts.shape[0], max_facets, _d(A), _d(b))
+    return A, b, m
+
+
+def hull2d_contains(A, b, m, p):
+    return bool(lib().orc_hull2d_contains(_d(_f64(A)), _d(_f64(b)), m, _d(_f64(p))))
+
+
+def quintic_fit(knots_t, knots_pva):
+    knots_t, knots_pva = _f64(knots_t), _f64(knots_pva)
+    K1, dim = knots_t.shape[0], knots_pva.shape[2]
+    coeffs = np.zeros((K1 - 1, dim, 6))
+    lib().orc_quintic_fit(_d(knots_t), _d(knots_pva), K1, dim, _d(coeffs))
+    return coeffs
+
+
+def quintic_eval(knots_t, coeffs, tq):
+    knots_t, coeffs, tq = _f64(knots_t), _f64(coeffs), _f64(tq)
+    K1, dim = knots_t.shape[0], coeffs.shape[1]
+    pva = np.zeros((tq.shape[0], 3, dim))
+    idx = np.zeros(tq.shape[0], dtype=np.int32)
+    lib().orc_quintic_eval(_d(knots_t), _d(coeffs), K1, dim, _d(tq), tq.shape[0], _d(pva),
+                           _i(idx))
+    return pva, idx
+
+
+def default_params(horizon, **kw):
+    p = OrcParams()
+    p.horizon = horizon
+    p.max_facets = kw.get("max_facets", 8)
+    p.max_iter = kw.get("max_iter", 50)
+    p.reserved = 0
+    p.dt = kw.get("dt", 0.02)
+    for name, val in (("w_xi", 1e2), ("w_vrp", 1.0), ("w_terminal", 1e3)):
+        v = kw.get(name, val)
+        getattr(p, name)[0] = v if np.isscalar(v) else v[0]
+        getattr(p, name)[1] = v if np.isscalar(v) else v[1]
+    p.tol_mu = kw.get("tol_mu", 1e-15)
+    p.tol_primal = kw.get("tol_primal", 1e-10)
+    p.tol_dual = kw.get("tol_dual", 1e-9)
+    return p
+
+
+def dcm_mpc_solve(prob, params=None, index=0):
+    """Solve problem `index` of a batch dict (keys as produced by blf.problems)."""
+    N = prob["omega"].shape[1]
+    p = params or default_params(N)
+    xi = np.zeros((N + 1, 2))
+    vrp = np.zeros((N, 2))
+    it = np.zeros(1, dtype=np.int32)
+    g = lambda k: np.ascontiguousarray(prob[k][index])
+    st = lib().orc_dcm_mpc_solve(ctypes.byref(p), _d(g("xi_init")), _d(g("omega")),
+                                 _d(g("xi_ref")), _d(g("vrp_ref")), _d(g("A")), _d(g("b")),
+                                 _i(g("nfacets")), _d(xi), _d(vrp), _i(it))
+    return st, xi, vrp, int(it[0])
+
+
+def dcm_mpc_solve_batch(prob, params=None, threads=1, count=None):
+    B = prob["omega"].shape[0] if count is None else count
+    N = prob["omega"].shape[1]
+    p = params or default_params(N)
+    xi = np.zeros((B, N + 1, 2))
+    vrp = np.zeros((B, N, 2))
+    status = np.zeros(B, dtype=np.int32)
+    iters = np.zeros(B, dtype=np.int32)
+    g = lambda k: np.ascontiguousarray(prob[k][:B])
+    lib().orc_dcm_mpc_solve_batch(ctypes.byref(p), B, threads, _d(g("xi_init")), _d(g("omega")),
+                                  _d(g("xi_ref")), _d(g("vrp_ref")), _d(g("A")), _d(g("b")),
+                                  _i(g("nfacets")), _d(xi), _d(vrp), _i(status), _i(iters))
+    return status, xi, vrp, iters
+
+
+def wave_tree_sum(c):
+    c = _f64(c)
+    return lib().orc_wave_tree_sum(_d(c), c.shape[0])
+
+
+def assemble_constraints(prob, max_facets=8):
+    """Per-knot support polygon H-rep from the generator's corner sets, via the oracle hull."""
+    corners, ncorners = prob["corners"], prob["ncorners"]
+    B, N1 = ncorners.shape
+    N = N1 - 1
+    A = np.zeros((B, N, max_facets, 2))
+    b = np.zeros((B, N, max_facets))
+    m = np.zeros((B, N), dtype=np.int32)
+    for i in range(B):
+        for k in range(N):
+            A[i, k], b[i, k], m[i, k] = hull2d_hrep(corners[i, k, :ncorners[i, k]], max_facets)
+    out = dict(prob)
+    out.update(A=A, b=b, nfacets=m)
+    return out

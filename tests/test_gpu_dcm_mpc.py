@@ -1,0 +1,108 @@
+"""GPU parity of the batched DCM-MPC QP (blf_dcm_mpc_solve) against the CPU oracle.
+
+The oracle (oracle/blf_oracle.c:orc_dcm_mpc_solve) and the kernel evaluate the same IPM in the
+same expression order with FMA contraction off on both sides, so the bar is bit equality of
+xi, vrp, status and iteration count.  The north-star tolerance (fp64 trajectory error < 1e-9)
+is asserted as well, as the floor every run must clear.
+"""
+import numpy as np
+import pytest
+import torch
+
+from blf import problems as P
+from blf import native
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9   # north_star: fp64 trajectory error < 1e-9 vs the reference CPU path
+
+
+def _to_dev(prob, keys=("xi_init", "omega", "xi_ref", "vrp_ref", "A", "b", "nfacets")):
+    return {k: torch.from_numpy(np.ascontiguousarray(prob[k])).cuda() for k in keys}
+
+
+def _gpu_problem(handle, prob):
+    dev = _to_dev(prob, ("xi_init", "omega", "xi_ref", "vrp_ref"))
+    corners = torch.from_numpy(prob["corners"]).cuda()
+    ncorners = torch.from_numpy(prob["ncorners"]).cuda()
+    A, b, nf = handle.assemble_constraints(corners, ncorners)
+    dev.update(A=A, b=b, nfacets=nf)
+    return dev
+
+
+@pytest.mark.parametrize("horizon,footsteps,batch", [(100, 6, 96), (50, 4, 64), (130, 8, 32)])
+def test_dcm_mpc_matches_oracle_bitwise(handle, oracle, horizon, footsteps, batch):
+    prob = P.make_batch(batch, horizon=horizon, n_footsteps=footsteps, seed=11)
+    dev = _gpu_problem(handle, prob)
+    # the device hull feeds the QP; the oracle gets the same A, b, nfacets
+    host = dict(prob)
+    for k in ("A", "b", "nfacets"):
+        host[k] = dev[k].cpu().numpy()
+    out = handle.dcm_mpc_solve(dev)
+    torch.cuda.synchronize()
+    st_o, xi_o, vrp_o, it_o = oracle.dcm_mpc_solve_batch(host, threads=8)
+    xi_g, vrp_g = out["xi"].cpu().numpy(), out["vrp"].cpu().numpy()
+    st_g, it_g = out["status"].cpu().numpy(), out["iters"].cpu().numpy()
+    assert (st_g == 0).all(), st_g
+    assert (st_o == 0).all()
+    np.testing.assert_array_equal(it_g, it_o)
+    assert np.abs(xi_g - xi_o).max() <= TOL
+    assert np.abs(vrp_g - vrp_o).max() <= TOL
+    np.testing.assert_array_equal(xi_g, xi_o)
+    np.testing.assert_array_equal(vrp_g, vrp_o)
+
+
+def test_dcm_mpc_solution_properties(handle):
+    """Size-independent checks on a larger batch: feasibility, the reference Euler step between
+    consecutive knots, and xi_0 = xi_init."""
+    B, N = 2048, 100
+    prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=5)
+    dev = _gpu_problem(handle, prob)
+    out = handle.dcm_mpc_solve(dev)
+    xi, vrp = out["xi"], out["vrp"]
+    assert (out["status"] == 0).all()
+    assert torch.equal(xi[:, 0], dev["xi_init"])
+    A, b, nf = dev["A"], dev["b"], dev["nfacets"]
+    viol = torch.einsum("bkij,bkj->bki", A, vrp) - b
+    mask = torch.arange(A.shape[2], device=A.device)[None, None, :] < nf[:, :, None]
+    assert viol[mask].max().item() <= 1e-12
+    w = dev["omega"]
+    step = xi[:, :-1] + (w[..., None] * xi[:, :-1] + (-w[..., None]) * vrp) * 0.02
+    assert (step - xi[:, 1:]).abs().max().item() <= 1e-12
+
+
+def test_dcm_mpc_edge_cases(handle, oracle):
+    B, N = 8, 20
+    prob = P.make_batch(B, horizon=N, n_footsteps=4, seed=3)
+    host = oracle.assemble_constraints(prob)
+    # problem 1: no constraints at all (equality-only QP); problem 2: a bad facet count
+    host["nfacets"][1, :] = 0
+    host["nfacets"][2, 5] = 9
+    dev = _to_dev(host)
+    out = handle.dcm_mpc_solve(dev)
+    st_o, xi_o, vrp_o, it_o = oracle.dcm_mpc_solve_batch(host, threads=1)
+    st_g = out["status"].cpu().numpy()
+    np.testing.assert_array_equal(st_g, st_o)
+    assert st_g[2] == native.QP_BAD_FACETS and st_g[1] == native.QP_SOLVED
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), it_o)
+    np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi_o)
+    np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)
+
+
+def test_dcm_mpc_horizon_one_and_empty_batch(handle, oracle):
+    prob = P.make_batch(4, horizon=1, n_footsteps=2, seed=1)
+    host = oracle.assemble_constraints(prob)
+    out = handle.dcm_mpc_solve(_to_dev(host))
+    st_o, xi_o, vrp_o, it_o = oracle.dcm_mpc_solve_batch(host, threads=1)
+    np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi_o)
+    np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)
+    empty = {k: v[:0] for k, v in _to_dev(host).items()}
+    res = handle.dcm_mpc_solve(empty)
+    assert res["xi"].shape[0] == 0
+
+
+def test_dcm_mpc_rejects_bad_params(handle):
+    prob = P.make_batch(2, horizon=10, n_footsteps=4, seed=1)
+    dev = _gpu_problem(handle, prob)
+    p = native.default_params(10, max_facets=8, dt=-1.0)
+    with pytest.raises(native.BlfError):
+        handle.dcm_mpc_solve(dev, params=p)

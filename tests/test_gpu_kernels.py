@@ -1,0 +1,149 @@
+"""GPU parity of the rollout, hull and spline kernels against the oracle (bit-exact: same
+expression order, no FMA contraction on either side) and against the reference's own fixtures."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from blf import native
+from blf import problems as P
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _d(a, dtype=torch.float64):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dtype).cuda()
+
+
+def test_lti_integrator_matches_reference_test_and_oracle(handle, oracle):
+    """IntegratorTest.cpp:27-75: A=[[0,1],[-2,-2]], B=[0,2]^T, u=1, dT=1e-4, 20000 calls of
+    integrate(0, dT); solution isApprox(closed form, 1e-3) before every call."""
+    with open(os.path.join(GOLDEN, "integrator_lti.json")) as f:
+        g = json.load(f)
+    A = _d(np.array(g["A"]))
+    B = _d(np.array(g["B"]))
+    u = _d(np.array([[1.0]]))
+    x = _d(np.zeros((1, 2)))
+    dT = g["dT"]
+    xo = np.zeros(2)
+    checkpoints = {c[0]: np.array(c[1:]) for c in g["checkpoints"]}
+    for i in range(g["calls"]):
+        if i in checkpoints:
+            # bit-exact vs the fixture (oracle-generated, closed-form-checked at every step)
+            np.testing.assert_array_equal(x.cpu().numpy()[0], checkpoints[i])
+        handle.lti_euler_integrate(A, B, u, x, 0.0, dT, dT, shared=True)
+        _, xo, _ = oracle.lti_euler_integrate(g["A"], g["B"], [1.0], xo, 0.0, dT, dT)
+    np.testing.assert_array_equal(x.cpu().numpy()[0], xo)
+    t = dT * g["calls"]
+    closed = np.array([1 - np.exp(-t) * (np.cos(t) + np.sin(t)), 2 * np.exp(-t) * np.sin(t)])
+    assert np.linalg.norm(xo - closed) <= 1e-3 * min(np.linalg.norm(xo), np.linalg.norm(closed))
+
+
+@pytest.mark.parametrize("t0,t1,dT", [(0.0, 0.05, 0.01), (1.0, 1.04, 0.01), (0.0, 1e-4, 1e-4),
+                                      (0.3, 2.0, 0.07)])
+def test_lti_integrator_step_schedule(handle, oracle, t0, t1, dT):
+    rng = np.random.default_rng(0)
+    B, n, m = 257, 3, 2
+    A = rng.uniform(-1, 1, (B, n, n))
+    Bm = rng.uniform(-1, 1, (B, n, m))
+    u = rng.uniform(-1, 1, (B, m))
+    x0 = rng.uniform(-1, 1, (B, n))
+    x = _d(x0)
+    handle.lti_euler_integrate(_d(A), _d(Bm), _d(u), x, t0, t1, dT)
+    xg = x.cpu().numpy()
+    for i in range(0, B, 37):
+        st, xo, _ = oracle.lti_euler_integrate(A[i], Bm[i], u[i], x0[i], t0, t1, dT)
+        assert st == 0
+        np.testing.assert_array_equal(xg[i], xo)
+
+
+def test_lti_integrator_errors(handle):
+    A = _d(np.eye(2)); B = _d(np.ones((2, 1))); u = _d(np.ones((1, 1))); x = _d(np.zeros((1, 2)))
+    with pytest.raises(native.BlfError) as e:
+        handle.lti_euler_integrate(A, B, u, x, 1.0, 0.5, 0.1, shared=True)
+    assert e.value.code == 4
+    with pytest.raises(native.BlfError) as e:
+        handle.lti_euler_integrate(A, B, u, x, 0.0, 1.0, 0.0, shared=True)
+    assert e.value.code == 4
+    with pytest.raises(native.BlfError) as e:
+        handle.lti_euler_integrate(A, B, u, x, 1.0, 1.0, 0.1, shared=True)
+    assert e.value.code == 5
+
+
+def test_dcm_rollout_bitwise(handle, oracle):
+    prob = P.make_batch(300, horizon=100, seed=2)
+    rng = np.random.default_rng(1)
+    vrp = prob["vrp_ref"] + rng.normal(0, 0.01, prob["vrp_ref"].shape)
+    out = handle.dcm_euler_rollout(_d(prob["xi_init"]), _d(prob["omega"]), _d(vrp), 0.02)
+    og = out.cpu().numpy()
+    for i in range(0, 300, 7):
+        ref = oracle.dcm_euler_rollout(prob["xi_init"][i], prob["omega"][i], vrp[i], 0.02)
+        np.testing.assert_array_equal(og[i], ref)
+
+
+def test_hull2d_matches_oracle_and_qhull_fixture(handle, oracle):
+    with open(os.path.join(GOLDEN, "hull2d.json")) as f:
+        cases = json.load(f)["cases"]
+    B = len(cases)
+    P_ = 16
+    pts = np.zeros((B, P_, 2))
+    npts = np.zeros(B, dtype=np.int32)
+    for i, c in enumerate(cases):
+        p = np.array(c["points"])
+        pts[i, :len(p)] = p
+        npts[i] = len(p)
+    A, b, nf = handle.hull2d_hrep(_d(pts), _d(npts, torch.int32), 8)
+    A, b, nf = A.cpu().numpy(), b.cpu().numpy(), nf.cpu().numpy()
+    for i, c in enumerate(cases):
+        Ao, bo, mo = oracle.hull2d_hrep(pts[i, :npts[i]], 8)
+        assert nf[i] == mo
+        np.testing.assert_array_equal(A[i], Ao)
+        np.testing.assert_array_equal(b[i], bo)
+        # Qhull "Qt" fixture: same facet set (order is Qhull-internal), tol 1e-12
+        if c["nfacets"] > 8:
+            assert nf[i] == -1
+            continue
+        assert nf[i] == c["nfacets"]
+        mine = sorted(map(tuple, np.round(np.c_[A[i, :nf[i]], b[i, :nf[i]]], 12)))
+        ref = sorted(map(tuple, np.round(np.c_[np.array(c["A"]), np.array(c["b"])], 12)))
+        np.testing.assert_allclose(np.array(mine), np.array(ref), atol=1e-12)
+
+
+def test_hull2d_contains(handle, oracle):
+    rng = np.random.default_rng(4)
+    B = 4096
+    prob = P.make_batch(B // 8, horizon=7, seed=9)
+    pts = prob["corners"][:, :8].reshape(-1, 8, 2)
+    npts = prob["ncorners"][:, :8].reshape(-1).astype(np.int32)
+    A, b, nf = handle.hull2d_hrep(_d(pts), _d(npts, torch.int32), 8)
+    q = pts.mean(axis=1) + rng.normal(0, 0.08, (pts.shape[0], 2))
+    inside = handle.hull2d_contains(A, b, nf, _d(q)).cpu().numpy()
+    An, bn, nn = A.cpu().numpy(), b.cpu().numpy(), nf.cpu().numpy()
+    for i in range(0, pts.shape[0], 13):
+        assert inside[i] == oracle.hull2d_contains(An[i], bn[i], int(nn[i]), q[i])
+    # every corner belongs to its own hull up to rounding of b = n.v (ConvexHullHelperTest idea)
+    assert (np.einsum("bij,bkj->bik", An, pts) - bn[:, :, None] <= 1e-15).all()
+
+
+def test_quintic_fit_eval_bitwise_and_knot_rule(handle, oracle):
+    prob = P.make_batch(64, horizon=100, n_footsteps=6, seed=8)
+    kt, kp, tq = P.swing_splines(prob, queries=40)
+    tq = tq.copy()
+    tq[:, 0] -= 0.01     # before the first knot -> idx -1 (getPresentContact end())
+    tq[:, -1] += 0.01    # after the last knot -> idx K
+    tq[:, 5] = kt[:, 1]  # exactly on the apex knot -> that knot (`<=`)
+    coeffs = handle.quintic_fit(_d(kt), _d(kp))
+    pva, idx = handle.quintic_eval(_d(kt), coeffs, _d(tq))
+    cg, pg, ig = coeffs.cpu().numpy(), pva.cpu().numpy(), idx.cpu().numpy()
+    for s in range(0, kt.shape[0], 5):
+        co = oracle.quintic_fit(kt[s], kp[s])
+        np.testing.assert_array_equal(cg[s], co)
+        po, io = oracle.quintic_eval(kt[s], co, tq[s])
+        np.testing.assert_array_equal(ig[s], io)
+        np.testing.assert_array_equal(pg[s], po)
+        for j, t in enumerate(tq[s]):
+            assert io[j] == oracle.present_index(kt[s], t)
+    assert (ig[:, 0] == -1).all() and (ig[:, -1] == 2).all() and (ig[:, 5] == 1).all()
