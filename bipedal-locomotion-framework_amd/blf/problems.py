@@ -100,10 +100,11 @@ def make_batch(batch, horizon=100, n_footsteps=6, dt=0.02, seed=SEED, start=0):
     F = n_footsteps
     rows = np.arange(start, start + batch, dtype=np.uint64)
     # per-problem Philox streams keyed by the global problem index
-    draws = np.empty((batch, F, 3 + 2 + 1))
+    R = max(F, 3)
+    draws = np.empty((batch, R, 6))
     for r, gi in enumerate(rows):
         rng = np.random.Generator(np.random.Philox(key=[seed, int(gi)]))
-        draws[r] = rng.random((F, 6))
+        draws[r] = rng.random((R, 6))
     u = draws * 2.0 - 1.0                                       # U(-1, 1)
     poses = np.zeros((batch, F, 3))
     poses[:, 0] = np.stack([np.zeros(batch), 0.10 + 0.02 * u[:, 0, 0], 0.1 * u[:, 0, 1]], -1)

@@ -179,7 +179,7 @@ void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon)
     p->w_xi[0] = p->w_xi[1] = 1e2;
     p->w_vrp[0] = p->w_vrp[1] = 1.0;
     p->w_terminal[0] = p->w_terminal[1] = 1e3;
-    p->tol_mu = 1e-15;
+    p->tol_mu = 1e-16;
     p->tol_primal = 1e-10;
     p->tol_dual = 1e-9;
 }

@@ -21,33 +21,41 @@ struct KParams {
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_mu, tol_p, tol_d;
 };
 
-// LDS carve-up (in doubles), sized by N.
+// LDS carve-up (in doubles), sized by N.  The same code computes the launch size on the host
+// (Lds(nullptr, ...).total), so the allocation always covers every array.
 struct Lds {
-    double *xi, *al, *be, *a2, *b2, *R, *Hi, *Pn, *g, *d, *qx, *kff, *dr, *dxi, *om, *xir, *red;
-    __device__ Lds(double* base, int N, int NW)
+    double *xi, *al, *be, *a2, *b2, *W, *Hi, *Pn, *g, *d, *qx, *kff, *dr, *dxi, *om, *xir, *red;
+    size_t total;   // doubles
+    __host__ __device__ Lds(double* base, int N, int NW)
     {
-        xi = base;              // [N+1][2]
-        al = xi + 2 * (N + 1);  // [N]
-        be = al + N;
-        a2 = be + N;
-        b2 = a2 + N;
-        R = b2 + N;             // [N][3]
-        Hi = R + 3 * N;         // [N][3]
-        Pn = Hi + 3 * N;        // [N][3]
-        g = Pn + 3 * N;         // [N][2]
-        d = g + 2 * N;          // [N][2]
-        qx = d + 2 * N;         // [N][2]  Q (xi_k - xi_ref_k), k >= 1
-        kff = qx + 2 * N;       // [N][2]
-        dr = kff + 2 * N;       // [N][2]
-        dxi = dr + 2 * N;       // [N+1][2] (also the costates nu at start-up)
-        om = dxi + 2 * (N + 1); // [N]
-        xir = om + N;           // [N+1][2]
-        red = xir + 2 * (N + 1);// [4][NW] + 4 scalars
-        (void)NW;
+        size_t o = 0;
+        auto take = [&](size_t n) {
+            double* p = base ? base + o : nullptr;
+            o += n;
+            return p;
+        };
+        xi = take(2 * (N + 1));   // [N+1][2]
+        al = take(N);             // [N]
+        be = take(N);
+        a2 = take(N);
+        b2 = take(N);
+        W = take(4 * N);          // [N][4]  A^T diag(lam/s) A (3) + its determinant
+        Hi = take(3 * N);         // [N][3]
+        Pn = take(3 * N);         // [N][3]
+        g = take(2 * N);          // [N][2]
+        d = take(2 * N);          // [N][2]
+        qx = take(2 * N);         // [N][2]  Q (xi_k - xi_ref_k), k >= 1
+        kff = take(2 * N);        // [N][2]
+        dr = take(2 * N);         // [N][2]
+        dxi = take(2 * (N + 1));  // [N+1][2] (also the costates nu at start-up)
+        om = take(N);             // [N]
+        xir = take(2 * (N + 1));  // [N+1][2]
+        red = take(4 * NW + 8);   // [NW] reduction scratch + flags
+        total = o;
     }
 };
 
-__host__ __device__ inline int lds_doubles(int N, int NW) { return 28 * N + 6 + 4 * NW + 8; }
+inline size_t lds_doubles(int N, int NW) { return Lds(nullptr, N, NW).total; }
 
 template <int NW>
 __device__ __forceinline__ double block_sum(double v, double* red)
@@ -92,21 +100,27 @@ __device__ __forceinline__ double block_keepmin(double v, double* red)
     return t;
 }
 
-// Backward Riccati sweep (thread 0).  pass 0: factor (writes Hi, Pn) + solve; pass 1: solve
-// reusing Hi, Pn.  Returns false if a KKT block is not positive definite.
-__device__ bool backward_sweep(const Lds& L, const KParams& k, int pass, double pv0, double pv1)
+// Backward Riccati sweep (thread 0) = oracle dcm_backward.  factor: builds Hi_k = H_k^{-1} and
+// Pn_k = P_{k+1}; otherwise reuses them.  Returns false if some H_k is not positive definite.
+__device__ bool backward_sweep(const Lds& L, const KParams& k, bool factor, double pv0, double pv1)
 {
     bool ok = true;
     double P00 = k.Pw0, P01 = 0.0, P11 = k.Pw1;
     for (int s = k.N - 1; s >= 0; --s) {
         double h00, h01, h11;
         const double b2 = L.b2[s];
-        if (pass == 0) {
-            const double R00 = L.R[3 * s], R01 = L.R[3 * s + 1], R11 = L.R[3 * s + 2];
-            const double H00 = R00 + b2 * P00;
-            const double H01 = R01 + b2 * P01;
-            const double H11 = R11 + b2 * P11;
-            const double det = H00 * H11 - H01 * H01;
+        if (factor) {
+            // H = B + W, B = R + b2 P_{k+1}: det H = det B + tr(adj(B) W) + det W (all >= 0)
+            const double B00 = k.Rw0 + b2 * P00;
+            const double B01 = b2 * P01;
+            const double B11 = k.Rw1 + b2 * P11;
+            const double W00 = L.W[4 * s], W01 = L.W[4 * s + 1], W11 = L.W[4 * s + 2];
+            const double H00 = B00 + W00;
+            const double H01 = B01 + W01;
+            const double H11 = B11 + W11;
+            const double detB = B00 * B11 - B01 * B01;
+            const double trW = (B11 * W00 + B00 * W11) - 2.0 * (B01 * W01);
+            const double det = (detB + trW) + L.W[4 * s + 3];
             if (!(det > 0.0) || __builtin_isinf(det)) ok = false;
             const double idet = 1.0 / det;
             h00 = H11 * idet;
@@ -134,20 +148,23 @@ __device__ bool backward_sweep(const Lds& L, const KParams& k, int pass, double 
             const double pk1 = P01 * k0 + P11 * k1;
             const double npv0 = L.qx[2 * s] + al * (t0 - be * pk0);
             const double npv1 = L.qx[2 * s + 1] + al * (t1 - be * pk1);
-            if (pass == 0) {
-                const double R00 = L.R[3 * s], R01 = L.R[3 * s + 1], R11 = L.R[3 * s + 2];
+            if (factor) {
+                // P_k = Q + a^2 (P - b^2 P H^-1 P)
+                const double a2 = L.a2[s];
                 const double M00 = P00 * h00 + P01 * h01;
                 const double M01 = P00 * h01 + P01 * h11;
                 const double M10 = P01 * h00 + P11 * h01;
                 const double M11 = P01 * h01 + P11 * h11;
-                const double T00 = M00 * R00 + M01 * R01;
-                const double T01 = M00 * R01 + M01 * R11;
-                const double T10 = M10 * R00 + M11 * R01;
-                const double T11 = M10 * R01 + M11 * R11;
-                const double a2 = L.a2[s];
-                P00 = k.Qw0 + a2 * T00;
-                P11 = k.Qw1 + a2 * T11;
-                P01 = a2 * (0.5 * (T01 + T10));
+                const double S00 = M00 * P00 + M01 * P01;
+                const double S01 = M00 * P01 + M01 * P11;
+                const double S10 = M10 * P00 + M11 * P01;
+                const double S11 = M10 * P01 + M11 * P11;
+                const double n00 = k.Qw0 + a2 * (P00 - b2 * S00);
+                const double n11 = k.Qw1 + a2 * (P11 - b2 * S11);
+                const double n01 = a2 * (P01 - b2 * (0.5 * (S01 + S10)));
+                P00 = n00;
+                P01 = n01;
+                P11 = n11;
             }
             pv0 = npv0;
             pv1 = npv1;
@@ -156,8 +173,7 @@ __device__ bool backward_sweep(const Lds& L, const KParams& k, int pass, double 
     return ok;
 }
 
-// Forward sweep (thread 0): dr_k = alpha beta Hi_k (P_{k+1} dxi_k) + kff_k,
-// dxi_{k+1} = (alpha dxi_k - beta dr_k) + d_k.
+// Forward sweep (thread 0) = oracle dcm_forward.
 __device__ void forward_sweep(const Lds& L, int N)
 {
     double x0 = 0.0, x1 = 0.0;
@@ -184,6 +200,54 @@ __device__ void forward_sweep(const Lds& L, int N)
     }
 }
 
+// The knot a thread owns: facet rows, slacks, multipliers and the knot's VRP in registers.
+struct Stage {
+    double a0[kMaxFacets], a1[kMaxFacets], h[kMaxFacets], s[kMaxFacets], lam[kMaxFacets];
+    double rp[kMaxFacets], pr[kMaxFacets];
+    int m;
+    double r0, r1, rr0, rr1, xr0, xr1, w, be;
+};
+
+// Stage-parallel residual pass = the body of oracle dcm_residuals for one knot.  Writes the
+// Euler defect and Q(xi_{k+1} - xi_ref_{k+1}) (or the terminal pv) to LDS; returns pres, ck,
+// rho in registers.  mfac: the facet count to use (0 for the unconstrained warm start).
+__device__ __forceinline__ void stage_residuals(Stage& S, int mfac, int k, int N, const KParams& P,
+                                                const Lds& L, double* flag, double& pres,
+                                                double& ck, double& rh0, double& rh1)
+{
+    rh0 = P.Rw0 * (S.r0 - S.rr0);
+    rh1 = P.Rw1 * (S.r1 - S.rr1);
+#pragma unroll
+    for (int i = 0; i < kMaxFacets; ++i) {
+        if (i < mfac) {
+            const double gr = S.a0[i] * S.r0 + S.a1[i] * S.r1;
+            const double rpi = (gr + S.s[i]) - S.h[i];
+            S.rp[i] = rpi;
+            pres = nanmax(pres, fabs(rpi));
+            ck = ck + S.s[i] * S.lam[i];
+            rh0 = rh0 + S.a0[i] * S.lam[i];
+            rh1 = rh1 + S.a1[i] * S.lam[i];
+        }
+    }
+    const double x0 = L.xi[2 * k], x1 = L.xi[2 * k + 1];
+    const double y0 = L.xi[2 * (k + 1)], y1 = L.xi[2 * (k + 1) + 1];
+    const double dx0 = S.w * x0 + (-S.w) * S.r0;
+    const double dk0 = (x0 + dx0 * P.dt) - y0;
+    const double dx1 = S.w * x1 + (-S.w) * S.r1;
+    const double dk1 = (x1 + dx1 * P.dt) - y1;
+    L.d[2 * k] = dk0;
+    L.d[2 * k + 1] = dk1;
+    pres = nanmax(pres, fabs(dk0));
+    pres = nanmax(pres, fabs(dk1));
+    if (k + 1 < N) {
+        L.qx[2 * (k + 1)] = P.Qw0 * (y0 - S.xr0);
+        L.qx[2 * (k + 1) + 1] = P.Qw1 * (y1 - S.xr1);
+    } else {
+        flag[1] = P.Pw0 * (y0 - S.xr0);
+        flag[2] = P.Pw1 * (y1 - S.xr1);
+    }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
@@ -198,54 +262,55 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
     const int N = P.N, M = P.M;
     Lds L(smem, N, NW);
     double* red = L.red;               // [NW] scratch for block reductions
-    double* flag = L.red + 4 * NW;     // shared scalars: [0] bad, [1] pvN0, [2] pvN1
+    double* flag = L.red + 4 * NW;     // shared scalars: [0] factor failed, [1..2] terminal pv
 
     const int k = threadIdx.x;
     const bool own = k < N;
     const int64_t p = blockIdx.x;
 
-    // ---- load the stage (knot) this thread owns ----
-    double a0[kMaxFacets], a1[kMaxFacets], h[kMaxFacets], s[kMaxFacets], lam[kMaxFacets];
-    double rp[kMaxFacets], pr[kMaxFacets];
-    int m = 0;
-    double r0 = 0.0, r1 = 0.0, rr0 = 0.0, rr1 = 0.0, xr0 = 0.0, xr1 = 0.0;
-    double w = 0.0, al = 0.0, be = 0.0;
+    // ---- load the knot this thread owns ----
+    Stage S;
+    S.m = 0;
+    S.r0 = S.r1 = S.rr0 = S.rr1 = S.xr0 = S.xr1 = S.w = S.be = 0.0;
+#pragma unroll
+    for (int i = 0; i < kMaxFacets; ++i) {
+        S.a0[i] = 0.0; S.a1[i] = 0.0; S.h[i] = 0.0;
+        S.s[i] = 1.0; S.lam[i] = 0.0; S.rp[i] = 0.0; S.pr[i] = 0.0;
+    }
     bool bad = false;
     if (own) {
         const int64_t st = p * N + k;
-        m = nfacets[st];
-        bad = (m < 0 || m > M);
+        S.m = nfacets[st];
+        bad = (S.m < 0 || S.m > M);
         const double* Ak = Ain + st * M * 2;
         const double* bk = bin + st * M;
 #pragma unroll
         for (int i = 0; i < kMaxFacets; ++i) {
             if (i < M) {
-                a0[i] = Ak[2 * i];
-                a1[i] = Ak[2 * i + 1];
-                h[i] = bk[i];
-            } else {
-                a0[i] = 0.0; a1[i] = 0.0; h[i] = 0.0;
+                S.a0[i] = Ak[2 * i];
+                S.a1[i] = Ak[2 * i + 1];
+                S.h[i] = bk[i];
             }
         }
-        w = omega[st];
-        be = P.dt * w;
-        al = 1.0 + be;
+        S.w = omega[st];
+        S.be = P.dt * S.w;
+        const double al = 1.0 + S.be;
         L.al[k] = al;
-        L.be[k] = be;
+        L.be[k] = S.be;
         L.a2[k] = al * al;
-        L.b2[k] = be * be;
-        L.om[k] = w;
-        rr0 = vrp_ref[2 * st];
-        rr1 = vrp_ref[2 * st + 1];
-        r0 = rr0;
-        r1 = rr1;
-        L.dr[2 * k] = rr0;      // scratch: initial VRP for the rollout below
-        L.dr[2 * k + 1] = rr1;
+        L.b2[k] = S.be * S.be;
+        L.om[k] = S.w;
+        S.rr0 = vrp_ref[2 * st];
+        S.rr1 = vrp_ref[2 * st + 1];
+        S.r0 = S.rr0;
+        S.r1 = S.rr1;
+        L.dr[2 * k] = S.rr0;      // scratch: initial VRP for the rollout below
+        L.dr[2 * k + 1] = S.rr1;
         const int64_t sx = p * (N + 1) + (k + 1);
-        xr0 = xi_ref[2 * sx];
-        xr1 = xi_ref[2 * sx + 1];
-        L.xir[2 * (k + 1)] = xr0;
-        L.xir[2 * (k + 1) + 1] = xr1;
+        S.xr0 = xi_ref[2 * sx];
+        S.xr1 = xi_ref[2 * sx + 1];
+        L.xir[2 * (k + 1)] = S.xr0;
+        L.xir[2 * (k + 1) + 1] = S.xr1;
     }
     if (k == 0) {
         L.xi[0] = xi_init[2 * p];
@@ -255,7 +320,7 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
     }
     const bool any_bad = __syncthreads_or(bad);
 
-    // ---- initial state: reference Euler rollout of vrp_ref (thread 0) ----
+    // ---- initial state 1: reference Euler rollout of vrp_ref (thread 0) ----
     if (k == 0) {
         for (int q = 0; q < N; ++q) {
             const double wq = L.om[q];
@@ -273,31 +338,48 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
     if (any_bad) {
         status = BLF_QP_BAD_FACETS;
     } else {
-        // ---- s, lam initial values; ntot; initial dual residual bound ----
-        int mi = 0;
+        // ---- initial state 2: full Newton step of the unconstrained QP (W = 0, lam = 0) ----
+        {
+            double pres = 0.0, ck = 0.0, rh0 = 0.0, rh1 = 0.0;
+            if (own) {
+                stage_residuals(S, 0, k, N, P, L, flag, pres, ck, rh0, rh1);
+                L.W[4 * k] = 0.0; L.W[4 * k + 1] = 0.0; L.W[4 * k + 2] = 0.0; L.W[4 * k + 3] = 0.0;
+                L.g[2 * k] = rh0;
+                L.g[2 * k + 1] = rh1;
+            }
+            __syncthreads();
+            if (k == 0) {
+                const bool ok = backward_sweep(L, P, true, flag[1], flag[2]);
+                flag[0] = ok ? 0.0 : 1.0;
+                forward_sweep(L, N);
+            }
+            __syncthreads();
+            if (own) {
+                S.r0 = S.r0 + L.dr[2 * k];
+                S.r1 = S.r1 + L.dr[2 * k + 1];
+                L.xi[2 * (k + 1)] = L.xi[2 * (k + 1)] + L.dxi[2 * (k + 1)];
+                L.xi[2 * (k + 1) + 1] = L.xi[2 * (k + 1) + 1] + L.dxi[2 * (k + 1) + 1];
+            }
+        }
+        const bool init_bad = flag[0] != 0.0;
+        // ---- initial state 3: s = max(b - A r, 1e-2), lam = 1; ntot ----
 #pragma unroll
         for (int i = 0; i < kMaxFacets; ++i) {
-            if (i < m) {
-                const double gr = a0[i] * r0 + a1[i] * r1;
-                const double sl = h[i] - gr;
-                s[i] = sl > 1e-2 ? sl : 1e-2;
-                lam[i] = 1.0;
-            } else {
-                s[i] = 1.0;
-                lam[i] = 0.0;
+            if (i < S.m) {
+                const double gr = S.a0[i] * S.r0 + S.a1[i] * S.r1;
+                const double sl = S.h[i] - gr;
+                S.s[i] = sl > 1e-2 ? sl : 1e-2;
+                S.lam[i] = 1.0;
             }
-            rp[i] = 0.0;
-            pr[i] = 0.0;
         }
-        mi = m;
-        int ntot = wave_isum(mi);
+        int ntot = wave_isum(S.m);
         if constexpr (NW > 1) {
             if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (double)ntot;
             __syncthreads();
             ntot = 0;
             for (int i = 0; i < NW; ++i) ntot += (int)red[i];
-            __syncthreads();
         }
+        __syncthreads();
         // costates nu (single shooting) for the initial dual residual, thread 0 -> L.dxi
         if (k == 0) {
             double n0 = P.Pw0 * (L.xi[2 * N] - L.xir[2 * N]);
@@ -315,55 +397,24 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
         __syncthreads();
         double dres = 0.0;
         if (own) {
-            double rj0 = P.Rw0 * (r0 - rr0);
-            double rj1 = P.Rw1 * (r1 - rr1);
+            double rj0 = P.Rw0 * (S.r0 - S.rr0);
+            double rj1 = P.Rw1 * (S.r1 - S.rr1);
 #pragma unroll
             for (int i = 0; i < kMaxFacets; ++i)
-                if (i < m) {
-                    rj0 = rj0 + a0[i] * lam[i];
-                    rj1 = rj1 + a1[i] * lam[i];
+                if (i < S.m) {
+                    rj0 = rj0 + S.a0[i] * S.lam[i];
+                    rj1 = rj1 + S.a1[i] * S.lam[i];
                 }
-            dres = nanmax(dres, fabs(rj0 - be * L.dxi[2 * (k + 1)]));
-            dres = nanmax(dres, fabs(rj1 - be * L.dxi[2 * (k + 1) + 1]));
+            dres = nanmax(dres, fabs(rj0 - S.be * L.dxi[2 * (k + 1)]));
+            dres = nanmax(dres, fabs(rj1 - S.be * L.dxi[2 * (k + 1) + 1]));
         }
         dres = block_nanmax<NW>(dres, red);
+        if (init_bad) status = BLF_QP_NUMERICAL;
 
-        for (it = 0;; ++it) {
+        for (it = 0; status == 0; ++it) {
             // ---- residuals (stage-parallel) ----
             double pres = 0.0, ck = 0.0, rh0 = 0.0, rh1 = 0.0;
-            if (own) {
-                rh0 = P.Rw0 * (r0 - rr0);
-                rh1 = P.Rw1 * (r1 - rr1);
-#pragma unroll
-                for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < m) {
-                        const double gr = a0[i] * r0 + a1[i] * r1;
-                        const double rpi = (gr + s[i]) - h[i];
-                        rp[i] = rpi;
-                        pres = nanmax(pres, fabs(rpi));
-                        ck = ck + s[i] * lam[i];
-                        rh0 = rh0 + a0[i] * lam[i];
-                        rh1 = rh1 + a1[i] * lam[i];
-                    }
-                }
-                const double x0 = L.xi[2 * k], x1 = L.xi[2 * k + 1];
-                const double y0 = L.xi[2 * (k + 1)], y1 = L.xi[2 * (k + 1) + 1];
-                const double dx0 = w * x0 + (-w) * r0;
-                const double dk0 = (x0 + dx0 * P.dt) - y0;
-                const double dx1 = w * x1 + (-w) * r1;
-                const double dk1 = (x1 + dx1 * P.dt) - y1;
-                L.d[2 * k] = dk0;
-                L.d[2 * k + 1] = dk1;
-                pres = nanmax(pres, fabs(dk0));
-                pres = nanmax(pres, fabs(dk1));
-                if (k + 1 < N) {
-                    L.qx[2 * (k + 1)] = P.Qw0 * (y0 - xr0);
-                    L.qx[2 * (k + 1) + 1] = P.Qw1 * (y1 - xr1);
-                } else {
-                    flag[1] = P.Pw0 * (y0 - xr0);
-                    flag[2] = P.Pw1 * (y1 - xr1);
-                }
-            }
+            if (own) stage_residuals(S, S.m, k, N, P, L, flag, pres, ck, rh0, rh1);
             const double csum = block_sum<NW>(ck, red);
             const double mu = ntot > 0 ? csum / (double)ntot : 0.0;
             pres = block_nanmax<NW>(pres, red);
@@ -371,37 +422,47 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
                 status = BLF_QP_NUMERICAL;
                 break;
             }
-            if (mu <= P.tol_mu && pres <= P.tol_p && dres <= P.tol_d) {
-                status = BLF_QP_SOLVED;
-                break;
-            }
+            if (mu <= P.tol_mu && pres <= P.tol_p && dres <= P.tol_d) break;   // solved
             if (it >= P.max_iter) {
                 status = BLF_QP_MAX_ITER;
                 break;
             }
 
-            // ---- R' and the affine right-hand side (stage-parallel) ----
+            // ---- W = A^T diag(lam/s) A, det W, affine right-hand side (stage-parallel) ----
             if (own) {
-                double R00 = P.Rw0, R01 = 0.0, R11 = P.Rw1;
+                double W00 = 0.0, W01 = 0.0, W11 = 0.0, dW = 0.0;
                 double g0 = rh0, g1 = rh1;
+                double sg[kMaxFacets];
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < m) {
-                        const double sg = lam[i] / s[i];
-                        const double t0 = sg * a0[i];
-                        const double t1 = sg * a1[i];
-                        R00 = R00 + t0 * a0[i];
-                        R01 = R01 + t0 * a1[i];
-                        R11 = R11 + t1 * a1[i];
-                        const double rc = s[i] * lam[i];
-                        const double e = (lam[i] * rp[i] - rc) / s[i];
-                        g0 = g0 + a0[i] * e;
-                        g1 = g1 + a1[i] * e;
+                    sg[i] = 0.0;
+                    if (i < S.m) {
+                        sg[i] = S.lam[i] / S.s[i];
+                        const double t0 = sg[i] * S.a0[i];
+                        const double t1 = sg[i] * S.a1[i];
+                        W00 = W00 + t0 * S.a0[i];
+                        W01 = W01 + t0 * S.a1[i];
+                        W11 = W11 + t1 * S.a1[i];
+                        const double rc = S.s[i] * S.lam[i];
+                        const double e = (S.lam[i] * S.rp[i] - rc) / S.s[i];
+                        g0 = g0 + S.a0[i] * e;
+                        g1 = g1 + S.a1[i] * e;
                     }
                 }
-                L.R[3 * k] = R00;
-                L.R[3 * k + 1] = R01;
-                L.R[3 * k + 2] = R11;
+#pragma unroll
+                for (int i = 1; i < kMaxFacets; ++i) {
+#pragma unroll
+                    for (int j = 0; j < i; ++j) {
+                        if (i < S.m) {
+                            const double cr = S.a0[i] * S.a1[j] - S.a1[i] * S.a0[j];
+                            dW = dW + (sg[i] * sg[j]) * (cr * cr);
+                        }
+                    }
+                }
+                L.W[4 * k] = W00;
+                L.W[4 * k + 1] = W01;
+                L.W[4 * k + 2] = W11;
+                L.W[4 * k + 3] = dW;
                 L.g[2 * k] = g0;
                 L.g[2 * k + 1] = g1;
             }
@@ -409,7 +470,7 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
 
             // ---- affine (predictor) Newton step: factor + solve on thread 0 ----
             if (k == 0) {
-                const bool ok = backward_sweep(L, P, 0, flag[1], flag[2]);
+                const bool ok = backward_sweep(L, P, true, flag[1], flag[2]);
                 flag[0] = ok ? 0.0 : 1.0;
                 forward_sweep(L, N);
             }
@@ -423,13 +484,13 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
                 dr1 = L.dr[2 * k + 1];
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < m) {
-                        const double rc = s[i] * lam[i];
-                        const double ds = (-rp[i]) - (a0[i] * dr0 + a1[i] * dr1);
-                        const double dl = ((-rc) - lam[i] * ds) / s[i];
-                        if (ds < 0.0) smax = keepmin(smax, (-s[i]) / ds);
-                        if (dl < 0.0) smax = keepmin(smax, (-lam[i]) / dl);
-                        pr[i] = ds * dl;
+                    if (i < S.m) {
+                        const double rc = S.s[i] * S.lam[i];
+                        const double ds = (-S.rp[i]) - (S.a0[i] * dr0 + S.a1[i] * dr1);
+                        const double dl = ((-rc) - S.lam[i] * ds) / S.s[i];
+                        if (ds < 0.0) smax = keepmin(smax, (-S.s[i]) / ds);
+                        if (dl < 0.0) smax = keepmin(smax, (-S.lam[i]) / dl);
+                        S.pr[i] = ds * dl;
                     }
                 }
             }
@@ -439,11 +500,11 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
             if (own) {
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < m) {
-                        const double rc = s[i] * lam[i];
-                        const double ds = (-rp[i]) - (a0[i] * dr0 + a1[i] * dr1);
-                        const double dl = ((-rc) - lam[i] * ds) / s[i];
-                        ck = ck + (s[i] + a_aff * ds) * (lam[i] + a_aff * dl);
+                    if (i < S.m) {
+                        const double rc = S.s[i] * S.lam[i];
+                        const double ds = (-S.rp[i]) - (S.a0[i] * dr0 + S.a1[i] * dr1);
+                        const double dl = ((-rc) - S.lam[i] * ds) / S.s[i];
+                        ck = ck + (S.s[i] + a_aff * ds) * (S.lam[i] + a_aff * dl);
                     }
                 }
             }
@@ -456,16 +517,16 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
             }
             const double sigma_mu = sigma * mu;
 
-            // ---- corrector right-hand side (stage-parallel) ----
+            // ---- corrector right-hand side (stage-parallel) + solve (thread 0) ----
             if (own) {
                 double g0 = rh0, g1 = rh1;
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < m) {
-                        const double rc = (s[i] * lam[i] + pr[i]) - sigma_mu;
-                        const double e = (lam[i] * rp[i] - rc) / s[i];
-                        g0 = g0 + a0[i] * e;
-                        g1 = g1 + a1[i] * e;
+                    if (i < S.m) {
+                        const double rc = (S.s[i] * S.lam[i] + S.pr[i]) - sigma_mu;
+                        const double e = (S.lam[i] * S.rp[i] - rc) / S.s[i];
+                        g0 = g0 + S.a0[i] * e;
+                        g1 = g1 + S.a1[i] * e;
                     }
                 }
                 L.g[2 * k] = g0;
@@ -473,7 +534,7 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
             }
             __syncthreads();
             if (k == 0) {
-                backward_sweep(L, P, 1, flag[1], flag[2]);
+                backward_sweep(L, P, false, flag[1], flag[2]);
                 forward_sweep(L, N);
             }
             __syncthreads();
@@ -485,14 +546,14 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
                 dr1 = L.dr[2 * k + 1];
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < m) {
-                        const double rc = (s[i] * lam[i] + pr[i]) - sigma_mu;
-                        const double ds = (-rp[i]) - (a0[i] * dr0 + a1[i] * dr1);
-                        const double dl = ((-rc) - lam[i] * ds) / s[i];
-                        if (ds < 0.0) smax = keepmin(smax, (-s[i]) / ds);
-                        if (dl < 0.0) smax = keepmin(smax, (-lam[i]) / dl);
-                        rp[i] = ds;
-                        pr[i] = dl;
+                    if (i < S.m) {
+                        const double rc = (S.s[i] * S.lam[i] + S.pr[i]) - sigma_mu;
+                        const double ds = (-S.rp[i]) - (S.a0[i] * dr0 + S.a1[i] * dr1);
+                        const double dl = ((-rc) - S.lam[i] * ds) / S.s[i];
+                        if (ds < 0.0) smax = keepmin(smax, (-S.s[i]) / ds);
+                        if (dl < 0.0) smax = keepmin(smax, (-S.lam[i]) / dl);
+                        S.rp[i] = ds;
+                        S.pr[i] = dl;
                     }
                 }
             }
@@ -504,15 +565,15 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
             const double step = 0.99 * smax;
             const double a = step < 1.0 ? step : 1.0;
             if (own) {
-                r0 = r0 + a * dr0;
-                r1 = r1 + a * dr1;
+                S.r0 = S.r0 + a * dr0;
+                S.r1 = S.r1 + a * dr1;
                 L.xi[2 * (k + 1)] = L.xi[2 * (k + 1)] + a * L.dxi[2 * (k + 1)];
                 L.xi[2 * (k + 1) + 1] = L.xi[2 * (k + 1) + 1] + a * L.dxi[2 * (k + 1) + 1];
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < m) {
-                        s[i] = s[i] + a * rp[i];
-                        lam[i] = lam[i] + a * pr[i];
+                    if (i < S.m) {
+                        S.s[i] = S.s[i] + a * S.rp[i];
+                        S.lam[i] = S.lam[i] + a * S.pr[i];
                     }
                 }
             }
@@ -522,10 +583,11 @@ __global__ __launch_bounds__(NT) void dcm_mpc_ipm_kernel(
     }
 
     // ---- outputs ----
+    __syncthreads();
     if (own) {
         const int64_t st = p * N + k;
-        vrp_out[2 * st] = r0;
-        vrp_out[2 * st + 1] = r1;
+        vrp_out[2 * st] = S.r0;
+        vrp_out[2 * st + 1] = S.r1;
         const int64_t sx = p * (N + 1) + (k + 1);
         xi_out[2 * sx] = L.xi[2 * (k + 1)];
         xi_out[2 * sx + 1] = L.xi[2 * (k + 1) + 1];

@@ -154,7 +154,7 @@ typedef struct blf_dcm_mpc_solution {
     int32_t* iters;          /* [B]  IPM iterations taken                                   */
 } blf_dcm_mpc_solution;
 
-/* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-15,
+/* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-16,
  * tol_primal 1e-10, tol_dual 1e-9, max_iter 50, max_facets 8). */
 void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);
 

@@ -300,6 +300,174 @@ double orc_wave_tree_sum(const double* c, int n)
 
 #define MF 8
 
+/* Working state of one QP solve (all arrays owned by the caller of dcm_ws_alloc). */
+typedef struct {
+    int N, M, ntot;
+    double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1;
+    const double *omega, *xi_ref, *vrp_ref, *A, *b;
+    const int32_t* nf;
+    double *al, *be, *a2, *b2;          /* [N] */
+    double *s, *lam, *rp, *prod;        /* [N][MF] */
+    double *W;                          /* [N][4]  A^T diag(lam/s) A (3), det of it (1) */
+    double *Hi, *Pn;                    /* [N][3] */
+    double *g, *d, *rho, *kff, *dr, *qx; /* [N][2] */
+    double *c;                          /* [N] */
+    double *dxi, *nu;                   /* [N+1][2] */
+    double *xi, *vrp;                   /* outputs, updated in place */
+} dcm_ws;
+
+/* Stage-parallel residual pass (the device runs one thread per knot): primal residuals
+ * rp = A r + s - b, complementarity partials c_k, rho = R (r - r_ref) + A^T lam, Euler defects
+ * d_k (reference step order) and Q (xi_k - xi_ref_k).  Returns max |rp|, |d| (NaN-propagating). */
+static double dcm_residuals(dcm_ws* w)
+{
+    const int N = w->N, M = w->M;
+    double pres = 0.0;
+    for (int k = 0; k < N; ++k) {
+        const int m = w->nf[k];
+        const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
+        double ck = 0.0;
+        double rh0 = w->Rw0 * (r0 - w->vrp_ref[2 * k]);
+        double rh1 = w->Rw1 * (r1 - w->vrp_ref[2 * k + 1]);
+        for (int i = 0; i < m; ++i) {
+            const double* a = w->A + (k * M + i) * 2;
+            const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
+            const double gr = a[0] * r0 + a[1] * r1;
+            const double rpi = (gr + si) - w->b[k * M + i];
+            w->rp[k * MF + i] = rpi;
+            const double e = fabs(rpi);
+            if (e > pres || e != e) pres = e;
+            ck = ck + si * li;
+            rh0 = rh0 + a[0] * li;
+            rh1 = rh1 + a[1] * li;
+        }
+        w->c[k] = ck;
+        w->rho[2 * k] = rh0;
+        w->rho[2 * k + 1] = rh1;
+        const double om = w->omega[k];
+        for (int j = 0; j < 2; ++j) {
+            const double x = w->xi[2 * k + j];
+            const double dx = om * x + (-om) * w->vrp[2 * k + j];
+            const double dk = (x + dx * w->dt) - w->xi[2 * (k + 1) + j];
+            w->d[2 * k + j] = dk;
+            const double e = fabs(dk);
+            if (e > pres || e != e) pres = e;
+        }
+        if (k >= 1) {
+            w->qx[2 * k] = w->Qw0 * (w->xi[2 * k] - w->xi_ref[2 * k]);
+            w->qx[2 * k + 1] = w->Qw1 * (w->xi[2 * k + 1] - w->xi_ref[2 * k + 1]);
+        }
+    }
+    return pres;
+}
+
+/* Backward Riccati sweep (sequential over knots).  factor != 0: builds Hi_k = H_k^{-1},
+ * Pn_k = P_{k+1} (returns 0 if some H_k is not positive definite); factor == 0: reuses them.
+ * Either way solves for the feed-forward kff with right-hand side g. */
+static int dcm_backward(dcm_ws* w, int factor)
+{
+    const int N = w->N;
+    int ok = 1;
+    double P00 = w->Pw0, P01 = 0.0, P11 = w->Pw1;
+    double pv0 = w->Pw0 * (w->xi[2 * N] - w->xi_ref[2 * N]);
+    double pv1 = w->Pw1 * (w->xi[2 * N + 1] - w->xi_ref[2 * N + 1]);
+    for (int k = N - 1; k >= 0; --k) {
+        double h00, h01, h11;
+        const double b2 = w->b2[k];
+        if (factor) {
+            /* H = B + W, B = R + b2 P_{k+1} (SPD, well conditioned), W PSD:
+             * det H = det B + tr(adj(B) W) + det W, every term >= 0 — no cancellation when
+             * the barrier weights inside W are huge */
+            const double B00 = w->Rw0 + b2 * P00;
+            const double B01 = b2 * P01;
+            const double B11 = w->Rw1 + b2 * P11;
+            const double W00 = w->W[4 * k], W01 = w->W[4 * k + 1], W11 = w->W[4 * k + 2];
+            const double H00 = B00 + W00;
+            const double H01 = B01 + W01;
+            const double H11 = B11 + W11;
+            const double detB = B00 * B11 - B01 * B01;
+            const double trW = (B11 * W00 + B00 * W11) - 2.0 * (B01 * W01);
+            const double det = (detB + trW) + w->W[4 * k + 3];
+            if (!(det > 0.0) || isinf(det)) ok = 0;
+            const double idet = 1.0 / det;
+            h00 = H11 * idet;
+            h01 = -(H01 * idet);
+            h11 = H00 * idet;
+            w->Hi[3 * k] = h00; w->Hi[3 * k + 1] = h01; w->Hi[3 * k + 2] = h11;
+            w->Pn[3 * k] = P00; w->Pn[3 * k + 1] = P01; w->Pn[3 * k + 2] = P11;
+        } else {
+            h00 = w->Hi[3 * k]; h01 = w->Hi[3 * k + 1]; h11 = w->Hi[3 * k + 2];
+            P00 = w->Pn[3 * k]; P01 = w->Pn[3 * k + 1]; P11 = w->Pn[3 * k + 2];
+        }
+        const double be = w->be[k];
+        const double d0 = w->d[2 * k], d1 = w->d[2 * k + 1];
+        const double t0 = (P00 * d0 + P01 * d1) + pv0;
+        const double t1 = (P01 * d0 + P11 * d1) + pv1;
+        const double hu0 = w->g[2 * k] - be * t0;
+        const double hu1 = w->g[2 * k + 1] - be * t1;
+        const double k0 = -(h00 * hu0 + h01 * hu1);
+        const double k1 = -(h01 * hu0 + h11 * hu1);
+        w->kff[2 * k] = k0;
+        w->kff[2 * k + 1] = k1;
+        if (k > 0) {
+            const double al = w->al[k];
+            const double pk0 = P00 * k0 + P01 * k1;
+            const double pk1 = P01 * k0 + P11 * k1;
+            const double npv0 = w->qx[2 * k] + al * (t0 - be * pk0);
+            const double npv1 = w->qx[2 * k + 1] + al * (t1 - be * pk1);
+            if (factor) {
+                /* P_k = Q + a^2 (P - b^2 P H^-1 P)  (never multiplies by the huge W) */
+                const double a2 = w->a2[k];
+                const double M00 = P00 * h00 + P01 * h01;
+                const double M01 = P00 * h01 + P01 * h11;
+                const double M10 = P01 * h00 + P11 * h01;
+                const double M11 = P01 * h01 + P11 * h11;
+                const double S00 = M00 * P00 + M01 * P01;
+                const double S01 = M00 * P01 + M01 * P11;
+                const double S10 = M10 * P00 + M11 * P01;
+                const double S11 = M10 * P01 + M11 * P11;
+                const double n00 = w->Qw0 + a2 * (P00 - b2 * S00);
+                const double n11 = w->Qw1 + a2 * (P11 - b2 * S11);
+                const double n01 = a2 * (P01 - b2 * (0.5 * (S01 + S10)));
+                P00 = n00;
+                P01 = n01;
+                P11 = n11;
+            }
+            pv0 = npv0;
+            pv1 = npv1;
+        }
+    }
+    return ok;
+}
+
+/* Forward sweep: dr_k = (alpha beta) Hi_k (P_{k+1} dxi_k) + kff_k,
+ * dxi_{k+1} = (alpha dxi_k - beta dr_k) + d_k, dxi_0 = 0. */
+static void dcm_forward(dcm_ws* w)
+{
+    double x0 = 0.0, x1 = 0.0;
+    w->dxi[0] = 0.0;
+    w->dxi[1] = 0.0;
+    for (int k = 0; k < w->N; ++k) {
+        const double q00 = w->Pn[3 * k], q01 = w->Pn[3 * k + 1], q11 = w->Pn[3 * k + 2];
+        const double u0 = q00 * x0 + q01 * x1;
+        const double u1 = q01 * x0 + q11 * x1;
+        const double v0 = w->Hi[3 * k] * u0 + w->Hi[3 * k + 1] * u1;
+        const double v1 = w->Hi[3 * k + 1] * u0 + w->Hi[3 * k + 2] * u1;
+        const double al = w->al[k], be = w->be[k];
+        const double ab = al * be;
+        const double r0 = ab * v0 + w->kff[2 * k];
+        const double r1 = ab * v1 + w->kff[2 * k + 1];
+        w->dr[2 * k] = r0;
+        w->dr[2 * k + 1] = r1;
+        const double n0 = (al * x0 - be * r0) + w->d[2 * k];
+        const double n1 = (al * x1 - be * r1) + w->d[2 * k + 1];
+        w->dxi[2 * (k + 1)] = n0;
+        w->dxi[2 * (k + 1) + 1] = n1;
+        x0 = n0;
+        x1 = n1;
+    }
+}
+
 int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const double* omega,
                       const double* xi_ref, const double* vrp_ref, const double* Ain,
                       const double* bin, const int32_t* nfacets, double* xi, double* vrp,
@@ -307,33 +475,25 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
 {
     const int N = prm->horizon;
     const int M = prm->max_facets;
-    const double dt = prm->dt;
-    const double Qw0 = prm->w_xi[0], Qw1 = prm->w_xi[1];
-    const double Rw0 = prm->w_vrp[0], Rw1 = prm->w_vrp[1];
-    const double Pw0 = prm->w_terminal[0], Pw1 = prm->w_terminal[1];
-
-    /* per-stage work arrays */
-    double* al = (double*)malloc(sizeof(double) * N * 4);
-    double* be = al + N;
-    double* a2 = al + 2 * N;
-    double* b2 = al + 3 * N;
-    double* s = (double*)malloc(sizeof(double) * N * MF * 4);
-    double* lam = s + N * MF;
-    double* rp = s + 2 * N * MF;
-    double* prod = s + 3 * N * MF;
-    double* st = (double*)malloc(sizeof(double) * N * 26 + (N + 1) * 4 * sizeof(double));
-    double* R = st;              /* [N][3]  R' */
-    double* Hi = st + 3 * N;     /* [N][3]  (R' + b2 P_{k+1})^{-1} */
-    double* Pn = st + 6 * N;     /* [N][3]  P_{k+1} */
-    double* g = st + 9 * N;      /* [N][2] */
-    double* d = st + 11 * N;     /* [N][2] */
-    double* rho = st + 13 * N;   /* [N][2] */
-    double* kff = st + 15 * N;   /* [N][2] */
-    double* dr = st + 17 * N;    /* [N][2] */
-    double* c = st + 19 * N;     /* [N]    */
-    double* qx = st + 20 * N;    /* [N][2] Q(xi_k - xiref_k), k = 1..N-1 at index k */
-    double* dxi = st + 26 * N;   /* [N+1][2] */
-    double* nu = dxi + 2 * (N + 1);  /* [N+1][2] */
+    dcm_ws ws;
+    dcm_ws* w = &ws;
+    w->N = N; w->M = M; w->dt = prm->dt;
+    w->Qw0 = prm->w_xi[0]; w->Qw1 = prm->w_xi[1];
+    w->Rw0 = prm->w_vrp[0]; w->Rw1 = prm->w_vrp[1];
+    w->Pw0 = prm->w_terminal[0]; w->Pw1 = prm->w_terminal[1];
+    w->omega = omega; w->xi_ref = xi_ref; w->vrp_ref = vrp_ref; w->A = Ain; w->b = bin;
+    w->nf = nfacets; w->xi = xi; w->vrp = vrp;
+    double* mem = (double*)malloc(sizeof(double) * ((size_t)N * (4 + 4 * MF + 4 + 6 + 12 + 1) +
+                                                    4 * (size_t)(N + 1)));
+    double* q = mem;
+    w->al = q; q += N; w->be = q; q += N; w->a2 = q; q += N; w->b2 = q; q += N;
+    w->s = q; q += N * MF; w->lam = q; q += N * MF; w->rp = q; q += N * MF; w->prod = q; q += N * MF;
+    w->W = q; q += 4 * N;
+    w->Hi = q; q += 3 * N; w->Pn = q; q += 3 * N;
+    w->g = q; q += 2 * N; w->d = q; q += 2 * N; w->rho = q; q += 2 * N; w->kff = q; q += 2 * N;
+    w->dr = q; q += 2 * N; w->qx = q; q += 2 * N;
+    w->c = q; q += N;
+    w->dxi = q; q += 2 * (N + 1); w->nu = q; q += 2 * (N + 1);
 
     int status = 0, it = 0;
     int ntot = 0;
@@ -341,21 +501,51 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         if (nfacets[k] < 0 || nfacets[k] > M) status = 3;
         else ntot += nfacets[k];
     }
+    w->ntot = ntot;
 
-    /* init: vrp = vrp_ref; xi = reference Euler rollout; s = max(b - A r, 1e-2); lam = 1 */
+    /* ---- initial point ----
+     * 1. vrp = vrp_ref, xi = reference Euler rollout from xi_init;
+     * 2. one full Newton step of the QP WITHOUT the polygon constraints (the unconstrained LQ
+     *    optimum; W = 0, lam = 0): for the unstable DCM the open-loop rollout is far from
+     *    dual feasible (costates grow like alpha^N), this step makes the linear residuals O(1);
+     * 3. s = max(b - A r, 1e-2), lam = 1. */
     for (int k = 0; k < N; ++k) {
-        be[k] = dt * omega[k];
-        al[k] = 1.0 + be[k];
-        a2[k] = al[k] * al[k];
-        b2[k] = be[k] * be[k];
+        w->be[k] = w->dt * omega[k];
+        w->al[k] = 1.0 + w->be[k];
+        w->a2[k] = w->al[k] * w->al[k];
+        w->b2[k] = w->be[k] * w->be[k];
         vrp[2 * k] = vrp_ref[2 * k];
         vrp[2 * k + 1] = vrp_ref[2 * k + 1];
     }
-    orc_dcm_euler_rollout(xi_init, omega, vrp, N, dt, xi);
+    orc_dcm_euler_rollout(xi_init, omega, vrp, N, w->dt, xi);
     if (status == 3) {
         if (iters_out) *iters_out = 0;
-        free(al); free(s); free(st);
+        free(mem);
         return 3;
+    }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < MF; ++i) { w->s[k * MF + i] = 1.0; w->lam[k * MF + i] = 0.0; }
+    {
+        const int nf_saved = w->ntot;
+        int32_t* zero = (int32_t*)calloc(N, sizeof(int32_t));
+        w->nf = zero;                      /* no facets: rho = R (r - r_ref), W = 0 */
+        dcm_residuals(w);
+        w->nf = nfacets;
+        w->ntot = nf_saved;
+        free(zero);
+        for (int k = 0; k < N; ++k) {
+            w->W[4 * k] = 0.0; w->W[4 * k + 1] = 0.0; w->W[4 * k + 2] = 0.0; w->W[4 * k + 3] = 0.0;
+            w->g[2 * k] = w->rho[2 * k];
+            w->g[2 * k + 1] = w->rho[2 * k + 1];
+        }
+        if (!dcm_backward(w, 1)) status = 2;
+        dcm_forward(w);
+        for (int k = 0; k < N; ++k) {
+            vrp[2 * k] = vrp[2 * k] + w->dr[2 * k];
+            vrp[2 * k + 1] = vrp[2 * k + 1] + w->dr[2 * k + 1];
+            xi[2 * (k + 1)] = xi[2 * (k + 1)] + w->dxi[2 * (k + 1)];
+            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + w->dxi[2 * (k + 1) + 1];
+        }
     }
     for (int k = 0; k < N; ++k) {
         const int m = nfacets[k];
@@ -364,252 +554,169 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                 const double* a = Ain + (k * M + i) * 2;
                 const double gr = a[0] * vrp[2 * k] + a[1] * vrp[2 * k + 1];
                 double sl = bin[k * M + i] - gr;
-                s[k * MF + i] = sl > 1e-2 ? sl : 1e-2;
-                lam[k * MF + i] = 1.0;
-            } else {
-                s[k * MF + i] = 1.0;
-                lam[k * MF + i] = 0.0;
+                w->s[k * MF + i] = sl > 1e-2 ? sl : 1e-2;
+                w->lam[k * MF + i] = 1.0;
             }
         }
     }
 
-    /* initial dual residual (single-shooting costates): dres0 = max |rho_k - beta_k nu_{k+1}| */
-    double dres;
+    /* initial dual residual (single-shooting costates): dres0 = max |rho_k - beta_k nu_{k+1}|;
+     * it then contracts by (1 - a) with every damped Newton step (the QP's linear residuals). */
+    double dres = 0.0;
     {
-        nu[2 * N] = Pw0 * (xi[2 * N] - xi_ref[2 * N]);
-        nu[2 * N + 1] = Pw1 * (xi[2 * N + 1] - xi_ref[2 * N + 1]);
+        double* nu = w->nu;
+        nu[2 * N] = w->Pw0 * (xi[2 * N] - xi_ref[2 * N]);
+        nu[2 * N + 1] = w->Pw1 * (xi[2 * N + 1] - xi_ref[2 * N + 1]);
         for (int k = N - 1; k >= 1; --k) {
-            nu[2 * k] = Qw0 * (xi[2 * k] - xi_ref[2 * k]) + al[k] * nu[2 * (k + 1)];
-            nu[2 * k + 1] = Qw1 * (xi[2 * k + 1] - xi_ref[2 * k + 1]) + al[k] * nu[2 * (k + 1) + 1];
+            nu[2 * k] = w->Qw0 * (xi[2 * k] - xi_ref[2 * k]) + w->al[k] * nu[2 * (k + 1)];
+            nu[2 * k + 1] = w->Qw1 * (xi[2 * k + 1] - xi_ref[2 * k + 1]) + w->al[k] * nu[2 * (k + 1) + 1];
         }
-        dres = 0.0;
         for (int k = 0; k < N; ++k) {
             const int m = nfacets[k];
             for (int j = 0; j < 2; ++j) {
-                double rj = (j == 0 ? Rw0 : Rw1) * (vrp[2 * k + j] - vrp_ref[2 * k + j]);
-                for (int i = 0; i < m; ++i) rj = rj + Ain[(k * M + i) * 2 + j] * lam[k * MF + i];
-                const double e = fabs(rj - be[k] * nu[2 * (k + 1) + j]);
+                double rj = (j == 0 ? w->Rw0 : w->Rw1) * (vrp[2 * k + j] - vrp_ref[2 * k + j]);
+                for (int i = 0; i < m; ++i) rj = rj + Ain[(k * M + i) * 2 + j] * w->lam[k * MF + i];
+                const double e = fabs(rj - w->be[k] * nu[2 * (k + 1) + j]);
                 if (e > dres || e != e) dres = e;
             }
         }
     }
+    if (status == 2) {
+        if (iters_out) *iters_out = 0;
+        free(mem);
+        return 2;
+    }
 
     for (it = 0;; ++it) {
-        /* ---- residuals (stage-parallel on the device) ---- */
-        double pres = 0.0;
-        for (int k = 0; k < N; ++k) {
-            const int m = nfacets[k];
-            const double r0 = vrp[2 * k], r1 = vrp[2 * k + 1];
-            double ck = 0.0;
-            double rh0 = Rw0 * (r0 - vrp_ref[2 * k]);
-            double rh1 = Rw1 * (r1 - vrp_ref[2 * k + 1]);
-            for (int i = 0; i < m; ++i) {
-                const double* a = Ain + (k * M + i) * 2;
-                const double si = s[k * MF + i], li = lam[k * MF + i];
-                const double gr = a[0] * r0 + a[1] * r1;
-                const double rpi = (gr + si) - bin[k * M + i];
-                rp[k * MF + i] = rpi;
-                const double e = fabs(rpi);
-                if (e > pres || e != e) pres = e;
-                ck = ck + si * li;
-                rh0 = rh0 + a[0] * li;
-                rh1 = rh1 + a[1] * li;
-            }
-            c[k] = ck;
-            rho[2 * k] = rh0;
-            rho[2 * k + 1] = rh1;
-            const double w = omega[k];
-            for (int j = 0; j < 2; ++j) {
-                const double x = xi[2 * k + j];
-                const double dx = w * x + (-w) * vrp[2 * k + j];
-                const double dk = (x + dx * dt) - xi[2 * (k + 1) + j];
-                d[2 * k + j] = dk;
-                const double e = fabs(dk);
-                if (e > pres || e != e) pres = e;
-            }
-            if (k >= 1) {
-                qx[2 * k] = Qw0 * (xi[2 * k] - xi_ref[2 * k]);
-                qx[2 * k + 1] = Qw1 * (xi[2 * k + 1] - xi_ref[2 * k + 1]);
-            }
-        }
-        const double mu = ntot > 0 ? orc_wave_tree_sum(c, N) / (double)ntot : 0.0;
+        const double pres = dcm_residuals(w);
+        const double mu = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
         if (!(mu == mu) || !(pres == pres) || !(dres == dres) || isinf(mu)) { status = 2; break; }
         if (mu <= prm->tol_mu && pres <= prm->tol_primal && dres <= prm->tol_dual) { status = 0; break; }
         if (it >= prm->max_iter) { status = 1; break; }
 
-        /* ---- R' = R + A^T diag(lam/s) A, affine rhs g (stage-parallel) ---- */
+        /* ---- W = A^T diag(lam/s) A, det(W) as a sum of non-negative terms, affine rhs g
+         *      (stage-parallel) ---- */
         for (int k = 0; k < N; ++k) {
             const int m = nfacets[k];
-            double R00 = Rw0, R01 = 0.0, R11 = Rw1;
-            double g0 = rho[2 * k], g1 = rho[2 * k + 1];
+            double W00 = 0.0, W01 = 0.0, W11 = 0.0, dW = 0.0;
+            double g0 = w->rho[2 * k], g1 = w->rho[2 * k + 1];
+            double sgv[MF];
             for (int i = 0; i < m; ++i) {
                 const double* a = Ain + (k * M + i) * 2;
-                const double si = s[k * MF + i], li = lam[k * MF + i];
+                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
                 const double sg = li / si;
+                sgv[i] = sg;
                 const double t0 = sg * a[0];
                 const double t1 = sg * a[1];
-                R00 = R00 + t0 * a[0];
-                R01 = R01 + t0 * a[1];
-                R11 = R11 + t1 * a[1];
+                W00 = W00 + t0 * a[0];
+                W01 = W01 + t0 * a[1];
+                W11 = W11 + t1 * a[1];
                 const double rc = si * li;
-                const double e = (li * rp[k * MF + i] - rc) / si;
+                const double e = (li * w->rp[k * MF + i] - rc) / si;
                 g0 = g0 + a[0] * e;
                 g1 = g1 + a[1] * e;
             }
-            R[3 * k] = R00; R[3 * k + 1] = R01; R[3 * k + 2] = R11;
-            g[2 * k] = g0; g[2 * k + 1] = g1;
+            /* det(sum_i sg_i a_i a_i^T) = sum_{i<j} sg_i sg_j (a_i x a_j)^2 */
+            for (int i = 1; i < m; ++i) {
+                const double* ai = Ain + (k * M + i) * 2;
+                for (int j = 0; j < i; ++j) {
+                    const double* aj = Ain + (k * M + j) * 2;
+                    const double cr = ai[0] * aj[1] - ai[1] * aj[0];
+                    dW = dW + (sgv[i] * sgv[j]) * (cr * cr);
+                }
+            }
+            w->W[4 * k] = W00; w->W[4 * k + 1] = W01; w->W[4 * k + 2] = W11; w->W[4 * k + 3] = dW;
+            w->g[2 * k] = g0; w->g[2 * k + 1] = g1;
         }
 
-        /* ---- two Newton solves (affine, then corrector) ---- */
-        double amax = 0.0, a_aff = 0.0, sigma_mu = 0.0;
-        for (int pass = 0; pass < 2; ++pass) {
-            /* backward sweep (factor on pass 0, reuse on pass 1) */
-            double P00 = Pw0, P01 = 0.0, P11 = Pw1;
-            double pv0 = Pw0 * (xi[2 * N] - xi_ref[2 * N]);
-            double pv1 = Pw1 * (xi[2 * N + 1] - xi_ref[2 * N + 1]);
-            for (int k = N - 1; k >= 0; --k) {
-                double h00, h01, h11;
-                if (pass == 0) {
-                    const double H00 = R[3 * k] + b2[k] * P00;
-                    const double H01 = R[3 * k + 1] + b2[k] * P01;
-                    const double H11 = R[3 * k + 2] + b2[k] * P11;
-                    const double det = H00 * H11 - H01 * H01;
-                    if (!(det > 0.0) || isinf(det)) status = 2;
-                    const double idet = 1.0 / det;
-                    h00 = H11 * idet;
-                    h01 = -(H01 * idet);
-                    h11 = H00 * idet;
-                    Hi[3 * k] = h00; Hi[3 * k + 1] = h01; Hi[3 * k + 2] = h11;
-                    Pn[3 * k] = P00; Pn[3 * k + 1] = P01; Pn[3 * k + 2] = P11;
-                } else {
-                    h00 = Hi[3 * k]; h01 = Hi[3 * k + 1]; h11 = Hi[3 * k + 2];
-                    P00 = Pn[3 * k]; P01 = Pn[3 * k + 1]; P11 = Pn[3 * k + 2];
-                }
-                const double d0 = d[2 * k], d1 = d[2 * k + 1];
-                const double t0 = (P00 * d0 + P01 * d1) + pv0;
-                const double t1 = (P01 * d0 + P11 * d1) + pv1;
-                const double hu0 = g[2 * k] - be[k] * t0;
-                const double hu1 = g[2 * k + 1] - be[k] * t1;
-                const double k0 = -(h00 * hu0 + h01 * hu1);
-                const double k1 = -(h01 * hu0 + h11 * hu1);
-                kff[2 * k] = k0; kff[2 * k + 1] = k1;
-                if (k > 0) {
-                    const double pk0 = P00 * k0 + P01 * k1;
-                    const double pk1 = P01 * k0 + P11 * k1;
-                    const double npv0 = qx[2 * k] + al[k] * (t0 - be[k] * pk0);
-                    const double npv1 = qx[2 * k + 1] + al[k] * (t1 - be[k] * pk1);
-                    if (pass == 0) {
-                        const double R00 = R[3 * k], R01 = R[3 * k + 1], R11 = R[3 * k + 2];
-                        const double M00 = P00 * h00 + P01 * h01;
-                        const double M01 = P00 * h01 + P01 * h11;
-                        const double M10 = P01 * h00 + P11 * h01;
-                        const double M11 = P01 * h01 + P11 * h11;
-                        const double T00 = M00 * R00 + M01 * R01;
-                        const double T01 = M00 * R01 + M01 * R11;
-                        const double T10 = M10 * R00 + M11 * R01;
-                        const double T11 = M10 * R01 + M11 * R11;
-                        P00 = Qw0 + a2[k] * T00;
-                        P11 = Qw1 + a2[k] * T11;
-                        P01 = a2[k] * (0.5 * (T01 + T10));
-                    }
-                    pv0 = npv0;
-                    pv1 = npv1;
-                }
+        /* ---- affine (predictor) step ---- */
+        if (!dcm_backward(w, 1)) status = 2;
+        dcm_forward(w);
+        double smax = INFINITY;
+        for (int k = 0; k < N; ++k) {
+            const int m = nfacets[k];
+            for (int i = 0; i < m; ++i) {
+                const double* a = Ain + (k * M + i) * 2;
+                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
+                const double rc = si * li;
+                const double ds = (-w->rp[k * MF + i]) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
+                const double dl = ((-rc) - li * ds) / si;
+                if (ds < 0.0) { const double qq = (-si) / ds; if (qq < smax) smax = qq; }
+                if (dl < 0.0) { const double qq = (-li) / dl; if (qq < smax) smax = qq; }
+                w->prod[k * MF + i] = ds * dl;
             }
-            /* forward sweep */
-            dxi[0] = 0.0; dxi[1] = 0.0;
-            for (int k = 0; k < N; ++k) {
-                const double q00 = Pn[3 * k], q01 = Pn[3 * k + 1], q11 = Pn[3 * k + 2];
-                const double x0 = dxi[2 * k], x1 = dxi[2 * k + 1];
-                const double u0 = q00 * x0 + q01 * x1;
-                const double u1 = q01 * x0 + q11 * x1;
-                const double v0 = Hi[3 * k] * u0 + Hi[3 * k + 1] * u1;
-                const double v1 = Hi[3 * k + 1] * u0 + Hi[3 * k + 2] * u1;
-                const double ab = al[k] * be[k];
-                const double r0 = ab * v0 + kff[2 * k];
-                const double r1 = ab * v1 + kff[2 * k + 1];
-                dr[2 * k] = r0; dr[2 * k + 1] = r1;
-                dxi[2 * (k + 1)] = (al[k] * x0 - be[k] * r0) + d[2 * k];
-                dxi[2 * (k + 1) + 1] = (al[k] * x1 - be[k] * r1) + d[2 * k + 1];
+        }
+        const double a_aff = smax < 1.0 ? smax : 1.0;
+        for (int k = 0; k < N; ++k) {
+            const int m = nfacets[k];
+            double ck = 0.0;
+            for (int i = 0; i < m; ++i) {
+                const double* a = Ain + (k * M + i) * 2;
+                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
+                const double rc = si * li;
+                const double ds = (-w->rp[k * MF + i]) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
+                const double dl = ((-rc) - li * ds) / si;
+                ck = ck + (si + a_aff * ds) * (li + a_aff * dl);
             }
-            /* facets: ds, dl, step length (stage-parallel + min) */
-            double smax = INFINITY;
-            for (int k = 0; k < N; ++k) {
-                const int m = nfacets[k];
-                for (int i = 0; i < m; ++i) {
-                    const double* a = Ain + (k * M + i) * 2;
-                    const double si = s[k * MF + i], li = lam[k * MF + i];
-                    const double rc = (pass == 0) ? si * li
-                                                  : (si * li + prod[k * MF + i]) - sigma_mu;
-                    const double ds = (-rp[k * MF + i]) - (a[0] * dr[2 * k] + a[1] * dr[2 * k + 1]);
-                    const double dl = ((-rc) - li * ds) / si;
-                    if (ds < 0.0) { const double q = (-si) / ds; if (q < smax) smax = q; }
-                    if (dl < 0.0) { const double q = (-li) / dl; if (q < smax) smax = q; }
-                    if (pass == 0) prod[k * MF + i] = ds * dl;
-                    else { rp[k * MF + i] = ds; prod[k * MF + i] = dl; }  /* keep for update */
-                }
+            w->c[k] = ck;
+        }
+        const double mu_aff = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
+        double sigma = 0.0;
+        if (mu > 0.0) {
+            const double qq = mu_aff / mu;
+            sigma = (qq * qq) * qq;
+        }
+        const double sigma_mu = sigma * mu;
+
+        /* ---- corrector: rhs (stage-parallel), solve reusing the factorization ---- */
+        for (int k = 0; k < N; ++k) {
+            const int m = nfacets[k];
+            double g0 = w->rho[2 * k], g1 = w->rho[2 * k + 1];
+            for (int i = 0; i < m; ++i) {
+                const double* a = Ain + (k * M + i) * 2;
+                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
+                const double rc = (si * li + w->prod[k * MF + i]) - sigma_mu;
+                const double e = (li * w->rp[k * MF + i] - rc) / si;
+                g0 = g0 + a[0] * e;
+                g1 = g1 + a[1] * e;
             }
-            if (pass == 0) {
-                a_aff = smax < 1.0 ? smax : 1.0;
-                /* mu_aff from the affine step (recompute ds, dl from stored products: we need the
-                 * factors, so recompute them) */
-                for (int k = 0; k < N; ++k) {
-                    const int m = nfacets[k];
-                    double ck = 0.0;
-                    for (int i = 0; i < m; ++i) {
-                        const double* a = Ain + (k * M + i) * 2;
-                        const double si = s[k * MF + i], li = lam[k * MF + i];
-                        const double rc = si * li;
-                        const double ds = (-rp[k * MF + i]) - (a[0] * dr[2 * k] + a[1] * dr[2 * k + 1]);
-                        const double dl = ((-rc) - li * ds) / si;
-                        ck = ck + (si + a_aff * ds) * (li + a_aff * dl);
-                    }
-                    c[k] = ck;
-                }
-                const double mu_aff = ntot > 0 ? orc_wave_tree_sum(c, N) / (double)ntot : 0.0;
-                double sigma = 0.0;
-                if (mu > 0.0) {
-                    const double q = mu_aff / mu;
-                    sigma = (q * q) * q;
-                }
-                sigma_mu = sigma * mu;
-                /* corrector rhs g (stage-parallel) */
-                for (int k = 0; k < N; ++k) {
-                    const int m = nfacets[k];
-                    double g0 = rho[2 * k], g1 = rho[2 * k + 1];
-                    for (int i = 0; i < m; ++i) {
-                        const double* a = Ain + (k * M + i) * 2;
-                        const double si = s[k * MF + i], li = lam[k * MF + i];
-                        const double rc = (si * li + prod[k * MF + i]) - sigma_mu;
-                        const double e = (li * rp[k * MF + i] - rc) / si;
-                        g0 = g0 + a[0] * e;
-                        g1 = g1 + a[1] * e;
-                    }
-                    g[2 * k] = g0; g[2 * k + 1] = g1;
-                }
-            } else {
-                amax = smax;
+            w->g[2 * k] = g0; w->g[2 * k + 1] = g1;
+        }
+        dcm_backward(w, 0);
+        dcm_forward(w);
+        smax = INFINITY;
+        for (int k = 0; k < N; ++k) {
+            const int m = nfacets[k];
+            for (int i = 0; i < m; ++i) {
+                const double* a = Ain + (k * M + i) * 2;
+                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
+                const double rc = (si * li + w->prod[k * MF + i]) - sigma_mu;
+                const double ds = (-w->rp[k * MF + i]) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
+                const double dl = ((-rc) - li * ds) / si;
+                if (ds < 0.0) { const double qq = (-si) / ds; if (qq < smax) smax = qq; }
+                if (dl < 0.0) { const double qq = (-li) / dl; if (qq < smax) smax = qq; }
+                w->rp[k * MF + i] = ds;      /* keep the step for the update */
+                w->prod[k * MF + i] = dl;
             }
         }
         if (status == 2) break;
-        const double step = 0.99 * amax;
+        const double step = 0.99 * smax;
         const double a = step < 1.0 ? step : 1.0;
-        /* update (stage-parallel) */
         for (int k = 0; k < N; ++k) {
-            vrp[2 * k] = vrp[2 * k] + a * dr[2 * k];
-            vrp[2 * k + 1] = vrp[2 * k + 1] + a * dr[2 * k + 1];
-            xi[2 * (k + 1)] = xi[2 * (k + 1)] + a * dxi[2 * (k + 1)];
-            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + a * dxi[2 * (k + 1) + 1];
+            vrp[2 * k] = vrp[2 * k] + a * w->dr[2 * k];
+            vrp[2 * k + 1] = vrp[2 * k + 1] + a * w->dr[2 * k + 1];
+            xi[2 * (k + 1)] = xi[2 * (k + 1)] + a * w->dxi[2 * (k + 1)];
+            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + a * w->dxi[2 * (k + 1) + 1];
             const int m = nfacets[k];
             for (int i = 0; i < m; ++i) {
-                s[k * MF + i] = s[k * MF + i] + a * rp[k * MF + i];
-                lam[k * MF + i] = lam[k * MF + i] + a * prod[k * MF + i];
+                w->s[k * MF + i] = w->s[k * MF + i] + a * w->rp[k * MF + i];
+                w->lam[k * MF + i] = w->lam[k * MF + i] + a * w->prod[k * MF + i];
             }
         }
         dres = dres * (1.0 - a);
     }
     if (iters_out) *iters_out = it;
-    free(al); free(s); free(st);
+    free(mem);
     return status;
 }
 

@@ -164,7 +164,7 @@ def default_params(horizon, **kw):
         v = kw.get(name, val)
         getattr(p, name)[0] = v if np.isscalar(v) else v[0]
         getattr(p, name)[1] = v if np.isscalar(v) else v[1]
-    p.tol_mu = kw.get("tol_mu", 1e-15)
+    p.tol_mu = kw.get("tol_mu", 1e-16)
     p.tol_primal = kw.get("tol_primal", 1e-10)
     p.tol_dual = kw.get("tol_dual", 1e-9)
     return p

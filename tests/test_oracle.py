@@ -1,0 +1,194 @@
+"""CPU tests: the oracle against the reference's own test data (golden fixtures) and against
+independent solutions.  No GPU needed."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from blf import problems as P
+from dense_qp import certify
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _g(name):
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        return json.load(f)
+
+
+# ---- ForwardEuler<LinearTimeInvariantSystem> (IntegratorTest.cpp:27-75) ----------------------
+def test_integrator_lti_reference_test():
+    g = _g("integrator_lti")
+    cps = {c[0]: np.array(c[1:]) for c in g["checkpoints"]}
+    x = np.zeros(2)
+    for i in range(g["calls"]):
+        t = g["dT"] * i
+        closed = np.array([1 - np.exp(-t) * (np.cos(t) + np.sin(t)), 2 * np.exp(-t) * np.sin(t)])
+        assert np.linalg.norm(x - closed) <= 1e-3 * min(np.linalg.norm(x), np.linalg.norm(closed))
+        if i in cps:
+            np.testing.assert_array_equal(x, cps[i])
+        st, x, n = O.lti_euler_integrate(g["A"], g["B"], g["u"], x, 0.0, g["dT"], g["dT"])
+        assert st == 0 and n == 1
+    np.testing.assert_array_equal(x, g["final"])
+
+
+def test_integrator_step_schedule_quirks():
+    ramp = dict(A=[[0.0]], B=[[1.0]], u=[1.0])
+    # dT=0.01, T=0.05: 5 steps, the last spans 2 dT from the stale time -> ends at 0.06
+    st, x, n = O.lti_euler_integrate(ramp["A"], ramp["B"], ramp["u"], [0.0], 0.0, 0.05, 0.01)
+    assert st == 0 and n == 5 and abs(x[0] - 0.06) < 1e-15
+    # t0=1, T=1.04: ceil(4.000000000000004) = 5 steps
+    st, x, n = O.lti_euler_integrate(ramp["A"], ramp["B"], ramp["u"], [0.0], 1.0, 1.04, 0.01)
+    assert st == 0 and n == 5
+    # errors: t0 > T and dT <= 0 are rejected; t0 == T is refused (the reference never returns)
+    assert O.lti_euler_integrate(ramp["A"], ramp["B"], ramp["u"], [0.0], 1.0, 0.5, 0.1)[0] == 4
+    assert O.lti_euler_integrate(ramp["A"], ramp["B"], ramp["u"], [0.0], 0.0, 1.0, 0.0)[0] == 4
+    assert O.lti_euler_integrate(ramp["A"], ramp["B"], ramp["u"], [0.0], 1.0, 1.0, 0.1)[0] == 5
+
+
+def test_dcm_rollout_is_the_lti_step():
+    rng = np.random.default_rng(0)
+    N = 40
+    om = rng.uniform(4, 4.5, N)
+    r = rng.normal(0, 0.1, (N, 2))
+    xi = O.dcm_euler_rollout([0.01, -0.02], om, r, 0.02)
+    x = np.array([0.01, -0.02])
+    for k in range(N):   # one integrate(0, dt) of the LTI system A = w I, B = -w I per knot
+        st, x, _ = O.lti_euler_integrate(om[k] * np.eye(2), -om[k] * np.eye(2), r[k], x, 0.0,
+                                         0.02, 0.02)
+        np.testing.assert_array_equal(x, xi[k + 1])
+
+
+# ---- ContactPhaseList / ContactList ------------------------------------------------------------
+def test_contact_phases_reference_fixture():
+    g = _g("contact_phases")
+    names = sorted(g["lists"])          # std::map<std::string, ContactList> order
+    lists = [g["lists"][n] for n in names]
+    begin, end, active = O.contact_phases(lists)
+    assert len(begin) == len(g["phases"]) == 8
+    for p, (b0, e0, act) in enumerate(g["phases"]):
+        assert begin[p] == b0 and end[p] == e0
+        want = {names.index(k): v for k, v in act.items()}
+        got = {l: int(c) for l, c in enumerate(active[p]) if c >= 0}
+        assert got == want
+
+
+def test_contact_phase_quirk_next_deactivation():
+    # ContactPhaseList.cpp:60 compares the NEXT deactivation with the next activation: a
+    # coincident deactivation/activation yields a zero-length phase
+    begin, end, active = O.contact_phases([[(0.0, 1.0)], [(1.0, 2.0)]])
+    assert list(zip(begin, end)) == [(0.0, 1.0), (1.0, 1.0), (1.0, 2.0)]
+
+
+def test_present_contact_reference_fixture():
+    g = _g("contact_list")
+    acts = np.array([c[0] for c in g["contacts"]])
+    for t, want in g["present"]:
+        assert O.present_index(acts, t) == want
+
+
+def test_generator_phases_match_oracle():
+    for F, N in ((4, 50), (6, 100), (8, 130)):
+        sched = P.contact_schedule(F, N)
+        dt = 0.02
+        mine = P.phases_from_schedule(sched, dt)
+        lists = [[(a * dt, d * dt) for a, d, _ in sched[f]] for f in ("left", "right")]
+        begin, end, active = O.contact_phases(lists)
+        assert len(mine) == len(begin)
+        for (b0, e0, act), bo, eo, ao in zip(mine, begin, end, active):
+            assert b0 == bo and e0 == eo
+            assert act == {l: int(c) for l, c in enumerate(ao) if c >= 0}
+
+
+# ---- ConvexHullHelper (2-D) ------------------------------------------------------------------
+def test_hull_matches_qhull_fixture():
+    for c in _g("hull2d")["cases"]:
+        pts = np.array(c["points"])
+        A, b, m = O.hull2d_hrep(pts, 16)
+        assert m == c["nfacets"]
+        mine = np.array(sorted(map(tuple, np.c_[A[:m], b[:m]])))
+        ref = np.array(sorted(map(tuple, np.c_[np.array(c["A"]), np.array(c["b"])])))
+        np.testing.assert_allclose(mine, ref, atol=1e-12)
+        # ConvexHullHelperTest.cpp:53-62 idea: every input point belongs (up to the rounding of
+        # b = n.v), a far point does not
+        assert (pts @ A[:m].T - b[:m] <= 1e-15).all()
+        assert not O.hull2d_contains(A, b, m, pts.mean(0) + 10.0)
+        assert O.hull2d_contains(A, b, m, pts.mean(0))
+
+
+def test_hull_padding_and_degenerate():
+    A, b, m = O.hull2d_hrep(np.array([[0.0, 0], [1, 1], [2, 2]]), 8)   # collinear
+    assert m == -1 and not A.any() and not b.any()
+    A, b, m = O.hull2d_hrep(np.array([[np.cos(a), np.sin(a)] for a in np.linspace(0, 6, 12)]), 8)
+    assert m == -1   # needs 12 rows > 8 slots
+    A, b, m = O.hull2d_hrep(np.array([[0.0, 0], [1, 0], [0, 1], [1, 0], [0, 0]]), 8)  # duplicates
+    assert m == 3
+
+
+# ---- QuinticSpline --------------------------------------------------------------------------
+def test_quintic_coefficients_match_sympy():
+    for c in _g("quintic")["cases"]:
+        kt = np.array([0.0, c["T"]])
+        kp = np.array([[[c["p0"]], [c["v0"]], [c["a0"]]], [[c["p1"]], [c["v1"]], [c["a1"]]]])
+        co = O.quintic_fit(kt, kp)[0, 0]
+        np.testing.assert_allclose(co, c["coeffs"], rtol=1e-10, atol=1e-10)
+        pva, idx = O.quintic_eval(kt, O.quintic_fit(kt, kp), np.array([0.0, c["T"]]))
+        np.testing.assert_allclose(pva[0, :, 0], [c["p0"], c["v0"], c["a0"]], atol=1e-12)
+        np.testing.assert_allclose(pva[1, :, 0], [c["p1"], c["v1"], c["a1"]], atol=1e-9)
+        assert list(idx) == [0, 1]
+
+
+# ---- DCM-MPC QP -----------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def qp_batch():
+    return O.assemble_constraints(P.make_batch(12, horizon=100, n_footsteps=6, seed=77))
+
+
+def test_dcm_mpc_oracle_against_dense_certificate(qp_batch):
+    worst = 0.0
+    for i in range(qp_batch["omega"].shape[0]):
+        st, xi, vrp, it = O.dcm_mpc_solve(qp_batch, index=i)
+        assert st == 0 and 5 <= it <= 30
+        xi_d, r_d = certify(qp_batch, i, xi, vrp)
+        worst = max(worst, np.abs(xi - xi_d).max(), np.abs(vrp - r_d).max())
+    assert worst < 1e-9, worst
+
+
+def test_dcm_mpc_unconstrained_is_lq_optimum():
+    prob = O.assemble_constraints(P.make_batch(2, horizon=30, n_footsteps=4, seed=1))
+    prob["nfacets"][:] = 0
+    st, xi, vrp, it = O.dcm_mpc_solve(prob, index=0)
+    assert st == 0 and it == 0     # the LQ warm start already is the optimum of an equality-only QP
+    xi_d, r_d = certify(prob, 0, xi, vrp)
+    assert np.abs(xi - xi_d).max() < 1e-10 and np.abs(vrp - r_d).max() < 1e-10
+
+
+def test_dcm_mpc_bad_facets_and_batch_driver(qp_batch):
+    prob = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in qp_batch.items()}
+    prob["nfacets"][3, 7] = 9
+    st, xi, vrp, it = O.dcm_mpc_solve_batch(prob, threads=3)
+    assert st[3] == 3 and it[3] == 0
+    np.testing.assert_array_equal(vrp[3], prob["vrp_ref"][3])
+    assert (np.delete(st, 3) == 0).all()
+    # the threaded driver gives the same bits as the single-problem call
+    for i in (0, 5, 11):
+        s1, x1, r1, i1 = O.dcm_mpc_solve(prob, index=i)
+        np.testing.assert_array_equal(x1, xi[i])
+        np.testing.assert_array_equal(r1, vrp[i])
+
+
+def test_wave_tree_sum_order():
+    rng = np.random.default_rng(3)
+    for n in (1, 5, 64, 100, 128, 300):
+        c = rng.uniform(0, 1, n) * 10.0 ** rng.integers(-8, 8, n)
+        ref = 0.0
+        for w in range(0, n, 64):
+            v = np.zeros(64)
+            blk = c[w:w + 64]
+            v[:len(blk)] = blk
+            for off in (32, 16, 8, 4, 2, 1):
+                v = v + v[np.arange(64) ^ off]
+            ref = v[0] if w == 0 else ref + v[0]
+        assert O.wave_tree_sum(c) == ref

@@ -10,7 +10,8 @@ rc=$?
 echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 if [ "${SKIP_BENCH:-0}" = "1" ]; then exit $rc; fi
-timeout -k 10 300 python bench.py ${BENCH_ARGS:-"--steps 10 --warmup 2 --cpu-seconds 3"} > gpurun_out/bench.log 2>&1
+BENCH_ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 3}
+timeout -k 10 300 python bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1
 rc2=$?
 echo "bench rc=$rc2"; tail -5 gpurun_out/bench.log
 exit $rc2
