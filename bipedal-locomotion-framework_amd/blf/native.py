@@ -10,6 +10,8 @@ import os
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG, "lib", "libblf.so")
+# diagnostic builds only (tools/kbench.py): BLF_LIB points at e.g. lib/libblf_stamps.so
+LIB_PATH = os.environ.get("BLF_LIB", LIB_PATH)
 
 BLF_OK = 0
 STATUS_NAMES = {0: "BLF_OK", 1: "BLF_ERR_INVALID_ARGUMENT", 2: "BLF_ERR_HIP",

@@ -1,0 +1,60 @@
+"""Kernel micro-benchmark of blf_dcm_mpc_solve (diagnostics; not the driver's bench.py).
+
+Times the solve on the bench workload with HIP events and, when the loaded library is the
+stamp-instrumented diagnostic build (BLF_LIB=.../libblf_stamps.so), prints where thread 0 of the
+first 64 workgroups spends its cycles.
+  python tools/kbench.py [--batch 4096] [--horizon 100] [--reps 10]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bipedal-locomotion-framework_amd"))
+
+import torch  # noqa: E402
+from blf import native  # noqa: E402
+from blf import problems as P  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--horizon", type=int, default=100)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    h = native.Handle(0)
+    prob = P.make_batch(args.batch, horizon=args.horizon, n_footsteps=6)
+    d = {k: torch.from_numpy(prob[k]).cuda() for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
+    A, b, nf = h.assemble_constraints(torch.from_numpy(prob["corners"]).cuda(),
+                                      torch.from_numpy(prob["ncorners"]).cuda())
+    d.update(A=A, b=b, nfacets=nf)
+    out = h.dcm_mpc_solve(d)
+    torch.cuda.synchronize()
+    L = native.lib()
+    stamps = getattr(L, "blf_debug_stamps", None) if hasattr(L, "blf_debug_stamps") else None
+    buf = (ctypes.c_ulonglong * 8)()
+    if stamps is not None:
+        stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        stamps(ctypes.cast(buf, ctypes.c_void_p), 1)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.reps):
+        h.dcm_mpc_solve(d, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.reps
+    print(f"lib={native.LIB_PATH} batch={args.batch} N={args.horizon}: {ms:.3f} ms/solve, "
+          f"{args.batch / ms * 1e3:.0f} QP/s, mean iters {out['iters'].float().mean().item():.2f}, "
+          f"status!=0: {int((out['status'] != 0).sum())}")
+    if stamps is not None:
+        stamps(ctypes.cast(buf, ctypes.c_void_p), 0)
+        tot, fac, sol, its = buf[0], buf[1], buf[2], buf[3]
+        print(f"thread0 cycles per QP: total {tot / 64 / args.reps:.0f}  per iteration: "
+              f"factor+fwd {fac / its:.0f}, solve+fwd {sol / its:.0f}, "
+              f"rest {(tot - fac - sol) / its:.0f}  (iters counted {its / 64 / args.reps:.2f})")
+
+
+if __name__ == "__main__":
+    main()
