@@ -34,6 +34,22 @@ def algorithmic_bytes_per_qp(N, M):
     return 8 * f64 + 4 * i32
 
 
+def profiled_traffic():
+    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 summary
+    (profiles/*_summary.json, written by tools/summarize_profile.py from separate FETCH_SIZE /
+    WRITE_SIZE passes); bench.py cannot read PMC counters itself."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime)
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        s = json.load(f)
+    t = s.get("hbm_traffic_per_launch")
+    if not t or "dcm_mpc_ipm" not in s.get("dominant_kernel", ""):
+        return None, None
+    return t["total_bytes_corrected"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(host, N, seconds, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -144,6 +160,7 @@ def main():
         total = world * B * args.steps
         bpq = algorithmic_bytes_per_qp(N, M)
         achieved = bpq * B / (kernel_ms * 1e-3) / 1e9
+        traffic, traffic_src = profiled_traffic()
         fp64_tf = flops / (kernel_ms * 1e-3) / 1e12
         line = {
             "metric": "DCM-MPC QP solves/sec (batch, horizon=100)",
@@ -163,7 +180,8 @@ def main():
                        "batch_per_gpu": B, "horizon": N, "max_facets": M,
                        "parallelism": f"shard{world} (independent problems)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "dcm_mpc_ipm_kernel<128>", "kernel_ms": kernel_ms,
                          "bytes_per_qp": bpq,
                          "fp64_valu": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,

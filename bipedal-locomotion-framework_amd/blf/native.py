@@ -20,7 +20,7 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 
 # every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
-            "blf_lti_euler_integrate", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
+            "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_quintic_fit", "blf_quintic_eval",
             "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_flops_per_iter"]
 
@@ -68,6 +68,7 @@ def lib():
         L.blf_version.restype = ctypes.c_char_p
         L.blf_lti_euler_integrate.argtypes = [_vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _i64,
                                               _f64, _f64, _f64, _vp]
+        L.blf_lti_dynamics.argtypes = [_vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp]
         L.blf_dcm_euler_rollout.argtypes = [_vp, _vp, _vp, _vp, _i32, _f64, _vp, _i64, _vp]
         L.blf_hull2d_hrep.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
         L.blf_hull2d_contains.argtypes = [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp]
@@ -184,6 +185,20 @@ class Handle:
             1 if shared else 0, _ptr(u, torch.float64, (batch, m), "u"),
             _ptr(x, torch.float64, (batch, n), "x"), batch, t0, t1, dT, _stream(stream)))
         return x
+
+    def lti_dynamics(self, A, Bm, u, x, shared=False, stream=None):
+        torch = _torch()
+        batch, n = x.shape
+        m = u.shape[-1]
+        ashape = (n, n) if shared else (batch, n, n)
+        bshape = (n, m) if shared else (batch, n, m)
+        dx = torch.empty_like(x)
+        _check(lib().blf_lti_dynamics(
+            self._h, n, m, _ptr(A, torch.float64, ashape, "A"), _ptr(Bm, torch.float64, bshape, "B"),
+            1 if shared else 0, _ptr(u, torch.float64, (batch, m), "u"),
+            _ptr(x, torch.float64, (batch, n), "x"), _ptr(dx, torch.float64, (batch, n), "dx"),
+            batch, _stream(stream)))
+        return dx
 
     def dcm_euler_rollout(self, xi0, omega, vrp, dt, out=None, stream=None):
         torch = _torch()

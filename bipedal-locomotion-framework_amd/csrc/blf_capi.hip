@@ -102,6 +102,18 @@ blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m, con
                             (hipStream_t)stream);
 }
 
+blf_status blf_lti_dynamics(blf_handle* handle, int32_t n, int32_t m, const double* A,
+                            const double* Bm, int32_t shared_matrices, const double* u,
+                            const double* x, double* dx, int64_t batch, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_lti_dynamics: null handle");
+    BLF_REQUIRE(n >= 1 && n <= 8 && m >= 1 && m <= 8, "blf_lti_dynamics: n=%d m=%d outside [1, 8]",
+                n, m);
+    BLF_REQUIRE(batch >= 0, "blf_lti_dynamics: negative batch");
+    BLF_REQUIRE(batch == 0 || (A && Bm && u && x && dx), "blf_lti_dynamics: null buffer");
+    return launch_lti_dynamics(n, m, A, Bm, shared_matrices, u, x, dx, batch, (hipStream_t)stream);
+}
+
 blf_status blf_dcm_euler_rollout(blf_handle* handle, const double* xi0, const double* omega,
                                  const double* vrp, int32_t horizon, double dt, double* xi_out,
                                  int64_t batch, void* stream)

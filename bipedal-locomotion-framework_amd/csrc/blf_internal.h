@@ -27,6 +27,9 @@ struct Handle {
 blf_status launch_lti_euler(int n, int m, const double* A, const double* Bm, int shared,
                             const double* u, double* x, int64_t batch, int32_t nsteps,
                             double dT, double dT_last, hipStream_t s);
+blf_status launch_lti_dynamics(int n, int m, const double* A, const double* Bm, int shared,
+                               const double* u, const double* x, double* dx, int64_t batch,
+                               hipStream_t s);
 blf_status launch_dcm_rollout(const double* xi0, const double* omega, const double* vrp,
                               int32_t N, double dt, double* xi_out, int64_t batch,
                               hipStream_t s);

@@ -69,6 +69,27 @@ __global__ __launch_bounds__(256) void lti_euler_kernel(int n, int m, const doub
         if (r < n) x[q * n + r] = xr[r];
 }
 
+__global__ __launch_bounds__(256) void lti_dynamics_kernel(int n, int m,
+                                                           const double* __restrict__ A,
+                                                           const double* __restrict__ Bm,
+                                                           int shared,
+                                                           const double* __restrict__ u,
+                                                           const double* __restrict__ x,
+                                                           double* __restrict__ dx, int64_t batch)
+{
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= batch) return;
+    const double* Aq = shared ? A : A + q * n * n;
+    const double* Bq = shared ? Bm : Bm + q * n * m;
+    for (int r = 0; r < n; ++r) {
+        double ax = Aq[r * n] * x[q * n];
+        for (int c = 1; c < n; ++c) ax = ax + Aq[r * n + c] * x[q * n + c];
+        double bu = Bq[r * m] * u[q * m];
+        for (int c = 1; c < m; ++c) bu = bu + Bq[r * m + c] * u[q * m + c];
+        dx[q * n + r] = ax + bu;
+    }
+}
+
 // 64 problems per workgroup (one wave), knots staged in chunks of KC.
 constexpr int KC = 16;
 
@@ -138,6 +159,16 @@ blf_status launch_lti_euler(int n, int m, const double* A, const double* Bm, int
     hipLaunchKernelGGL(lti_euler_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, m, A, Bm,
                        shared, u, x, batch, nsteps, dT, dT_last);
     return check_hip(hipGetLastError(), "lti_euler_kernel launch");
+}
+
+blf_status launch_lti_dynamics(int n, int m, const double* A, const double* Bm, int shared,
+                               const double* u, const double* x, double* dx, int64_t batch,
+                               hipStream_t s)
+{
+    if (batch == 0) return BLF_OK;
+    hipLaunchKernelGGL(lti_dynamics_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256), 0, s,
+                       n, m, A, Bm, shared, u, x, dx, batch);
+    return check_hip(hipGetLastError(), "lti_dynamics_kernel launch");
 }
 
 blf_status launch_dcm_rollout(const double* xi0, const double* omega, const double* vrp,

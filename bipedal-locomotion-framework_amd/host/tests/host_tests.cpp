@@ -1,0 +1,372 @@
+/**
+ * @file host_tests.cpp
+ * The reference's Catch2 tests for the DCM path, restated against the C++ adapters:
+ *   ContactListTest.cpp:28-118, ContactPhaseListTest.cpp:15-153, VariablesHandlerTest.cpp:15-35
+ *   (host bookkeeping, run everywhere), IntegratorTest.cpp:27-75 (device), a 2-D
+ *   ConvexHullHelperTest (device), the QuinticSpline and TimeVaryingDCMPlanner::advance (device).
+ * usage: blf_host_tests [cpu|gpu|all]   (exit status = number of failed checks)
+ */
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <iostream>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include <BipedalLocomotion/ParametersHandler/IParametersHandler.h>
+#include <BipedalLocomotion/Planners/ContactList.h>
+#include <BipedalLocomotion/Planners/ContactPhaseList.h>
+#include <BipedalLocomotion/Planners/ConvexHullHelper.h>
+#include <BipedalLocomotion/Planners/QuinticSpline.h>
+#include <BipedalLocomotion/Planners/TimeVaryingDCMPlanner.h>
+#include <BipedalLocomotion/System/ForwardEuler.h>
+#include <BipedalLocomotion/System/LinearTimeInvariantSystem.h>
+#include <BipedalLocomotion/System/VariablesHandler.h>
+
+using namespace BipedalLocomotion;
+using namespace BipedalLocomotion::Planners;
+using namespace BipedalLocomotion::System;
+
+static int g_failed = 0, g_checks = 0;
+#define REQUIRE(cond)                                                                          \
+    do {                                                                                       \
+        ++g_checks;                                                                            \
+        if (!(cond)) {                                                                         \
+            ++g_failed;                                                                        \
+            std::fprintf(stderr, "  FAILED %s:%d: %s\n", __FILE__, __LINE__, #cond);           \
+        }                                                                                      \
+    } while (0)
+#define REQUIRE_FALSE(cond) REQUIRE(!(cond))
+
+static bool sameContact(const Contact& a, const Contact& b)
+{
+    return a.type == b.type && a.name == b.name && a.activationTime == b.activationTime &&
+           a.deactivationTime == b.deactivationTime && a.pose.position == b.pose.position &&
+           a.pose.rotation == b.pose.rotation;
+}
+
+// ---- ContactListTest.cpp:28-118 ----------------------------------------------------------------
+static void testContactList()
+{
+    auto fresh = [](Contact& p1, Contact& p2) {
+        ContactList list;
+        p1 = Contact{};
+        p2 = Contact{};
+        p1.activationTime = 0.1;
+        p1.deactivationTime = 0.5;
+        p2.activationTime = 1.0;
+        p2.deactivationTime = 1.5;
+        REQUIRE(list.addContact(p2));   // insertion out of order
+        REQUIRE(list.addContact(p1));
+        return list;
+    };
+    Contact p1, p2;
+    {   // insertion order + size
+        ContactList list = fresh(p1, p2);
+        REQUIRE(sameContact(p1, *list.firstContact()));
+        REQUIRE(sameContact(p2, *list.lastContact()));
+        Contact p3;
+        p3.activationTime = 0.6;
+        p3.deactivationTime = 0.8;
+        REQUIRE(list.addContact(p3));
+        REQUIRE(list.size() == 3);
+        REQUIRE(sameContact(p3, *(++list.begin())));
+    }
+    {   // invalid (overlapping) insertion; touching intervals are rejected too
+        ContactList list = fresh(p1, p2);
+        Contact p3;
+        p3.activationTime = 0.9;
+        p3.deactivationTime = 1.6;
+        REQUIRE_FALSE(list.addContact(p3));
+        Contact p4;
+        p4.activationTime = 1.5;
+        p4.deactivationTime = 2.0;
+        REQUIRE_FALSE(list.addContact(p4));
+        Contact bad;
+        bad.activationTime = 3.0;
+        bad.deactivationTime = 2.0;
+        REQUIRE_FALSE(list.addContact(bad));
+    }
+    {   // edit
+        ContactList list = fresh(p1, p2);
+        Contact p2m = p2;
+        p2m.type = ContactType::POINT;
+        REQUIRE(list.editContact(list.lastContact(), p2m));
+        REQUIRE(sameContact(p2m, *list.lastContact()));
+    }
+    {   // present step (`<=` rule)
+        ContactList list = fresh(p1, p2);
+        REQUIRE(sameContact(p2, *list.getPresentContact(1.2)));
+        REQUIRE(sameContact(p2, *list.getPresentContact(1.6)));
+        REQUIRE(sameContact(p1, *list.getPresentContact(0.6)));
+        REQUIRE(list.getPresentContact(0.0) == list.end());
+        REQUIRE(list.keepOnlyPresentContact(0.6));
+        REQUIRE(list.size() == 1 && sameContact(p1, *list.begin()));
+    }
+    {   // clear
+        ContactList list = fresh(p1, p2);
+        list.clear();
+        REQUIRE(list.size() == 0);
+    }
+    {   // accessor over 51 contacts
+        ContactList list = fresh(p1, p2);
+        bool ok = true;
+        for (std::size_t i = 0; i < 49; ++i)
+            ok = ok && list.addContact(Transform::Identity(), 2.0 + i, 2.5 + i);
+        REQUIRE(ok);
+        REQUIRE(list.size() == 51);
+        auto it = list.begin();
+        for (std::size_t i = 0; i < list.size(); ++i, ++it) ok = ok && sameContact(list[i], *it);
+        REQUIRE(ok);
+    }
+}
+
+// ---- ContactPhaseListTest.cpp:15-153 -----------------------------------------------------------
+static void testContactPhaseList()
+{
+    ContactList left, right, additional;
+    left.setDefaultName("left");
+    right.setDefaultName("right");
+    additional.setDefaultName("additional");
+    REQUIRE(left.addContact(Transform::Identity(), 0.0, 1.0));
+    REQUIRE(left.addContact(Transform::Identity(), 2.0, 5.0));
+    REQUIRE(left.addContact(Transform::Identity(), 6.0, 7.0));
+    REQUIRE(right.addContact(Transform::Identity(), 0.0, 3.0));
+    REQUIRE(right.addContact(Transform::Identity(), 4.0, 7.0));
+    REQUIRE(additional.addContact(Transform::Identity(), 4.0, 5.0));
+    REQUIRE(additional.addContact(Transform::Identity(), 6.0, 7.5));
+
+    ContactPhaseList phases;
+    REQUIRE(phases.setLists({additional, left, right}));
+    REQUIRE(phases.size() == 8);
+    const ContactListMap& lists = phases.lists();
+    auto L = lists.at("left").begin();
+    auto R = lists.at("right").begin();
+    auto A = lists.at("additional").begin();
+    struct Expect { double b, e; std::vector<std::pair<std::string, ContactList::const_iterator*>> act; };
+    auto check = [&](const ContactPhase& ph, double b, double e,
+                     std::vector<std::pair<std::string, ContactList::const_iterator>> act) {
+        REQUIRE(ph.beginTime == b);
+        REQUIRE(ph.endTime == e);
+        REQUIRE(ph.activeContacts.size() == act.size());
+        for (auto& [name, it] : act) REQUIRE(ph.isListIncluded(name) && ph.activeContacts.at(name) == it);
+    };
+    auto ph = phases.begin();
+    check(*ph++, 0.0, 1.0, {{"left", L}, {"right", R}});
+    ++L;
+    check(*ph++, 1.0, 2.0, {{"right", R}});
+    check(*ph++, 2.0, 3.0, {{"left", L}, {"right", R}});
+    ++R;
+    check(*ph++, 3.0, 4.0, {{"left", L}});
+    check(*ph++, 4.0, 5.0, {{"left", L}, {"right", R}, {"additional", A}});
+    ++L;
+    ++A;
+    check(*ph++, 5.0, 6.0, {{"right", R}});
+    check(*ph++, 6.0, 7.0, {{"left", L}, {"right", R}, {"additional", A}});
+    ++L;
+    ++R;
+    check(*ph++, 7.0, 7.5, {{"additional", A}});
+    ++A;
+    REQUIRE(ph == phases.end());
+    REQUIRE(L == lists.at("left").end());
+    REQUIRE(R == lists.at("right").end());
+    REQUIRE(A == lists.at("additional").end());
+    REQUIRE(phases.phaseIndexAt(4.0) == 4 && phases.phaseIndexAt(7.5) == -1);
+
+    ContactList dup;
+    dup.setDefaultName("left");
+    REQUIRE_FALSE(phases.setLists({left, dup}));
+}
+
+// ---- VariablesHandlerTest.cpp:15-35 ------------------------------------------------------------
+static void testVariablesHandler()
+{
+    VariablesHandler handler;
+    REQUIRE(handler.addVariable("variable_1", 42));
+    REQUIRE(handler.addVariable("variable_2", 35));
+    REQUIRE_FALSE(handler.addVariable("variable_1", 3));
+    REQUIRE(handler.getVariable("variable_1").offset == 0);
+    REQUIRE(handler.getVariable("variable_1").size == 42);
+    REQUIRE(handler.getVariable("variable_2").offset == 42);
+    REQUIRE(handler.getVariable("variable_2").size == 35);
+    REQUIRE(handler.getNumberOfVariables() == 77);
+    REQUIRE_FALSE(handler.getVariable("variable_3").isValid());
+}
+
+// ---- IntegratorTest.cpp:27-75 (device) --------------------------------------------------------
+static void testIntegratorLTI()
+{
+    constexpr double dT = 0.0001;
+    constexpr double tolerance = 1e-3;
+    constexpr double simulationTime = 2;
+    auto system = std::make_shared<LinearTimeInvariantSystem>();
+    blf::MatrixXd A(2, 2, {0, 1, -2, -2});
+    blf::MatrixXd b(2, 1, {0, 2});
+    REQUIRE(system->setSystemMatrices(A, b));
+    system->setControlInput({blf::VectorXd{1.0}});
+    system->setState({blf::VectorXd{0.0, 0.0}});
+    ForwardEuler<LinearTimeInvariantSystem> integrator(dT);
+    REQUIRE(integrator.setDynamicalSystem(system));
+    REQUIRE_FALSE(integrator.setDynamicalSystem(system));   // set once only
+    bool ok = true;
+    for (int i = 0; i < simulationTime / dT; i++)
+    {
+        const auto& [x] = integrator.getSolution();
+        const double t = dT * i;
+        const double e0 = 1 - std::exp(-t) * (std::cos(t) + std::sin(t));
+        const double e1 = 2 * std::exp(-t) * std::sin(t);
+        const double dn = std::hypot(x(0) - e0, x(1) - e1);
+        ok = ok && dn <= tolerance * std::min(std::hypot(x(0), x(1)), std::hypot(e0, e1));
+        ok = ok && integrator.integrate(0, dT);
+        if (!ok) break;
+    }
+    REQUIRE(ok);
+    // dynamics() on the device: dx = A x + B u
+    std::tuple<blf::VectorXd> dx;
+    REQUIRE(system->dynamics(0.0, dx));
+    const auto& [xs] = integrator.getSolution();
+    REQUIRE(std::get<0>(dx)(0) == 0.0 * xs(0) + 1.0 * xs(1) + 0.0 * 1.0);
+    // error semantics: t0 > T, T == t0 (the reference never returns: refused here)
+    REQUIRE_FALSE(integrator.integrate(1.0, 0.5));
+    REQUIRE_FALSE(integrator.integrate(1.0, 1.0));
+    ForwardEuler<LinearTimeInvariantSystem> bad(-1.0);
+    REQUIRE(bad.setDynamicalSystem(system));
+    REQUIRE_FALSE(bad.integrate(0.0, 1.0));
+}
+
+// ---- ConvexHullHelper (device, 2-D) -----------------------------------------------------------
+static void testConvexHull()
+{
+    ConvexHullHelper helper;
+    // two feet in staggered double support (the planners' polygons)
+    blf::MatrixXd p(2, 8);
+    const double xs[8] = {0.06, 0.06, -0.06, -0.06, 0.26, 0.26, 0.14, 0.14};
+    const double ys[8] = {0.145, 0.055, 0.145, 0.055, -0.055, -0.145, -0.055, -0.145};
+    for (int j = 0; j < 8; ++j) { p(0, j) = xs[j]; p(1, j) = ys[j]; }
+    REQUIRE(helper.buildConvexHull(p));
+    REQUIRE(helper.getA().rows() == 6 && helper.getA().cols() == 2);
+    double cx = 0.0, cy = 0.0;
+    for (int j = 0; j < 8; ++j) { cx += xs[j] / 8; cy += ys[j] / 8; }
+    for (int j = 0; j < 8; ++j)   // every corner, pulled 0.1 % towards the centroid, is inside
+        REQUIRE(helper.doesPointBelongToConvexHull(
+            blf::VectorXd{cx + 0.999 * (xs[j] - cx), cy + 0.999 * (ys[j] - cy)}));
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.0, 0.0 - 1.0}));
+    REQUIRE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.1, 0.0}));
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.1, 0.0, 0.0}));   // wrong size
+    // 3-D input (ConvexHullHelperTest.cpp's points) is outside the accelerated path
+    blf::MatrixXd p3(3, 8);
+    REQUIRE_FALSE(helper.buildConvexHull(p3));
+}
+
+// ---- QuinticSpline (device) -------------------------------------------------------------------
+static void testQuinticSpline()
+{
+    QuinticSpline spline;
+    // swing foot: lift at 0.2 s, apex at 0.5 s, land at 0.8 s; x: 0 -> 0.2, z: 0 -> 0.05 -> 0
+    const std::vector<double> t = {0.2, 0.5, 0.8};
+    const std::vector<double> pos = {0.0, 0.0, 0.1, 0.05, 0.2, 0.0};
+    const std::vector<double> vel = {0.0, 0.0, 0.2 / 0.6, 0.0, 0.0, 0.0};
+    const std::vector<double> acc = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    REQUIRE(spline.setKnots(t, 2, pos, vel, acc));
+    std::vector<double> pva;
+    std::vector<int32_t> idx;
+    REQUIRE(spline.evaluate({0.1, 0.2, 0.5, 0.8, 0.9}, pva, idx));
+    REQUIRE(idx.size() == 5 && idx[0] == -1 && idx[1] == 0 && idx[2] == 1 && idx[3] == 2 && idx[4] == 2);
+    auto at = [&](int q, int k, int d) { return pva[(q * 3 + k) * 2 + d]; };
+    REQUIRE(std::fabs(at(1, 0, 0) - 0.0) < 1e-15 && std::fabs(at(1, 1, 0)) < 1e-15);
+    REQUIRE(std::fabs(at(2, 0, 1) - 0.05) < 1e-12 && std::fabs(at(2, 1, 1)) < 1e-12);
+    REQUIRE(std::fabs(at(3, 0, 0) - 0.2) < 1e-12 && std::fabs(at(3, 1, 0)) < 1e-10);
+    REQUIRE_FALSE(spline.setKnots({0.0, 0.0}, 1, {0, 0}, {0, 0}, {0, 0}));
+}
+
+// ---- TimeVaryingDCMPlanner::advance (device) ---------------------------------------------------
+static ContactPhaseList walkingPlan(double stride, double yaw)
+{
+    ContactList left, right;
+    left.setDefaultName("left");
+    right.setDefaultName("right");
+    const double dt = 0.02;
+    left.addContact(Transform::fromPlanar(0.0, 0.1, yaw), 0 * dt, 50 * dt);
+    left.addContact(Transform::fromPlanar(2 * stride, 0.1, -yaw), 80 * dt, 400 * dt);
+    right.addContact(Transform::fromPlanar(0.0, -0.1, -yaw), 0 * dt, 10 * dt);
+    right.addContact(Transform::fromPlanar(stride, -0.1, yaw), 40 * dt, 400 * dt);
+    ContactPhaseList plan;
+    plan.setLists({left, right});
+    return plan;
+}
+
+static void testPlanner()
+{
+    auto handler = std::make_shared<ParametersHandler::StdImplementation>();
+    handler->setParameter("horizon", 100);
+    handler->setParameter("sampling_time", 0.02);
+    handler->setParameter("dcm_weight", std::vector<double>{100.0});
+    handler->setParameter("vrp_weight", std::vector<double>{1.0, 1.0});
+    handler->setParameter("terminal_weight", std::vector<double>{1000.0});
+    TimeVaryingDCMPlanner planner;
+    REQUIRE(planner.initialize(handler));
+    REQUIRE_FALSE(planner.isValid());
+    REQUIRE_FALSE(planner.advance());   // no plans yet
+    std::vector<ContactPhaseList> plans;
+    std::vector<std::array<double, 2>> xi0;
+    for (int b = 0; b < 16; ++b)
+    {
+        plans.push_back(walkingPlan(0.18 + 0.005 * b, 0.01 * (b - 8)));
+        xi0.push_back({{0.0 + 0.001 * b, 0.0}});
+    }
+    REQUIRE(planner.setContactPhaseLists(plans));
+    REQUIRE(planner.setInitialDCM(xi0));
+    for (int step = 0; step < 5; ++step)
+    {
+        REQUIRE(planner.advance());
+        REQUIRE(planner.isValid());
+        const DCMPlanBatch& plan = planner.get();
+        REQUIRE(plan.batch == 16 && plan.horizon == 100);
+        REQUIRE(plan.initialTime == step * 0.02);
+        // the plan starts at the previous plan's xi_1 and follows the Euler DCM step
+        bool dyn = true;
+        for (int b = 0; b < 16; ++b)
+        {
+            const double* xi = &plan.dcm[static_cast<std::size_t>(b) * 101 * 2];
+            const double* r = &plan.vrp[static_cast<std::size_t>(b) * 100 * 2];
+            for (int k = 0; k < 100; ++k)
+            {
+                const double w = std::sqrt(9.81 / 0.53);
+                for (int j = 0; j < 2; ++j)
+                {
+                    const double nxt = xi[2 * k + j] + (w * xi[2 * k + j] + (-w) * r[2 * k + j]) * 0.02;
+                    dyn = dyn && std::fabs(nxt - xi[2 * (k + 1) + j]) < 1e-12;
+                }
+            }
+        }
+        REQUIRE(dyn);
+    }
+}
+
+int main(int argc, char** argv)
+{
+    const std::string which = argc > 1 ? argv[1] : "all";
+    const bool cpu = which == "cpu" || which == "all";
+    const bool gpu = which == "gpu" || which == "all";
+    struct T { const char* name; bool device; std::function<void()> fn; };
+    const std::vector<T> tests = {
+        {"ContactList", false, testContactList},
+        {"ContactPhaseList", false, testContactPhaseList},
+        {"VariablesHandler", false, testVariablesHandler},
+        {"Integrator - Linear system", true, testIntegratorLTI},
+        {"Convex Hull helper (2-D)", true, testConvexHull},
+        {"QuinticSpline", true, testQuinticSpline},
+        {"TimeVaryingDCMPlanner advance", true, testPlanner},
+    };
+    for (const auto& t : tests)
+    {
+        if ((t.device && !gpu) || (!t.device && !cpu)) continue;
+        const int before = g_failed;
+        t.fn();
+        std::printf("%-32s %s\n", t.name, g_failed == before ? "ok" : "FAILED");
+    }
+    std::printf("%d checks, %d failed\n", g_checks, g_failed);
+    return g_failed;
+}

@@ -73,6 +73,12 @@ blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m,
                                    double initial_time, double final_time, double dT,
                                    void* stream);
 
+/* LinearTimeInvariantSystem::dynamics (LinearTimeInvariantSystem.cpp:40-74), batched:
+ * dx = A x + B u with the same summation order as blf_lti_euler_integrate; dx: [B][n]. */
+blf_status blf_lti_dynamics(blf_handle* handle, int32_t n, int32_t m, const double* A,
+                            const double* Bm, int32_t shared_matrices, const double* u,
+                            const double* x, double* dx, int64_t batch, void* stream);
+
 /* ---- 2. DCM rollout: one reference Euler step per knot -------------------------------------
  * xi_{k+1} = xi_k + ((omega_k * xi_k) + (-omega_k * r_k)) * dt,  k = 0..N-1
  * xi0: [B][2], omega: [B][N], vrp: [B][N][2], xi_out: [B][N+1][2] (xi_out[:,0] = xi0).       */

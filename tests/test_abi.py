@@ -1,0 +1,70 @@
+"""CPU tests of the drop-in boundary: the library loads, exports every entry point the header
+declares, and its host-only entry points behave (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from blf import native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "blf", "blf_c.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(blf_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_and_library_exports_every_symbol():
+    declared = _declared()
+    assert set(declared) == set(native.EXPORTED), (declared, native.EXPORTED)
+    out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (blf_[a-z0-9_]+)$", out, flags=re.M))
+    missing = set(declared) - exported
+    assert not missing, missing
+
+
+def test_library_is_built_for_gfx950_only():
+    # the .hip_fatbin bundle names one code object per offload target
+    out = subprocess.run(["strings", native.LIB_PATH], capture_output=True, text=True).stdout
+    targets = set(re.findall(r"amdgcn-amd-amdhsa--(gfx\w+)", out))
+    assert targets == {"gfx950"}, targets
+    assert "nvptx" not in out
+
+
+def test_host_only_entry_points_without_gpu():
+    L = native.lib()
+    p = native.default_params(100)
+    assert p.horizon == 100 and p.max_facets == 8 and p.max_iter == 50
+    assert p.tol_mu == 1e-16 and p.tol_primal == 1e-10 and p.tol_dual == 1e-9
+    assert tuple(p.w_xi) == (100.0, 100.0) and tuple(p.w_terminal) == (1000.0, 1000.0)
+    assert native.flops_per_iter(100, 500) == 79 * 500 + 184 * 100
+    assert native.version().startswith("blf-mi355x")
+    # argument validation happens before any device work: a null handle is rejected
+    rc = L.blf_dcm_mpc_solve(None, ctypes.byref(p), None, 1, None, None)
+    assert rc == 1 and "null" in native.last_error()
+    rc = L.blf_lti_euler_integrate(None, 2, 1, None, None, 1, None, None, 1, 0.0, 1.0, 0.1, None)
+    assert rc == 1
+
+
+def test_create_fails_loudly_without_a_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    with pytest.raises(native.BlfError) as e:
+        native.Handle(0)
+    assert e.value.code == 2
+
+
+def test_oracle_is_not_linked_by_the_product():
+    for lib in ("libblf.so", "libblf_host.so"):
+        path = os.path.join(os.path.dirname(native.LIB_PATH), lib)
+        out = subprocess.run(["ldd", path], capture_output=True, text=True).stdout
+        assert "oracle" not in out
+        syms = subprocess.run(["nm", "-D", path], capture_output=True, text=True).stdout
+        assert "orc_" not in syms

@@ -1,0 +1,69 @@
+"""Condense a tools/profile_round.sh run (gpurun_out/prof) into profiles/<tag>_*.
+
+Writes <tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary, verbatim) and
+<tag>_summary.json: per-dispatch averages of the PMC counters for every kernel, and for the
+dominant kernel the HBM traffic per launch computed as the guide prescribes
+(MI355X_MICROARCH.md 'HBM'): FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE under-reports
+wide coalesced reads by 2x on gfx950, so both the raw and the x2-corrected read bytes are given.
+  python tools/summarize_profile.py r01 [gpurun_out/prof]
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    if not os.path.exists(path):
+        return out
+    for r in csv.DictReader(open(path)):
+        out[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    tag = sys.argv[1]
+    src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
+    pmc = collections.defaultdict(dict)
+    for sub in ("fetch", "write", "sq"):
+        for kname, cs in counters(os.path.join(src, sub, "run_counter_collection.csv")).items():
+            for c, v in cs.items():
+                pmc[kname][c] = {"dispatches": len(v), "mean_per_dispatch": sum(v) / len(v)}
+    dom = max(stats, key=lambda k: float(stats[k]["TotalDurationNs"]))
+    d = pmc.get(dom, {})
+    fetch_kib = d.get("FETCH_SIZE", {}).get("mean_per_dispatch")
+    write_kib = d.get("WRITE_SIZE", {}).get("mean_per_dispatch")
+    summary = {
+        "source": "tools/profile_round.sh (rocprofv3 --kernel-trace --stats; separate --pmc passes "
+                  "FETCH_SIZE | WRITE_SIZE | SQ_*) on `python3 bench.py --steps 10 --warmup 2 --no-cpu`",
+        "dominant_kernel": dom,
+        "dominant_avg_ns": float(stats[dom]["AverageNs"]),
+        "dominant_calls": int(stats[dom]["Calls"]),
+        "hbm_traffic_per_launch": None if fetch_kib is None or write_kib is None else {
+            "fetch_bytes_raw": fetch_kib * 1024,
+            "fetch_bytes_x2_corrected": 2 * fetch_kib * 1024,
+            "write_bytes": write_kib * 1024,
+            "total_bytes_corrected": (2 * fetch_kib + write_kib) * 1024,
+            "note": "FETCH_SIZE/WRITE_SIZE are KiB and count L2 misses to the fabric "
+                    "(Infinity-Cache hits included); gfx950 FETCH_SIZE reads 1/2 of wide "
+                    "coalesced stream bytes (MI355X_MICROARCH.md HBM section)"},
+        "pmc_per_kernel": pmc,
+    }
+    with open(os.path.join(dst, f"{tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: summary[k] for k in ("dominant_kernel", "dominant_avg_ns",
+                                               "hbm_traffic_per_launch")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
