@@ -3,7 +3,7 @@
 Workload (BASELINE.json configs[1]): per GPU, a batch of 4096 horizon-100 time-varying DCM MPC
 QPs (6-footstep plans, M = 8 facet slots, fp64), inputs resident in HBM.  One step = one
 blf_dcm_mpc_solve over the whole per-GPU batch (every QP solved from a cold start to
-tol_mu 1e-15).  Multi-GPU: one process per GPU (torch.distributed.run), each rank solves its own
+tol_mu 1e-16).  Multi-GPU: one process per GPU (torch.distributed.run), each rank solves its own
 shard of independent problems — no data-path collective (scaling "weak"); the RCCL gather of the
 solutions to rank 0 is timed separately and reported as gather_ms.
 
