@@ -51,6 +51,8 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
 __device__ __forceinline__ double nanmax(double a, double b) { return (b > a || b != b) ? b : a; }
 // min that ignores NaN candidates (matches `if (q < m) m = q`).
 __device__ __forceinline__ double keepmin(double a, double b) { return (b < a) ? b : a; }
+// max that ignores NaN candidates (matches the oracle's keepmax).
+__device__ __forceinline__ double keepmax(double a, double b) { return (b > a) ? b : a; }
 
 // xor-butterfly over the 64 lanes; every lane ends with the identical value because fp addition
 // is commutative: lane l and lane l^off both compute the same two operands.
@@ -70,6 +72,12 @@ __device__ __forceinline__ double wave_keepmin(double v)
 {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = keepmin(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+__device__ __forceinline__ double wave_keepmax(double v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = keepmax(v, __shfl_xor(v, off, kWave));
     return v;
 }
 __device__ __forceinline__ int wave_isum(int v)

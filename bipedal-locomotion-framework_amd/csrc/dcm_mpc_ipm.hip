@@ -1,16 +1,25 @@
 // dcm_mpc_ipm.hip — batched time-varying DCM MPC QP (TimeVaryingDCMPlanner).
 //
-// One workgroup per QP, one thread per knot ("stage") k < N, NT = 64*ceil(N/64) threads.
-// Stage-parallel work (residuals, barrier Hessian R'_k = R + A_k^T diag(lam/s) A_k, Newton
-// right-hand sides, per-facet step / update) runs on all lanes with the stage's facets held in
-// registers; the Riccati recursion over the knots (backward factor/solve, forward rollout of the
-// Newton step) is inherently sequential and runs on thread 0 out of LDS.  Reductions (mean
-// complementarity, max residual, step length) are xor-butterflies over each wavefront plus an
-// ordered sum over waves — the exact order the oracle's orc_wave_tree_sum restates.
+// One workgroup per QP, one thread per knot k < N, NW = ceil(N/64) wavefronts.  Everything a knot
+// owns — its slacks, multipliers, 1/s, VRP, DCM xi_{k+1}, the Newton-system blocks of the knot —
+// lives in that thread's registers for the whole solve; LDS holds only the facet rows (read in
+// every phase) and a few boundary values exchanged between wavefronts.
 //
-// Every arithmetic expression mirrors oracle/blf_oracle.c:orc_dcm_mpc_solve term for term and
-// the file is built with -ffp-contract=off, so device and oracle iterates agree bit for bit
-// (verified by tests/test_gpu_dcm_mpc.py).  DESIGN.md section 4 is the algorithm statement.
+// The Newton system is block tridiagonal in time.  Its factorization needs ONE nonlinear
+// recursion over the knots, the information-form Riccati recursion
+//     Y_k = Z_k (Q Z_k + alpha_k^2 I)^{-1},   Z_k = Y_{k+1} + E_k,   Y = P^{-1},
+// which runs lane after lane: the lane owning knot k evaluates its step with the other lanes
+// masked off, and the 3-double state moves to the next lane through v_readlane (SGPRs) — no
+// memory traffic and a single division on the critical path.  Every other sequential piece is
+// an affine recursion (costates, the forward rollout of the Newton step) and runs as a
+// Kogge-Stone scan over the 64 lanes of each wavefront (6 levels of __shfl + a 2x2 compose),
+// then one boundary value per wavefront through LDS.  All remaining work (residuals, barrier
+// Hessians, right-hand sides, step lengths, updates) is knot-parallel.
+//
+// Every expression mirrors oracle/blf_oracle.c:orc_dcm_mpc_solve term for term (the scans in the
+// same combine order, the reductions in the same xor-butterfly order) and the file is built with
+// -ffp-contract=off, so device and oracle iterates agree bit for bit (tests/test_gpu_dcm_mpc.py).
+// DESIGN.md section 4 is the algorithm statement.
 #include "blf_internal.h"
 
 namespace blf {
@@ -18,11 +27,11 @@ namespace {
 
 #ifdef BLF_STAMPS
 // Diagnostic build only (make stamps): per-phase cycle sums of thread 0 for the first 64 QPs.
-// [0] whole kernel, [1] factor sweep + forward, [2] solve sweep + forward, [3] iterations.
+// [0] whole kernel, [1] factorization, [2] both solves, [3] iterations.
 __device__ unsigned long long g_blf_stamps[8];
 #define STAMP(t) unsigned long long t = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, t0) \
-    do { if (blockIdx.x < 64) atomicAdd(&g_blf_stamps[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
+    do { if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_blf_stamps[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
 #else
 #define STAMP(t)
 #define STAMP_ADD(slot, t0)
@@ -33,300 +42,487 @@ struct KParams {
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_mu, tol_p, tol_d;
 };
 
-// LDS carve-up (in doubles), sized by N.  The same code computes the launch size on the host
-// (Lds(nullptr, ...).total), so the allocation always covers every array.
-//
-// Everything the Riccati sweeps exchange with the knot threads lives in one 144-byte record per
-// knot, so a sweep step addresses one base pointer and moves its data with ds_read_b128 /
-// ds_write_b128 at immediate offsets.  144 B = 36 dwords: the knot threads' 16-byte accesses
-// to their own records are bank-conflict free (36 k mod 32 = 4 k).
-//   R[k]: 0-3 W00 W01 W11 detW | 4-5 g (rhs; the forward sweep overwrites it with dr)
-//         6-7 d (Euler defect) | 8-9 Q (xi_k - xi_ref_k) | 10 alpha 11 beta 12 alpha^2 13 beta^2
-//         14-15 kff | 16 omega | 17 pad
-//   H[k]: 0-2 H_k^{-1} (00 01 11) | 3-5 P_{k+1} (00 01 11) | 6-7 pad
-constexpr int kRec = 18;
-constexpr int kHrec = 8;
+// LDS carve-up (doubles).  The host sizes the launch with the same code (Lds(nullptr, ...)).
+//   A2  [M][N] double2  facet normals, knot-contiguous per facet (conflict-free b128 reads)
+//   bb  [M][N]          facet offsets
+//   IS  [M][N]          1 / s of every facet, refreshed once per iteration (W-phase)
+//   bnd [NW][16]        per-wavefront boundary values (see the kB* slots)
+//   red [4][NW][2]      reduction scratch, four rotating slots (no second barrier needed)
+constexpr int kBY = 0;    // Y_{64w} (3): Riccati state handed from wavefront w to w-1
+constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
+constexpr int kBV = 8;    // v_{64w} (2): backward-scan value at the first knot of wavefront w
+constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last knot of wavefront w
+constexpr int kBXi = 12;  // xi_{64w+64} (2): DCM past the last knot of wavefront w
+constexpr int kBnd = 16;
 struct Lds {
-    double *R, *H, *xi, *dxi, *red;
-    size_t total;   // doubles
-    __host__ __device__ Lds(double* base, int N, int NW)
+    double2* A2;
+    double *bb, *IS, *bnd, *red, *flag;
+    size_t total;
+    __host__ __device__ Lds(double* base, int N, int M, int NW)
     {
         size_t o = 0;
         auto take = [&](size_t n) {
             double* p = base ? base + o : nullptr;
-            o += (n + 1) & ~size_t(1);   // keep every array 16-byte aligned
+            o += (n + 1) & ~size_t(1);
             return p;
         };
-        R = take((size_t)kRec * N);
-        H = take((size_t)kHrec * N);
-        xi = take(2 * (N + 1));   // [N+1][2]
-        dxi = take(2 * (N + 1));  // [N+1][2] (also the costates nu at start-up)
-        red = take(4 * NW + 8);   // [NW] reduction scratch + flags
+        A2 = reinterpret_cast<double2*>(take(2 * (size_t)M * N));
+        bb = take((size_t)M * N);
+        IS = take((size_t)M * N);
+        bnd = take((size_t)kBnd * NW);
+        red = take(8 * (size_t)NW);
+        flag = take(2);
         total = o;
     }
-    __device__ double* rec(int k) const { return R + (size_t)kRec * k; }
-    __device__ double& W(int k, int j) const { return R[kRec * k + j]; }
-    __device__ double& g(int k, int j) const { return R[kRec * k + 4 + j]; }
-    __device__ double& dr(int k, int j) const { return R[kRec * k + 4 + j]; }
-    __device__ double& d(int k, int j) const { return R[kRec * k + 6 + j]; }
-    __device__ double& qx(int k, int j) const { return R[kRec * k + 8 + j]; }
-    __device__ double& al(int k) const { return R[kRec * k + 10]; }
-    __device__ double& be(int k) const { return R[kRec * k + 11]; }
-    __device__ double& a2(int k) const { return R[kRec * k + 12]; }
-    __device__ double& b2(int k) const { return R[kRec * k + 13]; }
-    __device__ double& kff(int k, int j) const { return R[kRec * k + 14 + j]; }
-    __device__ double& om(int k) const { return R[kRec * k + 16]; }
-    __device__ double& Hi(int k, int j) const { return H[kHrec * k + j]; }
-    __device__ double& Pn(int k, int j) const { return H[kHrec * k + 3 + j]; }
 };
 
-inline size_t lds_doubles(int N, int NW) { return Lds(nullptr, N, NW).total; }
-
-template <int NW>
-__device__ __forceinline__ double block_sum(double v, double* red)
+__device__ __forceinline__ double rdlane(double x, int l)
 {
-    v = wave_sum(v);
-    if constexpr (NW == 1) return v;
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    double t = red[0];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) t = t + red[i];
-    __syncthreads();
-    return t;
-}
-template <int NW>
-__device__ __forceinline__ double block_nanmax(double v, double* red)
-{
-    v = wave_nanmax(v);
-    if constexpr (NW == 1) return v;
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    double t = red[0];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) t = nanmax(t, red[i]);
-    __syncthreads();
-    return t;
-}
-template <int NW>
-__device__ __forceinline__ double block_keepmin(double v, double* red)
-{
-    v = wave_keepmin(v);
-    if constexpr (NW == 1) return v;
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    double t = red[0];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) t = keepmin(t, red[i]);
-    __syncthreads();
-    return t;
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Backward Riccati sweep (thread 0) = oracle dcm_backward.  FACTOR: builds H_k^{-1} and
-// P_{k+1} (returns false if some H_k is not positive definite); otherwise reuses them.
-template <bool FACTOR>
-__device__ bool backward_sweep(const Lds& L, const KParams& k, double pv0, double pv1)
+// Block reductions: xor-butterfly per wavefront, then the wavefronts' values in order (the
+// oracle's orc_wave_tree_sum).  `slot` rotates over 4 scratch rows so that a row is never
+// rewritten before every wavefront has read it (each reduction ends with one barrier).
+template <int NW>
+struct Reduce {
+    double* red;
+    int nwa;      // wavefronts that own knots (ceil(N/64)); the rest hold no data
+    int slot = 0;
+    __device__ double* row() { double* r = red + 2 * NW * slot; slot = (slot + 1) & 3; return r; }
+    __device__ void sum_nanmax(double& s, double& m)
+    {
+        s = wave_sum(s);
+        m = wave_nanmax(m);
+        if constexpr (NW > 1) {
+            double* r = row();
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) { r[2 * w] = s; r[2 * w + 1] = m; }
+            __syncthreads();
+            s = r[0];
+            m = r[1];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) if (i < nwa) { s = s + r[2 * i]; m = nanmax(m, r[2 * i + 1]); }
+        }
+    }
+    __device__ double sum(double s)
+    {
+        s = wave_sum(s);
+        if constexpr (NW > 1) {
+            double* r = row();
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) r[2 * w] = s;
+            __syncthreads();
+            s = r[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) if (i < nwa) s = s + r[2 * i];
+        }
+        return s;
+    }
+    __device__ double keepmax(double q)
+    {
+        q = wave_keepmax(q);
+        if constexpr (NW > 1) {
+            double* r = row();
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) r[2 * w] = q;
+            __syncthreads();
+            q = r[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) if (i < nwa) q = ::blf::keepmax(q, r[2 * i]);
+        }
+        return q;
+    }
+    __device__ double nanmax_(double q)
+    {
+        q = wave_nanmax(q);
+        if constexpr (NW > 1) {
+            double* r = row();
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) r[2 * w] = q;
+            __syncthreads();
+            q = r[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) if (i < nwa) q = nanmax(q, r[2 * i]);
+        }
+        return q;
+    }
+};
+
+// 2x2 compose (row-major): n = a * b;  nc = a * c + e.
+#define COMPOSE(a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, e0, e1)                 \
+    do {                                                                         \
+        const double n0_ = a0 * b0 + a1 * b2;                                    \
+        const double n1_ = a0 * b1 + a1 * b3;                                    \
+        const double n2_ = a2 * b0 + a3 * b2;                                    \
+        const double n3_ = a2 * b1 + a3 * b3;                                    \
+        const double m0_ = (a0 * c0 + a1 * c1) + e0;                             \
+        const double m1_ = (a2 * c0 + a3 * c1) + e1;                             \
+        a0 = n0_; a1 = n1_; a2 = n2_; a3 = n3_; e0 = m0_; e1 = m1_;               \
+    } while (0)
+
+// Backward affine recursion v_k = G_k v_{k+1} + c_k, v_N = 0 (oracle scan_backward).  Lanes past
+// the last knot carry the zero element.  Returns v_{k+1} for this lane's knot.
+template <int NW>
+__device__ __forceinline__ void scan_backward(double g0, double g1, double g2, double g3, double c0,
+                                              double c1, double* bnd, int nwa, int wv, int lane,
+                                              double& vn0, double& vn1)
+{
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const double p0 = __shfl_down(g0, d, kWave), p1 = __shfl_down(g1, d, kWave);
+        const double p2 = __shfl_down(g2, d, kWave), p3 = __shfl_down(g3, d, kWave);
+        const double q0 = __shfl_down(c0, d, kWave), q1 = __shfl_down(c1, d, kWave);
+        if (lane + d < kWave) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
+    }
+    double v0 = c0, v1 = c1;
+    if constexpr (NW > 1) {
+        for (int w = nwa - 1; w >= 0; --w) {
+            if (wv == w) {
+                if (w < nwa - 1) {
+                    const double b0 = bnd[kBnd * (w + 1) + kBV], b1 = bnd[kBnd * (w + 1) + kBV + 1];
+                    v0 = (g0 * b0 + g1 * b1) + c0;
+                    v1 = (g2 * b0 + g3 * b1) + c1;
+                }
+                if (lane == 0) { bnd[kBnd * w + kBV] = v0; bnd[kBnd * w + kBV + 1] = v1; }
+            }
+            if (w > 0) __syncthreads();
+        }
+    }
+    vn0 = __shfl_down(v0, 1, kWave);
+    vn1 = __shfl_down(v1, 1, kWave);
+    if (lane == kWave - 1) {
+        vn0 = 0.0;
+        vn1 = 0.0;
+        if (NW > 1 && wv < nwa - 1) {
+            vn0 = bnd[kBnd * (wv + 1) + kBV];
+            vn1 = bnd[kBnd * (wv + 1) + kBV + 1];
+        }
+    }
+}
+
+// Forward affine recursion x_{k+1} = F_k x_k + f_k, x_0 = 0 (oracle scan_forward).  Returns
+// x_{k+1} (this lane's result) and x_k (its input).
+template <int NW>
+__device__ __forceinline__ void scan_forward(double g0, double g1, double g2, double g3, double c0,
+                                             double c1, double* bnd, int nwa, int wv, int lane, double& x0,
+                                             double& x1, double& xk0, double& xk1)
+{
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const double p0 = __shfl_up(g0, d, kWave), p1 = __shfl_up(g1, d, kWave);
+        const double p2 = __shfl_up(g2, d, kWave), p3 = __shfl_up(g3, d, kWave);
+        const double q0 = __shfl_up(c0, d, kWave), q1 = __shfl_up(c1, d, kWave);
+        if (lane >= d) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
+    }
+    x0 = c0;
+    x1 = c1;
+    if constexpr (NW > 1) {
+        for (int w = 0; w < nwa; ++w) {
+            if (wv == w) {
+                if (w > 0) {
+                    const double b0 = bnd[kBnd * (w - 1) + kBX], b1 = bnd[kBnd * (w - 1) + kBX + 1];
+                    x0 = (g0 * b0 + g1 * b1) + c0;
+                    x1 = (g2 * b0 + g3 * b1) + c1;
+                }
+                if (lane == kWave - 1) { bnd[kBnd * w + kBX] = x0; bnd[kBnd * w + kBX + 1] = x1; }
+            }
+            if (w < nwa - 1) __syncthreads();
+        }
+    }
+    xk0 = __shfl_up(x0, 1, kWave);
+    xk1 = __shfl_up(x1, 1, kWave);
+    if (lane == 0) {
+        xk0 = 0.0;
+        xk1 = 0.0;
+        if (NW > 1 && wv > 0) {
+            xk0 = bnd[kBnd * (wv - 1) + kBX];
+            xk1 = bnd[kBnd * (wv - 1) + kBX + 1];
+        }
+    }
+}
+
+// Per-knot state (registers of the knot's thread).
+struct Knot {
+    int m;                                      // facet count
+    double s[kMaxFacets], lam[kMaxFacets];
+    double r0, r1;                              // VRP
+    double x0, x1;                              // xi_{k+1}
+    double w, al, be;                           // omega_k, 1 + dt omega_k, dt omega_k
+    double rh0, rh1, d0, d1, qx0, qx1;          // dual residual part, Euler defect, Q(xi - xi_ref)
+    double P00, P01, P11;                       // P_{k+1}
+    double h00, h01, h11;                       // H_k^{-1}
+};
+
+// M = P_{k+1} H_k^{-1} (recomputed where needed: cheaper than 8 live VGPRs).
+struct Mmat {
+    double m00, m01, m10, m11;
+    __device__ __forceinline__ explicit Mmat(const Knot& K)
+    {
+        m00 = K.P00 * K.h00 + K.P01 * K.h01;
+        m01 = K.P00 * K.h01 + K.P01 * K.h11;
+        m10 = K.P01 * K.h00 + K.P11 * K.h01;
+        m11 = K.P01 * K.h01 + K.P11 * K.h11;
+    }
+};
+
+// The facet rows never change during a solve, so the compiler would hoist every phase's row loads
+// out of the IPM loop and keep 8 facets x 4 doubles live in VGPRs across it (spilling).  Each phase
+// indexes the rows through an opaque copy of the knot index instead, so they are re-read from LDS.
+__device__ __forceinline__ int opaque(int k)
+{
+    asm volatile("" : "+v"(k));
+    return k;
+}
+
+// Facet residual rp_i = (a . r + s_i) - b_i.
+__device__ __forceinline__ double facet_rp(const Knot& K, double2 a, double bi, int i)
+{
+    return ((a.x * K.r0 + a.y * K.r1) + K.s[i]) - bi;
+}
+
+// The affine slack / multiplier step of facet i for the VRP step (dra0, dra1) (oracle affine_step).
+__device__ __forceinline__ void affine_step(const Knot& K, double2 a, double bi, double is, int i,
+                                            double dra0, double dra1, double& ds, double& dl)
+{
+    const double rpi = facet_rp(K, a, bi, i);
+    ds = (-rpi) - (a.x * dra0 + a.y * dra1);
+    dl = -((K.lam[i] * (K.s[i] + ds)) * is);
+}
+
+// Residual pass (oracle dcm_residuals) for this lane's knot; xk = xi_k.  Returns pres, ck.
+__device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P, bool last,
+                                          const double2* A2, const double* bb, int N, int k,
+                                          int mmax, double xk0, double xk1, const double* rref,
+                                          const double* xref, double& pres, double& ck)
+{
+    pres = 0.0;
+    ck = 0.0;
+    double rh0 = P.Rw0 * (K.r0 - rref[0]);
+    double rh1 = P.Rw1 * (K.r1 - rref[1]);
+    if (facets) {
+        const int kx = opaque(k);
+#pragma unroll
+        for (int i = 0; i < kMaxFacets; ++i) {
+            if (i >= mmax) break;
+            if (i < K.m) {
+                const double2 a = A2[i * N + kx];
+                const double gr = a.x * K.r0 + a.y * K.r1;
+                const double rpi = (gr + K.s[i]) - bb[i * N + kx];
+                pres = nanmax(pres, fabs(rpi));
+                ck = ck + K.s[i] * K.lam[i];
+                rh0 = rh0 + a.x * K.lam[i];
+                rh1 = rh1 + a.y * K.lam[i];
+            }
+        }
+    }
+    K.rh0 = rh0;
+    K.rh1 = rh1;
+    const double dx0 = K.w * xk0 + (-K.w) * K.r0;
+    const double dk0 = (xk0 + dx0 * P.dt) - K.x0;
+    const double dx1 = K.w * xk1 + (-K.w) * K.r1;
+    const double dk1 = (xk1 + dx1 * P.dt) - K.x1;
+    K.d0 = dk0;
+    K.d1 = dk1;
+    pres = nanmax(pres, fabs(dk0));
+    pres = nanmax(pres, fabs(dk1));
+    const double q0 = last ? P.Pw0 : P.Qw0;
+    const double q1 = last ? P.Pw1 : P.Qw1;
+    K.qx0 = q0 * (K.x0 - xref[0]);
+    K.qx1 = q1 * (K.x1 - xref[1]);
+}
+
+// xi_k of this lane's knot (xi_{k+1} of the previous lane; lane 0: the boundary value).
+template <int NW>
+__device__ __forceinline__ void xi_prev(const Knot& K, const double* bnd, int wv, int lane,
+                                        double xi00, double xi01, double& xk0, double& xk1)
+{
+    xk0 = __shfl_up(K.x0, 1, kWave);
+    xk1 = __shfl_up(K.x1, 1, kWave);
+    if (lane == 0) {
+        xk0 = xi00;
+        xk1 = xi01;
+        if (NW > 1 && wv > 0) {
+            xk0 = bnd[kBnd * (wv - 1) + kBXi];
+            xk1 = bnd[kBnd * (wv - 1) + kBXi + 1];
+        }
+    }
+}
+
+// Factorization (oracle dcm_factor) from W = (W00, W01, W11, detW).  Leaves P_{k+1}, h, M in K.
+// Returns false on this lane if its K or H block is not positive definite.
+template <int NW>
+__device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, double W01,
+                                       double W11, double dW, double* bnd, int N, int nwa, int k,
+                                       int wv, int lane, bool own)
 {
     bool ok = true;
-    double P00 = k.Pw0, P01 = 0.0, P11 = k.Pw1;
-    for (int s = k.N - 1; s >= 0; --s) {
-        const double2* rc = reinterpret_cast<const double2*>(L.rec(s));
-        double2* hr = reinterpret_cast<double2*>(L.H + (size_t)kHrec * s);
-        const double2 gg = rc[2], dd = rc[3], qq = rc[4], ab = rc[5], sq = rc[6];
-        const double be = ab.y, al = ab.x, a2 = sq.x, b2 = sq.y;
-        double h00, h01, h11;
-        if (FACTOR) {
-            const double2 w0 = rc[0], w1 = rc[1];
-            // H = B + W, B = R + b2 P_{k+1}: det H = det B + tr(adj(B) W) + det W (all >= 0)
-            const double B00 = k.Rw0 + b2 * P00;
-            const double B01 = b2 * P01;
-            const double B11 = k.Rw1 + b2 * P11;
-            const double H00 = B00 + w0.x;
-            const double H01 = B01 + w0.y;
-            const double H11 = B11 + w1.x;
-            const double detB = B00 * B11 - B01 * B01;
-            const double trW = (B11 * w0.x + B00 * w1.x) - 2.0 * (B01 * w0.y);
-            const double det = (detB + trW) + w1.y;
-            if (!(det > 0.0) || __builtin_isinf(det)) ok = false;
-            const double idet = 1.0 / det;
-            h00 = H11 * idet;
-            h01 = -(H01 * idet);
-            h11 = H00 * idet;
-            hr[0] = make_double2(h00, h01);
-            hr[1] = make_double2(h11, P00);
-            hr[2] = make_double2(P01, P11);
-        } else {
-            const double2 x0 = hr[0], x1 = hr[1], x2 = hr[2];
-            h00 = x0.x; h01 = x0.y; h11 = x1.x;
-            P00 = x1.y; P01 = x2.x; P11 = x2.y;
-        }
-        const double t0 = (P00 * dd.x + P01 * dd.y) + pv0;
-        const double t1 = (P01 * dd.x + P11 * dd.y) + pv1;
-        const double hu0 = gg.x - be * t0;
-        const double hu1 = gg.y - be * t1;
-        const double k0 = -(h00 * hu0 + h01 * hu1);
-        const double k1 = -(h01 * hu0 + h11 * hu1);
-        reinterpret_cast<double2*>(L.rec(s))[7] = make_double2(k0, k1);
-        if (s > 0) {
-            const double pk0 = P00 * k0 + P01 * k1;
-            const double pk1 = P01 * k0 + P11 * k1;
-            const double npv0 = qq.x + al * (t0 - be * pk0);
-            const double npv1 = qq.y + al * (t1 - be * pk1);
-            if (FACTOR) {
-                // P_k = Q + a^2 (P - b^2 P H^-1 P)
-                const double M00 = P00 * h00 + P01 * h01;
-                const double M01 = P00 * h01 + P01 * h11;
-                const double M10 = P01 * h00 + P11 * h01;
-                const double M11 = P01 * h01 + P11 * h11;
-                const double S00 = M00 * P00 + M01 * P01;
-                const double S01 = M00 * P01 + M01 * P11;
-                const double S10 = M10 * P00 + M11 * P01;
-                const double S11 = M10 * P01 + M11 * P11;
-                const double n00 = k.Qw0 + a2 * (P00 - b2 * S00);
-                const double n11 = k.Qw1 + a2 * (P11 - b2 * S11);
-                const double n01 = a2 * (P01 - b2 * (0.5 * (S01 + S10)));
-                P00 = n00;
-                P01 = n01;
-                P11 = n11;
+    const double b2 = K.be * K.be;
+    const double a2 = K.al * K.al;
+    double E00 = 0.0, E01 = 0.0, E11 = 0.0;
+    if (own) {
+        const double detRW = (P.Rw0 * P.Rw1 + (P.Rw1 * W00 + P.Rw0 * W11)) + dW;
+        const double ie = b2 / detRW;
+        E00 = (P.Rw1 + W11) * ie;
+        E01 = -(W01 * ie);
+        E11 = (P.Rw0 + W00) * ie;
+    }
+    // sequential information-form Riccati over knots N-1 .. 1, one lane at a time
+    double Y00 = 1.0 / P.Pw0, Y01 = 0.0, Y11 = 1.0 / P.Pw1;
+    double Z00 = 0.0, Z01 = 0.0, Z11 = 0.0;
+    for (int w = nwa - 1; w >= 0; --w) {
+        if (wv == w) {
+            if (w < nwa - 1) {
+                Y00 = bnd[kBnd * (w + 1) + kBY];
+                Y01 = bnd[kBnd * (w + 1) + kBY + 1];
+                Y11 = bnd[kBnd * (w + 1) + kBY + 2];
             }
-            pv0 = npv0;
-            pv1 = npv1;
+            const int hi = (N < kWave * w + kWave ? N : kWave * w + kWave) - 1;
+            const int lo = kWave * w > 1 ? kWave * w : 1;
+            for (int kk = hi; kk >= lo; --kk) {
+                const int ls = kk - kWave * w;
+                double n00 = 0.0, n01 = 0.0, n11 = 0.0;
+                if (lane == ls) {
+                    Z00 = Y00 + E00;
+                    Z01 = Y01 + E01;
+                    Z11 = Y11 + E11;
+                    const double K00 = P.Qw0 * Z00 + a2;
+                    const double K01 = P.Qw0 * Z01;
+                    const double K10 = P.Qw1 * Z01;
+                    const double K11 = P.Qw1 * Z11 + a2;
+                    const double detK = K00 * K11 - K01 * K10;
+                    if (!(detK > 0.0) || __builtin_isinf(detK)) ok = false;
+                    const double ik = 1.0 / detK;
+                    n00 = (Z00 * K11 - Z01 * K10) * ik;
+                    n01 = (Z01 * K00 - Z00 * K01) * ik;
+                    n11 = (Z11 * K00 - Z01 * K01) * ik;
+                }
+                Y00 = rdlane(n00, ls);
+                Y01 = rdlane(n01, ls);
+                Y11 = rdlane(n11, ls);
+            }
+            if (w > 0) {
+                // hand Y_{64w} and P_{64w} (this wavefront's first knot) to wavefront w-1
+                if (lane == 0) {
+                    bnd[kBnd * w + kBY] = Y00;
+                    bnd[kBnd * w + kBY + 1] = Y01;
+                    bnd[kBnd * w + kBY + 2] = Y11;
+                    const double detZ = Z00 * Z11 - Z01 * Z01;
+                    const double iz = a2 / detZ;
+                    bnd[kBnd * w + kBP] = P.Qw0 + Z11 * iz;
+                    bnd[kBnd * w + kBP + 1] = -(Z01 * iz);
+                    bnd[kBnd * w + kBP + 2] = P.Qw1 + Z00 * iz;
+                }
+            }
         }
+        if (w > 0) __syncthreads();
+    }
+    // knot-parallel: P_k = Q + alpha^2 Z_k^{-1}; lane k takes P_{k+1} from lane k+1
+    double Pk00 = 0.0, Pk01 = 0.0, Pk11 = 0.0;
+    if (own && k >= 1) {
+        const double detZ = Z00 * Z11 - Z01 * Z01;
+        const double iz = a2 / detZ;
+        Pk00 = P.Qw0 + Z11 * iz;
+        Pk01 = -(Z01 * iz);
+        Pk11 = P.Qw1 + Z00 * iz;
+    }
+    double P00 = __shfl_down(Pk00, 1, kWave);
+    double P01 = __shfl_down(Pk01, 1, kWave);
+    double P11 = __shfl_down(Pk11, 1, kWave);
+    if (lane == kWave - 1 && NW > 1 && wv < nwa - 1) {
+        P00 = bnd[kBnd * (wv + 1) + kBP];
+        P01 = bnd[kBnd * (wv + 1) + kBP + 1];
+        P11 = bnd[kBnd * (wv + 1) + kBP + 2];
+    }
+    if (k == N - 1) {
+        P00 = P.Pw0;
+        P01 = 0.0;
+        P11 = P.Pw1;
+    }
+    K.P00 = P00;
+    K.P01 = P01;
+    K.P11 = P11;
+    if (own) {
+        const double B00 = P.Rw0 + b2 * P00;
+        const double B01 = b2 * P01;
+        const double B11 = P.Rw1 + b2 * P11;
+        const double H00 = B00 + W00;
+        const double H01 = B01 + W01;
+        const double H11 = B11 + W11;
+        const double detB = B00 * B11 - B01 * B01;
+        const double trW = (B11 * W00 + B00 * W11) - 2.0 * (B01 * W01);
+        const double det = (detB + trW) + dW;
+        if (!(det > 0.0) || __builtin_isinf(det)) ok = false;
+        const double idet = 1.0 / det;
+        K.h00 = H11 * idet;
+        K.h01 = -(H01 * idet);
+        K.h11 = H00 * idet;
     }
     return ok;
 }
 
-// Forward sweep (thread 0) = oracle dcm_forward.  dr_k overwrites g_k in the knot record.
-__device__ void forward_sweep(const Lds& L, int N)
+// Solve the factored Newton system for the right-hand side g (oracle dcm_solve).  Returns
+// dr (the VRP step of this knot) and dx (the DCM step of xi_{k+1}).
+template <int NW>
+__device__ __forceinline__ void solve(const Knot& K, double g0, double g1, double* bnd, int nwa,
+                                      int wv, int lane, bool own, double& dr0, double& dr1, double& dx0,
+                                      double& dx1)
 {
-    double x0 = 0.0, x1 = 0.0;
-    double2* dxi = reinterpret_cast<double2*>(L.dxi);
-    dxi[0] = make_double2(0.0, 0.0);
-    for (int s = 0; s < N; ++s) {
-        double2* rc = reinterpret_cast<double2*>(L.rec(s));
-        const double2* hr = reinterpret_cast<const double2*>(L.H + (size_t)kHrec * s);
-        const double2 h0 = hr[0], h1 = hr[1], h2 = hr[2];
-        const double2 dd = rc[3], ab = rc[5], kf = rc[7];
-        const double u0 = h1.y * x0 + h2.x * x1;
-        const double u1 = h2.x * x0 + h2.y * x1;
-        const double v0 = h0.x * u0 + h0.y * u1;
-        const double v1 = h0.y * u0 + h1.x * u1;
-        const double al = ab.x, be = ab.y;
-        const double abp = al * be;
-        const double r0 = abp * v0 + kf.x;
-        const double r1 = abp * v1 + kf.y;
-        rc[2] = make_double2(r0, r1);
-        const double n0 = (al * x0 - be * r0) + dd.x;
-        const double n1 = (al * x1 - be * r1) + dd.y;
-        dxi[s + 1] = make_double2(n0, n1);
-        x0 = n0;
-        x1 = n1;
+    const double b2 = K.be * K.be;
+    const double ab = K.al * K.be;
+    double G00 = 0.0, G01 = 0.0, G10 = 0.0, G11 = 0.0, c0 = 0.0, c1 = 0.0, y0 = 0.0, y1 = 0.0;
+    if (own) {
+        const Mmat Mm(K);
+        y0 = K.qx0 + (K.P00 * K.d0 + K.P01 * K.d1);
+        y1 = K.qx1 + (K.P01 * K.d0 + K.P11 * K.d1);
+        const double Mg0 = Mm.m00 * g0 + Mm.m01 * g1;
+        const double Mg1 = Mm.m10 * g0 + Mm.m11 * g1;
+        G00 = K.al * (1.0 - b2 * Mm.m00);
+        G01 = -(K.al * (b2 * Mm.m01));
+        G10 = -(K.al * (b2 * Mm.m10));
+        G11 = K.al * (1.0 - b2 * Mm.m11);
+        c0 = (G00 * y0 + G01 * y1) + ab * Mg0;
+        c1 = (G10 * y0 + G11 * y1) + ab * Mg1;
     }
+    double vn0, vn1;
+    scan_backward<NW>(G00, G01, G10, G11, c0, c1, bnd, nwa, wv, lane, vn0, vn1);
+    double k0 = 0.0, k1 = 0.0, f0 = 0.0, f1 = 0.0;
+    if (own) {
+        const double t0 = y0 + vn0;
+        const double t1 = y1 + vn1;
+        const double hu0 = g0 - K.be * t0;
+        const double hu1 = g1 - K.be * t1;
+        k0 = -(K.h00 * hu0 + K.h01 * hu1);
+        k1 = -(K.h01 * hu0 + K.h11 * hu1);
+        f0 = K.d0 - K.be * k0;
+        f1 = K.d1 - K.be * k1;
+    }
+    double xk0, xk1;
+    scan_forward<NW>(G00, G10, G01, G11, f0, f1, bnd, nwa, wv, lane, dx0, dx1, xk0, xk1);
+    const Mmat Mm(K);
+    dr0 = ab * (Mm.m00 * xk0 + Mm.m10 * xk1) + k0;
+    dr1 = ab * (Mm.m01 * xk0 + Mm.m11 * xk1) + k1;
 }
 
-// The knot a thread owns: slacks, multipliers, residual scratch and the knot's VRP in registers.
-struct Stage {
-    double s[kMaxFacets], lam[kMaxFacets];
-    int m;
-    double r0, r1, rr0, rr1, xr0, xr1, w, be;
-    double dra0, dra1;  // the affine (predictor) VRP step of this knot
-    const double* Ak;   // this knot's facet rows A_k [M][2] and offsets b_k [M] (global memory)
-    const double* bk;
-};
-
-// The facet rows are constant for the whole solve.  They are re-read (L2-resident) at the start
-// of every stage-parallel phase instead of being held in VGPRs across the IPM loop: that keeps the
-// stage threads' register footprint small enough for the software-pipelined Riccati sweeps to
-// run at two waves per SIMD.  The empty asm launders the pointers so LICM cannot hoist the loads
-// back out of the iteration loop.
-struct Rows {
-    double a0[kMaxFacets], a1[kMaxFacets], h[kMaxFacets];
-};
-
-__device__ __forceinline__ void load_rows(const Stage& S, Rows& F)
+// Publishes xi_{k+1} of lane 63 for the next wavefront's lane 0 (read after the next barrier).
+template <int NW>
+__device__ __forceinline__ void publish_xi(const Knot& K, double* bnd, int wv, int lane)
 {
-    const double* Ak = S.Ak;
-    const double* bk = S.bk;
-    asm volatile("" : "+v"(Ak), "+v"(bk));
-#pragma unroll
-    for (int i = 0; i < kMaxFacets; ++i) {
-        if (i < S.m) {
-            F.a0[i] = Ak[2 * i];
-            F.a1[i] = Ak[2 * i + 1];
-            F.h[i] = bk[i];
-        } else {
-            F.a0[i] = 0.0; F.a1[i] = 0.0; F.h[i] = 0.0;
+    if constexpr (NW > 1) {
+        if (lane == kWave - 1) {
+            bnd[kBnd * wv + kBXi] = K.x0;
+            bnd[kBnd * wv + kBXi + 1] = K.x1;
         }
     }
 }
 
-// Per-facet quantities are recomputed from (r, s, lam, A, b) and the stored affine VRP step
-// instead of being kept in registers across phases: the expressions are exactly the oracle's,
-// so the recomputed values are bit-identical, and the knot threads stay at <= 168 VGPRs.
-__device__ __forceinline__ double primal_res(const Stage& S, const Rows& F, int i)
-{
-    const double gr = F.a0[i] * S.r0 + F.a1[i] * S.r1;
-    return (gr + S.s[i]) - F.h[i];
-}
-
-__device__ __forceinline__ void affine_step(const Stage& S, const Rows& F, int i, double& ds,
-                                            double& dl)
-{
-    const double rc = S.s[i] * S.lam[i];
-    ds = (-primal_res(S, F, i)) - (F.a0[i] * S.dra0 + F.a1[i] * S.dra1);
-    dl = ((-rc) - S.lam[i] * ds) / S.s[i];
-}
-
-// Stage-parallel residual pass = the body of oracle dcm_residuals for one knot.  Writes the
-// Euler defect and Q(xi_{k+1} - xi_ref_{k+1}) (or the terminal pv) to LDS; returns pres, ck,
-// rho in registers.  mfac: the facet count to use (0 for the unconstrained warm start).
-__device__ __forceinline__ void stage_residuals(Stage& S, int mfac, int k, int N, const KParams& P,
-                                                const Lds& L, double* flag, double& pres,
-                                                double& ck, double& rh0, double& rh1)
-{
-    rh0 = P.Rw0 * (S.r0 - S.rr0);
-    rh1 = P.Rw1 * (S.r1 - S.rr1);
-    Rows F;
-    if (mfac > 0) load_rows(S, F);
-#pragma unroll
-    for (int i = 0; i < kMaxFacets; ++i) {
-        if (i < mfac) {
-            const double gr = F.a0[i] * S.r0 + F.a1[i] * S.r1;
-            const double rpi = (gr + S.s[i]) - F.h[i];
-            pres = nanmax(pres, fabs(rpi));
-            ck = ck + S.s[i] * S.lam[i];
-            rh0 = rh0 + F.a0[i] * S.lam[i];
-            rh1 = rh1 + F.a1[i] * S.lam[i];
-        }
-    }
-    const double x0 = L.xi[2 * k], x1 = L.xi[2 * k + 1];
-    const double y0 = L.xi[2 * (k + 1)], y1 = L.xi[2 * (k + 1) + 1];
-    const double dx0 = S.w * x0 + (-S.w) * S.r0;
-    const double dk0 = (x0 + dx0 * P.dt) - y0;
-    const double dx1 = S.w * x1 + (-S.w) * S.r1;
-    const double dk1 = (x1 + dx1 * P.dt) - y1;
-    L.d(k, 0) = dk0;
-    L.d(k, 1) = dk1;
-    pres = nanmax(pres, fabs(dk0));
-    pres = nanmax(pres, fabs(dk1));
-    if (k + 1 < N) {
-        L.qx((k + 1), 0) = P.Qw0 * (y0 - S.xr0);
-        L.qx((k + 1), 1) = P.Qw1 * (y1 - S.xr1);
-    } else {
-        flag[1] = P.Pw0 * (y0 - S.xr0);
-        flag[2] = P.Pw1 * (y1 - S.xr1);
-    }
-}
-
-template <int NT>
-// 3 waves per SIMD (<= 168 VGPRs): with ~25 KB of LDS per QP that is 6 two-wave workgroups
-// (6 QPs) per CU, and every SIMD keeps its own Riccati sweep streams in flight.
 #ifndef BLF_MIN_WAVES
-#define BLF_MIN_WAVES 3
+#define BLF_MIN_WAVES 2   // waves per SIMD the register allocation must allow (<= 256 VGPRs)
 #endif
+template <int NT>
 __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_ipm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -338,67 +534,75 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     constexpr int NW = NT / kWave;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
-    Lds L(smem, N, NW);
-    double* red = L.red;               // [NW] scratch for block reductions
-    double* flag = L.red + 4 * NW;     // shared scalars: [0] factor failed, [1..2] terminal pv
+    const Lds L(smem, N, M, NW);
+    double* bnd = L.bnd;
+    const int nwa = (N + kWave - 1) / kWave;
+    Reduce<NW> R{L.red, nwa};
 
     const int k = threadIdx.x;
+    const int lane = k & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(k >> 6);
     const bool own = k < N;
+    const bool last = k == N - 1;
     const int64_t p = blockIdx.x;
     STAMP(t_start);
 
     // ---- load the knot this thread owns ----
-    Stage S;
-    S.m = 0;
-    S.r0 = S.r1 = S.rr0 = S.rr1 = S.xr0 = S.xr1 = S.w = S.be = S.dra0 = S.dra1 = 0.0;
-    S.Ak = Ain;
-    S.bk = bin;
+    Knot K;
+    K.m = 0;
+    K.r0 = K.r1 = K.x0 = K.x1 = K.w = K.be = 0.0;
+    K.rh0 = K.rh1 = K.d0 = K.d1 = K.qx0 = K.qx1 = 0.0;
+    K.P00 = K.P01 = K.P11 = K.h00 = K.h01 = K.h11 = 0.0;
 #pragma unroll
-    for (int i = 0; i < kMaxFacets; ++i) {
-        S.s[i] = 1.0; S.lam[i] = 0.0;
-    }
+    for (int i = 0; i < kMaxFacets; ++i) { K.s[i] = 1.0; K.lam[i] = 0.0; }
     bool bad = false;
+    const double xi00 = xi_init[2 * p], xi01 = xi_init[2 * p + 1];
     if (own) {
         const int64_t st = p * N + k;
-        S.m = nfacets[st];
-        bad = (S.m < 0 || S.m > M);
-        S.Ak = Ain + st * M * 2;
-        S.bk = bin + st * M;
-        S.w = omega[st];
-        S.be = P.dt * S.w;
-        const double al = 1.0 + S.be;
-        L.al(k) = al;
-        L.be(k) = S.be;
-        L.a2(k) = al * al;
-        L.b2(k) = S.be * S.be;
-        L.om(k) = S.w;
-        S.rr0 = vrp_ref[2 * st];
-        S.rr1 = vrp_ref[2 * st + 1];
-        S.r0 = S.rr0;
-        S.r1 = S.rr1;
-        L.dr(k, 0) = S.rr0;      // scratch: initial VRP for the rollout below
-        L.dr(k, 1) = S.rr1;
-        const int64_t sx = p * (N + 1) + (k + 1);
-        S.xr0 = xi_ref[2 * sx];
-        S.xr1 = xi_ref[2 * sx + 1];
+        K.m = nfacets[st];
+        bad = (K.m < 0 || K.m > M);
+        if (bad) K.m = 0;
+        K.w = omega[st];
+        K.be = P.dt * K.w;
+        K.r0 = vrp_ref[2 * st];
+        K.r1 = vrp_ref[2 * st + 1];
+        const double* Ak = Ain + st * M * 2;
+        const double* bk = bin + st * M;
+        for (int i = 0; i < K.m; ++i) {
+            L.A2[i * N + k] = make_double2(Ak[2 * i], Ak[2 * i + 1]);
+            L.bb[i * N + k] = bk[i];
+        }
     }
-    if (k == 0) {
-        L.xi[0] = xi_init[2 * p];
-        L.xi[1] = xi_init[2 * p + 1];
+    K.al = 1.0 + K.be;
+    // this knot's references (re-read from global memory in every residual pass)
+    const int64_t kk_ = own ? p * N + k : 0;
+    const double* rref = vrp_ref + 2 * kk_;
+    const double* xref = xi_ref + 2 * (own ? p * (N + 1) + (k + 1) : 0);
+    int mmax = K.m;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int o = __shfl_xor(mmax, off, kWave);
+        mmax = o > mmax ? o : mmax;
     }
+    mmax = __builtin_amdgcn_readfirstlane(mmax);
     const bool any_bad = __syncthreads_or(bad);
 
-    // ---- initial state 1: reference Euler rollout of vrp_ref (thread 0) ----
-    if (k == 0) {
-        for (int q = 0; q < N; ++q) {
-            const double wq = L.om(q);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const double x = L.xi[2 * q + j];
-                const double dx = wq * x + (-wq) * L.dr(q, j);
-                L.xi[2 * (q + 1) + j] = x + dx * P.dt;
+    // ---- initial point 1: rollout of vrp_ref, xi_{k+1} = alpha_k xi_k - beta_k r_k ----
+    {
+        double f0 = 0.0, f1 = 0.0;
+        if (own) {
+            if (k == 0) {
+                f0 = K.al * xi00 - K.be * K.r0;
+                f1 = K.al * xi01 - K.be * K.r1;
+            } else {
+                f0 = -(K.be * K.r0);
+                f1 = -(K.be * K.r1);
             }
         }
+        const double ga = own ? K.al : 0.0;
+        double xk0, xk1;
+        scan_forward<NW>(ga, 0.0, 0.0, ga, f0, f1, bnd, nwa, wv, lane, K.x0, K.x1, xk0, xk1);
+        publish_xi<NW>(K, bnd, wv, lane);
     }
     __syncthreads();
 
@@ -406,98 +610,65 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     if (any_bad) {
         status = BLF_QP_BAD_FACETS;
     } else {
-        // ---- initial state 2: full Newton step of the unconstrained QP (W = 0, lam = 0) ----
+        double xk0, xk1, pres, ck;
+        // ---- initial point 2: full Newton step of the unconstrained QP (W = 0, lam = 0) ----
+        xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+        if (own) residuals(K, false, P, last, L.A2, L.bb, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+        bool ok = factor<NW>(K, P, 0.0, 0.0, 0.0, 0.0, bnd, N, nwa, k, wv, lane, own);
+        const bool init_bad = __syncthreads_or(!ok);
         {
-            double pres = 0.0, ck = 0.0, rh0 = 0.0, rh1 = 0.0;
+            double dr0, dr1, dx0, dx1;
+            solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
             if (own) {
-                stage_residuals(S, 0, k, N, P, L, flag, pres, ck, rh0, rh1);
-                L.W(k, 0) = 0.0; L.W(k, 1) = 0.0; L.W(k, 2) = 0.0; L.W(k, 3) = 0.0;
-                L.g(k, 0) = rh0;
-                L.g(k, 1) = rh1;
-            }
-            __syncthreads();
-            if (k == 0) {
-                const bool ok = backward_sweep<true>(L, P, flag[1], flag[2]);
-                flag[0] = ok ? 0.0 : 1.0;
-                forward_sweep(L, N);
-            }
-            __syncthreads();
-            if (own) {
-                S.r0 = S.r0 + L.dr(k, 0);
-                S.r1 = S.r1 + L.dr(k, 1);
-                const double y0 = L.xi[2 * (k + 1)] + L.dxi[2 * (k + 1)];
-                const double y1 = L.xi[2 * (k + 1) + 1] + L.dxi[2 * (k + 1) + 1];
-                L.xi[2 * (k + 1)] = y0;
-                L.xi[2 * (k + 1) + 1] = y1;
-                // Q (xi - xi_ref) terms of the start-up costate pass below
-                if (k + 1 < N) {
-                    L.qx(k + 1, 0) = P.Qw0 * (y0 - S.xr0);
-                    L.qx(k + 1, 1) = P.Qw1 * (y1 - S.xr1);
-                } else {
-                    flag[1] = P.Pw0 * (y0 - S.xr0);
-                    flag[2] = P.Pw1 * (y1 - S.xr1);
-                }
+                K.r0 = K.r0 + dr0;
+                K.r1 = K.r1 + dr1;
+                K.x0 = K.x0 + dx0;
+                K.x1 = K.x1 + dx1;
             }
         }
-        const bool init_bad = flag[0] != 0.0;
-        // ---- initial state 3: s = max(b - A r, 1e-2), lam = 1; ntot ----
-        Rows F;
-        load_rows(S, F);
-#pragma unroll
-        for (int i = 0; i < kMaxFacets; ++i) {
-            if (i < S.m) {
-                const double gr = F.a0[i] * S.r0 + F.a1[i] * S.r1;
-                const double sl = F.h[i] - gr;
-                S.s[i] = sl > 1e-2 ? sl : 1e-2;
-                S.lam[i] = 1.0;
-            }
-        }
-        int ntot = wave_isum(S.m);
-        if constexpr (NW > 1) {
-            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (double)ntot;
-            __syncthreads();
-            ntot = 0;
-            for (int i = 0; i < NW; ++i) ntot += (int)red[i];
-        }
-        __syncthreads();
-        // costates nu (single shooting) for the initial dual residual, thread 0 -> L.dxi
-        if (k == 0) {
-            double n0 = flag[1];
-            double n1 = flag[2];
-            L.dxi[2 * N] = n0;
-            L.dxi[2 * N + 1] = n1;
-            for (int q = N - 1; q >= 1; --q) {
-                const double aq = L.al(q);
-                n0 = L.qx(q, 0) + aq * n0;
-                n1 = L.qx(q, 1) + aq * n1;
-                L.dxi[2 * q] = n0;
-                L.dxi[2 * q + 1] = n1;
-            }
-        }
-        __syncthreads();
-        double dres = 0.0;
+        publish_xi<NW>(K, bnd, wv, lane);
+        // ---- initial point 3: s = max(b - A r, 1e-2), lam = 1 ----
         if (own) {
-            double rj0 = P.Rw0 * (S.r0 - S.rr0);
-            double rj1 = P.Rw1 * (S.r1 - S.rr1);
 #pragma unroll
-            for (int i = 0; i < kMaxFacets; ++i)
-                if (i < S.m) {
-                    rj0 = rj0 + F.a0[i] * S.lam[i];
-                    rj1 = rj1 + F.a1[i] * S.lam[i];
+            for (int i = 0; i < kMaxFacets; ++i) {
+                if (i >= mmax) break;
+                if (i < K.m) {
+                    const double2 a = L.A2[i * N + k];
+                    const double gr = a.x * K.r0 + a.y * K.r1;
+                    const double sl = L.bb[i * N + k] - gr;
+                    K.s[i] = sl > 1e-2 ? sl : 1e-2;
+                    K.lam[i] = 1.0;
                 }
-            dres = nanmax(dres, fabs(rj0 - S.be * L.dxi[2 * (k + 1)]));
-            dres = nanmax(dres, fabs(rj1 - S.be * L.dxi[2 * (k + 1) + 1]));
+            }
         }
-        dres = block_nanmax<NW>(dres, red);
+        const int ntot = (int)R.sum((double)K.m);   // exact: small integers
+        // ---- initial dual residual: costates nu_k = qx_k + alpha_k nu_{k+1} (backward scan) ----
+        xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+        if (own) residuals(K, true, P, last, L.A2, L.bb, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+        double dres = 0.0;
+        {
+            const double ga = own ? K.al : 0.0;
+            const double c0 = own ? K.al * K.qx0 : 0.0, c1 = own ? K.al * K.qx1 : 0.0;
+            double vn0, vn1;
+            scan_backward<NW>(ga, 0.0, 0.0, ga, c0, c1, bnd, nwa, wv, lane, vn0, vn1);
+            if (own) {
+                const double nu0 = K.qx0 + vn0;
+                const double nu1 = K.qx1 + vn1;
+                dres = nanmax(dres, fabs(K.rh0 - K.be * nu0));
+                dres = nanmax(dres, fabs(K.rh1 - K.be * nu1));
+            }
+        }
+        dres = R.nanmax_(dres);
         if (init_bad) status = BLF_QP_NUMERICAL;
 
         for (it = 0; status == 0; ++it) {
-            // ---- residuals (stage-parallel) ----
-            double pres = 0.0, ck = 0.0, rh0 = 0.0, rh1 = 0.0;
-            if (own) stage_residuals(S, S.m, k, N, P, L, flag, pres, ck, rh0, rh1);
-            const double csum = block_sum<NW>(ck, red);
-            const double mu = ntot > 0 ? csum / (double)ntot : 0.0;
-            pres = block_nanmax<NW>(pres, red);
+            // ---- residuals (knot-parallel) ----
+            xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+            pres = 0.0;
+            ck = 0.0;
+            if (own) residuals(K, true, P, last, L.A2, L.bb, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+            R.sum_nanmax(ck, pres);
+            const double mu = ntot > 0 ? ck / (double)ntot : 0.0;
             if (!(mu == mu) || !(pres == pres) || !(dres == dres) || __builtin_isinf(mu)) {
                 status = BLF_QP_NUMERICAL;
                 break;
@@ -508,191 +679,184 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 break;
             }
 
-            // ---- W = A^T diag(lam/s) A, det W, affine right-hand side (stage-parallel) ----
+            // ---- W-phase: 1/s, W = A^T diag(lam/s) A, det W, predictor rhs ----
+            double W00 = 0.0, W01 = 0.0, W11 = 0.0, dW = 0.0;
+            double g0 = K.rh0, g1 = K.rh1;
             if (own) {
-                Rows F;
-                load_rows(S, F);
-                double W00 = 0.0, W01 = 0.0, W11 = 0.0, dW = 0.0;
-                double g0 = rh0, g1 = rh1;
+                const int kx = opaque(k);
                 double sg[kMaxFacets];
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
                     sg[i] = 0.0;
-                    if (i < S.m) {
-                        sg[i] = S.lam[i] / S.s[i];
-                        const double t0 = sg[i] * F.a0[i];
-                        const double t1 = sg[i] * F.a1[i];
-                        W00 = W00 + t0 * F.a0[i];
-                        W01 = W01 + t0 * F.a1[i];
-                        W11 = W11 + t1 * F.a1[i];
-                        const double rc = S.s[i] * S.lam[i];
-                        const double e = (S.lam[i] * primal_res(S, F, i) - rc) / S.s[i];
-                        g0 = g0 + F.a0[i] * e;
-                        g1 = g1 + F.a1[i] * e;
+                    if (i >= mmax) break;
+                    if (i < K.m) {
+                        const double2 a = L.A2[i * N + kx];
+                        const double is = 1.0 / K.s[i];
+                        L.IS[i * N + kx] = is;
+                        sg[i] = K.lam[i] * is;
+                        const double t0 = sg[i] * a.x;
+                        const double t1 = sg[i] * a.y;
+                        W00 = W00 + t0 * a.x;
+                        W01 = W01 + t0 * a.y;
+                        W11 = W11 + t1 * a.y;
+                        const double rpi = facet_rp(K, a, L.bb[i * N + kx], i);
+                        const double e = (K.lam[i] * rpi - K.s[i] * K.lam[i]) * is;
+                        g0 = g0 + a.x * e;
+                        g1 = g1 + a.y * e;
                     }
                 }
 #pragma unroll
                 for (int i = 1; i < kMaxFacets; ++i) {
+                    if (i >= mmax) break;
+                    if (i < K.m) {
+                        const double2 ai = L.A2[i * N + kx];
 #pragma unroll
-                    for (int j = 0; j < i; ++j) {
-                        if (i < S.m) {
-                            const double cr = F.a0[i] * F.a1[j] - F.a1[i] * F.a0[j];
+                        for (int j = 0; j < i; ++j) {
+                            const double2 aj = L.A2[j * N + kx];
+                            const double cr = ai.x * aj.y - ai.y * aj.x;
                             dW = dW + (sg[i] * sg[j]) * (cr * cr);
                         }
                     }
                 }
-                L.W(k, 0) = W00;
-                L.W(k, 1) = W01;
-                L.W(k, 2) = W11;
-                L.W(k, 3) = dW;
-                L.g(k, 0) = g0;
-                L.g(k, 1) = g1;
             }
-            __syncthreads();
-
-            // ---- affine (predictor) Newton step: factor + solve on thread 0 ----
-            if (k == 0) {
-                STAMP(t_f);
-                const bool ok = backward_sweep<true>(L, P, flag[1], flag[2]);
-                flag[0] = ok ? 0.0 : 1.0;
-                forward_sweep(L, N);
-                STAMP_ADD(1, t_f);
+            STAMP(t_f);
+            ok = factor<NW>(K, P, W00, W01, W11, dW, bnd, N, nwa, k, wv, lane, own);
+            if (__syncthreads_or(!ok)) {
+                status = BLF_QP_NUMERICAL;
+                break;
             }
-            __syncthreads();
-            const bool factor_bad = flag[0] != 0.0;
+            STAMP_ADD(1, t_f);
 
-            double smax = __builtin_inf();
+            // ---- predictor ----
+            STAMP(t_s);
+            double dra0, dra1, dx0, dx1;
+            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dra0, dra1, dx0, dx1);
+            double q = 0.0;
             if (own) {
-                Rows F;
-                load_rows(S, F);
-                S.dra0 = L.dr(k, 0);
-                S.dra1 = L.dr(k, 1);
+                const int kx = opaque(k);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < S.m) {
+                    if (i >= mmax) break;
+                    if (i < K.m) {
                         double ds, dl;
-                        affine_step(S, F, i, ds, dl);
-                        if (ds < 0.0) smax = keepmin(smax, (-S.s[i]) / ds);
-                        if (dl < 0.0) smax = keepmin(smax, (-S.lam[i]) / dl);
+                        const double is = L.IS[i * N + kx];
+                        affine_step(K, L.A2[i * N + kx], L.bb[i * N + kx], is, i, dra0, dra1, ds, dl);
+                        if (ds < 0.0) q = keepmax(q, (-ds) * is);
+                        if (dl < 0.0) q = keepmax(q, (K.s[i] + ds) * is);
                     }
                 }
             }
-            smax = block_keepmin<NW>(smax, red);
-            const double a_aff = smax < 1.0 ? smax : 1.0;
+            const double qa = R.keepmax(q);
+            const double a_aff = qa > 1.0 ? 1.0 / qa : 1.0;
             ck = 0.0;
             if (own) {
-                Rows F;
-                load_rows(S, F);
+                const int kx = opaque(k);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < S.m) {
+                    if (i >= mmax) break;
+                    if (i < K.m) {
                         double ds, dl;
-                        affine_step(S, F, i, ds, dl);
-                        ck = ck + (S.s[i] + a_aff * ds) * (S.lam[i] + a_aff * dl);
+                        affine_step(K, L.A2[i * N + kx], L.bb[i * N + kx], L.IS[i * N + kx], i, dra0,
+                                    dra1, ds, dl);
+                        ck = ck + (K.s[i] + a_aff * ds) * (K.lam[i] + a_aff * dl);
                     }
                 }
             }
-            const double caff = block_sum<NW>(ck, red);
+            const double caff = R.sum(ck);
             const double mu_aff = ntot > 0 ? caff / (double)ntot : 0.0;
             double sigma = 0.0;
             if (mu > 0.0) {
-                const double q = mu_aff / mu;
-                sigma = (q * q) * q;
+                const double qq = mu_aff / mu;
+                sigma = (qq * qq) * qq;
             }
             const double sigma_mu = sigma * mu;
 
-            // ---- corrector right-hand side (stage-parallel) + solve (thread 0) ----
+            // ---- corrector ----
+            g0 = K.rh0;
+            g1 = K.rh1;
             if (own) {
-                Rows F;
-                load_rows(S, F);
-                double g0 = rh0, g1 = rh1;
+                const int kx = opaque(k);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < S.m) {
+                    if (i >= mmax) break;
+                    if (i < K.m) {
+                        const double2 a = L.A2[i * N + kx];
+                        const double bi = L.bb[i * N + kx];
+                        const double is = L.IS[i * N + kx];
                         double ds, dl;
-                        affine_step(S, F, i, ds, dl);
-                        const double rc = (S.s[i] * S.lam[i] + ds * dl) - sigma_mu;
-                        const double e = (S.lam[i] * primal_res(S, F, i) - rc) / S.s[i];
-                        g0 = g0 + F.a0[i] * e;
-                        g1 = g1 + F.a1[i] * e;
+                        affine_step(K, a, bi, is, i, dra0, dra1, ds, dl);
+                        const double rc = (K.s[i] * K.lam[i] + ds * dl) - sigma_mu;
+                        const double rpi = facet_rp(K, a, bi, i);
+                        const double e = (K.lam[i] * rpi - rc) * is;
+                        g0 = g0 + a.x * e;
+                        g1 = g1 + a.y * e;
                     }
                 }
-                L.g(k, 0) = g0;
-                L.g(k, 1) = g1;
             }
-            __syncthreads();
-            if (k == 0) {
-                STAMP(t_s);
-                backward_sweep<false>(L, P, flag[1], flag[2]);
-                forward_sweep(L, N);
-                STAMP_ADD(2, t_s);
-            }
-            __syncthreads();
-
-            // ---- corrector step length and update ----
-            smax = __builtin_inf();
-            double dr0 = 0.0, dr1 = 0.0;
+            double dr0, dr1;
+            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
+            STAMP_ADD(2, t_s);
+            q = 0.0;
             double cds[kMaxFacets], cdl[kMaxFacets];
             if (own) {
-                Rows F;
-                load_rows(S, F);
-                dr0 = L.dr(k, 0);
-                dr1 = L.dr(k, 1);
+                const int kx = opaque(k);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
                     cds[i] = 0.0;
                     cdl[i] = 0.0;
-                    if (i < S.m) {
+                    if (i >= mmax) break;
+                    if (i < K.m) {
+                        const double2 a = L.A2[i * N + kx];
+                        const double bi = L.bb[i * N + kx];
+                        const double is = L.IS[i * N + kx];
                         double ads, adl;
-                        affine_step(S, F, i, ads, adl);
-                        const double rc = (S.s[i] * S.lam[i] + ads * adl) - sigma_mu;
-                        const double ds = (-primal_res(S, F, i)) - (F.a0[i] * dr0 + F.a1[i] * dr1);
-                        const double dl = ((-rc) - S.lam[i] * ds) / S.s[i];
-                        if (ds < 0.0) smax = keepmin(smax, (-S.s[i]) / ds);
-                        if (dl < 0.0) smax = keepmin(smax, (-S.lam[i]) / dl);
+                        affine_step(K, a, bi, is, i, dra0, dra1, ads, adl);
+                        const double rc = (K.s[i] * K.lam[i] + ads * adl) - sigma_mu;
+                        const double rpi = facet_rp(K, a, bi, i);
+                        const double ds = (-rpi) - (a.x * dr0 + a.y * dr1);
+                        const double dl = ((-rc) - K.lam[i] * ds) * is;
+                        if (ds < 0.0) q = keepmax(q, (-ds) * is);
+                        if (dl < 0.0) q = keepmax(q, (-dl) / K.lam[i]);
                         cds[i] = ds;
                         cdl[i] = dl;
                     }
                 }
             }
-            smax = block_keepmin<NW>(smax, red);
-            if (factor_bad) {
-                status = BLF_QP_NUMERICAL;
-                break;
-            }
-            const double step = 0.99 * smax;
+            const double qc = R.keepmax(q);
+            const double step = qc > 0.0 ? 0.99 / qc : 1.0;
             const double a = step < 1.0 ? step : 1.0;
             if (own) {
-                S.r0 = S.r0 + a * dr0;
-                S.r1 = S.r1 + a * dr1;
-                L.xi[2 * (k + 1)] = L.xi[2 * (k + 1)] + a * L.dxi[2 * (k + 1)];
-                L.xi[2 * (k + 1) + 1] = L.xi[2 * (k + 1) + 1] + a * L.dxi[2 * (k + 1) + 1];
+                K.r0 = K.r0 + a * dr0;
+                K.r1 = K.r1 + a * dr1;
+                K.x0 = K.x0 + a * dx0;
+                K.x1 = K.x1 + a * dx1;
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i < S.m) {
-                        S.s[i] = S.s[i] + a * cds[i];
-                        S.lam[i] = S.lam[i] + a * cdl[i];
+                    if (i >= mmax) break;
+                    if (i < K.m) {
+                        K.s[i] = K.s[i] + a * cds[i];
+                        K.lam[i] = K.lam[i] + a * cdl[i];
                     }
                 }
             }
+            publish_xi<NW>(K, bnd, wv, lane);
             dres = dres * (1.0 - a);
             __syncthreads();
         }
     }
 
     // ---- outputs ----
-    __syncthreads();
     if (own) {
         const int64_t st = p * N + k;
-        vrp_out[2 * st] = S.r0;
-        vrp_out[2 * st + 1] = S.r1;
+        vrp_out[2 * st] = K.r0;
+        vrp_out[2 * st + 1] = K.r1;
         const int64_t sx = p * (N + 1) + (k + 1);
-        xi_out[2 * sx] = L.xi[2 * (k + 1)];
-        xi_out[2 * sx + 1] = L.xi[2 * (k + 1) + 1];
+        xi_out[2 * sx] = K.x0;
+        xi_out[2 * sx + 1] = K.x1;
     }
     if (k == 0) {
-        xi_out[2 * p * (N + 1)] = L.xi[0];
-        xi_out[2 * p * (N + 1) + 1] = L.xi[1];
+        xi_out[2 * p * (N + 1)] = xi00;
+        xi_out[2 * p * (N + 1) + 1] = xi01;
         status_out[p] = status;
         iters_out[p] = it;
         STAMP_ADD(0, t_start);
@@ -706,8 +870,10 @@ template <int NT>
 blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb, int64_t batch,
                      const blf_dcm_mpc_solution* sol, hipStream_t s)
 {
-    const size_t lds = sizeof(double) * lds_doubles(kp.N, NT / kWave);
-    if (lds > 160 * 1024) return set_error(BLF_ERR_UNSUPPORTED, "horizon %d needs %zu B of LDS", kp.N, lds);
+    const size_t lds = sizeof(double) * Lds(nullptr, kp.N, kp.M, NT / kWave).total;
+    if (lds > 160 * 1024)
+        return set_error(BLF_ERR_UNSUPPORTED, "horizon %d with %d facet slots needs %zu B of LDS",
+                         kp.N, kp.M, lds);
     hipLaunchKernelGGL(dcm_mpc_ipm_kernel<NT>, dim3((unsigned)batch), dim3(NT), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                        pb->nfacets, sol->xi, sol->vrp, sol->status, sol->iters);

@@ -299,32 +299,174 @@ double orc_wave_tree_sum(const double* c, int n)
 }
 
 #define MF 8
+#define WV 64
 
-/* Working state of one QP solve (all arrays owned by the caller of dcm_ws_alloc). */
+/* Working state of one QP solve.  Per-knot arrays are indexed by the knot k = 64 w + lane: the
+ * device runs one thread per knot, NW = ceil(N / 64) wavefronts per QP. */
 typedef struct {
-    int N, M, ntot;
+    int N, M, NW, ntot;
+    int scans;                             /* 1: device-order Kogge-Stone scans, 0: sequential */
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1;
     const double *omega, *xi_ref, *vrp_ref, *A, *b;
     const int32_t* nf;
-    double *al, *be, *a2, *b2;          /* [N] */
-    double *s, *lam, *rp, *prod;        /* [N][MF] */
-    double *W;                          /* [N][4]  A^T diag(lam/s) A (3), det of it (1) */
-    double *Hi, *Pn;                    /* [N][3] */
-    double *g, *d, *rho, *kff, *dr, *qx; /* [N][2] */
-    double *c;                          /* [N] */
-    double *dxi, *nu;                   /* [N+1][2] */
-    double *xi, *vrp;                   /* outputs, updated in place */
+    double *al, *be, *a2, *b2, *ab;        /* [N] */
+    double *s, *lam, *is, *cds, *cdl;      /* [N][MF] slacks, multipliers, 1/s, step */
+    double *W;                             /* [N][4] A^T diag(lam/s) A (3), its determinant (1) */
+    double *E, *Z, *Pn, *h;                /* [N][3] */
+    double *G, *Mm;                        /* [N][4]: G_k, M_k = P_{k+1} h_k */
+    double *rh, *g, *d, *qx, *dr, *dra;    /* [N][2] */
+    double *c, *q;                         /* [N] reduction partials */
+    double *sc, *sg;                       /* [N][2], [N][4] scan elements */
+    double *v, *x;                         /* [N+1][2] scan results */
+    double *xi, *vrp;                      /* outputs, updated in place */
 } dcm_ws;
 
-/* Stage-parallel residual pass (the device runs one thread per knot): primal residuals
- * rp = A r + s - b, complementarity partials c_k, rho = R (r - r_ref) + A^T lam, Euler defects
- * d_k (reference step order) and Q (xi_k - xi_ref_k).  Returns max |rp|, |d| (NaN-propagating). */
-static double dcm_residuals(dcm_ws* w)
+static double keepmax(double q, double x) { return x > q ? x : q; }
+static double nanmax(double q, double x) { return (x > q || x != x) ? x : q; }
+
+/* Backward affine recursion v_k = G_k v_{k+1} + c_k (v_N = 0) the way the device evaluates it:
+ * a Kogge-Stone scan over the 64 lanes of each wavefront (lane l combines with lane l + d from
+ * the previous level, d = 1, 2, ..., 32; lanes past the last knot hold the zero element), then
+ * the wavefronts from last to first apply the first knot's value of the next wavefront.
+ * Result: w->v[k] = v_k for k < N, w->v[N] = 0. */
+static void scan_backward(dcm_ws* w, const double* G, const double* c)
+{
+    const int N = w->N;
+    w->v[2 * N] = 0.0;
+    w->v[2 * N + 1] = 0.0;
+    if (!w->scans) {   /* CPU-efficient sequential recursion (cpu_baseline timing only) */
+        for (int k = N - 1; k >= 0; --k) {
+            const double* g = G + 4 * k;
+            const double vn0 = w->v[2 * (k + 1)], vn1 = w->v[2 * (k + 1) + 1];
+            w->v[2 * k] = (g[0] * vn0 + g[1] * vn1) + c[2 * k];
+            w->v[2 * k + 1] = (g[2] * vn0 + g[3] * vn1) + c[2 * k + 1];
+        }
+        return;
+    }
+    for (int wv = w->NW - 1; wv >= 0; --wv) {
+        double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
+        for (int l = 0; l < WV; ++l) {
+            const int k = WV * wv + l;
+            for (int j = 0; j < 4; ++j) g[l][j] = k < N ? G[4 * k + j] : 0.0;
+            for (int j = 0; j < 2; ++j) e[l][j] = k < N ? c[2 * k + j] : 0.0;
+        }
+        for (int dd = 1; dd < WV; dd <<= 1) {
+            for (int l = 0; l < WV; ++l) {
+                if (l + dd < WV) {
+                    const double* a = g[l];
+                    const double* bq = g[l + dd];
+                    const double* ce = e[l + dd];
+                    ng[l][0] = a[0] * bq[0] + a[1] * bq[2];
+                    ng[l][1] = a[0] * bq[1] + a[1] * bq[3];
+                    ng[l][2] = a[2] * bq[0] + a[3] * bq[2];
+                    ng[l][3] = a[2] * bq[1] + a[3] * bq[3];
+                    ne[l][0] = (a[0] * ce[0] + a[1] * ce[1]) + e[l][0];
+                    ne[l][1] = (a[2] * ce[0] + a[3] * ce[1]) + e[l][1];
+                } else {
+                    memcpy(ng[l], g[l], sizeof(ng[l]));
+                    memcpy(ne[l], e[l], sizeof(ne[l]));
+                }
+            }
+            memcpy(g, ng, sizeof(g));
+            memcpy(e, ne, sizeof(e));
+        }
+        for (int l = 0; l < WV; ++l) {
+            const int k = WV * wv + l;
+            if (k >= N) break;
+            if (wv == w->NW - 1) {
+                w->v[2 * k] = e[l][0];
+                w->v[2 * k + 1] = e[l][1];
+            } else {
+                const double vn0 = w->v[2 * WV * (wv + 1)], vn1 = w->v[2 * WV * (wv + 1) + 1];
+                w->v[2 * k] = (g[l][0] * vn0 + g[l][1] * vn1) + e[l][0];
+                w->v[2 * k + 1] = (g[l][2] * vn0 + g[l][3] * vn1) + e[l][1];
+            }
+        }
+    }
+}
+
+/* Forward affine recursion x_{k+1} = F_k x_k + f_k (x_0 = 0): Kogge-Stone per wavefront (lane l
+ * combines with lane l - d), then the wavefronts from first to last apply the last value of the
+ * previous wavefront.  F is given as [N][4] row-major; `transpose` uses F_k = G_k^T.
+ * Result: w->x[k + 1] for k < N, w->x[0] = 0. */
+static void scan_forward(dcm_ws* w, const double* F, int transpose, const double* f)
+{
+    const int N = w->N;
+    w->x[0] = 0.0;
+    w->x[1] = 0.0;
+    if (!w->scans) {   /* CPU-efficient sequential recursion (cpu_baseline timing only) */
+        for (int k = 0; k < N; ++k) {
+            const double* F_ = F + 4 * k;
+            const double f01 = transpose ? F_[2] : F_[1], f10 = transpose ? F_[1] : F_[2];
+            const double x0 = w->x[2 * k], x1 = w->x[2 * k + 1];
+            w->x[2 * (k + 1)] = (F_[0] * x0 + f01 * x1) + f[2 * k];
+            w->x[2 * (k + 1) + 1] = (f10 * x0 + F_[3] * x1) + f[2 * k + 1];
+        }
+        return;
+    }
+    for (int wv = 0; wv < w->NW; ++wv) {
+        double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
+        for (int l = 0; l < WV; ++l) {
+            const int k = WV * wv + l;
+            if (k < N) {
+                const double* Fk = F + 4 * k;
+                g[l][0] = Fk[0];
+                g[l][1] = transpose ? Fk[2] : Fk[1];
+                g[l][2] = transpose ? Fk[1] : Fk[2];
+                g[l][3] = Fk[3];
+                e[l][0] = f[2 * k];
+                e[l][1] = f[2 * k + 1];
+            } else {
+                g[l][0] = g[l][1] = g[l][2] = g[l][3] = 0.0;
+                e[l][0] = e[l][1] = 0.0;
+            }
+        }
+        for (int dd = 1; dd < WV; dd <<= 1) {
+            for (int l = 0; l < WV; ++l) {
+                if (l - dd >= 0) {
+                    const double* a = g[l];
+                    const double* bq = g[l - dd];
+                    const double* ce = e[l - dd];
+                    ng[l][0] = a[0] * bq[0] + a[1] * bq[2];
+                    ng[l][1] = a[0] * bq[1] + a[1] * bq[3];
+                    ng[l][2] = a[2] * bq[0] + a[3] * bq[2];
+                    ng[l][3] = a[2] * bq[1] + a[3] * bq[3];
+                    ne[l][0] = (a[0] * ce[0] + a[1] * ce[1]) + e[l][0];
+                    ne[l][1] = (a[2] * ce[0] + a[3] * ce[1]) + e[l][1];
+                } else {
+                    memcpy(ng[l], g[l], sizeof(ng[l]));
+                    memcpy(ne[l], e[l], sizeof(ne[l]));
+                }
+            }
+            memcpy(g, ng, sizeof(g));
+            memcpy(e, ne, sizeof(e));
+        }
+        for (int l = 0; l < WV; ++l) {
+            const int k = WV * wv + l;
+            if (k >= N) break;
+            if (wv == 0) {
+                w->x[2 * (k + 1)] = e[l][0];
+                w->x[2 * (k + 1) + 1] = e[l][1];
+            } else {
+                const double x0 = w->x[2 * WV * wv], x1 = w->x[2 * WV * wv + 1];
+                w->x[2 * (k + 1)] = (g[l][0] * x0 + g[l][1] * x1) + e[l][0];
+                w->x[2 * (k + 1) + 1] = (g[l][2] * x0 + g[l][3] * x1) + e[l][1];
+            }
+        }
+    }
+}
+
+/* Stage-parallel residual pass (one device thread per knot): rp = A r + s - b is recomputed
+ * where needed; here complementarity partials c_k, rh = R (r - r_ref) + A^T lam, the Euler
+ * defects d_k (reference step order, ForwardEuler.tpp:37-45 over LinearTimeInvariantSystem.cpp:71)
+ * and qx_k = Q (xi_{k+1} - xi_ref_{k+1}) (knot N-1: the terminal gradient P (xi_N - xi_ref_N)).
+ * use_facets = 0: no facets (the warm start).  Returns max |rp|, |d| (NaN-propagating). */
+static double dcm_residuals(dcm_ws* w, int use_facets)
 {
     const int N = w->N, M = w->M;
     double pres = 0.0;
     for (int k = 0; k < N; ++k) {
-        const int m = w->nf[k];
+        const int m = use_facets ? w->nf[k] : 0;
         const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
         double ck = 0.0;
         double rh0 = w->Rw0 * (r0 - w->vrp_ref[2 * k]);
@@ -334,138 +476,226 @@ static double dcm_residuals(dcm_ws* w)
             const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
             const double gr = a[0] * r0 + a[1] * r1;
             const double rpi = (gr + si) - w->b[k * M + i];
-            w->rp[k * MF + i] = rpi;
-            const double e = fabs(rpi);
-            if (e > pres || e != e) pres = e;
+            pres = nanmax(pres, fabs(rpi));
             ck = ck + si * li;
             rh0 = rh0 + a[0] * li;
             rh1 = rh1 + a[1] * li;
         }
         w->c[k] = ck;
-        w->rho[2 * k] = rh0;
-        w->rho[2 * k + 1] = rh1;
+        w->rh[2 * k] = rh0;
+        w->rh[2 * k + 1] = rh1;
         const double om = w->omega[k];
-        for (int j = 0; j < 2; ++j) {
-            const double x = w->xi[2 * k + j];
-            const double dx = om * x + (-om) * w->vrp[2 * k + j];
-            const double dk = (x + dx * w->dt) - w->xi[2 * (k + 1) + j];
-            w->d[2 * k + j] = dk;
-            const double e = fabs(dk);
-            if (e > pres || e != e) pres = e;
-        }
-        if (k >= 1) {
-            w->qx[2 * k] = w->Qw0 * (w->xi[2 * k] - w->xi_ref[2 * k]);
-            w->qx[2 * k + 1] = w->Qw1 * (w->xi[2 * k + 1] - w->xi_ref[2 * k + 1]);
+        {
+            const double x0 = w->xi[2 * k], x1 = w->xi[2 * k + 1];
+            const double y0 = w->xi[2 * (k + 1)], y1 = w->xi[2 * (k + 1) + 1];
+            const double dx0 = om * x0 + (-om) * r0;
+            const double dk0 = (x0 + dx0 * w->dt) - y0;
+            const double dx1 = om * x1 + (-om) * r1;
+            const double dk1 = (x1 + dx1 * w->dt) - y1;
+            w->d[2 * k] = dk0;
+            w->d[2 * k + 1] = dk1;
+            pres = nanmax(pres, fabs(dk0));
+            pres = nanmax(pres, fabs(dk1));
+            if (k + 1 < N) {
+                w->qx[2 * k] = w->Qw0 * (y0 - w->xi_ref[2 * (k + 1)]);
+                w->qx[2 * k + 1] = w->Qw1 * (y1 - w->xi_ref[2 * (k + 1) + 1]);
+            } else {
+                w->qx[2 * k] = w->Pw0 * (y0 - w->xi_ref[2 * (k + 1)]);
+                w->qx[2 * k + 1] = w->Pw1 * (y1 - w->xi_ref[2 * (k + 1) + 1]);
+            }
         }
     }
     return pres;
 }
 
-/* Backward Riccati sweep (sequential over knots).  factor != 0: builds Hi_k = H_k^{-1},
- * Pn_k = P_{k+1} (returns 0 if some H_k is not positive definite); factor == 0: reuses them.
- * Either way solves for the feed-forward kff with right-hand side g. */
-static int dcm_backward(dcm_ws* w, int factor)
+/* Factorization of the Newton system for the barrier Hessian blocks W_k.
+ * 1. E_k = beta_k^2 (R + W_k)^{-1}                                           (knot-parallel)
+ * 2. information-form Riccati, sequential k = N-1 .. 1 (one lane at a time on the device):
+ *      Z_k = Y_{k+1} + E_k,  K = Q Z_k + alpha_k^2 I,  Y_k = Z_k K^{-1}  (= P_k^{-1}),
+ *    Y_N = P_N^{-1}: a single division on the recursion's critical path;
+ * 3. P_k = Q + alpha_k^2 Z_k^{-1}, H_k = R + W_k + beta_k^2 P_{k+1}, h_k = H_k^{-1},
+ *    M_k = P_{k+1} h_k, G_k = alpha_k (I - beta_k^2 M_k)                     (knot-parallel)
+ * Returns 0 if some K or H_k is not positive definite (status NUMERICAL). */
+static int dcm_factor(dcm_ws* w)
 {
     const int N = w->N;
     int ok = 1;
-    double P00 = w->Pw0, P01 = 0.0, P11 = w->Pw1;
-    double pv0 = w->Pw0 * (w->xi[2 * N] - w->xi_ref[2 * N]);
-    double pv1 = w->Pw1 * (w->xi[2 * N + 1] - w->xi_ref[2 * N + 1]);
-    for (int k = N - 1; k >= 0; --k) {
-        double h00, h01, h11;
+    for (int k = 0; k < N; ++k) {
+        const double* Wk = w->W + 4 * k;
+        const double detRW = (w->Rw0 * w->Rw1 + (w->Rw1 * Wk[0] + w->Rw0 * Wk[2])) + Wk[3];
+        const double ie = w->b2[k] / detRW;
+        w->E[3 * k] = (w->Rw1 + Wk[2]) * ie;
+        w->E[3 * k + 1] = -(Wk[1] * ie);
+        w->E[3 * k + 2] = (w->Rw0 + Wk[0]) * ie;
+    }
+    double Y00 = 1.0 / w->Pw0, Y01 = 0.0, Y11 = 1.0 / w->Pw1;
+    for (int k = N - 1; k >= 1; --k) {
+        const double Z00 = Y00 + w->E[3 * k];
+        const double Z01 = Y01 + w->E[3 * k + 1];
+        const double Z11 = Y11 + w->E[3 * k + 2];
+        w->Z[3 * k] = Z00; w->Z[3 * k + 1] = Z01; w->Z[3 * k + 2] = Z11;
+        const double K00 = w->Qw0 * Z00 + w->a2[k];
+        const double K01 = w->Qw0 * Z01;
+        const double K10 = w->Qw1 * Z01;
+        const double K11 = w->Qw1 * Z11 + w->a2[k];
+        const double detK = K00 * K11 - K01 * K10;
+        if (!(detK > 0.0) || isinf(detK)) ok = 0;
+        const double ik = 1.0 / detK;
+        Y00 = (Z00 * K11 - Z01 * K10) * ik;
+        Y01 = (Z01 * K00 - Z00 * K01) * ik;
+        Y11 = (Z11 * K00 - Z01 * K01) * ik;
+    }
+    for (int k = 1; k < N; ++k) {
+        const double* Z = w->Z + 3 * k;
+        const double detZ = Z[0] * Z[2] - Z[1] * Z[1];
+        const double iz = w->a2[k] / detZ;
+        w->Pn[3 * (k - 1)] = w->Qw0 + Z[2] * iz;       /* P_k, needed by knot k - 1 */
+        w->Pn[3 * (k - 1) + 1] = -(Z[1] * iz);
+        w->Pn[3 * (k - 1) + 2] = w->Qw1 + Z[0] * iz;
+    }
+    w->Pn[3 * (N - 1)] = w->Pw0;
+    w->Pn[3 * (N - 1) + 1] = 0.0;
+    w->Pn[3 * (N - 1) + 2] = w->Pw1;
+    for (int k = 0; k < N; ++k) {
+        const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
+        const double* Wk = w->W + 4 * k;
         const double b2 = w->b2[k];
-        if (factor) {
-            /* H = B + W, B = R + b2 P_{k+1} (SPD, well conditioned), W PSD:
-             * det H = det B + tr(adj(B) W) + det W, every term >= 0 — no cancellation when
-             * the barrier weights inside W are huge */
-            const double B00 = w->Rw0 + b2 * P00;
-            const double B01 = b2 * P01;
-            const double B11 = w->Rw1 + b2 * P11;
-            const double W00 = w->W[4 * k], W01 = w->W[4 * k + 1], W11 = w->W[4 * k + 2];
-            const double H00 = B00 + W00;
-            const double H01 = B01 + W01;
-            const double H11 = B11 + W11;
-            const double detB = B00 * B11 - B01 * B01;
-            const double trW = (B11 * W00 + B00 * W11) - 2.0 * (B01 * W01);
-            const double det = (detB + trW) + w->W[4 * k + 3];
-            if (!(det > 0.0) || isinf(det)) ok = 0;
-            const double idet = 1.0 / det;
-            h00 = H11 * idet;
-            h01 = -(H01 * idet);
-            h11 = H00 * idet;
-            w->Hi[3 * k] = h00; w->Hi[3 * k + 1] = h01; w->Hi[3 * k + 2] = h11;
-            w->Pn[3 * k] = P00; w->Pn[3 * k + 1] = P01; w->Pn[3 * k + 2] = P11;
-        } else {
-            h00 = w->Hi[3 * k]; h01 = w->Hi[3 * k + 1]; h11 = w->Hi[3 * k + 2];
-            P00 = w->Pn[3 * k]; P01 = w->Pn[3 * k + 1]; P11 = w->Pn[3 * k + 2];
-        }
-        const double be = w->be[k];
-        const double d0 = w->d[2 * k], d1 = w->d[2 * k + 1];
-        const double t0 = (P00 * d0 + P01 * d1) + pv0;
-        const double t1 = (P01 * d0 + P11 * d1) + pv1;
-        const double hu0 = w->g[2 * k] - be * t0;
-        const double hu1 = w->g[2 * k + 1] - be * t1;
-        const double k0 = -(h00 * hu0 + h01 * hu1);
-        const double k1 = -(h01 * hu0 + h11 * hu1);
-        w->kff[2 * k] = k0;
-        w->kff[2 * k + 1] = k1;
-        if (k > 0) {
-            const double al = w->al[k];
-            const double pk0 = P00 * k0 + P01 * k1;
-            const double pk1 = P01 * k0 + P11 * k1;
-            const double npv0 = w->qx[2 * k] + al * (t0 - be * pk0);
-            const double npv1 = w->qx[2 * k + 1] + al * (t1 - be * pk1);
-            if (factor) {
-                /* P_k = Q + a^2 (P - b^2 P H^-1 P)  (never multiplies by the huge W) */
-                const double a2 = w->a2[k];
-                const double M00 = P00 * h00 + P01 * h01;
-                const double M01 = P00 * h01 + P01 * h11;
-                const double M10 = P01 * h00 + P11 * h01;
-                const double M11 = P01 * h01 + P11 * h11;
-                const double S00 = M00 * P00 + M01 * P01;
-                const double S01 = M00 * P01 + M01 * P11;
-                const double S10 = M10 * P00 + M11 * P01;
-                const double S11 = M10 * P01 + M11 * P11;
-                const double n00 = w->Qw0 + a2 * (P00 - b2 * S00);
-                const double n11 = w->Qw1 + a2 * (P11 - b2 * S11);
-                const double n01 = a2 * (P01 - b2 * (0.5 * (S01 + S10)));
-                P00 = n00;
-                P01 = n01;
-                P11 = n11;
-            }
-            pv0 = npv0;
-            pv1 = npv1;
-        }
+        /* det H = det B + tr(adj(B) W) + det W, B = R + b2 P: no cancellation for huge W */
+        const double B00 = w->Rw0 + b2 * P00;
+        const double B01 = b2 * P01;
+        const double B11 = w->Rw1 + b2 * P11;
+        const double H00 = B00 + Wk[0];
+        const double H01 = B01 + Wk[1];
+        const double H11 = B11 + Wk[2];
+        const double detB = B00 * B11 - B01 * B01;
+        const double trW = (B11 * Wk[0] + B00 * Wk[2]) - 2.0 * (B01 * Wk[1]);
+        const double det = (detB + trW) + Wk[3];
+        if (!(det > 0.0) || isinf(det)) ok = 0;
+        const double idet = 1.0 / det;
+        const double h00 = H11 * idet, h01 = -(H01 * idet), h11 = H00 * idet;
+        w->h[3 * k] = h00; w->h[3 * k + 1] = h01; w->h[3 * k + 2] = h11;
+        const double M00 = P00 * h00 + P01 * h01;
+        const double M01 = P00 * h01 + P01 * h11;
+        const double M10 = P01 * h00 + P11 * h01;
+        const double M11 = P01 * h01 + P11 * h11;
+        double* Mk = w->Mm + 4 * k;
+        Mk[0] = M00; Mk[1] = M01; Mk[2] = M10; Mk[3] = M11;
+        const double al = w->al[k];
+        double* G = w->G + 4 * k;
+        G[0] = al * (1.0 - b2 * M00);
+        G[1] = -(al * (b2 * M01));
+        G[2] = -(al * (b2 * M10));
+        G[3] = al * (1.0 - b2 * M11);
     }
     return ok;
 }
 
-/* Forward sweep: dr_k = (alpha beta) Hi_k (P_{k+1} dxi_k) + kff_k,
- * dxi_{k+1} = (alpha dxi_k - beta dr_k) + d_k, dxi_0 = 0. */
-static void dcm_forward(dcm_ws* w)
+/* Solve the factored Newton system for the right-hand side g:
+ *   c_k = G_k (qx_k + P_{k+1} d_k) + alpha beta M_k g_k;  v: backward scan;
+ *   t = (qx + P d) + v_{k+1};  kff = -h (g - beta t);  f = d - beta kff;
+ *   dxi_{k+1} = G_k^T dxi_k + f_k: forward scan;  dr_k = alpha beta M_k^T dxi_k + kff_k. */
+static void dcm_solve(dcm_ws* w)
 {
-    double x0 = 0.0, x1 = 0.0;
-    w->dxi[0] = 0.0;
-    w->dxi[1] = 0.0;
-    for (int k = 0; k < w->N; ++k) {
-        const double q00 = w->Pn[3 * k], q01 = w->Pn[3 * k + 1], q11 = w->Pn[3 * k + 2];
-        const double u0 = q00 * x0 + q01 * x1;
-        const double u1 = q01 * x0 + q11 * x1;
-        const double v0 = w->Hi[3 * k] * u0 + w->Hi[3 * k + 1] * u1;
-        const double v1 = w->Hi[3 * k + 1] * u0 + w->Hi[3 * k + 2] * u1;
-        const double al = w->al[k], be = w->be[k];
-        const double ab = al * be;
-        const double r0 = ab * v0 + w->kff[2 * k];
-        const double r1 = ab * v1 + w->kff[2 * k + 1];
-        w->dr[2 * k] = r0;
-        w->dr[2 * k + 1] = r1;
-        const double n0 = (al * x0 - be * r0) + w->d[2 * k];
-        const double n1 = (al * x1 - be * r1) + w->d[2 * k + 1];
-        w->dxi[2 * (k + 1)] = n0;
-        w->dxi[2 * (k + 1) + 1] = n1;
-        x0 = n0;
-        x1 = n1;
+    const int N = w->N;
+    for (int k = 0; k < N; ++k) {
+        const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
+        const double d0 = w->d[2 * k], d1 = w->d[2 * k + 1];
+        const double y0 = w->qx[2 * k] + (P00 * d0 + P01 * d1);
+        const double y1 = w->qx[2 * k + 1] + (P01 * d0 + P11 * d1);
+        const double* Mk = w->Mm + 4 * k;
+        const double M00 = Mk[0], M01 = Mk[1], M10 = Mk[2], M11 = Mk[3];
+        const double g0 = w->g[2 * k], g1 = w->g[2 * k + 1];
+        const double Mg0 = M00 * g0 + M01 * g1;
+        const double Mg1 = M10 * g0 + M11 * g1;
+        const double* G = w->G + 4 * k;
+        w->sc[2 * k] = (G[0] * y0 + G[1] * y1) + w->ab[k] * Mg0;
+        w->sc[2 * k + 1] = (G[2] * y0 + G[3] * y1) + w->ab[k] * Mg1;
     }
+    scan_backward(w, w->G, w->sc);
+    for (int k = 0; k < N; ++k) {
+        const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
+        const double d0 = w->d[2 * k], d1 = w->d[2 * k + 1];
+        const double y0 = w->qx[2 * k] + (P00 * d0 + P01 * d1);
+        const double y1 = w->qx[2 * k + 1] + (P01 * d0 + P11 * d1);
+        const double t0 = y0 + w->v[2 * (k + 1)];
+        const double t1 = y1 + w->v[2 * (k + 1) + 1];
+        const double be = w->be[k];
+        const double hu0 = w->g[2 * k] - be * t0;
+        const double hu1 = w->g[2 * k + 1] - be * t1;
+        const double h00 = w->h[3 * k], h01 = w->h[3 * k + 1], h11 = w->h[3 * k + 2];
+        const double k0 = -(h00 * hu0 + h01 * hu1);
+        const double k1 = -(h01 * hu0 + h11 * hu1);
+        w->dr[2 * k] = k0;                        /* kff until the forward scan is done */
+        w->dr[2 * k + 1] = k1;
+        w->sc[2 * k] = d0 - be * k0;
+        w->sc[2 * k + 1] = d1 - be * k1;
+    }
+    scan_forward(w, w->G, 1, w->sc);
+    for (int k = 0; k < N; ++k) {
+        const double* Mk = w->Mm + 4 * k;
+        const double M00 = Mk[0], M01 = Mk[1], M10 = Mk[2], M11 = Mk[3];
+        const double x0 = w->x[2 * k], x1 = w->x[2 * k + 1];
+        const double ab = w->ab[k];
+        w->dr[2 * k] = ab * (M00 * x0 + M10 * x1) + w->dr[2 * k];
+        w->dr[2 * k + 1] = ab * (M01 * x0 + M11 * x1) + w->dr[2 * k + 1];
+    }
+}
+
+/* W-phase (knot-parallel): 1/s, W = A^T diag(lam/s) A, det W = sum_{i<j} sg_i sg_j (a_i x a_j)^2
+ * (a sum of non-negative terms), and the predictor right-hand side g = rh + A^T e,
+ * e_i = (lam_i rp_i - s_i lam_i) / s_i. */
+static void dcm_wphase(dcm_ws* w)
+{
+    const int N = w->N, M = w->M;
+    for (int k = 0; k < N; ++k) {
+        const int m = w->nf[k];
+        const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
+        double W00 = 0.0, W01 = 0.0, W11 = 0.0, dW = 0.0;
+        double g0 = w->rh[2 * k], g1 = w->rh[2 * k + 1];
+        double sgv[MF];
+        for (int i = 0; i < m; ++i) {
+            const double* a = w->A + (k * M + i) * 2;
+            const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
+            const double is = 1.0 / si;
+            w->is[k * MF + i] = is;
+            const double sg = li * is;
+            sgv[i] = sg;
+            const double t0 = sg * a[0];
+            const double t1 = sg * a[1];
+            W00 = W00 + t0 * a[0];
+            W01 = W01 + t0 * a[1];
+            W11 = W11 + t1 * a[1];
+            const double rpi = ((a[0] * r0 + a[1] * r1) + si) - w->b[k * M + i];
+            const double e = (li * rpi - si * li) * is;
+            g0 = g0 + a[0] * e;
+            g1 = g1 + a[1] * e;
+        }
+        for (int i = 1; i < m; ++i) {
+            const double* ai = w->A + (k * M + i) * 2;
+            for (int j = 0; j < i; ++j) {
+                const double* aj = w->A + (k * M + j) * 2;
+                const double cr = ai[0] * aj[1] - ai[1] * aj[0];
+                dW = dW + (sgv[i] * sgv[j]) * (cr * cr);
+            }
+        }
+        double* Wk = w->W + 4 * k;
+        Wk[0] = W00; Wk[1] = W01; Wk[2] = W11; Wk[3] = dW;
+        w->g[2 * k] = g0;
+        w->g[2 * k + 1] = g1;
+    }
+}
+
+/* The affine (predictor) slack / multiplier step of facet i of knot k for the VRP step dra:
+ * ds = -rp - a . dra,  dl = -(lam (s + ds)) / s  (= (-s lam - lam ds) / s). */
+static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
+{
+    const double* a = w->A + (k * w->M + i) * 2;
+    const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
+    const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
+    const double rpi = ((a[0] * r0 + a[1] * r1) + si) - w->b[k * w->M + i];
+    const double dsv = (-rpi) - (a[0] * w->dra[2 * k] + a[1] * w->dra[2 * k + 1]);
+    *ds = dsv;
+    *dl = -((li * (si + dsv)) * w->is[k * MF + i]);
 }
 
 int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const double* omega,
@@ -477,109 +707,112 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
     const int M = prm->max_facets;
     dcm_ws ws;
     dcm_ws* w = &ws;
-    w->N = N; w->M = M; w->dt = prm->dt;
+    w->N = N; w->M = M; w->NW = (N + WV - 1) / WV; w->dt = prm->dt;
+    w->scans = prm->sequential ? 0 : 1;
     w->Qw0 = prm->w_xi[0]; w->Qw1 = prm->w_xi[1];
     w->Rw0 = prm->w_vrp[0]; w->Rw1 = prm->w_vrp[1];
     w->Pw0 = prm->w_terminal[0]; w->Pw1 = prm->w_terminal[1];
     w->omega = omega; w->xi_ref = xi_ref; w->vrp_ref = vrp_ref; w->A = Ain; w->b = bin;
     w->nf = nfacets; w->xi = xi; w->vrp = vrp;
-    double* mem = (double*)malloc(sizeof(double) * ((size_t)N * (4 + 4 * MF + 4 + 6 + 12 + 1) +
-                                                    4 * (size_t)(N + 1)));
-    double* q = mem;
-    w->al = q; q += N; w->be = q; q += N; w->a2 = q; q += N; w->b2 = q; q += N;
-    w->s = q; q += N * MF; w->lam = q; q += N * MF; w->rp = q; q += N * MF; w->prod = q; q += N * MF;
-    w->W = q; q += 4 * N;
-    w->Hi = q; q += 3 * N; w->Pn = q; q += 3 * N;
-    w->g = q; q += 2 * N; w->d = q; q += 2 * N; w->rho = q; q += 2 * N; w->kff = q; q += 2 * N;
-    w->dr = q; q += 2 * N; w->qx = q; q += 2 * N;
-    w->c = q; q += N;
-    w->dxi = q; q += 2 * (N + 1); w->nu = q; q += 2 * (N + 1);
+    const size_t per_knot = 5 + 5 * MF + 4 + 4 * 3 + 8 + 6 * 2 + 2 + 2 + 4;
+    double* mem = (double*)calloc((size_t)N * per_knot + 4 * (size_t)(N + 1), sizeof(double));
+    double* p = mem;
+    w->al = p; p += N; w->be = p; p += N; w->a2 = p; p += N; w->b2 = p; p += N; w->ab = p; p += N;
+    w->s = p; p += N * MF; w->lam = p; p += N * MF; w->is = p; p += N * MF;
+    w->cds = p; p += N * MF; w->cdl = p; p += N * MF;
+    w->W = p; p += 4 * N;
+    w->E = p; p += 3 * N; w->Z = p; p += 3 * N; w->Pn = p; p += 3 * N; w->h = p; p += 3 * N;
+    w->G = p; p += 4 * N; w->Mm = p; p += 4 * N;
+    w->rh = p; p += 2 * N; w->g = p; p += 2 * N; w->d = p; p += 2 * N; w->qx = p; p += 2 * N;
+    w->dr = p; p += 2 * N; w->dra = p; p += 2 * N;
+    w->c = p; p += N; w->q = p; p += N;
+    w->sc = p; p += 2 * N; w->sg = p; p += 4 * N;
+    w->v = p; p += 2 * (N + 1); w->x = p; p += 2 * (N + 1);
 
-    int status = 0, it = 0;
-    int ntot = 0;
+    int status = 0, it = 0, ntot = 0;
     for (int k = 0; k < N; ++k) {
         if (nfacets[k] < 0 || nfacets[k] > M) status = 3;
         else ntot += nfacets[k];
     }
     w->ntot = ntot;
-
-    /* ---- initial point ----
-     * 1. vrp = vrp_ref, xi = reference Euler rollout from xi_init;
-     * 2. one full Newton step of the QP WITHOUT the polygon constraints (the unconstrained LQ
-     *    optimum; W = 0, lam = 0): for the unstable DCM the open-loop rollout is far from
-     *    dual feasible (costates grow like alpha^N), this step makes the linear residuals O(1);
-     * 3. s = max(b - A r, 1e-2), lam = 1. */
     for (int k = 0; k < N; ++k) {
         w->be[k] = w->dt * omega[k];
         w->al[k] = 1.0 + w->be[k];
         w->a2[k] = w->al[k] * w->al[k];
         w->b2[k] = w->be[k] * w->be[k];
+        w->ab[k] = w->al[k] * w->be[k];
         vrp[2 * k] = vrp_ref[2 * k];
         vrp[2 * k + 1] = vrp_ref[2 * k + 1];
+        for (int i = 0; i < MF; ++i) { w->s[k * MF + i] = 1.0; w->lam[k * MF + i] = 0.0; }
     }
-    orc_dcm_euler_rollout(xi_init, omega, vrp, N, w->dt, xi);
+    /* ---- initial point 1: xi rolled out from vrp_ref by the affine forward scan
+     *      xi_{k+1} = alpha_k xi_k - beta_k r_k (xi_0 folded into knot 0's element) ---- */
+    for (int k = 0; k < N; ++k) {
+        double* G = w->sg + 4 * k;
+        G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
+        if (k == 0) {
+            w->sc[0] = w->al[0] * xi_init[0] - w->be[0] * vrp[0];
+            w->sc[1] = w->al[0] * xi_init[1] - w->be[0] * vrp[1];
+        } else {
+            w->sc[2 * k] = -(w->be[k] * vrp[2 * k]);
+            w->sc[2 * k + 1] = -(w->be[k] * vrp[2 * k + 1]);
+        }
+    }
+    scan_forward(w, w->sg, 0, w->sc);
+    xi[0] = xi_init[0];
+    xi[1] = xi_init[1];
+    for (int k = 1; k <= N; ++k) { xi[2 * k] = w->x[2 * k]; xi[2 * k + 1] = w->x[2 * k + 1]; }
     if (status == 3) {
         if (iters_out) *iters_out = 0;
         free(mem);
         return 3;
     }
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < MF; ++i) { w->s[k * MF + i] = 1.0; w->lam[k * MF + i] = 0.0; }
-    {
-        const int nf_saved = w->ntot;
-        int32_t* zero = (int32_t*)calloc(N, sizeof(int32_t));
-        w->nf = zero;                      /* no facets: rho = R (r - r_ref), W = 0 */
-        dcm_residuals(w);
-        w->nf = nfacets;
-        w->ntot = nf_saved;
-        free(zero);
-        for (int k = 0; k < N; ++k) {
-            w->W[4 * k] = 0.0; w->W[4 * k + 1] = 0.0; w->W[4 * k + 2] = 0.0; w->W[4 * k + 3] = 0.0;
-            w->g[2 * k] = w->rho[2 * k];
-            w->g[2 * k + 1] = w->rho[2 * k + 1];
-        }
-        if (!dcm_backward(w, 1)) status = 2;
-        dcm_forward(w);
-        for (int k = 0; k < N; ++k) {
-            vrp[2 * k] = vrp[2 * k] + w->dr[2 * k];
-            vrp[2 * k + 1] = vrp[2 * k + 1] + w->dr[2 * k + 1];
-            xi[2 * (k + 1)] = xi[2 * (k + 1)] + w->dxi[2 * (k + 1)];
-            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + w->dxi[2 * (k + 1) + 1];
-        }
+    /* ---- initial point 2: one full Newton step of the QP without the polygon constraints
+     *      (W = 0, lam = 0): the unconstrained LQ optimum.  For the unstable DCM the rollout is far
+     *      from dual feasible (costates grow like alpha^N); this step makes the linear residuals
+     *      vanish up to rounding. ---- */
+    dcm_residuals(w, 0);
+    for (int k = 0; k < N; ++k) {
+        w->W[4 * k] = 0.0; w->W[4 * k + 1] = 0.0; w->W[4 * k + 2] = 0.0; w->W[4 * k + 3] = 0.0;
+        w->g[2 * k] = w->rh[2 * k];
+        w->g[2 * k + 1] = w->rh[2 * k + 1];
     }
+    if (!dcm_factor(w)) status = 2;
+    dcm_solve(w);
+    for (int k = 0; k < N; ++k) {
+        vrp[2 * k] = vrp[2 * k] + w->dr[2 * k];
+        vrp[2 * k + 1] = vrp[2 * k + 1] + w->dr[2 * k + 1];
+        xi[2 * (k + 1)] = xi[2 * (k + 1)] + w->x[2 * (k + 1)];
+        xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
+    }
+    /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1 ---- */
     for (int k = 0; k < N; ++k) {
         const int m = nfacets[k];
-        for (int i = 0; i < MF; ++i) {
-            if (i < m) {
-                const double* a = Ain + (k * M + i) * 2;
-                const double gr = a[0] * vrp[2 * k] + a[1] * vrp[2 * k + 1];
-                double sl = bin[k * M + i] - gr;
-                w->s[k * MF + i] = sl > 1e-2 ? sl : 1e-2;
-                w->lam[k * MF + i] = 1.0;
-            }
+        for (int i = 0; i < m; ++i) {
+            const double* a = Ain + (k * M + i) * 2;
+            const double gr = a[0] * vrp[2 * k] + a[1] * vrp[2 * k + 1];
+            const double sl = bin[k * M + i] - gr;
+            w->s[k * MF + i] = sl > 1e-2 ? sl : 1e-2;
+            w->lam[k * MF + i] = 1.0;
         }
     }
-
-    /* initial dual residual (single-shooting costates): dres0 = max |rho_k - beta_k nu_{k+1}|;
-     * it then contracts by (1 - a) with every damped Newton step (the QP's linear residuals). */
+    /* ---- initial dual residual with single-shooting costates nu_k = qx_k + alpha_k nu_{k+1}
+     *      (backward scan of v_k = alpha_k nu_{k+1}); it then contracts by (1 - a) with every
+     *      Newton step (the QP's linear residuals) ---- */
     double dres = 0.0;
-    {
-        double* nu = w->nu;
-        nu[2 * N] = w->Pw0 * (xi[2 * N] - xi_ref[2 * N]);
-        nu[2 * N + 1] = w->Pw1 * (xi[2 * N + 1] - xi_ref[2 * N + 1]);
-        for (int k = N - 1; k >= 1; --k) {
-            nu[2 * k] = w->Qw0 * (xi[2 * k] - xi_ref[2 * k]) + w->al[k] * nu[2 * (k + 1)];
-            nu[2 * k + 1] = w->Qw1 * (xi[2 * k + 1] - xi_ref[2 * k + 1]) + w->al[k] * nu[2 * (k + 1) + 1];
-        }
-        for (int k = 0; k < N; ++k) {
-            const int m = nfacets[k];
-            for (int j = 0; j < 2; ++j) {
-                double rj = (j == 0 ? w->Rw0 : w->Rw1) * (vrp[2 * k + j] - vrp_ref[2 * k + j]);
-                for (int i = 0; i < m; ++i) rj = rj + Ain[(k * M + i) * 2 + j] * w->lam[k * MF + i];
-                const double e = fabs(rj - w->be[k] * nu[2 * (k + 1) + j]);
-                if (e > dres || e != e) dres = e;
-            }
-        }
+    dcm_residuals(w, 1);
+    for (int k = 0; k < N; ++k) {
+        double* G = w->sg + 4 * k;
+        G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
+        w->sc[2 * k] = w->al[k] * w->qx[2 * k];
+        w->sc[2 * k + 1] = w->al[k] * w->qx[2 * k + 1];
+    }
+    scan_backward(w, w->sg, w->sc);
+    for (int k = 0; k < N; ++k) {
+        const double nu0 = w->qx[2 * k] + w->v[2 * (k + 1)];
+        const double nu1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
+        dres = nanmax(dres, fabs(w->rh[2 * k] - w->be[k] * nu0));
+        dres = nanmax(dres, fabs(w->rh[2 * k + 1] - w->be[k] * nu1));
     }
     if (status == 2) {
         if (iters_out) *iters_out = 0;
@@ -588,75 +821,38 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
     }
 
     for (it = 0;; ++it) {
-        const double pres = dcm_residuals(w);
+        const double pres = dcm_residuals(w, 1);
         const double mu = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
         if (!(mu == mu) || !(pres == pres) || !(dres == dres) || isinf(mu)) { status = 2; break; }
         if (mu <= prm->tol_mu && pres <= prm->tol_primal && dres <= prm->tol_dual) { status = 0; break; }
         if (it >= prm->max_iter) { status = 1; break; }
 
-        /* ---- W = A^T diag(lam/s) A, det(W) as a sum of non-negative terms, affine rhs g
-         *      (stage-parallel) ---- */
-        for (int k = 0; k < N; ++k) {
-            const int m = nfacets[k];
-            double W00 = 0.0, W01 = 0.0, W11 = 0.0, dW = 0.0;
-            double g0 = w->rho[2 * k], g1 = w->rho[2 * k + 1];
-            double sgv[MF];
-            for (int i = 0; i < m; ++i) {
-                const double* a = Ain + (k * M + i) * 2;
-                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
-                const double sg = li / si;
-                sgv[i] = sg;
-                const double t0 = sg * a[0];
-                const double t1 = sg * a[1];
-                W00 = W00 + t0 * a[0];
-                W01 = W01 + t0 * a[1];
-                W11 = W11 + t1 * a[1];
-                const double rc = si * li;
-                const double e = (li * w->rp[k * MF + i] - rc) / si;
-                g0 = g0 + a[0] * e;
-                g1 = g1 + a[1] * e;
-            }
-            /* det(sum_i sg_i a_i a_i^T) = sum_{i<j} sg_i sg_j (a_i x a_j)^2 */
-            for (int i = 1; i < m; ++i) {
-                const double* ai = Ain + (k * M + i) * 2;
-                for (int j = 0; j < i; ++j) {
-                    const double* aj = Ain + (k * M + j) * 2;
-                    const double cr = ai[0] * aj[1] - ai[1] * aj[0];
-                    dW = dW + (sgv[i] * sgv[j]) * (cr * cr);
-                }
-            }
-            w->W[4 * k] = W00; w->W[4 * k + 1] = W01; w->W[4 * k + 2] = W11; w->W[4 * k + 3] = dW;
-            w->g[2 * k] = g0; w->g[2 * k + 1] = g1;
-        }
+        dcm_wphase(w);
+        if (!dcm_factor(w)) { status = 2; break; }
 
-        /* ---- affine (predictor) step ---- */
-        if (!dcm_backward(w, 1)) status = 2;
-        dcm_forward(w);
-        double smax = INFINITY;
+        /* ---- predictor ---- */
+        dcm_solve(w);
+        double qmax = 0.0;
         for (int k = 0; k < N; ++k) {
+            w->dra[2 * k] = w->dr[2 * k];
+            w->dra[2 * k + 1] = w->dr[2 * k + 1];
             const int m = nfacets[k];
             for (int i = 0; i < m; ++i) {
-                const double* a = Ain + (k * M + i) * 2;
-                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
-                const double rc = si * li;
-                const double ds = (-w->rp[k * MF + i]) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
-                const double dl = ((-rc) - li * ds) / si;
-                if (ds < 0.0) { const double qq = (-si) / ds; if (qq < smax) smax = qq; }
-                if (dl < 0.0) { const double qq = (-li) / dl; if (qq < smax) smax = qq; }
-                w->prod[k * MF + i] = ds * dl;
+                double ds, dl;
+                affine_step(w, k, i, &ds, &dl);
+                const double is = w->is[k * MF + i];
+                if (ds < 0.0) qmax = keepmax(qmax, (-ds) * is);
+                if (dl < 0.0) qmax = keepmax(qmax, (w->s[k * MF + i] + ds) * is);
             }
         }
-        const double a_aff = smax < 1.0 ? smax : 1.0;
+        const double a_aff = qmax > 1.0 ? 1.0 / qmax : 1.0;
         for (int k = 0; k < N; ++k) {
             const int m = nfacets[k];
             double ck = 0.0;
             for (int i = 0; i < m; ++i) {
-                const double* a = Ain + (k * M + i) * 2;
-                const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
-                const double rc = si * li;
-                const double ds = (-w->rp[k * MF + i]) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
-                const double dl = ((-rc) - li * ds) / si;
-                ck = ck + (si + a_aff * ds) * (li + a_aff * dl);
+                double ds, dl;
+                affine_step(w, k, i, &ds, &dl);
+                ck = ck + (w->s[k * MF + i] + a_aff * ds) * (w->lam[k * MF + i] + a_aff * dl);
             }
             w->c[k] = ck;
         }
@@ -668,49 +864,56 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         }
         const double sigma_mu = sigma * mu;
 
-        /* ---- corrector: rhs (stage-parallel), solve reusing the factorization ---- */
+        /* ---- corrector: rhs (knot-parallel), solve with the same factorization ---- */
         for (int k = 0; k < N; ++k) {
             const int m = nfacets[k];
-            double g0 = w->rho[2 * k], g1 = w->rho[2 * k + 1];
+            const double r0 = vrp[2 * k], r1 = vrp[2 * k + 1];
+            double g0 = w->rh[2 * k], g1 = w->rh[2 * k + 1];
             for (int i = 0; i < m; ++i) {
                 const double* a = Ain + (k * M + i) * 2;
                 const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
-                const double rc = (si * li + w->prod[k * MF + i]) - sigma_mu;
-                const double e = (li * w->rp[k * MF + i] - rc) / si;
+                double ds, dl;
+                affine_step(w, k, i, &ds, &dl);
+                const double rc = (si * li + ds * dl) - sigma_mu;
+                const double rpi = ((a[0] * r0 + a[1] * r1) + si) - bin[k * M + i];
+                const double e = (li * rpi - rc) * w->is[k * MF + i];
                 g0 = g0 + a[0] * e;
                 g1 = g1 + a[1] * e;
             }
-            w->g[2 * k] = g0; w->g[2 * k + 1] = g1;
+            w->g[2 * k] = g0;
+            w->g[2 * k + 1] = g1;
         }
-        dcm_backward(w, 0);
-        dcm_forward(w);
-        smax = INFINITY;
+        dcm_solve(w);
+        qmax = 0.0;
         for (int k = 0; k < N; ++k) {
             const int m = nfacets[k];
+            const double r0 = vrp[2 * k], r1 = vrp[2 * k + 1];
             for (int i = 0; i < m; ++i) {
                 const double* a = Ain + (k * M + i) * 2;
                 const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
-                const double rc = (si * li + w->prod[k * MF + i]) - sigma_mu;
-                const double ds = (-w->rp[k * MF + i]) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
-                const double dl = ((-rc) - li * ds) / si;
-                if (ds < 0.0) { const double qq = (-si) / ds; if (qq < smax) smax = qq; }
-                if (dl < 0.0) { const double qq = (-li) / dl; if (qq < smax) smax = qq; }
-                w->rp[k * MF + i] = ds;      /* keep the step for the update */
-                w->prod[k * MF + i] = dl;
+                double ads, adl;
+                affine_step(w, k, i, &ads, &adl);
+                const double rc = (si * li + ads * adl) - sigma_mu;
+                const double rpi = ((a[0] * r0 + a[1] * r1) + si) - bin[k * M + i];
+                const double ds = (-rpi) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
+                const double dl = ((-rc) - li * ds) * w->is[k * MF + i];
+                if (ds < 0.0) qmax = keepmax(qmax, (-ds) * w->is[k * MF + i]);
+                if (dl < 0.0) qmax = keepmax(qmax, (-dl) / li);
+                w->cds[k * MF + i] = ds;
+                w->cdl[k * MF + i] = dl;
             }
         }
-        if (status == 2) break;
-        const double step = 0.99 * smax;
+        const double step = qmax > 0.0 ? 0.99 / qmax : 1.0;
         const double a = step < 1.0 ? step : 1.0;
         for (int k = 0; k < N; ++k) {
             vrp[2 * k] = vrp[2 * k] + a * w->dr[2 * k];
             vrp[2 * k + 1] = vrp[2 * k + 1] + a * w->dr[2 * k + 1];
-            xi[2 * (k + 1)] = xi[2 * (k + 1)] + a * w->dxi[2 * (k + 1)];
-            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + a * w->dxi[2 * (k + 1) + 1];
+            xi[2 * (k + 1)] = xi[2 * (k + 1)] + a * w->x[2 * (k + 1)];
+            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + a * w->x[2 * (k + 1) + 1];
             const int m = nfacets[k];
             for (int i = 0; i < m; ++i) {
-                w->s[k * MF + i] = w->s[k * MF + i] + a * w->rp[k * MF + i];
-                w->lam[k * MF + i] = w->lam[k * MF + i] + a * w->prod[k * MF + i];
+                w->s[k * MF + i] = w->s[k * MF + i] + a * w->cds[k * MF + i];
+                w->lam[k * MF + i] = w->lam[k * MF + i] + a * w->cdl[k * MF + i];
             }
         }
         dres = dres * (1.0 - a);

@@ -59,8 +59,11 @@ void orc_quintic_fit(const double* knots_t, const double* knots_pva, int nknots,
 void orc_quintic_eval(const double* knots_t, const double* coeffs, int nknots, int dim,
                       const double* tq, int nq, double* pva, int32_t* knot_idx);
 
+/* sequential != 0: evaluate the affine recursions as plain sequential loops (the CPU-efficient
+ * form, used only for bench.py's cpu_baseline timing); 0: the device's Kogge-Stone scan order,
+ * bit-identical to the kernel (every parity test). */
 typedef struct orc_dcm_params {
-    int32_t horizon, max_facets, max_iter, reserved;
+    int32_t horizon, max_facets, max_iter, sequential;
     double dt, w_xi[2], w_vrp[2], w_terminal[2], tol_mu, tol_primal, tol_dual;
 } orc_dcm_params;
 

@@ -18,7 +18,7 @@ _ip = ctypes.POINTER(ctypes.c_int32)
 
 class OrcParams(ctypes.Structure):
     _fields_ = [("horizon", ctypes.c_int32), ("max_facets", ctypes.c_int32),
-                ("max_iter", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("max_iter", ctypes.c_int32), ("sequential", ctypes.c_int32),
                 ("dt", ctypes.c_double), ("w_xi", ctypes.c_double * 2),
                 ("w_vrp", ctypes.c_double * 2), ("w_terminal", ctypes.c_double * 2),
                 ("tol_mu", ctypes.c_double), ("tol_primal", ctypes.c_double),
@@ -158,7 +158,7 @@ def default_params(horizon, **kw):
     p.horizon = horizon
     p.max_facets = kw.get("max_facets", 8)
     p.max_iter = kw.get("max_iter", 50)
-    p.reserved = 0
+    p.sequential = int(kw.get("sequential", 0))
     p.dt = kw.get("dt", 0.02)
     for name, val in (("w_xi", 1e2), ("w_vrp", 1.0), ("w_terminal", 1e3)):
         v = kw.get(name, val)
