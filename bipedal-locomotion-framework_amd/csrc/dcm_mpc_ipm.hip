@@ -5,16 +5,15 @@
 // lives in that thread's registers for the whole solve; LDS holds only the facet rows (read in
 // every phase) and a few boundary values exchanged between wavefronts.
 //
-// The Newton system is block tridiagonal in time.  Its factorization needs ONE nonlinear
-// recursion over the knots, the information-form Riccati recursion
-//     Y_k = Z_k (Q Z_k + alpha_k^2 I)^{-1},   Z_k = Y_{k+1} + E_k,   Y = P^{-1},
-// which runs lane after lane: the lane owning knot k evaluates its step with the other lanes
-// masked off, and the 3-double state moves to the next lane through v_readlane (SGPRs) — no
-// memory traffic and a single division on the critical path.  Every other sequential piece is
-// an affine recursion (costates, the forward rollout of the Newton step) and runs as a
-// Kogge-Stone scan over the 64 lanes of each wavefront (6 levels of __shfl + a 2x2 compose),
-// then one boundary value per wavefront through LDS.  All remaining work (residuals, barrier
-// Hessians, right-hand sides, step lengths, updates) is knot-parallel.
+// The Newton system is block tridiagonal in time and is solved without any sequential loop over
+// the knots: every recursion runs as a Kogge-Stone scan over the 64 lanes of a wavefront
+// (6 levels of ds_bpermute + a compose), then one boundary value per wavefront through LDS.
+//  * the Riccati recursion P_k = Q + alpha_k^2 P_{k+1} (I + E_k P_{k+1})^{-1} composes its
+//    maps f(P) = H + A^T P (I + G P)^{-1} A in the structure-preserving doubling form (only
+//    I + G H, eigenvalues >= 1, is ever inverted);
+//  * the costate recursion and the forward rollout of the Newton step are affine maps.
+// All remaining work (residuals, barrier Hessians, right-hand sides, step lengths, updates) is
+// knot-parallel.
 //
 // Every expression mirrors oracle/blf_oracle.c:orc_dcm_mpc_solve term for term (the scans in the
 // same combine order, the reductions in the same xor-butterfly order) and the file is built with
@@ -48,7 +47,6 @@ struct KParams {
 //   IS  [M][N]          1 / s of every facet, refreshed once per iteration (W-phase)
 //   bnd [NW][16]        per-wavefront boundary values (see the kB* slots)
 //   red [4][NW][2]      reduction scratch, four rotating slots (no second barrier needed)
-constexpr int kBY = 0;    // Y_{64w} (3): Riccati state handed from wavefront w to w-1
 constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
 constexpr int kBV = 8;    // v_{64w} (2): backward-scan value at the first knot of wavefront w
 constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last knot of wavefront w
@@ -75,14 +73,6 @@ struct Lds {
         total = o;
     }
 };
-
-__device__ __forceinline__ double rdlane(double x, int l)
-{
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_readlane((int)b, l);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 
 // Block reductions: xor-butterfly per wavefront, then the wavefronts' values in order (the
 // oracle's orc_wave_tree_sum).  `slot` rotates over 4 scratch rows so that a row is never
@@ -152,6 +142,26 @@ struct Reduce {
     }
 };
 
+// The facet rows never change during a solve, so the compiler would hoist every phase's row loads
+// out of the IPM loop and keep 8 facets x 4 doubles live in VGPRs across it (spilling).  Each phase
+// indexes the rows through an opaque copy of the knot index instead, so they are re-read from LDS.
+__device__ __forceinline__ int opaque(int k)
+{
+    asm volatile("" : "+v"(k));
+    return k;
+}
+
+// Lane shuffles for the scans.  The source-lane address is recomputed from an opaque lane id
+// at every call: hoisted out of the IPM loop, the twelve shift addresses would stay live in
+// VGPRs for the whole kernel.  Out-of-range sources wrap; the scans never use those values.
+__device__ __forceinline__ double bperm(int addr, double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // 2x2 compose (row-major): n = a * b;  nc = a * c + e.
 #define COMPOSE(a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, e0, e1)                 \
     do {                                                                         \
@@ -171,12 +181,14 @@ __device__ __forceinline__ void scan_backward(double g0, double g1, double g2, d
                                               double c1, double* bnd, int nwa, int wv, int lane,
                                               double& vn0, double& vn1)
 {
+    const int ln = opaque(lane);
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
-        const double p0 = __shfl_down(g0, d, kWave), p1 = __shfl_down(g1, d, kWave);
-        const double p2 = __shfl_down(g2, d, kWave), p3 = __shfl_down(g3, d, kWave);
-        const double q0 = __shfl_down(c0, d, kWave), q1 = __shfl_down(c1, d, kWave);
-        if (lane + d < kWave) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
+        const int ad = ((ln + d) & (kWave - 1)) << 2;
+        const double p0 = bperm(ad, g0), p1 = bperm(ad, g1);
+        const double p2 = bperm(ad, g2), p3 = bperm(ad, g3);
+        const double q0 = bperm(ad, c0), q1 = bperm(ad, c1);
+        if (ln + d < kWave) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
     }
     double v0 = c0, v1 = c1;
     if constexpr (NW > 1) {
@@ -192,8 +204,9 @@ __device__ __forceinline__ void scan_backward(double g0, double g1, double g2, d
             if (w > 0) __syncthreads();
         }
     }
-    vn0 = __shfl_down(v0, 1, kWave);
-    vn1 = __shfl_down(v1, 1, kWave);
+    const int a1 = ((ln + 1) & (kWave - 1)) << 2;
+    vn0 = bperm(a1, v0);
+    vn1 = bperm(a1, v1);
     if (lane == kWave - 1) {
         vn0 = 0.0;
         vn1 = 0.0;
@@ -211,12 +224,14 @@ __device__ __forceinline__ void scan_forward(double g0, double g1, double g2, do
                                              double c1, double* bnd, int nwa, int wv, int lane, double& x0,
                                              double& x1, double& xk0, double& xk1)
 {
+    const int ln = opaque(lane);
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
-        const double p0 = __shfl_up(g0, d, kWave), p1 = __shfl_up(g1, d, kWave);
-        const double p2 = __shfl_up(g2, d, kWave), p3 = __shfl_up(g3, d, kWave);
-        const double q0 = __shfl_up(c0, d, kWave), q1 = __shfl_up(c1, d, kWave);
-        if (lane >= d) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
+        const int ad = ((ln - d) & (kWave - 1)) << 2;
+        const double p0 = bperm(ad, g0), p1 = bperm(ad, g1);
+        const double p2 = bperm(ad, g2), p3 = bperm(ad, g3);
+        const double q0 = bperm(ad, c0), q1 = bperm(ad, c1);
+        if (ln >= d) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
     }
     x0 = c0;
     x1 = c1;
@@ -233,8 +248,9 @@ __device__ __forceinline__ void scan_forward(double g0, double g1, double g2, do
             if (w < nwa - 1) __syncthreads();
         }
     }
-    xk0 = __shfl_up(x0, 1, kWave);
-    xk1 = __shfl_up(x1, 1, kWave);
+    const int a1 = ((ln - 1) & (kWave - 1)) << 2;
+    xk0 = bperm(a1, x0);
+    xk1 = bperm(a1, x1);
     if (lane == 0) {
         xk0 = 0.0;
         xk1 = 0.0;
@@ -268,15 +284,6 @@ struct Mmat {
         m11 = K.P01 * K.h01 + K.P11 * K.h11;
     }
 };
-
-// The facet rows never change during a solve, so the compiler would hoist every phase's row loads
-// out of the IPM loop and keep 8 facets x 4 doubles live in VGPRs across it (spilling).  Each phase
-// indexes the rows through an opaque copy of the knot index instead, so they are re-read from LDS.
-__device__ __forceinline__ int opaque(int k)
-{
-    asm volatile("" : "+v"(k));
-    return k;
-}
 
 // Facet residual rp_i = (a . r + s_i) - b_i.
 __device__ __forceinline__ double facet_rp(const Knot& K, double2 a, double bi, int i)
@@ -352,6 +359,79 @@ __device__ __forceinline__ void xi_prev(const Knot& K, const double* bnd, int wv
     }
 }
 
+// Riccati map element f(P) = H + A^T P (I + G P)^{-1} A (oracle rc_el); knot k: A = alpha_k I,
+// G = E_k, H = Q.  rc_combine(e, q): e <- e o q (q the later knots), the structure-preserving
+// doubling composition — it inverts only I + G H (eigenvalues >= 1).
+struct Rc {
+    double a0, a1, a2, a3, g0, g1, g2, h0, h1, h2;
+};
+
+__device__ __forceinline__ bool rc_combine(Rc& e, const Rc& q)
+{
+    const double T00 = 1.0 + (e.g0 * q.h0 + e.g1 * q.h1);
+    const double T01 = e.g0 * q.h1 + e.g1 * q.h2;
+    const double T10 = e.g1 * q.h0 + e.g2 * q.h1;
+    const double T11 = 1.0 + (e.g1 * q.h1 + e.g2 * q.h2);
+    const double detT = T00 * T11 - T01 * T10;
+    const bool ok = (detT > 0.0) && !__builtin_isinf(detT);
+    const double it = 1.0 / detT;
+    const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
+    const double U00 = Ti00 * e.a0 + Ti01 * e.a2;
+    const double U01 = Ti00 * e.a1 + Ti01 * e.a3;
+    const double U10 = Ti10 * e.a0 + Ti11 * e.a2;
+    const double U11 = Ti10 * e.a1 + Ti11 * e.a3;
+    const double V00 = q.a0 * Ti00 + q.a1 * Ti10;
+    const double V01 = q.a0 * Ti01 + q.a1 * Ti11;
+    const double V10 = q.a2 * Ti00 + q.a3 * Ti10;
+    const double V11 = q.a2 * Ti01 + q.a3 * Ti11;
+    const double X00 = V00 * e.g0 + V01 * e.g1;
+    const double X01 = V00 * e.g1 + V01 * e.g2;
+    const double X10 = V10 * e.g0 + V11 * e.g1;
+    const double X11 = V10 * e.g1 + V11 * e.g2;
+    const double Y00 = q.h0 * e.a0 + q.h1 * e.a2;
+    const double Y01 = q.h0 * e.a1 + q.h1 * e.a3;
+    const double Y10 = q.h1 * e.a0 + q.h2 * e.a2;
+    const double Y11 = q.h1 * e.a1 + q.h2 * e.a3;
+    Rc r;
+    r.a0 = q.a0 * U00 + q.a1 * U10;
+    r.a1 = q.a0 * U01 + q.a1 * U11;
+    r.a2 = q.a2 * U00 + q.a3 * U10;
+    r.a3 = q.a2 * U01 + q.a3 * U11;
+    r.g0 = (X00 * q.a0 + X01 * q.a1) + q.g0;
+    r.g1 = (X00 * q.a2 + X01 * q.a3) + q.g1;
+    r.g2 = (X10 * q.a2 + X11 * q.a3) + q.g2;
+    r.h0 = (U00 * Y00 + U10 * Y10) + e.h0;
+    r.h1 = (U00 * Y01 + U10 * Y11) + e.h1;
+    r.h2 = (U01 * Y01 + U11 * Y11) + e.h2;
+    e = r;
+    return ok;
+}
+
+__device__ __forceinline__ bool rc_apply(const Rc& e, double P00, double P01, double P11,
+                                         double& o00, double& o01, double& o11)
+{
+    const double S00 = 1.0 + (e.g0 * P00 + e.g1 * P01);
+    const double S01 = e.g0 * P01 + e.g1 * P11;
+    const double S10 = e.g1 * P00 + e.g2 * P01;
+    const double S11 = 1.0 + (e.g1 * P01 + e.g2 * P11);
+    const double detS = S00 * S11 - S01 * S10;
+    const bool ok = (detS > 0.0) && !__builtin_isinf(detS);
+    const double is = 1.0 / detS;
+    const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
+    const double W00 = P00 * Si00 + P01 * Si10;
+    const double W01 = P00 * Si01 + P01 * Si11;
+    const double W10 = P01 * Si00 + P11 * Si10;
+    const double W11 = P01 * Si01 + P11 * Si11;
+    const double Z00 = W00 * e.a0 + W01 * e.a2;
+    const double Z01 = W00 * e.a1 + W01 * e.a3;
+    const double Z10 = W10 * e.a0 + W11 * e.a2;
+    const double Z11 = W10 * e.a1 + W11 * e.a3;
+    o00 = (e.a0 * Z00 + e.a2 * Z10) + e.h0;
+    o01 = (e.a0 * Z01 + e.a2 * Z11) + e.h1;
+    o11 = (e.a1 * Z01 + e.a3 * Z11) + e.h2;
+    return ok;
+}
+
 // Factorization (oracle dcm_factor) from W = (W00, W01, W11, detW).  Leaves P_{k+1}, h, M in K.
 // Returns false on this lane if its K or H block is not positive definite.
 template <int NW>
@@ -361,7 +441,6 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
 {
     bool ok = true;
     const double b2 = K.be * K.be;
-    const double a2 = K.al * K.al;
     double E00 = 0.0, E01 = 0.0, E11 = 0.0;
     if (own) {
         const double detRW = (P.Rw0 * P.Rw1 + (P.Rw1 * W00 + P.Rw0 * W11)) + dW;
@@ -370,68 +449,51 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
         E01 = -(W01 * ie);
         E11 = (P.Rw0 + W00) * ie;
     }
-    // sequential information-form Riccati over knots N-1 .. 1, one lane at a time
-    double Y00 = 1.0 / P.Pw0, Y01 = 0.0, Y11 = 1.0 / P.Pw1;
-    double Z00 = 0.0, Z01 = 0.0, Z11 = 0.0;
+    // P_k for every knot: Kogge-Stone scan of Riccati map elements over the wavefront's lanes
+    // (oracle dcm_factor / rc_combine), then P_k = f_{k..}(P at the next wavefront's first knot)
+    Rc e;
+    if (own) {
+        e.a0 = K.al; e.a1 = 0.0; e.a2 = 0.0; e.a3 = K.al;
+        e.g0 = E00; e.g1 = E01; e.g2 = E11;
+        e.h0 = P.Qw0; e.h1 = 0.0; e.h2 = P.Qw1;
+    } else {
+        e.a0 = 1.0; e.a1 = 0.0; e.a2 = 0.0; e.a3 = 1.0;
+        e.g0 = e.g1 = e.g2 = 0.0;
+        e.h0 = e.h1 = e.h2 = 0.0;
+    }
+    const int ln = opaque(lane);
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const int ad = ((ln + d) & (kWave - 1)) << 2;
+        Rc q;
+        q.a0 = bperm(ad, e.a0); q.a1 = bperm(ad, e.a1); q.a2 = bperm(ad, e.a2); q.a3 = bperm(ad, e.a3);
+        q.g0 = bperm(ad, e.g0); q.g1 = bperm(ad, e.g1); q.g2 = bperm(ad, e.g2);
+        q.h0 = bperm(ad, e.h0); q.h1 = bperm(ad, e.h1); q.h2 = bperm(ad, e.h2);
+        if (ln + d < kWave) ok = rc_combine(e, q) && ok;
+    }
+    double Pk00 = 0.0, Pk01 = 0.0, Pk11 = 0.0;
     for (int w = nwa - 1; w >= 0; --w) {
         if (wv == w) {
+            double b0 = P.Pw0, b1 = 0.0, b2v = P.Pw1;
             if (w < nwa - 1) {
-                Y00 = bnd[kBnd * (w + 1) + kBY];
-                Y01 = bnd[kBnd * (w + 1) + kBY + 1];
-                Y11 = bnd[kBnd * (w + 1) + kBY + 2];
+                b0 = bnd[kBnd * (w + 1) + kBP];
+                b1 = bnd[kBnd * (w + 1) + kBP + 1];
+                b2v = bnd[kBnd * (w + 1) + kBP + 2];
             }
-            const int hi = (N < kWave * w + kWave ? N : kWave * w + kWave) - 1;
-            const int lo = kWave * w > 1 ? kWave * w : 1;
-            for (int kk = hi; kk >= lo; --kk) {
-                const int ls = kk - kWave * w;
-                double n00 = 0.0, n01 = 0.0, n11 = 0.0;
-                if (lane == ls) {
-                    Z00 = Y00 + E00;
-                    Z01 = Y01 + E01;
-                    Z11 = Y11 + E11;
-                    const double K00 = P.Qw0 * Z00 + a2;
-                    const double K01 = P.Qw0 * Z01;
-                    const double K10 = P.Qw1 * Z01;
-                    const double K11 = P.Qw1 * Z11 + a2;
-                    const double detK = K00 * K11 - K01 * K10;
-                    if (!(detK > 0.0) || __builtin_isinf(detK)) ok = false;
-                    const double ik = 1.0 / detK;
-                    n00 = (Z00 * K11 - Z01 * K10) * ik;
-                    n01 = (Z01 * K00 - Z00 * K01) * ik;
-                    n11 = (Z11 * K00 - Z01 * K01) * ik;
-                }
-                Y00 = rdlane(n00, ls);
-                Y01 = rdlane(n01, ls);
-                Y11 = rdlane(n11, ls);
-            }
-            if (w > 0) {
-                // hand Y_{64w} and P_{64w} (this wavefront's first knot) to wavefront w-1
-                if (lane == 0) {
-                    bnd[kBnd * w + kBY] = Y00;
-                    bnd[kBnd * w + kBY + 1] = Y01;
-                    bnd[kBnd * w + kBY + 2] = Y11;
-                    const double detZ = Z00 * Z11 - Z01 * Z01;
-                    const double iz = a2 / detZ;
-                    bnd[kBnd * w + kBP] = P.Qw0 + Z11 * iz;
-                    bnd[kBnd * w + kBP + 1] = -(Z01 * iz);
-                    bnd[kBnd * w + kBP + 2] = P.Qw1 + Z00 * iz;
-                }
+            ok = rc_apply(e, b0, b1, b2v, Pk00, Pk01, Pk11) && ok;
+            if (lane == 0 && w > 0) {
+                bnd[kBnd * w + kBP] = Pk00;
+                bnd[kBnd * w + kBP + 1] = Pk01;
+                bnd[kBnd * w + kBP + 2] = Pk11;
             }
         }
         if (w > 0) __syncthreads();
     }
-    // knot-parallel: P_k = Q + alpha^2 Z_k^{-1}; lane k takes P_{k+1} from lane k+1
-    double Pk00 = 0.0, Pk01 = 0.0, Pk11 = 0.0;
-    if (own && k >= 1) {
-        const double detZ = Z00 * Z11 - Z01 * Z01;
-        const double iz = a2 / detZ;
-        Pk00 = P.Qw0 + Z11 * iz;
-        Pk01 = -(Z01 * iz);
-        Pk11 = P.Qw1 + Z00 * iz;
-    }
-    double P00 = __shfl_down(Pk00, 1, kWave);
-    double P01 = __shfl_down(Pk01, 1, kWave);
-    double P11 = __shfl_down(Pk11, 1, kWave);
+    // lane k takes P_{k+1} from lane k+1
+    const int a1 = ((ln + 1) & (kWave - 1)) << 2;
+    double P00 = bperm(a1, Pk00);
+    double P01 = bperm(a1, Pk01);
+    double P11 = bperm(a1, Pk11);
     if (lane == kWave - 1 && NW > 1 && wv < nwa - 1) {
         P00 = bnd[kBnd * (wv + 1) + kBP];
         P01 = bnd[kBnd * (wv + 1) + kBP + 1];
@@ -520,7 +582,7 @@ __device__ __forceinline__ void publish_xi(const Knot& K, double* bnd, int wv, i
 }
 
 #ifndef BLF_MIN_WAVES
-#define BLF_MIN_WAVES 2   // waves per SIMD the register allocation must allow (<= 256 VGPRs)
+#define BLF_MIN_WAVES 3   // waves per SIMD the register allocation must allow (<= 168 VGPRs)
 #endif
 template <int NT>
 __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_ipm_kernel(
@@ -797,13 +859,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
             STAMP_ADD(2, t_s);
             q = 0.0;
-            double cds[kMaxFacets], cdl[kMaxFacets];
             if (own) {
                 const int kx = opaque(k);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    cds[i] = 0.0;
-                    cdl[i] = 0.0;
                     if (i >= mmax) break;
                     if (i < K.m) {
                         const double2 a = L.A2[i * N + kx];
@@ -817,8 +876,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         const double dl = ((-rc) - K.lam[i] * ds) * is;
                         if (ds < 0.0) q = keepmax(q, (-ds) * is);
                         if (dl < 0.0) q = keepmax(q, (-dl) / K.lam[i]);
-                        cds[i] = ds;
-                        cdl[i] = dl;
+                        L.IS[i * N + kx] = dl;   // 1/s is dead now: keep the multiplier step
                     }
                 }
             }
@@ -826,18 +884,21 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             const double step = qc > 0.0 ? 0.99 / qc : 1.0;
             const double a = step < 1.0 ? step : 1.0;
             if (own) {
-                K.r0 = K.r0 + a * dr0;
-                K.r1 = K.r1 + a * dr1;
-                K.x0 = K.x0 + a * dx0;
-                K.x1 = K.x1 + a * dx1;
+                const int kx = opaque(k);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
                     if (i >= mmax) break;
                     if (i < K.m) {
-                        K.s[i] = K.s[i] + a * cds[i];
-                        K.lam[i] = K.lam[i] + a * cdl[i];
+                        const double2 fa = L.A2[i * N + kx];
+                        const double ds = (-facet_rp(K, fa, L.bb[i * N + kx], i)) - (fa.x * dr0 + fa.y * dr1);
+                        K.s[i] = K.s[i] + a * ds;
+                        K.lam[i] = K.lam[i] + a * L.IS[i * N + kx];
                     }
                 }
+                K.r0 = K.r0 + a * dr0;   // after the facet steps, which use the old r
+                K.r1 = K.r1 + a * dr1;
+                K.x0 = K.x0 + a * dx0;
+                K.x1 = K.x1 + a * dx1;
             }
             publish_xi<NW>(K, bnd, wv, lane);
             dres = dres * (1.0 - a);

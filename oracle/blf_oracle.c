@@ -312,7 +312,7 @@ typedef struct {
     double *al, *be, *a2, *b2, *ab;        /* [N] */
     double *s, *lam, *is, *cds, *cdl;      /* [N][MF] slacks, multipliers, 1/s, step */
     double *W;                             /* [N][4] A^T diag(lam/s) A (3), its determinant (1) */
-    double *E, *Z, *Pn, *h;                /* [N][3] */
+    double *E, *Pn, *h;                    /* [N][3] */
     double *G, *Mm;                        /* [N][4]: G_k, M_k = P_{k+1} h_k */
     double *rh, *g, *d, *qx, *dr, *dra;    /* [N][2] */
     double *c, *q;                         /* [N] reduction partials */
@@ -508,14 +508,90 @@ static double dcm_residuals(dcm_ws* w, int use_facets)
     return pres;
 }
 
+/* Riccati map element f(P) = H + A^T P (I + G P)^{-1} A (A 2x2 row-major, G and H symmetric).
+ * Knot k: A = alpha_k I, G = E_k = beta_k^2 (R + W_k)^{-1}, H = Q, so P_k = f_k(P_{k+1}).
+ * rc_combine(e1, e2) = e1 o e2 (e1 the earlier knot):
+ *   T = I + G1 H2,  U = T^{-1} A1,  A = A2 U,  G = (A2 T^{-1}) G1 A2^T + G2,  H = U^T (H2 A1) + H1
+ * (the structure-preserving doubling composition: only (I + G H)^{-1}, eigenvalues >= 1). */
+typedef struct { double a[4], g[3], h[3]; } rc_el;
+
+static int rc_combine(rc_el* e1, const rc_el* e2)
+{
+    const double* A1 = e1->a; const double* G1 = e1->g; const double* H1 = e1->h;
+    const double* A2 = e2->a; const double* G2 = e2->g; const double* H2 = e2->h;
+    const double T00 = 1.0 + (G1[0] * H2[0] + G1[1] * H2[1]);
+    const double T01 = G1[0] * H2[1] + G1[1] * H2[2];
+    const double T10 = G1[1] * H2[0] + G1[2] * H2[1];
+    const double T11 = 1.0 + (G1[1] * H2[1] + G1[2] * H2[2]);
+    const double detT = T00 * T11 - T01 * T10;
+    const int ok = (detT > 0.0) && !isinf(detT);
+    const double it = 1.0 / detT;
+    const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
+    const double U00 = Ti00 * A1[0] + Ti01 * A1[2];
+    const double U01 = Ti00 * A1[1] + Ti01 * A1[3];
+    const double U10 = Ti10 * A1[0] + Ti11 * A1[2];
+    const double U11 = Ti10 * A1[1] + Ti11 * A1[3];
+    const double V00 = A2[0] * Ti00 + A2[1] * Ti10;
+    const double V01 = A2[0] * Ti01 + A2[1] * Ti11;
+    const double V10 = A2[2] * Ti00 + A2[3] * Ti10;
+    const double V11 = A2[2] * Ti01 + A2[3] * Ti11;
+    const double X00 = V00 * G1[0] + V01 * G1[1];
+    const double X01 = V00 * G1[1] + V01 * G1[2];
+    const double X10 = V10 * G1[0] + V11 * G1[1];
+    const double X11 = V10 * G1[1] + V11 * G1[2];
+    const double Y00 = H2[0] * A1[0] + H2[1] * A1[2];
+    const double Y01 = H2[0] * A1[1] + H2[1] * A1[3];
+    const double Y10 = H2[1] * A1[0] + H2[2] * A1[2];
+    const double Y11 = H2[1] * A1[1] + H2[2] * A1[3];
+    rc_el r;
+    r.a[0] = A2[0] * U00 + A2[1] * U10;
+    r.a[1] = A2[0] * U01 + A2[1] * U11;
+    r.a[2] = A2[2] * U00 + A2[3] * U10;
+    r.a[3] = A2[2] * U01 + A2[3] * U11;
+    r.g[0] = (X00 * A2[0] + X01 * A2[1]) + G2[0];
+    r.g[1] = (X00 * A2[2] + X01 * A2[3]) + G2[1];
+    r.g[2] = (X10 * A2[2] + X11 * A2[3]) + G2[2];
+    r.h[0] = (U00 * Y00 + U10 * Y10) + H1[0];
+    r.h[1] = (U00 * Y01 + U10 * Y11) + H1[1];
+    r.h[2] = (U01 * Y01 + U11 * Y11) + H1[2];
+    *e1 = r;
+    return ok;
+}
+
+/* P_out = f(e, P) */
+static int rc_apply(const rc_el* e, double P00, double P01, double P11, double* out)
+{
+    const double* A = e->a; const double* G = e->g; const double* H = e->h;
+    const double S00 = 1.0 + (G[0] * P00 + G[1] * P01);
+    const double S01 = G[0] * P01 + G[1] * P11;
+    const double S10 = G[1] * P00 + G[2] * P01;
+    const double S11 = 1.0 + (G[1] * P01 + G[2] * P11);
+    const double detS = S00 * S11 - S01 * S10;
+    const int ok = (detS > 0.0) && !isinf(detS);
+    const double is = 1.0 / detS;
+    const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
+    const double W00 = P00 * Si00 + P01 * Si10;
+    const double W01 = P00 * Si01 + P01 * Si11;
+    const double W10 = P01 * Si00 + P11 * Si10;
+    const double W11 = P01 * Si01 + P11 * Si11;
+    const double Z00 = W00 * A[0] + W01 * A[2];
+    const double Z01 = W00 * A[1] + W01 * A[3];
+    const double Z10 = W10 * A[0] + W11 * A[2];
+    const double Z11 = W10 * A[1] + W11 * A[3];
+    out[0] = (A[0] * Z00 + A[2] * Z10) + H[0];
+    out[1] = (A[0] * Z01 + A[2] * Z11) + H[1];
+    out[2] = (A[1] * Z01 + A[3] * Z11) + H[2];
+    return ok;
+}
+
 /* Factorization of the Newton system for the barrier Hessian blocks W_k.
  * 1. E_k = beta_k^2 (R + W_k)^{-1}                                           (knot-parallel)
- * 2. information-form Riccati, sequential k = N-1 .. 1 (one lane at a time on the device):
- *      Z_k = Y_{k+1} + E_k,  K = Q Z_k + alpha_k^2 I,  Y_k = Z_k K^{-1}  (= P_k^{-1}),
- *    Y_N = P_N^{-1}: a single division on the recursion's critical path;
- * 3. P_k = Q + alpha_k^2 Z_k^{-1}, H_k = R + W_k + beta_k^2 P_{k+1}, h_k = H_k^{-1},
- *    M_k = P_{k+1} h_k, G_k = alpha_k (I - beta_k^2 M_k)                     (knot-parallel)
- * Returns 0 if some K or H_k is not positive definite (status NUMERICAL). */
+ * 2. P_k for every knot by a Kogge-Stone scan of Riccati map elements over the 64 lanes of each
+ *    wavefront (lane l composes with lane l + d), then P_k = f_{k..}(P at the next wavefront's
+ *    first knot, or P_N = diag(Pw)), wavefronts from last to first;
+ * 3. H_k = R + W_k + beta_k^2 P_{k+1}, h_k = H_k^{-1}, M_k = P_{k+1} h_k,
+ *    G_k = alpha_k (I - beta_k^2 M_k)                                         (knot-parallel)
+ * Returns 0 if some (I + G H), (I + G P) or H_k is not positive definite (status NUMERICAL). */
 static int dcm_factor(dcm_ws* w)
 {
     const int N = w->N;
@@ -528,30 +604,53 @@ static int dcm_factor(dcm_ws* w)
         w->E[3 * k + 1] = -(Wk[1] * ie);
         w->E[3 * k + 2] = (w->Rw0 + Wk[0]) * ie;
     }
-    double Y00 = 1.0 / w->Pw0, Y01 = 0.0, Y11 = 1.0 / w->Pw1;
-    for (int k = N - 1; k >= 1; --k) {
-        const double Z00 = Y00 + w->E[3 * k];
-        const double Z01 = Y01 + w->E[3 * k + 1];
-        const double Z11 = Y11 + w->E[3 * k + 2];
-        w->Z[3 * k] = Z00; w->Z[3 * k + 1] = Z01; w->Z[3 * k + 2] = Z11;
-        const double K00 = w->Qw0 * Z00 + w->a2[k];
-        const double K01 = w->Qw0 * Z01;
-        const double K10 = w->Qw1 * Z01;
-        const double K11 = w->Qw1 * Z11 + w->a2[k];
-        const double detK = K00 * K11 - K01 * K10;
-        if (!(detK > 0.0) || isinf(detK)) ok = 0;
-        const double ik = 1.0 / detK;
-        Y00 = (Z00 * K11 - Z01 * K10) * ik;
-        Y01 = (Z01 * K00 - Z00 * K01) * ik;
-        Y11 = (Z11 * K00 - Z01 * K01) * ik;
+    double Pb0 = w->Pw0, Pb1 = 0.0, Pb2 = w->Pw1;      /* P at the next wavefront's first knot */
+    if (!w->scans) {   /* CPU-efficient sequential recursion P_k = f_k(P_{k+1}) (cpu_baseline only) */
+        for (int k = N - 1; k >= 1; --k) {
+            rc_el e;
+            e.a[0] = w->al[k]; e.a[1] = 0.0; e.a[2] = 0.0; e.a[3] = w->al[k];
+            e.g[0] = w->E[3 * k]; e.g[1] = w->E[3 * k + 1]; e.g[2] = w->E[3 * k + 2];
+            e.h[0] = w->Qw0; e.h[1] = 0.0; e.h[2] = w->Qw1;
+            double out[3];
+            if (!rc_apply(&e, Pb0, Pb1, Pb2, out)) ok = 0;
+            w->Pn[3 * (k - 1)] = out[0]; w->Pn[3 * (k - 1) + 1] = out[1]; w->Pn[3 * (k - 1) + 2] = out[2];
+            Pb0 = out[0]; Pb1 = out[1]; Pb2 = out[2];
+        }
     }
-    for (int k = 1; k < N; ++k) {
-        const double* Z = w->Z + 3 * k;
-        const double detZ = Z[0] * Z[2] - Z[1] * Z[1];
-        const double iz = w->a2[k] / detZ;
-        w->Pn[3 * (k - 1)] = w->Qw0 + Z[2] * iz;       /* P_k, needed by knot k - 1 */
-        w->Pn[3 * (k - 1) + 1] = -(Z[1] * iz);
-        w->Pn[3 * (k - 1) + 2] = w->Qw1 + Z[0] * iz;
+    for (int wv = w->scans ? w->NW - 1 : -1; wv >= 0; --wv) {
+        rc_el e[WV], ne[WV];
+        for (int l = 0; l < WV; ++l) {
+            const int k = WV * wv + l;
+            if (k < N) {
+                e[l].a[0] = w->al[k]; e[l].a[1] = 0.0; e[l].a[2] = 0.0; e[l].a[3] = w->al[k];
+                e[l].g[0] = w->E[3 * k]; e[l].g[1] = w->E[3 * k + 1]; e[l].g[2] = w->E[3 * k + 2];
+                e[l].h[0] = w->Qw0; e[l].h[1] = 0.0; e[l].h[2] = w->Qw1;
+            } else {
+                e[l].a[0] = 1.0; e[l].a[1] = 0.0; e[l].a[2] = 0.0; e[l].a[3] = 1.0;
+                e[l].g[0] = e[l].g[1] = e[l].g[2] = 0.0;
+                e[l].h[0] = e[l].h[1] = e[l].h[2] = 0.0;
+            }
+        }
+        for (int dd = 1; dd < WV; dd <<= 1) {
+            for (int l = 0; l < WV; ++l) {
+                ne[l] = e[l];
+                if (l + dd < WV && !rc_combine(&ne[l], &e[l + dd])) ok = 0;
+            }
+            memcpy(e, ne, sizeof(e));
+        }
+        double Pw0v = 0.0, Pw1v = 0.0, Pw2v = 0.0;
+        for (int l = 0; l < WV; ++l) {
+            const int k = WV * wv + l;
+            double out[3];
+            if (!rc_apply(&e[l], Pb0, Pb1, Pb2, out)) ok = 0;
+            if (l == 0) { Pw0v = out[0]; Pw1v = out[1]; Pw2v = out[2]; }
+            if (k >= 1 && k < N) {
+                w->Pn[3 * (k - 1)] = out[0];        /* P_k, needed by knot k - 1 */
+                w->Pn[3 * (k - 1) + 1] = out[1];
+                w->Pn[3 * (k - 1) + 2] = out[2];
+            }
+        }
+        Pb0 = Pw0v; Pb1 = Pw1v; Pb2 = Pw2v;
     }
     w->Pn[3 * (N - 1)] = w->Pw0;
     w->Pn[3 * (N - 1) + 1] = 0.0;
@@ -714,14 +813,14 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
     w->Pw0 = prm->w_terminal[0]; w->Pw1 = prm->w_terminal[1];
     w->omega = omega; w->xi_ref = xi_ref; w->vrp_ref = vrp_ref; w->A = Ain; w->b = bin;
     w->nf = nfacets; w->xi = xi; w->vrp = vrp;
-    const size_t per_knot = 5 + 5 * MF + 4 + 4 * 3 + 8 + 6 * 2 + 2 + 2 + 4;
+    const size_t per_knot = 5 + 5 * MF + 4 + 3 * 3 + 8 + 6 * 2 + 2 + 2 + 4;
     double* mem = (double*)calloc((size_t)N * per_knot + 4 * (size_t)(N + 1), sizeof(double));
     double* p = mem;
     w->al = p; p += N; w->be = p; p += N; w->a2 = p; p += N; w->b2 = p; p += N; w->ab = p; p += N;
     w->s = p; p += N * MF; w->lam = p; p += N * MF; w->is = p; p += N * MF;
     w->cds = p; p += N * MF; w->cdl = p; p += N * MF;
     w->W = p; p += 4 * N;
-    w->E = p; p += 3 * N; w->Z = p; p += 3 * N; w->Pn = p; p += 3 * N; w->h = p; p += 3 * N;
+    w->E = p; p += 3 * N; w->Pn = p; p += 3 * N; w->h = p; p += 3 * N;
     w->G = p; p += 4 * N; w->Mm = p; p += 4 * N;
     w->rh = p; p += 2 * N; w->g = p; p += 2 * N; w->d = p; p += 2 * N; w->qx = p; p += 2 * N;
     w->dr = p; p += 2 * N; w->dra = p; p += 2 * N;
