@@ -26,7 +26,8 @@ namespace {
 
 #ifdef BLF_STAMPS
 // Diagnostic build only (make stamps): per-phase cycle sums of thread 0 for the first 64 QPs.
-// [0] whole kernel, [1] factorization, [2] both solves, [3] iterations.
+// [0] whole kernel, [1] factorization, [2] predictor solve .. corrector solve, [3] iterations,
+// [4] residuals + reduction, [5] W-phase, [6] predictor solve, [7] corrector step + update.
 __device__ unsigned long long g_blf_stamps[8];
 #define STAMP(t) unsigned long long t = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, t0) \
@@ -725,6 +726,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
 
         for (it = 0; status == 0; ++it) {
             // ---- residuals (knot-parallel) ----
+            STAMP(t_r);
             xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
             pres = 0.0;
             ck = 0.0;
@@ -735,6 +737,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 status = BLF_QP_NUMERICAL;
                 break;
             }
+            STAMP_ADD(4, t_r);
             if (mu <= P.tol_mu && pres <= P.tol_p && dres <= P.tol_d) break;   // solved
             if (it >= P.max_iter) {
                 status = BLF_QP_MAX_ITER;
@@ -742,22 +745,21 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             }
 
             // ---- W-phase: 1/s, W = A^T diag(lam/s) A, det W, predictor rhs ----
+            STAMP(t_w);
             double W00 = 0.0, W01 = 0.0, W11 = 0.0, dW = 0.0;
             double g0 = K.rh0, g1 = K.rh1;
             if (own) {
                 const int kx = opaque(k);
-                double sg[kMaxFacets];
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    sg[i] = 0.0;
                     if (i >= mmax) break;
                     if (i < K.m) {
                         const double2 a = L.A2[i * N + kx];
                         const double is = 1.0 / K.s[i];
                         L.IS[i * N + kx] = is;
-                        sg[i] = K.lam[i] * is;
-                        const double t0 = sg[i] * a.x;
-                        const double t1 = sg[i] * a.y;
+                        const double sg = K.lam[i] * is;
+                        const double t0 = sg * a.x;
+                        const double t1 = sg * a.y;
                         W00 = W00 + t0 * a.x;
                         W01 = W01 + t0 * a.y;
                         W11 = W11 + t1 * a.y;
@@ -767,20 +769,26 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         g1 = g1 + a.y * e;
                     }
                 }
+                // sg_i = lam_i / s_i is recomputed from the stored 1/s (bit-identical) rather than
+                // kept in an 8-entry register array across the pair loop (which spilled)
 #pragma unroll
                 for (int i = 1; i < kMaxFacets; ++i) {
                     if (i >= mmax) break;
                     if (i < K.m) {
-                        const double2 ai = L.A2[i * N + kx];
+                        const int ki = opaque(k);
+                        const double2 ai = L.A2[i * N + ki];
+                        const double sgi = K.lam[i] * L.IS[i * N + ki];
 #pragma unroll
                         for (int j = 0; j < i; ++j) {
-                            const double2 aj = L.A2[j * N + kx];
+                            const double2 aj = L.A2[j * N + ki];
+                            const double sgj = K.lam[j] * L.IS[j * N + ki];
                             const double cr = ai.x * aj.y - ai.y * aj.x;
-                            dW = dW + (sg[i] * sg[j]) * (cr * cr);
+                            dW = dW + (sgi * sgj) * (cr * cr);
                         }
                     }
                 }
             }
+            STAMP_ADD(5, t_w);
             STAMP(t_f);
             ok = factor<NW>(K, P, W00, W01, W11, dW, bnd, N, nwa, k, wv, lane, own);
             if (__syncthreads_or(!ok)) {
@@ -793,6 +801,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             STAMP(t_s);
             double dra0, dra1, dx0, dx1;
             solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dra0, dra1, dx0, dx1);
+            STAMP_ADD(6, t_s);
             double q = 0.0;
             if (own) {
                 const int kx = opaque(k);
@@ -858,6 +867,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             double dr0, dr1;
             solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
             STAMP_ADD(2, t_s);
+            STAMP(t_c);
             q = 0.0;
             if (own) {
                 const int kx = opaque(k);
@@ -903,6 +913,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             publish_xi<NW>(K, bnd, wv, lane);
             dres = dres * (1.0 - a);
             __syncthreads();
+            STAMP_ADD(7, t_c);
         }
     }
 

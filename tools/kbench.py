@@ -51,10 +51,13 @@ def main():
     if stamps is not None:
         stamps(ctypes.cast(buf, ctypes.c_void_p), 0)
         tot, fac, sol, its = buf[0], buf[1], buf[2], buf[3]
+        res, wph, pred, step = buf[4], buf[5], buf[6], buf[7]
         print(f"thread0 cycles per QP: total {tot / 64 / args.reps:.0f}  per iteration: "
-              f"factor+fwd {fac / its:.0f}, solve+fwd {sol / its:.0f}, "
-              f"rest {(tot - fac - sol) / its:.0f}  (iters counted {its / 64 / args.reps:.2f})")
-
+              f"residuals {res / its:.0f}, W-phase {wph / its:.0f}, factor {fac / its:.0f}, "
+              f"predictor solve {pred / its:.0f}, ratio+mu_aff+corr-rhs+corr-solve "
+              f"{(sol - pred) / its:.0f}, step+update {step / its:.0f}, "
+              f"unaccounted {(tot - res - wph - fac - sol - step) / its:.0f} "
+              f"(iters counted {its / 64 / args.reps:.2f})")
 
 if __name__ == "__main__":
     main()
