@@ -39,7 +39,8 @@ def profiled_traffic():
     (profiles/*_summary.json, written by tools/summarize_profile.py from separate FETCH_SIZE /
     WRITE_SIZE passes); bench.py cannot read PMC counters itself."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime)
+    # newest by name (profiles/rNN_<tag>_summary.json; file times do not survive the copy to a box)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -55,10 +56,13 @@ def cpu_baseline(host, N, seconds, threads):
     import numpy as np
     import oracle as O
     B = host["omega"].shape[0]
-    O.dcm_mpc_solve_batch(host, threads=threads, count=min(B, 64))   # warm-up
+    # the CPU-efficient form of the same algorithm: sequential recursions instead of the device's
+    # lane scans (oracle `sequential` mode; identical iterates up to rounding)
+    prm = O.default_params(N, max_facets=host["b"].shape[2], sequential=1)
+    O.dcm_mpc_solve_batch(host, params=prm, threads=threads, count=min(B, 64))   # warm-up
     solved, t0 = 0, time.perf_counter()
     while True:
-        st, _, _, _ = O.dcm_mpc_solve_batch(host, threads=threads)
+        st, _, _, _ = O.dcm_mpc_solve_batch(host, params=prm, threads=threads)
         solved += B
         el = time.perf_counter() - t0
         if el >= seconds:
@@ -67,11 +71,12 @@ def cpu_baseline(host, N, seconds, threads):
     # single-problem latency (one thread), BASELINE.md C1-style figure at this horizon
     t1 = time.perf_counter()
     for i in range(20):
-        O.dcm_mpc_solve(host, index=i)
+        O.dcm_mpc_solve(host, params=prm, index=i)
     lat_us = (time.perf_counter() - t1) / 20 * 1e6
     return dict(value=solved / el, unit="QP/s", cores=threads, kind="port",
                 sample=f"{solved} solves = {solved // B} passes over the same {B} horizon-{N} QPs "
-                       f"in {el:.2f} s wall on {threads} threads (oracle/blf_oracle.c, gcc -O2)",
+                       f"in {el:.2f} s wall on {threads} threads (oracle/blf_oracle.c sequential "
+                       f"mode, gcc -O2, one problem per thread)",
                 single_thread_latency_us=round(lat_us, 1))
 
 
@@ -147,12 +152,11 @@ def main():
     # RCCL gather of every rank's solutions to rank 0 (timed separately, not in `value`)
     gather_ms = None
     if world > 1:
-        payload = torch.cat([out["xi"].reshape(B, -1), out["vrp"].reshape(B, -1),
-                             out["status"].to(torch.float64)[:, None]], dim=1)
-        bufs = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
-        dist.barrier(); torch.cuda.synchronize()
+        from blf import distributed as D
+        dist.barrier()
+        torch.cuda.synchronize()
         tg = time.perf_counter()
-        dist.gather(payload, bufs, dst=0)
+        D.gather_solutions(out, N, dst=0)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
@@ -163,7 +167,7 @@ def main():
         traffic, traffic_src = profiled_traffic()
         fp64_tf = flops / (kernel_ms * 1e-3) / 1e12
         line = {
-            "metric": "DCM-MPC QP solves/sec (batch, horizon=100)",
+            "metric": "DCM-MPC QP solves/sec (batch, horizon=100) at 1/2/4/8 MI355X",
             "value": total / elapsed,
             "unit": "QP/s",
             "n_gpus": world,

@@ -221,13 +221,15 @@ blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* param
 
 double blf_dcm_mpc_flops_per_iter(int32_t horizon, int64_t active_facets)
 {
-    // Counted from dcm_mpc_ipm.hip, per IPM iteration (fp64 add/sub/mul/div = 1 flop each;
-    // negations, fabs, min/max and compares not counted):
-    //   per facet: residual 11, R' + affine rhs 17, affine step 11, mu_aff 14,
-    //              corrector rhs 10, corrector step 12, update 4                    = 79
-    //   per knot:  residual/defect/Q-terms 20, backward factor+solve 74, backward solve 32,
-    //              two forward sweeps 2 x 25, update 8                               = 184
-    return 79.0 * (double)active_facets + 184.0 * (double)horizon;
+    // Algorithmic flops of one IPM iteration, counted on the sequential restatement of the
+    // algorithm (fp64 add/sub/mul/div = 1 flop, negation / fabs / compares
+    // not counted) — the device's lane scans do more arithmetic than this on purpose:
+    //   per knot:  residuals 20, E 10, Riccati step 40, H^-1 / M / G 45, two solves 2 x 66,
+    //              update 8                                                         = 255
+    //   per facet: residual 11, W-phase 22, affine ratio 16, mu_aff 18, corrector rhs 27,
+    //              corrector step 31, update 12                                     = 137
+    //   per facet pair (det W): 6, i.e. 3 m(m-1) per knot; taken as 12 per facet (m ~ 5)
+    return 149.0 * (double)active_facets + 255.0 * (double)horizon;
 }
 
 }  // extern "C"
