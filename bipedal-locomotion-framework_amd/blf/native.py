@@ -22,7 +22,9 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_quintic_fit", "blf_quintic_eval",
-            "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_flops_per_iter"]
+            "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_flops_per_iter",
+            "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
+            "blf_fbk_euler_integrate"]
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -80,6 +82,13 @@ def lib():
                                         ctypes.POINTER(DcmMpcProblem), _i64,
                                         ctypes.POINTER(DcmMpcSolution), _vp]
         L.blf_dcm_mpc_flops_per_iter.argtypes = [_i32, _i64]
+        L.blf_contact_model_eval.argtypes = [_vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                             _vp, _vp]
+        L.blf_contact_point_wrench.argtypes = [_vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _i32,
+                                               _vp, _vp, _vp]
+        L.blf_fbk_dynamics.argtypes = [_vp, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]
+        L.blf_fbk_euler_integrate.argtypes = [_vp, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _i64,
+                                              _f64, _f64, _f64, _vp]
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         for name in EXPORTED:
             if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
@@ -305,3 +314,70 @@ class Handle:
         npts = ncorners[:, :N].reshape(B * N).contiguous()
         A, b, nf = self.hull2d_hrep(pts, npts, max_facets, stream=stream)
         return A.view(B, N, max_facets, 2), b.view(B, N, max_facets), nf.view(B, N)
+
+    # ---- config 5: contact model and floating-base kinematics ---------------------------------
+    def _contact_inputs(self, params, twist, pose, null_pose):
+        torch = _torch()
+        B = twist.shape[0]
+        shared = params.dim() == 1
+        pp = _ptr(params, torch.float64, (4,) if shared else (B, 4), "params")
+        return (B, shared, pp, _ptr(twist, torch.float64, (B, 6), "twist"),
+                _ptr(pose, torch.float64, (B, 12), "pose"),
+                _ptr(null_pose, torch.float64, (B, 12), "null_pose"))
+
+    def contact_model_eval(self, params, twist, pose, null_pose,
+                           outputs=("wrench", "autonomous", "control", "regressor"), stream=None):
+        """ContinuousContactModel for a batch: params [B,4] or [4] (L, W, k, b), twist [B,6],
+        pose / null_pose [B,12] = (p, R row-major).  Returns the requested outputs."""
+        torch = _torch()
+        B, shared, pp, tw, ps, ns = self._contact_inputs(params, twist, pose, null_pose)
+        shapes = dict(wrench=(B, 6), autonomous=(B, 6), control=(B, 6, 6), regressor=(B, 6, 2))
+        out = {k: torch.empty(shapes[k], dtype=torch.float64, device=twist.device) for k in outputs}
+        ptrs = [ctypes.c_void_p(out[k].data_ptr()) if k in out else None
+                for k in ("wrench", "autonomous", "control", "regressor")]
+        _check(lib().blf_contact_model_eval(self._h, pp, 1 if shared else 0, tw, ps, ns, B,
+                                            *ptrs, _stream(stream)))
+        return out
+
+    def contact_point_wrench(self, params, twist, pose, null_pose, points, stream=None):
+        """Force / torque at points [B,Q,2] of each contact surface -> ([B,Q,3], [B,Q,3])."""
+        torch = _torch()
+        B, shared, pp, tw, ps, ns = self._contact_inputs(params, twist, pose, null_pose)
+        Q = points.shape[1]
+        f = torch.empty((B, Q, 3), dtype=torch.float64, device=twist.device)
+        t = torch.empty_like(f)
+        _check(lib().blf_contact_point_wrench(
+            self._h, pp, 1 if shared else 0, tw, ps, ns, B,
+            _ptr(points, torch.float64, (B, Q, 2), "points"), Q, ctypes.c_void_p(f.data_ptr()),
+            ctypes.c_void_p(t.data_ptr()), _stream(stream)))
+        return f, t
+
+    def fbk_dynamics(self, rho, rot, twist, joint_vel, stream=None):
+        """FloatingBaseSystemKinematics::dynamics: rot [B,3,3], twist [B,6], joint_vel [B,n]."""
+        torch = _torch()
+        B, n = joint_vel.shape
+        dp = torch.empty((B, 3), dtype=torch.float64, device=twist.device)
+        dR = torch.empty((B, 3, 3), dtype=torch.float64, device=twist.device)
+        dq = torch.empty((B, n), dtype=torch.float64, device=twist.device)
+        _check(lib().blf_fbk_dynamics(
+            self._h, n, float(rho), _ptr(rot, torch.float64, (B, 3, 3), "rot"),
+            _ptr(twist, torch.float64, (B, 6), "twist"),
+            _ptr(joint_vel, torch.float64, (B, n), "joint_vel") if n else None,
+            ctypes.c_void_p(dp.data_ptr()), ctypes.c_void_p(dR.data_ptr()),
+            ctypes.c_void_p(dq.data_ptr()) if n else None, B, _stream(stream)))
+        return dp, dR, dq
+
+    def fbk_euler_integrate(self, rho, pos, rot, joints, twist, joint_vel, t0, t1, dT,
+                            stream=None):
+        """ForwardEuler<FloatingBaseSystemKinematics>::integrate in place on pos [B,3],
+        rot [B,3,3], joints [B,n] with constant twist [B,6] and joint_vel [B,n]."""
+        torch = _torch()
+        B, n = joints.shape
+        _check(lib().blf_fbk_euler_integrate(
+            self._h, n, float(rho), _ptr(pos, torch.float64, (B, 3), "pos"),
+            _ptr(rot, torch.float64, (B, 3, 3), "rot"),
+            _ptr(joints, torch.float64, (B, n), "joints") if n else None,
+            _ptr(twist, torch.float64, (B, 6), "twist"),
+            _ptr(joint_vel, torch.float64, (B, n), "joint_vel") if n else None,
+            B, float(t0), float(t1), float(dT), _stream(stream)))
+        return pos, rot, joints

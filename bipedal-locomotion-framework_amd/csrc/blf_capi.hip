@@ -39,6 +39,34 @@ struct blf_handle {
         if (!(cond)) return set_error(BLF_ERR_INVALID_ARGUMENT, __VA_ARGS__);              \
     } while (0)
 
+// FixedStepIntegrator::integrate's step schedule (FixedStepIntegrator.tpp:21-72): validation in
+// the reference's order, iterations = ceil((T - t0) / dT); steps 0..iterations-2 advance by dT and
+// the last one by T - currentTime with the stale currentTime = t0 + dT (iterations - 2) (:48-64).
+static blf_status step_schedule(double initial_time, double final_time, double dT,
+                                int* iterations_out, double* dT_last_out)
+{
+    if (initial_time > final_time)                                                      // :26-30
+        return set_error(BLF_ERR_TIME_INTERVAL,
+                         "[FixedStepIntegrator::integrate] The final time has to be greater than "
+                         "the initial one.");
+    if (!(dT > 0))                                                                      // :40-46
+        return set_error(BLF_ERR_TIME_INTERVAL,
+                         "[FixedStepIntegrator::integrate] The sampling time must be a strictly "
+                         "positive number.");
+    if (initial_time == final_time)
+        return set_error(BLF_ERR_EMPTY_INTERVAL,
+                         "integrate(t, t): the reference loops forever here "
+                         "(FixedStepIntegrator.tpp:51, size_t i < -1); refused");
+    const double q = ceil((final_time - initial_time) / dT);                            // :48
+    if (!(q < 2.0e9)) return set_error(BLF_ERR_UNSUPPORTED, "too many integration steps");
+    const int iterations = (int)q;
+    double currentTime = initial_time;
+    if (iterations >= 2) currentTime = initial_time + dT * (double)(iterations - 2);   // :53
+    *iterations_out = iterations;
+    *dT_last_out = final_time - currentTime;                                            // :64
+    return BLF_OK;
+}
+
 extern "C" {
 
 blf_status blf_create(blf_handle** handle, int32_t device)
@@ -79,25 +107,10 @@ blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m, con
                 "blf_lti_euler_integrate: n=%d m=%d outside [1, 8]", n, m);
     BLF_REQUIRE(batch >= 0, "blf_lti_euler_integrate: negative batch");
     BLF_REQUIRE(batch == 0 || (A && Bm && u && x), "blf_lti_euler_integrate: null buffer");
-    // FixedStepIntegrator.tpp:28-46
-    if (initial_time > final_time)
-        return set_error(BLF_ERR_TIME_INTERVAL,
-                         "[FixedStepIntegrator::integrate] The final time has to be greater than "
-                         "the initial one.");
-    if (!(dT > 0))
-        return set_error(BLF_ERR_TIME_INTERVAL,
-                         "[FixedStepIntegrator::integrate] The sampling time must be a strictly "
-                         "positive number.");
-    if (initial_time == final_time)
-        return set_error(BLF_ERR_EMPTY_INTERVAL,
-                         "integrate(t, t): the reference loops forever here "
-                         "(FixedStepIntegrator.tpp:96-99); refused");
-    const double q = ceil((final_time - initial_time) / dT);   // :96
-    if (!(q < 2.0e9)) return set_error(BLF_ERR_UNSUPPORTED, "too many integration steps");
-    const int iterations = (int)q;
-    double currentTime = initial_time;
-    if (iterations >= 2) currentTime = initial_time + dT * (double)(iterations - 2);   // :101
-    const double dT_last = final_time - currentTime;                                    // :112
+    int iterations = 0;
+    double dT_last = 0.0;
+    const blf_status st = step_schedule(initial_time, final_time, dT, &iterations, &dT_last);
+    if (st != BLF_OK) return st;
     return launch_lti_euler(n, m, A, Bm, shared_matrices, u, x, batch, iterations, dT, dT_last,
                             (hipStream_t)stream);
 }
@@ -230,6 +243,73 @@ double blf_dcm_mpc_flops_per_iter(int32_t horizon, int64_t active_facets)
     //              corrector step 31, update 12                                     = 137
     //   per facet pair (det W): 6, i.e. 3 m(m-1) per knot; taken as 12 per facet (m ~ 5)
     return 149.0 * (double)active_facets + 255.0 * (double)horizon;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+blf_status blf_contact_model_eval(blf_handle* handle, const double* params, int32_t shared_params,
+                                  const double* twist, const double* pose,
+                                  const double* null_pose, int64_t batch, double* wrench,
+                                  double* autonomous, double* control, double* regressor,
+                                  void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_contact_model_eval: null handle");
+    BLF_REQUIRE(batch >= 0, "blf_contact_model_eval: negative batch");
+    BLF_REQUIRE(batch == 0 || (params && twist && pose && null_pose),
+                "blf_contact_model_eval: null input buffer");
+    BLF_REQUIRE(wrench || autonomous || control || regressor,
+                "blf_contact_model_eval: no output requested");
+    return launch_contact_eval(params, shared_params, twist, pose, null_pose, batch, wrench,
+                               autonomous, control, regressor, (hipStream_t)stream);
+}
+
+blf_status blf_contact_point_wrench(blf_handle* handle, const double* params,
+                                    int32_t shared_params, const double* twist, const double* pose,
+                                    const double* null_pose, int64_t batch, const double* points,
+                                    int32_t npoints, double* force, double* torque, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_contact_point_wrench: null handle");
+    BLF_REQUIRE(batch >= 0 && npoints >= 0, "blf_contact_point_wrench: negative size");
+    BLF_REQUIRE(batch == 0 || npoints == 0 ||
+                    (params && twist && pose && null_pose && points && force && torque),
+                "blf_contact_point_wrench: null buffer");
+    return launch_contact_point(params, shared_params, twist, pose, null_pose, batch, points,
+                                npoints, force, torque, (hipStream_t)stream);
+}
+
+blf_status blf_fbk_dynamics(blf_handle* handle, int32_t ndof, double rho, const double* rot,
+                            const double* twist, const double* joint_vel, double* dpos,
+                            double* drot, double* djoints, int64_t batch, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_fbk_dynamics: null handle");
+    BLF_REQUIRE(ndof >= 0 && ndof <= BLF_FBK_MAX_DOFS, "blf_fbk_dynamics: ndof=%d outside [0, %d]",
+                ndof, BLF_FBK_MAX_DOFS);
+    BLF_REQUIRE(batch >= 0, "blf_fbk_dynamics: negative batch");
+    BLF_REQUIRE(batch == 0 || (rot && twist && dpos && drot && (ndof == 0 || (joint_vel && djoints))),
+                "blf_fbk_dynamics: null buffer");
+    return launch_fbk_dynamics(ndof, rho, rot, twist, joint_vel, dpos, drot, djoints, batch,
+                               (hipStream_t)stream);
+}
+
+blf_status blf_fbk_euler_integrate(blf_handle* handle, int32_t ndof, double rho, double* pos,
+                                   double* rot, double* joints, const double* twist,
+                                   const double* joint_vel, int64_t batch, double initial_time,
+                                   double final_time, double dT, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_fbk_euler_integrate: null handle");
+    BLF_REQUIRE(ndof >= 0 && ndof <= BLF_FBK_MAX_DOFS,
+                "blf_fbk_euler_integrate: ndof=%d outside [0, %d]", ndof, BLF_FBK_MAX_DOFS);
+    BLF_REQUIRE(batch >= 0, "blf_fbk_euler_integrate: negative batch");
+    BLF_REQUIRE(batch == 0 || (pos && rot && twist && (ndof == 0 || (joints && joint_vel))),
+                "blf_fbk_euler_integrate: null buffer");
+    int iterations = 0;
+    double dT_last = 0.0;
+    const blf_status st = step_schedule(initial_time, final_time, dT, &iterations, &dT_last);
+    if (st != BLF_OK) return st;
+    return launch_fbk_euler(ndof, rho, pos, rot, joints, twist, joint_vel, batch, iterations, dT,
+                            dT_last, (hipStream_t)stream);
 }
 
 }  // extern "C"

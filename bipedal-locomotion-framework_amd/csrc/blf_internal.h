@@ -45,6 +45,20 @@ blf_status launch_quintic_eval(const double* kt, const double* coeffs, int32_t K
                                int32_t* idx, hipStream_t s);
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
                           int64_t batch, const blf_dcm_mpc_solution* sol, hipStream_t s);
+blf_status launch_contact_eval(const double* prm, int shared, const double* twist,
+                               const double* pose, const double* null_pose, int64_t batch,
+                               double* wrench, double* autonomous, double* control,
+                               double* regressor, hipStream_t s);
+blf_status launch_contact_point(const double* prm, int shared, const double* twist,
+                                const double* pose, const double* null_pose, int64_t batch,
+                                const double* points, int32_t Q, double* force, double* torque,
+                                hipStream_t s);
+blf_status launch_fbk_dynamics(int n, double rho, const double* rot, const double* twist,
+                               const double* joint_vel, double* dpos, double* drot,
+                               double* djoints, int64_t batch, hipStream_t s);
+blf_status launch_fbk_euler(int n, double rho, double* pos, double* rot, double* joints,
+                            const double* twist, const double* joint_vel, int64_t batch,
+                            int32_t nsteps, double dT, double dT_last, hipStream_t s);
 
 // ---- device helpers ----
 // NaN-propagating max (matches the oracle's `if (e > m || e != e) m = e`).

@@ -7,6 +7,8 @@
 #define BLF_BIPEDAL_LOCOMOTION_PLANNERS_CONTACT_H
 
 #include <array>
+
+#include <blf/spatial.h>
 #include <cmath>
 #include <string>
 
@@ -16,30 +18,8 @@ namespace Planners
 {
 
 /** Homogeneous transform: p + R x. */
-struct Transform
-{
-    std::array<double, 3> position{{0.0, 0.0, 0.0}};
-    std::array<double, 9> rotation{{1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}};
-
-    static Transform Identity() { return Transform{}; }
-    /** Planar pose: translation (x, y, z) and a yaw rotation about z. */
-    static Transform fromPlanar(double x, double y, double yaw, double z = 0.0)
-    {
-        Transform t;
-        t.position = {{x, y, z}};
-        const double c = std::cos(yaw), s = std::sin(yaw);
-        t.rotation = {{c, -s, 0.0, s, c, 0.0, 0.0, 0.0, 1.0}};
-        return t;
-    }
-    /** Apply to a point. */
-    std::array<double, 3> apply(const std::array<double, 3>& x) const
-    {
-        std::array<double, 3> out;
-        for (int r = 0; r < 3; ++r)
-            out[r] = position[r] + (rotation[3 * r] * x[0] + rotation[3 * r + 1] * x[1] + rotation[3 * r + 2] * x[2]);
-        return out;
-    }
-};
+/** iDynTree::Transform stand-in (blf/spatial.h). */
+using Transform = blf::Transform;
 
 enum class ContactType
 {

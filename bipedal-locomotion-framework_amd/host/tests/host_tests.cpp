@@ -3,7 +3,9 @@
  * The reference's Catch2 tests for the DCM path, restated against the C++ adapters:
  *   ContactListTest.cpp:28-118, ContactPhaseListTest.cpp:15-153, VariablesHandlerTest.cpp:15-35
  *   (host bookkeeping, run everywhere), IntegratorTest.cpp:27-75 (device), a 2-D
- *   ConvexHullHelperTest (device), the QuinticSpline and TimeVaryingDCMPlanner::advance (device).
+ *   ConvexHullHelperTest (device), the QuinticSpline and TimeVaryingDCMPlanner::advance (device),
+ *   ContinousContactModelTest.cpp:30-214 (device) and FloatingBaseSystemKinematics under
+ *   ForwardEuler (device).
  * usage: blf_host_tests [cpu|gpu|all]   (exit status = number of failed checks)
  */
 #include <cmath>
@@ -15,12 +17,16 @@
 #include <string>
 #include <vector>
 
+#include <random>
+
+#include <BipedalLocomotion/ContactModels/ContinuousContactModel.h>
 #include <BipedalLocomotion/ParametersHandler/IParametersHandler.h>
 #include <BipedalLocomotion/Planners/ContactList.h>
 #include <BipedalLocomotion/Planners/ContactPhaseList.h>
 #include <BipedalLocomotion/Planners/ConvexHullHelper.h>
 #include <BipedalLocomotion/Planners/QuinticSpline.h>
 #include <BipedalLocomotion/Planners/TimeVaryingDCMPlanner.h>
+#include <BipedalLocomotion/System/FloatingBaseSystemKinematics.h>
 #include <BipedalLocomotion/System/ForwardEuler.h>
 #include <BipedalLocomotion/System/LinearTimeInvariantSystem.h>
 #include <BipedalLocomotion/System/VariablesHandler.h>
@@ -345,6 +351,182 @@ static void testPlanner()
     }
 }
 
+
+// ---- ContinousContactModelTest.cpp:30-214 ------------------------------------------------------
+static blf::Matrix3 rpy(double r, double p, double y)   // iDynTree Rotation::RPY = Rz(y) Ry(p) Rx(r)
+{
+    const double cr = std::cos(r), sr = std::sin(r), cp = std::cos(p), sp = std::sin(p);
+    const double cy = std::cos(y), sy = std::sin(y);
+    return {{cy * cp, cy * sp * sr - sy * cr, cy * sp * cr + sy * sr,
+             sy * cp, sy * sp * sr + cy * cr, sy * sp * cr - cy * sr,
+             -sp, cp * sr, cp * cr}};
+}
+
+static blf::Matrix3 expSkew(const blf::Vector3& v)   // Rodrigues
+{
+    const double th = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    blf::Matrix3 K{{0, -v[2], v[1], v[2], 0, -v[0], -v[1], v[0], 0}}, K2{}, R{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) K2[3 * i + j] += K[3 * i + k] * K[3 * k + j];
+    const double a = th > 0 ? std::sin(th) / th : 1.0, b = th > 0 ? (1 - std::cos(th)) / (th * th) : 0.5;
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + a * K[i] + b * K2[i];
+    return R;
+}
+
+static blf::Matrix3 matmul(const blf::Matrix3& A, const blf::Matrix3& B)
+{
+    blf::Matrix3 C{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) C[3 * i + j] += A[3 * i + k] * B[3 * k + j];
+    return C;
+}
+
+static void testContinuousContact()
+{
+    using ContactModels::ContinuousContactModel;
+    blf::Transform world_T_link;
+    world_T_link.rotation = rpy(-0.15, 0.2, 0.1);
+    world_T_link.position = {{-0.02, 0.01, 0.005}};
+    const blf::Transform nullForceTransform = blf::Transform::Identity();
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<double> u(-1.0, 1.0);
+    blf::Twist linkVelocity;
+    for (auto& x : linkVelocity) x = u(rng);
+    constexpr double springCoeff = 2000.0, damperCoeff = 100.0, length = 0.12, width = 0.09;
+    auto handler = std::make_shared<ParametersHandler::StdImplementation>();
+    handler->setParameter("spring_coeff", springCoeff);
+    handler->setParameter("damper_coeff", damperCoeff);
+    handler->setParameter("length", length);
+    handler->setParameter("width", width);
+
+    ContinuousContactModel model;
+    REQUIRE(model.initialize(handler));
+    model.setState(linkVelocity, world_T_link);
+    model.setNullForceTransform(nullForceTransform);
+
+    {   // "Test contact wrench": Monte Carlo integral of the point forces, tol 1e-2
+        std::default_random_engine generator;
+        generator.seed(42);
+        std::uniform_real_distribution<double> xAxis(-length / 2, length / 2), yAxis(-width / 2, width / 2);
+        const unsigned samples = 10000;
+        std::vector<double> pts(2 * samples), f, t;
+        for (unsigned i = 0; i < samples; ++i)
+        {
+            pts[2 * i] = xAxis(generator);
+            pts[2 * i + 1] = yAxis(generator);
+        }
+        REQUIRE(model.getWrenchesAtPoints(pts, f, t));
+        const double scale = length * width * std::abs(world_T_link.rotation[8]) / samples;
+        const blf::Wrench& w = model.getContactWrench();
+        for (int i = 0; i < 3; ++i)
+        {
+            double F = 0.0, T = 0.0;
+            for (unsigned k = 0; k < samples; ++k) { F += f[3 * k + i]; T += t[3 * k + i]; }
+            REQUIRE(std::abs(F * scale - w[i]) <= 1e-2);
+            REQUIRE(std::abs(T * scale - w[3 + i]) <= 1e-2);
+        }
+        // single-point getters agree with the batched call
+        const blf::Vector3 f0 = model.getForceAtPoint(pts[0], pts[1]);
+        const blf::Vector3 t0 = model.getTorqueGeneratedAtPoint(pts[0], pts[1]);
+        for (int i = 0; i < 3; ++i) REQUIRE(f0[i] == f[i] && t0[i] == t[i]);
+        const blf::Vector3 out = model.getForceAtPoint(length, 0.0);
+        REQUIRE(out[0] == 0.0 && out[1] == 0.0 && out[2] == 0.0);
+    }
+    {   // "Test regressor", tol 1e-7
+        const blf::MatrixXd& reg = model.getRegressor();
+        const blf::Wrench& w = model.getContactWrench();
+        for (int i = 0; i < 6; ++i)
+            REQUIRE(std::abs(reg(i, 0) * springCoeff + reg(i, 1) * damperCoeff - w[i]) <= 1e-7);
+    }
+    {   // cache protocol (ContactModel.cpp:12-92): cached until the state changes
+        const blf::Wrench w1 = model.getContactWrench();
+        const blf::Wrench* p1 = &model.getContactWrench();
+        REQUIRE(p1 == &model.getContactWrench() && *p1 == w1);
+        blf::Twist other = linkVelocity;
+        other[0] += 0.5;
+        model.setState(other, world_T_link);
+        REQUIRE(model.getContactWrench()[0] != w1[0]);
+        model.setState(linkVelocity, world_T_link);
+        REQUIRE(model.getContactWrench() == w1);
+        model.damperCoeff() = 0.0;           // the accessors do not invalidate (as the reference)
+        REQUIRE(model.getContactWrench() == w1);
+        model.setNullForceTransform(nullForceTransform);
+        REQUIRE(model.getContactWrench()[0] != w1[0]);
+        model.damperCoeff() = damperCoeff;
+        model.setNullForceTransform(nullForceTransform);
+    }
+    {   // "Test contact dynamics": FD of the wrench vs autonomous + control * acc, tol 1e-4
+        const double h = 1e-6;
+        blf::Vector6 acc;
+        acc.fill(1.0);
+        blf::Vector6 rate = model.getAutonomousDynamics();
+        const blf::Matrix6x6& C = model.getControlMatrix();
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) rate[i] += C[6 * i + j] * acc[j];
+        blf::Wrench w[2];
+        for (int s = 0; s < 2; ++s)
+        {
+            const double sg = s == 0 ? -1.0 : 1.0;
+            blf::Transform T = world_T_link;
+            for (int i = 0; i < 3; ++i) T.position[i] += sg * linkVelocity[i] * h;
+            T.rotation = matmul(expSkew({{sg * linkVelocity[3] * h, sg * linkVelocity[4] * h,
+                                          sg * linkVelocity[5] * h}}), world_T_link.rotation);
+            blf::Twist v = linkVelocity;
+            for (int i = 0; i < 6; ++i) v[i] += sg * acc[i] * h;
+            model.setState(v, T);
+            model.setNullForceTransform(nullForceTransform);
+            w[s] = model.getContactWrench();
+        }
+        for (int i = 0; i < 6; ++i) REQUIRE(std::abs((w[1][i] - w[0][i]) / (2 * h) - rate[i]) <= 1e-4);
+    }
+    {   // missing parameter
+        auto bad = std::make_shared<ParametersHandler::StdImplementation>();
+        bad->setParameter("length", length);
+        ContinuousContactModel m2;
+        REQUIRE_FALSE(m2.initialize(bad));
+    }
+}
+
+// ---- FloatingBaseSystemKinematics under ForwardEuler (FloatingBaseSystemKinematics.cpp:36-73) ---
+static void testFloatingBaseKinematics()
+{
+    auto system = std::make_shared<FloatingBaseSystemKinematics>();
+    auto handler = std::make_shared<ParametersHandler::StdImplementation>();
+    handler->setParameter("rho", 0.01);
+    REQUIRE(system->initalize(handler));
+    const blf::Matrix3 R0 = rpy(0.1, -0.2, 0.3);
+    blf::VectorXd s(24, 0.0), sd(24, 0.0);
+    for (int i = 0; i < 24; ++i) sd[i] = 0.1 * i - 1.0;
+    const blf::Vector6 twist{{0.1, -0.2, 0.05, 0.3, -0.1, 0.2}};
+    REQUIRE(system->setState({blf::Vector3{{0.0, 0.0, 0.53}}, R0, s}));
+    REQUIRE(system->setControlInput({twist, sd}));
+    FloatingBaseSystemKinematics::StateDerivativeType dx;
+    REQUIRE(system->dynamics(0.0, dx));
+    const auto& [dp, dR, ds] = dx;
+    const blf::Matrix3 W{{0, -twist[5], twist[4], twist[5], 0, -twist[3], -twist[4], twist[3], 0}};
+    const blf::Matrix3 WR = matmul(W, R0);
+    for (int i = 0; i < 3; ++i) REQUIRE(dp[i] == twist[i]);
+    for (int i = 0; i < 9; ++i) REQUIRE(std::abs(dR[i] - WR[i]) < 1e-14);   // orthonormal R
+    for (int i = 0; i < 24; ++i) REQUIRE(ds[i] == sd[i]);
+
+    ForwardEuler<FloatingBaseSystemKinematics> integrator(1e-4);
+    REQUIRE(integrator.setDynamicalSystem(system));
+    const double T = 0.5;
+    for (int k = 0; k < 5; ++k) REQUIRE(integrator.integrate(0.1 * k, 0.1 * (k + 1)));
+    const auto& [p, R, q] = integrator.getSolution();
+    // the stale-time last step adds one dT per call: t_eff = T + 5 dT
+    const double te = T + 5 * 1e-4;
+    REQUIRE(std::abs(p[2] - (0.53 + twist[2] * te)) < 1e-12);
+    REQUIRE(std::abs(q[23] - sd[23] * te) < 1e-12);
+    const blf::Matrix3 Rex = matmul(expSkew({{twist[3] * te, twist[4] * te, twist[5] * te}}), R0);
+    for (int i = 0; i < 9; ++i) REQUIRE(std::abs(R[i] - Rex[i]) < 1e-4);
+    // wrong sizes
+    REQUIRE(system->setControlInput({twist, blf::VectorXd(3, 0.0)}));
+    REQUIRE_FALSE(system->dynamics(0.0, dx));
+}
+
 int main(int argc, char** argv)
 {
     const std::string which = argc > 1 ? argv[1] : "all";
@@ -359,6 +541,8 @@ int main(int argc, char** argv)
         {"Convex Hull helper (2-D)", true, testConvexHull},
         {"QuinticSpline", true, testQuinticSpline},
         {"TimeVaryingDCMPlanner advance", true, testPlanner},
+        {"Continuous Contact", true, testContinuousContact},
+        {"FloatingBaseSystemKinematics", true, testFloatingBaseKinematics},
     };
     for (const auto& t : tests)
     {

@@ -20,6 +20,15 @@
  *   blf_hull2d_contains       Planners/src/ConvexHullHelper.cpp:101-117 (doesPointBelongToConvexHull)
  *   blf_quintic_fit/_eval     ABSENT in the reference (QuinticSpline); knot rule
  *                             of Planners/src/ContactList.cpp:190-202 (getPresentContact, `<=`)
+ *   blf_contact_model_eval    ContactModels/src/ContinuousContactModel.cpp:79-171, 223-254 behind the
+ *                             lazy getters of ContactModels/src/ContactModel.cpp:12-92
+ *                             (getContactWrench / getAutonomousDynamics / getControlMatrix /
+ *                             getRegressor)
+ *   blf_contact_point_wrench  ContinuousContactModel.cpp:173-221 (getForceAtPoint,
+ *                             getTorqueGeneratedAtPoint)
+ *   blf_fbk_dynamics          System/src/FloatingBaseSystemKinematics.cpp:36-73
+ *   blf_fbk_euler_integrate   ForwardEuler<FloatingBaseSystemKinematics>::integrate
+ *                             (FixedStepIntegrator.tpp:21-72 + ForwardEuler.tpp:18-49)
  *   blf_dcm_mpc_solve         ABSENT in the reference (TimeVaryingDCMPlanner QP),
  *                             driven through System/Advanceable.h:24-46 (advance()) by the C++ host
  *                             adapter blf::Planners::TimeVaryingDCMPlanner
@@ -167,6 +176,47 @@ void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
                              const blf_dcm_mpc_problem* problem, int64_t batch,
                              const blf_dcm_mpc_solution* solution, void* stream);
+
+/* ---- 6. Contact model (ContinuousContactModel), batched ------------------------------------
+ * Rectangular L x W patch, spring k, damper b (ContinuousContactModel.h:22-57).
+ * params: [B][4] = {length, width, spring_coeff, damper_coeff} (or one shared [4] when
+ * shared_params != 0); twist: [B][6] = {v, w} in mixed representation; pose, null_pose:
+ * [B][12] = {p[3], R[9] row-major} (world_T_link and the null-force transform).
+ * Outputs (NULL = not computed): wrench [B][6] = {force, torque}; autonomous [B][6] and
+ * control [B][36] (6x6 row-major), with d(wrench)/dt = autonomous + control * (dv, dw);
+ * regressor [B][12] (6x2 row-major), wrench = regressor * (k, b).
+ * As the reference: the wrench and the regressor scale by |R22|, the autonomous dynamics and
+ * the control matrix by R22 (no abs, ContinuousContactModel.cpp:127-170).                   */
+blf_status blf_contact_model_eval(blf_handle* handle, const double* params, int32_t shared_params,
+                                  const double* twist, const double* pose,
+                                  const double* null_pose, int64_t batch, double* wrench,
+                                  double* autonomous, double* control, double* regressor,
+                                  void* stream);
+
+/* Force and torque (about the contact frame origin) generated at Q points (x, y) of each contact
+ * surface: points [B][Q][2] -> force, torque [B][Q][3]; zero outside the rectangle.           */
+blf_status blf_contact_point_wrench(blf_handle* handle, const double* params,
+                                    int32_t shared_params, const double* twist, const double* pose,
+                                    const double* null_pose, int64_t batch, const double* points,
+                                    int32_t npoints, double* force, double* torque, void* stream);
+
+/* ---- 7. Floating-base kinematics (FloatingBaseSystemKinematics), batched -------------------
+ * State (p [B][3], R [B][9] row-major, s [B][ndof]); input (twist [B][6] mixed, s_dot [B][ndof]):
+ *   dp = v,  dR = -R.colwise().cross(w) + rho/2 ((R R^T)^{-1} - I) R,  ds = s_dot
+ * (Baumgarte parameter rho, default 0.01 in the reference).  ndof <= BLF_FBK_MAX_DOFS.      */
+#define BLF_FBK_MAX_DOFS 64
+blf_status blf_fbk_dynamics(blf_handle* handle, int32_t ndof, double rho, const double* rot,
+                            const double* twist, const double* joint_vel, double* dpos,
+                            double* drot, double* djoints, int64_t batch, void* stream);
+
+/* ForwardEuler<FloatingBaseSystemKinematics>::integrate(t0, T) with the inputs held constant:
+ * the step schedule and error codes of blf_lti_euler_integrate; every step updates each state
+ * element x += dx * dT_i (no re-projection onto SO(3), as ForwardEuler.tpp:37-45).
+ * pos, rot, joints are updated in place.                                                      */
+blf_status blf_fbk_euler_integrate(blf_handle* handle, int32_t ndof, double rho, double* pos,
+                                   double* rot, double* joints, const double* twist,
+                                   const double* joint_vel, int64_t batch, double initial_time,
+                                   double final_time, double dT, void* stream);
 
 /* Algorithmic flop count of one IPM iteration of one problem (what the fp64 roofline field
  * of bench.py is computed from); `active_facets` = sum_k nfacets[k]. */

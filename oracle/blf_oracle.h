@@ -21,6 +21,9 @@
  *   orc_hull2d_contains      Planners/src/ConvexHullHelper.cpp:101-117
  *   orc_quintic_*            ABSENT in the reference: parity unpinned against the
  *                            reference; pinned by boundary-condition identities + sympy fixtures
+ *   orc_contact_* / orc_fbk_* blf_oracle_contact.c: ContinuousContactModel.cpp:79-254 and
+ *                            FloatingBaseSystemKinematics.cpp:36-73 (config 5 rows), pinned by the
+ *                            properties of ContactModels/tests/ContinousContactModelTest.cpp
  *   orc_dcm_mpc_solve        ABSENT in the reference: parity unpinned against the
  *                            reference; pinned by an independent dense KKT solve (iteratively
  *                            refined) of the same QP in tests/test_oracle_dcm_mpc.py
@@ -85,6 +88,25 @@ void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threa
 /* Tree sum with the device's reduction order: c has n entries, padded with
  * zeros to 64*ceil(n/64); per 64-block xor-butterfly, then block sums left to right. */
 double orc_wave_tree_sum(const double* c, int n);
+
+/* ContinuousContactModel (one contact).  prm = {length, width, spring_coeff, damper_coeff};
+ * twist = {v[3], w[3]} (mixed); pose / null_pose = {p[3], R[9] row-major}.  Outputs (NULL to skip):
+ * wrench[6] = {force, torque}, autonomous[6], control[36] (6x6 row-major), regressor[12] (6x2). */
+void orc_contact_eval(const double* prm, const double* twist, const double* pose,
+                      const double* null_pose, double* wrench, double* autonomous,
+                      double* control, double* regressor);
+/* getForceAtPoint / getTorqueGeneratedAtPoint at (x, y) of the contact surface. */
+void orc_contact_point(const double* prm, const double* twist, const double* pose,
+                       const double* null_pose, double x, double y, double* force, double* torque);
+/* FloatingBaseSystemKinematics::dynamics: rot[9] row-major, twist[6] mixed, joint_vel[n];
+ * outputs dpos[3], drot[9], djoints[n]. */
+void orc_fbk_dynamics(int n, double rho, const double* rot, const double* twist,
+                      const double* joint_vel, double* dpos, double* drot, double* djoints);
+/* ForwardEuler<FloatingBaseSystemKinematics>::integrate(t0, t1) with constant inputs; the state
+ * (pos[3], rot[9], joints[n], n <= 64) is updated in place.  Returns 0 or a BLF_ERR_* code. */
+int orc_fbk_euler_integrate(int n, double rho, double* pos, double* rot, double* joints,
+                            const double* twist, const double* joint_vel, double t0, double t1,
+                            double dT);
 
 #ifdef __cplusplus
 }

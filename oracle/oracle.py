@@ -61,6 +61,15 @@ def lib():
                                               _dp, _dp, _ip, _ip]
         L.orc_wave_tree_sum.restype = ctypes.c_double
         L.orc_wave_tree_sum.argtypes = [_dp, ctypes.c_int]
+        L.orc_contact_eval.argtypes = [_dp] * 8
+        L.orc_contact_point.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_double, ctypes.c_double,
+                                        _dp, _dp]
+        L.orc_fbk_dynamics.argtypes = [ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp, _dp,
+                                       _dp]
+        L.orc_fbk_euler_integrate.restype = ctypes.c_int
+        L.orc_fbk_euler_integrate.argtypes = [ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp,
+                                              _dp, ctypes.c_double, ctypes.c_double,
+                                              ctypes.c_double]
         _LIB = L
     return _LIB
 
@@ -218,3 +227,53 @@ def assemble_constraints(prob, max_facets=8):
     out = dict(prob)
     out.update(A=A, b=b, nfacets=m)
     return out
+
+
+# ---- config 5: ContinuousContactModel and FloatingBaseSystemKinematics ----------------------
+def contact_eval(prm, twist, pose, null_pose):
+    """One contact: returns wrench[6], autonomous[6], control[6,6], regressor[6,2]."""
+    prm, twist, pose, null_pose = _f64(prm), _f64(twist), _f64(pose), _f64(null_pose)
+    w, a, c, r = np.zeros(6), np.zeros(6), np.zeros(36), np.zeros(12)
+    lib().orc_contact_eval(_d(prm), _d(twist), _d(pose), _d(null_pose), _d(w), _d(a), _d(c),
+                           _d(r))
+    return w, a, c.reshape(6, 6), r.reshape(6, 2)
+
+
+def contact_eval_batch(prm, twist, pose, null_pose):
+    """Batched: prm [B,4] (or [4]), twist [B,6], pose / null_pose [B,12]."""
+    B = twist.shape[0]
+    prm = np.broadcast_to(_f64(prm), (B, 4))
+    out = [np.zeros((B, 6)), np.zeros((B, 6)), np.zeros((B, 6, 6)), np.zeros((B, 6, 2))]
+    for q in range(B):
+        res = contact_eval(prm[q], twist[q], pose[q], null_pose[q])
+        for o, r in zip(out, res):
+            o[q] = r
+    return out
+
+
+def contact_point(prm, twist, pose, null_pose, x, y):
+    prm, twist, pose, null_pose = _f64(prm), _f64(twist), _f64(pose), _f64(null_pose)
+    f, t = np.zeros(3), np.zeros(3)
+    lib().orc_contact_point(_d(prm), _d(twist), _d(pose), _d(null_pose), float(x), float(y),
+                            _d(f), _d(t))
+    return f, t
+
+
+def fbk_dynamics(rho, rot, twist, joint_vel):
+    rot, twist, joint_vel = _f64(rot), _f64(twist), _f64(joint_vel)
+    n = joint_vel.shape[0]
+    dp, dR, dq = np.zeros(3), np.zeros(9), np.zeros(max(n, 1))
+    lib().orc_fbk_dynamics(n, rho, _d(rot.reshape(-1)), _d(twist), _d(joint_vel if n else np.zeros(1)),
+                           _d(dp), _d(dR), _d(dq))
+    return dp, dR.reshape(3, 3), dq[:n]
+
+
+def fbk_euler_integrate(rho, pos, rot, joints, twist, joint_vel, t0, t1, dT):
+    pos, rot, joints = _f64(pos).copy(), _f64(rot).reshape(-1).copy(), _f64(joints).copy()
+    twist, joint_vel = _f64(twist), _f64(joint_vel)
+    n = joints.shape[0]
+    jz = joints if n else np.zeros(1)
+    jv = joint_vel if n else np.zeros(1)
+    st = lib().orc_fbk_euler_integrate(n, rho, _d(pos), _d(rot), _d(jz), _d(twist), _d(jv),
+                                       t0, t1, dT)
+    return st, pos, rot.reshape(3, 3), joints

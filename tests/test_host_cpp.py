@@ -1,6 +1,7 @@
 """Runs the C++17 adapter tests (bipedal-locomotion-framework_amd/host/tests/host_tests.cpp):
 the reference's Catch2 tests for ContactList, ContactPhaseList and VariablesHandler on the host,
-and the device-backed IntegratorTest / ConvexHullHelper / QuinticSpline / planner cases."""
+and the device-backed IntegratorTest / ConvexHullHelper / QuinticSpline / planner /
+ContinousContactModelTest / FloatingBaseSystemKinematics cases."""
 import os
 import subprocess
 
@@ -34,5 +35,6 @@ def test_host_bookkeeping_tests():
 def test_host_device_tests():
     out = _run("gpu")
     for name in ("Integrator - Linear system", "Convex Hull helper (2-D)", "QuinticSpline",
-                 "TimeVaryingDCMPlanner advance"):
+                 "TimeVaryingDCMPlanner advance", "Continuous Contact",
+                 "FloatingBaseSystemKinematics"):
         assert any(line.startswith(name) and line.rstrip().endswith("ok") for line in out.splitlines()), out
