@@ -24,12 +24,32 @@ EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
             "blf_hull2d_contains", "blf_quintic_fit", "blf_quintic_eval",
             "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_flops_per_iter",
             "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
-            "blf_fbk_euler_integrate"]
+            "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate"]
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
 _f64 = ctypes.c_double
+
+
+class FbModel(ctypes.Structure):
+    """blf_fb_model (include/blf/blf_c.h); every pointer is device memory."""
+    _fields_ = [("ndof", _i32), ("nframes", _i32), ("parent", _vp), ("joint_origin", _vp),
+                ("joint_rot", _vp), ("joint_axis", _vp), ("link_mass", _vp), ("link_com", _vp),
+                ("link_inertia", _vp), ("frame_link", _vp), ("frame_pose", _vp),
+                ("gravity", _f64 * 3), ("rho", _f64)]
+
+
+class FbState(ctypes.Structure):
+    _fields_ = [("base_vel", _vp), ("joint_vel", _vp), ("base_pos", _vp), ("base_rot", _vp),
+                ("joint_pos", _vp)]
+
+
+class FbContacts(ctypes.Structure):
+    _fields_ = [("ncontacts", _i32), ("frame", _vp), ("params", _vp), ("null_pose", _vp)]
+
+
+FB_STATE_KEYS = ("base_vel", "joint_vel", "base_pos", "base_rot", "joint_pos")
 
 
 class BlfError(RuntimeError):
@@ -89,6 +109,12 @@ def lib():
         L.blf_fbk_dynamics.argtypes = [_vp, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]
         L.blf_fbk_euler_integrate.argtypes = [_vp, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _i64,
                                               _f64, _f64, _f64, _vp]
+        L.blf_fbd_dynamics.argtypes = [_vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), _vp,
+                                       ctypes.POINTER(FbContacts), _vp, _i64,
+                                       ctypes.POINTER(FbState), _vp]
+        L.blf_fbd_euler_integrate.argtypes = [_vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState),
+                                              _vp, ctypes.POINTER(FbContacts), _vp, _i64, _f64,
+                                              _f64, _f64, _vp]
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         for name in EXPORTED:
             if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
@@ -381,3 +407,86 @@ class Handle:
             _ptr(joint_vel, torch.float64, (B, n), "joint_vel") if n else None,
             B, float(t0), float(t1), float(dT), _stream(stream)))
         return pos, rot, joints
+
+    # ---- config 5: floating-base dynamics ------------------------------------------------------
+    def fb_model(self, model, rho=0.01, gravity=(0.0, 0.0, -9.81)):
+        """Upload a blf/robot.py model; returns an object keeping the device arrays alive."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+
+        class _M:
+            pass
+        dm = _M()
+        f64 = lambda a: torch.as_tensor(a, dtype=torch.float64).contiguous().to(dev)
+        i32 = lambda a: torch.as_tensor(a, dtype=torch.int32).contiguous().to(dev)
+        dm.t = dict(parent=i32(model["parent"]), joint_origin=f64(model["joint_origin"]),
+                    joint_rot=f64(model["joint_rot"]), joint_axis=f64(model["joint_axis"]),
+                    link_mass=f64(model["link_mass"]), link_com=f64(model["link_com"]),
+                    link_inertia=f64(model["link_inertia"]), frame_link=i32(model["frame_link"]),
+                    frame_pose=f64(model["frame_pose"]))
+        c = FbModel()
+        c.ndof = int(model["n"])
+        c.nframes = int(len(model["frame_link"]))
+        for k, v in dm.t.items():
+            setattr(c, k, _vp(v.data_ptr()))
+        for i in range(3):
+            c.gravity[i] = gravity[i]
+        c.rho = rho
+        dm.c = c
+        dm.n = c.ndof
+        return dm
+
+    def _fb_state(self, st, B, n):
+        torch = _torch()
+        shapes = dict(base_vel=(B, 6), joint_vel=(B, n), base_pos=(B, 3), base_rot=(B, 3, 3),
+                      joint_pos=(B, n))
+        c = FbState()
+        for k in FB_STATE_KEYS:
+            setattr(c, k, _ptr(st[k], torch.float64, shapes[k], k))
+        return c
+
+    def _fb_contacts(self, contacts, B):
+        torch = _torch()
+        c = FbContacts()
+        if not contacts:
+            c.ncontacts = 0
+            return c
+        C = contacts["frame"].shape[0]
+        c.ncontacts = C
+        c.frame = _ptr(contacts["frame"], torch.int32, (C,), "frame")
+        c.params = _ptr(contacts["params"], torch.float64, (C, 4), "params")
+        c.null_pose = _ptr(contacts["null_pose"], torch.float64, (B, C, 12), "null_pose")
+        return c
+
+    def fbd_dynamics(self, dm, state, torque, contacts=None, mass_reg=None, stream=None):
+        """FloatingBaseDynamicalSystem::dynamics for a batch.  state: dict of device tensors
+        (base_vel [B,6], joint_vel [B,n], base_pos [B,3], base_rot [B,3,3], joint_pos [B,n]);
+        torque [B,n]; contacts: dict(frame [C] int32, params [C,4], null_pose [B,C,12]).
+        Returns the derivative with the same keys (base_vel -> base acceleration, ...)."""
+        torch = _torch()
+        B, n = state["joint_pos"].shape
+        out = {k: torch.empty_like(state[k]) for k in FB_STATE_KEYS}
+        NV = n + 6
+        reg = _ptr(mass_reg, torch.float64, (NV, NV), "mass_reg") if mass_reg is not None else None
+        st, oc = self._fb_state(state, B, n), self._fb_state(out, B, n)
+        ct = self._fb_contacts(contacts, B)
+        _check(lib().blf_fbd_dynamics(self._h, ctypes.byref(dm.c), ctypes.byref(st),
+                                      _ptr(torque, torch.float64, (B, n), "torque"),
+                                      ctypes.byref(ct), reg, B, ctypes.byref(oc),
+                                      _stream(stream)))
+        return out
+
+    def fbd_euler_integrate(self, dm, state, torque, t0, t1, dT, contacts=None, mass_reg=None,
+                            stream=None):
+        """ForwardEuler<FloatingBaseDynamicalSystem>::integrate in place on `state`."""
+        torch = _torch()
+        B, n = state["joint_pos"].shape
+        NV = n + 6
+        reg = _ptr(mass_reg, torch.float64, (NV, NV), "mass_reg") if mass_reg is not None else None
+        st = self._fb_state(state, B, n)
+        ct = self._fb_contacts(contacts, B)
+        _check(lib().blf_fbd_euler_integrate(self._h, ctypes.byref(dm.c), ctypes.byref(st),
+                                             _ptr(torque, torch.float64, (B, n), "torque"),
+                                             ctypes.byref(ct), reg, B, float(t0), float(t1),
+                                             float(dT), _stream(stream)))
+        return state

@@ -1,0 +1,100 @@
+"""Synthetic floating-base robot models for the config-5 closed loop (BASELINE.json configs[4]:
+"30-DoF": a 6-DoF floating base + 24 revolute joints).
+
+The reference obtains the rigid-body terms from iDynTree KinDynComputations on a URDF model
+(src/System/src/FloatingBaseSystemDynamics.cpp:163-206); neither iDynTree nor a robot description
+ships here, so the model is a synthetic humanoid-like kinematic tree with randomised but physical
+link masses and inertias (seeded).  Layout, consumed by blf_fbd_* (include/blf/blf_c.h) and by the
+test oracle:
+
+  parent       [n]      int32   parent LINK of joint j (link 0 = base); joint j moves link j + 1;
+                                parent[j] <= j (topological order)
+  joint_origin [n][3]           joint frame origin in the parent link frame
+  joint_rot    [n][3][3]        fixed rotation parent link -> joint frame
+  joint_axis   [n][3]           unit rotation axis in the joint frame (= child link frame at q=0)
+  link_mass    [n+1]
+  link_com     [n+1][3]         centre of mass in the link frame
+  link_inertia [n+1][3][3]      rotational inertia about the COM, link frame (SPD)
+  frame_link   [F]      int32   link a frame is attached to
+  frame_pose   [F][12]          (p, R row-major) of the frame in its link frame
+"""
+import numpy as np
+
+# (name, parent link name, origin in parent, axis) of the 24 joints
+_TREE = [
+    # left leg (hip yaw/roll/pitch, knee, ankle pitch/roll)
+    ("l_hip_yaw", "base", (0.0, 0.09, -0.06), "z"), ("l_hip_roll", "l_hip_yaw", (0, 0, -0.03), "x"),
+    ("l_hip_pitch", "l_hip_roll", (0, 0, 0), "y"), ("l_knee", "l_hip_pitch", (0, 0, -0.22), "y"),
+    ("l_ankle_pitch", "l_knee", (0, 0, -0.22), "y"), ("l_ankle_roll", "l_ankle_pitch", (0, 0, 0), "x"),
+    # right leg
+    ("r_hip_yaw", "base", (0.0, -0.09, -0.06), "z"), ("r_hip_roll", "r_hip_yaw", (0, 0, -0.03), "x"),
+    ("r_hip_pitch", "r_hip_roll", (0, 0, 0), "y"), ("r_knee", "r_hip_pitch", (0, 0, -0.22), "y"),
+    ("r_ankle_pitch", "r_knee", (0, 0, -0.22), "y"), ("r_ankle_roll", "r_ankle_pitch", (0, 0, 0), "x"),
+    # torso
+    ("torso_pitch", "base", (0.0, 0.0, 0.08), "y"), ("torso_roll", "torso_pitch", (0, 0, 0.04), "x"),
+    ("torso_yaw", "torso_roll", (0, 0, 0.04), "z"),
+    # arms
+    ("l_shoulder_pitch", "torso_yaw", (0.0, 0.14, 0.20), "y"),
+    ("l_shoulder_roll", "l_shoulder_pitch", (0, 0.02, 0), "x"),
+    ("l_shoulder_yaw", "l_shoulder_roll", (0, 0, -0.08), "z"), ("l_elbow", "l_shoulder_yaw", (0, 0, -0.10), "y"),
+    ("r_shoulder_pitch", "torso_yaw", (0.0, -0.14, 0.20), "y"),
+    ("r_shoulder_roll", "r_shoulder_pitch", (0, -0.02, 0), "x"),
+    ("r_shoulder_yaw", "r_shoulder_roll", (0, 0, -0.08), "z"), ("r_elbow", "r_shoulder_yaw", (0, 0, -0.10), "y"),
+    # neck
+    ("neck_pitch", "torso_yaw", (0.0, 0.0, 0.26), "y"),
+]
+_AXES = {"x": (1.0, 0.0, 0.0), "y": (0.0, 1.0, 0.0), "z": (0.0, 0.0, 1.0)}
+
+
+def _rotvec(v):
+    th = np.linalg.norm(v)
+    K = np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
+    if th == 0:
+        return np.eye(3)
+    return np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+
+
+def humanoid24(seed=2020):
+    """The synthetic 6 + 24 DoF model used by config 5, with sole frames on both ankle-roll links."""
+    rng = np.random.default_rng(seed)
+    names = ["base"] + [t[0] for t in _TREE]
+    n = len(_TREE)
+    parent = np.array([names.index(t[1]) for t in _TREE], dtype=np.int32)
+    joint_origin = np.array([t[2] for t in _TREE], dtype=np.float64)
+    # small fixed mounting rotations so the joint frames are not all aligned with the parent
+    joint_rot = np.stack([_rotvec(rng.normal(size=3) * 0.05) for _ in range(n)])
+    joint_axis = np.array([_AXES[t[3]] for t in _TREE], dtype=np.float64)
+    masses = rng.uniform(0.4, 3.0, n + 1)
+    masses[0] = 8.0                                          # pelvis / base
+    com = rng.normal(size=(n + 1, 3)) * 0.02
+    inertia = np.zeros((n + 1, 3, 3))
+    for l in range(n + 1):
+        Q = _rotvec(rng.normal(size=3))
+        d = rng.uniform(0.3, 1.0, 3) * masses[l] * 0.004
+        d[2] = min(d[2], d[0] + d[1] - 1e-6)                 # triangle inequality of principal moments
+        inertia[l] = Q @ np.diag(d) @ Q.T
+    feet = [names.index("l_ankle_roll"), names.index("r_ankle_roll")]   # names index = link index
+    frame_link = np.array(feet, dtype=np.int32)
+    frame_pose = np.zeros((2, 12))
+    for f in range(2):
+        frame_pose[f, :3] = (0.02, 0.0, -0.06)
+        frame_pose[f, 3:] = np.eye(3).reshape(-1)
+    return dict(n=n, parent=parent, joint_origin=joint_origin, joint_rot=joint_rot,
+                joint_axis=joint_axis, link_mass=masses, link_com=com, link_inertia=inertia,
+                frame_link=frame_link, frame_pose=frame_pose, names=names)
+
+
+def random_states(model, batch, seed=0, spread=0.3):
+    """Batch of floating-base states near a standing pose: base at 0.75 m, joints within
+    +-spread rad, velocities ~N(0, 0.5)."""
+    rng = np.random.default_rng(seed)
+    n = model["n"]
+    base_rot = np.stack([_rotvec(rng.normal(size=3) * 0.1) for _ in range(batch)])
+    return dict(
+        base_vel=rng.normal(size=(batch, 6)) * 0.5,
+        joint_vel=rng.normal(size=(batch, n)) * 0.5,
+        base_pos=np.column_stack([rng.normal(size=(batch, 2)) * 0.01, np.full(batch, 0.75)]),
+        base_rot=base_rot,
+        joint_pos=rng.uniform(-spread, spread, (batch, n)),
+        joint_torque=rng.normal(size=(batch, n)) * 5.0,
+    )

@@ -313,3 +313,64 @@ blf_status blf_fbk_euler_integrate(blf_handle* handle, int32_t ndof, double rho,
 }
 
 }  // extern "C"
+
+static blf_status check_fbd(const char* fn, blf_handle* handle, const blf_fb_model* model,
+                            const blf_fb_state* state, const double* tau,
+                            const blf_fb_contacts* contacts, int64_t batch)
+{
+    BLF_REQUIRE(handle != nullptr, "%s: null handle", fn);
+    BLF_REQUIRE(model != nullptr && state != nullptr, "%s: null model / state", fn);
+    BLF_REQUIRE(model->ndof >= 1 && model->ndof <= BLF_FBD_MAX_DOFS, "%s: ndof=%d outside [1, %d]",
+                fn, model->ndof, BLF_FBD_MAX_DOFS);
+    BLF_REQUIRE(batch >= 0, "%s: negative batch", fn);
+    BLF_REQUIRE(model->parent && model->joint_origin && model->joint_rot && model->joint_axis &&
+                    model->link_mass && model->link_com && model->link_inertia,
+                "%s: null model array", fn);
+    BLF_REQUIRE(batch == 0 || (state->base_vel && state->joint_vel && state->base_pos &&
+                               state->base_rot && state->joint_pos && tau),
+                "%s: null state buffer", fn);
+    const int C = contacts ? contacts->ncontacts : 0;
+    BLF_REQUIRE(C >= 0 && C <= BLF_FBD_MAX_CONTACTS, "%s: %d contacts outside [0, %d]", fn, C,
+                BLF_FBD_MAX_CONTACTS);
+    BLF_REQUIRE(C == 0 || (contacts->frame && contacts->params && contacts->null_pose &&
+                           model->frame_link && model->frame_pose && model->nframes > 0),
+                "%s: null contact buffer", fn);
+    if (fbd_lds_bytes(model->ndof, C) > 160 * 1024)
+        return set_error(BLF_ERR_UNSUPPORTED, "%s: model too large for one workgroup's LDS", fn);
+    return BLF_OK;
+}
+
+extern "C" {
+
+blf_status blf_fbd_dynamics(blf_handle* handle, const blf_fb_model* model,
+                            const blf_fb_state* state, const double* joint_torque,
+                            const blf_fb_contacts* contacts, const double* mass_reg,
+                            int64_t batch, const blf_fb_state* out, void* stream)
+{
+    blf_status st = check_fbd("blf_fbd_dynamics", handle, model, state, joint_torque, contacts, batch);
+    if (st != BLF_OK) return st;
+    BLF_REQUIRE(out != nullptr && (batch == 0 || (out->base_vel && out->joint_vel && out->base_pos &&
+                                                  out->base_rot && out->joint_pos)),
+                "blf_fbd_dynamics: null output buffer");
+    return launch_fbd_dynamics(model, state, joint_torque, contacts, mass_reg, batch, out,
+                               (hipStream_t)stream);
+}
+
+blf_status blf_fbd_euler_integrate(blf_handle* handle, const blf_fb_model* model,
+                                   const blf_fb_state* state, const double* joint_torque,
+                                   const blf_fb_contacts* contacts, const double* mass_reg,
+                                   int64_t batch, double initial_time, double final_time,
+                                   double dT, void* stream)
+{
+    blf_status st = check_fbd("blf_fbd_euler_integrate", handle, model, state, joint_torque,
+                              contacts, batch);
+    if (st != BLF_OK) return st;
+    int iterations = 0;
+    double dT_last = 0.0;
+    st = step_schedule(initial_time, final_time, dT, &iterations, &dT_last);
+    if (st != BLF_OK) return st;
+    return launch_fbd_euler(model, state, joint_torque, contacts, mass_reg, batch, iterations, dT,
+                            dT_last, (hipStream_t)stream);
+}
+
+}  // extern "C"

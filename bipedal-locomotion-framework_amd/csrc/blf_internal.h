@@ -56,6 +56,13 @@ blf_status launch_contact_point(const double* prm, int shared, const double* twi
 blf_status launch_fbk_dynamics(int n, double rho, const double* rot, const double* twist,
                                const double* joint_vel, double* dpos, double* drot,
                                double* djoints, int64_t batch, hipStream_t s);
+blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
+                               const blf_fb_contacts* ct, const double* reg, int64_t batch,
+                               const blf_fb_state* out, hipStream_t s);
+blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
+                            const blf_fb_contacts* ct, const double* reg, int64_t batch,
+                            int32_t nsteps, double dT, double dT_last, hipStream_t s);
+size_t fbd_lds_bytes(int n, int C);
 blf_status launch_fbk_euler(int n, double rho, double* pos, double* rot, double* joints,
                             const double* twist, const double* joint_vel, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s);

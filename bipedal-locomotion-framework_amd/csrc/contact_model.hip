@@ -9,19 +9,10 @@
 //    points per contact, one lane per (contact, point).
 // Built with -ffp-contract=off; every expression in the order of oracle/blf_oracle_contact.c.
 #include "blf_internal.h"
+#include "contact_math.h"
 
 namespace blf {
 namespace {
-
-struct V3 {
-    double x, y, z;
-};
-
-__device__ __forceinline__ V3 cross(V3 a, V3 b)
-{
-    return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
-}
-__device__ __forceinline__ double at(const V3& a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 
 // skew(e)^2 = e e^T - |e|^2 I, row-major
 __device__ __forceinline__ void skew2(V3 e, double* S)
@@ -62,16 +53,7 @@ __global__ __launch_bounds__(256) void contact_eval_kernel(
     const V3 t1 = cross(e1, r01), t2 = cross(e2, r02);
     const V3 c1 = cross(e1, w), c2 = cross(e2, w);
     const V3 u1 = cross(e1, c1), u2 = cross(e2, c2);   // skew(e) skew(e) w
-    if (wrench) {
-        const double cf = aR * area;
-        const double ct = aR * area / 12.0;
-        double* o = wrench + 6 * q;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            o[i] = cf * (k * (p0[i] - p[i]) - b * v[i]);
-            o[3 + i] = ct * (LL * (b * at(u1, i) + k * at(t1, i)) + WW * (b * at(u2, i) + k * at(t2, i)));
-        }
-    }
+    if (wrench) contact_wrench(pr, tw, ps, ns, wrench + 6 * q);
     if (autonomous) {
         const V3 rd2 = cross(w, V3{R[2], R[5], R[8]});   // (skew(w) R) e3
         const V3 ed1 = cross(w, e1), ed2 = cross(w, e2);

@@ -54,6 +54,9 @@ public:
     bool getWrenchesAtPoints(const std::vector<double>& points, std::vector<double>& force,
                              std::vector<double>& torque);
 
+    const double& length() const { return m_length; }
+    const double& width() const { return m_width; }
+    const blf::Transform& nullForceTransform() const { return m_nullForceTransform; }
     const double& springCoeff() const { return m_springCoeff; }
     double& springCoeff() { return m_springCoeff; }
     const double& damperCoeff() const { return m_damperCoeff; }

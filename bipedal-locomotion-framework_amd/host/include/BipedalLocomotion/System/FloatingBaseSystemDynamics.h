@@ -1,0 +1,88 @@
+/**
+ * @file FloatingBaseSystemDynamics.h
+ * Drop-in for src/System/include/BipedalLocomotion/System/FloatingBaseSystemDynamics.h:30-157
+ * (src/System/src/FloatingBaseSystemDynamics.cpp):
+ *   state      (base velocity (mixed), joint velocities, base position, base orientation,
+ *               joint positions)
+ *   input      (joint torques, contact wrenches)
+ *   derivative (base acceleration, joint accelerations, base linear velocity, base rotation rate,
+ *               joint velocities)
+ * The reference takes M, h and the frame Jacobians from iDynTree KinDynComputations, set with
+ * setKinDyn(); this build has no iDynTree, so the robot is given as a kinematic tree with
+ * setRobotModel() (blf::RobotModel, the layout of blf/robot.py) and the rigid-body terms are
+ * computed on the device (blf_fbd_dynamics / blf_fbd_euler_integrate, include/blf/blf_c.h).
+ * Contacts must be ContinuousContactModel instances (their formula is evaluated in the kernel).
+ * Divergence: the contact models are not left in the frame state after dynamics() (the reference
+ * calls contactModel->setState as a side effect, FloatingBaseSystemDynamics.cpp:225-226).
+ */
+#ifndef BLF_BIPEDAL_LOCOMOTION_SYSTEM_FLOATING_BASE_SYSTEM_DYNAMICS_H
+#define BLF_BIPEDAL_LOCOMOTION_SYSTEM_FLOATING_BASE_SYSTEM_DYNAMICS_H
+
+#include <tuple>
+#include <vector>
+
+#include <BipedalLocomotion/System/ContactWrench.h>
+#include <BipedalLocomotion/System/DynamicalSystem.h>
+#include <blf/dense.h>
+#include <blf/device.h>
+#include <blf/spatial.h>
+
+namespace blf
+{
+/** Kinematic tree of revolute joints on a floating base (see blf_fb_model in blf_c.h). */
+struct RobotModel
+{
+    int ndof{0};
+    std::vector<int32_t> parent;       /**< [n]        */
+    std::vector<double> jointOrigin;   /**< [n][3]     */
+    std::vector<double> jointRotation; /**< [n][9]     */
+    std::vector<double> jointAxis;     /**< [n][3]     */
+    std::vector<double> linkMass;      /**< [n+1]      */
+    std::vector<double> linkCom;       /**< [n+1][3]   */
+    std::vector<double> linkInertia;   /**< [n+1][9]   */
+    std::vector<int32_t> frameLink;    /**< [F]        */
+    std::vector<double> framePose;     /**< [F][12]    */
+};
+} // namespace blf
+
+namespace BipedalLocomotion
+{
+namespace System
+{
+
+class FloatingBaseDynamicalSystem
+    : public DynamicalSystem<
+          std::tuple<blf::Vector6, blf::VectorXd, blf::Vector3, blf::Matrix3, blf::VectorXd>,
+          std::tuple<blf::Vector6, blf::VectorXd, blf::Vector3, blf::Matrix3, blf::VectorXd>,
+          std::tuple<blf::VectorXd, std::vector<ContactWrench>>>
+{
+    static constexpr std::size_t m_baseDoFs = 6;
+    std::size_t m_actuatedDoFs{0};
+    double m_rho{0.01};
+    blf::Vector3 m_gravity{{0.0, 0.0, -9.81}};
+    bool m_hasModel{false};
+    bool m_useMassMatrixRegularizationTerm{false};
+    blf::RobotModel m_model;
+    blf::DeviceBuffer<int32_t> m_dParent, m_dFrameLink, m_dContactFrame;
+    blf::DeviceBuffer<double> m_dOrigin, m_dRot, m_dAxis, m_dMass, m_dCom, m_dInertia, m_dFramePose;
+    blf::DeviceBuffer<double> m_dReg, m_dState, m_dTau, m_dContactParams, m_dNullPose, m_dOut;
+
+    bool prepare(const char* where, blf_fb_model& model, blf_fb_state& state,
+                 blf_fb_contacts& contacts);
+
+public:
+    bool initalize(std::weak_ptr<ParametersHandler::IParametersHandler> handler) final;
+    void setGravityVector(const blf::Vector3& gravity) { m_gravity = gravity; }
+    /** Replaces setKinDyn(): the robot model whose rigid-body terms the device computes. */
+    bool setRobotModel(const blf::RobotModel& model);
+    bool setMassMatrixRegularization(const blf::MatrixXd& matrix);
+    bool dynamics(const double& time, StateDerivativeType& stateDerivative) final;
+
+    /** Device hook used by ForwardEuler<FloatingBaseDynamicalSystem>. */
+    bool forwardEulerIntegrate(double initialTime, double finalTime, double dT);
+};
+
+} // namespace System
+} // namespace BipedalLocomotion
+
+#endif

@@ -1,0 +1,232 @@
+/**
+ * @file FloatingBaseSystemDynamics.cpp
+ * Checks and messages follow src/System/src/FloatingBaseSystemDynamics.cpp:17-120; the dynamics
+ * (:102-251) run on the device through blf_fbd_dynamics / blf_fbd_euler_integrate.
+ */
+#include <iostream>
+
+#include <BipedalLocomotion/ContactModels/ContinuousContactModel.h>
+#include <BipedalLocomotion/System/FloatingBaseSystemDynamics.h>
+
+using namespace BipedalLocomotion::System;
+using namespace BipedalLocomotion::ParametersHandler;
+
+bool FloatingBaseDynamicalSystem::initalize(std::weak_ptr<IParametersHandler> handler)
+{
+    auto ptr = handler.lock();
+    if (ptr == nullptr)
+    {
+        std::cerr << "[FloatingBaseDynamicalSystem::initalize] The parameter handler is expired. "
+                     "Please call the function passing a pointer pointing an already allocated "
+                     "memory."
+                  << std::endl;
+        return false;
+    }
+    if (!ptr->getParameter("rho", m_rho))
+    {
+        std::cerr << "[FloatingBaseDynamicalSystem::initalize] Unable to load the Baumgarte "
+                     "stabilization parameter."
+                  << std::endl;
+        return false;
+    }
+    return true;
+}
+
+bool FloatingBaseDynamicalSystem::setRobotModel(const blf::RobotModel& model)
+{
+    const std::size_t n = static_cast<std::size_t>(model.ndof);
+    const std::size_t F = model.frameLink.size();
+    if (model.ndof < 1 || model.ndof > BLF_FBD_MAX_DOFS || model.parent.size() != n
+        || model.jointOrigin.size() != 3 * n || model.jointRotation.size() != 9 * n
+        || model.jointAxis.size() != 3 * n || model.linkMass.size() != n + 1
+        || model.linkCom.size() != 3 * (n + 1) || model.linkInertia.size() != 9 * (n + 1)
+        || model.framePose.size() != 12 * F)
+    {
+        std::cerr << "[FloatingBaseDynamicalSystem::setRobotModel] Corrupted robot model."
+                  << std::endl;
+        return false;
+    }
+    for (std::size_t j = 0; j < n; ++j)
+        if (model.parent[j] < 0 || model.parent[j] > static_cast<int32_t>(j))
+        {
+            std::cerr << "[FloatingBaseDynamicalSystem::setRobotModel] The joints must be in "
+                         "topological order (parent[j] <= j)."
+                      << std::endl;
+            return false;
+        }
+    m_model = model;
+    m_actuatedDoFs = n;
+    m_hasModel = m_dParent.upload(model.parent) && m_dOrigin.upload(model.jointOrigin)
+                 && m_dRot.upload(model.jointRotation) && m_dAxis.upload(model.jointAxis)
+                 && m_dMass.upload(model.linkMass) && m_dCom.upload(model.linkCom)
+                 && m_dInertia.upload(model.linkInertia) && m_dFrameLink.upload(model.frameLink)
+                 && m_dFramePose.upload(model.framePose);
+    return m_hasModel;
+}
+
+bool FloatingBaseDynamicalSystem::setMassMatrixRegularization(const blf::MatrixXd& matrix)
+{
+    if (!m_hasModel)
+    {
+        std::cerr << "[FloatingBaseDynamicalSystem::setMassMatrixRegularization] Please call "
+                     "'setRobotModel()' before."
+                  << std::endl;
+        return false;
+    }
+    const std::size_t rightSize = m_actuatedDoFs + m_baseDoFs;
+    if (rightSize != matrix.rows() || matrix.cols() != matrix.rows())
+    {
+        std::cerr << "[FloatingBaseDynamicalSystem::setMassMatrixRegularization] The size of the "
+                     "regularization matrix is not correct. The correct size is: "
+                  << rightSize << " x " << rightSize << ". While the input of the function is a "
+                  << matrix.rows() << " x " << matrix.cols() << " matrix." << std::endl;
+        return false;
+    }
+    m_useMassMatrixRegularizationTerm = m_dReg.upload(matrix.data(), rightSize * rightSize);
+    return m_useMassMatrixRegularizationTerm;
+}
+
+// device state layout: base vel 6 | joint vel n | base pos 3 | base rot 9 | joint pos n
+bool FloatingBaseDynamicalSystem::prepare(const char* where, blf_fb_model& model,
+                                          blf_fb_state& state, blf_fb_contacts& contacts)
+{
+    if (!m_hasModel)
+    {
+        std::cerr << "[" << where << "] Please call 'setRobotModel()' before." << std::endl;
+        return false;
+    }
+    const auto& [baseVelocity, jointVelocity, basePosition, baseOrientation, jointPositions] = m_state;
+    const auto& [jointTorques, contactWrenches] = m_controlInput;
+    const std::size_t n = m_actuatedDoFs;
+    if (jointVelocity.size() != n || jointPositions.size() != n || jointTorques.size() != n)
+    {
+        std::cerr << "[" << where << "] Wrong size of the vectors." << std::endl;
+        return false;
+    }
+    if (contactWrenches.size() > BLF_FBD_MAX_CONTACTS)
+    {
+        std::cerr << "[" << where << "] At most " << BLF_FBD_MAX_CONTACTS << " contacts." << std::endl;
+        return false;
+    }
+    std::vector<double> st(18 + 2 * n);
+    for (int i = 0; i < 6; ++i) st[i] = baseVelocity[i];
+    for (std::size_t i = 0; i < n; ++i) st[6 + i] = jointVelocity[i];
+    for (int i = 0; i < 3; ++i) st[6 + n + i] = basePosition[i];
+    for (int i = 0; i < 9; ++i) st[9 + n + i] = baseOrientation[i];
+    for (std::size_t i = 0; i < n; ++i) st[18 + n + i] = jointPositions[i];
+    std::vector<int32_t> frames;
+    std::vector<double> params, nulls;
+    for (const auto& c : contactWrenches)
+    {
+        auto ptr = c.contactModel().lock();
+        auto cm = std::dynamic_pointer_cast<ContactModels::ContinuousContactModel>(ptr);
+        if (cm == nullptr)
+        {
+            std::cerr << "[" << where << "] The contact model associated to the frame " << c.index()
+                      << " has expired or is not a ContinuousContactModel." << std::endl;
+            return false;
+        }
+        if (c.index() < 0 || c.index() >= static_cast<int>(m_model.frameLink.size()))
+        {
+            std::cerr << "[" << where << "] Unknown frame " << c.index() << "." << std::endl;
+            return false;
+        }
+        frames.push_back(c.index());
+        params.insert(params.end(), {cm->length(), cm->width(), cm->springCoeff(), cm->damperCoeff()});
+        const auto np = cm->nullForceTransform().packed();
+        nulls.insert(nulls.end(), np.begin(), np.end());
+    }
+    if (!m_dState.upload(st) || !m_dTau.upload(jointTorques.data(), n)
+        || !m_dContactFrame.upload(frames) || !m_dContactParams.upload(params)
+        || !m_dNullPose.upload(nulls))
+        return false;
+    model.ndof = static_cast<int32_t>(n);
+    model.nframes = static_cast<int32_t>(m_model.frameLink.size());
+    model.parent = m_dParent.data();
+    model.joint_origin = m_dOrigin.data();
+    model.joint_rot = m_dRot.data();
+    model.joint_axis = m_dAxis.data();
+    model.link_mass = m_dMass.data();
+    model.link_com = m_dCom.data();
+    model.link_inertia = m_dInertia.data();
+    model.frame_link = m_dFrameLink.data();
+    model.frame_pose = m_dFramePose.data();
+    for (int i = 0; i < 3; ++i) model.gravity[i] = m_gravity[i];
+    model.rho = m_rho;
+    double* s = m_dState.data();
+    state.base_vel = s;
+    state.joint_vel = s + 6;
+    state.base_pos = s + 6 + n;
+    state.base_rot = s + 9 + n;
+    state.joint_pos = s + 18 + n;
+    contacts.ncontacts = static_cast<int32_t>(frames.size());
+    contacts.frame = m_dContactFrame.data();
+    contacts.params = m_dContactParams.data();
+    contacts.null_pose = m_dNullPose.data();
+    return true;
+}
+
+bool FloatingBaseDynamicalSystem::dynamics(const double& time, StateDerivativeType& stateDerivative)
+{
+    (void)time;
+    const char* where = "FloatingBaseDynamicalSystem::dynamics";
+    blf_fb_model model;
+    blf_fb_state state;
+    blf_fb_contacts contacts;
+    blf_handle* h = blf::threadHandle();
+    if (h == nullptr || !prepare(where, model, state, contacts)) return false;
+    const std::size_t n = m_actuatedDoFs;
+    if (!m_dOut.resize(18 + 2 * n)) return false;
+    double* o = m_dOut.data();
+    blf_fb_state out{o, o + 6, o + 6 + n, o + 9 + n, o + 18 + n};
+    if (!blf::report(blf_fbd_dynamics(h, &model, &state, m_dTau.data(), &contacts,
+                                      m_useMassMatrixRegularizationTerm ? m_dReg.data() : nullptr,
+                                      1, &out, nullptr),
+                     where))
+        return false;
+    std::vector<double> host(18 + 2 * n);
+    if (!m_dOut.download(host.data(), host.size())) return false;
+    auto& [baseAcceleration, jointAcceleration, baseLinearVelocity, baseRotationRate,
+           jointVelocityOutput] = stateDerivative;
+    for (int i = 0; i < 6; ++i) baseAcceleration[i] = host[i];
+    jointAcceleration.resize(n);
+    jointVelocityOutput.resize(n);
+    for (std::size_t i = 0; i < n; ++i)
+    {
+        jointAcceleration[i] = host[6 + i];
+        jointVelocityOutput[i] = host[18 + n + i];
+    }
+    for (int i = 0; i < 3; ++i) baseLinearVelocity[i] = host[6 + n + i];
+    for (int i = 0; i < 9; ++i) baseRotationRate[i] = host[9 + n + i];
+    return true;
+}
+
+bool FloatingBaseDynamicalSystem::forwardEulerIntegrate(double initialTime, double finalTime,
+                                                        double dT)
+{
+    const char* where = "FixedStepIntegrator::integrate";
+    blf_fb_model model;
+    blf_fb_state state;
+    blf_fb_contacts contacts;
+    blf_handle* h = blf::threadHandle();
+    if (h == nullptr || !prepare(where, model, state, contacts)) return false;
+    if (!blf::report(blf_fbd_euler_integrate(h, &model, &state, m_dTau.data(), &contacts,
+                                             m_useMassMatrixRegularizationTerm ? m_dReg.data()
+                                                                               : nullptr,
+                                             1, initialTime, finalTime, dT, nullptr),
+                     where))
+        return false;
+    const std::size_t n = m_actuatedDoFs;
+    std::vector<double> host(18 + 2 * n);
+    if (!m_dState.download(host.data(), host.size())) return false;
+    auto& [baseVelocity, jointVelocity, basePosition, baseOrientation, jointPositions] = m_state;
+    for (int i = 0; i < 6; ++i) baseVelocity[i] = host[i];
+    for (std::size_t i = 0; i < n; ++i)
+    {
+        jointVelocity[i] = host[6 + i];
+        jointPositions[i] = host[18 + n + i];
+    }
+    for (int i = 0; i < 3; ++i) basePosition[i] = host[6 + n + i];
+    for (int i = 0; i < 9; ++i) baseOrientation[i] = host[9 + n + i];
+    return true;
+}

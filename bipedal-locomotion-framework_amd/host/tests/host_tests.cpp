@@ -26,6 +26,7 @@
 #include <BipedalLocomotion/Planners/ConvexHullHelper.h>
 #include <BipedalLocomotion/Planners/QuinticSpline.h>
 #include <BipedalLocomotion/Planners/TimeVaryingDCMPlanner.h>
+#include <BipedalLocomotion/System/FloatingBaseSystemDynamics.h>
 #include <BipedalLocomotion/System/FloatingBaseSystemKinematics.h>
 #include <BipedalLocomotion/System/ForwardEuler.h>
 #include <BipedalLocomotion/System/LinearTimeInvariantSystem.h>
@@ -527,6 +528,86 @@ static void testFloatingBaseKinematics()
     REQUIRE_FALSE(system->dynamics(0.0, dx));
 }
 
+// ---- FloatingBaseDynamicalSystem (FloatingBaseSystemDynamics.cpp:102-251) on a 3-joint chain ---
+static blf::RobotModel chainModel()
+{
+    blf::RobotModel m;
+    m.ndof = 3;
+    m.parent = {0, 1, 2};
+    m.jointOrigin = {0.0, 0.0, -0.1, 0.0, 0.0, -0.3, 0.0, 0.0, -0.3};
+    m.jointRotation.clear();
+    for (int j = 0; j < 3; ++j) m.jointRotation.insert(m.jointRotation.end(), {1, 0, 0, 0, 1, 0, 0, 0, 1});
+    m.jointAxis = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 1.0, 0.0};
+    m.linkMass = {5.0, 2.0, 1.5, 1.0};
+    m.linkCom = {0.0, 0.0, 0.0, 0.0, 0.0, -0.15, 0.0, 0.0, -0.15, 0.05, 0.0, -0.02};
+    m.linkInertia.clear();
+    for (double mass : m.linkMass)
+        m.linkInertia.insert(m.linkInertia.end(), {0.01 * mass, 0, 0, 0, 0.012 * mass, 0, 0, 0, 0.008 * mass});
+    m.frameLink = {3};
+    m.framePose = {0.02, 0.0, -0.05, 1, 0, 0, 0, 1, 0, 0, 0, 1};
+    return m;
+}
+
+static void testFloatingBaseDynamics()
+{
+    auto system = std::make_shared<FloatingBaseDynamicalSystem>();
+    auto handler = std::make_shared<ParametersHandler::StdImplementation>();
+    handler->setParameter("rho", 0.01);
+    REQUIRE(system->initalize(handler));
+    REQUIRE(system->setRobotModel(chainModel()));
+    const blf::Matrix3 R0 = rpy(0.05, -0.1, 0.2);
+    blf::VectorXd zero3(3, 0.0), q(3, 0.0);
+    q[0] = 0.2; q[1] = -0.4; q[2] = 0.3;
+    // free fall: nu = 0, tau = 0, no contacts -> base acceleration = g, joints at rest
+    REQUIRE(system->setState({blf::Vector6{}, zero3, blf::Vector3{{0.0, 0.0, 1.0}}, R0, q}));
+    REQUIRE(system->setControlInput({zero3, {}}));
+    FloatingBaseDynamicalSystem::StateDerivativeType dx;
+    REQUIRE(system->dynamics(0.0, dx));
+    const auto& [ba, ja, dp, dR, dq] = dx;
+    REQUIRE(std::abs(ba[2] + 9.81) < 1e-10);
+    for (int i : {0, 1, 3, 4, 5}) REQUIRE(std::abs(ba[i]) < 1e-10);
+    for (int i = 0; i < 3; ++i) REQUIRE(std::abs(ja[i]) < 1e-10);
+    // ForwardEuler free fall: v_k = g k dT, z_k = z0 + g dT^2 k (k - 1) / 2 (k = number of steps)
+    ForwardEuler<FloatingBaseDynamicalSystem> integrator(0.01);
+    REQUIRE(integrator.setDynamicalSystem(system));
+    REQUIRE(integrator.integrate(0.0, 0.1));
+    const auto& [bv, jv, bp, bR, jp] = integrator.getSolution();
+    // the FixedStepIntegrator schedule: ceil((T - t0) / dT) calls, the last one with the stale time
+    const int iterations = static_cast<int>(std::ceil((0.1 - 0.0) / 0.01));
+    const double last = 0.1 - (iterations >= 2 ? 0.01 * (iterations - 2) : 0.0);
+    double v = 0.0, z = 1.0;
+    for (int k = 0; k < iterations; ++k)
+    {
+        const double h = k + 1 < iterations ? 0.01 : last;
+        z += v * h;
+        v += -9.81 * h;
+    }
+    REQUIRE(std::abs(bv[2] - v) < 1e-10 && std::abs(bp[2] - z) < 1e-10);
+    // the foot (z ~ 0.25) is below the null-force height 0.5: the contact pushes the robot up
+    auto contact = std::make_shared<ContactModels::ContinuousContactModel>();
+    auto cp = std::make_shared<ParametersHandler::StdImplementation>();
+    cp->setParameter("length", 0.12);
+    cp->setParameter("width", 0.09);
+    cp->setParameter("spring_coeff", 3.0e4);
+    cp->setParameter("damper_coeff", 300.0);
+    REQUIRE(contact->initialize(cp));
+    blf::Transform nullT;
+    nullT.position = {{0.0, 0.0, 0.5}};
+    contact->setNullForceTransform(nullT);
+    REQUIRE(system->setState({blf::Vector6{}, zero3, blf::Vector3{{0.0, 0.0, 1.0}}, R0, q}));
+    REQUIRE(system->setControlInput({zero3, {ContactWrench(0, contact)}}));
+    REQUIRE(system->dynamics(0.0, dx));
+    REQUIRE(std::isfinite(std::get<0>(dx)[2]) && std::get<0>(dx)[2] > -9.81 + 1e-3);   // pushed up
+    // wrong sizes and a missing model are refused
+    REQUIRE(system->setControlInput({blf::VectorXd(2, 0.0), {}}));
+    REQUIRE_FALSE(system->dynamics(0.0, dx));
+    FloatingBaseDynamicalSystem empty;
+    REQUIRE_FALSE(empty.dynamics(0.0, dx));
+    REQUIRE_FALSE(empty.setMassMatrixRegularization(blf::MatrixXd(9, 9)));
+    REQUIRE_FALSE(system->setMassMatrixRegularization(blf::MatrixXd(8, 8)));
+    REQUIRE(system->setMassMatrixRegularization(blf::MatrixXd(9, 9)));
+}
+
 int main(int argc, char** argv)
 {
     const std::string which = argc > 1 ? argv[1] : "all";
@@ -543,6 +624,7 @@ int main(int argc, char** argv)
         {"TimeVaryingDCMPlanner advance", true, testPlanner},
         {"Continuous Contact", true, testContinuousContact},
         {"FloatingBaseSystemKinematics", true, testFloatingBaseKinematics},
+        {"FloatingBaseDynamicalSystem", true, testFloatingBaseDynamics},
     };
     for (const auto& t : tests)
     {

@@ -29,6 +29,10 @@
  *   blf_fbk_dynamics          System/src/FloatingBaseSystemKinematics.cpp:36-73
  *   blf_fbk_euler_integrate   ForwardEuler<FloatingBaseSystemKinematics>::integrate
  *                             (FixedStepIntegrator.tpp:21-72 + ForwardEuler.tpp:18-49)
+ *   blf_fbd_dynamics          System/src/FloatingBaseSystemDynamics.cpp:102-251
+ *                             (FloatingBaseDynamicalSystem::dynamics; the rigid-body terms that the
+ *                             reference takes from iDynTree KinDynComputations are computed here)
+ *   blf_fbd_euler_integrate   ForwardEuler<FloatingBaseDynamicalSystem>::integrate
  *   blf_dcm_mpc_solve         ABSENT in the reference (TimeVaryingDCMPlanner QP),
  *                             driven through System/Advanceable.h:24-46 (advance()) by the C++ host
  *                             adapter blf::Planners::TimeVaryingDCMPlanner
@@ -217,6 +221,69 @@ blf_status blf_fbk_euler_integrate(blf_handle* handle, int32_t ndof, double rho,
                                    double* rot, double* joints, const double* twist,
                                    const double* joint_vel, int64_t batch, double initial_time,
                                    double final_time, double dT, void* stream);
+
+/* ---- 8. Floating-base dynamics (FloatingBaseDynamicalSystem), batched ----------------------
+ * A kinematic tree of ndof revolute joints on a 6-DoF floating base (the robot model the reference
+ * loads into iDynTree KinDynComputations; blf/robot.py documents the layout).  All pointers are
+ * device memory.  Link 0 is the base; joint j moves link j + 1, whose parent link is parent[j]
+ * (<= j).  Velocities are in the MIXED representation (iDynTree's default): the base twist is
+ * (dp_B/dt, omega_B) in world coordinates.                                                      */
+#define BLF_FBD_MAX_DOFS 48
+#define BLF_FBD_MAX_CONTACTS 8
+typedef struct blf_fb_model {
+    int32_t ndof;                 /* n, 1..BLF_FBD_MAX_DOFS                                 */
+    int32_t nframes;              /* F, frames contacts may be attached to                  */
+    const int32_t* parent;        /* [n]                                                     */
+    const double* joint_origin;   /* [n][3]  joint origin in the parent link frame           */
+    const double* joint_rot;      /* [n][9]  fixed rotation parent link -> joint frame        */
+    const double* joint_axis;     /* [n][3]  unit axis in the joint frame                    */
+    const double* link_mass;      /* [n+1]                                                   */
+    const double* link_com;       /* [n+1][3] COM in the link frame                         */
+    const double* link_inertia;   /* [n+1][9] inertia about the COM, link frame              */
+    const int32_t* frame_link;    /* [F]                                                     */
+    const double* frame_pose;     /* [F][12] (p, R) of the frame in its link frame           */
+    double gravity[3];            /* (0, 0, -9.81) in the reference                          */
+    double rho;                   /* Baumgarte parameter of the base rotation rate           */
+} blf_fb_model;
+
+/* The state tuple (FloatingBaseSystemDynamics.h: base velocity, joint velocities, base position,
+ * base orientation, joint positions); the same struct carries the state derivative (base
+ * acceleration, joint accelerations, base linear velocity, base rotation rate, joint velocities). */
+typedef struct blf_fb_state {
+    double* base_vel;   /* [B][6]  */
+    double* joint_vel;  /* [B][n]  */
+    double* base_pos;   /* [B][3]  */
+    double* base_rot;   /* [B][9]  row-major */
+    double* joint_pos;  /* [B][n]  */
+} blf_fb_state;
+
+/* Contacts of the control input (the reference's std::vector<ContactWrench>): a
+ * ContinuousContactModel on each listed frame, updated with the frame's world transform and
+ * mixed velocity before its wrench is mapped through the frame Jacobian. */
+typedef struct blf_fb_contacts {
+    int32_t ncontacts;            /* 0..BLF_FBD_MAX_CONTACTS                                  */
+    const int32_t* frame;         /* [C] frame indices                                       */
+    const double* params;         /* [C][4] (length, width, spring_coeff, damper_coeff)      */
+    const double* null_pose;      /* [B][C][12] null-force transforms                        */
+} blf_fb_contacts;
+
+/* FloatingBaseDynamicalSystem::dynamics for a batch:
+ *   nu_dot = LLT(M [+ mass_reg]) \ (-h + sum_c J_c^T w_c + [0; tau]),  dp = v_B,
+ *   dR = -R.colwise().cross(w_B) + rho/2 ((R R^T)^{-1} - I) R,  ds = s_dot
+ * joint_torque [B][n]; mass_reg [(n+6)^2] row-major or NULL; out receives the derivative. */
+blf_status blf_fbd_dynamics(blf_handle* handle, const blf_fb_model* model,
+                            const blf_fb_state* state, const double* joint_torque,
+                            const blf_fb_contacts* contacts, const double* mass_reg,
+                            int64_t batch, const blf_fb_state* out, void* stream);
+
+/* ForwardEuler<FloatingBaseDynamicalSystem>::integrate(t0, T): the schedule and errors of
+ * blf_lti_euler_integrate; each step evaluates the dynamics at the current state (torques and
+ * contact parameters held constant) and updates every state element x += dx * dT_i.           */
+blf_status blf_fbd_euler_integrate(blf_handle* handle, const blf_fb_model* model,
+                                   const blf_fb_state* state, const double* joint_torque,
+                                   const blf_fb_contacts* contacts, const double* mass_reg,
+                                   int64_t batch, double initial_time, double final_time,
+                                   double dT, void* stream);
 
 /* Algorithmic flop count of one IPM iteration of one problem (what the fp64 roofline field
  * of bench.py is computed from); `active_facets` = sum_k nfacets[k]. */

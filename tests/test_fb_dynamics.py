@@ -1,0 +1,112 @@
+"""CPU tests of the floating-base dynamics oracle (oracle/fb_dynamics.py), the checker of the
+blf_fbd_* kernels.  The reference's rigid-body terms come from iDynTree,
+absent here, and the reference has no test for this class, so parity is UNPINNED;
+the oracle is validated by self-consistency at several random states of the synthetic 30-DoF
+model (blf/robot.py):
+  * M symmetric positive definite, M[0:3, 0:3] = total mass I;
+  * 1/2 nu^T M nu equals the kinetic energy summed link by link;
+  * nu^T h(g = 0) = 1/2 nu^T (dM/dt) nu  (skew-symmetry of dM/dt - 2C; dM/dt by central differences
+    along the motion);
+  * nu^T (h - h(g = 0)) = dV/dt = -sum_l m_l g . v_com,l;
+  * the equation of motion M nu_dot + h = [0; tau] + sum_c J_c^T w_c holds for the solution."""
+import numpy as np
+import pytest
+
+import fb_dynamics as F
+import oracle as O
+from blf import robot
+
+MODEL = robot.humanoid24()
+
+
+def state_i(st, i):
+    return {k: v[i] for k, v in st.items()}
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_mass_matrix_and_energy(seed):
+    st = state_i(robot.random_states(MODEL, 1, seed=seed), 0)
+    K = F.kinematics(MODEL, st["base_pos"], st["base_rot"], st["joint_pos"], st["base_vel"],
+                     st["joint_vel"])
+    M, h = F.mass_and_bias(MODEL, K)
+    assert np.abs(M - M.T).max() < 1e-13
+    assert np.linalg.eigvalsh(M).min() > 0
+    np.testing.assert_allclose(M[:3, :3], MODEL["link_mass"].sum() * np.eye(3), atol=1e-12)
+    nu = np.concatenate([st["base_vel"], st["joint_vel"]])
+    T = 0.0
+    for l in range(MODEL["n"] + 1):
+        R = K["R"][l]
+        c = K["p"][l] + R @ MODEL["link_com"][l]
+        vc = K["v"][l] + np.cross(K["w"][l], c - K["p"][l])
+        T += 0.5 * MODEL["link_mass"][l] * vc @ vc
+        T += 0.5 * K["w"][l] @ (R @ MODEL["link_inertia"][l] @ R.T) @ K["w"][l]
+    assert abs(0.5 * nu @ M @ nu - T) < 1e-12 * max(1.0, T)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_bias_forces_power_identities(seed):
+    st = state_i(robot.random_states(MODEL, 1, seed=10 + seed), 0)
+    K = F.kinematics(MODEL, st["base_pos"], st["base_rot"], st["joint_pos"], st["base_vel"],
+                     st["joint_vel"])
+    M, h = F.mass_and_bias(MODEL, K)
+    _, h0 = F.mass_and_bias(MODEL, K, gravity=np.zeros(3))
+    nu = np.concatenate([st["base_vel"], st["joint_vel"]])
+    dt = 1e-6
+    w = st["base_vel"][3:]
+
+    def M_at(sign):
+        Rn = F.rot_axis(w / np.linalg.norm(w), sign * dt * np.linalg.norm(w)) @ st["base_rot"]
+        K2 = F.kinematics(MODEL, st["base_pos"] + sign * dt * st["base_vel"][:3], Rn,
+                          st["joint_pos"] + sign * dt * st["joint_vel"], st["base_vel"],
+                          st["joint_vel"])
+        return F.mass_and_bias(MODEL, K2)[0]
+
+    Mdot = (M_at(1) - M_at(-1)) / (2 * dt)
+    assert abs(nu @ h0 - 0.5 * nu @ Mdot @ nu) < 1e-7 * max(1.0, abs(nu @ h0))
+    dV = 0.0
+    for l in range(MODEL["n"] + 1):
+        c = K["p"][l] + K["R"][l] @ MODEL["link_com"][l]
+        vc = K["v"][l] + np.cross(K["w"][l], c - K["p"][l])
+        dV -= MODEL["link_mass"][l] * F.G @ vc
+    assert abs(nu @ (h - h0) - dV) < 1e-10 * max(1.0, abs(dV))
+
+
+def contact_setup(B, seed=0):
+    rng = np.random.default_rng(seed)
+    params = np.array([[0.12, 0.09, 3.0e4, 300.0]] * 2)
+    null = np.zeros((B, 2, 12))
+    null[:, :, :3] = rng.normal(size=(B, 2, 3)) * 0.01
+    null[:, :, 3:] = np.eye(3).reshape(-1)
+    return np.array([0, 1], dtype=np.int32), params, null
+
+
+def test_equation_of_motion_with_contacts():
+    st = robot.random_states(MODEL, 2, seed=4)
+    frames, params, null = contact_setup(2)
+    for i in range(2):
+        ba, ja, dp, dR, dq = F.dynamics(MODEL, st, i, contacts=frames, contact_params=params,
+                                        null_poses=null[i])
+        s = state_i(st, i)
+        K = F.kinematics(MODEL, s["base_pos"], s["base_rot"], s["joint_pos"], s["base_vel"],
+                         s["joint_vel"])
+        M, h = F.mass_and_bias(MODEL, K)
+        rhs = -h.copy()
+        rhs[6:] += s["joint_torque"]
+        for c, f in enumerate(frames):
+            pf, Rf, vel, J = F.frame_state(MODEL, K, f)
+            wr = O.contact_eval(params[c], vel, np.concatenate([pf, Rf.reshape(-1)]), null[i][c])[0]
+            rhs += J.T @ wr
+        acc = np.concatenate([ba, ja])
+        np.testing.assert_allclose(M @ acc, rhs, atol=1e-8 * np.abs(rhs).max())
+        np.testing.assert_array_equal(dp, s["base_vel"][:3])
+        np.testing.assert_array_equal(dq, s["joint_vel"])
+
+
+def test_frame_jacobian_matches_frame_velocity():
+    st = state_i(robot.random_states(MODEL, 1, seed=8), 0)
+    K = F.kinematics(MODEL, st["base_pos"], st["base_rot"], st["joint_pos"], st["base_vel"],
+                     st["joint_vel"])
+    nu = np.concatenate([st["base_vel"], st["joint_vel"]])
+    for f in range(2):
+        _, _, vel, J = F.frame_state(MODEL, K, f)
+        np.testing.assert_allclose(J @ nu, vel, atol=1e-13)

@@ -1,0 +1,113 @@
+"""GPU parity of the floating-base dynamics kernels (blf_fbd_dynamics / blf_fbd_euler_integrate,
+SURVEY.md 8(a) row 6) against the numpy restatement oracle/fb_dynamics.py on the synthetic
+30-DoF model (blf/robot.py).  fp64 throughout; the two sides sum in different orders (LAPACK
+Cholesky vs the kernel's right-looking one), so the comparison is at a relative tolerance of
+1e-9 on the accelerations (north_star: fp64 error < 1e-9), exact on the kinematic part that does
+not go through the mass matrix."""
+import numpy as np
+import pytest
+import torch
+
+import fb_dynamics as F
+from blf import native, robot
+
+pytestmark = pytest.mark.gpu
+MODEL = robot.humanoid24()
+TOL = 1e-9
+
+
+def _d(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
+
+
+def contacts_for(B, seed=0):
+    rng = np.random.default_rng(seed)
+    params = np.array([[0.12, 0.09, 3.0e4, 300.0]] * 2)
+    null = np.zeros((B, 2, 12))
+    null[:, :, :3] = rng.normal(size=(B, 2, 3)) * 0.01
+    null[:, :, 3:] = np.eye(3).reshape(-1)
+    host = dict(frame=np.array([0, 1], dtype=np.int32), params=params, null_pose=null)
+    dev = dict(frame=_d(host["frame"], torch.int32), params=_d(params), null_pose=_d(null))
+    return host, dev
+
+
+def rel_err(a, b):
+    return np.abs(a - b).max() / max(1.0, np.abs(b).max())
+
+
+@pytest.mark.parametrize("with_contacts", [False, True])
+def test_fbd_dynamics_vs_oracle(handle, with_contacts):
+    B = 96
+    st = robot.random_states(MODEL, B, seed=21)
+    dm = handle.fb_model(MODEL)
+    dst = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    host, dev = contacts_for(B) if with_contacts else (None, None)
+    out = handle.fbd_dynamics(dm, dst, _d(st["joint_torque"]), contacts=dev)
+    out = {k: v.cpu().numpy() for k, v in out.items()}
+    for i in range(0, B, 7):
+        kw = {}
+        if with_contacts:
+            kw = dict(contacts=host["frame"], contact_params=host["params"],
+                      null_poses=host["null_pose"][i])
+        ba, ja, dp, dR, dq = F.dynamics(MODEL, st, i, **kw)
+        assert rel_err(out["base_vel"][i], ba) < TOL
+        assert rel_err(out["joint_vel"][i], ja) < TOL
+        np.testing.assert_array_equal(out["base_pos"][i], dp)
+        np.testing.assert_allclose(out["base_rot"][i], dR, atol=1e-15)
+        np.testing.assert_array_equal(out["joint_pos"][i], dq)
+
+
+def test_fbd_mass_regularization(handle):
+    B = 8
+    st = robot.random_states(MODEL, B, seed=3)
+    dm = handle.fb_model(MODEL)
+    reg = 0.05 * np.eye(30)
+    out = handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS},
+                              _d(st["joint_torque"]), mass_reg=_d(reg))
+    ja = out["joint_vel"].cpu().numpy()
+    for i in range(B):
+        ref = F.dynamics(MODEL, st, i, reg=reg)[1]
+        assert rel_err(ja[i], ref) < TOL
+
+
+@pytest.mark.parametrize("t0,t1,dT", [(0.0, 0.004, 0.001), (0.0, 0.0025, 0.001)])
+def test_fbd_euler_vs_oracle(handle, t0, t1, dT):
+    B = 16
+    st = robot.random_states(MODEL, B, seed=5)
+    host, dev = contacts_for(B, seed=1)
+    dm = handle.fb_model(MODEL)
+    dst = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    handle.fbd_euler_integrate(dm, dst, _d(st["joint_torque"]), t0, t1, dT, contacts=dev)
+    got = {k: v.cpu().numpy() for k, v in dst.items()}
+    for i in (0, 5, 15):
+        ref = F.euler_integrate(MODEL, st, i, t0, t1, dT, contacts=host["frame"],
+                                contact_params=host["params"], null_poses=host["null_pose"][i])
+        for k in native.FB_STATE_KEYS:
+            assert rel_err(got[k][i], ref[k]) < TOL, k
+
+
+def test_fbd_config5_batch_runs(handle):
+    """BASELINE configs[4] size: 16384 systems of the 30-DoF model with two foot contacts."""
+    B = 16384
+    st = robot.random_states(MODEL, B, seed=9)
+    host, dev = contacts_for(B, seed=2)
+    dm = handle.fb_model(MODEL)
+    out = handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS},
+                              _d(st["joint_torque"]), contacts=dev)
+    acc = out["joint_vel"].cpu().numpy()
+    assert np.isfinite(acc).all()
+    i = B - 1
+    ref = F.dynamics(MODEL, st, i, contacts=host["frame"], contact_params=host["params"],
+                     null_poses=host["null_pose"][i])[1]
+    assert rel_err(acc[i], ref) < TOL
+
+
+def test_fbd_errors(handle):
+    st = robot.random_states(MODEL, 2, seed=1)
+    dm = handle.fb_model(MODEL)
+    dst = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    tau = _d(st["joint_torque"])
+    for (t0, t1, dT), code in (((1.0, 0.0, 0.1), 4), ((0.0, 1.0, -1.0), 4), ((0.5, 0.5, 0.1), 5)):
+        with pytest.raises(native.BlfError) as e:
+            handle.fbd_euler_integrate(dm, dst, tau, t0, t1, dT)
+        assert e.value.code == code

@@ -36,5 +36,5 @@ def test_host_device_tests():
     out = _run("gpu")
     for name in ("Integrator - Linear system", "Convex Hull helper (2-D)", "QuinticSpline",
                  "TimeVaryingDCMPlanner advance", "Continuous Contact",
-                 "FloatingBaseSystemKinematics"):
+                 "FloatingBaseSystemKinematics", "FloatingBaseDynamicalSystem"):
         assert any(line.startswith(name) and line.rstrip().endswith("ok") for line in out.splitlines()), out
