@@ -89,7 +89,13 @@ def main():
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
+                    help="c2 (default, the driver's metric): configs[1]; c3: configs[2] pipeline "
+                         "(hull H-rep + QP + swing splines, B=65536); c5: configs[4] closed loop "
+                         "(QP + 30-DoF floating-base dynamics with contacts, B=16384)")
     args = ap.parse_args()
+    if args.workload != "c2":
+        return other_workload(args)
 
     import numpy as np
     import torch
@@ -205,6 +211,97 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _timed(fn, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def other_workload(args):
+    """Secondary single-GPU measurements of BASELINE configs[2] and configs[4] (not the driver's
+    headline line; DESIGN.md section 9 records them)."""
+    import numpy as np
+    import torch
+    from blf import native
+    from blf import problems as P
+    from blf import robot
+    h = native.Handle(0)
+    dev = torch.device("cuda", 0)
+    N = args.horizon
+    if args.workload == "c3":
+        B = 65536
+        prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED)
+        d = {k: torch.from_numpy(prob[k]).to(dev) for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
+        corners = torch.from_numpy(prob["corners"]).to(dev)
+        ncorners = torch.from_numpy(prob["ncorners"]).to(dev)
+        kt, kp, tq = (torch.from_numpy(a).to(dev) for a in P.swing_splines(prob, queries=32))
+        params = native.default_params(N)
+        out = {}
+
+        def step():
+            A, b, nf = h.assemble_constraints(corners, ncorners)
+            d.update(A=A, b=b, nfacets=nf)
+            out["qp"] = h.dcm_mpc_solve(d, params)
+            coeffs = h.quintic_fit(kt, kp)
+            out["sp"] = h.quintic_eval(kt, coeffs, tq)
+
+        sec = _timed(step, args.steps, args.warmup)
+        assert int((out["qp"]["status"] != 0).sum()) == 0
+        line = {"metric": "DCM-MPC pipeline solves/sec (hull H-rep + QP + swing splines)",
+                "value": B / sec, "unit": "QP/s", "n_gpus": 1, "ms_per_step": sec * 1e3,
+                "steps": args.steps, "warmup": args.warmup, "dtype": "f64",
+                "config": {"workload": f"configs[2]: batch={B}, horizon={N}, "
+                                       f"{B * (N)} support polygons, {kt.shape[0]} swing splines "
+                                       f"x 32 queries", "batch_per_gpu": B}}
+    else:
+        B = 16384
+        prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED)
+        d = {k: torch.from_numpy(prob[k]).to(dev) for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
+        A, b, nf = h.assemble_constraints(torch.from_numpy(prob["corners"]).to(dev),
+                                          torch.from_numpy(prob["ncorners"]).to(dev))
+        d.update(A=A, b=b, nfacets=nf)
+        params = native.default_params(N)
+        model = robot.humanoid24()
+        dm = h.fb_model(model)
+        st = robot.random_states(model, B, seed=1)
+        state = {k: torch.from_numpy(st[k]).to(dev) for k in native.FB_STATE_KEYS}
+        tau = torch.from_numpy(st["joint_torque"]).to(dev)
+        null = np.zeros((B, 2, 12))
+        null[:, :, 3:] = np.eye(3).reshape(-1)
+        contacts = dict(frame=torch.tensor([0, 1], dtype=torch.int32, device=dev),
+                        params=torch.tensor([[0.12, 0.09, 3.0e4, 300.0]] * 2, dtype=torch.float64,
+                                            device=dev),
+                        null_pose=torch.from_numpy(null).to(dev))
+        period, dT = 0.01, 0.001          # one 10 ms control period of 1 ms Euler steps
+        out = {}
+
+        def step():
+            out["qp"] = h.dcm_mpc_solve(d, params)
+            h.fbd_euler_integrate(dm, state, tau, 0.0, period, dT, contacts=contacts)
+
+        sec = _timed(step, args.steps, args.warmup)
+        nsteps = int(np.ceil(period / dT))
+        t_dyn = _timed(lambda: h.fbd_euler_integrate(dm, state, tau, 0.0, period, dT,
+                                                     contacts=contacts), args.steps, 1)
+        line = {"metric": "closed-loop control periods/sec (DCM-MPC + 30-DoF floating-base "
+                          "dynamics with 2 ContinuousContactModel feet)",
+                "value": B / sec, "unit": "system-periods/s", "n_gpus": 1,
+                "ms_per_step": sec * 1e3, "steps": args.steps, "warmup": args.warmup,
+                "dtype": "f64",
+                "fb_dynamics_evals_per_s": B * nsteps / t_dyn,
+                "fb_dynamics_ms_per_period": t_dyn * 1e3,
+                "config": {"workload": f"configs[4] on one GPU: batch={B} robots, horizon-{N} QP "
+                                       f"+ {nsteps} Euler steps of the 6+24 DoF dynamics per "
+                                       f"period", "batch_per_gpu": B}}
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
