@@ -75,31 +75,70 @@ __device__ __forceinline__ double keepmin(double a, double b) { return (b < a) ?
 // max that ignores NaN candidates (matches the oracle's keepmax).
 __device__ __forceinline__ double keepmax(double a, double b) { return (b > a) ? b : a; }
 
-// xor-butterfly over the 64 lanes; every lane ends with the identical value because fp addition
-// is commutative: lane l and lane l^off both compute the same two operands.
+// Cross-lane moves of a double that stay in the VALU (no LDS round trip): DPP quad permutes and
+// row mirrors, and gfx950's v_permlane16_swap / v_permlane32_swap.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// v_permlane16_swap(x, x) returns (x with its odd rows replaced by the even rows, x with its even
+// rows replaced by the odd rows); lane l takes its row partner (l ^ 16) from the half that moved
+// into its own row.  v_permlane32_swap likewise for the two 32-lane halves (l ^ 32).
+__device__ __forceinline__ double swap16_f64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    const bool odd = (threadIdx.x >> 4) & 1;
+    const int l = odd ? lo[0] : lo[1];
+    const int h = odd ? hi[0] : hi[1];
+    return __longlong_as_double(((long long)h << 32) | (unsigned int)l);
+}
+__device__ __forceinline__ double swap32_f64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    const bool upper = (threadIdx.x >> 5) & 1;
+    const int l = upper ? lo[0] : lo[1];
+    const int h = upper ? hi[0] : hi[1];
+    return __longlong_as_double(((long long)h << 32) | (unsigned int)l);
+}
+
+// Butterfly over the 64 lanes, xor distances 1, 2, 4, 8, 16, 32 in that order (the oracle's
+// orc_wave_tree_sum).  After the 1- and 2-steps every quad holds one value and after the 4-step
+// every half-row does, so the half-row / row mirrors combine exactly the partners lane ^ 4 and
+// lane ^ 8 would; every lane ends with the identical value (fp addition is commutative).
+template <typename Op>
+__device__ __forceinline__ double wave_reduce(double v, Op op)
+{
+    v = op(v, dpp_f64<0xB1>(v));    // quad_perm [1,0,3,2]: lane ^ 1
+    v = op(v, dpp_f64<0x4E>(v));    // quad_perm [2,3,0,1]: lane ^ 2
+    v = op(v, dpp_f64<0x141>(v));   // row_half_mirror
+    v = op(v, dpp_f64<0x140>(v));   // row_mirror
+    v = op(v, swap16_f64(v));       // lane ^ 16
+    v = op(v, swap32_f64(v));       // lane ^ 32
+    return v;
+}
 __device__ __forceinline__ double wave_sum(double v)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, kWave);
-    return v;
+    return wave_reduce(v, [](double a, double b) { return a + b; });
 }
 __device__ __forceinline__ double wave_nanmax(double v)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = nanmax(v, __shfl_xor(v, off, kWave));
-    return v;
+    return wave_reduce(v, [](double a, double b) { return nanmax(a, b); });
 }
 __device__ __forceinline__ double wave_keepmin(double v)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = keepmin(v, __shfl_xor(v, off, kWave));
-    return v;
+    return wave_reduce(v, [](double a, double b) { return keepmin(a, b); });
 }
 __device__ __forceinline__ double wave_keepmax(double v)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = keepmax(v, __shfl_xor(v, off, kWave));
-    return v;
+    return wave_reduce(v, [](double a, double b) { return keepmax(a, b); });
 }
 __device__ __forceinline__ int wave_isum(int v)
 {

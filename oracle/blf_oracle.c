@@ -289,7 +289,7 @@ double orc_wave_tree_sum(const double* c, int n)
     for (int w = 0; w < nblk; ++w) {
         double v[64], t[64];
         for (int l = 0; l < 64; ++l) v[l] = (64 * w + l < n) ? c[64 * w + l] : 0.0;
-        for (int off = 32; off >= 1; off >>= 1) {
+        for (int off = 1; off <= 32; off <<= 1) {      /* the device's DPP / permlane order */
             for (int l = 0; l < 64; ++l) t[l] = v[l] + v[l ^ off];
             memcpy(v, t, sizeof(v));
         }

@@ -86,7 +86,8 @@ void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threa
                              int32_t* iters);
 
 /* Tree sum with the device's reduction order: c has n entries, padded with
- * zeros to 64*ceil(n/64); per 64-block xor-butterfly, then block sums left to right. */
+ * zeros to 64*ceil(n/64); per 64-block xor-butterfly (distances 1, 2, 4, ..., 32), then block
+ * sums left to right. */
 double orc_wave_tree_sum(const double* c, int n);
 
 /* ContinuousContactModel (one contact).  prm = {length, width, spring_coeff, damper_coeff};

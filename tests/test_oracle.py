@@ -188,7 +188,7 @@ def test_wave_tree_sum_order():
             v = np.zeros(64)
             blk = c[w:w + 64]
             v[:len(blk)] = blk
-            for off in (32, 16, 8, 4, 2, 1):
+            for off in (1, 2, 4, 8, 16, 32):   # the device butterfly order (DPP, permlane)
                 v = v + v[np.arange(64) ^ off]
             ref = v[0] if w == 0 else ref + v[0]
         assert O.wave_tree_sum(c) == ref
