@@ -106,9 +106,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL (backend "nccl") over xGMI on a node; BLF_BENCH_BACKEND=gloo rehearses the multi-rank
+    # path on a single GPU (every rank then shares device LOCAL_RANK % device_count)
+    backend = os.environ.get("BLF_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     h = native.Handle(local)
@@ -146,7 +153,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps      # one launch per step on this stream
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -162,7 +170,8 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        D.gather_solutions(out, N, dst=0)
+        D.gather_solutions(out if backend == "nccl" else {k: v.cpu() for k, v in out.items()},
+                           N, dst=0)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
