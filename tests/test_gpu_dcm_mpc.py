@@ -106,3 +106,60 @@ def test_dcm_mpc_rejects_bad_params(handle):
     p = native.default_params(10, max_facets=8, dt=-1.0)
     with pytest.raises(native.BlfError):
         handle.dcm_mpc_solve(dev, params=p)
+
+
+def _bitwise_vs_oracle(handle, oracle, host, params=None, oparams=None):
+    out = handle.dcm_mpc_solve(_to_dev(host), params=params)
+    st_o, xi_o, vrp_o, it_o = oracle.dcm_mpc_solve_batch(host, params=oparams, threads=8)
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), st_o)
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), it_o)
+    np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi_o)
+    np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)
+    return st_o, it_o
+
+
+@pytest.mark.parametrize("horizon", [63, 64, 65, 127, 128, 129, 200, 256, 300])
+def test_dcm_mpc_wavefront_boundaries(handle, oracle, horizon):
+    """Horizons around the 64-knot wavefront boundaries and multi-wavefront workgroups (the
+    scans' cross-wavefront steps, padding wavefronts of the 256 / 512-thread variants)."""
+    prob = P.make_batch(12, horizon=horizon, n_footsteps=8, seed=horizon)
+    host = oracle.assemble_constraints(prob)
+    st, _ = _bitwise_vs_oracle(handle, oracle, host)
+    assert (st == 0).all()
+
+
+@pytest.mark.parametrize("M", [4, 6])
+def test_dcm_mpc_fewer_facet_slots(handle, oracle, M):
+    prob = P.make_batch(16, horizon=80, n_footsteps=6, seed=M)
+    host = oracle.assemble_constraints(prob, max_facets=M)
+    if (host["nfacets"] < 0).any():
+        pytest.skip("a polygon needs more facet slots")
+    p = native.default_params(80, max_facets=M)
+    op = oracle.default_params(80, max_facets=M)
+    _bitwise_vs_oracle(handle, oracle, host, p, op)
+
+
+def test_dcm_mpc_other_weights_and_iteration_cap(handle, oracle):
+    prob = P.make_batch(16, horizon=60, n_footsteps=5, seed=77)
+    host = oracle.assemble_constraints(prob)
+    kw = dict(w_xi=(10.0, 30.0), w_vrp=(2.0, 0.5), w_terminal=(100.0, 500.0), dt=0.015)
+    _bitwise_vs_oracle(handle, oracle, host, native.default_params(60, **kw),
+                       oracle.default_params(60, **kw))
+    # a cap below the iterations needed: MAX_ITER with iters == cap on both sides
+    st, it = _bitwise_vs_oracle(handle, oracle, host, native.default_params(60, max_iter=4),
+                                oracle.default_params(60, max_iter=4))
+    assert (st == native.QP_MAX_ITER).all() and (it == 4).all()
+
+
+def test_dcm_mpc_infeasible_and_nonfinite_inputs(handle, oracle):
+    prob = P.make_batch(6, horizon=40, n_footsteps=4, seed=13)
+    host = oracle.assemble_constraints(prob)
+    # problem 0, knot 10: two opposite half-planes that exclude each other (empty polygon)
+    host["A"][0, 10, :2] = [[1.0, 0.0], [-1.0, 0.0]]
+    host["b"][0, 10, :2] = [-1.0, -1.0]
+    host["nfacets"][0, 10] = 2
+    # problem 1: a NaN CoM frequency
+    host["omega"][1, 3] = np.nan
+    st, _ = _bitwise_vs_oracle(handle, oracle, host)
+    assert st[0] != native.QP_SOLVED and st[1] != native.QP_SOLVED
+    assert (st[2:] == native.QP_SOLVED).all()
