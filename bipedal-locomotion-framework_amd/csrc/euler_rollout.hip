@@ -11,6 +11,7 @@
 //    coalesced (problem-major layout).
 // Built with -ffp-contract=off: bit-identical to oracle/blf_oracle.c.
 #include "blf_internal.h"
+#include "slab.h"
 
 namespace blf {
 namespace {
@@ -90,9 +91,78 @@ __global__ __launch_bounds__(256) void lti_dynamics_kernel(int n, int m,
     }
 }
 
-// 64 problems per workgroup (one wave), knots staged in chunks of KC.
+// 64 problems per workgroup (one wave), knots staged in chunks of KC.  The chunk's omega and
+// vrp rows are loaded by the whole wave with consecutive lanes on consecutive doubles (one batch
+// of loads per lane, 16 B each on full aligned chunks), transposed through LDS; the recurrence
+// runs lane-per-problem and the xi chunk leaves through LDS the same way.  (Prefetching the next
+// chunk during the recurrence measured no faster and cost 96 VGPRs.)
 constexpr int KC = 16;
+constexpr int kRollSw = 2 * KC + 1;   // padded LDS row of the vrp / xi chunk
 
+struct RollChunk {
+    double om[KC];       // omega [64][KC]   : double2 element u * 64 + lane
+    double r[2 * KC];    // vrp   [64][2 KC] : double2 element u * 64 + lane
+};
+
+// Full chunks of a full tile (64 problems x KC knots) with 16-B aligned rows: the element ->
+// (row, column) map is compile-time and every global access moves 16 B per lane.
+//   omega chunk: 64 rows x KC/2 double2, vrp / xi chunk: 64 rows x KC double2.
+__device__ __forceinline__ void roll_load_full(RollChunk& c, const double* __restrict__ omega,
+                                               const double* __restrict__ vrp, int64_t p0, int N,
+                                               int kb, int lane)
+{
+#pragma unroll
+    for (int u = 0; u < KC / 2; ++u) {
+        const int j = u * 64 + lane, r = j / (KC / 2), c2 = j % (KC / 2);
+        const double2 v = *reinterpret_cast<const double2*>(omega + (p0 + r) * N + kb + 2 * c2);
+        c.om[2 * u] = v.x;
+        c.om[2 * u + 1] = v.y;
+    }
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+        const int j = u * 64 + lane, r = j / KC, c2 = j % KC;
+        const double2 v =
+            *reinterpret_cast<const double2*>(vrp + (p0 + r) * 2 * N + 2 * kb + 2 * c2);
+        c.r[2 * u] = v.x;
+        c.r[2 * u + 1] = v.y;
+    }
+}
+
+__device__ __forceinline__ void roll_to_lds_full(const RollChunk& c, double* s_om, double* s_r,
+                                                 int lane)
+{
+#pragma unroll
+    for (int u = 0; u < KC / 2; ++u) {
+        const int j = u * 64 + lane, r = j / (KC / 2), c2 = j % (KC / 2);
+        s_om[r * (KC + 1) + 2 * c2] = c.om[2 * u];
+        s_om[r * (KC + 1) + 2 * c2 + 1] = c.om[2 * u + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+        const int j = u * 64 + lane, r = j / KC, c2 = j % KC;
+        s_r[r * kRollSw + 2 * c2] = c.r[2 * u];
+        s_r[r * kRollSw + 2 * c2 + 1] = c.r[2 * u + 1];
+    }
+}
+
+__device__ __forceinline__ void roll_store_full(double* __restrict__ xi_out, const double* s_x,
+                                                int64_t p0, int N, int kb, int lane)
+{
+    double2 v[KC];
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+        const int j = u * 64 + lane, r = j / KC, c2 = j % KC;
+        v[u].x = s_x[r * kRollSw + 2 * c2];
+        v[u].y = s_x[r * kRollSw + 2 * c2 + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+        const int j = u * 64 + lane, r = j / KC, c2 = j % KC;
+        *reinterpret_cast<double2*>(xi_out + (p0 + r) * 2 * (N + 1) + 2 * (kb + 1) + 2 * c2) = v[u];
+    }
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(64) void dcm_rollout_kernel(const double* __restrict__ xi0,
                                                          const double* __restrict__ omega,
                                                          const double* __restrict__ vrp,
@@ -100,10 +170,10 @@ __global__ __launch_bounds__(64) void dcm_rollout_kernel(const double* __restric
                                                          double* __restrict__ xi_out,
                                                          int64_t batch)
 {
-    // per chunk: omega [64][KC], vrp [64][KC][2] (overwritten in place by xi) ; +1 padding per
-    // row breaks the power-of-two stride between lanes (bank conflicts on the per-lane reads).
+    // per chunk: omega [64][KC], vrp [64][KC][2] (overwritten in place by xi); rows padded to an
+    // odd number of doubles so the per-lane row reads do not conflict.
     __shared__ double s_om[64 * (KC + 1)];
-    __shared__ double s_r[64 * (2 * KC + 1)];
+    __shared__ double s_r[64 * kRollSw];
     double* s_x = s_r;
     const int lane = threadIdx.x;
     const int64_t p0 = (int64_t)blockIdx.x * 64;
@@ -116,34 +186,36 @@ __global__ __launch_bounds__(64) void dcm_rollout_kernel(const double* __restric
         xi_out[2 * q * (N + 1)] = x0;
         xi_out[2 * q * (N + 1) + 1] = x1;
     }
+    // VEC: omega / vrp / xi_out 16-B aligned and N even (every row of every array aligned)
+    auto full = [&](int kb) { return VEC && nprob == 64 && kb + KC <= N; };
     for (int kb = 0; kb < N; kb += KC) {
         const int kc = (N - kb) < KC ? (N - kb) : KC;
-        // cooperative, coalesced loads of the chunk: row p of omega is contiguous
-        for (int e = lane; e < nprob * kc; e += 64) {
-            const int pr = e / kc, kk = e % kc;
-            s_om[pr * (KC + 1) + kk] = omega[(p0 + pr) * N + kb + kk];
-        }
-        for (int e = lane; e < nprob * 2 * kc; e += 64) {
-            const int pr = e / (2 * kc), kk = e % (2 * kc);
-            s_r[pr * (2 * KC + 1) + kk] = vrp[(p0 + pr) * 2 * N + 2 * kb + kk];
+        {
+            RollChunk c;
+            if (full(kb)) {
+                roll_load_full(c, omega, vrp, p0, N, kb, lane);
+                roll_to_lds_full(c, s_om, s_r, lane);
+            } else {   // tail chunk, partial tile or unaligned rows
+                slab_load<64, 8>(s_om, KC + 1, omega + p0 * N + kb, N, nprob, kc);
+                slab_load<64, 8>(s_r, kRollSw, vrp + p0 * 2 * N + 2 * kb, 2 * N, nprob, 2 * kc);
+            }
         }
         __syncthreads();
         if (lane < nprob) {
             for (int kk = 0; kk < kc; ++kk) {
                 const double w = s_om[lane * (KC + 1) + kk];
-                const double dx0 = w * x0 + (-w) * s_r[lane * (2 * KC + 1) + 2 * kk];
-                const double dx1 = w * x1 + (-w) * s_r[lane * (2 * KC + 1) + 2 * kk + 1];
+                const double dx0 = w * x0 + (-w) * s_r[lane * kRollSw + 2 * kk];
+                const double dx1 = w * x1 + (-w) * s_r[lane * kRollSw + 2 * kk + 1];
                 x0 = x0 + dx0 * dt;
                 x1 = x1 + dx1 * dt;
-                s_x[lane * (2 * KC + 1) + 2 * kk] = x0;
-                s_x[lane * (2 * KC + 1) + 2 * kk + 1] = x1;
+                s_x[lane * kRollSw + 2 * kk] = x0;
+                s_x[lane * kRollSw + 2 * kk + 1] = x1;
             }
         }
         __syncthreads();
-        for (int e = lane; e < nprob * 2 * kc; e += 64) {
-            const int pr = e / (2 * kc), kk = e % (2 * kc);
-            xi_out[(p0 + pr) * 2 * (N + 1) + 2 * (kb + 1) + kk] = s_x[pr * (2 * KC + 1) + kk];
-        }
+        if (full(kb)) roll_store_full(xi_out, s_x, p0, N, kb, lane);
+        else slab_store<64, 8>(xi_out + p0 * 2 * (N + 1) + 2 * (kb + 1), 2 * (N + 1), s_x,
+                               kRollSw, nprob, 2 * kc);
         __syncthreads();
     }
 }
@@ -177,8 +249,13 @@ blf_status launch_dcm_rollout(const double* xi0, const double* omega, const doub
 {
     if (batch == 0) return BLF_OK;
     const int64_t blocks = ceil_div(batch, 64);
-    hipLaunchKernelGGL(dcm_rollout_kernel, dim3((unsigned)blocks), dim3(64), 0, s, xi0, omega,
-                       vrp, N, dt, xi_out, batch);
+    const bool vec = (N % 2 == 0) && ((((uintptr_t)omega | (uintptr_t)vrp | (uintptr_t)xi_out) & 15) == 0);
+    if (vec)
+        hipLaunchKernelGGL(dcm_rollout_kernel<true>, dim3((unsigned)blocks), dim3(64), 0, s, xi0,
+                           omega, vrp, N, dt, xi_out, batch);
+    else
+        hipLaunchKernelGGL(dcm_rollout_kernel<false>, dim3((unsigned)blocks), dim3(64), 0, s, xi0,
+                           omega, vrp, N, dt, xi_out, batch);
     return check_hip(hipGetLastError(), "dcm_rollout_kernel launch");
 }
 

@@ -3,10 +3,10 @@
 //
 //  * hull2d_kernel: one lane per polygon (ConvexHullHelper::buildConvexHull + getA/getB,
 //    src/Planners/src/ConvexHullHelper.cpp:35-99).  The workgroup's contiguous slab of input
-//    points is staged through LDS with coalesced loads (rows padded to an odd number of doubles so
-//    the per-lane reads are bank-conflict free); each lane then sorts its points (insertion sort,
-//    p <= 16) and runs Andrew's monotone chain with a `cross <= 0` pop, which merges collinear
-//    boundary points the way Qhull's "Qt" facet merge does.  Output rows: unit outward normal,
+//    points is loaded coalesced and transposed into lane-minor LDS arrays; each lane then sorts
+//    its points in place (insertion sort, p <= 16) and runs Andrew's monotone chain with a
+//    `cross <= 0` pop, which merges collinear boundary points the way Qhull's "Qt" facet merge
+//    does.  The facets are then computed and stored by (polygon, facet) pair, coalesced.  Output rows: unit outward normal,
 //    b = n . v (inside: A x <= b), counter-clockwise from the leftmost-lowest vertex.
 //  * hull2d_contains_kernel: doesPointBelongToConvexHull (ConvexHullHelper.cpp:101-117): strict
 //    `(A p)_i > b_i` rejects, no tolerance.
@@ -15,12 +15,12 @@
 //    t_j <= t, -1 if none; the evaluated segment is that index clamped to [0, K-1].
 // Built with -ffp-contract=off; same expression order as oracle/blf_oracle.c.
 #include "blf_internal.h"
+#include "slab.h"
 
 namespace blf {
 namespace {
 
 constexpr int kHullBlock = 64;
-constexpr int kPmax = BLF_HULL_MAX_POINTS;
 
 __device__ __forceinline__ double cross3(double ox, double oy, double ax, double ay, double bx,
                                          double by)
@@ -28,6 +28,26 @@ __device__ __forceinline__ double cross3(double ox, double oy, double ax, double
     return (ax - ox) * (by - oy) - (ay - oy) * (bx - ox);
 }
 
+// Dynamic LDS of hull2d_kernel, per workgroup of 64 polygons (one per lane), lane-minor so that
+// the data-dependent indices of the sort and the chain never conflict:
+//   X, Y   [P][64] doubles: the polygon's points, sorted in place by the lane
+//   stack  [2P+2][64] int32: the monotone chain, as positions in the sorted arrays
+//   nf     [64] int32
+__host__ __device__ inline size_t hull2d_lds_bytes(int P, int /*M*/)
+{
+    return sizeof(double) * kHullBlock * 2 * P + sizeof(int32_t) * kHullBlock * (2 * P + 3);
+}
+
+__device__ __forceinline__ int hull2d_rows(int64_t batch, int64_t p0)
+{
+    return (int)((batch - p0) < kHullBlock ? (batch - p0) : kHullBlock);
+}
+
+// Phase 1 (lane per polygon): insertion sort of the coordinates by (x, y) with the oracle's
+// comparisons in the oracle's order (a stable sort, identical for any input including NaN), then
+// Andrew's monotone chain with the top two stack points held in registers (LDS is read only on a
+// pop).  Phase 2 (after a barrier): consecutive threads take consecutive (polygon, facet) pairs,
+// compute the facet once and store A as 16-B and b as 8-B coalesced writes.
 __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __restrict__ pts,
                                                             const int32_t* __restrict__ npts,
                                                             int32_t P, int32_t M, int64_t batch,
@@ -35,91 +55,142 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                                                             double* __restrict__ bout,
                                                             int32_t* __restrict__ nfout)
 {
-    __shared__ double s_pts[kHullBlock * (2 * kPmax + 1)];
-    __shared__ unsigned char s_idx[kPmax][kHullBlock];
-    __shared__ unsigned char s_H[2 * kPmax + 2][kHullBlock];
+    extern __shared__ double hull_smem[];
     const int t = threadIdx.x;
     const int64_t p0 = (int64_t)blockIdx.x * kHullBlock;
-    const int nprob = (int)((batch - p0) < kHullBlock ? (batch - p0) : kHullBlock);
-    const int row = 2 * P;            // doubles per polygon in global memory
-    const int srow = 2 * P + 1;       // padded LDS row (odd stride)
-    const double* src = pts + p0 * row;
-    for (int e = t; e < nprob * row; e += kHullBlock) {
-        const int r = e / row, c = e - r * row;
-        s_pts[r * srow + c] = src[e];
+    const int nprob = hull2d_rows(batch, p0);
+    double* s_x = hull_smem;                                               // [P][64]
+    double* s_y = s_x + kHullBlock * P;                                    // [P][64]
+    int32_t* s_stk = reinterpret_cast<int32_t*>(s_y + kHullBlock * P);     // [2P+2][64]
+    int32_t* s_nf = s_stk + kHullBlock * (2 * P + 2);                      // [64]
+    {
+        // coalesced load of the [64][P][2] slab, transposed into X / Y (8 loads per lane in flight)
+        const double* src = pts + p0 * 2 * P;
+        const int n = nprob * 2 * P;
+        const SlabIdx ix(2 * P);
+        for (int base = 0; base < n; base += 8 * kHullBlock) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = base + u * kHullBlock + t;
+                if (e < n) v[u] = src[e];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = base + u * kHullBlock + t;
+                if (e < n) {
+                    const int r = ix.row(e), c = e - r * 2 * P;
+                    (c & 1 ? s_y : s_x)[(c >> 1) * kHullBlock + r] = v[u];
+                }
+            }
+        }
     }
     __syncthreads();
-    const int64_t q = p0 + t;
-    if (t >= nprob) return;
-    const double* X = s_pts + t * srow;   // X[2*i], X[2*i+1]
-    double* Aq = Aout + q * M * 2;
-    double* bq = bout + q * M;
-    for (int i = 0; i < M; ++i) {
-        Aq[2 * i] = 0.0;
-        Aq[2 * i + 1] = 0.0;
-        bq[i] = 0.0;
-    }
-    const int n = npts[q];
-    if (n < 3 || n > P) {
-        nfout[q] = -1;
-        return;
-    }
-    // insertion sort by (x, y)
-    for (int i = 0; i < n; ++i) s_idx[i][t] = (unsigned char)i;
-    for (int i = 1; i < n; ++i) {
-        const int v = s_idx[i][t];
-        const double vx = X[2 * v], vy = X[2 * v + 1];
-        int j = i - 1;
-        while (j >= 0) {
-            const int u = s_idx[j][t];
-            const double ux = X[2 * u], uy = X[2 * u + 1];
-            if (!(ux > vx || (ux == vx && uy > vy))) break;
-            s_idx[j + 1][t] = (unsigned char)u;
-            --j;
+#define HX(i) s_x[(i) * kHullBlock + t]
+#define HY(i) s_y[(i) * kHullBlock + t]
+#define STK(i) s_stk[(i) * kHullBlock + t]
+    const int n = t < nprob ? npts[p0 + t] : 0;
+    int nf = -1;
+    if (t < nprob && n >= 3 && n <= P) {
+        for (int i = 1; i < n; ++i) {
+            const double vx = HX(i), vy = HY(i);
+            int j = i - 1;
+            while (j >= 0) {
+                const double ux = HX(j), uy = HY(j);
+                if (!(ux > vx || (ux == vx && uy > vy))) break;
+                HX(j + 1) = ux;
+                HY(j + 1) = uy;
+                --j;
+            }
+            HX(j + 1) = vx;
+            HY(j + 1) = vy;
         }
-        s_idx[j + 1][t] = (unsigned char)v;
-    }
-    // monotone chain
-    int k = 0;
-    for (int i = 0; i < n; ++i) {
-        const int v = s_idx[i][t];
-        const double px = X[2 * v], py = X[2 * v + 1];
-        while (k >= 2) {
-            const int a = s_H[k - 2][t], b = s_H[k - 1][t];
-            if (cross3(X[2 * a], X[2 * a + 1], X[2 * b], X[2 * b + 1], px, py) <= 0.0) --k;
-            else break;
+        // monotone chain; (ax, ay) = STK(k-2), (bx, by) = STK(k-1) when they exist
+        int k = 0;
+        double ax = 0.0, ay = 0.0, bx = 0.0, by = 0.0;
+        for (int i = 0; i < n; ++i) {
+            const double px = HX(i), py = HY(i);
+            while (k >= 2) {
+                if (cross3(ax, ay, bx, by, px, py) <= 0.0) {
+                    --k;
+                    bx = ax;
+                    by = ay;
+                    if (k >= 2) {
+                        const int a = STK(k - 2);
+                        ax = HX(a);
+                        ay = HY(a);
+                    }
+                } else {
+                    break;
+                }
+            }
+            STK(k++) = i;
+            ax = bx;
+            ay = by;
+            bx = px;
+            by = py;
         }
-        s_H[k++][t] = (unsigned char)v;
-    }
-    const int lower = k + 1;
-    for (int i = n - 2; i >= 0; --i) {
-        const int v = s_idx[i][t];
-        const double px = X[2 * v], py = X[2 * v + 1];
-        while (k >= lower) {
-            const int a = s_H[k - 2][t], b = s_H[k - 1][t];
-            if (cross3(X[2 * a], X[2 * a + 1], X[2 * b], X[2 * b + 1], px, py) <= 0.0) --k;
-            else break;
+        const int lower = k + 1;
+        for (int i = n - 2; i >= 0; --i) {
+            const double px = HX(i), py = HY(i);
+            while (k >= lower) {
+                if (cross3(ax, ay, bx, by, px, py) <= 0.0) {
+                    --k;
+                    bx = ax;
+                    by = ay;
+                    if (k >= 2) {
+                        const int a = STK(k - 2);
+                        ax = HX(a);
+                        ay = HY(a);
+                    }
+                } else {
+                    break;
+                }
+            }
+            STK(k++) = i;
+            ax = bx;
+            ay = by;
+            bx = px;
+            by = py;
         }
-        s_H[k++][t] = (unsigned char)v;
+        const int nv = k - 1;
+        if (nv >= 3 && nv <= M) nf = nv;
     }
-    const int nv = k - 1;
-    if (nv < 3 || nv > M) {
-        nfout[q] = -1;
-        return;
+#undef HX
+#undef HY
+#undef STK
+    if (t < nprob) {
+        s_nf[t] = nf;
+        nfout[p0 + t] = nf;
     }
-    for (int j = 0; j < nv; ++j) {
-        const int a = s_H[j][t], b = s_H[j + 1][t];
-        const double v0x = X[2 * a], v0y = X[2 * a + 1];
-        const double ex = X[2 * b] - v0x;
-        const double ey = X[2 * b + 1] - v0y;
-        const double len = sqrt(ex * ex + ey * ey);
-        const double nx = ey / len;
-        const double ny = (-ex) / len;
-        Aq[2 * j] = nx;
-        Aq[2 * j + 1] = ny;
-        bq[j] = nx * v0x + ny * v0y;
+    __syncthreads();
+    // phase 2: (polygon r, facet j) pairs in output order
+    const int npair = nprob * M;
+    double* Ab = Aout + p0 * 2 * M;
+    double* bb = bout + p0 * M;
+    const bool vecA = ((uintptr_t)Ab & 15) == 0;
+    const SlabIdx im(M);
+    for (int e = t; e < npair; e += kHullBlock) {
+        const int r = im.row(e), j = e - r * M;
+        double nx = 0.0, ny = 0.0, bj = 0.0;
+        if (j < s_nf[r]) {
+            const int a = s_stk[j * kHullBlock + r], b = s_stk[(j + 1) * kHullBlock + r];
+            const double v0x = s_x[a * kHullBlock + r], v0y = s_y[a * kHullBlock + r];
+            const double ex = s_x[b * kHullBlock + r] - v0x;
+            const double ey = s_y[b * kHullBlock + r] - v0y;
+            const double len = sqrt(ex * ex + ey * ey);
+            nx = ey / len;
+            ny = (-ex) / len;
+            bj = nx * v0x + ny * v0y;
+        }
+        if (vecA) {
+            *reinterpret_cast<double2*>(Ab + 2 * e) = make_double2(nx, ny);
+        } else {
+            Ab[2 * e] = nx;
+            Ab[2 * e + 1] = ny;
+        }
+        bb[e] = bj;
     }
-    nfout[q] = nv;
 }
 
 __global__ __launch_bounds__(256) void hull2d_contains_kernel(const double* __restrict__ A,
@@ -178,39 +249,48 @@ __global__ __launch_bounds__(256) void quintic_fit_kernel(const double* __restri
     c[5] = ((6.0 * h - 3.0 * (hv * T)) + 0.5 * (ha * T2)) / T5;
 }
 
-// one lane per (spline, query)
-__global__ __launch_bounds__(256) void quintic_eval_kernel(const double* __restrict__ kt,
-                                                           const double* __restrict__ coeffs,
-                                                           int32_t K1, int32_t D, int64_t S,
-                                                           const double* __restrict__ tq,
-                                                           int32_t Q, double* __restrict__ pva,
-                                                           int32_t* __restrict__ idx)
+// one lane per (spline, query); the workgroup's [256][3][D] output slab is staged in LDS and
+// written with coalesced 16-B stores (slab.h)
+constexpr int kEvalBlock = 256;
+
+__global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* __restrict__ kt,
+                                                                  const double* __restrict__ coeffs,
+                                                                  int32_t K1, int32_t D, int64_t S,
+                                                                  const double* __restrict__ tq,
+                                                                  int32_t Q, double* __restrict__ pva,
+                                                                  int32_t* __restrict__ idx)
 {
+    __shared__ double s_out[kEvalBlock * 9];
     const int K = K1 - 1;
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= S * Q) return;
-    const int64_t sp = gid / Q;
-    const double* t = kt + sp * K1;
-    const double tt = tq[gid];
-    int raw = -1;
-    for (int j = K1 - 1; j >= 0; --j)
-        if (t[j] <= tt) {
-            raw = j;
-            break;
+    const int W = 3 * D, SW = odd_stride(W);
+    const int64_t g0 = (int64_t)blockIdx.x * kEvalBlock;
+    const int64_t gid = g0 + threadIdx.x;
+    const int rows = (int)((S * Q - g0) < kEvalBlock ? (S * Q - g0) : kEvalBlock);
+    if (gid < S * Q) {
+        const int64_t sp = gid / Q;
+        const double* t = kt + sp * K1;
+        const double tt = tq[gid];
+        // last j with t_j <= t: a forward pass keeps the knot loads independent of each other
+        int raw = -1;
+        for (int j = 0; j < K1; ++j)
+            if (t[j] <= tt) raw = j;
+        idx[gid] = raw;
+        const int seg = raw < 0 ? 0 : (raw > K - 1 ? K - 1 : raw);
+        const double tau = tt - t[seg];
+        double* o = s_out + threadIdx.x * SW;
+        for (int d = 0; d < D; ++d) {
+            const double* c = coeffs + ((sp * K + seg) * D + d) * 6;
+            const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5];
+            const double p = c0 + tau * (c1 + tau * (c2 + tau * (c3 + tau * (c4 + tau * c5))));
+            const double v = c1 + tau * (2.0 * c2 + tau * (3.0 * c3 + tau * (4.0 * c4 + tau * (5.0 * c5))));
+            const double a = 2.0 * c2 + tau * (6.0 * c3 + tau * (12.0 * c4 + tau * (20.0 * c5)));
+            o[d] = p;
+            o[D + d] = v;
+            o[2 * D + d] = a;
         }
-    idx[gid] = raw;
-    const int seg = raw < 0 ? 0 : (raw > K - 1 ? K - 1 : raw);
-    const double tau = tt - t[seg];
-    for (int d = 0; d < D; ++d) {
-        const double* c = coeffs + ((sp * K + seg) * D + d) * 6;
-        const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5];
-        const double p = c0 + tau * (c1 + tau * (c2 + tau * (c3 + tau * (c4 + tau * c5))));
-        const double v = c1 + tau * (2.0 * c2 + tau * (3.0 * c3 + tau * (4.0 * c4 + tau * (5.0 * c5))));
-        const double a = 2.0 * c2 + tau * (6.0 * c3 + tau * (12.0 * c4 + tau * (20.0 * c5)));
-        pva[(gid * 3 + 0) * D + d] = p;
-        pva[(gid * 3 + 1) * D + d] = v;
-        pva[(gid * 3 + 2) * D + d] = a;
     }
+    __syncthreads();
+    slab_store<kEvalBlock, 4>(pva + g0 * W, W, s_out, SW, rows, W);
 }
 
 }  // namespace
@@ -220,8 +300,16 @@ blf_status launch_hull2d(const double* pts, const int32_t* npts, int32_t P, int3
 {
     if (batch == 0) return BLF_OK;
     const int64_t blocks = ceil_div(batch, kHullBlock);
-    hipLaunchKernelGGL(hull2d_kernel, dim3((unsigned)blocks), dim3(kHullBlock), 0, s, pts, npts, P,
-                       M, batch, A, b, nf);
+    const size_t lds = hull2d_lds_bytes(P, M);
+    if (lds > 65536) {
+        const blf_status st = check_hip(
+            hipFuncSetAttribute((const void*)hull2d_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            "hull2d_kernel LDS attribute");
+        if (st != BLF_OK) return st;
+    }
+    hipLaunchKernelGGL(hull2d_kernel, dim3((unsigned)blocks), dim3(kHullBlock), lds, s, pts, npts,
+                       P, M, batch, A, b, nf);
     return check_hip(hipGetLastError(), "hull2d_kernel launch");
 }
 
@@ -250,8 +338,8 @@ blf_status launch_quintic_eval(const double* kt, const double* coeffs, int32_t K
 {
     const int64_t n = S * Q;
     if (n == 0) return BLF_OK;
-    hipLaunchKernelGGL(quintic_eval_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, kt,
-                       coeffs, K1, D, S, tq, Q, pva, idx);
+    hipLaunchKernelGGL(quintic_eval_kernel, dim3((unsigned)ceil_div(n, kEvalBlock)),
+                       dim3(kEvalBlock), 0, s, kt, coeffs, K1, D, S, tq, Q, pva, idx);
     return check_hip(hipGetLastError(), "quintic_eval_kernel launch");
 }
 

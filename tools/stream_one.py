@@ -1,0 +1,46 @@
+"""Run one streaming kernel a few times (for rocprofv3 counter passes):
+  python tools/stream_one.py rollout|hull|quintic|contact"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bipedal-locomotion-framework_amd"))
+from blf import native  # noqa: E402
+
+
+def main(which):
+    h = native.Handle(0)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    rnd = lambda *s: torch.rand(*s, dtype=torch.float64, device=dev, generator=g)
+    if which == "rollout":
+        B, N = 262144, 100
+        xi0, om, vrp = rnd(B, 2), rnd(B, N) * 4 + 3, rnd(B, N, 2)
+        out = torch.empty(B, N + 1, 2, dtype=torch.float64, device=dev)
+        fn = lambda: h.dcm_euler_rollout(xi0, om, vrp, 0.02, out=out)
+    elif which == "hull":
+        P = 2 * 1024 * 1024
+        ang = rnd(P, 8) * 6.283
+        pts = torch.stack([torch.cos(ang), torch.sin(ang)], dim=-1).contiguous()
+        npts = torch.full((P,), 8, dtype=torch.int32, device=dev)
+        fn = lambda: h.hull2d_hrep(pts, npts, 8)
+    elif which == "quintic":
+        S, Q = 1024 * 1024, 32
+        kt = torch.cumsum(rnd(S, 3) + 0.1, dim=1).contiguous()
+        co = h.quintic_fit(kt, rnd(S, 3, 3, 3))
+        tq = (kt[:, :1] + (kt[:, 2:] - kt[:, :1]) * rnd(S, Q)).contiguous()
+        fn = lambda: h.quintic_eval(kt, co, tq)
+    else:
+        C = 4 * 1024 * 1024
+        prm = torch.tensor([0.12, 0.09, 2000.0, 100.0], dtype=torch.float64, device=dev)
+        tw, pose, null = rnd(C, 6), rnd(C, 12), rnd(C, 12)
+        fn = lambda: h.contact_model_eval(prm, tw, pose, null)
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
