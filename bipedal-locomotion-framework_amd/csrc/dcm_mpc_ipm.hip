@@ -163,15 +163,23 @@ __device__ __forceinline__ double bperm(int addr, double x)
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Fused forms used throughout (and in the same places by oracle/blf_oracle.c):
+//   FD2(a, b, c, d)    = a b + c d      as fma(a, b, c d)
+//   FD3(a, b, c, d, e) = a b + c d + e  as fma(a, b, fma(c, d, e))
+// fma is correctly rounded on both sides, so kernel and oracle stay bit-identical; it saves one
+// VALU op per product pair (the kernel is VALU-issue bound).
+#define FD2(a, b, c, d) fma((a), (b), (c) * (d))
+#define FD3(a, b, c, d, e) fma((a), (b), fma((c), (d), (e)))
+
 // 2x2 compose (row-major): n = a * b;  nc = a * c + e.
 #define COMPOSE(a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, e0, e1)                 \
     do {                                                                         \
-        const double n0_ = a0 * b0 + a1 * b2;                                    \
-        const double n1_ = a0 * b1 + a1 * b3;                                    \
-        const double n2_ = a2 * b0 + a3 * b2;                                    \
-        const double n3_ = a2 * b1 + a3 * b3;                                    \
-        const double m0_ = (a0 * c0 + a1 * c1) + e0;                             \
-        const double m1_ = (a2 * c0 + a3 * c1) + e1;                             \
+        const double n0_ = FD2(a0, b0, a1, b2);                                  \
+        const double n1_ = FD2(a0, b1, a1, b3);                                  \
+        const double n2_ = FD2(a2, b0, a3, b2);                                  \
+        const double n3_ = FD2(a2, b1, a3, b3);                                  \
+        const double m0_ = FD3(a0, c0, a1, c1, e0);                              \
+        const double m1_ = FD3(a2, c0, a3, c1, e1);                              \
         a0 = n0_; a1 = n1_; a2 = n2_; a3 = n3_; e0 = m0_; e1 = m1_;               \
     } while (0)
 
@@ -197,8 +205,8 @@ __device__ __forceinline__ void scan_backward(double g0, double g1, double g2, d
             if (wv == w) {
                 if (w < nwa - 1) {
                     const double b0 = bnd[kBnd * (w + 1) + kBV], b1 = bnd[kBnd * (w + 1) + kBV + 1];
-                    v0 = (g0 * b0 + g1 * b1) + c0;
-                    v1 = (g2 * b0 + g3 * b1) + c1;
+                    v0 = FD3(g0, b0, g1, b1, c0);
+                    v1 = FD3(g2, b0, g3, b1, c1);
                 }
                 if (lane == 0) { bnd[kBnd * w + kBV] = v0; bnd[kBnd * w + kBV + 1] = v1; }
             }
@@ -241,8 +249,8 @@ __device__ __forceinline__ void scan_forward(double g0, double g1, double g2, do
             if (wv == w) {
                 if (w > 0) {
                     const double b0 = bnd[kBnd * (w - 1) + kBX], b1 = bnd[kBnd * (w - 1) + kBX + 1];
-                    x0 = (g0 * b0 + g1 * b1) + c0;
-                    x1 = (g2 * b0 + g3 * b1) + c1;
+                    x0 = FD3(g0, b0, g1, b1, c0);
+                    x1 = FD3(g2, b0, g3, b1, c1);
                 }
                 if (lane == kWave - 1) { bnd[kBnd * w + kBX] = x0; bnd[kBnd * w + kBX + 1] = x1; }
             }
@@ -279,17 +287,17 @@ struct Mmat {
     double m00, m01, m10, m11;
     __device__ __forceinline__ explicit Mmat(const Knot& K)
     {
-        m00 = K.P00 * K.h00 + K.P01 * K.h01;
-        m01 = K.P00 * K.h01 + K.P01 * K.h11;
-        m10 = K.P01 * K.h00 + K.P11 * K.h01;
-        m11 = K.P01 * K.h01 + K.P11 * K.h11;
+        m00 = FD2(K.P00, K.h00, K.P01, K.h01);
+        m01 = FD2(K.P00, K.h01, K.P01, K.h11);
+        m10 = FD2(K.P01, K.h00, K.P11, K.h01);
+        m11 = FD2(K.P01, K.h01, K.P11, K.h11);
     }
 };
 
 // Facet residual rp_i = (a . r + s_i) - b_i.
 __device__ __forceinline__ double facet_rp(const Knot& K, double2 a, double bi, int i)
 {
-    return ((a.x * K.r0 + a.y * K.r1) + K.s[i]) - bi;
+    return (FD2(a.x, K.r0, a.y, K.r1) + K.s[i]) - bi;
 }
 
 // The affine slack / multiplier step of facet i for the VRP step (dra0, dra1) (oracle affine_step).
@@ -297,7 +305,7 @@ __device__ __forceinline__ void affine_step(const Knot& K, double2 a, double bi,
                                             double dra0, double dra1, double& ds, double& dl)
 {
     const double rpi = facet_rp(K, a, bi, i);
-    ds = (-rpi) - (a.x * dra0 + a.y * dra1);
+    ds = (-rpi) - FD2(a.x, dra0, a.y, dra1);
     dl = -((K.lam[i] * (K.s[i] + ds)) * is);
 }
 
@@ -318,21 +326,21 @@ __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P
             if (i >= mmax) break;
             if (i < K.m) {
                 const double2 a = A2[i * N + kx];
-                const double gr = a.x * K.r0 + a.y * K.r1;
+                const double gr = FD2(a.x, K.r0, a.y, K.r1);
                 const double rpi = (gr + K.s[i]) - bb[i * N + kx];
                 pres = nanmax(pres, fabs(rpi));
-                ck = ck + K.s[i] * K.lam[i];
-                rh0 = rh0 + a.x * K.lam[i];
-                rh1 = rh1 + a.y * K.lam[i];
+                ck = fma(K.s[i], K.lam[i], ck);
+                rh0 = fma(a.x, K.lam[i], rh0);
+                rh1 = fma(a.y, K.lam[i], rh1);
             }
         }
     }
     K.rh0 = rh0;
     K.rh1 = rh1;
-    const double dx0 = K.w * xk0 + (-K.w) * K.r0;
-    const double dk0 = (xk0 + dx0 * P.dt) - K.x0;
-    const double dx1 = K.w * xk1 + (-K.w) * K.r1;
-    const double dk1 = (xk1 + dx1 * P.dt) - K.x1;
+    const double dx0 = FD2(K.w, xk0, -K.w, K.r0);
+    const double dk0 = fma(dx0, P.dt, xk0) - K.x0;
+    const double dx1 = FD2(K.w, xk1, -K.w, K.r1);
+    const double dk1 = fma(dx1, P.dt, xk1) - K.x1;
     K.d0 = dk0;
     K.d1 = dk1;
     pres = nanmax(pres, fabs(dk0));
@@ -369,41 +377,41 @@ struct Rc {
 
 __device__ __forceinline__ bool rc_combine(Rc& e, const Rc& q)
 {
-    const double T00 = 1.0 + (e.g0 * q.h0 + e.g1 * q.h1);
-    const double T01 = e.g0 * q.h1 + e.g1 * q.h2;
-    const double T10 = e.g1 * q.h0 + e.g2 * q.h1;
-    const double T11 = 1.0 + (e.g1 * q.h1 + e.g2 * q.h2);
-    const double detT = T00 * T11 - T01 * T10;
+    const double T00 = FD3(e.g0, q.h0, e.g1, q.h1, 1.0);
+    const double T01 = FD2(e.g0, q.h1, e.g1, q.h2);
+    const double T10 = FD2(e.g1, q.h0, e.g2, q.h1);
+    const double T11 = FD3(e.g1, q.h1, e.g2, q.h2, 1.0);
+    const double detT = fma(T00, T11, -(T01 * T10));
     const bool ok = (detT > 0.0) && !__builtin_isinf(detT);
     const double it = 1.0 / detT;
     const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
-    const double U00 = Ti00 * e.a0 + Ti01 * e.a2;
-    const double U01 = Ti00 * e.a1 + Ti01 * e.a3;
-    const double U10 = Ti10 * e.a0 + Ti11 * e.a2;
-    const double U11 = Ti10 * e.a1 + Ti11 * e.a3;
-    const double V00 = q.a0 * Ti00 + q.a1 * Ti10;
-    const double V01 = q.a0 * Ti01 + q.a1 * Ti11;
-    const double V10 = q.a2 * Ti00 + q.a3 * Ti10;
-    const double V11 = q.a2 * Ti01 + q.a3 * Ti11;
-    const double X00 = V00 * e.g0 + V01 * e.g1;
-    const double X01 = V00 * e.g1 + V01 * e.g2;
-    const double X10 = V10 * e.g0 + V11 * e.g1;
-    const double X11 = V10 * e.g1 + V11 * e.g2;
-    const double Y00 = q.h0 * e.a0 + q.h1 * e.a2;
-    const double Y01 = q.h0 * e.a1 + q.h1 * e.a3;
-    const double Y10 = q.h1 * e.a0 + q.h2 * e.a2;
-    const double Y11 = q.h1 * e.a1 + q.h2 * e.a3;
+    const double U00 = FD2(Ti00, e.a0, Ti01, e.a2);
+    const double U01 = FD2(Ti00, e.a1, Ti01, e.a3);
+    const double U10 = FD2(Ti10, e.a0, Ti11, e.a2);
+    const double U11 = FD2(Ti10, e.a1, Ti11, e.a3);
+    const double V00 = FD2(q.a0, Ti00, q.a1, Ti10);
+    const double V01 = FD2(q.a0, Ti01, q.a1, Ti11);
+    const double V10 = FD2(q.a2, Ti00, q.a3, Ti10);
+    const double V11 = FD2(q.a2, Ti01, q.a3, Ti11);
+    const double X00 = FD2(V00, e.g0, V01, e.g1);
+    const double X01 = FD2(V00, e.g1, V01, e.g2);
+    const double X10 = FD2(V10, e.g0, V11, e.g1);
+    const double X11 = FD2(V10, e.g1, V11, e.g2);
+    const double Y00 = FD2(q.h0, e.a0, q.h1, e.a2);
+    const double Y01 = FD2(q.h0, e.a1, q.h1, e.a3);
+    const double Y10 = FD2(q.h1, e.a0, q.h2, e.a2);
+    const double Y11 = FD2(q.h1, e.a1, q.h2, e.a3);
     Rc r;
-    r.a0 = q.a0 * U00 + q.a1 * U10;
-    r.a1 = q.a0 * U01 + q.a1 * U11;
-    r.a2 = q.a2 * U00 + q.a3 * U10;
-    r.a3 = q.a2 * U01 + q.a3 * U11;
-    r.g0 = (X00 * q.a0 + X01 * q.a1) + q.g0;
-    r.g1 = (X00 * q.a2 + X01 * q.a3) + q.g1;
-    r.g2 = (X10 * q.a2 + X11 * q.a3) + q.g2;
-    r.h0 = (U00 * Y00 + U10 * Y10) + e.h0;
-    r.h1 = (U00 * Y01 + U10 * Y11) + e.h1;
-    r.h2 = (U01 * Y01 + U11 * Y11) + e.h2;
+    r.a0 = FD2(q.a0, U00, q.a1, U10);
+    r.a1 = FD2(q.a0, U01, q.a1, U11);
+    r.a2 = FD2(q.a2, U00, q.a3, U10);
+    r.a3 = FD2(q.a2, U01, q.a3, U11);
+    r.g0 = FD3(X00, q.a0, X01, q.a1, q.g0);
+    r.g1 = FD3(X00, q.a2, X01, q.a3, q.g1);
+    r.g2 = FD3(X10, q.a2, X11, q.a3, q.g2);
+    r.h0 = FD3(U00, Y00, U10, Y10, e.h0);
+    r.h1 = FD3(U00, Y01, U10, Y11, e.h1);
+    r.h2 = FD3(U01, Y01, U11, Y11, e.h2);
     e = r;
     return ok;
 }
@@ -411,25 +419,25 @@ __device__ __forceinline__ bool rc_combine(Rc& e, const Rc& q)
 __device__ __forceinline__ bool rc_apply(const Rc& e, double P00, double P01, double P11,
                                          double& o00, double& o01, double& o11)
 {
-    const double S00 = 1.0 + (e.g0 * P00 + e.g1 * P01);
-    const double S01 = e.g0 * P01 + e.g1 * P11;
-    const double S10 = e.g1 * P00 + e.g2 * P01;
-    const double S11 = 1.0 + (e.g1 * P01 + e.g2 * P11);
-    const double detS = S00 * S11 - S01 * S10;
+    const double S00 = FD3(e.g0, P00, e.g1, P01, 1.0);
+    const double S01 = FD2(e.g0, P01, e.g1, P11);
+    const double S10 = FD2(e.g1, P00, e.g2, P01);
+    const double S11 = FD3(e.g1, P01, e.g2, P11, 1.0);
+    const double detS = fma(S00, S11, -(S01 * S10));
     const bool ok = (detS > 0.0) && !__builtin_isinf(detS);
     const double is = 1.0 / detS;
     const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
-    const double W00 = P00 * Si00 + P01 * Si10;
-    const double W01 = P00 * Si01 + P01 * Si11;
-    const double W10 = P01 * Si00 + P11 * Si10;
-    const double W11 = P01 * Si01 + P11 * Si11;
-    const double Z00 = W00 * e.a0 + W01 * e.a2;
-    const double Z01 = W00 * e.a1 + W01 * e.a3;
-    const double Z10 = W10 * e.a0 + W11 * e.a2;
-    const double Z11 = W10 * e.a1 + W11 * e.a3;
-    o00 = (e.a0 * Z00 + e.a2 * Z10) + e.h0;
-    o01 = (e.a0 * Z01 + e.a2 * Z11) + e.h1;
-    o11 = (e.a1 * Z01 + e.a3 * Z11) + e.h2;
+    const double W00 = FD2(P00, Si00, P01, Si10);
+    const double W01 = FD2(P00, Si01, P01, Si11);
+    const double W10 = FD2(P01, Si00, P11, Si10);
+    const double W11 = FD2(P01, Si01, P11, Si11);
+    const double Z00 = FD2(W00, e.a0, W01, e.a2);
+    const double Z01 = FD2(W00, e.a1, W01, e.a3);
+    const double Z10 = FD2(W10, e.a0, W11, e.a2);
+    const double Z11 = FD2(W10, e.a1, W11, e.a3);
+    o00 = FD3(e.a0, Z00, e.a2, Z10, e.h0);
+    o01 = FD3(e.a0, Z01, e.a2, Z11, e.h1);
+    o11 = FD3(e.a1, Z01, e.a3, Z11, e.h2);
     return ok;
 }
 
@@ -444,7 +452,7 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
     const double b2 = K.be * K.be;
     double E00 = 0.0, E01 = 0.0, E11 = 0.0;
     if (own) {
-        const double detRW = (P.Rw0 * P.Rw1 + (P.Rw1 * W00 + P.Rw0 * W11)) + dW;
+        const double detRW = fma(P.Rw0, P.Rw1, FD2(P.Rw1, W00, P.Rw0, W11)) + dW;
         const double ie = b2 / detRW;
         E00 = (P.Rw1 + W11) * ie;
         E01 = -(W01 * ie);
@@ -509,14 +517,14 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
     K.P01 = P01;
     K.P11 = P11;
     if (own) {
-        const double B00 = P.Rw0 + b2 * P00;
+        const double B00 = fma(b2, P00, P.Rw0);
         const double B01 = b2 * P01;
-        const double B11 = P.Rw1 + b2 * P11;
+        const double B11 = fma(b2, P11, P.Rw1);
         const double H00 = B00 + W00;
         const double H01 = B01 + W01;
         const double H11 = B11 + W11;
-        const double detB = B00 * B11 - B01 * B01;
-        const double trW = (B11 * W00 + B00 * W11) - 2.0 * (B01 * W01);
+        const double detB = fma(B00, B11, -(B01 * B01));
+        const double trW = FD2(B11, W00, B00, W11) - 2.0 * (B01 * W01);
         const double det = (detB + trW) + dW;
         if (!(det > 0.0) || __builtin_isinf(det)) ok = false;
         const double idet = 1.0 / det;
@@ -539,16 +547,16 @@ __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, doubl
     double G00 = 0.0, G01 = 0.0, G10 = 0.0, G11 = 0.0, c0 = 0.0, c1 = 0.0, y0 = 0.0, y1 = 0.0;
     if (own) {
         const Mmat Mm(K);
-        y0 = K.qx0 + (K.P00 * K.d0 + K.P01 * K.d1);
-        y1 = K.qx1 + (K.P01 * K.d0 + K.P11 * K.d1);
-        const double Mg0 = Mm.m00 * g0 + Mm.m01 * g1;
-        const double Mg1 = Mm.m10 * g0 + Mm.m11 * g1;
-        G00 = K.al * (1.0 - b2 * Mm.m00);
+        y0 = FD3(K.P00, K.d0, K.P01, K.d1, K.qx0);
+        y1 = FD3(K.P01, K.d0, K.P11, K.d1, K.qx1);
+        const double Mg0 = FD2(Mm.m00, g0, Mm.m01, g1);
+        const double Mg1 = FD2(Mm.m10, g0, Mm.m11, g1);
+        G00 = K.al * fma(-b2, Mm.m00, 1.0);
         G01 = -(K.al * (b2 * Mm.m01));
         G10 = -(K.al * (b2 * Mm.m10));
-        G11 = K.al * (1.0 - b2 * Mm.m11);
-        c0 = (G00 * y0 + G01 * y1) + ab * Mg0;
-        c1 = (G10 * y0 + G11 * y1) + ab * Mg1;
+        G11 = K.al * fma(-b2, Mm.m11, 1.0);
+        c0 = FD3(G00, y0, G01, y1, ab * Mg0);
+        c1 = FD3(G10, y0, G11, y1, ab * Mg1);
     }
     double vn0, vn1;
     scan_backward<NW>(G00, G01, G10, G11, c0, c1, bnd, nwa, wv, lane, vn0, vn1);
@@ -556,18 +564,18 @@ __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, doubl
     if (own) {
         const double t0 = y0 + vn0;
         const double t1 = y1 + vn1;
-        const double hu0 = g0 - K.be * t0;
-        const double hu1 = g1 - K.be * t1;
-        k0 = -(K.h00 * hu0 + K.h01 * hu1);
-        k1 = -(K.h01 * hu0 + K.h11 * hu1);
-        f0 = K.d0 - K.be * k0;
-        f1 = K.d1 - K.be * k1;
+        const double hu0 = fma(-K.be, t0, g0);
+        const double hu1 = fma(-K.be, t1, g1);
+        k0 = -FD2(K.h00, hu0, K.h01, hu1);
+        k1 = -FD2(K.h01, hu0, K.h11, hu1);
+        f0 = fma(-K.be, k0, K.d0);
+        f1 = fma(-K.be, k1, K.d1);
     }
     double xk0, xk1;
     scan_forward<NW>(G00, G10, G01, G11, f0, f1, bnd, nwa, wv, lane, dx0, dx1, xk0, xk1);
     const Mmat Mm(K);
-    dr0 = ab * (Mm.m00 * xk0 + Mm.m10 * xk1) + k0;
-    dr1 = ab * (Mm.m01 * xk0 + Mm.m11 * xk1) + k1;
+    dr0 = fma(ab, FD2(Mm.m00, xk0, Mm.m10, xk1), k0);
+    dr1 = fma(ab, FD2(Mm.m01, xk0, Mm.m11, xk1), k1);
 }
 
 // Publishes xi_{k+1} of lane 63 for the next wavefront's lane 0 (read after the next barrier).
@@ -655,8 +663,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         double f0 = 0.0, f1 = 0.0;
         if (own) {
             if (k == 0) {
-                f0 = K.al * xi00 - K.be * K.r0;
-                f1 = K.al * xi01 - K.be * K.r1;
+                f0 = fma(K.al, xi00, -(K.be * K.r0));
+                f1 = fma(K.al, xi01, -(K.be * K.r1));
             } else {
                 f0 = -(K.be * K.r0);
                 f1 = -(K.be * K.r1);
@@ -697,7 +705,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 if (i >= mmax) break;
                 if (i < K.m) {
                     const double2 a = L.A2[i * N + k];
-                    const double gr = a.x * K.r0 + a.y * K.r1;
+                    const double gr = FD2(a.x, K.r0, a.y, K.r1);
                     const double sl = L.bb[i * N + k] - gr;
                     K.s[i] = sl > 1e-2 ? sl : 1e-2;
                     K.lam[i] = 1.0;
@@ -717,8 +725,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             if (own) {
                 const double nu0 = K.qx0 + vn0;
                 const double nu1 = K.qx1 + vn1;
-                dres = nanmax(dres, fabs(K.rh0 - K.be * nu0));
-                dres = nanmax(dres, fabs(K.rh1 - K.be * nu1));
+                dres = nanmax(dres, fabs(fma(-K.be, nu0, K.rh0)));
+                dres = nanmax(dres, fabs(fma(-K.be, nu1, K.rh1)));
             }
         }
         dres = R.nanmax_(dres);
@@ -760,13 +768,13 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         const double sg = K.lam[i] * is;
                         const double t0 = sg * a.x;
                         const double t1 = sg * a.y;
-                        W00 = W00 + t0 * a.x;
-                        W01 = W01 + t0 * a.y;
-                        W11 = W11 + t1 * a.y;
+                        W00 = fma(t0, a.x, W00);
+                        W01 = fma(t0, a.y, W01);
+                        W11 = fma(t1, a.y, W11);
                         const double rpi = facet_rp(K, a, L.bb[i * N + kx], i);
-                        const double e = (K.lam[i] * rpi - K.s[i] * K.lam[i]) * is;
-                        g0 = g0 + a.x * e;
-                        g1 = g1 + a.y * e;
+                        const double e = fma(K.lam[i], rpi, -(K.s[i] * K.lam[i])) * is;
+                        g0 = fma(a.x, e, g0);
+                        g1 = fma(a.y, e, g1);
                     }
                 }
                 // sg_i = lam_i / s_i is recomputed from the stored 1/s (bit-identical) rather than
@@ -782,8 +790,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         for (int j = 0; j < i; ++j) {
                             const double2 aj = L.A2[j * N + ki];
                             const double sgj = K.lam[j] * L.IS[j * N + ki];
-                            const double cr = ai.x * aj.y - ai.y * aj.x;
-                            dW = dW + (sgi * sgj) * (cr * cr);
+                            const double cr = fma(ai.x, aj.y, -(ai.y * aj.x));
+                            dW = fma(sgi * sgj, cr * cr, dW);
                         }
                     }
                 }
@@ -829,7 +837,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         double ds, dl;
                         affine_step(K, L.A2[i * N + kx], L.bb[i * N + kx], L.IS[i * N + kx], i, dra0,
                                     dra1, ds, dl);
-                        ck = ck + (K.s[i] + a_aff * ds) * (K.lam[i] + a_aff * dl);
+                        ck = fma(fma(a_aff, ds, K.s[i]), fma(a_aff, dl, K.lam[i]), ck);
                     }
                 }
             }
@@ -856,11 +864,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         const double is = L.IS[i * N + kx];
                         double ds, dl;
                         affine_step(K, a, bi, is, i, dra0, dra1, ds, dl);
-                        const double rc = (K.s[i] * K.lam[i] + ds * dl) - sigma_mu;
+                        const double rc = FD2(K.s[i], K.lam[i], ds, dl) - sigma_mu;
                         const double rpi = facet_rp(K, a, bi, i);
-                        const double e = (K.lam[i] * rpi - rc) * is;
-                        g0 = g0 + a.x * e;
-                        g1 = g1 + a.y * e;
+                        const double e = fma(K.lam[i], rpi, -rc) * is;
+                        g0 = fma(a.x, e, g0);
+                        g1 = fma(a.y, e, g1);
                     }
                 }
             }
@@ -880,10 +888,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         const double is = L.IS[i * N + kx];
                         double ads, adl;
                         affine_step(K, a, bi, is, i, dra0, dra1, ads, adl);
-                        const double rc = (K.s[i] * K.lam[i] + ads * adl) - sigma_mu;
+                        const double rc = FD2(K.s[i], K.lam[i], ads, adl) - sigma_mu;
                         const double rpi = facet_rp(K, a, bi, i);
-                        const double ds = (-rpi) - (a.x * dr0 + a.y * dr1);
-                        const double dl = ((-rc) - K.lam[i] * ds) * is;
+                        const double ds = (-rpi) - FD2(a.x, dr0, a.y, dr1);
+                        const double dl = fma(-K.lam[i], ds, -rc) * is;
                         if (ds < 0.0) q = keepmax(q, (-ds) * is);
                         if (dl < 0.0) q = keepmax(q, (-dl) / K.lam[i]);
                         L.IS[i * N + kx] = dl;   // 1/s is dead now: keep the multiplier step
@@ -900,15 +908,15 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i >= mmax) break;
                     if (i < K.m) {
                         const double2 fa = L.A2[i * N + kx];
-                        const double ds = (-facet_rp(K, fa, L.bb[i * N + kx], i)) - (fa.x * dr0 + fa.y * dr1);
-                        K.s[i] = K.s[i] + a * ds;
-                        K.lam[i] = K.lam[i] + a * L.IS[i * N + kx];
+                        const double ds = (-facet_rp(K, fa, L.bb[i * N + kx], i)) - FD2(fa.x, dr0, fa.y, dr1);
+                        K.s[i] = fma(a, ds, K.s[i]);
+                        K.lam[i] = fma(a, L.IS[i * N + kx], K.lam[i]);
                     }
                 }
-                K.r0 = K.r0 + a * dr0;   // after the facet steps, which use the old r
-                K.r1 = K.r1 + a * dr1;
-                K.x0 = K.x0 + a * dx0;
-                K.x1 = K.x1 + a * dx1;
+                K.r0 = fma(a, dr0, K.r0);   // after the facet steps, which use the old r
+                K.r1 = fma(a, dr1, K.r1);
+                K.x0 = fma(a, dx0, K.x0);
+                K.x1 = fma(a, dx1, K.x1);
             }
             publish_xi<NW>(K, bnd, wv, lane);
             dres = dres * (1.0 - a);

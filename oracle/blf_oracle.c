@@ -301,6 +301,12 @@ double orc_wave_tree_sum(const double* c, int n)
 #define MF 8
 #define WV 64
 
+/* Fused forms, used in exactly the places the kernel uses them (csrc/dcm_mpc_ipm.hip):
+ *   FD2(a, b, c, d) = a b + c d as fma(a, b, c d);  FD3(a, b, c, d, e) = fma(a, b, fma(c, d, e)).
+ * C fma() is correctly rounded like v_fma_f64, so oracle and kernel stay bit-identical. */
+#define FD2(a, b, c, d) fma((a), (b), (c) * (d))
+#define FD3(a, b, c, d, e) fma((a), (b), fma((c), (d), (e)))
+
 /* Working state of one QP solve.  Per-knot arrays are indexed by the knot k = 64 w + lane: the
  * device runs one thread per knot, NW = ceil(N / 64) wavefronts per QP. */
 typedef struct {
@@ -338,8 +344,8 @@ static void scan_backward(dcm_ws* w, const double* G, const double* c)
         for (int k = N - 1; k >= 0; --k) {
             const double* g = G + 4 * k;
             const double vn0 = w->v[2 * (k + 1)], vn1 = w->v[2 * (k + 1) + 1];
-            w->v[2 * k] = (g[0] * vn0 + g[1] * vn1) + c[2 * k];
-            w->v[2 * k + 1] = (g[2] * vn0 + g[3] * vn1) + c[2 * k + 1];
+            w->v[2 * k] = FD3(g[0], vn0, g[1], vn1, c[2 * k]);
+            w->v[2 * k + 1] = FD3(g[2], vn0, g[3], vn1, c[2 * k + 1]);
         }
         return;
     }
@@ -356,12 +362,12 @@ static void scan_backward(dcm_ws* w, const double* G, const double* c)
                     const double* a = g[l];
                     const double* bq = g[l + dd];
                     const double* ce = e[l + dd];
-                    ng[l][0] = a[0] * bq[0] + a[1] * bq[2];
-                    ng[l][1] = a[0] * bq[1] + a[1] * bq[3];
-                    ng[l][2] = a[2] * bq[0] + a[3] * bq[2];
-                    ng[l][3] = a[2] * bq[1] + a[3] * bq[3];
-                    ne[l][0] = (a[0] * ce[0] + a[1] * ce[1]) + e[l][0];
-                    ne[l][1] = (a[2] * ce[0] + a[3] * ce[1]) + e[l][1];
+                    ng[l][0] = FD2(a[0], bq[0], a[1], bq[2]);
+                    ng[l][1] = FD2(a[0], bq[1], a[1], bq[3]);
+                    ng[l][2] = FD2(a[2], bq[0], a[3], bq[2]);
+                    ng[l][3] = FD2(a[2], bq[1], a[3], bq[3]);
+                    ne[l][0] = FD3(a[0], ce[0], a[1], ce[1], e[l][0]);
+                    ne[l][1] = FD3(a[2], ce[0], a[3], ce[1], e[l][1]);
                 } else {
                     memcpy(ng[l], g[l], sizeof(ng[l]));
                     memcpy(ne[l], e[l], sizeof(ne[l]));
@@ -378,8 +384,8 @@ static void scan_backward(dcm_ws* w, const double* G, const double* c)
                 w->v[2 * k + 1] = e[l][1];
             } else {
                 const double vn0 = w->v[2 * WV * (wv + 1)], vn1 = w->v[2 * WV * (wv + 1) + 1];
-                w->v[2 * k] = (g[l][0] * vn0 + g[l][1] * vn1) + e[l][0];
-                w->v[2 * k + 1] = (g[l][2] * vn0 + g[l][3] * vn1) + e[l][1];
+                w->v[2 * k] = FD3(g[l][0], vn0, g[l][1], vn1, e[l][0]);
+                w->v[2 * k + 1] = FD3(g[l][2], vn0, g[l][3], vn1, e[l][1]);
             }
         }
     }
@@ -399,8 +405,8 @@ static void scan_forward(dcm_ws* w, const double* F, int transpose, const double
             const double* F_ = F + 4 * k;
             const double f01 = transpose ? F_[2] : F_[1], f10 = transpose ? F_[1] : F_[2];
             const double x0 = w->x[2 * k], x1 = w->x[2 * k + 1];
-            w->x[2 * (k + 1)] = (F_[0] * x0 + f01 * x1) + f[2 * k];
-            w->x[2 * (k + 1) + 1] = (f10 * x0 + F_[3] * x1) + f[2 * k + 1];
+            w->x[2 * (k + 1)] = FD3(F_[0], x0, f01, x1, f[2 * k]);
+            w->x[2 * (k + 1) + 1] = FD3(f10, x0, F_[3], x1, f[2 * k + 1]);
         }
         return;
     }
@@ -427,12 +433,12 @@ static void scan_forward(dcm_ws* w, const double* F, int transpose, const double
                     const double* a = g[l];
                     const double* bq = g[l - dd];
                     const double* ce = e[l - dd];
-                    ng[l][0] = a[0] * bq[0] + a[1] * bq[2];
-                    ng[l][1] = a[0] * bq[1] + a[1] * bq[3];
-                    ng[l][2] = a[2] * bq[0] + a[3] * bq[2];
-                    ng[l][3] = a[2] * bq[1] + a[3] * bq[3];
-                    ne[l][0] = (a[0] * ce[0] + a[1] * ce[1]) + e[l][0];
-                    ne[l][1] = (a[2] * ce[0] + a[3] * ce[1]) + e[l][1];
+                    ng[l][0] = FD2(a[0], bq[0], a[1], bq[2]);
+                    ng[l][1] = FD2(a[0], bq[1], a[1], bq[3]);
+                    ng[l][2] = FD2(a[2], bq[0], a[3], bq[2]);
+                    ng[l][3] = FD2(a[2], bq[1], a[3], bq[3]);
+                    ne[l][0] = FD3(a[0], ce[0], a[1], ce[1], e[l][0]);
+                    ne[l][1] = FD3(a[2], ce[0], a[3], ce[1], e[l][1]);
                 } else {
                     memcpy(ng[l], g[l], sizeof(ng[l]));
                     memcpy(ne[l], e[l], sizeof(ne[l]));
@@ -449,8 +455,8 @@ static void scan_forward(dcm_ws* w, const double* F, int transpose, const double
                 w->x[2 * (k + 1) + 1] = e[l][1];
             } else {
                 const double x0 = w->x[2 * WV * wv], x1 = w->x[2 * WV * wv + 1];
-                w->x[2 * (k + 1)] = (g[l][0] * x0 + g[l][1] * x1) + e[l][0];
-                w->x[2 * (k + 1) + 1] = (g[l][2] * x0 + g[l][3] * x1) + e[l][1];
+                w->x[2 * (k + 1)] = FD3(g[l][0], x0, g[l][1], x1, e[l][0]);
+                w->x[2 * (k + 1) + 1] = FD3(g[l][2], x0, g[l][3], x1, e[l][1]);
             }
         }
     }
@@ -474,12 +480,12 @@ static double dcm_residuals(dcm_ws* w, int use_facets)
         for (int i = 0; i < m; ++i) {
             const double* a = w->A + (k * M + i) * 2;
             const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
-            const double gr = a[0] * r0 + a[1] * r1;
+            const double gr = FD2(a[0], r0, a[1], r1);
             const double rpi = (gr + si) - w->b[k * M + i];
             pres = nanmax(pres, fabs(rpi));
-            ck = ck + si * li;
-            rh0 = rh0 + a[0] * li;
-            rh1 = rh1 + a[1] * li;
+            ck = fma(si, li, ck);
+            rh0 = fma(a[0], li, rh0);
+            rh1 = fma(a[1], li, rh1);
         }
         w->c[k] = ck;
         w->rh[2 * k] = rh0;
@@ -488,10 +494,10 @@ static double dcm_residuals(dcm_ws* w, int use_facets)
         {
             const double x0 = w->xi[2 * k], x1 = w->xi[2 * k + 1];
             const double y0 = w->xi[2 * (k + 1)], y1 = w->xi[2 * (k + 1) + 1];
-            const double dx0 = om * x0 + (-om) * r0;
-            const double dk0 = (x0 + dx0 * w->dt) - y0;
-            const double dx1 = om * x1 + (-om) * r1;
-            const double dk1 = (x1 + dx1 * w->dt) - y1;
+            const double dx0 = FD2(om, x0, -om, r0);
+            const double dk0 = fma(dx0, w->dt, x0) - y0;
+            const double dx1 = FD2(om, x1, -om, r1);
+            const double dk1 = fma(dx1, w->dt, x1) - y1;
             w->d[2 * k] = dk0;
             w->d[2 * k + 1] = dk1;
             pres = nanmax(pres, fabs(dk0));
@@ -519,41 +525,41 @@ static int rc_combine(rc_el* e1, const rc_el* e2)
 {
     const double* A1 = e1->a; const double* G1 = e1->g; const double* H1 = e1->h;
     const double* A2 = e2->a; const double* G2 = e2->g; const double* H2 = e2->h;
-    const double T00 = 1.0 + (G1[0] * H2[0] + G1[1] * H2[1]);
-    const double T01 = G1[0] * H2[1] + G1[1] * H2[2];
-    const double T10 = G1[1] * H2[0] + G1[2] * H2[1];
-    const double T11 = 1.0 + (G1[1] * H2[1] + G1[2] * H2[2]);
-    const double detT = T00 * T11 - T01 * T10;
+    const double T00 = FD3(G1[0], H2[0], G1[1], H2[1], 1.0);
+    const double T01 = FD2(G1[0], H2[1], G1[1], H2[2]);
+    const double T10 = FD2(G1[1], H2[0], G1[2], H2[1]);
+    const double T11 = FD3(G1[1], H2[1], G1[2], H2[2], 1.0);
+    const double detT = fma(T00, T11, -(T01 * T10));
     const int ok = (detT > 0.0) && !isinf(detT);
     const double it = 1.0 / detT;
     const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
-    const double U00 = Ti00 * A1[0] + Ti01 * A1[2];
-    const double U01 = Ti00 * A1[1] + Ti01 * A1[3];
-    const double U10 = Ti10 * A1[0] + Ti11 * A1[2];
-    const double U11 = Ti10 * A1[1] + Ti11 * A1[3];
-    const double V00 = A2[0] * Ti00 + A2[1] * Ti10;
-    const double V01 = A2[0] * Ti01 + A2[1] * Ti11;
-    const double V10 = A2[2] * Ti00 + A2[3] * Ti10;
-    const double V11 = A2[2] * Ti01 + A2[3] * Ti11;
-    const double X00 = V00 * G1[0] + V01 * G1[1];
-    const double X01 = V00 * G1[1] + V01 * G1[2];
-    const double X10 = V10 * G1[0] + V11 * G1[1];
-    const double X11 = V10 * G1[1] + V11 * G1[2];
-    const double Y00 = H2[0] * A1[0] + H2[1] * A1[2];
-    const double Y01 = H2[0] * A1[1] + H2[1] * A1[3];
-    const double Y10 = H2[1] * A1[0] + H2[2] * A1[2];
-    const double Y11 = H2[1] * A1[1] + H2[2] * A1[3];
+    const double U00 = FD2(Ti00, A1[0], Ti01, A1[2]);
+    const double U01 = FD2(Ti00, A1[1], Ti01, A1[3]);
+    const double U10 = FD2(Ti10, A1[0], Ti11, A1[2]);
+    const double U11 = FD2(Ti10, A1[1], Ti11, A1[3]);
+    const double V00 = FD2(A2[0], Ti00, A2[1], Ti10);
+    const double V01 = FD2(A2[0], Ti01, A2[1], Ti11);
+    const double V10 = FD2(A2[2], Ti00, A2[3], Ti10);
+    const double V11 = FD2(A2[2], Ti01, A2[3], Ti11);
+    const double X00 = FD2(V00, G1[0], V01, G1[1]);
+    const double X01 = FD2(V00, G1[1], V01, G1[2]);
+    const double X10 = FD2(V10, G1[0], V11, G1[1]);
+    const double X11 = FD2(V10, G1[1], V11, G1[2]);
+    const double Y00 = FD2(H2[0], A1[0], H2[1], A1[2]);
+    const double Y01 = FD2(H2[0], A1[1], H2[1], A1[3]);
+    const double Y10 = FD2(H2[1], A1[0], H2[2], A1[2]);
+    const double Y11 = FD2(H2[1], A1[1], H2[2], A1[3]);
     rc_el r;
-    r.a[0] = A2[0] * U00 + A2[1] * U10;
-    r.a[1] = A2[0] * U01 + A2[1] * U11;
-    r.a[2] = A2[2] * U00 + A2[3] * U10;
-    r.a[3] = A2[2] * U01 + A2[3] * U11;
-    r.g[0] = (X00 * A2[0] + X01 * A2[1]) + G2[0];
-    r.g[1] = (X00 * A2[2] + X01 * A2[3]) + G2[1];
-    r.g[2] = (X10 * A2[2] + X11 * A2[3]) + G2[2];
-    r.h[0] = (U00 * Y00 + U10 * Y10) + H1[0];
-    r.h[1] = (U00 * Y01 + U10 * Y11) + H1[1];
-    r.h[2] = (U01 * Y01 + U11 * Y11) + H1[2];
+    r.a[0] = FD2(A2[0], U00, A2[1], U10);
+    r.a[1] = FD2(A2[0], U01, A2[1], U11);
+    r.a[2] = FD2(A2[2], U00, A2[3], U10);
+    r.a[3] = FD2(A2[2], U01, A2[3], U11);
+    r.g[0] = FD3(X00, A2[0], X01, A2[1], G2[0]);
+    r.g[1] = FD3(X00, A2[2], X01, A2[3], G2[1]);
+    r.g[2] = FD3(X10, A2[2], X11, A2[3], G2[2]);
+    r.h[0] = FD3(U00, Y00, U10, Y10, H1[0]);
+    r.h[1] = FD3(U00, Y01, U10, Y11, H1[1]);
+    r.h[2] = FD3(U01, Y01, U11, Y11, H1[2]);
     *e1 = r;
     return ok;
 }
@@ -562,25 +568,25 @@ static int rc_combine(rc_el* e1, const rc_el* e2)
 static int rc_apply(const rc_el* e, double P00, double P01, double P11, double* out)
 {
     const double* A = e->a; const double* G = e->g; const double* H = e->h;
-    const double S00 = 1.0 + (G[0] * P00 + G[1] * P01);
-    const double S01 = G[0] * P01 + G[1] * P11;
-    const double S10 = G[1] * P00 + G[2] * P01;
-    const double S11 = 1.0 + (G[1] * P01 + G[2] * P11);
-    const double detS = S00 * S11 - S01 * S10;
+    const double S00 = FD3(G[0], P00, G[1], P01, 1.0);
+    const double S01 = FD2(G[0], P01, G[1], P11);
+    const double S10 = FD2(G[1], P00, G[2], P01);
+    const double S11 = FD3(G[1], P01, G[2], P11, 1.0);
+    const double detS = fma(S00, S11, -(S01 * S10));
     const int ok = (detS > 0.0) && !isinf(detS);
     const double is = 1.0 / detS;
     const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
-    const double W00 = P00 * Si00 + P01 * Si10;
-    const double W01 = P00 * Si01 + P01 * Si11;
-    const double W10 = P01 * Si00 + P11 * Si10;
-    const double W11 = P01 * Si01 + P11 * Si11;
-    const double Z00 = W00 * A[0] + W01 * A[2];
-    const double Z01 = W00 * A[1] + W01 * A[3];
-    const double Z10 = W10 * A[0] + W11 * A[2];
-    const double Z11 = W10 * A[1] + W11 * A[3];
-    out[0] = (A[0] * Z00 + A[2] * Z10) + H[0];
-    out[1] = (A[0] * Z01 + A[2] * Z11) + H[1];
-    out[2] = (A[1] * Z01 + A[3] * Z11) + H[2];
+    const double W00 = FD2(P00, Si00, P01, Si10);
+    const double W01 = FD2(P00, Si01, P01, Si11);
+    const double W10 = FD2(P01, Si00, P11, Si10);
+    const double W11 = FD2(P01, Si01, P11, Si11);
+    const double Z00 = FD2(W00, A[0], W01, A[2]);
+    const double Z01 = FD2(W00, A[1], W01, A[3]);
+    const double Z10 = FD2(W10, A[0], W11, A[2]);
+    const double Z11 = FD2(W10, A[1], W11, A[3]);
+    out[0] = FD3(A[0], Z00, A[2], Z10, H[0]);
+    out[1] = FD3(A[0], Z01, A[2], Z11, H[1]);
+    out[2] = FD3(A[1], Z01, A[3], Z11, H[2]);
     return ok;
 }
 
@@ -598,7 +604,7 @@ static int dcm_factor(dcm_ws* w)
     int ok = 1;
     for (int k = 0; k < N; ++k) {
         const double* Wk = w->W + 4 * k;
-        const double detRW = (w->Rw0 * w->Rw1 + (w->Rw1 * Wk[0] + w->Rw0 * Wk[2])) + Wk[3];
+        const double detRW = fma(w->Rw0, w->Rw1, FD2(w->Rw1, Wk[0], w->Rw0, Wk[2])) + Wk[3];
         const double ie = w->b2[k] / detRW;
         w->E[3 * k] = (w->Rw1 + Wk[2]) * ie;
         w->E[3 * k + 1] = -(Wk[1] * ie);
@@ -660,31 +666,31 @@ static int dcm_factor(dcm_ws* w)
         const double* Wk = w->W + 4 * k;
         const double b2 = w->b2[k];
         /* det H = det B + tr(adj(B) W) + det W, B = R + b2 P: no cancellation for huge W */
-        const double B00 = w->Rw0 + b2 * P00;
+        const double B00 = fma(b2, P00, w->Rw0);
         const double B01 = b2 * P01;
-        const double B11 = w->Rw1 + b2 * P11;
+        const double B11 = fma(b2, P11, w->Rw1);
         const double H00 = B00 + Wk[0];
         const double H01 = B01 + Wk[1];
         const double H11 = B11 + Wk[2];
-        const double detB = B00 * B11 - B01 * B01;
-        const double trW = (B11 * Wk[0] + B00 * Wk[2]) - 2.0 * (B01 * Wk[1]);
+        const double detB = fma(B00, B11, -(B01 * B01));
+        const double trW = FD2(B11, Wk[0], B00, Wk[2]) - 2.0 * (B01 * Wk[1]);
         const double det = (detB + trW) + Wk[3];
         if (!(det > 0.0) || isinf(det)) ok = 0;
         const double idet = 1.0 / det;
         const double h00 = H11 * idet, h01 = -(H01 * idet), h11 = H00 * idet;
         w->h[3 * k] = h00; w->h[3 * k + 1] = h01; w->h[3 * k + 2] = h11;
-        const double M00 = P00 * h00 + P01 * h01;
-        const double M01 = P00 * h01 + P01 * h11;
-        const double M10 = P01 * h00 + P11 * h01;
-        const double M11 = P01 * h01 + P11 * h11;
+        const double M00 = FD2(P00, h00, P01, h01);
+        const double M01 = FD2(P00, h01, P01, h11);
+        const double M10 = FD2(P01, h00, P11, h01);
+        const double M11 = FD2(P01, h01, P11, h11);
         double* Mk = w->Mm + 4 * k;
         Mk[0] = M00; Mk[1] = M01; Mk[2] = M10; Mk[3] = M11;
         const double al = w->al[k];
         double* G = w->G + 4 * k;
-        G[0] = al * (1.0 - b2 * M00);
+        G[0] = al * fma(-b2, M00, 1.0);
         G[1] = -(al * (b2 * M01));
         G[2] = -(al * (b2 * M10));
-        G[3] = al * (1.0 - b2 * M11);
+        G[3] = al * fma(-b2, M11, 1.0);
     }
     return ok;
 }
@@ -699,35 +705,35 @@ static void dcm_solve(dcm_ws* w)
     for (int k = 0; k < N; ++k) {
         const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
         const double d0 = w->d[2 * k], d1 = w->d[2 * k + 1];
-        const double y0 = w->qx[2 * k] + (P00 * d0 + P01 * d1);
-        const double y1 = w->qx[2 * k + 1] + (P01 * d0 + P11 * d1);
+        const double y0 = FD3(P00, d0, P01, d1, w->qx[2 * k]);
+        const double y1 = FD3(P01, d0, P11, d1, w->qx[2 * k + 1]);
         const double* Mk = w->Mm + 4 * k;
         const double M00 = Mk[0], M01 = Mk[1], M10 = Mk[2], M11 = Mk[3];
         const double g0 = w->g[2 * k], g1 = w->g[2 * k + 1];
-        const double Mg0 = M00 * g0 + M01 * g1;
-        const double Mg1 = M10 * g0 + M11 * g1;
+        const double Mg0 = FD2(M00, g0, M01, g1);
+        const double Mg1 = FD2(M10, g0, M11, g1);
         const double* G = w->G + 4 * k;
-        w->sc[2 * k] = (G[0] * y0 + G[1] * y1) + w->ab[k] * Mg0;
-        w->sc[2 * k + 1] = (G[2] * y0 + G[3] * y1) + w->ab[k] * Mg1;
+        w->sc[2 * k] = FD3(G[0], y0, G[1], y1, w->ab[k] * Mg0);
+        w->sc[2 * k + 1] = FD3(G[2], y0, G[3], y1, w->ab[k] * Mg1);
     }
     scan_backward(w, w->G, w->sc);
     for (int k = 0; k < N; ++k) {
         const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
         const double d0 = w->d[2 * k], d1 = w->d[2 * k + 1];
-        const double y0 = w->qx[2 * k] + (P00 * d0 + P01 * d1);
-        const double y1 = w->qx[2 * k + 1] + (P01 * d0 + P11 * d1);
+        const double y0 = FD3(P00, d0, P01, d1, w->qx[2 * k]);
+        const double y1 = FD3(P01, d0, P11, d1, w->qx[2 * k + 1]);
         const double t0 = y0 + w->v[2 * (k + 1)];
         const double t1 = y1 + w->v[2 * (k + 1) + 1];
         const double be = w->be[k];
-        const double hu0 = w->g[2 * k] - be * t0;
-        const double hu1 = w->g[2 * k + 1] - be * t1;
+        const double hu0 = fma(-be, t0, w->g[2 * k]);
+        const double hu1 = fma(-be, t1, w->g[2 * k + 1]);
         const double h00 = w->h[3 * k], h01 = w->h[3 * k + 1], h11 = w->h[3 * k + 2];
-        const double k0 = -(h00 * hu0 + h01 * hu1);
-        const double k1 = -(h01 * hu0 + h11 * hu1);
+        const double k0 = -FD2(h00, hu0, h01, hu1);
+        const double k1 = -FD2(h01, hu0, h11, hu1);
         w->dr[2 * k] = k0;                        /* kff until the forward scan is done */
         w->dr[2 * k + 1] = k1;
-        w->sc[2 * k] = d0 - be * k0;
-        w->sc[2 * k + 1] = d1 - be * k1;
+        w->sc[2 * k] = fma(-be, k0, d0);
+        w->sc[2 * k + 1] = fma(-be, k1, d1);
     }
     scan_forward(w, w->G, 1, w->sc);
     for (int k = 0; k < N; ++k) {
@@ -735,8 +741,8 @@ static void dcm_solve(dcm_ws* w)
         const double M00 = Mk[0], M01 = Mk[1], M10 = Mk[2], M11 = Mk[3];
         const double x0 = w->x[2 * k], x1 = w->x[2 * k + 1];
         const double ab = w->ab[k];
-        w->dr[2 * k] = ab * (M00 * x0 + M10 * x1) + w->dr[2 * k];
-        w->dr[2 * k + 1] = ab * (M01 * x0 + M11 * x1) + w->dr[2 * k + 1];
+        w->dr[2 * k] = fma(ab, FD2(M00, x0, M10, x1), w->dr[2 * k]);
+        w->dr[2 * k + 1] = fma(ab, FD2(M01, x0, M11, x1), w->dr[2 * k + 1]);
     }
 }
 
@@ -761,20 +767,20 @@ static void dcm_wphase(dcm_ws* w)
             sgv[i] = sg;
             const double t0 = sg * a[0];
             const double t1 = sg * a[1];
-            W00 = W00 + t0 * a[0];
-            W01 = W01 + t0 * a[1];
-            W11 = W11 + t1 * a[1];
-            const double rpi = ((a[0] * r0 + a[1] * r1) + si) - w->b[k * M + i];
-            const double e = (li * rpi - si * li) * is;
-            g0 = g0 + a[0] * e;
-            g1 = g1 + a[1] * e;
+            W00 = fma(t0, a[0], W00);
+            W01 = fma(t0, a[1], W01);
+            W11 = fma(t1, a[1], W11);
+            const double rpi = (FD2(a[0], r0, a[1], r1) + si) - w->b[k * M + i];
+            const double e = fma(li, rpi, -(si * li)) * is;
+            g0 = fma(a[0], e, g0);
+            g1 = fma(a[1], e, g1);
         }
         for (int i = 1; i < m; ++i) {
             const double* ai = w->A + (k * M + i) * 2;
             for (int j = 0; j < i; ++j) {
                 const double* aj = w->A + (k * M + j) * 2;
-                const double cr = ai[0] * aj[1] - ai[1] * aj[0];
-                dW = dW + (sgv[i] * sgv[j]) * (cr * cr);
+                const double cr = fma(ai[0], aj[1], -(ai[1] * aj[0]));
+                dW = fma(sgv[i] * sgv[j], cr * cr, dW);
             }
         }
         double* Wk = w->W + 4 * k;
@@ -791,8 +797,8 @@ static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
     const double* a = w->A + (k * w->M + i) * 2;
     const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
     const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
-    const double rpi = ((a[0] * r0 + a[1] * r1) + si) - w->b[k * w->M + i];
-    const double dsv = (-rpi) - (a[0] * w->dra[2 * k] + a[1] * w->dra[2 * k + 1]);
+    const double rpi = (FD2(a[0], r0, a[1], r1) + si) - w->b[k * w->M + i];
+    const double dsv = (-rpi) - FD2(a[0], w->dra[2 * k], a[1], w->dra[2 * k + 1]);
     *ds = dsv;
     *dl = -((li * (si + dsv)) * w->is[k * MF + i]);
 }
@@ -850,8 +856,8 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         double* G = w->sg + 4 * k;
         G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
         if (k == 0) {
-            w->sc[0] = w->al[0] * xi_init[0] - w->be[0] * vrp[0];
-            w->sc[1] = w->al[0] * xi_init[1] - w->be[0] * vrp[1];
+            w->sc[0] = fma(w->al[0], xi_init[0], -(w->be[0] * vrp[0]));
+            w->sc[1] = fma(w->al[0], xi_init[1], -(w->be[0] * vrp[1]));
         } else {
             w->sc[2 * k] = -(w->be[k] * vrp[2 * k]);
             w->sc[2 * k + 1] = -(w->be[k] * vrp[2 * k + 1]);
@@ -889,7 +895,7 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         const int m = nfacets[k];
         for (int i = 0; i < m; ++i) {
             const double* a = Ain + (k * M + i) * 2;
-            const double gr = a[0] * vrp[2 * k] + a[1] * vrp[2 * k + 1];
+            const double gr = FD2(a[0], vrp[2 * k], a[1], vrp[2 * k + 1]);
             const double sl = bin[k * M + i] - gr;
             w->s[k * MF + i] = sl > 1e-2 ? sl : 1e-2;
             w->lam[k * MF + i] = 1.0;
@@ -910,8 +916,8 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
     for (int k = 0; k < N; ++k) {
         const double nu0 = w->qx[2 * k] + w->v[2 * (k + 1)];
         const double nu1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
-        dres = nanmax(dres, fabs(w->rh[2 * k] - w->be[k] * nu0));
-        dres = nanmax(dres, fabs(w->rh[2 * k + 1] - w->be[k] * nu1));
+        dres = nanmax(dres, fabs(fma(-w->be[k], nu0, w->rh[2 * k])));
+        dres = nanmax(dres, fabs(fma(-w->be[k], nu1, w->rh[2 * k + 1])));
     }
     if (status == 2) {
         if (iters_out) *iters_out = 0;
@@ -951,7 +957,7 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
             for (int i = 0; i < m; ++i) {
                 double ds, dl;
                 affine_step(w, k, i, &ds, &dl);
-                ck = ck + (w->s[k * MF + i] + a_aff * ds) * (w->lam[k * MF + i] + a_aff * dl);
+                ck = fma(fma(a_aff, ds, w->s[k * MF + i]), fma(a_aff, dl, w->lam[k * MF + i]), ck);
             }
             w->c[k] = ck;
         }
@@ -973,11 +979,11 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                 const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
                 double ds, dl;
                 affine_step(w, k, i, &ds, &dl);
-                const double rc = (si * li + ds * dl) - sigma_mu;
-                const double rpi = ((a[0] * r0 + a[1] * r1) + si) - bin[k * M + i];
-                const double e = (li * rpi - rc) * w->is[k * MF + i];
-                g0 = g0 + a[0] * e;
-                g1 = g1 + a[1] * e;
+                const double rc = FD2(si, li, ds, dl) - sigma_mu;
+                const double rpi = (FD2(a[0], r0, a[1], r1) + si) - bin[k * M + i];
+                const double e = fma(li, rpi, -rc) * w->is[k * MF + i];
+                g0 = fma(a[0], e, g0);
+                g1 = fma(a[1], e, g1);
             }
             w->g[2 * k] = g0;
             w->g[2 * k + 1] = g1;
@@ -992,10 +998,10 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                 const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
                 double ads, adl;
                 affine_step(w, k, i, &ads, &adl);
-                const double rc = (si * li + ads * adl) - sigma_mu;
-                const double rpi = ((a[0] * r0 + a[1] * r1) + si) - bin[k * M + i];
-                const double ds = (-rpi) - (a[0] * w->dr[2 * k] + a[1] * w->dr[2 * k + 1]);
-                const double dl = ((-rc) - li * ds) * w->is[k * MF + i];
+                const double rc = FD2(si, li, ads, adl) - sigma_mu;
+                const double rpi = (FD2(a[0], r0, a[1], r1) + si) - bin[k * M + i];
+                const double ds = (-rpi) - FD2(a[0], w->dr[2 * k], a[1], w->dr[2 * k + 1]);
+                const double dl = fma(-li, ds, -rc) * w->is[k * MF + i];
                 if (ds < 0.0) qmax = keepmax(qmax, (-ds) * w->is[k * MF + i]);
                 if (dl < 0.0) qmax = keepmax(qmax, (-dl) / li);
                 w->cds[k * MF + i] = ds;
@@ -1005,14 +1011,14 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         const double step = qmax > 0.0 ? 0.99 / qmax : 1.0;
         const double a = step < 1.0 ? step : 1.0;
         for (int k = 0; k < N; ++k) {
-            vrp[2 * k] = vrp[2 * k] + a * w->dr[2 * k];
-            vrp[2 * k + 1] = vrp[2 * k + 1] + a * w->dr[2 * k + 1];
-            xi[2 * (k + 1)] = xi[2 * (k + 1)] + a * w->x[2 * (k + 1)];
-            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + a * w->x[2 * (k + 1) + 1];
+            vrp[2 * k] = fma(a, w->dr[2 * k], vrp[2 * k]);
+            vrp[2 * k + 1] = fma(a, w->dr[2 * k + 1], vrp[2 * k + 1]);
+            xi[2 * (k + 1)] = fma(a, w->x[2 * (k + 1)], xi[2 * (k + 1)]);
+            xi[2 * (k + 1) + 1] = fma(a, w->x[2 * (k + 1) + 1], xi[2 * (k + 1) + 1]);
             const int m = nfacets[k];
             for (int i = 0; i < m; ++i) {
-                w->s[k * MF + i] = w->s[k * MF + i] + a * w->cds[k * MF + i];
-                w->lam[k * MF + i] = w->lam[k * MF + i] + a * w->cdl[k * MF + i];
+                w->s[k * MF + i] = fma(a, w->cds[k * MF + i], w->s[k * MF + i]);
+                w->lam[k * MF + i] = fma(a, w->cdl[k * MF + i], w->lam[k * MF + i]);
             }
         }
         dres = dres * (1.0 - a);
