@@ -81,8 +81,10 @@ template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v)
 {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    // every lane has a valid source for these patterns, so no "old" value (update_dpp's first
+    // operand would cost a zeroing v_mov per half)
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 // v_permlane16_swap(x, x) returns (x with its odd rows replaced by the even rows, x with its even

@@ -152,6 +152,16 @@ __device__ __forceinline__ int opaque(int k)
     return k;
 }
 
+// The facet-count predicates (i < m_k per lane, i < mmax per QP) never change during a solve, so
+// the compiler would hoist all 8 of each out of the IPM loop as 64-bit lane masks and spill them
+// to VGPR lanes (46 SGPRs; every use then costs two v_readlane).  Each facet loop reads the counts
+// through these opaque copies instead, so the masks are recomputed per phase (one v_cmp each).
+__device__ __forceinline__ int opaque_s(int k)
+{
+    asm volatile("" : "+s"(k));
+    return k;
+}
+
 // Lane shuffles for the scans.  The source-lane address is recomputed from an opaque lane id
 // at every call: hoisted out of the IPM loop, the twelve shift addresses would stay live in
 // VGPRs for the whole kernel.  Out-of-range sources wrap; the scans never use those values.
@@ -321,10 +331,11 @@ __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P
     double rh1 = P.Rw1 * (K.r1 - rref[1]);
     if (facets) {
         const int kx = opaque(k);
+        const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
         for (int i = 0; i < kMaxFacets; ++i) {
-            if (i >= mmax) break;
-            if (i < K.m) {
+            if (i >= mm) break;
+            if (i < km) {
                 const double2 a = A2[i * N + kx];
                 const double gr = FD2(a.x, K.r0, a.y, K.r1);
                 const double rpi = (gr + K.s[i]) - bb[i * N + kx];
@@ -758,10 +769,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             double g0 = K.rh0, g1 = K.rh1;
             if (own) {
                 const int kx = opaque(k);
+                const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i >= mmax) break;
-                    if (i < K.m) {
+                    if (i >= mm) break;
+                    if (i < km) {
                         const double2 a = L.A2[i * N + kx];
                         const double is = 1.0 / K.s[i];
                         L.IS[i * N + kx] = is;
@@ -781,8 +793,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 // kept in an 8-entry register array across the pair loop (which spilled)
 #pragma unroll
                 for (int i = 1; i < kMaxFacets; ++i) {
-                    if (i >= mmax) break;
-                    if (i < K.m) {
+                    if (i >= mm) break;
+                    if (i < km) {
                         const int ki = opaque(k);
                         const double2 ai = L.A2[i * N + ki];
                         const double sgi = K.lam[i] * L.IS[i * N + ki];
@@ -813,10 +825,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             double q = 0.0;
             if (own) {
                 const int kx = opaque(k);
+                const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i >= mmax) break;
-                    if (i < K.m) {
+                    if (i >= mm) break;
+                    if (i < km) {
                         double ds, dl;
                         const double is = L.IS[i * N + kx];
                         affine_step(K, L.A2[i * N + kx], L.bb[i * N + kx], is, i, dra0, dra1, ds, dl);
@@ -830,10 +843,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             ck = 0.0;
             if (own) {
                 const int kx = opaque(k);
+                const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i >= mmax) break;
-                    if (i < K.m) {
+                    if (i >= mm) break;
+                    if (i < km) {
                         double ds, dl;
                         affine_step(K, L.A2[i * N + kx], L.bb[i * N + kx], L.IS[i * N + kx], i, dra0,
                                     dra1, ds, dl);
@@ -855,10 +869,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             g1 = K.rh1;
             if (own) {
                 const int kx = opaque(k);
+                const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i >= mmax) break;
-                    if (i < K.m) {
+                    if (i >= mm) break;
+                    if (i < km) {
                         const double2 a = L.A2[i * N + kx];
                         const double bi = L.bb[i * N + kx];
                         const double is = L.IS[i * N + kx];
@@ -879,10 +894,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             q = 0.0;
             if (own) {
                 const int kx = opaque(k);
+                const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i >= mmax) break;
-                    if (i < K.m) {
+                    if (i >= mm) break;
+                    if (i < km) {
                         const double2 a = L.A2[i * N + kx];
                         const double bi = L.bb[i * N + kx];
                         const double is = L.IS[i * N + kx];
@@ -903,10 +919,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             const double a = step < 1.0 ? step : 1.0;
             if (own) {
                 const int kx = opaque(k);
+                const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i >= mmax) break;
-                    if (i < K.m) {
+                    if (i >= mm) break;
+                    if (i < km) {
                         const double2 fa = L.A2[i * N + kx];
                         const double ds = (-facet_rp(K, fa, L.bb[i * N + kx], i)) - FD2(fa.x, dr0, fa.y, dr1);
                         K.s[i] = fma(a, ds, K.s[i]);
