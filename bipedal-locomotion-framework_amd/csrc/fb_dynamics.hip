@@ -4,46 +4,92 @@
 // bias forces h and the contact-frame Jacobians from iDynTree KinDynComputations and then solves
 //   nu_dot = LLT(M [+ reg]) \ (-h + sum_c J_c^T w_c + [0; tau]).
 // Here the rigid-body terms are computed directly, in the mixed representation (base velocity
-// (dp_B/dt, w_B), world coordinates), for a kinematic tree of revolute joints:
-//   M = sum_l m_l Jv_l^T Jv_l + Jw_l^T I_l Jw_l            (Jv at the link COM, I_l = R Ic R^T)
-//   h = sum_l Jv_l^T m_l (a_l - g) + Jw_l^T (I_l al_l + w_l x I_l w_l)   (accelerations at nu_dot=0)
-// One 64-lane workgroup per system.  The tree recursion (poses, velocities, bias accelerations)
-// runs on lane 0 with the per-joint rotations precomputed lane-parallel; the per-link terms, the
-// mass-matrix entries (one lane per (i, j) of the lower triangle, a bitmask of each link's
-// ancestor joints selecting the nonzero Jacobian columns), the bias forces and the contact
-// Jacobians are lane-parallel; the Cholesky factorization is right-looking with the trailing
-// update spread over the lanes.  Everything lives in LDS.  The ForwardEuler kernel keeps the
-// state in LDS across its steps.  Checked against the numpy restatement oracle/fb_dynamics.py.
+// (dp_B/dt, w_B), world coordinates), for a kinematic tree of revolute joints, with spatial
+// quantities taken about the WORLD ORIGIN, where a composite inertia is a plain sum:
+//   link l:   spatial inertia I_l = (m, h = m c, Ibar = I_c + m(|c|^2 1 - c c^T)) (10 numbers),
+//             spatial force   F_l = (tau_c + c x f, f),  f = m (a_c - g), tau_c = I_c al + w x I_c w
+//             (accelerations at nu_dot = 0);
+//   column:   motion axis S = (w, u): base linear e_a -> (0, e_a); base angular e_a -> (e_a, p_B x e_a);
+//             joint j -> (z_j, o_j x z_j);
+//   M_ij  = S_j^T (Ic_sub(i) S_i)  when column j acts on the subtree moved by column i (i >= j),
+//   rhs_c = [tau] - S_c^T (sum of F_l over the subtree of c  -  contact wrenches on it, taken about
+//           the origin),
+// which is exactly sum_l m Jv^T Jv + Jw^T I Jw, h and J_c^T w_c of the Jacobian form
+// (oracle/fb_dynamics.py evaluates that form; the two agree to rounding).
+// One 64-lane workgroup (one wavefront) per system, everything in LDS:
+//   1. per-joint rotations, lane per joint;  2. forward kinematics level by level over the tree
+//   depth (lane per joint of the level);  3. per-link spatial inertia / force, lane per link;
+//   4. contact wrenches, lane per contact;  5. subtree sums, lane per (subtree, parameter), the
+//   ancestor bitmask of each link selecting the members;  6. column axes, their composite products
+//   and the right-hand side, lane per column;  7. M, lane per lower-triangle entry;  8. Cholesky,
+//   left-looking with one lane per row (one barrier per column);  9. forward and back
+//   substitution with the right-hand side in registers (lane per row, pivots broadcast by
+//   v_readlane, reciprocal pivots precomputed).
 #include "blf_internal.h"
 #include "contact_math.h"
 #include "fbk_math.h"
 
 namespace blf {
+
+#ifdef BLF_STAMPS
+// Diagnostic build only (make stamps): per-phase cycle sums of lane 0 for the first 64 systems.
+__device__ unsigned long long g_fbd_stamps[12];
+#define FSTAMP(t) unsigned long long t = __builtin_amdgcn_s_memtime()
+#define FSTAMP_ADD(slot, t0) \
+    do { if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_fbd_stamps[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
+extern "C" int blf_debug_fbd_stamps(unsigned long long* out, int reset)
+{
+    unsigned long long h[12];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fbd_stamps), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < 12; ++i) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[12] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fbd_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define FSTAMP(t)
+#define FSTAMP_ADD(slot, t0)
+#endif
+
 namespace {
 
-constexpr int kLinkRec = 40;   // R 9 | p 3 | w 3 | v 3 | al 3 | a 3 | c 3 | Iw 6 (xx xy xz yy yz zz) | f 3 | tq 3 | pad 1
-constexpr int kR = 0, kP = 9, kW = 12, kV = 15, kAl = 18, kA = 21, kC = 24, kIw = 27, kF = 33, kTq = 36;
+// link record: R 9 | p 3 | w 3 | v 3 | al 3 | a 3 | spatial inertia 10 (m, h, Ibar xx xy xz yy yz zz)
+//              | spatial force 6 (tau_O, f)
+constexpr int kLinkRec = 40;
+constexpr int kR = 0, kP = 9, kW = 12, kV = 15, kAl = 18, kA = 21, kSI = 24, kSF = 34;
+constexpr int kComp = 16;   // subtree sum: spatial inertia 10 | spatial force 6
+constexpr int kCs = 16;     // contact scratch: point 3 | wrench 6 | link 1 | spatial wrench 6
 
 struct Smem {
-    double *link, *jrot, *jz, *jo, *M, *rhs, *cscr, *st;
+    double *link, *jrot, *jz, *jo, *comp, *sax, *rhs, *cscr, *st;
     unsigned long long* anc;
+    int ms;   // row stride of L (odd: the per-lane row accesses do not conflict)
     size_t total;
     __host__ __device__ Smem(double* base, int n, int C)
     {
         const int L = n + 1, NV = n + 6;
+        ms = NV | 1;
         size_t o = 0;
         auto take = [&](size_t k) {
             double* p = base ? base + o : nullptr;
             o += (k + 1) & ~size_t(1);
             return p;
         };
-        link = take((size_t)kLinkRec * L);
+        // link records; after the mass matrix is assembled the same space holds L (NV rows)
+        const size_t lk = (size_t)kLinkRec * L, lm = (size_t)NV * ms;
+        link = take(lk > lm ? lk : lm);
         jrot = take(12 * (size_t)n);           // E_j Rot(a_j, s_j) (9) | E_j a_j (3)
         jz = take(3 * (size_t)n);
         jo = take(3 * (size_t)n);
-        M = take((size_t)NV * NV);
+        // subtree sums [j] (joint j's subtree) and [n] (every link); later the pivot-column
+        // buffers of the factorization (2 NV)
+        const size_t cp = (size_t)kComp * (n + 1);
+        comp = take(cp > 2 * (size_t)NV ? cp : 2 * (size_t)NV);
+        sax = take(6 * (size_t)NV);
         rhs = take((size_t)NV);
-        cscr = take(16 * (size_t)(C > 0 ? C : 1));   // per contact: point (3) | wrench (6) | link (1)
+        cscr = take((size_t)kCs * (C > 0 ? C : 1));
         st = take(18 + 2 * (size_t)n + (size_t)NV + 9);   // Euler state (6 + n + 3 + 9 + n) + acc + dR
         anc = reinterpret_cast<unsigned long long*>(take((size_t)L));
         total = o;
@@ -72,32 +118,9 @@ __device__ __forceinline__ void cross3(const double* a, const double* b, double*
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
-// Jacobian column `col` (mixed) of a point x rigidly attached to a link: linear jv, angular jw.
-// Caller guarantees the column is visible from the link (base column or an ancestor joint).
-__device__ __forceinline__ void jac_col(const Smem& S, int col, const double* x, const double* pB,
-                                        double* jv, double* jw)
+__device__ __forceinline__ double dot3(const double* a, const double* b)
 {
-    if (col < 3) {
-        jv[0] = col == 0 ? 1.0 : 0.0; jv[1] = col == 1 ? 1.0 : 0.0; jv[2] = col == 2 ? 1.0 : 0.0;
-        jw[0] = jw[1] = jw[2] = 0.0;
-    } else if (col < 6) {
-        const int i = col - 3;
-        const double e[3] = {i == 0 ? 1.0 : 0.0, i == 1 ? 1.0 : 0.0, i == 2 ? 1.0 : 0.0};
-        const double d[3] = {x[0] - pB[0], x[1] - pB[1], x[2] - pB[2]};
-        cross3(e, d, jv);                       // column i of -skew(x - p_B)
-        jw[0] = e[0]; jw[1] = e[1]; jw[2] = e[2];
-    } else {
-        const int j = col - 6;
-        const double* z = S.jz + 3 * j;
-        const double d[3] = {x[0] - S.jo[3 * j], x[1] - S.jo[3 * j + 1], x[2] - S.jo[3 * j + 2]};
-        cross3(z, d, jv);
-        jw[0] = z[0]; jw[1] = z[1]; jw[2] = z[2];
-    }
-}
-
-__device__ __forceinline__ bool visible(const Smem& S, int col, int link)
-{
-    return col < 6 || ((S.anc[link] >> (col - 6)) & 1ull);
+    return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
 }
 
 // sym 3x3 (xx xy xz yy yz zz) times vector
@@ -108,16 +131,97 @@ __device__ __forceinline__ void sym_mv(const double* I, const double* x, double*
     y[2] = (I[2] * x[0] + I[4] * x[1]) + I[5] * x[2];
 }
 
+__device__ __forceinline__ double bcast(double v, int src)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// r[lane] of a register row (the diagonal entry of the lane's own row), compile-time indexed.
+template <int NVMAX>
+__device__ __forceinline__ double bcast_own_diag(const double* r, int lane)
+{
+    double d = 0.0;
+#pragma unroll
+    for (int k = 0; k < NVMAX; ++k)
+        if (lane == k) d = r[k];
+    return d;
+}
+
+// Tree topology, the same for every system and every Euler step: built once per workgroup.
+// Lane j < n: joint j's parent link, origin, depth and child mask; anc[l] (LDS) every link's
+// ancestor-joint mask.
+struct Topo {
+    int P, depth, maxdepth;
+    double o0, o1, o2;
+    unsigned long long cmask, bmask;
+};
+
+__device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
+{
+    const int n = m.n, lane = threadIdx.x;
+    const bool jl = lane < n;
+    Topo t;
+    t.P = jl ? m.parent[lane] : 0;
+    t.o0 = jl ? m.jorig[3 * lane] : 0.0;
+    t.o1 = jl ? m.jorig[3 * lane + 1] : 0.0;
+    t.o2 = jl ? m.jorig[3 * lane + 2] : 0.0;
+    // walk to the base through the parents held by the other lanes (joint Q - 1 moves link Q)
+    unsigned long long an = jl ? 1ull << lane : 0ull;
+    int depth = 0, Q = t.P;
+    for (int it = 0; it < n; ++it) {
+        const bool up = jl && Q > 0;
+        if (!__ballot(up)) break;
+        const int q = __shfl(t.P, up ? Q - 1 : 0, kWave);
+        if (up) {
+            ++depth;
+            an |= 1ull << (Q - 1);
+            Q = q;
+        }
+    }
+    t.depth = depth;
+    if (jl) S.anc[lane + 1] = an;
+    if (lane == 0) S.anc[0] = 0ull;
+    t.cmask = 0ull;
+    for (int j = 0; j < n; ++j) {
+        const unsigned long long b = __ballot(jl && t.P == j + 1);
+        if (lane == j) t.cmask = b;
+    }
+    t.bmask = __ballot(jl && t.P == 0);
+    int md = depth;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int q = __shfl_xor(md, off, kWave);
+        md = q > md ? q : md;
+    }
+    t.maxdepth = __builtin_amdgcn_readfirstlane(md);
+    __syncthreads();
+    return t;
+}
+
 // One evaluation of the dynamics for the system whose state sits in LDS (bv, jv, bp, bR, jp).
 // Leaves the generalized acceleration in S.rhs and returns false if the factorization failed.
-__device__ bool fbd_eval(const Model& m, const Smem& S, const double* bv, const double* jvel,
-                         const double* bp, const double* bR, const double* jp,
-                         const double* tau, const Contacts& ct, int64_t sys, const double* reg)
+// NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
+// registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
+// steps 6-9.
+template <int NVMAX>
+__device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
+                                         const double* jvel, const double* bp, const double* bR,
+                                         const double* jp, const double* tau, const Contacts& ct,
+                                         int64_t sys, const double* reg, const Topo& T)
 {
-    const int n = m.n, L = n + 1, NV = n + 6;
+    const int n = m.n, L = n + 1, NV = n + 6, MS = S.ms;
     const int lane = threadIdx.x;
-    // 1. per-joint rotation E_j Rot(a_j, s_j) (Rodrigues) and E_j a_j, lane-parallel
-    for (int j = lane; j < n; j += kWave) {
+    const bool jl = lane < n;   // n <= 48 < 64: one joint per lane
+    FSTAMP(f_t0);
+    FSTAMP(f_t);
+    // 1. per-joint rotation E_j Rot(a_j, s_j) (Rodrigues) and E_j a_j, lane per joint
+    const int depth = T.depth, P = T.P, maxdepth = T.maxdepth;
+    const double sd = jl ? jvel[lane] : 0.0;
+    if (jl) {
+        const int j = lane;
         const double* a = m.jaxis + 3 * j;
         const double* E = m.jrot + 9 * j;
         double sn, cs;
@@ -141,8 +245,6 @@ __device__ bool fbd_eval(const Model& m, const Smem& S, const double* bv, const 
             out[9 + r] = (E[3 * r] * a[0] + E[3 * r + 1] * a[1]) + E[3 * r + 2] * a[2];
         }
     }
-    __syncthreads();
-    // 2. tree recursion on lane 0: poses, mixed velocities, nu_dot = 0 accelerations
     if (lane == 0) {
         double* b = S.link;
         for (int i = 0; i < 9; ++i) b[kR + i] = bR[i];
@@ -150,112 +252,113 @@ __device__ bool fbd_eval(const Model& m, const Smem& S, const double* bv, const 
             b[kP + i] = bp[i]; b[kV + i] = bv[i]; b[kW + i] = bv[3 + i];
             b[kAl + i] = 0.0; b[kA + i] = 0.0;
         }
-        S.anc[0] = 0ull;
-        for (int j = 0; j < n; ++j) {
-            const int P = m.parent[j];
-            const double* pr = S.link + kLinkRec * P;
-            double* cr = S.link + kLinkRec * (j + 1);
-            const double* Ej = S.jrot + 12 * j;
-            const double* o = m.jorig + 3 * j;
+    }
+    __syncthreads();
+    FSTAMP_ADD(0, f_t);
+    FSTAMP(f_t1);
+    // 2. forward kinematics, one tree level at a time: poses, mixed velocities, nu_dot = 0
+    //    accelerations of every joint whose parent link is done
+    for (int lev = 0; lev <= maxdepth; ++lev) {
+        if (jl && depth == lev) {
+            const int j = lane;
+            // the parent link's record and this joint's rotation into registers first (the child
+            // record's stores could otherwise alias them and delay the loads)
+            double pr[24], Ej[12];
+            const double* prs = S.link + kLinkRec * P;
+#pragma unroll
+            for (int i = 0; i < 24; ++i) pr[i] = prs[i];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Ej[i] = S.jrot[12 * j + i];
+            const double o[3] = {T.o0, T.o1, T.o2};
             const double* RP = pr + kR;
-            double r[3], z[3];
+            double cR[9], r[3], z[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c)
-                    cr[kR + 3 * a + c] = (RP[3 * a] * Ej[c] + RP[3 * a + 1] * Ej[3 + c]) + RP[3 * a + 2] * Ej[6 + c];
+                    cR[3 * a + c] = (RP[3 * a] * Ej[c] + RP[3 * a + 1] * Ej[3 + c]) + RP[3 * a + 2] * Ej[6 + c];
                 r[a] = (RP[3 * a] * o[0] + RP[3 * a + 1] * o[1]) + RP[3 * a + 2] * o[2];
                 z[a] = (RP[3 * a] * Ej[9] + RP[3 * a + 1] * Ej[10]) + RP[3 * a + 2] * Ej[11];
             }
-            const double sd = jvel[j];
             const double zs[3] = {z[0] * sd, z[1] * sd, z[2] * sd};
-            double t1[3], t2[3], t3[3];
+            double t1[3], t2[3], t3[3], t4[3];
             cross3(pr + kW, r, t1);            // w_P x r
             cross3(pr + kW, zs, t2);           // w_P x z sd
+            cross3(pr + kAl, r, t3);           // al_P x r
+            cross3(pr + kW, t1, t4);           // w_P x (w_P x r)
+            double* cr = S.link + kLinkRec * (j + 1);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) cr[kR + i] = cR[i];
+#pragma unroll
             for (int a = 0; a < 3; ++a) {
-                cr[kP + a] = pr[kP + a] + r[a];
+                const double pc = pr[kP + a] + r[a];
+                cr[kP + a] = pc;
                 S.jz[3 * j + a] = z[a];
-                S.jo[3 * j + a] = cr[kP + a];
+                S.jo[3 * j + a] = pc;
                 cr[kW + a] = pr[kW + a] + zs[a];
                 cr[kV + a] = pr[kV + a] + t1[a];
                 cr[kAl + a] = pr[kAl + a] + t2[a];
+                cr[kA + a] = (pr[kA + a] + t3[a]) + t4[a];
             }
-            cross3(pr + kAl, r, t2);           // al_P x r
-            cross3(pr + kW, t1, t3);           // w_P x (w_P x r)
-            for (int a = 0; a < 3; ++a) cr[kA + a] = (pr[kA + a] + t2[a]) + t3[a];
-            S.anc[j + 1] = S.anc[P] | (1ull << j);
         }
+        __syncthreads();
     }
-    __syncthreads();
-    // 3. per-link COM, world inertia, Newton-Euler force / moment (lane-parallel)
+    FSTAMP_ADD(1, f_t1);
+    FSTAMP(f_t2);
+    // 3. per link: COM, world inertia, Newton-Euler force / moment, and the spatial inertia and
+    //    force about the world origin (lane per link)
     for (int l = lane; l < L; l += kWave) {
         double* k = S.link + kLinkRec * l;
         const double* R = k + kR;
         const double* cl = m.com + 3 * l;
         const double* Ic = m.inertia + 9 * l;
-        double rc[3];
+        double rc[3], c[3];
         for (int a = 0; a < 3; ++a) {
             rc[a] = (R[3 * a] * cl[0] + R[3 * a + 1] * cl[1]) + R[3 * a + 2] * cl[2];
-            k[kC + a] = k[kP + a] + rc[a];
+            c[a] = k[kP + a] + rc[a];
         }
         double RI[9];   // R Ic
         for (int a = 0; a < 3; ++a)
-            for (int c = 0; c < 3; ++c)
-                RI[3 * a + c] = (R[3 * a] * Ic[c] + R[3 * a + 1] * Ic[3 + c]) + R[3 * a + 2] * Ic[6 + c];
+            for (int b = 0; b < 3; ++b)
+                RI[3 * a + b] = (R[3 * a] * Ic[b] + R[3 * a + 1] * Ic[3 + b]) + R[3 * a + 2] * Ic[6 + b];
         const int ii[6] = {0, 0, 0, 1, 1, 2}, jj[6] = {0, 1, 2, 1, 2, 2};
+        double Iw[6];
         for (int e = 0; e < 6; ++e) {
-            const int a = ii[e], c = jj[e];
-            k[kIw + e] = (RI[3 * a] * R[3 * c] + RI[3 * a + 1] * R[3 * c + 1]) + RI[3 * a + 2] * R[3 * c + 2];
+            const int a = ii[e], b = jj[e];
+            Iw[e] = (RI[3 * a] * R[3 * b] + RI[3 * a + 1] * R[3 * b + 1]) + RI[3 * a + 2] * R[3 * b + 2];
         }
-        double t1[3], t2[3], t3[3];
+        double t1[3], t2[3], t3[3], f[3];
         cross3(k + kAl, rc, t1);
         cross3(k + kW, rc, t2);
         cross3(k + kW, t2, t3);
         const double ms = m.mass[l];
         const double g[3] = {m.g0, m.g1, m.g2};
-        for (int a = 0; a < 3; ++a) k[kF + a] = ms * (((k[kA + a] + t1[a]) + t3[a]) - g[a]);
-        double Ia[3], Iw[3];
-        sym_mv(k + kIw, k + kAl, Ia);
-        sym_mv(k + kIw, k + kW, Iw);
-        cross3(k + kW, Iw, t1);
-        for (int a = 0; a < 3; ++a) k[kTq + a] = Ia[a] + t1[a];
-    }
-    __syncthreads();
-    const double* pB = S.link + kP;
-    // 4. mass matrix, lower triangle, one lane per entry
-    const int ntri = NV * (NV + 1) / 2;
-    for (int e = lane; e < ntri; e += kWave) {
-        int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-        while ((i + 1) * (i + 2) / 2 <= e) ++i;
-        while (i * (i + 1) / 2 > e) --i;
-        const int j = e - i * (i + 1) / 2;
-        double acc = 0.0;
-        for (int l = 0; l < L; ++l) {
-            if (!visible(S, i, l) || !visible(S, j, l)) continue;
-            const double* k = S.link + kLinkRec * l;
-            double vi[3], wi[3], vj[3], wj[3], Iwj[3];
-            jac_col(S, i, k + kC, pB, vi, wi);
-            jac_col(S, j, k + kC, pB, vj, wj);
-            sym_mv(k + kIw, wj, Iwj);
-            acc = acc + (m.mass[l] * ((vi[0] * vj[0] + vi[1] * vj[1]) + vi[2] * vj[2])
-                         + ((wi[0] * Iwj[0] + wi[1] * Iwj[1]) + wi[2] * Iwj[2]));
+        for (int a = 0; a < 3; ++a) f[a] = ms * (((k[kA + a] + t1[a]) + t3[a]) - g[a]);
+        double Ia[3], Iwv[3], tq[3], cf[3];
+        sym_mv(Iw, k + kAl, Ia);
+        sym_mv(Iw, k + kW, Iwv);
+        cross3(k + kW, Iwv, t1);
+        for (int a = 0; a < 3; ++a) tq[a] = Ia[a] + t1[a];
+        cross3(c, f, cf);
+        const double cc = dot3(c, c);
+        double* si = k + kSI;
+        si[0] = ms;
+        si[1] = ms * c[0]; si[2] = ms * c[1]; si[3] = ms * c[2];
+        si[4] = Iw[0] + ms * (cc - c[0] * c[0]);
+        si[5] = Iw[1] - ms * (c[0] * c[1]);
+        si[6] = Iw[2] - ms * (c[0] * c[2]);
+        si[7] = Iw[3] + ms * (cc - c[1] * c[1]);
+        si[8] = Iw[4] - ms * (c[1] * c[2]);
+        si[9] = Iw[5] + ms * (cc - c[2] * c[2]);
+        double* sf = k + kSF;
+        for (int a = 0; a < 3; ++a) {
+            sf[a] = tq[a] + cf[a];
+            sf[3 + a] = f[a];
         }
-        S.M[NV * i + j] = acc + (reg ? reg[NV * i + j] : 0.0);
     }
-    // 5. bias forces, one lane per generalized coordinate
-    for (int c = lane; c < NV; c += kWave) {
-        double h = 0.0;
-        for (int l = 0; l < L; ++l) {
-            if (!visible(S, c, l)) continue;
-            const double* k = S.link + kLinkRec * l;
-            double jv[3], jw[3];
-            jac_col(S, c, k + kC, pB, jv, jw);
-            h = h + (((jv[0] * k[kF] + jv[1] * k[kF + 1]) + jv[2] * k[kF + 2])
-                     + ((jw[0] * k[kTq] + jw[1] * k[kTq + 1]) + jw[2] * k[kTq + 2]));
-        }
-        S.rhs[c] = (-h) + (c >= 6 ? tau[c - 6] : 0.0);
-    }
-    // 6. contacts: frame state + ContinuousContactModel wrench (lane c), then J_c^T w (lanes)
+    FSTAMP_ADD(2, f_t2);
+    FSTAMP(f_t3);
+    // 4. contacts: frame state + ContinuousContactModel wrench, and the wrench about the origin
     for (int c = lane; c < ct.C; c += kWave) {
         const int f = ct.frame[c];
         const int l = m.flink[f];
@@ -274,65 +377,164 @@ __device__ bool fbd_eval(const Model& m, const Smem& S, const double* bv, const 
             tw[a] = k[kV + a] + t1[a];
             tw[3 + a] = k[kW + a];
         }
-        double* sc = S.cscr + 16 * c;
+        double* sc = S.cscr + kCs * c;
         contact_wrench(ct.params + 4 * c, tw, pose, ct.null_pose + (sys * ct.C + c) * 12, sc + 3);
         sc[0] = pose[0]; sc[1] = pose[1]; sc[2] = pose[2];
         sc[9] = (double)l;
-    }
-    __syncthreads();
-    for (int col = lane; col < NV; col += kWave) {
-        double add = 0.0;
-        for (int c = 0; c < ct.C; ++c) {
-            const double* sc = S.cscr + 16 * c;
-            const int l = (int)sc[9];
-            if (!visible(S, col, l)) continue;
-            double jv[3], jw[3];
-            jac_col(S, col, sc, pB, jv, jw);
-            add = add + (((jv[0] * sc[3] + jv[1] * sc[4]) + jv[2] * sc[5])
-                         + ((jw[0] * sc[6] + jw[1] * sc[7]) + jw[2] * sc[8]));
+        double xf[3];
+        cross3(sc, sc + 3, xf);   // x_c x f_c
+        for (int a = 0; a < 3; ++a) {
+            sc[10 + a] = sc[6 + a] + xf[a];
+            sc[13 + a] = sc[3 + a];
         }
-        S.rhs[col] = S.rhs[col] + add;
     }
     __syncthreads();
-    // 7. Cholesky M = L L^T (lower, in place), right-looking
+    FSTAMP_ADD(3, f_t3);
+    FSTAMP(f_t4);
+    // 5. subtree sums of the spatial inertias and (link - contact) forces, from the leaves up:
+    //    joint j's sum = its link's terms + its children's sums (16 accumulators per lane)
+    for (int lev = maxdepth; lev >= -1; --lev) {
+        const bool mine = lev >= 0 ? (jl && depth == lev) : lane == 0;
+        if (mine) {
+            const int l = lev >= 0 ? lane + 1 : 0;               // the subtree's root link
+            const unsigned long long ch = lev >= 0 ? T.cmask : T.bmask;
+            double acc[kComp];
+#pragma unroll
+            for (int p = 0; p < kComp; ++p) acc[p] = S.link[kLinkRec * l + kSI + p];
+            for (int c = 0; c < ct.C; ++c) {
+                const double* sc = S.cscr + kCs * c;
+                if ((int)sc[9] == l)
+#pragma unroll
+                    for (int p = 10; p < kComp; ++p) acc[p] = acc[p] - sc[p];
+            }
+            for (unsigned long long b = ch; b; b &= b - 1) {
+                const double* cs = S.comp + kComp * __builtin_ctzll(b);
+#pragma unroll
+                for (int p = 0; p < kComp; ++p) acc[p] = acc[p] + cs[p];
+            }
+            double* dst = S.comp + kComp * (lev >= 0 ? lane : n);
+#pragma unroll
+            for (int p = 0; p < kComp; ++p) dst[p] = acc[p];
+        }
+        __syncthreads();
+    }
+    FSTAMP_ADD(4, f_t4);
+    FSTAMP(f_t5);
+    // 6. lane c: column axis S_c = (w, u) (to LDS), F_c = Ic S_c with Ic the subtree sum the
+    //    column moves (registers), rhs_c = [tau] - S_c^T (subtree force)
+    const double* pB = S.link + kP;
+    double y = 0.0, Fc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (lane < NV) {
+        const int c = lane;
+        double w[3] = {0.0, 0.0, 0.0}, u[3] = {0.0, 0.0, 0.0};
+        if (c < 3) {
+            u[c] = 1.0;
+        } else if (c < 6) {
+            w[c - 3] = 1.0;
+            cross3(pB, w, u);
+        } else {
+            const int j = c - 6;
+            for (int a = 0; a < 3; ++a) w[a] = S.jz[3 * j + a];
+            cross3(S.jo + 3 * j, w, u);
+        }
+        const double* I = S.comp + kComp * (c < 6 ? n : c - 6);
+        double Iwv[3], hu[3], wh[3];
+        sym_mv(I + 4, w, Iwv);
+        cross3(I + 1, u, hu);
+        cross3(w, I + 1, wh);
+        double* sa = S.sax + 6 * c;
+        for (int a = 0; a < 3; ++a) {
+            sa[a] = w[a];
+            sa[3 + a] = u[a];
+            Fc[a] = Iwv[a] + hu[a];
+            Fc[3 + a] = wh[a] + I[0] * u[a];
+        }
+        y = (c >= 6 ? tau[c - 6] : 0.0) - (dot3(w, I + 10) + dot3(u, I + 13));
+    }
+    const unsigned long long myanc = (lane >= 6 && lane < NV) ? S.anc[lane - 5] : 0ull;
+    __syncthreads();
+    FSTAMP_ADD(5, f_t5);
+    FSTAMP(f_t6);
+    // 7. row i of M in registers: M_ij = S_j . F_i when column j moves the subtree of column i
+    //    (j < 6, or joint j - 6 an ancestor of column i's link)
+    // (no branch per column: a branch between an LDS read and its use serialises the reads; an
+    // index past the last column is clamped and its value discarded by the row predicate)
+    double r[NVMAX];
+#pragma unroll
+    for (int j = 0; j < NVMAX; ++j) {
+        const double* sa = S.sax + 6 * (j < NV ? j : NV - 1);   // every lane reads the same S_j
+        const double v = dot3(sa, Fc) + dot3(sa + 3, Fc + 3);
+        const bool vis = j <= lane && lane < NV && (j < 6 || ((myanc >> (j - 6)) & 1ull));
+        r[j] = vis ? v : 0.0;
+    }
+    if (reg && lane < NV)
+#pragma unroll
+        for (int j = 0; j < NVMAX; ++j)
+            if (j < NV && j <= lane) r[j] = r[j] + reg[NV * lane + j];
+    FSTAMP_ADD(6, f_t6);
+    FSTAMP(f_t7);
+    // 8. Cholesky M = L L^T, right-looking, lane i keeps row i in registers; column k of the
+    //    rows below the pivot goes through an LDS buffer (two, alternating) and is read back as
+    //    broadcasts
     bool ok = true;
-    for (int k = 0; k < NV; ++k) {
-        const double piv = S.M[NV * k + k];
-        ok = ok && (piv > 0.0);
-        const double d = sqrt(piv);
-        __syncthreads();
-        for (int i = k + 1 + lane; i < NV; i += kWave) S.M[NV * i + k] = S.M[NV * i + k] / d;
-        if (lane == 0) S.M[NV * k + k] = d;
-        __syncthreads();
-        const int rem = NV - k - 1;
-        const int nup = rem * (rem + 1) / 2;
-        for (int e = lane; e < nup; e += kWave) {
-            int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-            while ((i + 1) * (i + 2) / 2 <= e) ++i;
-            while (i * (i + 1) / 2 > e) --i;
-            const int j = e - i * (i + 1) / 2;
-            const int I = k + 1 + i, J = k + 1 + j;
-            S.M[NV * I + J] = S.M[NV * I + J] - S.M[NV * I + k] * S.M[NV * J + k];
-        }
-        __syncthreads();
-    }
-    // 8. forward / back substitution on lane 0
-    if (lane == 0) {
-        for (int i = 0; i < NV; ++i) {
-            double s = S.rhs[i];
-            for (int k = 0; k < i; ++k) s = s - S.M[NV * i + k] * S.rhs[k];
-            S.rhs[i] = s / S.M[NV * i + i];
-        }
-        for (int i = NV - 1; i >= 0; --i) {
-            double s = S.rhs[i];
-            for (int k = i + 1; k < NV; ++k) s = s - S.M[NV * k + i] * S.rhs[k];
-            S.rhs[i] = s / S.M[NV * i + i];
+#pragma unroll
+    for (int k = 0; k < NVMAX; ++k) {
+        if (k < NV) {
+            const double piv = bcast(r[k], k);
+            ok = ok && (piv > 0.0);
+            // 1 / sqrt(piv): v_rsq_f64 and one Newton step (the factorization's accuracy is that
+            // of its rounding errors; parity with the oracle is at 1e-9)
+            double isq = __builtin_amdgcn_rsq(piv);
+            isq = isq * (1.5 - (0.5 * piv) * (isq * isq));
+            r[k] = lane == k ? piv * isq : (lane > k ? r[k] * isq : r[k]);
+            double* col = S.comp + (k & 1) * NV;
+            if (lane < NV) col[lane] = r[k];
+            __syncthreads();
+            // The row predicate goes into the multiplier (no branch: a branch would pull each
+            // column read into it and serialise the reads).  j >= NV touches only lanes past the
+            // matrix.
+#pragma unroll
+            for (int j = k + 1; j < NVMAX; ++j) {
+                const double ljk = col[j < NV ? j : NV - 1];
+                const double f = lane >= j ? r[k] : 0.0;
+                r[j] = r[j] - f * ljk;
+            }
         }
     }
+    FSTAMP_ADD(7, f_t7);
+    FSTAMP(f_t8);
+    // 9. L z = y with the rows in registers, then L^T x = z with row k of L read from LDS (the
+    //    link records are dead by now); lane k scales its own entry, one broadcast per step
+    const double idg = lane < NV ? 1.0 / bcast_own_diag<NVMAX>(r, lane) : 0.0;
+#pragma unroll
+    for (int k = 0; k < NVMAX; ++k) {   // k >= NV changes only lanes past the matrix
+        y = lane == k ? y * idg : y;
+        const double xk = bcast(y, k);
+        const double f = lane > k ? r[k] : 0.0;
+        y = y - f * xk;
+    }
+    double* Lm = S.link;
+    if (lane < NV)
+#pragma unroll
+        for (int j = 0; j < NVMAX; ++j)
+            if (j < NV && j <= lane) Lm[MS * lane + j] = r[j];
     __syncthreads();
+    double lki = (lane < NV - 1) ? Lm[MS * (NV - 1) + lane] : 0.0;
+    for (int k = NV - 1; k >= 0; --k) {
+        const double lnext = (k > 0 && lane < k - 1) ? Lm[MS * (k - 1) + lane] : 0.0;   // read ahead
+        if (lane == k) y = y * idg;
+        const double xk = bcast(y, k);
+        if (lane < k) y = y - lki * xk;
+        lki = lnext;
+    }
+    if (lane < NV) S.rhs[lane] = y;
+    __syncthreads();
+    FSTAMP_ADD(8, f_t8);
+    FSTAMP_ADD(9, f_t0);
     return ok;
 }
 
+template <int NVMAX>
 __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state st,
                                                           const double* __restrict__ tau,
                                                           Contacts ct, const double* reg,
@@ -354,8 +556,9 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
         loc[i] = v;
     }
     __syncthreads();
-    const bool ok = fbd_eval(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
-                             tau + (int64_t)n * q, ct, q, reg);
+    const Topo T = build_topo(m, S);
+    const bool ok = fbd_eval<NVMAX>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+                                    tau + (int64_t)n * q, ct, q, reg, T);
     const double nan = __builtin_nan("");
     for (int c = lane; c < NV; c += kWave) {
         const double a = ok ? S.rhs[c] : nan;
@@ -371,7 +574,8 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
     for (int j = lane; j < n; j += kWave) out.joint_pos[(int64_t)n * q + j] = loc[6 + j];
 }
 
-__global__ __launch_bounds__(64) void fbd_euler_kernel(Model m, blf_fb_state st,
+template <int NVMAX>
+__global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state st,
                                                        const double* __restrict__ tau,
                                                        Contacts ct, const double* reg,
                                                        int32_t nsteps, double dT, double dT_last)
@@ -393,11 +597,12 @@ __global__ __launch_bounds__(64) void fbd_euler_kernel(Model m, blf_fb_state st,
         loc[i] = v;
     }
     __syncthreads();
+    const Topo T = build_topo(m, S);
     bool ok = true;
     for (int32_t step = 0; step < nsteps; ++step) {
         const double h = step + 1 < nsteps ? dT : dT_last;
-        ok = fbd_eval(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
-                      tau + (int64_t)n * q, ct, q, reg) && ok;
+        ok = fbd_eval<NVMAX>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+                             tau + (int64_t)n * q, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         __syncthreads();
         // every element moves by its derivative at the start of the step (ForwardEuler.tpp:37-45):
@@ -464,8 +669,13 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 {
     if (batch == 0) return BLF_OK;
     const Contacts c = to_contacts(ct);
-    hipLaunchKernelGGL(fbd_dynamics_kernel, dim3((unsigned)batch), dim3(kWave),
-                       fbd_lds_bytes(md->ndof, c.C), s, to_model(md), *st, tau, c, reg, *out);
+    const size_t lds = fbd_lds_bytes(md->ndof, c.C);
+    if (md->ndof + 6 <= 32)
+        hipLaunchKernelGGL(fbd_dynamics_kernel<32>, dim3((unsigned)batch), dim3(kWave), lds, s,
+                           to_model(md), *st, tau, c, reg, *out);
+    else
+        hipLaunchKernelGGL(fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6>, dim3((unsigned)batch),
+                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, *out);
     return check_hip(hipGetLastError(), "fbd_dynamics_kernel launch");
 }
 
@@ -475,9 +685,13 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
 {
     if (batch == 0) return BLF_OK;
     const Contacts c = to_contacts(ct);
-    hipLaunchKernelGGL(fbd_euler_kernel, dim3((unsigned)batch), dim3(kWave),
-                       fbd_lds_bytes(md->ndof, c.C), s, to_model(md), *st, tau, c, reg, nsteps,
-                       dT, dT_last);
+    const size_t lds = fbd_lds_bytes(md->ndof, c.C);
+    if (md->ndof + 6 <= 32)
+        hipLaunchKernelGGL(fbd_euler_kernel<32>, dim3((unsigned)batch), dim3(kWave), lds, s,
+                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last);
+    else
+        hipLaunchKernelGGL(fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6>, dim3((unsigned)batch),
+                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last);
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
 }
 
