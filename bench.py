@@ -10,8 +10,8 @@ solutions to rank 0 is timed separately and reported as gather_ms.
 Prints ONE JSON line on rank 0 (the driver's contract), with two extra objects:
   roofline      HBM roofline of the dominant kernel (dcm_mpc_ipm), from the algorithmic bytes
                 per QP and the kernel's average duration measured with HIP
-                events on the launch stream; plus the counted-flop fp64 fraction (the roof that
-                actually binds this latency-bound kernel).
+                events on the launch stream; plus the counted-flop fp64 fraction and the VALU
+                issue fraction (the roof that binds this kernel).
   cpu_baseline  the CPU oracle (same IPM, C, -O2, one problem per thread) on this host's cores,
                 rank 0 only, on a bounded sample.
 """
@@ -34,10 +34,10 @@ def algorithmic_bytes_per_qp(N, M):
     return 8 * f64 + 4 * i32
 
 
-def profiled_traffic():
-    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 summary
-    (profiles/*_summary.json, written by tools/summarize_profile.py from separate FETCH_SIZE /
-    WRITE_SIZE passes); bench.py cannot read PMC counters itself."""
+def profiled_summary():
+    """The newest committed rocprofv3 summary of the dominant kernel (profiles/*_summary.json,
+    written by tools/summarize_profile.py from separate FETCH_SIZE / WRITE_SIZE / SQ passes);
+    bench.py cannot read PMC counters itself.  Returns (summary, path) or (None, None)."""
     import glob
     # newest by name (profiles/rNN_<tag>_summary.json; file times do not survive the copy to a box)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
@@ -45,10 +45,35 @@ def profiled_traffic():
         return None, None
     with open(files[-1]) as f:
         s = json.load(f)
-    t = s.get("hbm_traffic_per_launch")
-    if not t or "dcm_mpc_ipm" not in s.get("dominant_kernel", ""):
+    if "dcm_mpc_ipm" not in s.get("dominant_kernel", ""):
         return None, None
-    return t["total_bytes_corrected"], os.path.relpath(files[-1], ROOT)
+    return s, os.path.relpath(files[-1], ROOT)
+
+
+def profiled_traffic():
+    """HBM bytes per launch of the dominant kernel (corrected FETCH + WRITE), or None."""
+    s, path = profiled_summary()
+    t = s.get("hbm_traffic_per_launch") if s else None
+    if not t:
+        return None, None
+    return t["total_bytes_corrected"], path
+
+
+SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4
+
+
+def valu_issue(kernel_ms):
+    """The roof that binds the QP kernel: VALU issue.  VALU wave-instructions per launch from the
+    committed SQ_INSTS_VALU pass, x 4 SIMD cycles each, over the chip's SIMD cycles in the kernel
+    time measured here (1024 SIMDs at the 2.4 GHz peak clock)."""
+    s, path = profiled_summary()
+    v = s.get("valu_issue") if s else None
+    if not v:
+        return None
+    n = v["valu_insts_per_launch"]
+    return {"valu_insts_per_launch": n,
+            "frac": n * VALU_CYCLES / (SIMDS * CLOCK_HZ * kernel_ms * 1e-3),
+            "source": path}
 
 
 def cpu_baseline(host, N, seconds, threads):
@@ -205,6 +230,7 @@ def main():
                          "bytes_per_qp": bpq,
                          "fp64_valu": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
                                        "frac": fp64_tf / FP64_PEAK_TFLOPS},
+                         "valu_issue": valu_issue(kernel_ms),
                          "mean_ipm_iters": float(iters.float().mean())},
             "gather_ms": gather_ms,
         }

@@ -11,4 +11,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OU
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/fetch -o run -- python3 $BENCH > $OUT/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/write -o run -- python3 $BENCH > $OUT/write.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -T --output-format csv -d $OUT/sq -o run -- python3 $BENCH > $OUT/sq.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 -T --output-format csv -d $OUT/sq2 -o run -- python3 $BENCH > $OUT/sq2.log 2>&1 || exit $?
 find $OUT -name "*.csv" | head -50

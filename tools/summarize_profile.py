@@ -26,6 +26,28 @@ def counters(path):
     return out
 
 
+SIMDS = 1024          # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9      # peak engine clock
+VALU_CYCLES = 4       # a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles
+
+
+def valu_issue(d, avg_ns):
+    """The roof that binds the QP kernel: VALU issue.  SQ_INSTS_VALU counts wave-instructions per
+    dispatch; each takes 4 SIMD cycles; the chip offers SIMDS x clock x time SIMD cycles."""
+    n = d.get("SQ_INSTS_VALU", {}).get("mean_per_dispatch")
+    if n is None:
+        return None
+    out = {"valu_insts_per_launch": n,
+           "valu_cycles_per_launch": n * VALU_CYCLES,
+           "chip_simd_cycles_per_launch": SIMDS * CLOCK_HZ * avg_ns * 1e-9,
+           "frac": n * VALU_CYCLES / (SIMDS * CLOCK_HZ * avg_ns * 1e-9)}
+    f64 = [d.get(c, {}).get("mean_per_dispatch") for c in
+           ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")]
+    if None not in f64:
+        out["fp64_insts_per_launch"] = {"fma": f64[0], "mul": f64[1], "add": f64[2]}
+    return out
+
+
 def main():
     tag = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof")
@@ -35,7 +57,7 @@ def main():
                 os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
     pmc = collections.defaultdict(dict)
-    for sub in ("fetch", "write", "sq"):
+    for sub in ("fetch", "write", "sq", "sq2"):
         for kname, cs in counters(os.path.join(src, sub, "run_counter_collection.csv")).items():
             for c, v in cs.items():
                 pmc[kname][c] = {"dispatches": len(v), "mean_per_dispatch": sum(v) / len(v)}
@@ -57,6 +79,7 @@ def main():
             "note": "FETCH_SIZE/WRITE_SIZE are KiB and count L2 misses to the fabric "
                     "(Infinity-Cache hits included); gfx950 FETCH_SIZE reads 1/2 of wide "
                     "coalesced stream bytes (MI355X_MICROARCH.md HBM section)"},
+        "valu_issue": valu_issue(d, float(stats[dom]["AverageNs"])),
         "pmc_per_kernel": pmc,
     }
     with open(os.path.join(dst, f"{tag}_summary.json"), "w") as f:
