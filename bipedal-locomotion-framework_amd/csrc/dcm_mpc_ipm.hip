@@ -44,8 +44,9 @@ struct KParams {
 
 // LDS carve-up (doubles).  The host sizes the launch with the same code (Lds(nullptr, ...)).
 //   A2  [M][N] double2  facet normals, knot-contiguous per facet (conflict-free b128 reads)
-//   bb  [M][N]          facet offsets
-//   IS  [M][N]          1 / s of every facet, refreshed once per iteration (W-phase)
+//   BI  [M][N] double2  (b, 1/s) of every facet: the offsets, and 1/s refreshed once per
+//                       iteration (W-phase), overwritten by the corrector's multiplier step;
+//                       one address and one b128 read serve both
 //   bnd [NW][16]        per-wavefront boundary values (see the kB* slots)
 //   red [4][NW][2]      reduction scratch, four rotating slots (no second barrier needed)
 constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
@@ -54,8 +55,8 @@ constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last kn
 constexpr int kBXi = 12;  // xi_{64w+64} (2): DCM past the last knot of wavefront w
 constexpr int kBnd = 16;
 struct Lds {
-    double2* A2;
-    double *bb, *IS, *bnd, *red, *flag;
+    double2 *A2, *BI;   // facet rows: normal (a_x, a_y); (b, 1/s), 1/s later the multiplier step
+    double *bnd, *red, *flag;
     size_t total;
     __host__ __device__ Lds(double* base, int N, int M, int NW)
     {
@@ -66,8 +67,7 @@ struct Lds {
             return p;
         };
         A2 = reinterpret_cast<double2*>(take(2 * (size_t)M * N));
-        bb = take((size_t)M * N);
-        IS = take((size_t)M * N);
+        BI = reinterpret_cast<double2*>(take(2 * (size_t)M * N));
         bnd = take((size_t)kBnd * NW);
         red = take(8 * (size_t)NW);
         flag = take(2);
@@ -321,7 +321,7 @@ __device__ __forceinline__ void affine_step(const Knot& K, double2 a, double bi,
 
 // Residual pass (oracle dcm_residuals) for this lane's knot; xk = xi_k.  Returns pres, ck.
 __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P, bool last,
-                                          const double2* A2, const double* bb, int N, int k,
+                                          const double2* A2, const double2* BI, int N, int k,
                                           int mmax, double xk0, double xk1, const double* rref,
                                           const double* xref, double& pres, double& ck)
 {
@@ -338,7 +338,7 @@ __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P
             if (i < km) {
                 const double2 a = A2[i * N + kx];
                 const double gr = FD2(a.x, K.r0, a.y, K.r1);
-                const double rpi = (gr + K.s[i]) - bb[i * N + kx];
+                const double rpi = (gr + K.s[i]) - BI[i * N + kx].x;
                 pres = nanmax(pres, fabs(rpi));
                 ck = fma(K.s[i], K.lam[i], ck);
                 rh0 = fma(a.x, K.lam[i], rh0);
@@ -652,7 +652,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         const double* bk = bin + st * M;
         for (int i = 0; i < K.m; ++i) {
             L.A2[i * N + k] = make_double2(Ak[2 * i], Ak[2 * i + 1]);
-            L.bb[i * N + k] = bk[i];
+            L.BI[i * N + k].x = bk[i];
         }
     }
     K.al = 1.0 + K.be;
@@ -695,7 +695,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         double xk0, xk1, pres, ck;
         // ---- initial point 2: full Newton step of the unconstrained QP (W = 0, lam = 0) ----
         xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
-        if (own) residuals(K, false, P, last, L.A2, L.bb, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+        if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
         bool ok = factor<NW>(K, P, 0.0, 0.0, 0.0, 0.0, bnd, N, nwa, k, wv, lane, own);
         const bool init_bad = __syncthreads_or(!ok);
         {
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 if (i < K.m) {
                     const double2 a = L.A2[i * N + k];
                     const double gr = FD2(a.x, K.r0, a.y, K.r1);
-                    const double sl = L.bb[i * N + k] - gr;
+                    const double sl = L.BI[i * N + k].x - gr;
                     K.s[i] = sl > 1e-2 ? sl : 1e-2;
                     K.lam[i] = 1.0;
                 }
@@ -726,7 +726,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         const int ntot = (int)R.sum((double)K.m);   // exact: small integers
         // ---- initial dual residual: costates nu_k = qx_k + alpha_k nu_{k+1} (backward scan) ----
         xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
-        if (own) residuals(K, true, P, last, L.A2, L.bb, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+        if (own) residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
         double dres = 0.0;
         {
             const double ga = own ? K.al : 0.0;
@@ -749,7 +749,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
             pres = 0.0;
             ck = 0.0;
-            if (own) residuals(K, true, P, last, L.A2, L.bb, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+            if (own) residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
             R.sum_nanmax(ck, pres);
             const double mu = ntot > 0 ? ck / (double)ntot : 0.0;
             if (!(mu == mu) || !(pres == pres) || !(dres == dres) || __builtin_isinf(mu)) {
@@ -776,14 +776,14 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
                         const double is = 1.0 / K.s[i];
-                        L.IS[i * N + kx] = is;
+                        L.BI[i * N + kx].y = is;
                         const double sg = K.lam[i] * is;
                         const double t0 = sg * a.x;
                         const double t1 = sg * a.y;
                         W00 = fma(t0, a.x, W00);
                         W01 = fma(t0, a.y, W01);
                         W11 = fma(t1, a.y, W11);
-                        const double rpi = facet_rp(K, a, L.bb[i * N + kx], i);
+                        const double rpi = facet_rp(K, a, L.BI[i * N + kx].x, i);
                         const double e = fma(K.lam[i], rpi, -(K.s[i] * K.lam[i])) * is;
                         g0 = fma(a.x, e, g0);
                         g1 = fma(a.y, e, g1);
@@ -797,11 +797,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i < km) {
                         const int ki = opaque(k);
                         const double2 ai = L.A2[i * N + ki];
-                        const double sgi = K.lam[i] * L.IS[i * N + ki];
+                        const double sgi = K.lam[i] * L.BI[i * N + ki].y;
 #pragma unroll
                         for (int j = 0; j < i; ++j) {
                             const double2 aj = L.A2[j * N + ki];
-                            const double sgj = K.lam[j] * L.IS[j * N + ki];
+                            const double sgj = K.lam[j] * L.BI[j * N + ki].y;
                             const double cr = fma(ai.x, aj.y, -(ai.y * aj.x));
                             dW = fma(sgi * sgj, cr * cr, dW);
                         }
@@ -831,8 +831,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i >= mm) break;
                     if (i < km) {
                         double ds, dl;
-                        const double is = L.IS[i * N + kx];
-                        affine_step(K, L.A2[i * N + kx], L.bb[i * N + kx], is, i, dra0, dra1, ds, dl);
+                        const double is = L.BI[i * N + kx].y;
+                        affine_step(K, L.A2[i * N + kx], L.BI[i * N + kx].x, is, i, dra0, dra1, ds, dl);
                         if (ds < 0.0) q = keepmax(q, (-ds) * is);
                         if (dl < 0.0) q = keepmax(q, (K.s[i] + ds) * is);
                     }
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i >= mm) break;
                     if (i < km) {
                         double ds, dl;
-                        affine_step(K, L.A2[i * N + kx], L.bb[i * N + kx], L.IS[i * N + kx], i, dra0,
+                        affine_step(K, L.A2[i * N + kx], L.BI[i * N + kx].x, L.BI[i * N + kx].y, i, dra0,
                                     dra1, ds, dl);
                         ck = fma(fma(a_aff, ds, K.s[i]), fma(a_aff, dl, K.lam[i]), ck);
                     }
@@ -875,8 +875,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i >= mm) break;
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
-                        const double bi = L.bb[i * N + kx];
-                        const double is = L.IS[i * N + kx];
+                        const double bi = L.BI[i * N + kx].x;
+                        const double is = L.BI[i * N + kx].y;
                         double ds, dl;
                         affine_step(K, a, bi, is, i, dra0, dra1, ds, dl);
                         const double rc = FD2(K.s[i], K.lam[i], ds, dl) - sigma_mu;
@@ -900,8 +900,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i >= mm) break;
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
-                        const double bi = L.bb[i * N + kx];
-                        const double is = L.IS[i * N + kx];
+                        const double bi = L.BI[i * N + kx].x;
+                        const double is = L.BI[i * N + kx].y;
                         double ads, adl;
                         affine_step(K, a, bi, is, i, dra0, dra1, ads, adl);
                         const double rc = FD2(K.s[i], K.lam[i], ads, adl) - sigma_mu;
@@ -910,7 +910,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         const double dl = fma(-K.lam[i], ds, -rc) * is;
                         if (ds < 0.0) q = keepmax(q, (-ds) * is);
                         if (dl < 0.0) q = keepmax(q, (-dl) / K.lam[i]);
-                        L.IS[i * N + kx] = dl;   // 1/s is dead now: keep the multiplier step
+                        L.BI[i * N + kx].y = dl;   // 1/s is dead now: keep the multiplier step
                     }
                 }
             }
@@ -925,9 +925,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     if (i >= mm) break;
                     if (i < km) {
                         const double2 fa = L.A2[i * N + kx];
-                        const double ds = (-facet_rp(K, fa, L.bb[i * N + kx], i)) - FD2(fa.x, dr0, fa.y, dr1);
+                        const double ds = (-facet_rp(K, fa, L.BI[i * N + kx].x, i)) - FD2(fa.x, dr0, fa.y, dr1);
                         K.s[i] = fma(a, ds, K.s[i]);
-                        K.lam[i] = fma(a, L.IS[i * N + kx], K.lam[i]);
+                        K.lam[i] = fma(a, L.BI[i * N + kx].y, K.lam[i]);
                     }
                 }
                 K.r0 = fma(a, dr0, K.r0);   // after the facet steps, which use the old r
