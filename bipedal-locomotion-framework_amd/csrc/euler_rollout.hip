@@ -96,7 +96,11 @@ __global__ __launch_bounds__(256) void lti_dynamics_kernel(int n, int m,
 // of loads per lane, 16 B each on full aligned chunks), transposed through LDS; the recurrence
 // runs lane-per-problem and the xi chunk leaves through LDS the same way.  (Prefetching the next
 // chunk during the recurrence measured no faster and cost 96 VGPRs.)
-constexpr int KC = 16;
+#ifndef BLF_ROLL_KC
+#define BLF_ROLL_KC 32
+#endif
+constexpr int KC = BLF_ROLL_KC;   // knots per chunk: 64 x 98 x 8 B of LDS per wave (16: 12 % slower,
+                                  // per-chunk overhead; 50: the register chunk spills)
 constexpr int kRollSw = 2 * KC + 1;   // padded LDS row of the vrp / xi chunk
 
 struct RollChunk {
