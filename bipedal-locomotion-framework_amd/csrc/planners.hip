@@ -92,19 +92,62 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     const int n = t < nprob ? npts[p0 + t] : 0;
     int nf = -1;
     if (t < nprob && n >= 3 && n <= P) {
-        for (int i = 1; i < n; ++i) {
-            const double vx = HX(i), vy = HY(i);
-            int j = i - 1;
-            while (j >= 0) {
-                const double ux = HX(j), uy = HY(j);
-                if (!(ux > vx || (ux == vx && uy > vy))) break;
-                HX(j + 1) = ux;
-                HY(j + 1) = uy;
-                --j;
+        // Up to 8 points with finite coordinates: a 19-comparator sorting network in registers,
+        // branch-free, keyed (x, y, original index) -- for finite keys exactly the permutation of
+        // the stable insertion sort below.  Non-finite coordinates (NaN comparisons) keep the
+        // insertion sort, so every input sorts as the oracle sorts it.
+        bool done = false;
+        if (P <= 8) {
+            double x[8], y[8];
+            int id[8];
+            bool clean = true;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const bool in = i < n;
+                x[i] = in ? HX(i) : __builtin_inf();
+                y[i] = in ? HY(i) : __builtin_inf();
+                id[i] = i;
+                clean = clean && (!in || (__builtin_isfinite(x[i]) && __builtin_isfinite(y[i])));
             }
-            HX(j + 1) = vx;
-            HY(j + 1) = vy;
+            if (clean) {
+#define HULL_CE(a, b)                                                                       \
+    do {                                                                                    \
+        const bool g = x[a] > x[b] || (x[a] == x[b] && (y[a] > y[b] || (y[a] == y[b] && id[a] > id[b]))); \
+        const double xa = x[a], ya = y[a];                                                  \
+        const int ia = id[a];                                                               \
+        x[a] = g ? x[b] : xa; y[a] = g ? y[b] : ya; id[a] = g ? id[b] : ia;                 \
+        x[b] = g ? xa : x[b]; y[b] = g ? ya : y[b]; id[b] = g ? ia : id[b];                 \
+    } while (0)
+                HULL_CE(0, 2); HULL_CE(1, 3); HULL_CE(4, 6); HULL_CE(5, 7);
+                HULL_CE(0, 4); HULL_CE(1, 5); HULL_CE(2, 6); HULL_CE(3, 7);
+                HULL_CE(0, 1); HULL_CE(2, 3); HULL_CE(4, 5); HULL_CE(6, 7);
+                HULL_CE(2, 4); HULL_CE(3, 5);
+                HULL_CE(1, 4); HULL_CE(3, 6);
+                HULL_CE(1, 2); HULL_CE(3, 4); HULL_CE(5, 6);
+#undef HULL_CE
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (i < n) {
+                        HX(i) = x[i];
+                        HY(i) = y[i];
+                    }
+                done = true;
+            }
         }
+        if (!done)
+            for (int i = 1; i < n; ++i) {
+                const double vx = HX(i), vy = HY(i);
+                int j = i - 1;
+                while (j >= 0) {
+                    const double ux = HX(j), uy = HY(j);
+                    if (!(ux > vx || (ux == vx && uy > vy))) break;
+                    HX(j + 1) = ux;
+                    HY(j + 1) = uy;
+                    --j;
+                }
+                HX(j + 1) = vx;
+                HY(j + 1) = vy;
+            }
         // monotone chain; (ax, ay) = STK(k-2), (bx, by) = STK(k-1) when they exist
         int k = 0;
         double ax = 0.0, ay = 0.0, bx = 0.0, by = 0.0;

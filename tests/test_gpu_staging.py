@@ -125,3 +125,25 @@ def test_fbk_staging(handle, oracle, B, n, misalign):
         np.testing.assert_array_equal(dpos.cpu().numpy()[i], p)
         np.testing.assert_array_equal(dRot.cpu().numpy()[i], Rn)
         np.testing.assert_array_equal(dqq.cpu().numpy()[i], qn)
+
+
+def test_hull2d_ties_duplicates_nonfinite(handle, oracle):
+    """Sorting-network path (P <= 8) vs the insertion sort: equal x, duplicate points, collinear
+    runs, and NaN / inf coordinates (those polygons take the insertion-sort path)."""
+    rng = np.random.default_rng(17)
+    B, P_ = 96, 8
+    pts = np.round(rng.normal(size=(B, P_, 2)), 1)        # coarse grid: many equal x and y
+    npts = rng.integers(3, P_ + 1, B).astype(np.int32)
+    pts[::5, 1] = pts[::5, 0]                               # duplicate point
+    pts[1::5, :4, 0] = 0.3                                  # equal x for four points
+    pts[2::7, :5] = np.c_[np.arange(5) * 0.1, np.arange(5) * 0.2]   # collinear run
+    pts[3::11, 2, 0] = np.nan
+    pts[4::13, 1, 1] = np.inf
+    pts[5::17, 0, 0] = -np.inf
+    A, b, nf = handle.hull2d_hrep(_d(pts), _d(npts, torch.int32), 8)
+    A, b, nf = A.cpu().numpy(), b.cpu().numpy(), nf.cpu().numpy()
+    for i in range(B):
+        Ao, bo, mo = oracle.hull2d_hrep(pts[i, :npts[i]], 8)
+        assert nf[i] == mo, i
+        np.testing.assert_array_equal(A[i], Ao)
+        np.testing.assert_array_equal(b[i], bo)
