@@ -83,6 +83,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C "
                               f"bipedal-locomotion-framework_amd)")
+        # One HIP runtime per process: libblf.so needs libamdhip64.so.7, and torch ships its own
+        # copy.  Loaded after torch, libblf.so binds to torch's (same soname) and shares its
+        # device memory and streams; loaded first, the process would hold two runtimes and the
+        # one that initialises second sees no device.  So torch, when installed, is loaded first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         L.blf_create.argtypes = [ctypes.POINTER(_vp), _i32]
         L.blf_destroy.argtypes = [_vp]

@@ -68,3 +68,13 @@ def test_oracle_is_not_linked_by_the_product():
         assert "oracle" not in out
         syms = subprocess.run(["nm", "-D", path], capture_output=True, text=True).stdout
         assert "orc_" not in syms
+
+
+def test_lib_loads_after_torch_runtime():
+    """native.lib() maps torch's HIP runtime before libblf.so, so the library binds to it (one
+    runtime per process; loaded first, it would own the device and torch would see none)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, 'bipedal-locomotion-framework_amd'); "
+            "from blf import native; native.lib(); assert 'torch' in sys.modules")
+    subprocess.check_call([sys.executable, "-c", code], cwd=ROOT)
