@@ -5,11 +5,13 @@
  *   (host bookkeeping, run everywhere), IntegratorTest.cpp:27-75 (device), a 2-D
  *   ConvexHullHelperTest (device), the QuinticSpline and TimeVaryingDCMPlanner::advance (device),
  *   ContinousContactModelTest.cpp:30-214 (device) and FloatingBaseSystemKinematics under
- *   ForwardEuler (device).
+ *   ForwardEuler (device), and ParametersHandlerYarpTest.cpp:30-140 on the reference's own
+ *   config.ini (tests/golden/parameters_config.ini) read by StdImplementation::setFromFile.
  * usage: blf_host_tests [cpu|gpu|all]   (exit status = number of failed checks)
  */
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <iostream>
@@ -608,9 +610,88 @@ static void testFloatingBaseDynamics()
     REQUIRE(system->setMassMatrixRegularization(blf::MatrixXd(9, 9)));
 }
 
+// ---- ParametersHandlerYarpTest.cpp:30-140, on the reference's tests/config.ini -----------------
+static std::string g_golden = "tests/golden";
+
+static void testParametersHandler()
+{
+    using namespace ParametersHandler;
+    auto handler = std::make_shared<StdImplementation>();
+    REQUIRE(handler->setFromFile(g_golden + "/parameters_config.ini"));
+    int answer = 0;
+    REQUIRE(handler->getParameter("answer_to_the_ultimate_question_of_life", answer));
+    REQUIRE(answer == 42);
+    double pi = 0.0;
+    REQUIRE(handler->getParameter("pi", pi));
+    REQUIRE(pi == 3.14);
+    std::string john;
+    REQUIRE(handler->getParameter("John", john));
+    REQUIRE(john == "Smith");
+    REQUIRE_FALSE(handler->getParameter("pi", answer));   // 3.14 is not an integer
+    handler->setParameter("John", "Doe");
+    REQUIRE(handler->getParameter("John", john));
+    REQUIRE(john == "Doe");
+    const std::vector<int> fibonacci = {1, 1, 2, 3, 5, 8, 13, 21};
+    std::vector<int> fib;
+    REQUIRE(handler->getParameter("Fibonacci Numbers", fib));
+    REQUIRE(fib == fibonacci);
+    const std::vector<int> more = {21, 34, 55};
+    handler->setParameter("Fibonacci Numbers", more);
+    REQUIRE(handler->getParameter("Fibonacci Numbers", fib));
+    REQUIRE(fib == more);
+
+    // the [CARTOONS] section is a group
+    auto cartoons = handler->getGroup("CARTOONS").lock();
+    REQUIRE(cartoons);
+    if (cartoons)
+    {
+        std::vector<std::string> nephews;
+        REQUIRE(cartoons->getParameter("Donald's nephews", nephews));
+        REQUIRE((nephews == std::vector<std::string>{"Huey", "Dewey", "Louie"}));
+        REQUIRE(cartoons->getParameter("Fibonacci_Numbers", fib));
+        REQUIRE(fib == fibonacci);
+        REQUIRE(cartoons->getParameter("John", john));
+        REQUIRE(john == "Doe");
+    }
+    REQUIRE(handler->toString().find("CARTOONS") != std::string::npos);
+
+    // is Empty / set group / clear
+    auto fresh = std::make_shared<StdImplementation>();
+    REQUIRE_FALSE(fresh->getGroup("CARTOONS").lock());
+    auto group = std::make_shared<StdImplementation>();
+    REQUIRE(fresh->setGroup("CARTOONS", group));
+    REQUIRE(fresh->getGroup("CARTOONS").lock());
+    REQUIRE(group->isEmpty());
+    group->setParameter("value", 10);
+    REQUIRE_FALSE(group->isEmpty());
+    REQUIRE_FALSE(handler->isEmpty());
+    handler->clear();
+    REQUIRE(handler->isEmpty());
+    REQUIRE_FALSE(fresh->setGroup("null", nullptr));
+
+    // the keys the DCM path reads, from a file
+    auto cfg = std::make_shared<StdImplementation>();
+    REQUIRE(cfg->setFromString("// contact model\nlength 0.12\nwidth 0.09 # m\nspring_coeff 2000\n"
+                               "damper_coeff 100\nrho 0.01\nw_xi (100, 100)\nflag true\n"));
+    double len = 0.0, k = 0.0, rho = 0.0;
+    bool flag = false;
+    std::vector<double> wxi;
+    REQUIRE(cfg->getParameter("length", len) && len == 0.12);
+    REQUIRE(cfg->getParameter("spring_coeff", k) && k == 2000.0);
+    REQUIRE(cfg->getParameter("rho", rho) && rho == 0.01);
+    REQUIRE(cfg->getParameter("w_xi", wxi) && wxi.size() == 2 && wxi[1] == 100.0);
+    REQUIRE(cfg->getParameter("flag", flag) && flag);
+    ContactModels::ContinuousContactModel model;
+    REQUIRE(model.initialize(cfg));
+    REQUIRE_FALSE(StdImplementation().setFromFile(g_golden + "/does_not_exist.ini"));
+    REQUIRE_FALSE(cfg->setFromString("key (1, 2"));
+    REQUIRE(cfg->isEmpty());
+}
+
 int main(int argc, char** argv)
 {
     const std::string which = argc > 1 ? argv[1] : "all";
+    if (const char* g = std::getenv("BLF_GOLDEN_DIR")) g_golden = g;
     const bool cpu = which == "cpu" || which == "all";
     const bool gpu = which == "gpu" || which == "all";
     struct T { const char* name; bool device; std::function<void()> fn; };
@@ -618,6 +699,7 @@ int main(int argc, char** argv)
         {"ContactList", false, testContactList},
         {"ContactPhaseList", false, testContactPhaseList},
         {"VariablesHandler", false, testVariablesHandler},
+        {"ParametersHandler (config.ini)", false, testParametersHandler},
         {"Integrator - Linear system", true, testIntegratorLTI},
         {"Convex Hull helper (2-D)", true, testConvexHull},
         {"QuinticSpline", true, testQuinticSpline},

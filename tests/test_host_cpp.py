@@ -19,7 +19,8 @@ def _ensure_built():
 
 def _run(which):
     _ensure_built()
-    r = subprocess.run([BIN, which], capture_output=True, text=True, timeout=600)
+    env = dict(os.environ, BLF_GOLDEN_DIR=os.path.join(ROOT, "tests", "golden"))
+    r = subprocess.run([BIN, which], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failed" in r.stdout, r.stdout
     return r.stdout
@@ -27,7 +28,7 @@ def _run(which):
 
 def test_host_bookkeeping_tests():
     out = _run("cpu")
-    for name in ("ContactList", "ContactPhaseList", "VariablesHandler"):
+    for name in ("ContactList", "ContactPhaseList", "VariablesHandler", "ParametersHandler"):
         assert any(line.startswith(name) and line.rstrip().endswith("ok") for line in out.splitlines())
 
 
