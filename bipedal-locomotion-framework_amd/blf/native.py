@@ -22,7 +22,9 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_quintic_fit", "blf_quintic_eval",
-            "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_flops_per_iter",
+            "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_solve_warm",
+            "blf_dcm_phase_expand",
+            "blf_dcm_mpc_flops_per_iter",
             "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
             "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate"]
 
@@ -73,6 +75,16 @@ class DcmMpcSolution(ctypes.Structure):
     _fields_ = [("xi", _vp), ("vrp", _vp), ("status", _vp), ("iters", _vp)]
 
 
+class PhaseTable(ctypes.Structure):
+    _fields_ = [("max_phases", _i32), ("max_facets", _i32), ("nphases", _vp), ("begin", _vp),
+                ("end", _vp), ("A", _vp), ("b", _vp), ("nfacets", _vp), ("ref", _vp)]
+
+
+class DcmMpcWarmStart(ctypes.Structure):
+    _fields_ = [("vrp", _vp), ("lambda_", _vp), ("shift", _i32), ("reserved", _i32),
+                ("floor", _f64)]
+
+
 _LIB = None
 
 
@@ -109,6 +121,12 @@ def lib():
         L.blf_dcm_mpc_solve.argtypes = [_vp, ctypes.POINTER(DcmMpcParams),
                                         ctypes.POINTER(DcmMpcProblem), _i64,
                                         ctypes.POINTER(DcmMpcSolution), _vp]
+        L.blf_dcm_mpc_solve_warm.argtypes = [_vp, ctypes.POINTER(DcmMpcParams),
+                                             ctypes.POINTER(DcmMpcProblem),
+                                             ctypes.POINTER(DcmMpcWarmStart), _i64,
+                                             ctypes.POINTER(DcmMpcSolution), _vp, _vp]
+        L.blf_dcm_phase_expand.argtypes = [_vp, ctypes.POINTER(PhaseTable), _i64, _f64, _i32,
+                                           _i64, _vp, _vp, _vp, _vp, _vp, _vp]
         L.blf_dcm_mpc_flops_per_iter.argtypes = [_i32, _i64]
         L.blf_contact_model_eval.argtypes = [_vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                              _vp, _vp]
@@ -304,9 +322,12 @@ class Handle:
             _ptr(idx, torch.int32, (S, Q), "knot_idx"), _stream(stream)))
         return pva, idx
 
-    def dcm_mpc_solve(self, prob, params=None, out=None, stream=None):
+    def dcm_mpc_solve(self, prob, params=None, out=None, stream=None, warm=None,
+                      lambda_out=False):
         """prob: dict of device tensors xi_init [B,2], omega [B,N], xi_ref [B,N+1,2],
-        vrp_ref [B,N,2], A [B,N,M,2], b [B,N,M], nfacets [B,N] (int32)."""
+        vrp_ref [B,N,2], A [B,N,M,2], b [B,N,M], nfacets [B,N] (int32).
+        warm: None (cold start) or dict(vrp [B,N,2], lam [B,N,M], shift, floor)
+        (blf_dcm_mpc_solve_warm); lambda_out: also return the final multipliers out["lam"]."""
         torch = _torch()
         B, N = prob["omega"].shape
         M = prob["b"].shape[2]
@@ -332,9 +353,73 @@ class Handle:
             _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
             _ptr(out["status"], torch.int32, (B,), "status"),
             _ptr(out["iters"], torch.int32, (B,), "iters"))
-        self._keep = (pb, so)
-        _check(lib().blf_dcm_mpc_solve(self._h, ctypes.byref(p), ctypes.byref(pb), B,
-                                       ctypes.byref(so), _stream(stream)))
+        ws = None
+        if warm is not None:
+            ws = DcmMpcWarmStart(_ptr(warm["vrp"], torch.float64, (B, N, 2), "warm vrp"),
+                                 _ptr(warm["lam"], torch.float64, (B, N, M), "warm lam"),
+                                 int(warm.get("shift", 1)), 0, float(warm.get("floor", 1e-2)))
+        lam_ptr = None
+        if lambda_out:
+            if "lam" not in out:
+                out["lam"] = torch.empty((B, N, M), dtype=torch.float64, device=dev)
+            lam_ptr = _ptr(out["lam"], torch.float64, (B, N, M), "lam")
+        self._keep = (pb, so, ws)
+        if ws is None and lam_ptr is None:
+            _check(lib().blf_dcm_mpc_solve(self._h, ctypes.byref(p), ctypes.byref(pb), B,
+                                           ctypes.byref(so), _stream(stream)))
+        else:
+            _check(lib().blf_dcm_mpc_solve_warm(
+                self._h, ctypes.byref(p), ctypes.byref(pb),
+                ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(so), lam_ptr,
+                _stream(stream)))
+        return out
+
+    def phase_table(self, nphases, begin, end, corners, ncorners, max_facets=8, ref=None,
+                    stream=None):
+        """Device phase table: the H-rep of every phase's support polygon (blf_hull2d_hrep over
+        corners [B,P,C,2] / ncorners [B,P]) plus the phases' times and centroid references.
+        ref [B,P,2]: the phases' reference points (default: the centroid of the corners)."""
+        torch = _torch()
+        B, P, C, _ = corners.shape
+        A, b, nf = self.hull2d_hrep(corners.reshape(B * P, C, 2).contiguous(),
+                                    ncorners.reshape(B * P).contiguous(), max_facets,
+                                    stream=stream)
+        if ref is None:
+            cnt = ncorners.to(torch.float64).clamp(min=1)[..., None]
+            ref = (corners.sum(dim=2) / cnt).contiguous()
+        return dict(nphases=nphases, phase_begin=begin, phase_end=end,
+                    phase_A=A.view(B, P, max_facets, 2), phase_b=b.view(B, P, max_facets),
+                    phase_nf=nf.view(B, P), phase_ref=ref)
+
+    def dcm_phase_expand(self, table, start, dt, horizon, out=None, stream=None):
+        """blf_dcm_phase_expand: window arrays (A, b, nfacets, xi_ref, vrp_ref) of knots
+        (start + k) dt, k = 0..horizon, from a phase table (phase_table() or the same keys)."""
+        torch = _torch()
+        B, P = table["phase_begin"].shape
+        M = table["phase_b"].shape[2]
+        N = horizon
+        dev = table["phase_begin"].device
+        if out is None:
+            out = dict(A=torch.empty((B, N, M, 2), dtype=torch.float64, device=dev),
+                       b=torch.empty((B, N, M), dtype=torch.float64, device=dev),
+                       nfacets=torch.empty((B, N), dtype=torch.int32, device=dev),
+                       xi_ref=torch.empty((B, N + 1, 2), dtype=torch.float64, device=dev),
+                       vrp_ref=torch.empty((B, N, 2), dtype=torch.float64, device=dev))
+        tb = PhaseTable(P, M, _ptr(table["nphases"], torch.int32, (B,), "nphases"),
+                        _ptr(table["phase_begin"], torch.float64, (B, P), "phase_begin"),
+                        _ptr(table["phase_end"], torch.float64, (B, P), "phase_end"),
+                        _ptr(table["phase_A"], torch.float64, (B, P, M, 2), "phase_A"),
+                        _ptr(table["phase_b"], torch.float64, (B, P, M), "phase_b"),
+                        _ptr(table["phase_nf"], torch.int32, (B, P), "phase_nf"),
+                        _ptr(table["phase_ref"], torch.float64, (B, P, 2), "phase_ref"))
+        self._keep = tb
+        _check(lib().blf_dcm_phase_expand(
+            self._h, ctypes.byref(tb), int(start), float(dt), N, B,
+            _ptr(out["A"], torch.float64, (B, N, M, 2), "A"),
+            _ptr(out["b"], torch.float64, (B, N, M), "b"),
+            _ptr(out["nfacets"], torch.int32, (B, N), "nfacets"),
+            _ptr(out["xi_ref"], torch.float64, (B, N + 1, 2), "xi_ref"),
+            _ptr(out["vrp_ref"], torch.float64, (B, N, 2), "vrp_ref"), _stream(stream)))
         return out
 
     # --- C3 pipeline: corner sets -> polygons (device hull) -> QP arrays ---

@@ -119,22 +119,28 @@ def make_batch(batch, horizon=100, n_footsteps=6, dt=0.02, seed=SEED, start=0):
     phases = phases_from_schedule(lists, dt)
     corners_all = rectangle_corners(poses)                      # [B, F, 4, 2]
     foot_names = ["left", "right"]
-    corners = np.zeros((batch, horizon + 1, 8, 2))
-    ncorners = np.zeros((batch, horizon + 1), dtype=np.int32)
+    # the phase table: each phase's active-contact corners (sorted by list name) and centroid
+    NP = len(phases)
+    ph_corners = np.zeros((batch, NP, 8, 2))
+    ph_ncorners = np.zeros((batch, NP), dtype=np.int32)
+    for pi, (b0, e0, act) in enumerate(phases):
+        slots = [lists[foot_names[li]][ci][2] for li, ci in sorted(act.items())]
+        pts = np.concatenate([corners_all[:, sl] for sl in slots], axis=1)
+        ph_corners[:, pi, :pts.shape[1]] = pts
+        ph_ncorners[:, pi] = pts.shape[1]
+    ph_ref = ph_corners.sum(axis=2) / ph_ncorners[:, :, None].astype(np.float64)
+    # knot -> phase: begin <= t_k < end (t_k = k dt)
     knot_phase = np.full(horizon + 1, -1, dtype=np.int32)
     for k in range(horizon + 1):
         t = k * dt
         for pi, (b0, e0, act) in enumerate(phases):
             if b0 <= t < e0:
                 knot_phase[k] = pi
-                slots = [lists[foot_names[li]][ci][2] for li, ci in sorted(act.items())]
-                pts = np.concatenate([corners_all[:, sl] for sl in slots], axis=1)
-                corners[:, k, :pts.shape[1]] = pts
-                ncorners[:, k] = pts.shape[1]
                 break
         assert knot_phase[k] >= 0, "knot outside every contact phase"
-    cnt = ncorners[:, :, None].astype(np.float64)
-    centroid = corners.sum(axis=2) / cnt
+    corners = np.ascontiguousarray(ph_corners[:, knot_phase])
+    ncorners = np.ascontiguousarray(ph_ncorners[:, knot_phase])
+    centroid = np.ascontiguousarray(ph_ref[:, knot_phase])
     phi = 2.0 * np.pi * draws[:, 0, 5]
     z = 0.53 + 0.02 * np.sin(2.0 * np.pi * np.arange(horizon)[None, :] / horizon + phi[:, None])
     omega = np.sqrt(GRAVITY / z)
@@ -149,6 +155,12 @@ def make_batch(batch, horizon=100, n_footsteps=6, dt=0.02, seed=SEED, start=0):
         ncorners=np.ascontiguousarray(ncorners),
         poses=poses,
         knot_phase=knot_phase,
+        nphases=np.full(batch, NP, dtype=np.int32),
+        phase_begin=np.ascontiguousarray(np.broadcast_to([p[0] for p in phases], (batch, NP))),
+        phase_end=np.ascontiguousarray(np.broadcast_to([p[1] for p in phases], (batch, NP))),
+        phase_corners=ph_corners,
+        phase_ncorners=ph_ncorners,
+        phase_ref=np.ascontiguousarray(ph_ref),
         dt=dt,
         schedule=lists,
     )
@@ -182,3 +194,20 @@ def swing_splines(prob, apex_height=0.05, queries=32):
             tq.append(np.broadcast_to(np.linspace(t0, t1, queries), (B, queries)))
     return (np.ascontiguousarray(np.concatenate(kt)), np.ascontiguousarray(np.concatenate(kp)),
             np.ascontiguousarray(np.concatenate(tq)))
+
+
+def window(full, start, horizon, xi_init=None):
+    """Receding-horizon window [start, start + horizon) of a longer plan (make_batch with a
+    horizon of at least start + horizon): the per-knot arrays of knots start.., the references of
+    knots start..start+horizon, and xi_init (default: the plan's).  Works on numpy arrays and on
+    device tensors alike (the A, b, nfacets keys are sliced when present)."""
+    s, N = start, horizon
+    out = {"xi_init": full["xi_init"] if xi_init is None else xi_init}
+    for k in ("omega", "vrp_ref", "A", "b", "nfacets"):
+        if k in full:
+            out[k] = full[k][:, s:s + N]
+    out["xi_ref"] = full["xi_ref"][:, s:s + N + 1]
+    for k in list(out):
+        v = out[k]
+        out[k] = v.contiguous() if hasattr(v, "contiguous") else np.ascontiguousarray(v)
+    return out

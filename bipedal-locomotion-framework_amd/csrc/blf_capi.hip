@@ -1,5 +1,6 @@
 // blf_capi.hip — the extern "C" boundary declared in include/blf/blf_c.h: argument validation,
 // the reference's error semantics, and dispatch to the kernels' launchers.
+#include <cmath>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -209,9 +210,33 @@ void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon)
     p->tol_dual = 1e-9;
 }
 
-blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
-                             const blf_dcm_mpc_problem* problem, int64_t batch,
-                             const blf_dcm_mpc_solution* solution, void* stream)
+blf_status blf_dcm_phase_expand(blf_handle* handle, const blf_phase_table* ph,
+                                int64_t start_knot, double dt, int32_t horizon, int64_t batch,
+                                double* A, double* b, int32_t* nfacets, double* xi_ref,
+                                double* vrp_ref, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_dcm_phase_expand: null handle");
+    BLF_REQUIRE(ph != nullptr, "blf_dcm_phase_expand: null phase table");
+    BLF_REQUIRE(ph->max_phases >= 1, "blf_dcm_phase_expand: max_phases %d < 1", ph->max_phases);
+    BLF_REQUIRE(ph->max_facets >= 1 && ph->max_facets <= kMaxFacets,
+                "blf_dcm_phase_expand: max_facets %d outside [1, %d]", ph->max_facets, kMaxFacets);
+    BLF_REQUIRE(horizon >= 1, "blf_dcm_phase_expand: horizon %d < 1", horizon);
+    BLF_REQUIRE(dt > 0 && std::isfinite(dt), "blf_dcm_phase_expand: dt must be finite and > 0");
+    BLF_REQUIRE(start_knot >= 0, "blf_dcm_phase_expand: start_knot < 0");
+    BLF_REQUIRE(batch >= 0, "blf_dcm_phase_expand: negative batch");
+    BLF_REQUIRE(batch == 0 || (ph->nphases && ph->begin && ph->end && ph->A && ph->b &&
+                               ph->nfacets && ph->ref && A && b && nfacets && xi_ref && vrp_ref),
+                "blf_dcm_phase_expand: null buffer");
+    return launch_phase_expand(ph->max_phases, ph->nphases, ph->begin, ph->end, ph->A, ph->b,
+                               ph->nfacets, ph->ref, ph->max_facets, start_knot, dt, horizon,
+                               batch, A, b, nfacets, xi_ref, vrp_ref, (hipStream_t)stream);
+}
+
+blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                  const blf_dcm_mpc_problem* problem,
+                                  const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                                  const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                  void* stream)
 {
     BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve: null handle");
     BLF_REQUIRE(params && problem && solution, "blf_dcm_mpc_solve: null argument");
@@ -229,7 +254,25 @@ blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* param
                                problem->vrp_ref && problem->A && problem->b && problem->nfacets &&
                                solution->xi && solution->vrp && solution->status && solution->iters),
                 "blf_dcm_mpc_solve: null buffer");
-    return launch_dcm_mpc(params, problem, batch, solution, (hipStream_t)stream);
+    if (warm) {
+        BLF_REQUIRE(batch == 0 || (warm->vrp && warm->lambda),
+                    "blf_dcm_mpc_solve_warm: null warm-start buffer");
+        BLF_REQUIRE(warm->shift >= 0, "blf_dcm_mpc_solve_warm: shift %d < 0", warm->shift);
+        BLF_REQUIRE(warm->reserved == 0, "blf_dcm_mpc_solve_warm: reserved must be 0");
+        BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
+                    "blf_dcm_mpc_solve_warm: floor must be finite and > 0");
+        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out,
+                    "blf_dcm_mpc_solve_warm: warm-start buffers must not alias the outputs");
+    }
+    return launch_dcm_mpc(params, problem, warm, batch, solution, lambda_out, (hipStream_t)stream);
+}
+
+blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
+                             const blf_dcm_mpc_problem* problem, int64_t batch,
+                             const blf_dcm_mpc_solution* solution, void* stream)
+{
+    return blf_dcm_mpc_solve_warm(handle, params, problem, nullptr, batch, solution, nullptr,
+                                  stream);
 }
 
 double blf_dcm_mpc_flops_per_iter(int32_t horizon, int64_t active_facets)

@@ -43,8 +43,15 @@ blf_status launch_quintic_fit(const double* kt, const double* kp, int32_t K1, in
 blf_status launch_quintic_eval(const double* kt, const double* coeffs, int32_t K1, int32_t D,
                                int64_t S, const double* tq, int32_t Q, double* pva,
                                int32_t* idx, hipStream_t s);
+blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* begin,
+                               const double* end, const double* pA, const double* pb,
+                               const int32_t* pnf, const double* pref, int32_t M,
+                               int64_t start_knot, double dt, int32_t N, int64_t batch, double* A,
+                               double* b, int32_t* nfacets, double* xi_ref, double* vrp_ref,
+                               hipStream_t s);
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
-                          int64_t batch, const blf_dcm_mpc_solution* sol, hipStream_t s);
+                          const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                          const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);
 blf_status launch_contact_eval(const double* prm, int shared, const double* twist,
                                const double* pose, const double* null_pose, int64_t batch,
                                double* wrench, double* autonomous, double* control,

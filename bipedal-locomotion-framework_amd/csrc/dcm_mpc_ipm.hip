@@ -39,7 +39,9 @@ __device__ unsigned long long g_blf_stamps[8];
 
 struct KParams {
     int N, M, max_iter;
+    int ws_shift;        // warm start: knot k starts from knot k + ws_shift (ws_vrp != nullptr)
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_mu, tol_p, tol_d;
+    double ws_floor;     // warm start: s, lambda >= ws_floor
 };
 
 // LDS carve-up (doubles).  The host sizes the launch with the same code (Lds(nullptr, ...)).
@@ -609,9 +611,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
     const double* __restrict__ Ain, const double* __restrict__ bin,
-    const int32_t* __restrict__ nfacets, double* __restrict__ xi_out,
+    const int32_t* __restrict__ nfacets, const double* __restrict__ ws_vrp,
+    const double* __restrict__ ws_lam, double* __restrict__ xi_out,
     double* __restrict__ vrp_out, int32_t* __restrict__ status_out,
-    int32_t* __restrict__ iters_out)
+    int32_t* __restrict__ iters_out, double* __restrict__ lam_out)
 {
     constexpr int NW = NT / kWave;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -627,6 +630,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     const bool own = k < N;
     const bool last = k == N - 1;
     const int64_t p = blockIdx.x;
+    const bool warm = ws_vrp != nullptr;                  // uniform over the launch
+    const bool ws = warm && k + P.ws_shift < N;           // this knot starts from the warm start
     STAMP(t_start);
 
     // ---- load the knot this thread owns ----
@@ -646,8 +651,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         if (bad) K.m = 0;
         K.w = omega[st];
         K.be = P.dt * K.w;
-        K.r0 = vrp_ref[2 * st];
-        K.r1 = vrp_ref[2 * st + 1];
+        const double* r0 = ws ? ws_vrp + 2 * P.ws_shift : vrp_ref;
+        K.r0 = r0[2 * st];
+        K.r1 = r0[2 * st + 1];
         const double* Ak = Ain + st * M * 2;
         const double* bk = bin + st * M;
         for (int i = 0; i < K.m; ++i) {
@@ -693,24 +699,31 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         status = BLF_QP_BAD_FACETS;
     } else {
         double xk0, xk1, pres, ck;
-        // ---- initial point 2: full Newton step of the unconstrained QP (W = 0, lam = 0) ----
-        xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
-        if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
-        bool ok = factor<NW>(K, P, 0.0, 0.0, 0.0, 0.0, bnd, N, nwa, k, wv, lane, own);
-        const bool init_bad = __syncthreads_or(!ok);
-        {
-            double dr0, dr1, dx0, dx1;
-            solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
-            if (own) {
-                K.r0 = K.r0 + dr0;
-                K.r1 = K.r1 + dr1;
-                K.x0 = K.x0 + dx0;
-                K.x1 = K.x1 + dx1;
+        bool ok, init_bad = false;
+        // ---- initial point 2: full Newton step of the unconstrained QP (W = 0, lam = 0);
+        //      a warm start skips it ----
+        if (!warm) {
+            xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+            if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+            ok = factor<NW>(K, P, 0.0, 0.0, 0.0, 0.0, bnd, N, nwa, k, wv, lane, own);
+            init_bad = __syncthreads_or(!ok);
+            {
+                double dr0, dr1, dx0, dx1;
+                solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
+                if (own) {
+                    K.r0 = K.r0 + dr0;
+                    K.r1 = K.r1 + dr1;
+                    K.x0 = K.x0 + dx0;
+                    K.x1 = K.x1 + dx1;
+                }
             }
+            publish_xi<NW>(K, bnd, wv, lane);
         }
-        publish_xi<NW>(K, bnd, wv, lane);
-        // ---- initial point 3: s = max(b - A r, 1e-2), lam = 1 ----
+        // ---- initial point 3: s = max(b - A r, 1e-2), lam = 1;
+        //      warm knots: s = max(b - A r, floor), lam = max(lam_warm, floor) ----
         if (own) {
+            const double sfloor = ws ? P.ws_floor : 1e-2;
+            const double* lw = ws_lam + (ws ? (p * N + k + P.ws_shift) * M : 0);
 #pragma unroll
             for (int i = 0; i < kMaxFacets; ++i) {
                 if (i >= mmax) break;
@@ -718,8 +731,13 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     const double2 a = L.A2[i * N + k];
                     const double gr = FD2(a.x, K.r0, a.y, K.r1);
                     const double sl = L.BI[i * N + k].x - gr;
-                    K.s[i] = sl > 1e-2 ? sl : 1e-2;
-                    K.lam[i] = 1.0;
+                    K.s[i] = sl > sfloor ? sl : sfloor;
+                    if (ws) {
+                        const double l = lw[i];
+                        K.lam[i] = l > sfloor ? l : sfloor;
+                    } else {
+                        K.lam[i] = 1.0;
+                    }
                 }
             }
         }
@@ -950,6 +968,14 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         const int64_t sx = p * (N + 1) + (k + 1);
         xi_out[2 * sx] = K.x0;
         xi_out[2 * sx + 1] = K.x1;
+        if (lam_out) {
+            double* lo = lam_out + st * M;
+#pragma unroll
+            for (int i = 0; i < kMaxFacets; ++i) {
+                if (i >= M) break;
+                lo[i] = i < K.m ? K.lam[i] : 0.0;
+            }
+        }
     }
     if (k == 0) {
         xi_out[2 * p * (N + 1)] = xi00;
@@ -964,8 +990,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
 }
 
 template <int NT>
-blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb, int64_t batch,
-                     const blf_dcm_mpc_solution* sol, hipStream_t s)
+blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
+                     const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                     const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
 {
     const size_t lds = sizeof(double) * Lds(nullptr, kp.N, kp.M, NT / kWave).total;
     if (lds > 160 * 1024)
@@ -973,7 +1000,8 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb, int64_t b
                          kp.N, kp.M, lds);
     hipLaunchKernelGGL(dcm_mpc_ipm_kernel<NT>, dim3((unsigned)batch), dim3(NT), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
-                       pb->nfacets, sol->xi, sol->vrp, sol->status, sol->iters);
+                       pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr,
+                       sol->xi, sol->vrp, sol->status, sol->iters, lam_out);
     return check_hip(hipGetLastError(), "dcm_mpc_ipm_kernel launch");
 }
 
@@ -994,7 +1022,8 @@ extern "C" int blf_debug_stamps(unsigned long long* out, int reset)
 #endif
 
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
-                          int64_t batch, const blf_dcm_mpc_solution* sol, hipStream_t s)
+                          const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                          const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
 {
     KParams kp;
     kp.N = prm->horizon;
@@ -1007,14 +1036,16 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     kp.tol_mu = prm->tol_mu;
     kp.tol_p = prm->tol_primal;
     kp.tol_d = prm->tol_dual;
+    kp.ws_shift = warm ? warm->shift : 0;
+    kp.ws_floor = warm ? warm->floor : 0.0;
     if (batch == 0) return BLF_OK;
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     const int N = kp.N;
-    if (N <= 64) return launch_nt<64>(kp, pb, batch, sol, s);
-    if (N <= 128) return launch_nt<128>(kp, pb, batch, sol, s);
-    if (N <= 256) return launch_nt<256>(kp, pb, batch, sol, s);
-    if (N <= 512) return launch_nt<512>(kp, pb, batch, sol, s);
-    if (N <= 1024) return launch_nt<1024>(kp, pb, batch, sol, s);
+    if (N <= 64) return launch_nt<64>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 128) return launch_nt<128>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 256) return launch_nt<256>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 512) return launch_nt<512>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 1024) return launch_nt<1024>(kp, pb, warm, batch, sol, lam_out, s);
     return set_error(BLF_ERR_UNSUPPORTED, "horizon %d > 1024", N);
 }
 

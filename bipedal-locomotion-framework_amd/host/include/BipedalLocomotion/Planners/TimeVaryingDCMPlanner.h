@@ -4,15 +4,19 @@
  * snapshot), exposed through the reference's Advanceable surface
  * (src/System/include/BipedalLocomotion/System/Advanceable.h:24-46).
  *
- * Each advance():
- *   1. for every problem b and knot k = 0..N, t_k = (start + k) dt, finds the contact phase with
- *      begin <= t_k < end in that problem's ContactPhaseList and collects the corners
- *      pose * (+-L/2, +-W/2, 0) of its active contacts (the rectangle convention of
- *      ContinuousContactModel.h:32-36); r_ref_k = xi_ref_k = their centroid;
- *   2. builds every support polygon's H-rep on the device (blf_hull2d_hrep);
- *   3. solves all QPs on the device (blf_dcm_mpc_solve, include/blf/blf_c.h);
- *   4. publishes the plan (get()), then moves the window one knot forward, taking the planned
- *      xi_1 as the next initial DCM.
+ * setContactPhaseLists() stores the plans; the next advance() builds their phase table once: for
+ * every phase of every problem the corners pose * (+-L/2, +-W/2, 0) of its active contacts (the
+ * rectangle convention of ContinuousContactModel.h:32-36) and their centroid, uploaded, and the
+ * phases' support-polygon H-reps built on the device (blf_hull2d_hrep).  It stays resident.
+ *
+ * Each advance() then runs on the device only (stream-ordered, no host round trip):
+ *   1. blf_dcm_phase_expand: knot k of the window, t_k = (start + k) dt, takes the H-rep and
+ *      the centroid (r_ref_k = xi_ref_k) of the phase with begin <= t_k < end;
+ *   2. blf_dcm_mpc_solve_warm: all QPs, warm-started (after the first advance) from the previous
+ *      solution shifted by one knot;
+ *   3. the planned xi_1 becomes the next initial DCM (device-to-device copy), the window moves
+ *      one knot forward.
+ * get() / isValid() download the plan lazily, on the first call after an advance().
  * isValid() is true iff a plan exists and every problem's status is BLF_QP_SOLVED.
  */
 #ifndef BLF_BIPEDAL_LOCOMOTION_PLANNERS_TIME_VARYING_DCM_PLANNER_H
@@ -50,16 +54,38 @@ class TimeVaryingDCMPlanner : public System::Advanceable<DCMPlanBatch>
     double m_gravity{9.81};
     double m_footLength{0.12};
     double m_footWidth{0.09};
+    bool m_warmStart{true};
+    double m_warmFloor{1e-2};
     int m_start{0};
-    bool m_valid{false};
     std::vector<ContactPhaseList> m_plans;
     std::vector<double> m_xi0;       /**< [batch][2] */
     std::vector<double> m_height;    /**< [batch][horizon] CoM height per knot (empty: 0.53) */
-    DCMPlanBatch m_output;
 
-    blf::DeviceBuffer<double> m_dCorners, m_dXi0, m_dOmega, m_dXiRef, m_dVrpRef, m_dA, m_dB;
-    blf::DeviceBuffer<double> m_dXi, m_dVrp;
-    blf::DeviceBuffer<int32_t> m_dNCorners, m_dNf, m_dStatus, m_dIters;
+    // host view of the phase table: the span each problem's window must stay in
+    int m_maxPhases{0};
+    std::vector<double> m_planBegin, m_planEnd;   /**< [batch] first begin, last end */
+    std::vector<double> m_badBegin, m_badEnd;     /**< [batch] first phase without support */
+
+    bool m_tableDirty{true}, m_omegaDirty{true}, m_xi0Dirty{true};
+    bool m_haveWarm{false};
+    int m_cur{0};   /**< which of the ping-pong solution buffers holds the latest solve */
+    bool m_solved{false};
+
+    // lazily downloaded plan
+    mutable bool m_outputDirty{false};
+    mutable bool m_valid{false};
+    mutable DCMPlanBatch m_output;
+
+    // device-resident state
+    blf::DeviceBuffer<double> m_dPhBegin, m_dPhEnd, m_dPhCorners, m_dPhRef, m_dPhA, m_dPhB;
+    blf::DeviceBuffer<int32_t> m_dNPhases, m_dPhNCorners, m_dPhNf;
+    blf::DeviceBuffer<double> m_dXi0, m_dOmega, m_dXiRef, m_dVrpRef, m_dA, m_dB;
+    blf::DeviceBuffer<double> m_dXi, m_dVrp[2], m_dLam[2];
+    blf::DeviceBuffer<int32_t> m_dNf, m_dStatus, m_dIters;
+
+    bool buildPhaseTable(blf_handle* h);
+    bool checkWindow() const;
+    void download() const;
 
 public:
     TimeVaryingDCMPlanner();
@@ -67,23 +93,27 @@ public:
     /**
      * Keys (all optional): "horizon" (int), "sampling_time", "gravity", "foot_length",
      * "foot_width", "dcm_weight", "vrp_weight", "terminal_weight" (scalar or 2-vector),
-     * "tolerance" (tol_mu), "max_iterations" (int).
+     * "tolerance" (tol_mu), "max_iterations" (int), "warm_start" (bool, default true),
+     * "warm_start_floor" (default 1e-2).
      */
     bool initialize(std::weak_ptr<ParametersHandler::IParametersHandler> handler);
 
     /** One footstep plan per problem (the batch size). */
     bool setContactPhaseLists(const std::vector<ContactPhaseList>& plans);
-    /** Initial DCM per problem ([batch][2]). */
+    /** Initial DCM per problem ([batch][2]); otherwise each advance() starts at the previous
+     * plan's xi_1. */
     bool setInitialDCM(const std::vector<std::array<double, 2>>& xi0);
     /** CoM height per problem and knot ([batch][horizon]); omega_k = sqrt(g / z_k). */
     bool setCoMHeights(const std::vector<double>& heights);
 
-    const DCMPlanBatch& get() const final { return m_output; }
-    bool isValid() const final { return m_valid; }
+    const DCMPlanBatch& get() const final;
+    bool isValid() const final;
     bool advance() final;
 
     const blf_dcm_mpc_params& parameters() const { return m_params; }
     int currentKnot() const { return m_start; }
+    /** Device pointers of the latest plan (valid until the next advance() or destruction). */
+    blf_dcm_mpc_solution deviceSolution();
 };
 
 } // namespace Planners

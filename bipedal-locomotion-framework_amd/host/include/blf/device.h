@@ -83,6 +83,11 @@ public:
 /** Waits for all work queued by this thread on the default stream. */
 bool synchronize();
 
+/** Stream-ordered device-to-device copy of `rows` rows of `width` bytes between pitched
+ * layouts (hipMemcpy2DAsync on the default stream). */
+bool copyRows(void* dst, std::size_t dpitch, const void* src, std::size_t spitch,
+              std::size_t width, std::size_t rows);
+
 } // namespace blf
 
 #endif // BLF_HOST_DEVICE_H

@@ -1,10 +1,13 @@
 /**
  * @file TimeVaryingDCMPlanner.cpp
- * Host bookkeeping (knot -> phase -> active-contact corners) around the device pipeline
- * blf_hull2d_hrep -> blf_dcm_mpc_solve.
+ * Host bookkeeping (phases -> active-contact corners, once per plan) around the device pipeline
+ * blf_hull2d_hrep (once per plan) -> blf_dcm_phase_expand -> blf_dcm_mpc_solve_warm (per
+ * advance()).
  */
 #include <cmath>
 #include <iostream>
+#include <limits>
+#include <map>
 
 #include <BipedalLocomotion/Planners/TimeVaryingDCMPlanner.h>
 
@@ -42,6 +45,14 @@ bool TimeVaryingDCMPlanner::initialize(std::weak_ptr<ParametersHandler::IParamet
     ptr->getParameter("foot_length", m_footLength);
     ptr->getParameter("foot_width", m_footWidth);
     ptr->getParameter("tolerance", m_params.tol_mu);
+    ptr->getParameter("warm_start", m_warmStart);
+    ptr->getParameter("warm_start_floor", m_warmFloor);
+    if (!(m_warmFloor > 0) || !std::isfinite(m_warmFloor))
+    {
+        std::cerr << "[TimeVaryingDCMPlanner::initialize] warm_start_floor must be positive."
+                  << std::endl;
+        return false;
+    }
     int maxIter = m_params.max_iter;
     if (ptr->getParameter("max_iterations", maxIter)) m_params.max_iter = maxIter;
     auto weight = [&](const char* key, double* w) {
@@ -68,7 +79,9 @@ bool TimeVaryingDCMPlanner::initialize(std::weak_ptr<ParametersHandler::IParamet
         return false;
     }
     m_start = 0;
-    m_valid = false;
+    m_solved = false;
+    m_haveWarm = false;
+    m_tableDirty = m_omegaDirty = m_xi0Dirty = true;
     return true;
 }
 
@@ -79,9 +92,12 @@ bool TimeVaryingDCMPlanner::setContactPhaseLists(const std::vector<ContactPhaseL
         std::cerr << "[TimeVaryingDCMPlanner::setContactPhaseLists] Empty batch." << std::endl;
         return false;
     }
+    if (!m_plans.empty() && plans.size() != m_plans.size()) m_xi0Dirty = m_omegaDirty = true;
     m_plans = plans;
     m_start = 0;
-    m_valid = false;
+    m_solved = false;
+    m_haveWarm = false;   // the multipliers belong to the old plan's facets
+    m_tableDirty = true;
     return true;
 }
 
@@ -93,6 +109,7 @@ bool TimeVaryingDCMPlanner::setInitialDCM(const std::vector<std::array<double, 2
         m_xi0[2 * i] = xi0[i][0];
         m_xi0[2 * i + 1] = xi0[i][1];
     }
+    m_xi0Dirty = true;
     return true;
 }
 
@@ -106,14 +123,109 @@ bool TimeVaryingDCMPlanner::setCoMHeights(const std::vector<double>& heights)
             return false;
         }
     m_height = heights;
+    m_omegaDirty = true;
+    return true;
+}
+
+bool TimeVaryingDCMPlanner::buildPhaseTable(blf_handle* h)
+{
+    const int B = static_cast<int>(m_plans.size());
+    int P = 1;
+    for (const auto& plan : m_plans) P = std::max(P, static_cast<int>(plan.size()));
+    const std::size_t BP = static_cast<std::size_t>(B) * P;
+    std::vector<int32_t> nphases(B), ncorners(BP, 0);
+    std::vector<double> begin(BP, 0.0), end(BP, 0.0), corners(BP * kCorners * 2, 0.0),
+        ref(BP * 2, 0.0);
+    const double inf = std::numeric_limits<double>::infinity();
+    m_planBegin.assign(B, inf);
+    m_planEnd.assign(B, -inf);
+    m_badBegin.assign(B, inf);
+    m_badEnd.assign(B, -inf);
+    for (int b = 0; b < B; ++b)
+    {
+        const ContactPhaseList& plan = m_plans[b];
+        nphases[b] = static_cast<int32_t>(plan.size());
+        for (std::size_t p = 0; p < plan.size(); ++p)
+        {
+            const std::size_t row = static_cast<std::size_t>(b) * P + p;
+            begin[row] = plan[p].beginTime;
+            end[row] = plan[p].endTime;
+            // deterministic corner order: active contacts sorted by list name
+            std::map<std::string, ContactList::const_iterator> active(
+                plan[p].activeContacts.begin(), plan[p].activeContacts.end());
+            int c = 0;
+            double sx = 0.0, sy = 0.0;
+            for (const auto& entry : active)
+                for (double ex : {0.5, -0.5})
+                    for (double ey : {0.5, -0.5})
+                    {
+                        if (c >= kCorners) break;
+                        const auto q = entry.second->pose.apply(
+                            {{ex * m_footLength, ey * m_footWidth, 0.0}});
+                        corners[(row * kCorners + c) * 2] = q[0];
+                        corners[(row * kCorners + c) * 2 + 1] = q[1];
+                        sx += q[0];
+                        sy += q[1];
+                        ++c;
+                    }
+            ncorners[row] = c;
+            if (c > 0)
+            {
+                ref[2 * row] = sx / c;
+                ref[2 * row + 1] = sy / c;
+            }
+            else if (m_badBegin[b] == inf)
+            {   // no support polygon: a window touching this phase cannot be planned
+                m_badBegin[b] = plan[p].beginTime;
+                m_badEnd[b] = plan[p].endTime;
+            }
+            if (p == 0) m_planBegin[b] = plan[p].beginTime;
+            m_planEnd[b] = plan[p].endTime;
+        }
+    }
+    const int M = m_params.max_facets;
+    m_maxPhases = P;
+    if (!m_dNPhases.upload(nphases) || !m_dPhBegin.upload(begin) || !m_dPhEnd.upload(end) ||
+        !m_dPhCorners.upload(corners) || !m_dPhNCorners.upload(ncorners) ||
+        !m_dPhRef.upload(ref) || !m_dPhA.resize(BP * M * 2) || !m_dPhB.resize(BP * M) ||
+        !m_dPhNf.resize(BP))
+        return false;
+    return blf::report(blf_hull2d_hrep(h, m_dPhCorners.data(), m_dPhNCorners.data(), kCorners, M,
+                                       static_cast<int64_t>(BP), m_dPhA.data(), m_dPhB.data(),
+                                       m_dPhNf.data(), nullptr),
+                       "TimeVaryingDCMPlanner::advance");
+}
+
+bool TimeVaryingDCMPlanner::checkWindow() const
+{
+    // the plans' phases are contiguous (ContactPhaseList::createPhases), so every knot of the
+    // window lies in some phase iff the window lies in [first begin, last end)
+    const int N = m_params.horizon;
+    const double t0 = static_cast<double>(m_start) * m_params.dt;
+    const double t1 = static_cast<double>(m_start + N) * m_params.dt;
+    for (std::size_t b = 0; b < m_plans.size(); ++b)
+    {
+        if (!(m_planBegin[b] <= t0 && t1 < m_planEnd[b]))
+        {
+            std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b << ": the window ["
+                      << t0 << ", " << t1 << "] leaves the contact phases." << std::endl;
+            return false;
+        }
+        if (m_badBegin[b] <= t1 && t0 < m_badEnd[b])
+        {
+            std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b
+                      << ": no active contact in a phase of the window." << std::endl;
+            return false;
+        }
+    }
     return true;
 }
 
 bool TimeVaryingDCMPlanner::advance()
 {
-    m_valid = false;
     const int B = static_cast<int>(m_plans.size());
     const int N = m_params.horizon;
+    const int M = m_params.max_facets;
     if (B == 0 || static_cast<int>(m_xi0.size()) != 2 * B)
     {
         std::cerr << "[TimeVaryingDCMPlanner::advance] Set the contact phase lists and one "
@@ -130,116 +242,106 @@ bool TimeVaryingDCMPlanner::advance()
     blf_handle* h = blf::threadHandle();
     if (h == nullptr) return false;
 
-    // 1. knot -> phase -> corners of the active contacts (host bookkeeping)
-    std::vector<double> corners(static_cast<std::size_t>(B) * (N + 1) * kCorners * 2, 0.0);
-    std::vector<int32_t> ncorners(static_cast<std::size_t>(B) * (N + 1), 0);
-    std::vector<double> xiRef(static_cast<std::size_t>(B) * (N + 1) * 2);
-    std::vector<double> omega(static_cast<std::size_t>(B) * N);
-    for (int b = 0; b < B; ++b)
+    // 1. once per plan: phase table and its support polygons on the device
+    if (m_tableDirty)
     {
-        for (int k = 0; k <= N; ++k)
-        {
-            const double t = static_cast<double>(m_start + k) * m_params.dt;
-            const int phase = m_plans[b].phaseIndexAt(t);
-            if (phase < 0)
-            {
-                std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b << ": knot time " << t
-                          << " is outside every contact phase." << std::endl;
-                return false;
-            }
-            // deterministic corner order: active contacts sorted by list name
-            std::map<std::string, ContactList::const_iterator> active(
-                m_plans[b][phase].activeContacts.begin(), m_plans[b][phase].activeContacts.end());
-            const std::size_t base = (static_cast<std::size_t>(b) * (N + 1) + k);
-            int c = 0;
-            double sx = 0.0, sy = 0.0;
-            for (const auto& entry : active)
-            {
-                for (double ex : {0.5, -0.5})
-                    for (double ey : {0.5, -0.5})
-                    {
-                        if (c >= kCorners) break;
-                        const auto p = entry.second->pose.apply({{ex * m_footLength, ey * m_footWidth, 0.0}});
-                        corners[(base * kCorners + c) * 2] = p[0];
-                        corners[(base * kCorners + c) * 2 + 1] = p[1];
-                        sx += p[0];
-                        sy += p[1];
-                        ++c;
-                    }
-            }
-            if (c < 3)
-            {
-                std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b
-                          << ": no active contact at knot time " << t << "." << std::endl;
-                return false;
-            }
-            ncorners[base] = c;
-            xiRef[2 * base] = sx / c;
-            xiRef[2 * base + 1] = sy / c;
-            if (k < N)
-            {
-                const double z = m_height.empty() ? 0.53 : m_height[static_cast<std::size_t>(b) * N + k];
-                omega[static_cast<std::size_t>(b) * N + k] = std::sqrt(m_gravity / z);
-            }
-        }
+        if (!buildPhaseTable(h)) return false;
+        m_tableDirty = false;
     }
-    std::vector<double> vrpRef(static_cast<std::size_t>(B) * N * 2);
-    for (int b = 0; b < B; ++b)
-        for (int k = 0; k < N; ++k)
-            for (int j = 0; j < 2; ++j)
-                vrpRef[(static_cast<std::size_t>(b) * N + k) * 2 + j] =
-                    xiRef[(static_cast<std::size_t>(b) * (N + 1) + k) * 2 + j];
+    if (!checkWindow()) return false;
+    const std::size_t BN = static_cast<std::size_t>(B) * N;
+    if (m_omegaDirty)
+    {
+        std::vector<double> omega(BN);
+        for (std::size_t i = 0; i < BN; ++i)
+            omega[i] = std::sqrt(m_gravity / (m_height.empty() ? 0.53 : m_height[i]));
+        if (!m_dOmega.upload(omega)) return false;
+        m_omegaDirty = false;
+    }
+    if (m_xi0Dirty)
+    {
+        if (!m_dXi0.upload(m_xi0)) return false;
+        m_xi0Dirty = false;
+    }
 
-    // 2. support polygons on the device: knots 0..N-1 of every problem
-    const int M = m_params.max_facets;
-    const std::size_t polys = static_cast<std::size_t>(B) * N;
-    std::vector<double> cornersQP(polys * kCorners * 2);
-    std::vector<int32_t> ncornersQP(polys);
-    for (int b = 0; b < B; ++b)
-        for (int k = 0; k < N; ++k)
-        {
-            const std::size_t src = static_cast<std::size_t>(b) * (N + 1) + k;
-            const std::size_t dst = static_cast<std::size_t>(b) * N + k;
-            for (int c = 0; c < kCorners * 2; ++c) cornersQP[dst * kCorners * 2 + c] = corners[src * kCorners * 2 + c];
-            ncornersQP[dst] = ncorners[src];
-        }
-    if (!m_dCorners.upload(cornersQP) || !m_dNCorners.upload(ncornersQP) ||
-        !m_dA.resize(polys * M * 2) || !m_dB.resize(polys * M) || !m_dNf.resize(polys))
+    // 2. the window's per-knot arrays from the phase table
+    if (!m_dA.resize(BN * M * 2) || !m_dB.resize(BN * M) || !m_dNf.resize(BN) ||
+        !m_dXiRef.resize(static_cast<std::size_t>(B) * (N + 1) * 2) || !m_dVrpRef.resize(BN * 2))
         return false;
-    if (!blf::report(blf_hull2d_hrep(h, m_dCorners.data(), m_dNCorners.data(), kCorners, M,
-                                     static_cast<int64_t>(polys), m_dA.data(), m_dB.data(),
-                                     m_dNf.data(), nullptr),
+    blf_phase_table table{m_maxPhases,     M,             m_dNPhases.data(), m_dPhBegin.data(),
+                          m_dPhEnd.data(), m_dPhA.data(), m_dPhB.data(),     m_dPhNf.data(),
+                          m_dPhRef.data()};
+    if (!blf::report(blf_dcm_phase_expand(h, &table, m_start, m_params.dt, N, B, m_dA.data(),
+                                          m_dB.data(), m_dNf.data(), m_dXiRef.data(),
+                                          m_dVrpRef.data(), nullptr),
                      "TimeVaryingDCMPlanner::advance"))
         return false;
 
-    // 3. the QPs
-    if (!m_dXi0.upload(m_xi0) || !m_dOmega.upload(omega) || !m_dXiRef.upload(xiRef) ||
-        !m_dVrpRef.upload(vrpRef) || !m_dXi.resize(static_cast<std::size_t>(B) * (N + 1) * 2) ||
-        !m_dVrp.resize(static_cast<std::size_t>(B) * N * 2) || !m_dStatus.resize(B) ||
+    // 3. the QPs, warm-started from the previous solution shifted by one knot
+    const int nxt = m_solved ? 1 - m_cur : m_cur;
+    if (!m_dXi.resize(static_cast<std::size_t>(B) * (N + 1) * 2) ||
+        !m_dVrp[nxt].resize(BN * 2) || !m_dLam[nxt].resize(BN * M) || !m_dStatus.resize(B) ||
         !m_dIters.resize(B))
         return false;
     blf_dcm_mpc_problem prob{m_dXi0.data(), m_dOmega.data(), m_dXiRef.data(), m_dVrpRef.data(),
                              m_dA.data(),   m_dB.data(),     m_dNf.data()};
-    blf_dcm_mpc_solution sol{m_dXi.data(), m_dVrp.data(), m_dStatus.data(), m_dIters.data()};
-    if (!blf::report(blf_dcm_mpc_solve(h, &m_params, &prob, B, &sol, nullptr),
+    blf_dcm_mpc_solution sol{m_dXi.data(), m_dVrp[nxt].data(), m_dStatus.data(), m_dIters.data()};
+    blf_dcm_mpc_warm_start warm{m_dVrp[m_cur].data(), m_dLam[m_cur].data(), 1, 0, m_warmFloor};
+    const bool useWarm = m_warmStart && m_haveWarm && m_solved;
+    if (!blf::report(blf_dcm_mpc_solve_warm(h, &m_params, &prob, useWarm ? &warm : nullptr, B,
+                                            &sol, m_dLam[nxt].data(), nullptr),
                      "TimeVaryingDCMPlanner::advance"))
         return false;
 
-    // 4. publish, then shift the window
-    m_output.batch = B;
-    m_output.horizon = N;
-    m_output.initialTime = static_cast<double>(m_start) * m_params.dt;
-    if (!m_dXi.download(m_output.dcm) || !m_dVrp.download(m_output.vrp) ||
-        !m_dStatus.download(m_output.status) || !m_dIters.download(m_output.iterations))
+    // 4. the planned xi_1 is the next window's initial DCM; move the window
+    if (!blf::copyRows(m_dXi0.data(), 2 * sizeof(double), m_dXi.data() + 2,
+                       static_cast<std::size_t>(N + 1) * 2 * sizeof(double), 2 * sizeof(double),
+                       static_cast<std::size_t>(B)))
         return false;
-    bool ok = true;
-    for (int b = 0; b < B; ++b)
-    {
-        ok = ok && m_output.status[b] == BLF_QP_SOLVED;
-        m_xi0[2 * b] = m_output.dcm[(static_cast<std::size_t>(b) * (N + 1) + 1) * 2];
-        m_xi0[2 * b + 1] = m_output.dcm[(static_cast<std::size_t>(b) * (N + 1) + 1) * 2 + 1];
-    }
-    m_valid = ok;
+    m_cur = nxt;
+    m_solved = true;
+    m_haveWarm = true;
+    m_outputDirty = true;
+    m_output.initialTime = static_cast<double>(m_start) * m_params.dt;
     ++m_start;
     return true;
+}
+
+void TimeVaryingDCMPlanner::download() const
+{
+    if (!m_outputDirty) return;
+    m_outputDirty = false;
+    const int B = static_cast<int>(m_plans.size());
+    m_output.batch = B;
+    m_output.horizon = m_params.horizon;
+    bool ok = m_dXi.download(m_output.dcm) && m_dVrp[m_cur].download(m_output.vrp) &&
+              m_dStatus.download(m_output.status) && m_dIters.download(m_output.iterations);
+    if (ok)
+    {
+        for (int b = 0; b < B; ++b) ok = ok && m_output.status[b] == BLF_QP_SOLVED;
+    }
+    else
+    {
+        std::cerr << "[TimeVaryingDCMPlanner::get] Could not download the plan." << std::endl;
+    }
+    m_valid = ok;
+}
+
+const DCMPlanBatch& TimeVaryingDCMPlanner::get() const
+{
+    download();
+    return m_output;
+}
+
+bool TimeVaryingDCMPlanner::isValid() const
+{
+    if (!m_solved) return false;
+    download();
+    return m_valid;
+}
+
+blf_dcm_mpc_solution TimeVaryingDCMPlanner::deviceSolution()
+{
+    return blf_dcm_mpc_solution{m_dXi.data(), m_dVrp[m_cur].data(), m_dStatus.data(),
+                                m_dIters.data()};
 }

@@ -49,6 +49,19 @@ bool synchronize()
     return hipDeviceSynchronize() == hipSuccess;
 }
 
+bool copyRows(void* dst, std::size_t dpitch, const void* src, std::size_t spitch,
+              std::size_t width, std::size_t rows)
+{
+    if (rows == 0) return true;
+    if (hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToDevice,
+                         nullptr) != hipSuccess)
+    {
+        std::cerr << "[blf::copyRows] hipMemcpy2DAsync failed" << std::endl;
+        return false;
+    }
+    return true;
+}
+
 template <typename T> void* DeviceBuffer<T>::alloc(std::size_t bytes)
 {
     void* p = nullptr;

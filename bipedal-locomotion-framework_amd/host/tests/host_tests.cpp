@@ -352,6 +352,52 @@ static void testPlanner()
         }
         REQUIRE(dyn);
     }
+
+    // warm-started receding horizon vs cold re-solves: the same plans (up to the IPM's accuracy)
+    // in fewer iterations; the first advance is a cold solve either way
+    auto cold = std::make_shared<ParametersHandler::StdImplementation>();
+    cold->setParameter("horizon", 100);
+    cold->setParameter("warm_start", false);
+    TimeVaryingDCMPlanner warmPlanner, coldPlanner;
+    REQUIRE(warmPlanner.initialize(handler));
+    REQUIRE(coldPlanner.initialize(cold));
+    REQUIRE(warmPlanner.setContactPhaseLists(plans) && coldPlanner.setContactPhaseLists(plans));
+    REQUIRE(warmPlanner.setInitialDCM(xi0) && coldPlanner.setInitialDCM(xi0));
+    double itWarm = 0, itCold = 0, maxDiff = 0;
+    for (int step = 0; step < 40; ++step)
+    {
+        REQUIRE(warmPlanner.advance() && coldPlanner.advance());
+        REQUIRE(warmPlanner.isValid() && coldPlanner.isValid());
+        const DCMPlanBatch& a = warmPlanner.get();
+        const DCMPlanBatch& c = coldPlanner.get();
+        for (int b = 0; b < 16; ++b)
+        {
+            if (step == 0) REQUIRE(a.iterations[b] == c.iterations[b]);
+            else
+            {
+                itWarm += a.iterations[b];
+                itCold += c.iterations[b];
+            }
+        }
+        for (std::size_t i = 0; i < a.vrp.size(); ++i)
+            maxDiff = std::max(maxDiff, std::fabs(a.vrp[i] - c.vrp[i]));
+        // re-anchor both on the same initial DCM so the windows pose the same QPs
+        std::vector<std::array<double, 2>> x1;
+        for (int b = 0; b < 16; ++b)
+            x1.push_back({{c.dcm[(static_cast<std::size_t>(b) * 101 + 1) * 2],
+                           c.dcm[(static_cast<std::size_t>(b) * 101 + 1) * 2 + 1]}});
+        REQUIRE(warmPlanner.setInitialDCM(x1) && coldPlanner.setInitialDCM(x1));
+    }
+    REQUIRE(itWarm < 0.8 * itCold);
+    REQUIRE(maxDiff < 1e-6);
+    // a window that runs past the plan's last phase is refused
+    TimeVaryingDCMPlanner shortPlanner;
+    auto longH = std::make_shared<ParametersHandler::StdImplementation>();
+    longH->setParameter("horizon", 500);
+    REQUIRE(shortPlanner.initialize(longH));
+    REQUIRE(shortPlanner.setContactPhaseLists(plans) && shortPlanner.setInitialDCM(xi0));
+    REQUIRE_FALSE(shortPlanner.advance());
+    REQUIRE_FALSE(shortPlanner.isValid());
 }
 
 

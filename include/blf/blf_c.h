@@ -33,7 +33,9 @@
  *                             (FloatingBaseDynamicalSystem::dynamics; the rigid-body terms that the
  *                             reference takes from iDynTree KinDynComputations are computed here)
  *   blf_fbd_euler_integrate   ForwardEuler<FloatingBaseDynamicalSystem>::integrate
- *   blf_dcm_mpc_solve         ABSENT in the reference (TimeVaryingDCMPlanner QP),
+ *   blf_dcm_phase_expand      Planners/src/ContactPhaseList.cpp:16-84 phases looked up per knot with the
+ *                             getPresentContact rule (ContactList.cpp:190-202), SURVEY.md 8(f) item 2
+ *   blf_dcm_mpc_solve[_warm]  ABSENT in the reference (TimeVaryingDCMPlanner QP),
  *                             driven through System/Advanceable.h:24-46 (advance()) by the C++ host
  *                             adapter blf::Planners::TimeVaryingDCMPlanner
  */
@@ -173,6 +175,20 @@ typedef struct blf_dcm_mpc_solution {
     int32_t* iters;          /* [B]  IPM iterations taken                                   */
 } blf_dcm_mpc_solution;
 
+/* Warm start of a receding-horizon re-solve (TimeVaryingDCMPlanner::advance()):
+ * knot k of the new window starts from knot k + shift of a previous solution of the same plan
+ * (shift = 1 after the window moved one knot):
+ *   r_k = vrp[k + shift],  s_i = max(b_i - a_i r_k, floor),  lambda_i = max(lambda[k + shift][i], floor)
+ * and the cold start's LQ step is skipped.  Knots with k + shift >= N are new to the window and
+ * start cold (r_k = vrp_ref_k, s_i = max(b_i - a_i r_k, 1e-2), lambda_i = 1).                 */
+typedef struct blf_dcm_mpc_warm_start {
+    const double* vrp;       /* [B][N][2]  VRPs of the previous solve (must not alias the output) */
+    const double* lambda;    /* [B][N][M]  its multipliers (blf_dcm_mpc_solve_warm's lambda_out)  */
+    int32_t shift;           /* >= 0                                                          */
+    int32_t reserved;        /* must be 0                                                     */
+    double floor;            /* > 0, e.g. 1e-2                                                */
+} blf_dcm_mpc_warm_start;
+
 /* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-16,
  * tol_primal 1e-10, tol_dual 1e-9, max_iter 50, max_facets 8). */
 void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);
@@ -180,6 +196,44 @@ void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
                              const blf_dcm_mpc_problem* problem, int64_t batch,
                              const blf_dcm_mpc_solution* solution, void* stream);
+
+/* blf_dcm_mpc_solve from the warm start `warm` (NULL: the cold start, identical to
+ * blf_dcm_mpc_solve).  lambda_out [B][N][M] (or NULL) receives the final multipliers, zero in
+ * facet slots >= nfacets[k]; it is the next advance()'s warm->lambda.                         */
+blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                  const blf_dcm_mpc_problem* problem,
+                                  const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                                  const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                  void* stream);
+
+/* ---- 5b. Knot -> contact-phase expansion (receding-horizon windows on the device) -----------
+ * The phases of each problem's plan (ContactPhaseList::createPhases, Planners/src/
+ * ContactPhaseList.cpp:16-84), sorted by begin time, with the H-rep of each phase's support
+ * polygon (blf_hull2d_hrep over the phase's active-contact corners) and its reference point:
+ *   begin, end: [B][P];  A: [B][P][M][2];  b: [B][P][M];  nfacets: [B][P];  ref: [B][P][2];
+ *   nphases: [B] (phases >= nphases[q] are ignored).
+ * For the window of knots t_k = (start_knot + k) dt, k = 0..N, knot k belongs to phase
+ *   p = the last phase with begin_p <= t_k (the getPresentContact rule, ContactList.cpp:190-202)
+ * when t_k < end_p, else to no phase.  Outputs (the blf_dcm_mpc_problem arrays of the window):
+ *   A [B][N][M][2], b [B][N][M] = phase p's rows verbatim; nfacets [B][N] = phase p's count;
+ *   xi_ref [B][N+1][2] and vrp_ref [B][N][2] = phase p's reference point; a knot outside every
+ *   phase gets nfacets = -1 (the QP reports BLF_QP_BAD_FACETS) and zero rows / references.   */
+typedef struct blf_phase_table {
+    int32_t max_phases;        /* P >= 1                                                     */
+    int32_t max_facets;        /* M, 1..8                                                    */
+    const int32_t* nphases;    /* [B]                                                        */
+    const double* begin;       /* [B][P]                                                     */
+    const double* end;         /* [B][P]                                                     */
+    const double* A;           /* [B][P][M][2]                                               */
+    const double* b;           /* [B][P][M]                                                  */
+    const int32_t* nfacets;    /* [B][P]                                                     */
+    const double* ref;         /* [B][P][2]                                                  */
+} blf_phase_table;
+
+blf_status blf_dcm_phase_expand(blf_handle* handle, const blf_phase_table* phases,
+                                int64_t start_knot, double dt, int32_t horizon, int64_t batch,
+                                double* A, double* b, int32_t* nfacets, double* xi_ref,
+                                double* vrp_ref, void* stream);
 
 /* ---- 6. Contact model (ContinuousContactModel), batched ------------------------------------
  * Rectangular L x W patch, spring k, damper b (ContinuousContactModel.h:22-57).

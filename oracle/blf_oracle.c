@@ -279,6 +279,45 @@ void orc_quintic_eval(const double* knots_t, const double* coeffs, int nknots, i
     }
 }
 
+/* Knot -> contact-phase expansion of one problem (blf_dcm_phase_expand): knot k at
+ * t = (start + k) dt belongs to p = the last phase with begin_p <= t (binary search, the
+ * getPresentContact rule of Planners/src/ContactList.cpp:190-202) if t < end_p. */
+static int phase_of(const double* begin, const double* end, int n, double t)
+{
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (begin[mid] <= t) lo = mid + 1;
+        else hi = mid;
+    }
+    const int p = lo - 1;
+    return (p >= 0 && t < end[p]) ? p : -1;
+}
+
+void orc_dcm_phase_expand(int P, int M, int nphases, const double* begin, const double* end,
+                          const double* pA, const double* pb, const int32_t* pnf,
+                          const double* pref, int64_t start, double dt, int N, double* A,
+                          double* b, int32_t* nfacets, double* xi_ref, double* vrp_ref)
+{
+    const int np = nphases < 0 ? 0 : (nphases > P ? P : nphases);
+    for (int k = 0; k <= N; ++k) {
+        const double t = (double)(start + k) * dt;
+        const int p = phase_of(begin, end, np, t);
+        const double r0 = p >= 0 ? pref[2 * p] : 0.0, r1 = p >= 0 ? pref[2 * p + 1] : 0.0;
+        xi_ref[2 * k] = r0;
+        xi_ref[2 * k + 1] = r1;
+        if (k == N) break;
+        vrp_ref[2 * k] = r0;
+        vrp_ref[2 * k + 1] = r1;
+        nfacets[k] = p >= 0 ? pnf[p] : -1;
+        for (int i = 0; i < M; ++i) {
+            A[(k * M + i) * 2] = p >= 0 ? pA[(p * M + i) * 2] : 0.0;
+            A[(k * M + i) * 2 + 1] = p >= 0 ? pA[(p * M + i) * 2 + 1] : 0.0;
+            b[k * M + i] = p >= 0 ? pb[p * M + i] : 0.0;
+        }
+    }
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* DCM-MPC QP: Mehrotra primal-dual IPM + Riccati                        */
 /* ------------------------------------------------------------------------------------------ */
@@ -808,6 +847,15 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                       const double* bin, const int32_t* nfacets, double* xi, double* vrp,
                       int32_t* iters_out)
 {
+    return orc_dcm_mpc_solve_warm(prm, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, NULL,
+                                  xi, vrp, NULL, iters_out);
+}
+
+int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, const double* omega,
+                           const double* xi_ref, const double* vrp_ref, const double* Ain,
+                           const double* bin, const int32_t* nfacets, const orc_dcm_warm* warm,
+                           double* xi, double* vrp, double* lam_out, int32_t* iters_out)
+{
     const int N = prm->horizon;
     const int M = prm->max_facets;
     dcm_ws ws;
@@ -846,8 +894,12 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         w->a2[k] = w->al[k] * w->al[k];
         w->b2[k] = w->be[k] * w->be[k];
         w->ab[k] = w->al[k] * w->be[k];
-        vrp[2 * k] = vrp_ref[2 * k];
-        vrp[2 * k + 1] = vrp_ref[2 * k + 1];
+        /* start VRP: the warm start's knot k + shift, or (cold start, or a knot new to the
+         * window) the reference VRP */
+        const int ws = warm && k + warm->shift < N;
+        const double* r0 = ws ? warm->vrp + 2 * warm->shift : vrp_ref;
+        vrp[2 * k] = r0[2 * k];
+        vrp[2 * k + 1] = r0[2 * k + 1];
         for (int i = 0; i < MF; ++i) { w->s[k * MF + i] = 1.0; w->lam[k * MF + i] = 0.0; }
     }
     /* ---- initial point 1: xi rolled out from vrp_ref by the affine forward scan
@@ -867,38 +919,45 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
     xi[0] = xi_init[0];
     xi[1] = xi_init[1];
     for (int k = 1; k <= N; ++k) { xi[2 * k] = w->x[2 * k]; xi[2 * k + 1] = w->x[2 * k + 1]; }
-    if (status == 3) {
-        if (iters_out) *iters_out = 0;
-        free(mem);
-        return 3;
-    }
+    if (status == 3) goto done;
     /* ---- initial point 2: one full Newton step of the QP without the polygon constraints
      *      (W = 0, lam = 0): the unconstrained LQ optimum.  For the unstable DCM the rollout is far
      *      from dual feasible (costates grow like alpha^N); this step makes the linear residuals
      *      vanish up to rounding. ---- */
-    dcm_residuals(w, 0);
-    for (int k = 0; k < N; ++k) {
-        w->W[4 * k] = 0.0; w->W[4 * k + 1] = 0.0; w->W[4 * k + 2] = 0.0; w->W[4 * k + 3] = 0.0;
-        w->g[2 * k] = w->rh[2 * k];
-        w->g[2 * k + 1] = w->rh[2 * k + 1];
+    /*      A warm start skips it: its VRP is a previous optimum, already close. */
+    if (!warm) {
+        dcm_residuals(w, 0);
+        for (int k = 0; k < N; ++k) {
+            w->W[4 * k] = 0.0; w->W[4 * k + 1] = 0.0; w->W[4 * k + 2] = 0.0; w->W[4 * k + 3] = 0.0;
+            w->g[2 * k] = w->rh[2 * k];
+            w->g[2 * k + 1] = w->rh[2 * k + 1];
+        }
+        if (!dcm_factor(w)) status = 2;
+        dcm_solve(w);
+        for (int k = 0; k < N; ++k) {
+            vrp[2 * k] = vrp[2 * k] + w->dr[2 * k];
+            vrp[2 * k + 1] = vrp[2 * k + 1] + w->dr[2 * k + 1];
+            xi[2 * (k + 1)] = xi[2 * (k + 1)] + w->x[2 * (k + 1)];
+            xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
+        }
     }
-    if (!dcm_factor(w)) status = 2;
-    dcm_solve(w);
-    for (int k = 0; k < N; ++k) {
-        vrp[2 * k] = vrp[2 * k] + w->dr[2 * k];
-        vrp[2 * k + 1] = vrp[2 * k + 1] + w->dr[2 * k + 1];
-        xi[2 * (k + 1)] = xi[2 * (k + 1)] + w->x[2 * (k + 1)];
-        xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
-    }
-    /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1 ---- */
+    /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1; warm: s = max(b - A r, floor),
+     *      lam = max(lam_warm[src], floor) with the same source knot as the VRP ---- */
     for (int k = 0; k < N; ++k) {
         const int m = nfacets[k];
+        const int ws = warm && k + warm->shift < N;
+        const double sfloor = ws ? warm->floor : 1e-2;
         for (int i = 0; i < m; ++i) {
             const double* a = Ain + (k * M + i) * 2;
             const double gr = FD2(a[0], vrp[2 * k], a[1], vrp[2 * k + 1]);
             const double sl = bin[k * M + i] - gr;
-            w->s[k * MF + i] = sl > 1e-2 ? sl : 1e-2;
-            w->lam[k * MF + i] = 1.0;
+            w->s[k * MF + i] = sl > sfloor ? sl : sfloor;
+            if (ws) {
+                const double lw = warm->lambda[(k + warm->shift) * M + i];
+                w->lam[k * MF + i] = lw > sfloor ? lw : sfloor;
+            } else {
+                w->lam[k * MF + i] = 1.0;
+            }
         }
     }
     /* ---- initial dual residual with single-shooting costates nu_k = qx_k + alpha_k nu_{k+1}
@@ -919,11 +978,7 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         dres = nanmax(dres, fabs(fma(-w->be[k], nu0, w->rh[2 * k])));
         dres = nanmax(dres, fabs(fma(-w->be[k], nu1, w->rh[2 * k + 1])));
     }
-    if (status == 2) {
-        if (iters_out) *iters_out = 0;
-        free(mem);
-        return 2;
-    }
+    if (status == 2) goto done;
 
     for (it = 0;; ++it) {
         const double pres = dcm_residuals(w, 1);
@@ -1023,7 +1078,13 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
         }
         dres = dres * (1.0 - a);
     }
+done:
     if (iters_out) *iters_out = it;
+    if (lam_out) {   /* final multipliers, [N][M], zero in unused facet slots */
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < M; ++i)
+                lam_out[k * M + i] = (i < nfacets[k] && nfacets[k] <= M) ? w->lam[k * MF + i] : 0.0;
+    }
     free(mem);
     return status;
 }
@@ -1034,7 +1095,10 @@ typedef struct {
     int64_t batch;
     const double *xi_init, *omega, *xi_ref, *vrp_ref, *A, *b;
     const int32_t* nfacets;
-    double *xi, *vrp;
+    const double *vrp_ws, *lam_ws;
+    int32_t shift;
+    double floor;
+    double *xi, *vrp, *lam_out;
     int32_t *status, *iters;
     atomic_llong next;
 } batch_job;
@@ -1046,15 +1110,35 @@ static void* batch_worker(void* arg)
     for (;;) {
         const long long p = atomic_fetch_add(&J->next, 1);
         if (p >= J->batch) break;
-        J->status[p] = orc_dcm_mpc_solve(J->prm, J->xi_init + 2 * p, J->omega + (int64_t)N * p,
-                                         J->xi_ref + (int64_t)2 * (N + 1) * p,
-                                         J->vrp_ref + (int64_t)2 * N * p,
-                                         J->A + (int64_t)2 * N * M * p, J->b + (int64_t)N * M * p,
-                                         J->nfacets + (int64_t)N * p,
-                                         J->xi + (int64_t)2 * (N + 1) * p,
-                                         J->vrp + (int64_t)2 * N * p, J->iters + p);
+        orc_dcm_warm wm;
+        const orc_dcm_warm* wp = NULL;
+        if (J->vrp_ws) {
+            wm.vrp = J->vrp_ws + (int64_t)2 * N * p;
+            wm.lambda = J->lam_ws + (int64_t)N * M * p;
+            wm.shift = J->shift;
+            wm.reserved = 0;
+            wm.floor = J->floor;
+            wp = &wm;
+        }
+        J->status[p] = orc_dcm_mpc_solve_warm(
+            J->prm, J->xi_init + 2 * p, J->omega + (int64_t)N * p,
+            J->xi_ref + (int64_t)2 * (N + 1) * p, J->vrp_ref + (int64_t)2 * N * p,
+            J->A + (int64_t)2 * N * M * p, J->b + (int64_t)N * M * p, J->nfacets + (int64_t)N * p,
+            wp, J->xi + (int64_t)2 * (N + 1) * p, J->vrp + (int64_t)2 * N * p,
+            J->lam_out ? J->lam_out + (int64_t)N * M * p : NULL, J->iters + p);
     }
     return NULL;
+}
+
+static void run_batch(batch_job* J, int threads)
+{
+    atomic_init(&J->next, 0);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    for (int t = 1; t < threads; ++t) pthread_create(&th[t], NULL, batch_worker, J);
+    batch_worker(J);
+    for (int t = 1; t < threads; ++t) pthread_join(th[t], NULL);
 }
 
 void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threads,
@@ -1066,11 +1150,19 @@ void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threa
     batch_job J = {.prm = prm, .batch = batch, .xi_init = xi_init, .omega = omega,
                    .xi_ref = xi_ref, .vrp_ref = vrp_ref, .A = A, .b = b, .nfacets = nfacets,
                    .xi = xi, .vrp = vrp, .status = status, .iters = iters};
-    atomic_init(&J.next, 0);
-    if (threads < 1) threads = 1;
-    if (threads > 256) threads = 256;
-    pthread_t th[256];
-    for (int t = 1; t < threads; ++t) pthread_create(&th[t], NULL, batch_worker, &J);
-    batch_worker(&J);
-    for (int t = 1; t < threads; ++t) pthread_join(th[t], NULL);
+    run_batch(&J, threads);
+}
+
+void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int threads,
+                                  const double* xi_init, const double* omega, const double* xi_ref,
+                                  const double* vrp_ref, const double* A, const double* b,
+                                  const int32_t* nfacets, const double* vrp_ws,
+                                  const double* lam_ws, int32_t shift, double floor, double* xi,
+                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters)
+{
+    batch_job J = {.prm = prm, .batch = batch, .xi_init = xi_init, .omega = omega,
+                   .xi_ref = xi_ref, .vrp_ref = vrp_ref, .A = A, .b = b, .nfacets = nfacets,
+                   .vrp_ws = vrp_ws, .lam_ws = lam_ws, .shift = shift, .floor = floor,
+                   .xi = xi, .vrp = vrp, .lam_out = lam_out, .status = status, .iters = iters};
+    run_batch(&J, threads);
 }

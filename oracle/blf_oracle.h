@@ -14,6 +14,8 @@
  *                            pinned by Planners/tests/ContactPhaseListTest.cpp:15-153 (8 phases)
  *   orc_present_index        Planners/src/ContactList.cpp:190-202 (getPresentContact)
  *                            pinned by Planners/tests/ContactListTest.cpp:85-92
+ *   orc_dcm_phase_expand     the phases of ContactPhaseList.cpp:16-84 per knot with the
+ *                            getPresentContact rule (ContactList.cpp:190-202)
  *   orc_hull2d_hrep          Planners/src/ConvexHullHelper.cpp:35-99; arithmetic of the pinned
  *                            third-party dependency Qhull 8.0.0 ("Qt"), restated as a 2-D
  *                            monotone chain with collinear merge; pinned against scipy's bundled
@@ -54,6 +56,14 @@ int orc_contact_phases(int L, int C, const double* act, const double* deact,
 /* getPresentContact: index of the last element with activation_time <= t, or -1 (end()). */
 int orc_present_index(const double* activation_times, int n, double t);
 
+/* blf_dcm_phase_expand for one problem: phase table begin/end [P], pA [P][M][2], pb [P][M],
+ * pnf [P], pref [P][2] (nphases valid) -> A [N][M][2], b [N][M], nfacets [N], xi_ref [N+1][2],
+ * vrp_ref [N][2] of the window of knots (start + k) dt. */
+void orc_dcm_phase_expand(int P, int M, int nphases, const double* begin, const double* end,
+                          const double* pA, const double* pb, const int32_t* pnf,
+                          const double* pref, int64_t start, double dt, int N, double* A,
+                          double* b, int32_t* nfacets, double* xi_ref, double* vrp_ref);
+
 int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);
 int orc_hull2d_contains(const double* A, const double* b, int nfacets, const double* p);
 
@@ -77,6 +87,24 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                       const double* b, const int32_t* nfacets, double* xi, double* vrp,
                       int32_t* iters);
 
+/* Warm start of a receding-horizon re-solve ("Warm start"): knot k
+ * starts from knot src = min(k + shift, N - 1) of a previous solution: r_k = vrp[src],
+ * s = max(b - A r, floor), lam = max(lambda[src], floor); the LQ start step is skipped. */
+typedef struct orc_dcm_warm {
+    const double* vrp;      /* [N][2]  */
+    const double* lambda;   /* [N][M]  */
+    int32_t shift;
+    int32_t reserved;
+    double floor;
+} orc_dcm_warm;
+
+/* As orc_dcm_mpc_solve, from the warm start `warm` (NULL: the cold start), also writing the final
+ * multipliers to lam_out [N][M] (NULL: not written; zero in unused facet slots). */
+int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, const double* omega,
+                           const double* xi_ref, const double* vrp_ref, const double* A,
+                           const double* b, const int32_t* nfacets, const orc_dcm_warm* warm,
+                           double* xi, double* vrp, double* lam_out, int32_t* iters);
+
 /* Whole batch (problem-major arrays), split over `threads` POSIX threads (one problem per
  * thread at a time).  Used as bench.py's CPU baseline. */
 void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threads,
@@ -84,6 +112,14 @@ void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threa
                              const double* vrp_ref, const double* A, const double* b,
                              const int32_t* nfacets, double* xi, double* vrp, int32_t* status,
                              int32_t* iters);
+/* Batch with warm starts: vrp_ws [B][N][2] and lam_ws [B][N][M] (both NULL: cold starts),
+ * lam_out [B][N][M] or NULL. */
+void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int threads,
+                                  const double* xi_init, const double* omega, const double* xi_ref,
+                                  const double* vrp_ref, const double* A, const double* b,
+                                  const int32_t* nfacets, const double* vrp_ws,
+                                  const double* lam_ws, int32_t shift, double floor, double* xi,
+                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters);
 
 /* Tree sum with the device's reduction order: c has n entries, padded with
  * zeros to 64*ceil(n/64); per 64-block xor-butterfly (distances 1, 2, 4, ..., 32), then block

@@ -59,6 +59,12 @@ def lib():
         L.orc_dcm_mpc_solve_batch.argtypes = [ctypes.POINTER(OrcParams), ctypes.c_int64,
                                               ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _ip,
                                               _dp, _dp, _ip, _ip]
+        L.orc_dcm_mpc_solve_batch_warm.argtypes = [
+            ctypes.POINTER(OrcParams), ctypes.c_int64, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp,
+            _ip, _dp, _dp, ctypes.c_int32, ctypes.c_double, _dp, _dp, _dp, _ip, _ip]
+        L.orc_dcm_phase_expand.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp,
+                                           _dp, _dp, _ip, _dp, ctypes.c_int64, ctypes.c_double,
+                                           ctypes.c_int, _dp, _dp, _ip, _dp, _dp]
         L.orc_wave_tree_sum.restype = ctypes.c_double
         L.orc_wave_tree_sum.argtypes = [_dp, ctypes.c_int]
         L.orc_contact_eval.argtypes = [_dp] * 8
@@ -206,6 +212,48 @@ def dcm_mpc_solve_batch(prob, params=None, threads=1, count=None):
                                   _d(g("xi_ref")), _d(g("vrp_ref")), _d(g("A")), _d(g("b")),
                                   _i(g("nfacets")), _d(xi), _d(vrp), _i(status), _i(iters))
     return status, xi, vrp, iters
+
+
+def dcm_mpc_solve_batch_warm(prob, vrp_ws=None, lam_ws=None, shift=1, floor=1e-4,
+                             params=None, threads=1):
+    """Batch solve from warm starts (vrp_ws [B][N][2], lam_ws [B][N][M]; None: cold starts).
+    Returns status, xi, vrp, iters, lam [B][N][M] (final multipliers)."""
+    B, N = prob["omega"].shape
+    p = params or default_params(N)
+    M = p.max_facets
+    xi = np.zeros((B, N + 1, 2))
+    vrp = np.zeros((B, N, 2))
+    lam = np.zeros((B, N, M))
+    status = np.zeros(B, dtype=np.int32)
+    iters = np.zeros(B, dtype=np.int32)
+    g = lambda k: np.ascontiguousarray(prob[k])
+    ws_v = None if vrp_ws is None else _f64(vrp_ws)
+    ws_l = None if lam_ws is None else _f64(lam_ws)
+    lib().orc_dcm_mpc_solve_batch_warm(
+        ctypes.byref(p), B, threads, _d(g("xi_init")), _d(g("omega")), _d(g("xi_ref")),
+        _d(g("vrp_ref")), _d(g("A")), _d(g("b")), _i(g("nfacets")),
+        None if ws_v is None else _d(ws_v), None if ws_l is None else _d(ws_l), int(shift),
+        float(floor), _d(xi), _d(vrp), _d(lam), _i(status), _i(iters))
+    return status, xi, vrp, iters, lam
+
+
+def dcm_phase_expand(table, start, dt, horizon):
+    """table: nphases [B], phase_begin/phase_end [B,P], phase_A [B,P,M,2], phase_b [B,P,M],
+    phase_nf [B,P], phase_ref [B,P,2] -> dict(A, b, nfacets, xi_ref, vrp_ref) of the window."""
+    B, P = table["phase_begin"].shape
+    M = table["phase_b"].shape[2]
+    N = horizon
+    out = dict(A=np.zeros((B, N, M, 2)), b=np.zeros((B, N, M)),
+               nfacets=np.zeros((B, N), dtype=np.int32), xi_ref=np.zeros((B, N + 1, 2)),
+               vrp_ref=np.zeros((B, N, 2)))
+    c = lambda k, q: np.ascontiguousarray(table[k][q])
+    for q in range(B):
+        lib().orc_dcm_phase_expand(
+            P, M, int(table["nphases"][q]), _d(c("phase_begin", q)), _d(c("phase_end", q)),
+            _d(c("phase_A", q)), _d(c("phase_b", q)), _i(c("phase_nf", q)), _d(c("phase_ref", q)),
+            int(start), float(dt), N, _d(out["A"][q]), _d(out["b"][q]), _i(out["nfacets"][q]),
+            _d(out["xi_ref"][q]), _d(out["vrp_ref"][q]))
+    return out
 
 
 def wave_tree_sum(c):
