@@ -114,10 +114,11 @@ def main():
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
+    ap.add_argument("--workload", choices=("c2", "c3", "c5", "rh"), default="c2",
                     help="c2 (default, the driver's metric): configs[1]; c3: configs[2] pipeline "
                          "(hull H-rep + QP + swing splines, B=65536); c5: configs[4] closed loop "
-                         "(QP + 30-DoF floating-base dynamics with contacts, B=16384)")
+                         "(QP + 30-DoF floating-base dynamics with contacts, B=16384); rh: "
+                         "receding-horizon advance() (phase expansion + warm-started QP, B=4096)")
     args = ap.parse_args()
     if args.workload != "c2":
         return other_workload(args)
@@ -271,6 +272,8 @@ def other_workload(args):
     h = native.Handle(0)
     dev = torch.device("cuda", 0)
     N = args.horizon
+    if args.workload == "rh":
+        return receding_horizon(args, h, dev)
     if args.workload == "c3":
         B = 65536
         prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED)
@@ -336,6 +339,88 @@ def other_workload(args):
                 "config": {"workload": f"configs[4] on one GPU: batch={B} robots, horizon-{N} QP "
                                        f"+ {nsteps} Euler steps of the 6+24 DoF dynamics per "
                                        f"period", "batch_per_gpu": B}}
+    print(json.dumps(line), flush=True)
+
+
+def phase_expand_bytes(P, N, M):
+    """Algorithmic bytes of blf_dcm_phase_expand per problem: the phase table read once
+    (nphases, begin/end, A rows, b, counts, reference points) and the window written."""
+    return 4 + P * (16 + 24 * M + 4 + 16) + N * (24 * M + 4 + 16) + 16 * (N + 1)
+
+
+def receding_horizon(args, h, dev):
+    """TimeVaryingDCMPlanner::advance() on the device, B = 4096 plans: per step the knot -> phase
+    expansion of the window (blf_dcm_phase_expand), the warm-started solve
+    (blf_dcm_mpc_solve_warm, shifted previous VRPs and multipliers), and xi_1 -> next xi_init.
+    The phase polygons are built once (blf_hull2d_hrep over the phases) before timing."""
+    import torch
+    from blf import native
+    from blf import problems as P
+    B, N = args.batch, args.horizon
+    S = args.warmup + args.steps + 1
+    prob = P.make_batch(B, horizon=N + S, n_footsteps=8, seed=P.SEED)
+    t = lambda k, dt=None: torch.from_numpy(prob[k]).to(dev)
+    table = h.phase_table(t("nphases"), t("phase_begin"), t("phase_end"), t("phase_corners"),
+                          t("phase_ncorners"), ref=t("phase_ref"))
+    omega_full = t("omega")
+    M = table["phase_b"].shape[2]
+    params = native.default_params(N, max_facets=M)
+    stream = torch.cuda.current_stream()
+    state = dict(xi0=t("xi_init").clone(), prev=None, s=0)
+    bufs = [None, None]
+    iters = []
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def step(timed=False):
+        s = state["s"]
+        if timed:
+            ev[0].record(stream)
+        w = h.dcm_phase_expand(table, s, prob["dt"], N)
+        if timed:
+            ev[1].record(stream)
+        w.update(xi_init=state["xi0"], omega=omega_full[:, s:s + N].contiguous())
+        cur = s % 2
+        warm = None
+        if state["prev"] is not None:
+            warm = dict(vrp=state["prev"]["vrp"], lam=state["prev"]["lam"], shift=1, floor=1e-2)
+        if timed:
+            ev[2].record(stream)
+        out = h.dcm_mpc_solve(w, params, out=bufs[cur], warm=warm, lambda_out=True)
+        if timed:
+            ev[3].record(stream)
+        bufs[cur] = out
+        state["xi0"] = out["xi"][:, 1].contiguous()
+        state["prev"] = out
+        state["s"] = s + 1
+        iters.append(out["iters"])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    expand_ms, solve_ms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+        torch.cuda.synchronize()
+        expand_ms.append(ev[0].elapsed_time(ev[1]))
+        solve_ms.append(ev[2].elapsed_time(ev[3]))
+    sec = (time.perf_counter() - t0) / args.steps
+    assert int((state["prev"]["status"] != 0).sum()) == 0, "unsolved QPs in a window"
+    it = torch.stack(iters[args.warmup:]).float()
+    Pn = table["phase_begin"].shape[1]
+    ex_ms = sorted(expand_ms)[len(expand_ms) // 2]
+    ex_gbs = phase_expand_bytes(Pn, N, M) * B / (ex_ms * 1e-3) / 1e9
+    line = {"metric": "receding-horizon DCM-MPC advance()/sec (phase expansion + warm-started QP)",
+            "value": B / sec, "unit": "QP/s", "n_gpus": 1, "ms_per_step": sec * 1e3,
+            "steps": args.steps, "warmup": args.warmup, "dtype": "f64",
+            "mean_ipm_iters_warm": float(it.mean()),
+            "solve_ms_median": sorted(solve_ms)[len(solve_ms) // 2],
+            "phase_expand": {"kernel_ms_median": ex_ms, "bytes_per_problem":
+                             phase_expand_bytes(Pn, N, M), "achieved_gbs": ex_gbs,
+                             "frac_hbm": ex_gbs / HBM_PEAK_GBS},
+            "config": {"workload": f"batch={B} plans (8 footsteps, {Pn} phases), horizon={N}, "
+                                   f"window moved one knot per step, warm start shift 1 floor 1e-2",
+                       "batch_per_gpu": B}}
     print(json.dumps(line), flush=True)
 
 

@@ -606,7 +606,7 @@ __device__ __forceinline__ void publish_xi(const Knot& K, double* bnd, int wv, i
 #ifndef BLF_MIN_WAVES
 #define BLF_MIN_WAVES 3   // waves per SIMD the register allocation must allow (<= 168 VGPRs)
 #endif
-template <int NT>
+template <int NT, bool WARM, bool LAMOUT>
 __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_ipm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     const bool own = k < N;
     const bool last = k == N - 1;
     const int64_t p = blockIdx.x;
-    const bool warm = ws_vrp != nullptr;                  // uniform over the launch
+    constexpr bool warm = WARM;                           // a separate instantiation each way
     const bool ws = warm && k + P.ws_shift < N;           // this knot starts from the warm start
     STAMP(t_start);
 
@@ -968,7 +968,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         const int64_t sx = p * (N + 1) + (k + 1);
         xi_out[2 * sx] = K.x0;
         xi_out[2 * sx + 1] = K.x1;
-        if (lam_out) {
+        if (LAMOUT) {
             double* lo = lam_out + st * M;
 #pragma unroll
             for (int i = 0; i < kMaxFacets; ++i) {
@@ -998,7 +998,10 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
     if (lds > 160 * 1024)
         return set_error(BLF_ERR_UNSUPPORTED, "horizon %d with %d facet slots needs %zu B of LDS",
                          kp.N, kp.M, lds);
-    hipLaunchKernelGGL(dcm_mpc_ipm_kernel<NT>, dim3((unsigned)batch), dim3(NT), lds, s, kp,
+    auto kern = (warm != nullptr)
+                    ? (lam_out ? dcm_mpc_ipm_kernel<NT, true, true> : dcm_mpc_ipm_kernel<NT, true, false>)
+                    : (lam_out ? dcm_mpc_ipm_kernel<NT, false, true> : dcm_mpc_ipm_kernel<NT, false, false>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(NT), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                        pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr,
                        sol->xi, sol->vrp, sol->status, sol->iters, lam_out);
