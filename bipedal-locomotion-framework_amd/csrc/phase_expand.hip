@@ -10,11 +10,11 @@
 // and copies phase p's H-rep rows, facet count and reference point to the knot.  A knot outside
 // every phase gets nfacets = -1 (the QP then reports BLF_QP_BAD_FACETS) and zero rows/references.
 //
-// Mapping: one thread per (problem, knot 0..N, facet slot).  Consecutive threads write
-// consecutive 16-B A rows and 8-B offsets; the facet-slot-0 thread of a knot also writes the
-// knot's facet count and references.  The phase tables (a few hundred bytes per problem) are
-// read through the cache by the (N+1) M threads of the problem.  HBM-bound: the bytes written
-// are the per-knot arrays of the QP.
+// Mapping: one workgroup per problem.  The problem's phase table (a few hundred bytes per phase)
+// is staged into LDS with coalesced loads; one pass assigns every knot its phase (binary search
+// in LDS); then the workgroup writes the window's arrays with consecutive threads on consecutive
+// 16-B A rows, 8-B offsets, facet counts and 16-B references.  HBM-bound: the bytes written are
+// the per-knot arrays of the QP.
 #include "blf_internal.h"
 
 namespace blf {
@@ -22,8 +22,7 @@ namespace {
 
 constexpr int kExpandBlock = 256;
 
-__device__ __forceinline__ int phase_of(const double* __restrict__ begin,
-                                        const double* __restrict__ end, int n, double t)
+__device__ __forceinline__ int phase_of(const double* begin, const double* end, int n, double t)
 {
     int lo = 0, hi = n;
     while (lo < hi) {
@@ -35,44 +34,72 @@ __device__ __forceinline__ int phase_of(const double* __restrict__ begin,
     return (p >= 0 && t < end[p]) ? p : -1;
 }
 
+// Dynamic LDS (doubles first, 16-B aligned): A [P][M] double2, ref [P] double2, b [P][M],
+// begin [P], end [P], then nf [P] and the knot phases [N+1] as int32.
+__host__ __device__ inline size_t expand_lds_bytes(int P, int M, int N)
+{
+    return sizeof(double) * ((size_t)P * (3 * M + 4)) + sizeof(int32_t) * ((size_t)P + N + 1);
+}
+
 __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
     int32_t P, const int32_t* __restrict__ nphases, const double* __restrict__ pbegin,
     const double* __restrict__ pend, const double* __restrict__ pA, const double* __restrict__ pb,
     const int32_t* __restrict__ pnf, const double* __restrict__ pref, int32_t M,
-    int64_t start_knot, double dt, int32_t N, int64_t batch, double* __restrict__ A,
-    double* __restrict__ b, int32_t* __restrict__ nfacets, double* __restrict__ xi_ref,
-    double* __restrict__ vrp_ref)
+    int64_t start_knot, double dt, int32_t N, double* __restrict__ A, double* __restrict__ b,
+    int32_t* __restrict__ nfacets, double* __restrict__ xi_ref, double* __restrict__ vrp_ref)
 {
-    const int64_t t = (int64_t)blockIdx.x * kExpandBlock + threadIdx.x;
-    const int64_t per = (int64_t)(N + 1) * M;
-    if (t >= batch * per) return;
-    const int64_t q = t / per;                 // problem
-    const int r = (int)(t - q * per);
-    const int k = r / M;                       // knot 0..N
-    const int i = r - k * M;                   // facet slot
+    extern __shared__ __attribute__((aligned(16))) double xs[];
+    double2* sA = reinterpret_cast<double2*>(xs);            // [P][M]
+    double2* sRef = sA + (size_t)P * M;                       // [P]
+    double* sB = reinterpret_cast<double*>(sRef + P);         // [P][M]
+    double* sBeg = sB + (size_t)P * M;                        // [P]
+    double* sEnd = sBeg + P;                                  // [P]
+    int32_t* sNf = reinterpret_cast<int32_t*>(sEnd + P);      // [P]
+    int32_t* sPh = sNf + P;                                   // [N+1]
+    const int tid = threadIdx.x;
+    const int64_t q = blockIdx.x;
+
+    // 1. stage the phase table (coalesced, contiguous per problem)
     int np = nphases[q];
     np = np < 0 ? 0 : (np > P ? P : np);
-    const double tk = (double)(start_knot + k) * dt;
-    const int ph = phase_of(pbegin + q * P, pend + q * P, np, tk);
-    const int64_t src = q * P + ph;            // valid only if ph >= 0
-    if (k < N) {
-        const int64_t dst = (q * N + k) * M + i;
-        double2 a = make_double2(0.0, 0.0);
-        double bi = 0.0;
-        if (ph >= 0) {
-            a = reinterpret_cast<const double2*>(pA)[src * M + i];
-            bi = pb[src * M + i];
+    {
+        const double2* gA = reinterpret_cast<const double2*>(pA) + q * P * M;
+        for (int j = tid; j < np * M; j += kExpandBlock) sA[j] = gA[j];
+        const double* gB = pb + q * P * M;
+        for (int j = tid; j < np * M; j += kExpandBlock) sB[j] = gB[j];
+        const double2* gR = reinterpret_cast<const double2*>(pref) + q * P;
+        for (int j = tid; j < np; j += kExpandBlock) {
+            sRef[j] = gR[j];
+            sBeg[j] = pbegin[q * P + j];
+            sEnd[j] = pend[q * P + j];
+            sNf[j] = pnf[q * P + j];
         }
-        reinterpret_cast<double2*>(A)[dst] = a;
-        b[dst] = bi;
     }
-    if (i == 0) {
-        double2 ref = make_double2(0.0, 0.0);
-        if (ph >= 0) ref = reinterpret_cast<const double2*>(pref)[src];
-        reinterpret_cast<double2*>(xi_ref)[q * (N + 1) + k] = ref;
+    __syncthreads();
+    // 2. knot -> phase
+    for (int k = tid; k <= N; k += kExpandBlock)
+        sPh[k] = phase_of(sBeg, sEnd, np, (double)(start_knot + k) * dt);
+    __syncthreads();
+    // 3. the window's arrays, consecutive threads on consecutive elements
+    const int nm = N * M;
+    double2* oA = reinterpret_cast<double2*>(A) + q * nm;
+    double* oB = b + q * nm;
+    for (int j = tid; j < nm; j += kExpandBlock) {
+        const int k = j / M, i = j - k * M;
+        const int ph = sPh[k];
+        oA[j] = ph >= 0 ? sA[ph * M + i] : make_double2(0.0, 0.0);
+        oB[j] = ph >= 0 ? sB[ph * M + i] : 0.0;
+    }
+    double2* oX = reinterpret_cast<double2*>(xi_ref) + q * (N + 1);
+    double2* oR = reinterpret_cast<double2*>(vrp_ref) + q * N;
+    int32_t* oN = nfacets + q * N;
+    for (int k = tid; k <= N; k += kExpandBlock) {
+        const int ph = sPh[k];
+        const double2 ref = ph >= 0 ? sRef[ph] : make_double2(0.0, 0.0);
+        oX[k] = ref;
         if (k < N) {
-            reinterpret_cast<double2*>(vrp_ref)[q * N + k] = ref;
-            nfacets[q * N + k] = ph >= 0 ? pnf[src] : -1;
+            oR[k] = ref;
+            oN[k] = ph >= 0 ? sNf[ph] : -1;
         }
     }
 }
@@ -86,14 +113,17 @@ blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* 
                                double* b, int32_t* nfacets, double* xi_ref, double* vrp_ref,
                                hipStream_t s)
 {
-    const int64_t threads = batch * (int64_t)(N + 1) * M;
-    if (threads == 0) return BLF_OK;
-    const int64_t blocks = ceil_div(threads, kExpandBlock);
-    if (blocks > 0x7fffffffLL)
-        return set_error(BLF_ERR_UNSUPPORTED, "phase expansion of %lld knots too large",
-                         (long long)(threads / M));
-    hipLaunchKernelGGL(phase_expand_kernel, dim3((unsigned)blocks), dim3(kExpandBlock), 0, s, P,
-                       nphases, begin, end, pA, pb, pnf, pref, M, start_knot, dt, N, batch, A, b,
+    if (batch == 0) return BLF_OK;
+    if (batch > 0x7fffffffLL)
+        return set_error(BLF_ERR_UNSUPPORTED, "phase expansion of %lld problems too large",
+                         (long long)batch);
+    const size_t lds = expand_lds_bytes(P, M, N);
+    if (lds > 64 * 1024)
+        return set_error(BLF_ERR_UNSUPPORTED,
+                         "%d phases and a horizon of %d need %zu B of LDS (64 KiB at most)", P, N,
+                         lds);
+    hipLaunchKernelGGL(phase_expand_kernel, dim3((unsigned)batch), dim3(kExpandBlock), lds, s, P,
+                       nphases, begin, end, pA, pb, pnf, pref, M, start_knot, dt, N, A, b,
                        nfacets, xi_ref, vrp_ref);
     return check_hip(hipGetLastError(), "phase_expand_kernel launch");
 }

@@ -1,5 +1,6 @@
 """HBM roofline of the streaming kernels (the 40 % HBM bar applies to these):
-dcm_rollout, hull2d_hrep, quintic_eval, contact_model_eval, fbk_euler (1 step) on large batches.
+dcm_rollout, hull2d_hrep, quintic_eval, contact_model_eval, fbk_euler (1 step), phase_expand on
+large batches.
 achieved = algorithmic bytes / median kernel time (HIP events).
   python tools/stream_bench.py [--out gpurun_out/stream.json]"""
 import argparse
@@ -89,6 +90,19 @@ def main():
     pos, jt = rnd(F, 3), rnd(F, n)
     ms = timed(lambda: h.fbk_euler_integrate(0.01, pos, R, jt, tw, sd, 0.0, 0.001, 0.001))
     report("fbk_euler_kernel[1 step]", F * 8 * (2 * (3 + 9 + n) + 6 + n), ms, F, "systems")
+    del R, tw, sd, pos, jt
+    # dcm_phase_expand: 32768 plans of 13 phases, horizon-100 windows
+    from blf import problems as P
+    Bq, N = 32768, 100
+    prob = P.make_batch(Bq, horizon=N + 8, n_footsteps=8, seed=P.SEED)
+    t = lambda k: torch.from_numpy(prob[k]).to(dev)
+    table = h.phase_table(t("nphases"), t("phase_begin"), t("phase_end"), t("phase_corners"),
+                          t("phase_ncorners"), ref=t("phase_ref"))
+    Pn, M = table["phase_begin"].shape[1], 8
+    w = h.dcm_phase_expand(table, 3, prob["dt"], N)
+    ms = timed(lambda: h.dcm_phase_expand(table, 3, prob["dt"], N, out=w))
+    report("phase_expand_kernel", Bq * (4 + Pn * (16 + 24 * M + 4 + 16) + N * (24 * M + 4 + 16)
+                                        + 16 * (N + 1)), ms, Bq, "windows")
     if args.out:
         with open(args.out, "w") as f:
             json.dump(lines, f, indent=1)
