@@ -63,7 +63,7 @@ class BlfError(RuntimeError):
 class DcmMpcParams(ctypes.Structure):
     _fields_ = [("horizon", _i32), ("max_facets", _i32), ("max_iter", _i32), ("reserved", _i32),
                 ("dt", _f64), ("w_xi", _f64 * 2), ("w_vrp", _f64 * 2), ("w_terminal", _f64 * 2),
-                ("tol_mu", _f64), ("tol_primal", _f64), ("tol_dual", _f64)]
+                ("tol_mu", _f64), ("tol_primal", _f64), ("tol_dual", _f64), ("tol_polish", _f64)]
 
 
 class DcmMpcProblem(ctypes.Structure):
@@ -72,7 +72,7 @@ class DcmMpcProblem(ctypes.Structure):
 
 
 class DcmMpcSolution(ctypes.Structure):
-    _fields_ = [("xi", _vp), ("vrp", _vp), ("status", _vp), ("iters", _vp)]
+    _fields_ = [("xi", _vp), ("vrp", _vp), ("status", _vp), ("iters", _vp), ("polished", _vp)]
 
 
 class PhaseTable(ctypes.Structure):
@@ -327,7 +327,8 @@ class Handle:
         """prob: dict of device tensors xi_init [B,2], omega [B,N], xi_ref [B,N+1,2],
         vrp_ref [B,N,2], A [B,N,M,2], b [B,N,M], nfacets [B,N] (int32).
         warm: None (cold start) or dict(vrp [B,N,2], lam [B,N,M], shift, floor)
-        (blf_dcm_mpc_solve_warm); lambda_out: also return the final multipliers out["lam"]."""
+        (blf_dcm_mpc_solve_warm); lambda_out: also return the final multipliers out["lam"].
+        out["polished"] [B] says which solutions are the certified active-set polish."""
         torch = _torch()
         B, N = prob["omega"].shape
         M = prob["b"].shape[2]
@@ -339,7 +340,8 @@ class Handle:
             out = dict(xi=torch.empty((B, N + 1, 2), dtype=torch.float64, device=dev),
                        vrp=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
                        status=torch.empty((B,), dtype=torch.int32, device=dev),
-                       iters=torch.empty((B,), dtype=torch.int32, device=dev))
+                       iters=torch.empty((B,), dtype=torch.int32, device=dev),
+                       polished=torch.empty((B,), dtype=torch.int32, device=dev))
         pb = DcmMpcProblem(
             _ptr(prob["xi_init"], torch.float64, (B, 2), "xi_init"),
             _ptr(prob["omega"], torch.float64, (B, N), "omega"),
@@ -352,7 +354,8 @@ class Handle:
             _ptr(out["xi"], torch.float64, (B, N + 1, 2), "xi"),
             _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
             _ptr(out["status"], torch.int32, (B,), "status"),
-            _ptr(out["iters"], torch.int32, (B,), "iters"))
+            _ptr(out["iters"], torch.int32, (B,), "iters"),
+            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
         ws = None
         if warm is not None:
             ws = DcmMpcWarmStart(_ptr(warm["vrp"], torch.float64, (B, N, 2), "warm vrp"),

@@ -27,8 +27,9 @@ namespace {
 #ifdef BLF_STAMPS
 // Diagnostic build only (make stamps): per-phase cycle sums of thread 0 for the first 64 QPs.
 // [0] whole kernel, [1] factorization, [2] predictor solve .. corrector solve, [3] iterations,
-// [4] residuals + reduction, [5] W-phase, [6] predictor solve, [7] corrector step + update.
-__device__ unsigned long long g_blf_stamps[8];
+// [4] residuals + reduction, [5] W-phase, [6] predictor solve, [7] corrector step + update,
+// [8] polish attempts (cycles), [9] polish attempts (count).
+__device__ unsigned long long g_blf_stamps[10];
 #define STAMP(t) unsigned long long t = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, t0) \
     do { if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_blf_stamps[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
@@ -41,6 +42,7 @@ struct KParams {
     int N, M, max_iter;
     int ws_shift;        // warm start: knot k starts from knot k + ws_shift (ws_vrp != nullptr)
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_mu, tol_p, tol_d;
+    double tol_polish;   // > 0: try the active-set polish once mu <= tol_polish
     double ws_floor;     // warm start: s, lambda >= ws_floor
 };
 
@@ -454,23 +456,14 @@ __device__ __forceinline__ bool rc_apply(const Rc& e, double P00, double P01, do
     return ok;
 }
 
-// Factorization (oracle dcm_factor) from W = (W00, W01, W11, detW).  Leaves P_{k+1}, h, M in K.
-// Returns false on this lane if its K or H block is not positive definite.
+// Riccati sweep (oracle riccati_sweep) for this lane's E_k.  Leaves P_{k+1} in K.  Returns false
+// on this lane if some (I + G H) or (I + G P) is not positive definite.
 template <int NW>
-__device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, double W01,
-                                       double W11, double dW, double* bnd, int N, int nwa, int k,
-                                       int wv, int lane, bool own)
+__device__ __forceinline__ bool riccati(Knot& K, const KParams& P, double E00, double E01,
+                                        double E11, double* bnd, int N, int nwa, int k, int wv,
+                                        int lane, bool own)
 {
     bool ok = true;
-    const double b2 = K.be * K.be;
-    double E00 = 0.0, E01 = 0.0, E11 = 0.0;
-    if (own) {
-        const double detRW = fma(P.Rw0, P.Rw1, FD2(P.Rw1, W00, P.Rw0, W11)) + dW;
-        const double ie = b2 / detRW;
-        E00 = (P.Rw1 + W11) * ie;
-        E01 = -(W01 * ie);
-        E11 = (P.Rw0 + W00) * ie;
-    }
     // P_k for every knot: Kogge-Stone scan of Riccati map elements over the wavefront's lanes
     // (oracle dcm_factor / rc_combine), then P_k = f_{k..}(P at the next wavefront's first knot)
     Rc e;
@@ -529,10 +522,30 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
     K.P00 = P00;
     K.P01 = P01;
     K.P11 = P11;
+    return ok;
+}
+
+// Factorization (oracle dcm_factor) from W = (W00, W01, W11, detW).  Leaves P_{k+1}, h, M in K.
+// Returns false on this lane if its K or H block is not positive definite.
+template <int NW>
+__device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, double W01,
+                                       double W11, double dW, double* bnd, int N, int nwa, int k,
+                                       int wv, int lane, bool own)
+{
+    const double b2 = K.be * K.be;
+    double E00 = 0.0, E01 = 0.0, E11 = 0.0;
     if (own) {
-        const double B00 = fma(b2, P00, P.Rw0);
-        const double B01 = b2 * P01;
-        const double B11 = fma(b2, P11, P.Rw1);
+        const double detRW = fma(P.Rw0, P.Rw1, FD2(P.Rw1, W00, P.Rw0, W11)) + dW;
+        const double ie = b2 / detRW;
+        E00 = (P.Rw1 + W11) * ie;
+        E01 = -(W01 * ie);
+        E11 = (P.Rw0 + W00) * ie;
+    }
+    bool ok = riccati<NW>(K, P, E00, E01, E11, bnd, N, nwa, k, wv, lane, own);
+    if (own) {
+        const double B00 = fma(b2, K.P00, P.Rw0);
+        const double B01 = b2 * K.P01;
+        const double B11 = fma(b2, K.P11, P.Rw1);
         const double H00 = B00 + W00;
         const double H01 = B01 + W01;
         const double H11 = B11 + W11;
@@ -614,7 +627,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     const int32_t* __restrict__ nfacets, const double* __restrict__ ws_vrp,
     const double* __restrict__ ws_lam, double* __restrict__ xi_out,
     double* __restrict__ vrp_out, int32_t* __restrict__ status_out,
-    int32_t* __restrict__ iters_out, double* __restrict__ lam_out)
+    int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out)
 {
     constexpr int NW = NT / kWave;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -694,7 +707,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     }
     __syncthreads();
 
-    int status = 0, it = 0;
+    int status = 0, it = 0, polished = 0;
     if (any_bad) {
         status = BLF_QP_BAD_FACETS;
     } else {
@@ -775,6 +788,169 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 break;
             }
             STAMP_ADD(4, t_r);
+            if (P.tol_polish > 0.0 && mu <= P.tol_polish) {
+                // ---- active-set polish (oracle dcm_polish, DESIGN.md 4 "Polish"): one Newton
+                //      step of the QP with the guessed active facets as equalities, certified
+                //      (primal, stationarity, multiplier signs) or undone ----
+                STAMP(t_p);
+                const double sr0 = K.r0, sr1 = K.r1, sx0 = K.x0, sx1 = K.x1;
+                int pc = 0, pi1 = 0, pi2 = 0;
+                double E00 = 0.0, E01 = 0.0, E11 = 0.0;
+                bool okp = true;
+                if (own) {
+                    const int kx = opaque(k);
+                    const int km = opaque(K.m), mm = opaque_s(mmax);
+#pragma unroll
+                    for (int i = 0; i < kMaxFacets; ++i) {
+                        if (i >= mm) break;
+                        if (i < km && K.lam[i] > K.s[i]) {
+                            if (pc == 0) pi1 = i;
+                            else if (pc == 1) pi2 = i;
+                            ++pc;
+                        }
+                    }
+                    okp = pc <= 2;
+                    const double b2 = K.be * K.be;
+                    if (pc == 0) {
+                        E00 = b2 / P.Rw0;
+                        E11 = b2 / P.Rw1;
+                    } else if (pc == 1) {
+                        const double2 a = L.A2[pi1 * N + kx];
+                        const double aa = FD2(a.x, a.x, a.y, a.y);
+                        const double t = (FD2(a.x, sr0, a.y, sr1) - L.BI[pi1 * N + kx].x) / aa;
+                        K.r0 = fma(-t, a.x, sr0);
+                        K.r1 = fma(-t, a.y, sr1);
+                        const double u = a.y * a.y, v = a.x * a.x, q = a.x * a.y;
+                        const double ie = b2 / FD2(P.Rw0, u, P.Rw1, v);
+                        E00 = u * ie;
+                        E01 = -(q * ie);
+                        E11 = v * ie;
+                    } else {
+                        const double2 a = L.A2[pi1 * N + kx];
+                        const double2 e = L.A2[pi2 * N + kx];
+                        const double ba = L.BI[pi1 * N + kx].x, be = L.BI[pi2 * N + kx].x;
+                        const double det = fma(a.x, e.y, -(a.y * e.x));
+                        const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
+                        if (!(det * det > 1e-18 * (aa * ee))) okp = false;
+                        const double idet = 1.0 / det;
+                        K.r0 = fma(ba, e.y, -(a.y * be)) * idet;
+                        K.r1 = fma(a.x, be, -(ba * e.x)) * idet;
+                    }
+                    double pd, cd;
+                    residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
+                }
+                okp = riccati<NW>(K, P, E00, E01, E11, bnd, N, nwa, k, wv, lane, own) && okp;
+                if (own) {
+                    const double b2 = K.be * K.be;
+                    const double B00 = fma(b2, K.P00, P.Rw0);
+                    const double B01 = b2 * K.P01;
+                    const double B11 = fma(b2, K.P11, P.Rw1);
+                    if (pc == 0) {
+                        const double det = fma(B00, B11, -(B01 * B01));
+                        if (!(det > 0.0) || __builtin_isinf(det)) okp = false;
+                        const double idet = 1.0 / det;
+                        K.h00 = B11 * idet;
+                        K.h01 = -(B01 * idet);
+                        K.h11 = B00 * idet;
+                    } else if (pc == 1) {
+                        const double2 a = L.A2[pi1 * N + opaque(k)];
+                        const double u = a.y * a.y, v = a.x * a.x, q = a.x * a.y;
+                        const double tbt = FD3(B00, u, B11, v, -2.0 * (B01 * q));
+                        if (!(tbt > 0.0) || __builtin_isinf(tbt)) okp = false;
+                        const double itb = 1.0 / tbt;
+                        K.h00 = u * itb;
+                        K.h01 = -(q * itb);
+                        K.h11 = v * itb;
+                    } else {
+                        K.h00 = 0.0;
+                        K.h01 = 0.0;
+                        K.h11 = 0.0;
+                    }
+                }
+                {
+                    double dr0, dr1, dx0, dx1;
+                    solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
+                    if (own) {
+                        K.r0 = K.r0 + dr0;
+                        K.r1 = K.r1 + dr1;
+                        K.x0 = K.x0 + dx0;
+                        K.x1 = K.x1 + dx1;
+                    }
+                }
+                publish_xi<NW>(K, bnd, wv, lane);
+                __syncthreads();
+                // certificate: costates of the polished trajectory by single shooting
+                double xn0, xn1, pl1 = 0.0, pl2 = 0.0;
+                xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xn0, xn1);
+                if (own) {
+                    double pd, cd;
+                    residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xn0, xn1, rref, xref, pd, cd);
+                }
+                {
+                    const double ga = own ? K.al : 0.0;
+                    const double c0 = own ? K.al * K.qx0 : 0.0, c1 = own ? K.al * K.qx1 : 0.0;
+                    double vn0, vn1;
+                    scan_backward<NW>(ga, 0.0, 0.0, ga, c0, c1, bnd, nwa, wv, lane, vn0, vn1);
+                    if (own) {
+                        const int kx = opaque(k);
+                        const double nu0 = K.qx0 + vn0;
+                        const double nu1 = K.qx1 + vn1;
+                        const double g0 = fma(K.be, nu0, -K.rh0);
+                        const double g1 = fma(K.be, nu1, -K.rh1);
+                        if (pc == 0) {
+                            if (!(fabs(g0) <= P.tol_d) || !(fabs(g1) <= P.tol_d)) okp = false;
+                        } else if (pc == 1) {
+                            const double2 a = L.A2[pi1 * N + kx];
+                            pl1 = FD2(a.x, g0, a.y, g1) / FD2(a.x, a.x, a.y, a.y);
+                            if (!(pl1 >= -P.tol_d)) okp = false;
+                            if (!(fabs(fma(-pl1, a.x, g0)) <= P.tol_d) || !(fabs(fma(-pl1, a.y, g1)) <= P.tol_d))
+                                okp = false;
+                        } else {
+                            const double2 a = L.A2[pi1 * N + kx];
+                            const double2 e = L.A2[pi2 * N + kx];
+                            const double idet = 1.0 / fma(a.x, e.y, -(a.y * e.x));
+                            pl1 = fma(g0, e.y, -(e.x * g1)) * idet;
+                            pl2 = fma(a.x, g1, -(g0 * a.y)) * idet;
+                            if (!(pl1 >= -P.tol_d) || !(pl2 >= -P.tol_d)) okp = false;
+                        }
+                        const int km = opaque(K.m), mm = opaque_s(mmax);
+#pragma unroll
+                        for (int i = 0; i < kMaxFacets; ++i) {
+                            if (i >= mm) break;
+                            if (i < km) {
+                                const double2 a = L.A2[i * N + kx];
+                                if (!(FD2(a.x, K.r0, a.y, K.r1) - L.BI[i * N + kx].x <= P.tol_p)) okp = false;
+                            }
+                        }
+                    }
+                }
+                const bool rejected = __syncthreads_or(!okp);
+                STAMP_ADD(8, t_p);
+#ifdef BLF_STAMPS
+                if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_blf_stamps[9], 1ull);
+#endif
+                if (!rejected) {
+                    if (LAMOUT && own) {   // the optimum's multipliers: active facets, 0 elsewhere
+                        pl1 = pl1 > 0.0 ? pl1 : 0.0;
+                        pl2 = pl2 > 0.0 ? pl2 : 0.0;
+#pragma unroll
+                        for (int i = 0; i < kMaxFacets; ++i)
+                            K.lam[i] = (pc >= 1 && i == pi1) ? pl1 : (pc == 2 && i == pi2) ? pl2 : 0.0;
+                    }
+                    polished = 1;
+                    break;   // solved: the certified optimum
+                }
+                K.r0 = sr0;
+                K.r1 = sr1;
+                K.x0 = sx0;
+                K.x1 = sx1;
+                publish_xi<NW>(K, bnd, wv, lane);
+                __syncthreads();
+                if (own) {   // the iterate's gradient and defects again (the polish reused them)
+                    double pd, cd;
+                    residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
+                }
+            }
             if (mu <= P.tol_mu && pres <= P.tol_p && dres <= P.tol_d) break;   // solved
             if (it >= P.max_iter) {
                 status = BLF_QP_MAX_ITER;
@@ -982,6 +1158,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         xi_out[2 * p * (N + 1) + 1] = xi01;
         status_out[p] = status;
         iters_out[p] = it;
+        if (polished_out) polished_out[p] = polished;
         STAMP_ADD(0, t_start);
 #ifdef BLF_STAMPS
         if (blockIdx.x < 64) atomicAdd(&g_blf_stamps[3], (unsigned long long)it);
@@ -1004,7 +1181,7 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
     hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(NT), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                        pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr,
-                       sol->xi, sol->vrp, sol->status, sol->iters, lam_out);
+                       sol->xi, sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
     return check_hip(hipGetLastError(), "dcm_mpc_ipm_kernel launch");
 }
 
@@ -1013,11 +1190,11 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
 #ifdef BLF_STAMPS
 extern "C" int blf_debug_stamps(unsigned long long* out, int reset)
 {
-    unsigned long long h[8];
+    unsigned long long h[10];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_blf_stamps), sizeof(h)) != hipSuccess) return -1;
-    for (int i = 0; i < 8; ++i) out[i] = h[i];
+    for (int i = 0; i < 10; ++i) out[i] = h[i];
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_blf_stamps), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
@@ -1039,6 +1216,7 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     kp.tol_mu = prm->tol_mu;
     kp.tol_p = prm->tol_primal;
     kp.tol_d = prm->tol_dual;
+    kp.tol_polish = prm->tol_polish;
     kp.ws_shift = warm ? warm->shift : 0;
     kp.ws_floor = warm ? warm->floor : 0.0;
     if (batch == 0) return BLF_OK;

@@ -45,6 +45,7 @@ bool TimeVaryingDCMPlanner::initialize(std::weak_ptr<ParametersHandler::IParamet
     ptr->getParameter("foot_length", m_footLength);
     ptr->getParameter("foot_width", m_footWidth);
     ptr->getParameter("tolerance", m_params.tol_mu);
+    ptr->getParameter("polish_tolerance", m_params.tol_polish);
     ptr->getParameter("warm_start", m_warmStart);
     ptr->getParameter("warm_start_floor", m_warmFloor);
     if (!(m_warmFloor > 0) || !std::isfinite(m_warmFloor))

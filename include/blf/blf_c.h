@@ -156,6 +156,11 @@ typedef struct blf_dcm_mpc_params {
     double tol_mu;         /* stop when mean complementarity <= tol_mu ...                   */
     double tol_primal;     /* ... and max |primal residual|, |dynamics defect| <= tol_primal */
     double tol_dual;       /* ... and the tracked dual residual bound <= tol_dual            */
+    double tol_polish;     /* > 0: once mean complementarity <= tol_polish, try the active-set
+                            * polish: one Newton step of the QP with the guessed
+                            * active facets as equalities, accepted only if it certifies as the
+                            * optimum (primal feasible, stationary, multipliers >= 0 to
+                            * tol_primal / tol_dual); else the IPM goes on.  0: IPM only.     */
 } blf_dcm_mpc_params;
 
 typedef struct blf_dcm_mpc_problem {
@@ -173,6 +178,8 @@ typedef struct blf_dcm_mpc_solution {
     double* vrp;             /* [B][N][2]                                                   */
     int32_t* status;         /* [B]  BLF_QP_*                                               */
     int32_t* iters;          /* [B]  IPM iterations taken                                   */
+    int32_t* polished;       /* [B]  optional (NULL: not written): 1 if the solution is the
+                              *      certified active-set polish, 0 if the IPM's own iterate    */
 } blf_dcm_mpc_solution;
 
 /* Warm start of a receding-horizon re-solve (TimeVaryingDCMPlanner::advance()):
@@ -190,7 +197,7 @@ typedef struct blf_dcm_mpc_warm_start {
 } blf_dcm_mpc_warm_start;
 
 /* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-16,
- * tol_primal 1e-10, tol_dual 1e-9, max_iter 50, max_facets 8). */
+ * tol_primal 1e-10, tol_dual 1e-9, tol_polish 1e-6, max_iter 50, max_facets 8). */
 void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);
 
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,

@@ -629,26 +629,15 @@ static int rc_apply(const rc_el* e, double P00, double P01, double P11, double* 
     return ok;
 }
 
-/* Factorization of the Newton system for the barrier Hessian blocks W_k (DESIGN.md 4.3).
- * 1. E_k = beta_k^2 (R + W_k)^{-1}                                           (knot-parallel)
- * 2. P_k for every knot by a Kogge-Stone scan of Riccati map elements over the 64 lanes of each
- *    wavefront (lane l composes with lane l + d), then P_k = f_{k..}(P at the next wavefront's
- *    first knot, or P_N = diag(Pw)), wavefronts from last to first;
- * 3. H_k = R + W_k + beta_k^2 P_{k+1}, h_k = H_k^{-1}, M_k = P_{k+1} h_k,
- *    G_k = alpha_k (I - beta_k^2 M_k)                                         (knot-parallel)
- * Returns 0 if some (I + G H), (I + G P) or H_k is not positive definite (status NUMERICAL). */
-static int dcm_factor(dcm_ws* w)
+/* Riccati sweep for the per-knot E_k = w->E: P_k for every knot by a Kogge-Stone
+ * scan of Riccati map elements over the 64 lanes of each wavefront (lane l composes with lane
+ * l + d), then P_k = f_{k..}(P at the next wavefront's first knot, or P_N = diag(Pw)), wavefronts
+ * from last to first.  Leaves P_{k+1} in w->Pn[k].  Returns 0 if some (I + G H) or (I + G P) is
+ * not positive definite. */
+static int riccati_sweep(dcm_ws* w)
 {
     const int N = w->N;
     int ok = 1;
-    for (int k = 0; k < N; ++k) {
-        const double* Wk = w->W + 4 * k;
-        const double detRW = fma(w->Rw0, w->Rw1, FD2(w->Rw1, Wk[0], w->Rw0, Wk[2])) + Wk[3];
-        const double ie = w->b2[k] / detRW;
-        w->E[3 * k] = (w->Rw1 + Wk[2]) * ie;
-        w->E[3 * k + 1] = -(Wk[1] * ie);
-        w->E[3 * k + 2] = (w->Rw0 + Wk[0]) * ie;
-    }
     double Pb0 = w->Pw0, Pb1 = 0.0, Pb2 = w->Pw1;      /* P at the next wavefront's first knot */
     if (!w->scans) {   /* CPU-efficient sequential recursion P_k = f_k(P_{k+1}) (cpu_baseline only) */
         for (int k = N - 1; k >= 1; --k) {
@@ -700,6 +689,47 @@ static int dcm_factor(dcm_ws* w)
     w->Pn[3 * (N - 1)] = w->Pw0;
     w->Pn[3 * (N - 1) + 1] = 0.0;
     w->Pn[3 * (N - 1) + 2] = w->Pw1;
+    return ok;
+}
+
+/* M_k = P_{k+1} h_k and G_k = alpha_k (I - beta_k^2 M_k) from w->h[k] (knot-parallel). */
+static void mg_from_h(dcm_ws* w, int k)
+{
+    const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
+    const double h00 = w->h[3 * k], h01 = w->h[3 * k + 1], h11 = w->h[3 * k + 2];
+    const double b2 = w->b2[k];
+    const double M00 = FD2(P00, h00, P01, h01);
+    const double M01 = FD2(P00, h01, P01, h11);
+    const double M10 = FD2(P01, h00, P11, h01);
+    const double M11 = FD2(P01, h01, P11, h11);
+    double* Mk = w->Mm + 4 * k;
+    Mk[0] = M00; Mk[1] = M01; Mk[2] = M10; Mk[3] = M11;
+    const double al = w->al[k];
+    double* G = w->G + 4 * k;
+    G[0] = al * fma(-b2, M00, 1.0);
+    G[1] = -(al * (b2 * M01));
+    G[2] = -(al * (b2 * M10));
+    G[3] = al * fma(-b2, M11, 1.0);
+}
+
+/* Factorization of the Newton system for the barrier Hessian blocks W_k (DESIGN.md 4.3).
+ * 1. E_k = beta_k^2 (R + W_k)^{-1}                                           (knot-parallel)
+ * 2. P_k for every knot by the Riccati sweep (riccati_sweep)
+ * 3. H_k = R + W_k + beta_k^2 P_{k+1}, h_k = H_k^{-1}, M_k = P_{k+1} h_k,
+ *    G_k = alpha_k (I - beta_k^2 M_k)                                         (knot-parallel)
+ * Returns 0 if some (I + G H), (I + G P) or H_k is not positive definite (status NUMERICAL). */
+static int dcm_factor(dcm_ws* w)
+{
+    const int N = w->N;
+    for (int k = 0; k < N; ++k) {
+        const double* Wk = w->W + 4 * k;
+        const double detRW = fma(w->Rw0, w->Rw1, FD2(w->Rw1, Wk[0], w->Rw0, Wk[2])) + Wk[3];
+        const double ie = w->b2[k] / detRW;
+        w->E[3 * k] = (w->Rw1 + Wk[2]) * ie;
+        w->E[3 * k + 1] = -(Wk[1] * ie);
+        w->E[3 * k + 2] = (w->Rw0 + Wk[0]) * ie;
+    }
+    int ok = riccati_sweep(w);
     for (int k = 0; k < N; ++k) {
         const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
         const double* Wk = w->W + 4 * k;
@@ -716,20 +746,8 @@ static int dcm_factor(dcm_ws* w)
         const double det = (detB + trW) + Wk[3];
         if (!(det > 0.0) || isinf(det)) ok = 0;
         const double idet = 1.0 / det;
-        const double h00 = H11 * idet, h01 = -(H01 * idet), h11 = H00 * idet;
-        w->h[3 * k] = h00; w->h[3 * k + 1] = h01; w->h[3 * k + 2] = h11;
-        const double M00 = FD2(P00, h00, P01, h01);
-        const double M01 = FD2(P00, h01, P01, h11);
-        const double M10 = FD2(P01, h00, P11, h01);
-        const double M11 = FD2(P01, h01, P11, h11);
-        double* Mk = w->Mm + 4 * k;
-        Mk[0] = M00; Mk[1] = M01; Mk[2] = M10; Mk[3] = M11;
-        const double al = w->al[k];
-        double* G = w->G + 4 * k;
-        G[0] = al * fma(-b2, M00, 1.0);
-        G[1] = -(al * (b2 * M01));
-        G[2] = -(al * (b2 * M10));
-        G[3] = al * fma(-b2, M11, 1.0);
+        w->h[3 * k] = H11 * idet; w->h[3 * k + 1] = -(H01 * idet); w->h[3 * k + 2] = H00 * idet;
+        mg_from_h(w, k);
     }
     return ok;
 }
@@ -842,19 +860,185 @@ static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
     *dl = -((li * (si + dsv)) * w->is[k * MF + i]);
 }
 
+/* Costates of the current trajectory by single shooting, nu_k = qx_k + alpha_k nu_{k+1} (backward
+ * scan of v_k = alpha_k nu_{k+1}); needs dcm_residuals first.  Leaves v in w->v. */
+static void costate_scan(dcm_ws* w)
+{
+    for (int k = 0; k < w->N; ++k) {
+        double* G = w->sg + 4 * k;
+        G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
+        w->sc[2 * k] = w->al[k] * w->qx[2 * k];
+        w->sc[2 * k + 1] = w->al[k] * w->qx[2 * k + 1];
+    }
+    scan_backward(w, w->sg, w->sc);
+}
+
+/* Active-set polish ("Polish"; the kernel's polish block mirrors it term for term).
+ * From an interior iterate, guess the active set (facet i of knot k is active iff lam_i > s_i; at
+ * most two per knot), move each r_k onto its active lines, and take ONE Newton step of the
+ * equality-constrained QP, where knot k's VRP moves only along the active lines:
+ *   c_k = 0: E_k = beta^2 R^{-1},                 h_k = B^{-1}
+ *   c_k = 1: E_k = beta^2 t t^T / (t^T R t),      h_k = t t^T / (t^T B t),  t = (-a_y, a_x)
+ *   c_k = 2: E_k = 0,                             h_k = 0                   (r_k is the vertex)
+ * with B = R + beta^2 P_{k+1} — the W -> infinity limits of the barrier blocks.  The QP is
+ * quadratic, so the step lands on the equality-constrained optimum up to rounding.  It is then
+ * certified as the optimum of the inequality QP: every inactive facet satisfied (a r - b <= tol_p),
+ * stationarity R (r - r_ref) + A_act^T lam = beta nu_{k+1} (costates by single shooting) solved
+ * for the active multipliers with residual <= tol_d, and lam >= -tol_d.  Accepted: xi, vrp hold
+ * the polished optimum, lam its multipliers (max(lam, 0) on the active facets, 0 on the others)
+ * and 1 is returned.  Rejected: xi, vrp are restored, 0 is returned. */
+static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
+{
+    const int N = w->N, M = w->M;
+    int ok = 1;
+    int* pc = (int*)malloc(sizeof(int) * 3 * (size_t)N);
+    int* pi1 = pc + N;
+    int* pi2 = pc + 2 * N;
+    double* bak = (double*)malloc(sizeof(double) * (6 * (size_t)N + 2));
+    double* lm = bak + 4 * (size_t)N + 2;   /* [N][2] multipliers of the active facets */
+    memcpy(bak, w->vrp, sizeof(double) * 2 * N);
+    memcpy(bak + 2 * N, w->xi, sizeof(double) * (2 * (size_t)N + 2));
+    /* 1. active sets, projection onto the active lines, E_k (knot-parallel) */
+    for (int k = 0; k < N; ++k) {
+        const int m = w->nf[k];
+        int c = 0, i1 = 0, i2 = 0;
+        for (int i = 0; i < m; ++i) {
+            if (w->lam[k * MF + i] > w->s[k * MF + i]) {
+                if (c == 0) i1 = i;
+                else if (c == 1) i2 = i;
+                ++c;
+            }
+        }
+        if (c > 2) ok = 0;
+        pc[k] = c; pi1[k] = i1; pi2[k] = i2;
+        const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
+        const double b2 = w->b2[k];
+        double* E = w->E + 3 * k;
+        if (c == 0) {
+            E[0] = b2 / w->Rw0; E[1] = 0.0; E[2] = b2 / w->Rw1;
+        } else if (c == 1) {
+            const double* a = w->A + (k * M + i1) * 2;
+            const double aa = FD2(a[0], a[0], a[1], a[1]);
+            const double t = (FD2(a[0], r0, a[1], r1) - w->b[k * M + i1]) / aa;
+            w->vrp[2 * k] = fma(-t, a[0], r0);
+            w->vrp[2 * k + 1] = fma(-t, a[1], r1);
+            const double u = a[1] * a[1], v = a[0] * a[0], q = a[0] * a[1];
+            const double ie = b2 / FD2(w->Rw0, u, w->Rw1, v);
+            E[0] = u * ie; E[1] = -(q * ie); E[2] = v * ie;
+        } else {
+            const double* a = w->A + (k * M + i1) * 2;
+            const double* e = w->A + (k * M + i2) * 2;
+            const double ba = w->b[k * M + i1], be = w->b[k * M + i2];
+            const double det = fma(a[0], e[1], -(a[1] * e[0]));
+            const double aa = FD2(a[0], a[0], a[1], a[1]), ee = FD2(e[0], e[0], e[1], e[1]);
+            if (!(det * det > 1e-18 * (aa * ee))) ok = 0;      /* (nearly) parallel active facets */
+            const double idet = 1.0 / det;
+            w->vrp[2 * k] = fma(ba, e[1], -(a[1] * be)) * idet;
+            w->vrp[2 * k + 1] = fma(a[0], be, -(ba * e[0])) * idet;
+            E[0] = 0.0; E[1] = 0.0; E[2] = 0.0;
+        }
+    }
+    /* 2. residuals at (xi, projected r): gradient, Euler defects */
+    dcm_residuals(w, 0);
+    /* 3. Riccati sweep; 4. h_k of the active subspace (knot-parallel) */
+    if (!riccati_sweep(w)) ok = 0;
+    for (int k = 0; k < N; ++k) {
+        const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
+        const double b2 = w->b2[k];
+        const double B00 = fma(b2, P00, w->Rw0);
+        const double B01 = b2 * P01;
+        const double B11 = fma(b2, P11, w->Rw1);
+        double* h = w->h + 3 * k;
+        if (pc[k] == 0) {
+            const double det = fma(B00, B11, -(B01 * B01));
+            if (!(det > 0.0) || isinf(det)) ok = 0;
+            const double idet = 1.0 / det;
+            h[0] = B11 * idet; h[1] = -(B01 * idet); h[2] = B00 * idet;
+        } else if (pc[k] == 1) {
+            const double* a = w->A + (k * M + pi1[k]) * 2;
+            const double u = a[1] * a[1], v = a[0] * a[0], q = a[0] * a[1];
+            const double tbt = FD3(B00, u, B11, v, -2.0 * (B01 * q));
+            if (!(tbt > 0.0) || isinf(tbt)) ok = 0;
+            const double it = 1.0 / tbt;
+            h[0] = u * it; h[1] = -(q * it); h[2] = v * it;
+        } else {
+            h[0] = 0.0; h[1] = 0.0; h[2] = 0.0;
+        }
+        mg_from_h(w, k);
+    }
+    /* 5. the Newton step for g = R (r - r_ref) */
+    for (int k = 0; k < N; ++k) {
+        w->g[2 * k] = w->rh[2 * k];
+        w->g[2 * k + 1] = w->rh[2 * k + 1];
+    }
+    dcm_solve(w);
+    for (int k = 0; k < N; ++k) {
+        w->vrp[2 * k] = w->vrp[2 * k] + w->dr[2 * k];
+        w->vrp[2 * k + 1] = w->vrp[2 * k + 1] + w->dr[2 * k + 1];
+        w->xi[2 * (k + 1)] = w->xi[2 * (k + 1)] + w->x[2 * (k + 1)];
+        w->xi[2 * (k + 1) + 1] = w->xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
+    }
+    /* 6. certificate: primal feasibility, stationarity, dual feasibility (knot-parallel) */
+    dcm_residuals(w, 0);
+    costate_scan(w);
+    for (int k = 0; k < N; ++k) {
+        const double nu0 = w->qx[2 * k] + w->v[2 * (k + 1)];
+        const double nu1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
+        const double g0 = fma(w->be[k], nu0, -w->rh[2 * k]);
+        const double g1 = fma(w->be[k], nu1, -w->rh[2 * k + 1]);
+        const int c = pc[k];
+        double l1 = 0.0, l2 = 0.0;
+        if (c == 0) {
+            if (!(fabs(g0) <= tol_d) || !(fabs(g1) <= tol_d)) ok = 0;
+        } else if (c == 1) {
+            const double* a = w->A + (k * M + pi1[k]) * 2;
+            l1 = FD2(a[0], g0, a[1], g1) / FD2(a[0], a[0], a[1], a[1]);
+            if (!(l1 >= -tol_d)) ok = 0;
+            if (!(fabs(fma(-l1, a[0], g0)) <= tol_d) || !(fabs(fma(-l1, a[1], g1)) <= tol_d)) ok = 0;
+        } else {
+            const double* a = w->A + (k * M + pi1[k]) * 2;
+            const double* e = w->A + (k * M + pi2[k]) * 2;
+            const double idet = 1.0 / fma(a[0], e[1], -(a[1] * e[0]));
+            l1 = fma(g0, e[1], -(e[0] * g1)) * idet;
+            l2 = fma(a[0], g1, -(g0 * a[1])) * idet;
+            if (!(l1 >= -tol_d) || !(l2 >= -tol_d)) ok = 0;
+        }
+        lm[2 * k] = l1 > 0.0 ? l1 : 0.0;
+        lm[2 * k + 1] = l2 > 0.0 ? l2 : 0.0;
+        const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
+        for (int i = 0; i < w->nf[k]; ++i) {
+            const double* a = w->A + (k * M + i) * 2;
+            if (!(FD2(a[0], r0, a[1], r1) - w->b[k * M + i] <= tol_p)) ok = 0;
+        }
+    }
+    if (!ok) {
+        memcpy(w->vrp, bak, sizeof(double) * 2 * N);
+        memcpy(w->xi, bak + 2 * N, sizeof(double) * (2 * (size_t)N + 2));
+    } else {   /* the multipliers of the certified optimum: lam of the active facets, 0 elsewhere */
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < w->nf[k]; ++i)
+                w->lam[k * MF + i] = (pc[k] >= 1 && i == pi1[k]) ? lm[2 * k]
+                                     : (pc[k] == 2 && i == pi2[k]) ? lm[2 * k + 1] : 0.0;
+    }
+    free(pc);
+    free(bak);
+    return ok;
+}
+
 int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const double* omega,
                       const double* xi_ref, const double* vrp_ref, const double* Ain,
                       const double* bin, const int32_t* nfacets, double* xi, double* vrp,
                       int32_t* iters_out)
 {
     return orc_dcm_mpc_solve_warm(prm, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, NULL,
-                                  xi, vrp, NULL, iters_out);
+                                  xi, vrp, NULL, iters_out, NULL);
 }
 
 int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, const double* omega,
                            const double* xi_ref, const double* vrp_ref, const double* Ain,
                            const double* bin, const int32_t* nfacets, const orc_dcm_warm* warm,
-                           double* xi, double* vrp, double* lam_out, int32_t* iters_out)
+                           double* xi, double* vrp, double* lam_out, int32_t* iters_out,
+                           int32_t* polished_out)
 {
     const int N = prm->horizon;
     const int M = prm->max_facets;
@@ -882,7 +1066,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     w->sc = p; p += 2 * N; w->sg = p; p += 4 * N;
     w->v = p; p += 2 * (N + 1); w->x = p; p += 2 * (N + 1);
 
-    int status = 0, it = 0, ntot = 0;
+    int status = 0, it = 0, ntot = 0, polished = 0;
     for (int k = 0; k < N; ++k) {
         if (nfacets[k] < 0 || nfacets[k] > M) status = 3;
         else ntot += nfacets[k];
@@ -984,6 +1168,10 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         const double pres = dcm_residuals(w, 1);
         const double mu = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
         if (!(mu == mu) || !(pres == pres) || !(dres == dres) || isinf(mu)) { status = 2; break; }
+        if (prm->tol_polish > 0.0 && mu <= prm->tol_polish) {
+            if (dcm_polish(w, prm->tol_primal, prm->tol_dual)) { polished = 1; status = 0; break; }
+            dcm_residuals(w, 1);   /* the iterate's gradient and defects again (the polish reused them) */
+        }
         if (mu <= prm->tol_mu && pres <= prm->tol_primal && dres <= prm->tol_dual) { status = 0; break; }
         if (it >= prm->max_iter) { status = 1; break; }
 
@@ -1080,6 +1268,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     }
 done:
     if (iters_out) *iters_out = it;
+    if (polished_out) *polished_out = polished;
     if (lam_out) {   /* final multipliers, [N][M], zero in unused facet slots */
         for (int k = 0; k < N; ++k)
             for (int i = 0; i < M; ++i)
@@ -1099,7 +1288,7 @@ typedef struct {
     int32_t shift;
     double floor;
     double *xi, *vrp, *lam_out;
-    int32_t *status, *iters;
+    int32_t *status, *iters, *polished;
     atomic_llong next;
 } batch_job;
 
@@ -1125,7 +1314,8 @@ static void* batch_worker(void* arg)
             J->xi_ref + (int64_t)2 * (N + 1) * p, J->vrp_ref + (int64_t)2 * N * p,
             J->A + (int64_t)2 * N * M * p, J->b + (int64_t)N * M * p, J->nfacets + (int64_t)N * p,
             wp, J->xi + (int64_t)2 * (N + 1) * p, J->vrp + (int64_t)2 * N * p,
-            J->lam_out ? J->lam_out + (int64_t)N * M * p : NULL, J->iters + p);
+            J->lam_out ? J->lam_out + (int64_t)N * M * p : NULL, J->iters + p,
+            J->polished ? J->polished + p : NULL);
     }
     return NULL;
 }
@@ -1158,11 +1348,13 @@ void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int 
                                   const double* vrp_ref, const double* A, const double* b,
                                   const int32_t* nfacets, const double* vrp_ws,
                                   const double* lam_ws, int32_t shift, double floor, double* xi,
-                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters)
+                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters,
+                                  int32_t* polished)
 {
     batch_job J = {.prm = prm, .batch = batch, .xi_init = xi_init, .omega = omega,
                    .xi_ref = xi_ref, .vrp_ref = vrp_ref, .A = A, .b = b, .nfacets = nfacets,
                    .vrp_ws = vrp_ws, .lam_ws = lam_ws, .shift = shift, .floor = floor,
-                   .xi = xi, .vrp = vrp, .lam_out = lam_out, .status = status, .iters = iters};
+                   .xi = xi, .vrp = vrp, .lam_out = lam_out, .status = status, .iters = iters,
+                   .polished = polished};
     run_batch(&J, threads);
 }

@@ -78,6 +78,7 @@ void orc_quintic_eval(const double* knots_t, const double* coeffs, int nknots, i
 typedef struct orc_dcm_params {
     int32_t horizon, max_facets, max_iter, sequential;
     double dt, w_xi[2], w_vrp[2], w_terminal[2], tol_mu, tol_primal, tol_dual;
+    double tol_polish;   /* > 0: try the active-set polish once mu <= tol_polish */
 } orc_dcm_params;
 
 /* Solve one problem (arrays for this problem only, same layout as blf_dcm_mpc_problem).
@@ -99,11 +100,13 @@ typedef struct orc_dcm_warm {
 } orc_dcm_warm;
 
 /* As orc_dcm_mpc_solve, from the warm start `warm` (NULL: the cold start), also writing the final
- * multipliers to lam_out [N][M] (NULL: not written; zero in unused facet slots). */
+ * multipliers to lam_out [N][M] (NULL: not written; zero in unused facet slots) and whether the
+ * active-set polish was accepted to *polished (NULL: not written). */
 int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, const double* omega,
                            const double* xi_ref, const double* vrp_ref, const double* A,
                            const double* b, const int32_t* nfacets, const orc_dcm_warm* warm,
-                           double* xi, double* vrp, double* lam_out, int32_t* iters);
+                           double* xi, double* vrp, double* lam_out, int32_t* iters,
+                           int32_t* polished);
 
 /* Whole batch (problem-major arrays), split over `threads` POSIX threads (one problem per
  * thread at a time).  Used as bench.py's CPU baseline. */
@@ -113,13 +116,14 @@ void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threa
                              const int32_t* nfacets, double* xi, double* vrp, int32_t* status,
                              int32_t* iters);
 /* Batch with warm starts: vrp_ws [B][N][2] and lam_ws [B][N][M] (both NULL: cold starts),
- * lam_out [B][N][M] or NULL. */
+ * lam_out [B][N][M] or NULL, polished [B] or NULL. */
 void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int threads,
                                   const double* xi_init, const double* omega, const double* xi_ref,
                                   const double* vrp_ref, const double* A, const double* b,
                                   const int32_t* nfacets, const double* vrp_ws,
                                   const double* lam_ws, int32_t shift, double floor, double* xi,
-                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters);
+                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters,
+                                  int32_t* polished);
 
 /* Tree sum with the device's reduction order: c has n entries, padded with
  * zeros to 64*ceil(n/64); per 64-block xor-butterfly (distances 1, 2, 4, ..., 32), then block

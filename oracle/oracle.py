@@ -22,7 +22,7 @@ class OrcParams(ctypes.Structure):
                 ("dt", ctypes.c_double), ("w_xi", ctypes.c_double * 2),
                 ("w_vrp", ctypes.c_double * 2), ("w_terminal", ctypes.c_double * 2),
                 ("tol_mu", ctypes.c_double), ("tol_primal", ctypes.c_double),
-                ("tol_dual", ctypes.c_double)]
+                ("tol_dual", ctypes.c_double), ("tol_polish", ctypes.c_double)]
 
 
 def build():
@@ -61,7 +61,7 @@ def lib():
                                               _dp, _dp, _ip, _ip]
         L.orc_dcm_mpc_solve_batch_warm.argtypes = [
             ctypes.POINTER(OrcParams), ctypes.c_int64, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp,
-            _ip, _dp, _dp, ctypes.c_int32, ctypes.c_double, _dp, _dp, _dp, _ip, _ip]
+            _ip, _dp, _dp, ctypes.c_int32, ctypes.c_double, _dp, _dp, _dp, _ip, _ip, _ip]
         L.orc_dcm_phase_expand.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp,
                                            _dp, _dp, _ip, _dp, ctypes.c_int64, ctypes.c_double,
                                            ctypes.c_int, _dp, _dp, _ip, _dp, _dp]
@@ -182,6 +182,7 @@ def default_params(horizon, **kw):
     p.tol_mu = kw.get("tol_mu", 1e-16)
     p.tol_primal = kw.get("tol_primal", 1e-10)
     p.tol_dual = kw.get("tol_dual", 1e-9)
+    p.tol_polish = kw.get("tol_polish", 1e-6)   # blf_dcm_mpc_default_params
     return p
 
 
@@ -215,9 +216,10 @@ def dcm_mpc_solve_batch(prob, params=None, threads=1, count=None):
 
 
 def dcm_mpc_solve_batch_warm(prob, vrp_ws=None, lam_ws=None, shift=1, floor=1e-4,
-                             params=None, threads=1):
+                             params=None, threads=1, polished=None):
     """Batch solve from warm starts (vrp_ws [B][N][2], lam_ws [B][N][M]; None: cold starts).
-    Returns status, xi, vrp, iters, lam [B][N][M] (final multipliers)."""
+    Returns status, xi, vrp, iters, lam [B][N][M] (final multipliers); `polished` (an int32 [B]
+    array, optional) receives whether the active-set polish was accepted."""
     B, N = prob["omega"].shape
     p = params or default_params(N)
     M = p.max_facets
@@ -233,7 +235,8 @@ def dcm_mpc_solve_batch_warm(prob, vrp_ws=None, lam_ws=None, shift=1, floor=1e-4
         ctypes.byref(p), B, threads, _d(g("xi_init")), _d(g("omega")), _d(g("xi_ref")),
         _d(g("vrp_ref")), _d(g("A")), _d(g("b")), _i(g("nfacets")),
         None if ws_v is None else _d(ws_v), None if ws_l is None else _d(ws_l), int(shift),
-        float(floor), _d(xi), _d(vrp), _d(lam), _i(status), _i(iters))
+        float(floor), _d(xi), _d(vrp), _d(lam), _i(status), _i(iters),
+        None if polished is None else _i(polished))
     return status, xi, vrp, iters, lam
 
 

@@ -39,12 +39,15 @@ def test_dcm_mpc_matches_oracle_bitwise(handle, oracle, horizon, footsteps, batc
         host[k] = dev[k].cpu().numpy()
     out = handle.dcm_mpc_solve(dev)
     torch.cuda.synchronize()
-    st_o, xi_o, vrp_o, it_o = oracle.dcm_mpc_solve_batch(host, threads=8)
+    pol_o = np.zeros(batch, np.int32)
+    st_o, xi_o, vrp_o, it_o, _ = oracle.dcm_mpc_solve_batch_warm(host, threads=8, polished=pol_o)
     xi_g, vrp_g = out["xi"].cpu().numpy(), out["vrp"].cpu().numpy()
     st_g, it_g = out["status"].cpu().numpy(), out["iters"].cpu().numpy()
     assert (st_g == 0).all(), st_g
     assert (st_o == 0).all()
     np.testing.assert_array_equal(it_g, it_o)
+    np.testing.assert_array_equal(out["polished"].cpu().numpy(), pol_o)
+    assert pol_o.all()   # every default solve ends in the certified active-set polish
     assert np.abs(xi_g - xi_o).max() <= TOL
     assert np.abs(vrp_g - vrp_o).max() <= TOL
     np.testing.assert_array_equal(xi_g, xi_o)
@@ -163,3 +166,42 @@ def test_dcm_mpc_infeasible_and_nonfinite_inputs(handle, oracle):
     st, _ = _bitwise_vs_oracle(handle, oracle, host)
     assert st[0] != native.QP_SOLVED and st[1] != native.QP_SOLVED
     assert (st[2:] == native.QP_SOLVED).all()
+
+
+def test_dcm_mpc_ipm_only_matches_oracle_bitwise(handle, oracle):
+    """tol_polish = 0: the interior point method alone (stops at mu <= tol_mu), bit for bit."""
+    B, N = 48, 100
+    prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=21)
+    dev = _gpu_problem(handle, prob)
+    host = dict(prob)
+    for k in ("A", "b", "nfacets"):
+        host[k] = dev[k].cpu().numpy()
+    out = handle.dcm_mpc_solve(dev, params=native.default_params(N, tol_polish=0.0))
+    pol_o = np.ones(B, np.int32)
+    st_o, xi_o, vrp_o, it_o, _ = oracle.dcm_mpc_solve_batch_warm(
+        host, params=oracle.default_params(N, tol_polish=0.0), threads=8, polished=pol_o)
+    assert (st_o == 0).all() and not pol_o.any()
+    assert not out["polished"].any()
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), it_o)
+    np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi_o)
+    np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)
+
+
+def test_dcm_mpc_gpu_against_dense_certificate(handle):
+    """The device solutions against the independent dense KKT optimum (tests/dense_qp.py): the
+    polished optimum is exact to rounding, far inside north_star's 1e-9."""
+    import dense_qp
+    B, N = 512, 100
+    prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=33)
+    dev = _gpu_problem(handle, prob)
+    out = handle.dcm_mpc_solve(dev)
+    host = dict(prob)
+    for k in ("A", "b", "nfacets"):
+        host[k] = dev[k].cpu().numpy()
+    xi, vrp = out["xi"].cpu().numpy(), out["vrp"].cpu().numpy()
+    assert (out["status"] == 0).all() and out["polished"].all()
+    worst = 0.0
+    for i in range(0, B, 8):
+        xd, rd = dense_qp.certify(host, i, xi[i], vrp[i])
+        worst = max(worst, np.abs(xd - xi[i]).max(), np.abs(rd - vrp[i]).max())
+    assert worst < 1e-12, worst

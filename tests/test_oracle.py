@@ -146,14 +146,53 @@ def qp_batch():
     return O.assemble_constraints(P.make_batch(12, horizon=100, n_footsteps=6, seed=77))
 
 
-def test_dcm_mpc_oracle_against_dense_certificate(qp_batch):
+@pytest.mark.parametrize("tol_polish,bar", [(1e-6, 1e-12), (0.0, 1e-9)])
+def test_dcm_mpc_oracle_against_dense_certificate(qp_batch, tol_polish, bar):
+    """Default: the certified active-set polish, exact to rounding.  tol_polish = 0: the interior
+    point method alone, within north_star's 1e-9."""
     worst = 0.0
+    prm = O.default_params(100, tol_polish=tol_polish)
     for i in range(qp_batch["omega"].shape[0]):
-        st, xi, vrp, it = O.dcm_mpc_solve(qp_batch, index=i)
-        assert st == 0 and 5 <= it <= 30
+        st, xi, vrp, it = O.dcm_mpc_solve(qp_batch, prm, index=i)
+        assert st == 0 and 3 <= it <= 30
         xi_d, r_d = certify(qp_batch, i, xi, vrp)
         worst = max(worst, np.abs(xi - xi_d).max(), np.abs(vrp - r_d).max())
-    assert worst < 1e-9, worst
+    assert worst < bar, worst
+
+
+def test_dcm_mpc_polish_certifies_and_saves_iterations():
+    """The polish is accepted on every problem of a larger batch, matches the dense optimum to
+    1e-12 and needs fewer IPM iterations than the interior point method alone."""
+    prob = O.assemble_constraints(P.make_batch(96, horizon=100, n_footsteps=6, seed=78))
+    pol = np.zeros(96, np.int32)
+    st, xi, vrp, it, lam = O.dcm_mpc_solve_batch_warm(prob, threads=8, polished=pol)
+    st0, _, _, it0, _ = O.dcm_mpc_solve_batch_warm(prob, params=O.default_params(100, tol_polish=0.0),
+                                                   threads=8)
+    assert (st == 0).all() and (st0 == 0).all() and pol.all()
+    assert it.mean() < 0.7 * it0.mean(), (it.mean(), it0.mean())
+    for i in range(0, 96, 12):
+        xd, rd = certify(prob, i, xi[i], vrp[i])
+        assert np.abs(xd - xi[i]).max() < 1e-12 and np.abs(rd - vrp[i]).max() < 1e-12
+    # the polished multipliers: >= 0, zero off the active facets, complementary to the slacks
+    M = lam.shape[2]
+    used = np.arange(M)[None, None, :] < prob["nfacets"][:, :, None]
+    slack = prob["b"] - np.einsum("bkij,bkj->bki", prob["A"], vrp)
+    assert (lam[used] >= 0).all() and (lam[~used] == 0).all()
+    assert (np.abs(slack * lam)[used]).max() < 1e-12
+
+
+def test_dcm_mpc_polish_rejects_a_wrong_active_set():
+    """Rejected polishes leave the IPM iterate untouched: with tol_polish huge the first attempts
+    come before the active set is right, are refused by the certificate, and the solve still ends
+    at the same certified optimum."""
+    prob = O.assemble_constraints(P.make_batch(16, horizon=60, n_footsteps=4, seed=80))
+    pol = np.zeros(16, np.int32)
+    st, xi, vrp, it, _ = O.dcm_mpc_solve_batch_warm(prob, params=O.default_params(60, tol_polish=1e30),
+                                                    threads=4, polished=pol)
+    assert (st == 0).all() and pol.all() and (it >= 2).all()
+    for i in range(0, 16, 5):
+        xd, rd = certify(prob, i, xi[i], vrp[i])
+        assert np.abs(rd - vrp[i]).max() < 1e-12
 
 
 def test_dcm_mpc_unconstrained_is_lq_optimum():

@@ -39,8 +39,8 @@ def test_warm_start_same_optimum_fewer_iterations(oracle):
         # IPM's accuracy, so certify the warm solution against its own window's dense optimum
         for i in range(0, B, 16):
             xd, rd = dense_qp.certify(w, i, xi[i], vrp[i])
-            assert np.abs(rd - vrp[i]).max() < 1e-7
-            assert np.abs(xd - xi[i]).max() < 1e-7
+            assert np.abs(rd - vrp[i]).max() < 1e-12
+            assert np.abs(xd - xi[i]).max() < 1e-12
 
 
 def test_warm_start_multipliers_layout(oracle):

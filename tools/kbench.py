@@ -23,29 +23,39 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tol-polish", type=float, nargs="*", default=[None])
     args = ap.parse_args()
+    for tp in args.tol_polish:
+        run(args, tp)
+
+
+def run(args, tol_polish):
     h = native.Handle(0)
     prob = P.make_batch(args.batch, horizon=args.horizon, n_footsteps=6)
     d = {k: torch.from_numpy(prob[k]).cuda() for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
     A, b, nf = h.assemble_constraints(torch.from_numpy(prob["corners"]).cuda(),
                                       torch.from_numpy(prob["ncorners"]).cuda())
     d.update(A=A, b=b, nfacets=nf)
-    out = h.dcm_mpc_solve(d)
+    prm = native.default_params(args.horizon)
+    if tol_polish is not None:
+        prm.tol_polish = tol_polish
+    out = h.dcm_mpc_solve(d, params=prm)
     torch.cuda.synchronize()
     L = native.lib()
     stamps = getattr(L, "blf_debug_stamps", None) if hasattr(L, "blf_debug_stamps") else None
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 10)()
     if stamps is not None:
         stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         stamps(ctypes.cast(buf, ctypes.c_void_p), 1)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.reps):
-        h.dcm_mpc_solve(d, out=out)
+        h.dcm_mpc_solve(d, params=prm, out=out)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.reps
-    print(f"lib={native.LIB_PATH} batch={args.batch} N={args.horizon}: {ms:.3f} ms/solve, "
+    print(f"lib={native.LIB_PATH} batch={args.batch} N={args.horizon} tol_polish={prm.tol_polish:g}: "
+          f"{ms:.3f} ms/solve, polished {out['polished'].float().mean().item():.3f}, "
           f"{args.batch / ms * 1e3:.0f} QP/s, mean iters {out['iters'].float().mean().item():.2f}, "
           f"status!=0: {int((out['status'] != 0).sum())}")
     if stamps is not None:
@@ -56,8 +66,12 @@ def main():
               f"residuals {res / its:.0f}, W-phase {wph / its:.0f}, factor {fac / its:.0f}, "
               f"predictor solve {pred / its:.0f}, ratio+mu_aff+corr-rhs+corr-solve "
               f"{(sol - pred) / its:.0f}, step+update {step / its:.0f}, "
-              f"unaccounted {(tot - res - wph - fac - sol - step) / its:.0f} "
+              f"unaccounted {(tot - res - wph - fac - sol - step - buf[8]) / its:.0f} "
               f"(iters counted {its / 64 / args.reps:.2f})")
+        if buf[9]:
+            print(f"polish: {buf[9] / 64 / args.reps:.2f} attempts per QP, {buf[8] / buf[9]:.0f} cycles "
+                  f"per attempt; total per QP split: iterations {(tot - buf[8]) / 64 / args.reps:.0f}, "
+                  f"polish {buf[8] / 64 / args.reps:.0f}")
 
 if __name__ == "__main__":
     main()
