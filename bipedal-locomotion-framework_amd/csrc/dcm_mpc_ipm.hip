@@ -28,8 +28,9 @@ namespace {
 // Diagnostic build only (make stamps): per-phase cycle sums of thread 0 for the first 64 QPs.
 // [0] whole kernel, [1] factorization, [2] predictor solve .. corrector solve, [3] iterations,
 // [4] residuals + reduction, [5] W-phase, [6] predictor solve, [7] corrector step + update,
-// [8] polish attempts (cycles), [9] polish attempts (count).
-__device__ unsigned long long g_blf_stamps[10];
+// [8] polish attempts (cycles), [9] polish attempts (count), [10] load phase, [11] LQ start step,
+// [12] initial slacks / multipliers / dual residual.
+__device__ unsigned long long g_blf_stamps[16];
 #define STAMP(t) unsigned long long t = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, t0) \
     do { if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_blf_stamps[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
@@ -562,11 +563,11 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
 }
 
 // Solve the factored Newton system for the right-hand side g (oracle dcm_solve).  Returns
-// dr (the VRP step of this knot) and dx (the DCM step of xi_{k+1}).
+// dr (the VRP step of this knot), dx (the DCM step of xi_{k+1}) and v_{k+1} of the backward scan.
 template <int NW>
 __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, double* bnd, int nwa,
                                       int wv, int lane, bool own, double& dr0, double& dr1, double& dx0,
-                                      double& dx1)
+                                      double& dx1, double& vn0, double& vn1)
 {
     const double b2 = K.be * K.be;
     const double ab = K.al * K.be;
@@ -584,7 +585,6 @@ __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, doubl
         c0 = FD3(G00, y0, G01, y1, ab * Mg0);
         c1 = FD3(G10, y0, G11, y1, ab * Mg1);
     }
-    double vn0, vn1;
     scan_backward<NW>(G00, G01, G10, G11, c0, c1, bnd, nwa, wv, lane, vn0, vn1);
     double k0 = 0.0, k1 = 0.0, f0 = 0.0, f1 = 0.0;
     if (own) {
@@ -687,9 +687,18 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     }
     mmax = __builtin_amdgcn_readfirstlane(mmax);
     const bool any_bad = __syncthreads_or(bad);
+    STAMP_ADD(10, t_start);
 
-    // ---- initial point 1: rollout of vrp_ref, xi_{k+1} = alpha_k xi_k - beta_k r_k ----
-    {
+    // ---- initial point 1: a warm start rolls xi out from its VRPs, xi_{k+1} = alpha_k xi_k -
+    //      beta_k r_k; a cold start begins at xi = xi_ref (its LQ step is exact from any
+    //      trajectory) ----
+    if (!warm) {
+        if (own) {
+            K.x0 = xref[0];
+            K.x1 = xref[1];
+        }
+        publish_xi<NW>(K, bnd, wv, lane);
+    } else {
         double f0 = 0.0, f1 = 0.0;
         if (own) {
             if (k == 0) {
@@ -715,6 +724,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         bool ok, init_bad = false;
         // ---- initial point 2: full Newton step of the unconstrained QP (W = 0, lam = 0);
         //      a warm start skips it ----
+        STAMP(t_lq);
         if (!warm) {
             xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
             if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
@@ -722,7 +732,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             init_bad = __syncthreads_or(!ok);
             {
                 double dr0, dr1, dx0, dx1;
-                solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
+                double vn0, vn1;
+                solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1);
                 if (own) {
                     K.r0 = K.r0 + dr0;
                     K.r1 = K.r1 + dr1;
@@ -732,7 +743,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             }
             publish_xi<NW>(K, bnd, wv, lane);
         }
-        // ---- initial point 3: s = max(b - A r, 1e-2), lam = 1;
+        STAMP_ADD(11, t_lq);
+        STAMP(t_in);
+        // ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s;
         //      warm knots: s = max(b - A r, floor), lam = max(lam_warm, floor) ----
         if (own) {
             const double sfloor = ws ? P.ws_floor : 1e-2;
@@ -749,7 +762,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         const double l = lw[i];
                         K.lam[i] = l > sfloor ? l : sfloor;
                     } else {
-                        K.lam[i] = 1.0;
+                        K.lam[i] = 1e-2 / K.s[i];   // centred: s lam = 1e-2
                     }
                 }
             }
@@ -773,6 +786,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         }
         dres = R.nanmax_(dres);
         if (init_bad) status = BLF_QP_NUMERICAL;
+        STAMP_ADD(12, t_in);
 
         for (it = 0; status == 0; ++it) {
             // ---- residuals (knot-parallel) ----
@@ -794,7 +808,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 //      (primal, stationarity, multiplier signs) or undone ----
                 STAMP(t_p);
                 const double sr0 = K.r0, sr1 = K.r1, sx0 = K.x0, sx1 = K.x1;
-                int pc = 0, pi1 = 0, pi2 = 0;
+                int pc = 0, pi1 = 0, pi2 = 0, pk = 0;
                 double E00 = 0.0, E01 = 0.0, E11 = 0.0;
                 bool okp = true;
                 if (own) {
@@ -810,6 +824,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         }
                     }
                     okp = pc <= 2;
+                    pk = (pc < 3 ? pc : 2) | (pi1 << 2) | (pi2 << 5);
                     const double b2 = K.be * K.be;
                     if (pc == 0) {
                         E00 = b2 / P.Rw0;
@@ -840,6 +855,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
                 }
                 okp = riccati<NW>(K, P, E00, E01, E11, bnd, N, nwa, k, wv, lane, own) && okp;
+                pk = opaque(pk);
+                pc = pk & 3;
+                pi1 = (pk >> 2) & 7;
+                pi2 = (pk >> 5) & 7;
                 if (own) {
                     const double b2 = K.be * K.be;
                     const double B00 = fma(b2, K.P00, P.Rw0);
@@ -867,36 +886,26 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         K.h11 = 0.0;
                     }
                 }
+                double pl1 = 0.0, pl2 = 0.0;
                 {
-                    double dr0, dr1, dx0, dx1;
-                    solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
+                    // the Newton step; then the certificate: costates of the new point from the
+                    // solve, nu_k = P_{k+1} dxi_{k+1} + (qx_k + v_{k+1}) (oracle dcm_polish step 6)
+                    double dr0, dr1, dx0, dx1, vn0, vn1;
+                    solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1);
                     if (own) {
                         K.r0 = K.r0 + dr0;
                         K.r1 = K.r1 + dr1;
                         K.x0 = K.x0 + dx0;
                         K.x1 = K.x1 + dx1;
-                    }
-                }
-                publish_xi<NW>(K, bnd, wv, lane);
-                __syncthreads();
-                // certificate: costates of the polished trajectory by single shooting
-                double xn0, xn1, pl1 = 0.0, pl2 = 0.0;
-                xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xn0, xn1);
-                if (own) {
-                    double pd, cd;
-                    residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xn0, xn1, rref, xref, pd, cd);
-                }
-                {
-                    const double ga = own ? K.al : 0.0;
-                    const double c0 = own ? K.al * K.qx0 : 0.0, c1 = own ? K.al * K.qx1 : 0.0;
-                    double vn0, vn1;
-                    scan_backward<NW>(ga, 0.0, 0.0, ga, c0, c1, bnd, nwa, wv, lane, vn0, vn1);
-                    if (own) {
                         const int kx = opaque(k);
-                        const double nu0 = K.qx0 + vn0;
-                        const double nu1 = K.qx1 + vn1;
-                        const double g0 = fma(K.be, nu0, -K.rh0);
-                        const double g1 = fma(K.be, nu1, -K.rh1);
+                        const double s0 = K.qx0 + vn0;
+                        const double s1 = K.qx1 + vn1;
+                        const double nu0 = FD3(K.P00, dx0, K.P01, dx1, s0);
+                        const double nu1 = FD3(K.P01, dx0, K.P11, dx1, s1);
+                        const double rh0 = P.Rw0 * (K.r0 - rref[0]);
+                        const double rh1 = P.Rw1 * (K.r1 - rref[1]);
+                        const double g0 = fma(K.be, nu0, -rh0);
+                        const double g1 = fma(K.be, nu1, -rh1);
                         if (pc == 0) {
                             if (!(fabs(g0) <= P.tol_d) || !(fabs(g1) <= P.tol_d)) okp = false;
                         } else if (pc == 1) {
@@ -944,9 +953,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 K.r1 = sr1;
                 K.x0 = sx0;
                 K.x1 = sx1;
-                publish_xi<NW>(K, bnd, wv, lane);
-                __syncthreads();
-                if (own) {   // the iterate's gradient and defects again (the polish reused them)
+                // the iterate's gradient and defects again (the polish reused them); the wavefront
+                // boundary values were not touched, so xi_k comes back without a barrier
+                xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+                if (own) {
                     double pd, cd;
                     residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
                 }
@@ -1014,7 +1024,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             // ---- predictor ----
             STAMP(t_s);
             double dra0, dra1, dx0, dx1;
-            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dra0, dra1, dx0, dx1);
+            double vn0, vn1;
+            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dra0, dra1, dx0, dx1, vn0, vn1);
             STAMP_ADD(6, t_s);
             double q = 0.0;
             if (own) {
@@ -1082,7 +1093,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 }
             }
             double dr0, dr1;
-            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1);
+            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1);
             STAMP_ADD(2, t_s);
             STAMP(t_c);
             q = 0.0;
@@ -1190,11 +1201,11 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
 #ifdef BLF_STAMPS
 extern "C" int blf_debug_stamps(unsigned long long* out, int reset)
 {
-    unsigned long long h[10];
+    unsigned long long h[16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_blf_stamps), sizeof(h)) != hipSuccess) return -1;
-    for (int i = 0; i < 10; ++i) out[i] = h[i];
+    for (int i = 0; i < 16; ++i) out[i] = h[i];
     if (reset) {
-        unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_blf_stamps), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -55,7 +55,7 @@ class TimeVaryingDCMPlanner : public System::Advanceable<DCMPlanBatch>
     double m_footLength{0.12};
     double m_footWidth{0.09};
     bool m_warmStart{true};
-    double m_warmFloor{1e-2};
+    double m_warmFloor{1e-3};
     int m_start{0};
     std::vector<ContactPhaseList> m_plans;
     std::vector<double> m_xi0;       /**< [batch][2] */
@@ -95,7 +95,7 @@ public:
      * "foot_width", "dcm_weight", "vrp_weight", "terminal_weight" (scalar or 2-vector),
      * "tolerance" (tol_mu), "polish_tolerance" (tol_polish, default 1e-6; 0: interior point
      * only), "max_iterations" (int), "warm_start" (bool, default true), "warm_start_floor"
-     * (default 1e-2).
+     * (default 1e-3).
      */
     bool initialize(std::weak_ptr<ParametersHandler::IParametersHandler> handler);
 

@@ -187,7 +187,7 @@ typedef struct blf_dcm_mpc_solution {
  * (shift = 1 after the window moved one knot):
  *   r_k = vrp[k + shift],  s_i = max(b_i - a_i r_k, floor),  lambda_i = max(lambda[k + shift][i], floor)
  * and the cold start's LQ step is skipped.  Knots with k + shift >= N are new to the window and
- * start cold (r_k = vrp_ref_k, s_i = max(b_i - a_i r_k, 1e-2), lambda_i = 1).                 */
+ * start cold (r_k = vrp_ref_k, s_i = max(b_i - a_i r_k, 1e-2), lambda_i = 1e-2 / s_i).                 */
 typedef struct blf_dcm_mpc_warm_start {
     const double* vrp;       /* [B][N][2]  VRPs of the previous solve (must not alias the output) */
     const double* lambda;    /* [B][N][M]  its multipliers (blf_dcm_mpc_solve_warm's lambda_out)  */

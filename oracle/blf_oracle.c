@@ -860,19 +860,6 @@ static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
     *dl = -((li * (si + dsv)) * w->is[k * MF + i]);
 }
 
-/* Costates of the current trajectory by single shooting, nu_k = qx_k + alpha_k nu_{k+1} (backward
- * scan of v_k = alpha_k nu_{k+1}); needs dcm_residuals first.  Leaves v in w->v. */
-static void costate_scan(dcm_ws* w)
-{
-    for (int k = 0; k < w->N; ++k) {
-        double* G = w->sg + 4 * k;
-        G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
-        w->sc[2 * k] = w->al[k] * w->qx[2 * k];
-        w->sc[2 * k + 1] = w->al[k] * w->qx[2 * k + 1];
-    }
-    scan_backward(w, w->sg, w->sc);
-}
-
 /* Active-set polish ("Polish"; the kernel's polish block mirrors it term for term).
  * From an interior iterate, guess the active set (facet i of knot k is active iff lam_i > s_i; at
  * most two per knot), move each r_k onto its active lines, and take ONE Newton step of the
@@ -883,8 +870,8 @@ static void costate_scan(dcm_ws* w)
  * with B = R + beta^2 P_{k+1} — the W -> infinity limits of the barrier blocks.  The QP is
  * quadratic, so the step lands on the equality-constrained optimum up to rounding.  It is then
  * certified as the optimum of the inequality QP: every inactive facet satisfied (a r - b <= tol_p),
- * stationarity R (r - r_ref) + A_act^T lam = beta nu_{k+1} (costates by single shooting) solved
- * for the active multipliers with residual <= tol_d, and lam >= -tol_d.  Accepted: xi, vrp hold
+ * stationarity R (r - r_ref) + A_act^T lam = beta nu_k (the solve's costates of the new point)
+ * solved for the active multipliers with residual <= tol_d, and lam >= -tol_d.  Accepted: xi, vrp hold
  * the polished optimum, lam its multipliers (max(lam, 0) on the active facets, 0 on the others)
  * and 1 is returned.  Rejected: xi, vrp are restored, 0 is returned. */
 static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
@@ -978,14 +965,21 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
         w->xi[2 * (k + 1)] = w->xi[2 * (k + 1)] + w->x[2 * (k + 1)];
         w->xi[2 * (k + 1) + 1] = w->xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
     }
-    /* 6. certificate: primal feasibility, stationarity, dual feasibility (knot-parallel) */
-    dcm_residuals(w, 0);
-    costate_scan(w);
+    /* 6. certificate: primal feasibility, stationarity, dual feasibility (knot-parallel).  The
+     *    costates of the new point are the value-function gradients of the Riccati solve,
+     *    nu_k = P_{k+1} dxi_{k+1} + (qx_k + v_{k+1}) — through the closed loop, which contracts;
+     *    single shooting (nu_k = qx_k + alpha nu_{k+1}) would amplify rounding by alpha^N. */
     for (int k = 0; k < N; ++k) {
-        const double nu0 = w->qx[2 * k] + w->v[2 * (k + 1)];
-        const double nu1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
-        const double g0 = fma(w->be[k], nu0, -w->rh[2 * k]);
-        const double g1 = fma(w->be[k], nu1, -w->rh[2 * k + 1]);
+        const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
+        const double dx0 = w->x[2 * (k + 1)], dx1 = w->x[2 * (k + 1) + 1];
+        const double s0 = w->qx[2 * k] + w->v[2 * (k + 1)];
+        const double s1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
+        const double nu0 = FD3(P00, dx0, P01, dx1, s0);
+        const double nu1 = FD3(P01, dx0, P11, dx1, s1);
+        const double rh0 = w->Rw0 * (w->vrp[2 * k] - w->vrp_ref[2 * k]);
+        const double rh1 = w->Rw1 * (w->vrp[2 * k + 1] - w->vrp_ref[2 * k + 1]);
+        const double g0 = fma(w->be[k], nu0, -rh0);
+        const double g1 = fma(w->be[k], nu1, -rh1);
         const int c = pc[k];
         double l1 = 0.0, l2 = 0.0;
         if (c == 0) {
@@ -1086,23 +1080,28 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         vrp[2 * k + 1] = r0[2 * k + 1];
         for (int i = 0; i < MF; ++i) { w->s[k * MF + i] = 1.0; w->lam[k * MF + i] = 0.0; }
     }
-    /* ---- initial point 1: xi rolled out from vrp_ref by the affine forward scan
-     *      xi_{k+1} = alpha_k xi_k - beta_k r_k (xi_0 folded into knot 0's element) ---- */
-    for (int k = 0; k < N; ++k) {
-        double* G = w->sg + 4 * k;
-        G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
-        if (k == 0) {
-            w->sc[0] = fma(w->al[0], xi_init[0], -(w->be[0] * vrp[0]));
-            w->sc[1] = fma(w->al[0], xi_init[1], -(w->be[0] * vrp[1]));
-        } else {
-            w->sc[2 * k] = -(w->be[k] * vrp[2 * k]);
-            w->sc[2 * k + 1] = -(w->be[k] * vrp[2 * k + 1]);
-        }
-    }
-    scan_forward(w, w->sg, 0, w->sc);
+    /* ---- initial point 1: a warm start rolls xi out from its VRPs by the affine forward scan
+     *      xi_{k+1} = alpha_k xi_k - beta_k r_k (xi_0 folded into knot 0's element); a cold start
+     *      begins at xi = xi_ref (the LQ step below is exact from any trajectory) ---- */
     xi[0] = xi_init[0];
     xi[1] = xi_init[1];
-    for (int k = 1; k <= N; ++k) { xi[2 * k] = w->x[2 * k]; xi[2 * k + 1] = w->x[2 * k + 1]; }
+    if (warm) {
+        for (int k = 0; k < N; ++k) {
+            double* G = w->sg + 4 * k;
+            G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
+            if (k == 0) {
+                w->sc[0] = fma(w->al[0], xi_init[0], -(w->be[0] * vrp[0]));
+                w->sc[1] = fma(w->al[0], xi_init[1], -(w->be[0] * vrp[1]));
+            } else {
+                w->sc[2 * k] = -(w->be[k] * vrp[2 * k]);
+                w->sc[2 * k + 1] = -(w->be[k] * vrp[2 * k + 1]);
+            }
+        }
+        scan_forward(w, w->sg, 0, w->sc);
+        for (int k = 1; k <= N; ++k) { xi[2 * k] = w->x[2 * k]; xi[2 * k + 1] = w->x[2 * k + 1]; }
+    } else {
+        for (int k = 1; k <= N; ++k) { xi[2 * k] = xi_ref[2 * k]; xi[2 * k + 1] = xi_ref[2 * k + 1]; }
+    }
     if (status == 3) goto done;
     /* ---- initial point 2: one full Newton step of the QP without the polygon constraints
      *      (W = 0, lam = 0): the unconstrained LQ optimum.  For the unstable DCM the rollout is far
@@ -1125,7 +1124,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
         }
     }
-    /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1; warm: s = max(b - A r, floor),
+    /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s; warm: s = max(b - A r, floor),
      *      lam = max(lam_warm[src], floor) with the same source knot as the VRP ---- */
     for (int k = 0; k < N; ++k) {
         const int m = nfacets[k];
@@ -1140,7 +1139,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
                 const double lw = warm->lambda[(k + warm->shift) * M + i];
                 w->lam[k * MF + i] = lw > sfloor ? lw : sfloor;
             } else {
-                w->lam[k * MF + i] = 1.0;
+                w->lam[k * MF + i] = 1e-2 / w->s[k * MF + i];   /* centred: s lam = 1e-2 */
             }
         }
     }

@@ -148,10 +148,15 @@ def test_dcm_mpc_other_weights_and_iteration_cap(handle, oracle):
     kw = dict(w_xi=(10.0, 30.0), w_vrp=(2.0, 0.5), w_terminal=(100.0, 500.0), dt=0.015)
     _bitwise_vs_oracle(handle, oracle, host, native.default_params(60, **kw),
                        oracle.default_params(60, **kw))
-    # a cap below the iterations needed: MAX_ITER with iters == cap on both sides
-    st, it = _bitwise_vs_oracle(handle, oracle, host, native.default_params(60, max_iter=4),
-                                oracle.default_params(60, max_iter=4))
+    # a cap below the iterations needed: MAX_ITER with iters == cap on both sides (the interior
+    # point method alone, and with the polish, whose first successes come after 2 iterations)
+    st, it = _bitwise_vs_oracle(handle, oracle, host,
+                                native.default_params(60, max_iter=4, tol_polish=0.0),
+                                oracle.default_params(60, max_iter=4, tol_polish=0.0))
     assert (st == native.QP_MAX_ITER).all() and (it == 4).all()
+    st, it = _bitwise_vs_oracle(handle, oracle, host, native.default_params(60, max_iter=1),
+                                oracle.default_params(60, max_iter=1))
+    assert (st == native.QP_MAX_ITER).all() and (it == 1).all()
 
 
 def test_dcm_mpc_infeasible_and_nonfinite_inputs(handle, oracle):

@@ -43,7 +43,7 @@ def run(args, tol_polish):
     torch.cuda.synchronize()
     L = native.lib()
     stamps = getattr(L, "blf_debug_stamps", None) if hasattr(L, "blf_debug_stamps") else None
-    buf = (ctypes.c_ulonglong * 10)()
+    buf = (ctypes.c_ulonglong * 16)()
     if stamps is not None:
         stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         stamps(ctypes.cast(buf, ctypes.c_void_p), 1)
@@ -72,6 +72,9 @@ def run(args, tol_polish):
             print(f"polish: {buf[9] / 64 / args.reps:.2f} attempts per QP, {buf[8] / buf[9]:.0f} cycles "
                   f"per attempt; total per QP split: iterations {(tot - buf[8]) / 64 / args.reps:.0f}, "
                   f"polish {buf[8] / 64 / args.reps:.0f}")
+        q = 64 * args.reps
+        print(f"start-up per QP: loads {buf[10] / q:.0f}, LQ step {buf[11] / q:.0f}, "
+              f"slacks/multipliers/dual residual {buf[12] / q:.0f}")
 
 if __name__ == "__main__":
     main()
