@@ -53,11 +53,10 @@ struct KParams {
 //                       iteration (W-phase), overwritten by the corrector's multiplier step;
 //                       one address and one b128 read serve both
 //   bnd [NW][16]        per-wavefront boundary values (see the kB* slots)
-//   red [4][NW][2]      reduction scratch, four rotating slots (no second barrier needed)
+//   red [4][NW][4]      reduction scratch, four rotating slots (no second barrier needed)
 constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
 constexpr int kBV = 8;    // v_{64w} (2): backward-scan value at the first knot of wavefront w
 constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last knot of wavefront w
-constexpr int kBXi = 12;  // xi_{64w+64} (2): DCM past the last knot of wavefront w
 constexpr int kBnd = 16;
 struct Lds {
     double2 *A2, *BI;   // facet rows: normal (a_x, a_y); (b, 1/s), 1/s later the multiplier step
@@ -74,7 +73,7 @@ struct Lds {
         A2 = reinterpret_cast<double2*>(take(2 * (size_t)M * N));
         BI = reinterpret_cast<double2*>(take(2 * (size_t)M * N));
         bnd = take((size_t)kBnd * NW);
-        red = take(8 * (size_t)NW);
+        red = take(16 * (size_t)NW);
         flag = take(2);
         total = o;
     }
@@ -88,7 +87,7 @@ struct Reduce {
     double* red;
     int nwa;      // wavefronts that own knots (ceil(N/64)); the rest hold no data
     int slot = 0;
-    __device__ double* row() { double* r = red + 2 * NW * slot; slot = (slot + 1) & 3; return r; }
+    __device__ double* row() { double* r = red + 4 * NW * slot; slot = (slot + 1) & 3; return r; }
     __device__ void sum_nanmax(double& s, double& m)
     {
         s = wave_sum(s);
@@ -96,12 +95,41 @@ struct Reduce {
         if constexpr (NW > 1) {
             double* r = row();
             const int w = threadIdx.x >> 6;
-            if ((threadIdx.x & 63) == 0) { r[2 * w] = s; r[2 * w + 1] = m; }
+            if ((threadIdx.x & 63) == 0) { r[4 * w] = s; r[4 * w + 1] = m; }
             __syncthreads();
             s = r[0];
             m = r[1];
 #pragma unroll
-            for (int i = 1; i < NW; ++i) if (i < nwa) { s = s + r[2 * i]; m = nanmax(m, r[2 * i + 1]); }
+            for (int i = 1; i < NW; ++i) if (i < nwa) { s = s + r[4 * i]; m = nanmax(m, r[4 * i + 1]); }
+        }
+    }
+    // A step-length maximum and up to two sums in one exchange (one barrier).
+    template <int NS>
+    __device__ void max_sums(double& q, double& s1, double& s2)
+    {
+        q = wave_keepmax(q);
+        s1 = wave_sum(s1);
+        if constexpr (NS > 1) s2 = wave_sum(s2);
+        if constexpr (NW > 1) {
+            double* r = row();
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) {
+                r[4 * w] = q;
+                r[4 * w + 1] = s1;
+                if constexpr (NS > 1) r[4 * w + 2] = s2;
+            }
+            __syncthreads();
+            q = r[0];
+            s1 = r[1];
+            if constexpr (NS > 1) s2 = r[2];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) {
+                if (i < nwa) {
+                    q = ::blf::keepmax(q, r[4 * i]);
+                    s1 = s1 + r[4 * i + 1];
+                    if constexpr (NS > 1) s2 = s2 + r[4 * i + 2];
+                }
+            }
         }
     }
     __device__ double sum(double s)
@@ -110,11 +138,11 @@ struct Reduce {
         if constexpr (NW > 1) {
             double* r = row();
             const int w = threadIdx.x >> 6;
-            if ((threadIdx.x & 63) == 0) r[2 * w] = s;
+            if ((threadIdx.x & 63) == 0) r[4 * w] = s;
             __syncthreads();
             s = r[0];
 #pragma unroll
-            for (int i = 1; i < NW; ++i) if (i < nwa) s = s + r[2 * i];
+            for (int i = 1; i < NW; ++i) if (i < nwa) s = s + r[4 * i];
         }
         return s;
     }
@@ -124,11 +152,11 @@ struct Reduce {
         if constexpr (NW > 1) {
             double* r = row();
             const int w = threadIdx.x >> 6;
-            if ((threadIdx.x & 63) == 0) r[2 * w] = q;
+            if ((threadIdx.x & 63) == 0) r[4 * w] = q;
             __syncthreads();
             q = r[0];
 #pragma unroll
-            for (int i = 1; i < NW; ++i) if (i < nwa) q = ::blf::keepmax(q, r[2 * i]);
+            for (int i = 1; i < NW; ++i) if (i < nwa) q = ::blf::keepmax(q, r[4 * i]);
         }
         return q;
     }
@@ -138,11 +166,11 @@ struct Reduce {
         if constexpr (NW > 1) {
             double* r = row();
             const int w = threadIdx.x >> 6;
-            if ((threadIdx.x & 63) == 0) r[2 * w] = q;
+            if ((threadIdx.x & 63) == 0) r[4 * w] = q;
             __syncthreads();
             q = r[0];
 #pragma unroll
-            for (int i = 1; i < NW; ++i) if (i < nwa) q = nanmax(q, r[2 * i]);
+            for (int i = 1; i < NW; ++i) if (i < nwa) q = nanmax(q, r[4 * i]);
         }
         return q;
     }
@@ -367,20 +395,17 @@ __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P
     K.qx1 = q1 * (K.x1 - xref[1]);
 }
 
-// xi_k of this lane's knot (xi_{k+1} of the previous lane; lane 0: the boundary value).
-template <int NW>
-__device__ __forceinline__ void xi_prev(const Knot& K, const double* bnd, int wv, int lane,
-                                        double xi00, double xi01, double& xk0, double& xk1)
+// xi_k of this lane's knot: xi_{k+1} of the previous lane; lane 0 takes the wavefront's left boundary
+// xb = xi_{64 w}, which every wavefront tracks itself (from the forward scans' boundary values, with
+// the same arithmetic as the previous wavefront's last lane), so no barrier publishes it.
+__device__ __forceinline__ void xi_prev(const Knot& K, int lane, double xb0, double xb1, double& xk0,
+                                        double& xk1)
 {
     xk0 = __shfl_up(K.x0, 1, kWave);
     xk1 = __shfl_up(K.x1, 1, kWave);
     if (lane == 0) {
-        xk0 = xi00;
-        xk1 = xi01;
-        if (NW > 1 && wv > 0) {
-            xk0 = bnd[kBnd * (wv - 1) + kBXi];
-            xk1 = bnd[kBnd * (wv - 1) + kBXi + 1];
-        }
+        xk0 = xb0;
+        xk1 = xb1;
     }
 }
 
@@ -563,11 +588,12 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
 }
 
 // Solve the factored Newton system for the right-hand side g (oracle dcm_solve).  Returns
-// dr (the VRP step of this knot), dx (the DCM step of xi_{k+1}) and v_{k+1} of the backward scan.
+// dr (the VRP step of this knot), dx (the DCM step of xi_{k+1}), v_{k+1} of the backward scan and
+// the DCM step of xi_k (lane 0 of a wavefront: its left boundary, from the previous wavefront).
 template <int NW>
 __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, double* bnd, int nwa,
                                       int wv, int lane, bool own, double& dr0, double& dr1, double& dx0,
-                                      double& dx1, double& vn0, double& vn1)
+                                      double& dx1, double& vn0, double& vn1, double& xk0, double& xk1)
 {
     const double b2 = K.be * K.be;
     const double ab = K.al * K.be;
@@ -597,23 +623,10 @@ __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, doubl
         f0 = fma(-K.be, k0, K.d0);
         f1 = fma(-K.be, k1, K.d1);
     }
-    double xk0, xk1;
     scan_forward<NW>(G00, G10, G01, G11, f0, f1, bnd, nwa, wv, lane, dx0, dx1, xk0, xk1);
     const Mmat Mm(K);
     dr0 = fma(ab, FD2(Mm.m00, xk0, Mm.m10, xk1), k0);
     dr1 = fma(ab, FD2(Mm.m01, xk0, Mm.m11, xk1), k1);
-}
-
-// Publishes xi_{k+1} of lane 63 for the next wavefront's lane 0 (read after the next barrier).
-template <int NW>
-__device__ __forceinline__ void publish_xi(const Knot& K, double* bnd, int wv, int lane)
-{
-    if constexpr (NW > 1) {
-        if (lane == kWave - 1) {
-            bnd[kBnd * wv + kBXi] = K.x0;
-            bnd[kBnd * wv + kBXi + 1] = K.x1;
-        }
-    }
 }
 
 #ifndef BLF_MIN_WAVES
@@ -692,12 +705,17 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     // ---- initial point 1: a warm start rolls xi out from its VRPs, xi_{k+1} = alpha_k xi_k -
     //      beta_k r_k; a cold start begins at xi = xi_ref (its LQ step is exact from any
     //      trajectory) ----
+    // xb = xi_{64 wv}, the left boundary of this wavefront (lane 0 uses it; wavefront 0: xi_init)
+    double xb0 = xi00, xb1 = xi01;
     if (!warm) {
         if (own) {
             K.x0 = xref[0];
             K.x1 = xref[1];
+            if (wv > 0) {   // xi_ref_{64 wv}: the previous wavefront's last xi_{k+1}
+                xb0 = xref[-2];
+                xb1 = xref[-1];
+            }
         }
-        publish_xi<NW>(K, bnd, wv, lane);
     } else {
         double f0 = 0.0, f1 = 0.0;
         if (own) {
@@ -712,9 +730,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         const double ga = own ? K.al : 0.0;
         double xk0, xk1;
         scan_forward<NW>(ga, 0.0, 0.0, ga, f0, f1, bnd, nwa, wv, lane, K.x0, K.x1, xk0, xk1);
-        publish_xi<NW>(K, bnd, wv, lane);
+        if (wv > 0) {
+            xb0 = xk0;
+            xb1 = xk1;
+        }
     }
-    __syncthreads();
 
     int status = 0, it = 0, polished = 0;
     if (any_bad) {
@@ -726,22 +746,25 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         //      a warm start skips it ----
         STAMP(t_lq);
         if (!warm) {
-            xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+            xi_prev(K, lane, xb0, xb1, xk0, xk1);
             if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
             ok = factor<NW>(K, P, 0.0, 0.0, 0.0, 0.0, bnd, N, nwa, k, wv, lane, own);
             init_bad = __syncthreads_or(!ok);
             {
-                double dr0, dr1, dx0, dx1;
-                double vn0, vn1;
-                solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1);
+                double dr0, dr1, dx0, dx1, vn0, vn1, dxk0, dxk1;
+                solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1, dxk0,
+                          dxk1);
                 if (own) {
                     K.r0 = K.r0 + dr0;
                     K.r1 = K.r1 + dr1;
                     K.x0 = K.x0 + dx0;
                     K.x1 = K.x1 + dx1;
                 }
+                if (wv > 0) {
+                    xb0 = xb0 + dxk0;
+                    xb1 = xb1 + dxk1;
+                }
             }
-            publish_xi<NW>(K, bnd, wv, lane);
         }
         STAMP_ADD(11, t_lq);
         STAMP(t_in);
@@ -768,9 +791,15 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             }
         }
         const int ntot = (int)R.sum((double)K.m);   // exact: small integers
-        // ---- initial dual residual: costates nu_k = qx_k + alpha_k nu_{k+1} (backward scan) ----
-        xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+        // ---- initial mu, primal residual and dual residual (costates nu_k = qx_k + alpha_k
+        //      nu_{k+1}, backward scan); afterwards every step updates them (oracle: mu, pres and
+        //      dres are known at the top of every iteration) ----
+        xi_prev(K, lane, xb0, xb1, xk0, xk1);
+        pres = 0.0;
+        ck = 0.0;
         if (own) residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+        R.sum_nanmax(ck, pres);
+        double mu = ntot > 0 ? ck / (double)ntot : 0.0;
         double dres = 0.0;
         {
             const double ga = own ? K.al : 0.0;
@@ -791,12 +820,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         for (it = 0; status == 0; ++it) {
             // ---- residuals (knot-parallel) ----
             STAMP(t_r);
-            xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
-            pres = 0.0;
-            ck = 0.0;
-            if (own) residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
-            R.sum_nanmax(ck, pres);
-            const double mu = ntot > 0 ? ck / (double)ntot : 0.0;
+            xi_prev(K, lane, xb0, xb1, xk0, xk1);
+            if (it > 0 && own) {
+                double pd, cd;
+                residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
+            }
             if (!(mu == mu) || !(pres == pres) || !(dres == dres) || __builtin_isinf(mu)) {
                 status = BLF_QP_NUMERICAL;
                 break;
@@ -890,8 +918,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 {
                     // the Newton step; then the certificate: costates of the new point from the
                     // solve, nu_k = P_{k+1} dxi_{k+1} + (qx_k + v_{k+1}) (oracle dcm_polish step 6)
-                    double dr0, dr1, dx0, dx1, vn0, vn1;
-                    solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1);
+                    double dr0, dr1, dx0, dx1, vn0, vn1, dxk0, dxk1;
+                    solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1,
+                              dxk0, dxk1);
                     if (own) {
                         K.r0 = K.r0 + dr0;
                         K.r1 = K.r1 + dr1;
@@ -955,7 +984,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 K.x1 = sx1;
                 // the iterate's gradient and defects again (the polish reused them); the wavefront
                 // boundary values were not touched, so xi_k comes back without a barrier
-                xi_prev<NW>(K, bnd, wv, lane, xi00, xi01, xk0, xk1);
+                xi_prev(K, lane, xb0, xb1, xk0, xk1);
                 if (own) {
                     double pd, cd;
                     residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
@@ -1015,19 +1044,16 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             STAMP_ADD(5, t_w);
             STAMP(t_f);
             ok = factor<NW>(K, P, W00, W01, W11, dW, bnd, N, nwa, k, wv, lane, own);
-            if (__syncthreads_or(!ok)) {
-                status = BLF_QP_NUMERICAL;
-                break;
-            }
             STAMP_ADD(1, t_f);
 
             // ---- predictor ----
             STAMP(t_s);
-            double dra0, dra1, dx0, dx1;
-            double vn0, vn1;
-            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dra0, dra1, dx0, dx1, vn0, vn1);
+            double dra0, dra1, dx0, dx1, vn0, vn1, dxk0, dxk1;
+            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dra0, dra1, dx0, dx1, vn0, vn1, dxk0, dxk1);
             STAMP_ADD(6, t_s);
-            double q = 0.0;
+            // affine ratio test with U0 = sum s lam and U2 = sum ds dl in the same exchange:
+            // mu_aff = ((1 - a) U0 + a^2 U2) / ntot; a failed factorization votes through U0 = NaN
+            double q = 0.0, u0 = 0.0, u2 = 0.0;
             if (own) {
                 const int kx = opaque(k);
                 const int km = opaque(K.m), mm = opaque_s(mmax);
@@ -1040,28 +1066,19 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         affine_step(K, L.A2[i * N + kx], L.BI[i * N + kx].x, is, i, dra0, dra1, ds, dl);
                         if (ds < 0.0) q = keepmax(q, (-ds) * is);
                         if (dl < 0.0) q = keepmax(q, (K.s[i] + ds) * is);
+                        u0 = fma(K.s[i], K.lam[i], u0);
+                        u2 = fma(ds, dl, u2);
                     }
                 }
             }
-            const double qa = R.keepmax(q);
-            const double a_aff = qa > 1.0 ? 1.0 / qa : 1.0;
-            ck = 0.0;
-            if (own) {
-                const int kx = opaque(k);
-                const int km = opaque(K.m), mm = opaque_s(mmax);
-#pragma unroll
-                for (int i = 0; i < kMaxFacets; ++i) {
-                    if (i >= mm) break;
-                    if (i < km) {
-                        double ds, dl;
-                        affine_step(K, L.A2[i * N + kx], L.BI[i * N + kx].x, L.BI[i * N + kx].y, i, dra0,
-                                    dra1, ds, dl);
-                        ck = fma(fma(a_aff, ds, K.s[i]), fma(a_aff, dl, K.lam[i]), ck);
-                    }
-                }
+            if (!ok) u0 = __builtin_nan("");
+            R.template max_sums<2>(q, u0, u2);
+            if (!(u0 == u0) || !(u2 == u2)) {
+                status = BLF_QP_NUMERICAL;
+                break;
             }
-            const double caff = R.sum(ck);
-            const double mu_aff = ntot > 0 ? caff / (double)ntot : 0.0;
+            const double a_aff = q > 1.0 ? 1.0 / q : 1.0;
+            const double mu_aff = ntot > 0 ? fma(a_aff * a_aff, u2, (1.0 - a_aff) * u0) / (double)ntot : 0.0;
             double sigma = 0.0;
             if (mu > 0.0) {
                 const double qq = mu_aff / mu;
@@ -1093,10 +1110,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 }
             }
             double dr0, dr1;
-            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1);
+            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1, dxk0, dxk1);
             STAMP_ADD(2, t_s);
             STAMP(t_c);
             q = 0.0;
+            double t2 = 0.0;
             if (own) {
                 const int kx = opaque(k);
                 const int km = opaque(K.m), mm = opaque_s(mmax);
@@ -1116,11 +1134,12 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         if (ds < 0.0) q = keepmax(q, (-ds) * is);
                         if (dl < 0.0) q = keepmax(q, (-dl) / K.lam[i]);
                         L.BI[i * N + kx].y = dl;   // 1/s is dead now: keep the multiplier step
+                        t2 = fma(ds, dl, t2);
                     }
                 }
             }
-            const double qc = R.keepmax(q);
-            const double step = qc > 0.0 ? 0.99 / qc : 1.0;
+            R.template max_sums<1>(q, t2, t2);
+            const double step = q > 0.0 ? 0.99 / q : 1.0;
             const double a = step < 1.0 ? step : 1.0;
             if (own) {
                 const int kx = opaque(k);
@@ -1140,9 +1159,17 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 K.x0 = fma(a, dx0, K.x0);
                 K.x1 = fma(a, dx1, K.x1);
             }
-            publish_xi<NW>(K, bnd, wv, lane);
+            if (wv > 0) {   // the same update as the previous wavefront's last lane
+                xb0 = fma(a, dxk0, xb0);
+                xb1 = fma(a, dxk1, xb1);
+            }
             dres = dres * (1.0 - a);
-            __syncthreads();
+            pres = pres * (1.0 - a);
+            // sum (s + a ds)(lam + a dl) = U0 + a T1 + a^2 T2, T1 = -sum rc = -(U0 + U2 - ntot sigma mu)
+            if (ntot > 0) {
+                const double nt = (double)ntot;
+                mu = fma(a * a, t2, fma(a, fma(nt, sigma_mu, -u2), (1.0 - a) * u0)) / nt;
+            }
             STAMP_ADD(7, t_c);
         }
     }

@@ -1147,7 +1147,8 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      *      (backward scan of v_k = alpha_k nu_{k+1}); it then contracts by (1 - a) with every
      *      Newton step (the QP's linear residuals) ---- */
     double dres = 0.0;
-    dcm_residuals(w, 1);
+    double pres = dcm_residuals(w, 1);
+    double mu = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
     for (int k = 0; k < N; ++k) {
         double* G = w->sg + 4 * k;
         G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
@@ -1163,9 +1164,12 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     }
     if (status == 2) goto done;
 
+    /* mu, pres and dres are known at the top of every iteration without a reduction there: the
+     * start computes them, and each step updates them from sums gathered with the step-length
+     * maxima (mu: the exact quadratic in the step length; pres, dres: the linear residuals of an
+     * exact Newton step contract by (1 - a)) */
     for (it = 0;; ++it) {
-        const double pres = dcm_residuals(w, 1);
-        const double mu = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
+        if (it > 0) dcm_residuals(w, 1);   /* the iterate's gradient, defects, Q (xi - xi_ref) */
         if (!(mu == mu) || !(pres == pres) || !(dres == dres) || isinf(mu)) { status = 2; break; }
         if (prm->tol_polish > 0.0 && mu <= prm->tol_polish) {
             if (dcm_polish(w, prm->tol_primal, prm->tol_dual)) { polished = 1; status = 0; break; }
@@ -1175,35 +1179,34 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         if (it >= prm->max_iter) { status = 1; break; }
 
         dcm_wphase(w);
-        if (!dcm_factor(w)) { status = 2; break; }
+        const int fok = dcm_factor(w);
 
         /* ---- predictor ---- */
         dcm_solve(w);
+        /* affine ratio test with the complementarity sums U0 = sum s lam, U2 = sum ds dl: then
+         * mu_aff = ((1 - a) U0 + a^2 U2) / ntot, since s dl + lam ds = -s lam for this step */
         double qmax = 0.0;
         for (int k = 0; k < N; ++k) {
             w->dra[2 * k] = w->dr[2 * k];
             w->dra[2 * k + 1] = w->dr[2 * k + 1];
             const int m = nfacets[k];
+            double u0 = 0.0, u2 = 0.0;
             for (int i = 0; i < m; ++i) {
                 double ds, dl;
                 affine_step(w, k, i, &ds, &dl);
                 const double is = w->is[k * MF + i];
                 if (ds < 0.0) qmax = keepmax(qmax, (-ds) * is);
                 if (dl < 0.0) qmax = keepmax(qmax, (w->s[k * MF + i] + ds) * is);
+                u0 = fma(w->s[k * MF + i], w->lam[k * MF + i], u0);
+                u2 = fma(ds, dl, u2);
             }
+            w->c[k] = u0;
+            w->q[k] = u2;
         }
+        const double U0 = orc_wave_tree_sum(w->c, N), U2 = orc_wave_tree_sum(w->q, N);
+        if (!fok || !(U0 == U0) || !(U2 == U2)) { status = 2; break; }
         const double a_aff = qmax > 1.0 ? 1.0 / qmax : 1.0;
-        for (int k = 0; k < N; ++k) {
-            const int m = nfacets[k];
-            double ck = 0.0;
-            for (int i = 0; i < m; ++i) {
-                double ds, dl;
-                affine_step(w, k, i, &ds, &dl);
-                ck = fma(fma(a_aff, ds, w->s[k * MF + i]), fma(a_aff, dl, w->lam[k * MF + i]), ck);
-            }
-            w->c[k] = ck;
-        }
-        const double mu_aff = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
+        const double mu_aff = ntot > 0 ? fma(a_aff * a_aff, U2, (1.0 - a_aff) * U0) / (double)ntot : 0.0;
         double sigma = 0.0;
         if (mu > 0.0) {
             const double qq = mu_aff / mu;
@@ -1235,6 +1238,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         for (int k = 0; k < N; ++k) {
             const int m = nfacets[k];
             const double r0 = vrp[2 * k], r1 = vrp[2 * k + 1];
+            double t2 = 0.0;
             for (int i = 0; i < m; ++i) {
                 const double* a = Ain + (k * M + i) * 2;
                 const double si = w->s[k * MF + i], li = w->lam[k * MF + i];
@@ -1248,8 +1252,11 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
                 if (dl < 0.0) qmax = keepmax(qmax, (-dl) / li);
                 w->cds[k * MF + i] = ds;
                 w->cdl[k * MF + i] = dl;
+                t2 = fma(ds, dl, t2);
             }
+            w->q[k] = t2;
         }
+        const double T2 = orc_wave_tree_sum(w->q, N);
         const double step = qmax > 0.0 ? 0.99 / qmax : 1.0;
         const double a = step < 1.0 ? step : 1.0;
         for (int k = 0; k < N; ++k) {
@@ -1264,6 +1271,13 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             }
         }
         dres = dres * (1.0 - a);
+        pres = pres * (1.0 - a);
+        /* sum (s + a ds)(lam + a dl) = U0 + a T1 + a^2 T2 with T1 = sum (s dl + lam ds) = -sum rc
+         * = -(U0 + U2 - ntot sigma mu) for the corrector step */
+        if (ntot > 0) {
+            const double nt = (double)ntot;
+            mu = fma(a * a, T2, fma(a, fma(nt, sigma_mu, -U2), (1.0 - a) * U0)) / nt;
+        }
     }
 done:
     if (iters_out) *iters_out = it;
