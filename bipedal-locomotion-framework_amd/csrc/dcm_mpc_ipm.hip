@@ -103,6 +103,38 @@ struct Reduce {
             for (int i = 1; i < NW; ++i) if (i < nwa) { s = s + r[4 * i]; m = nanmax(m, r[4 * i + 1]); }
         }
     }
+    // Two sums and two NaN-propagating maxima in one exchange (the start-up statistics).
+    __device__ void sums_nanmaxes(double& s1, double& s2, double& m1, double& m2)
+    {
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        m1 = wave_nanmax(m1);
+        m2 = wave_nanmax(m2);
+        if constexpr (NW > 1) {
+            double* r = row();
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) {
+                r[4 * w] = s1;
+                r[4 * w + 1] = s2;
+                r[4 * w + 2] = m1;
+                r[4 * w + 3] = m2;
+            }
+            __syncthreads();
+            s1 = r[0];
+            s2 = r[1];
+            m1 = r[2];
+            m2 = r[3];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) {
+                if (i < nwa) {
+                    s1 = s1 + r[4 * i];
+                    s2 = s2 + r[4 * i + 1];
+                    m1 = nanmax(m1, r[4 * i + 2]);
+                    m2 = nanmax(m2, r[4 * i + 3]);
+                }
+            }
+        }
+    }
     // A step-length maximum and up to two sums in one exchange (one barrier).
     template <int NS>
     __device__ void max_sums(double& q, double& s1, double& s2)
@@ -770,9 +802,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         STAMP(t_in);
         // ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s;
         //      warm knots: s = max(b - A r, floor), lam = max(lam_warm, floor) ----
+        double dres = 0.0;
         if (own) {
             const double sfloor = ws ? P.ws_floor : 1e-2;
             const double* lw = ws_lam + (ws ? (p * N + k + P.ws_shift) * M : 0);
+            double al0 = 0.0, al1 = 0.0;   // A^T lam
 #pragma unroll
             for (int i = 0; i < kMaxFacets; ++i) {
                 if (i >= mmax) break;
@@ -787,21 +821,24 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     } else {
                         K.lam[i] = 1e-2 / K.s[i];   // centred: s lam = 1e-2
                     }
+                    al0 = fma(a.x, K.lam[i], al0);
+                    al1 = fma(a.y, K.lam[i], al1);
                 }
             }
+            // a cold start sits at the unconstrained optimum, R (r - r_ref) = beta nu: its dual
+            // residual is A^T lam exactly (single-shooting costates would only add rounding
+            // amplified by alpha^N)
+            if (!warm) dres = nanmax(nanmax(0.0, fabs(al0)), fabs(al1));
         }
-        const int ntot = (int)R.sum((double)K.m);   // exact: small integers
-        // ---- initial mu, primal residual and dual residual (costates nu_k = qx_k + alpha_k
-        //      nu_{k+1}, backward scan); afterwards every step updates them (oracle: mu, pres and
-        //      dres are known at the top of every iteration) ----
+        // ---- initial mu, primal residual and dual residual (warm start: costates nu_k = qx_k +
+        //      alpha_k nu_{k+1} by a backward scan), in one reduction with the facet count;
+        //      afterwards every step updates them (mu, pres and dres are known at the top of
+        //      every iteration) ----
         xi_prev(K, lane, xb0, xb1, xk0, xk1);
         pres = 0.0;
         ck = 0.0;
         if (own) residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
-        R.sum_nanmax(ck, pres);
-        double mu = ntot > 0 ? ck / (double)ntot : 0.0;
-        double dres = 0.0;
-        {
+        if (warm) {
             const double ga = own ? K.al : 0.0;
             const double c0 = own ? K.al * K.qx0 : 0.0, c1 = own ? K.al * K.qx1 : 0.0;
             double vn0, vn1;
@@ -813,7 +850,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 dres = nanmax(dres, fabs(fma(-K.be, nu1, K.rh1)));
             }
         }
-        dres = R.nanmax_(dres);
+        double mcount = (double)K.m;
+        R.sums_nanmaxes(mcount, ck, pres, dres);
+        const int ntot = (int)mcount;   // exact: small integers
+        double mu = ntot > 0 ? ck / (double)ntot : 0.0;
         if (init_bad) status = BLF_QP_NUMERICAL;
         STAMP_ADD(12, t_in);
 

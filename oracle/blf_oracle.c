@@ -1126,10 +1126,12 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     }
     /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s; warm: s = max(b - A r, floor),
      *      lam = max(lam_warm[src], floor) with the same source knot as the VRP ---- */
+    double dres = 0.0;
     for (int k = 0; k < N; ++k) {
         const int m = nfacets[k];
         const int ws = warm && k + warm->shift < N;
         const double sfloor = ws ? warm->floor : 1e-2;
+        double al0 = 0.0, al1 = 0.0;   /* A^T lam */
         for (int i = 0; i < m; ++i) {
             const double* a = Ain + (k * M + i) * 2;
             const double gr = FD2(a[0], vrp[2 * k], a[1], vrp[2 * k + 1]);
@@ -1141,26 +1143,32 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             } else {
                 w->lam[k * MF + i] = 1e-2 / w->s[k * MF + i];   /* centred: s lam = 1e-2 */
             }
+            al0 = fma(a[0], w->lam[k * MF + i], al0);
+            al1 = fma(a[1], w->lam[k * MF + i], al1);
         }
+        /* a cold start sits at the unconstrained optimum, R (r - r_ref) = beta nu: its dual
+         * residual is A^T lam exactly */
+        if (!warm) dres = nanmax(dres, nanmax(nanmax(0.0, fabs(al0)), fabs(al1)));
     }
-    /* ---- initial dual residual with single-shooting costates nu_k = qx_k + alpha_k nu_{k+1}
-     *      (backward scan of v_k = alpha_k nu_{k+1}); it then contracts by (1 - a) with every
-     *      Newton step (the QP's linear residuals) ---- */
-    double dres = 0.0;
+    /* ---- initial mu, primal residual, dual residual (a warm start: single-shooting costates
+     *      nu_k = qx_k + alpha_k nu_{k+1}, backward scan of v_k = alpha_k nu_{k+1}); each step then
+     *      carries them (the QP's linear residuals contract by (1 - a)) ---- */
     double pres = dcm_residuals(w, 1);
     double mu = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
-    for (int k = 0; k < N; ++k) {
-        double* G = w->sg + 4 * k;
-        G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
-        w->sc[2 * k] = w->al[k] * w->qx[2 * k];
-        w->sc[2 * k + 1] = w->al[k] * w->qx[2 * k + 1];
-    }
-    scan_backward(w, w->sg, w->sc);
-    for (int k = 0; k < N; ++k) {
-        const double nu0 = w->qx[2 * k] + w->v[2 * (k + 1)];
-        const double nu1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
-        dres = nanmax(dres, fabs(fma(-w->be[k], nu0, w->rh[2 * k])));
-        dres = nanmax(dres, fabs(fma(-w->be[k], nu1, w->rh[2 * k + 1])));
+    if (warm) {
+        for (int k = 0; k < N; ++k) {
+            double* G = w->sg + 4 * k;
+            G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
+            w->sc[2 * k] = w->al[k] * w->qx[2 * k];
+            w->sc[2 * k + 1] = w->al[k] * w->qx[2 * k + 1];
+        }
+        scan_backward(w, w->sg, w->sc);
+        for (int k = 0; k < N; ++k) {
+            const double nu0 = w->qx[2 * k] + w->v[2 * (k + 1)];
+            const double nu1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
+            dres = nanmax(dres, fabs(fma(-w->be[k], nu0, w->rh[2 * k])));
+            dres = nanmax(dres, fabs(fma(-w->be[k], nu1, w->rh[2 * k + 1])));
+        }
     }
     if (status == 2) goto done;
 
