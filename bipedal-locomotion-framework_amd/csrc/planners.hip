@@ -4,8 +4,9 @@
 //  * hull2d_kernel: one lane per polygon (ConvexHullHelper::buildConvexHull + getA/getB,
 //    src/Planners/src/ConvexHullHelper.cpp:35-99).  The workgroup's contiguous slab of input
 //    points is loaded coalesced and transposed into lane-minor LDS arrays; each lane then sorts
-//    its points in place (insertion sort, p <= 16) and runs Andrew's monotone chain with a
-//    `cross <= 0` pop, which merges collinear boundary points the way Qhull's "Qt" facet merge
+//    its points in place (a sorting network for p <= 8 finite points, else insertion sort) and
+//    runs Andrew's monotone chain with a `cross <= 0` pop (chain stack packed in a register for
+//    P <= 8), which merges collinear boundary points the way Qhull's "Qt" facet merge
 //    does.  The facets are then computed and stored by (polygon, facet) pair, coalesced.  Output rows: unit outward normal,
 //    b = n . v (inside: A x <= b), counter-clockwise from the leftmost-lowest vertex.
 //  * hull2d_contains_kernel: doesPointBelongToConvexHull (ConvexHullHelper.cpp:101-117): strict
@@ -31,10 +32,18 @@ __device__ __forceinline__ double cross3(double ox, double oy, double ax, double
 // Dynamic LDS of hull2d_kernel, per workgroup of 64 polygons (one per lane), lane-minor so that
 // the data-dependent indices of the sort and the chain never conflict:
 //   X, Y   [P][64] doubles: the polygon's points, sorted in place by the lane
-//   stack  [2P+2][64] int32: the monotone chain, as positions in the sorted arrays
+//   stack  P <= 8: [64] uint64, the monotone chain packed 3 bits per entry (at most 2P + 2 = 18
+//          entries), held in a register while the chain runs;
+//          P > 8: [2P+2][64] int32, the chain as positions in the sorted arrays
 //   nf     [64] int32
+// The packed stack frees 4 KB per workgroup (8.8 KB instead of 12.8 KB at P = 8): LDS is what
+// bounds the resident wavefronts of this latency-bound kernel.
+__host__ __device__ inline bool hull2d_packed(int P) { return P <= 8; }
 __host__ __device__ inline size_t hull2d_lds_bytes(int P, int /*M*/)
 {
+    if (hull2d_packed(P))
+        return sizeof(double) * kHullBlock * 2 * P + sizeof(uint64_t) * kHullBlock +
+               sizeof(int32_t) * kHullBlock;
     return sizeof(double) * kHullBlock * 2 * P + sizeof(int32_t) * kHullBlock * (2 * P + 3);
 }
 
@@ -48,6 +57,7 @@ __device__ __forceinline__ int hull2d_rows(int64_t batch, int64_t p0)
 // Andrew's monotone chain with the top two stack points held in registers (LDS is read only on a
 // pop).  Phase 2 (after a barrier): consecutive threads take consecutive (polygon, facet) pairs,
 // compute the facet once and store A as 16-B and b as 8-B coalesced writes.
+template <bool PK>
 __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __restrict__ pts,
                                                             const int32_t* __restrict__ npts,
                                                             int32_t P, int32_t M, int64_t batch,
@@ -61,8 +71,9 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     const int nprob = hull2d_rows(batch, p0);
     double* s_x = hull_smem;                                               // [P][64]
     double* s_y = s_x + kHullBlock * P;                                    // [P][64]
-    int32_t* s_stk = reinterpret_cast<int32_t*>(s_y + kHullBlock * P);     // [2P+2][64]
-    int32_t* s_nf = s_stk + kHullBlock * (2 * P + 2);                      // [64]
+    int32_t* s_stk = reinterpret_cast<int32_t*>(s_y + kHullBlock * P);     // [2P+2][64] (!PK)
+    uint64_t* s_pk = reinterpret_cast<uint64_t*>(s_y + kHullBlock * P);    // [64] (PK)
+    int32_t* s_nf = PK ? reinterpret_cast<int32_t*>(s_pk + kHullBlock) : s_stk + kHullBlock * (2 * P + 2);
     {
         // coalesced load of the [64][P][2] slab, transposed into X / Y (8 loads per lane in flight)
         const double* src = pts + p0 * 2 * P;
@@ -88,7 +99,14 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     __syncthreads();
 #define HX(i) s_x[(i) * kHullBlock + t]
 #define HY(i) s_y[(i) * kHullBlock + t]
-#define STK(i) s_stk[(i) * kHullBlock + t]
+    // the chain stack: packed 3-bit entries in a register (PK), else lane-minor int32 in LDS
+    uint64_t stk = 0;
+#define STK_GET(i) (PK ? (int)((stk >> (3 * (i))) & 7) : s_stk[(i) * kHullBlock + t])
+#define STK_SET(i, v)                                                                           \
+    do {                                                                                        \
+        if (PK) stk = (stk & ~(7ull << (3 * (i)))) | ((uint64_t)(v) << (3 * (i)));              \
+        else s_stk[(i) * kHullBlock + t] = (v);                                                 \
+    } while (0)
     const int n = t < nprob ? npts[p0 + t] : 0;
     int nf = -1;
     if (t < nprob && n >= 3 && n <= P) {
@@ -159,7 +177,7 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                     bx = ax;
                     by = ay;
                     if (k >= 2) {
-                        const int a = STK(k - 2);
+                        const int a = STK_GET(k - 2);
                         ax = HX(a);
                         ay = HY(a);
                     }
@@ -167,7 +185,8 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                     break;
                 }
             }
-            STK(k++) = i;
+            STK_SET(k, i);
+            ++k;
             ax = bx;
             ay = by;
             bx = px;
@@ -182,7 +201,7 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                     bx = ax;
                     by = ay;
                     if (k >= 2) {
-                        const int a = STK(k - 2);
+                        const int a = STK_GET(k - 2);
                         ax = HX(a);
                         ay = HY(a);
                     }
@@ -190,7 +209,8 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                     break;
                 }
             }
-            STK(k++) = i;
+            STK_SET(k, i);
+            ++k;
             ax = bx;
             ay = by;
             bx = px;
@@ -201,10 +221,12 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     }
 #undef HX
 #undef HY
-#undef STK
+#undef STK_GET
+#undef STK_SET
     if (t < nprob) {
         s_nf[t] = nf;
         nfout[p0 + t] = nf;
+        if (PK) s_pk[t] = stk;
     }
     __syncthreads();
     // phase 2: (polygon r, facet j) pairs in output order
@@ -217,7 +239,15 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
         const int r = im.row(e), j = e - r * M;
         double nx = 0.0, ny = 0.0, bj = 0.0;
         if (j < s_nf[r]) {
-            const int a = s_stk[j * kHullBlock + r], b = s_stk[(j + 1) * kHullBlock + r];
+            int a, b;
+            if (PK) {
+                const uint64_t sk = s_pk[r];
+                a = (int)((sk >> (3 * j)) & 7);
+                b = (int)((sk >> (3 * (j + 1))) & 7);
+            } else {
+                a = s_stk[j * kHullBlock + r];
+                b = s_stk[(j + 1) * kHullBlock + r];
+            }
             const double v0x = s_x[a * kHullBlock + r], v0y = s_y[a * kHullBlock + r];
             const double ex = s_x[b * kHullBlock + r] - v0x;
             const double ey = s_y[b * kHullBlock + r] - v0y;
@@ -344,15 +374,16 @@ blf_status launch_hull2d(const double* pts, const int32_t* npts, int32_t P, int3
     if (batch == 0) return BLF_OK;
     const int64_t blocks = ceil_div(batch, kHullBlock);
     const size_t lds = hull2d_lds_bytes(P, M);
+    auto kern = hull2d_packed(P) ? hull2d_kernel<true> : hull2d_kernel<false>;
     if (lds > 65536) {
         const blf_status st = check_hip(
-            hipFuncSetAttribute((const void*)hull2d_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds),
             "hull2d_kernel LDS attribute");
         if (st != BLF_OK) return st;
     }
-    hipLaunchKernelGGL(hull2d_kernel, dim3((unsigned)blocks), dim3(kHullBlock), lds, s, pts, npts,
-                       P, M, batch, A, b, nf);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kHullBlock), lds, s, pts, npts, P, M,
+                       batch, A, b, nf);
     return check_hip(hipGetLastError(), "hull2d_kernel launch");
 }
 
