@@ -210,3 +210,26 @@ def test_dcm_mpc_gpu_against_dense_certificate(handle):
         xd, rd = dense_qp.certify(host, i, xi[i], vrp[i])
         worst = max(worst, np.abs(xd - xi[i]).max(), np.abs(rd - vrp[i]).max())
     assert worst < 1e-12, worst
+
+
+def test_dcm_mpc_polish_refusal_matches_oracle_bitwise(handle, oracle):
+    """Duplicated facet rows (parallel or more than two active facets): the polish's refusal path
+    and the interior point method that then finishes alone, bit for bit with the oracle."""
+    prob = oracle.assemble_constraints(P.make_batch(8, horizon=40, n_footsteps=4, seed=81))
+    for q in range(8):
+        for k in range(40):
+            m = prob["nfacets"][q, k]
+            c = min(2, 8 - m)
+            prob["A"][q, k, m:m + c] = prob["A"][q, k, 0]
+            prob["b"][q, k, m:m + c] = prob["b"][q, k, 0]
+            prob["nfacets"][q, k] = m + c
+    dev = _to_dev(prob)
+    out = handle.dcm_mpc_solve(dev)
+    pol_o = np.zeros(8, np.int32)
+    st_o, xi_o, vrp_o, it_o, _ = oracle.dcm_mpc_solve_batch_warm(prob, threads=4, polished=pol_o)
+    assert not pol_o.all()
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), st_o)
+    np.testing.assert_array_equal(out["polished"].cpu().numpy(), pol_o)
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), it_o)
+    np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi_o)
+    np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)

@@ -231,3 +231,30 @@ def test_wave_tree_sum_order():
                 v = v + v[np.arange(64) ^ off]
             ref = v[0] if w == 0 else ref + v[0]
         assert O.wave_tree_sum(c) == ref
+
+
+def test_dcm_mpc_polish_refuses_degenerate_active_sets():
+    """Duplicated facet rows make two parallel facets active at once, and a third copy makes three:
+    the polish's vertex solve is singular or over-determined there, so the certificate refuses
+    (pc > 2, or parallel active normals) and the interior point method finishes alone, at the
+    same optimum as the problem without the copies."""
+    prob = O.assemble_constraints(P.make_batch(8, horizon=40, n_footsteps=4, seed=81))
+    st0, xi0, vrp0, it0, _ = O.dcm_mpc_solve_batch_warm(prob, threads=4)
+    dup = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in prob.items()}
+    for q in range(8):
+        for k in range(40):
+            m = dup["nfacets"][q, k]
+            c = min(2, 8 - m)           # repeat the first facet (up to twice)
+            dup["A"][q, k, m:m + c] = dup["A"][q, k, 0]
+            dup["b"][q, k, m:m + c] = dup["b"][q, k, 0]
+            dup["nfacets"][q, k] = m + c
+    pol = np.zeros(8, np.int32)
+    st, xi, vrp, it, _ = O.dcm_mpc_solve_batch_warm(dup, threads=4, polished=pol)
+    assert (st == 0).all() and (st0 == 0).all()
+    assert not pol.all()   # the refusal path ran
+    # wherever a duplicated facet is active the polish cannot certify; the IPM's own optimum agrees
+    for q in range(8):
+        if not pol[q]:
+            assert np.abs(vrp[q] - vrp0[q]).max() < 1e-6
+        else:
+            np.testing.assert_allclose(vrp[q], vrp0[q], atol=1e-12)
