@@ -857,6 +857,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         if (init_bad) status = BLF_QP_NUMERICAL;
         STAMP_ADD(12, t_in);
 
+        int drop = 0;         // polish pass 1: facets taken out of the guessed active set (bit i)
+        bool retry = false;   // the next loop top runs polish pass 1
         for (it = 0; status == 0; ++it) {
             // ---- residuals (knot-parallel) ----
             STAMP(t_r);
@@ -873,19 +875,21 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             if (P.tol_polish > 0.0 && mu <= P.tol_polish) {
                 // ---- active-set polish (oracle dcm_polish, DESIGN.md 4 "Polish"): one Newton
                 //      step of the QP with the guessed active facets as equalities, certified
-                //      (primal, stationarity, multiplier signs) or undone ----
+                //      (primal, stationarity, multiplier signs) or undone; facets whose
+                //      multiplier came out negative are dropped and the step retried once ----
                 STAMP(t_p);
                 const double sr0 = K.r0, sr1 = K.r1, sx0 = K.x0, sx1 = K.x1;
                 int pc = 0, pi1 = 0, pi2 = 0, pk = 0;
                 double E00 = 0.0, E01 = 0.0, E11 = 0.0;
-                bool okp = true;
+                bool okp = true, neg = false;
                 if (own) {
                     const int kx = opaque(k);
                     const int km = opaque(K.m), mm = opaque_s(mmax);
+                    const int dm = opaque(drop);
 #pragma unroll
                     for (int i = 0; i < kMaxFacets; ++i) {
                         if (i >= mm) break;
-                        if (i < km && K.lam[i] > K.s[i]) {
+                        if (i < km && K.lam[i] > K.s[i] && !((dm >> i) & 1)) {
                             if (pc == 0) pi1 = i;
                             else if (pc == 1) pi2 = i;
                             ++pc;
@@ -980,7 +984,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         } else if (pc == 1) {
                             const double2 a = L.A2[pi1 * N + kx];
                             pl1 = FD2(a.x, g0, a.y, g1) / FD2(a.x, a.x, a.y, a.y);
-                            if (!(pl1 >= -P.tol_d)) okp = false;
+                            if (!(pl1 >= -P.tol_d)) {
+                                okp = false;
+                                neg = true;
+                                drop |= 1 << pi1;
+                            }
                             if (!(fabs(fma(-pl1, a.x, g0)) <= P.tol_d) || !(fabs(fma(-pl1, a.y, g1)) <= P.tol_d))
                                 okp = false;
                         } else {
@@ -989,7 +997,16 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                             const double idet = 1.0 / fma(a.x, e.y, -(a.y * e.x));
                             pl1 = fma(g0, e.y, -(e.x * g1)) * idet;
                             pl2 = fma(a.x, g1, -(g0 * a.y)) * idet;
-                            if (!(pl1 >= -P.tol_d) || !(pl2 >= -P.tol_d)) okp = false;
+                            if (!(pl1 >= -P.tol_d)) {
+                                okp = false;
+                                neg = true;
+                                drop |= 1 << pi1;
+                            }
+                            if (!(pl2 >= -P.tol_d)) {
+                                okp = false;
+                                neg = true;
+                                drop |= 1 << pi2;
+                            }
                         }
                         const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
@@ -1022,6 +1039,16 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 K.r1 = sr1;
                 K.x0 = sx0;
                 K.x1 = sx1;
+                if (!retry && __syncthreads_or(neg)) {
+                    // pass 1: the same iterate, without the facets whose multiplier came out
+                    // negative; it runs this block again from the top of the loop (one copy of
+                    // the polish code) and does not count as an IPM iteration
+                    retry = true;
+                    --it;
+                    continue;
+                }
+                retry = false;
+                drop = 0;
                 // the iterate's gradient and defects again (the polish reused them); the wavefront
                 // boundary values were not touched, so xi_k comes back without a barrier
                 xi_prev(K, lane, xb0, xb1, xk0, xk1);

@@ -878,19 +878,26 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
 {
     const int N = w->N, M = w->M;
     int ok = 1;
-    int* pc = (int*)malloc(sizeof(int) * 3 * (size_t)N);
+    int* pc = (int*)malloc(sizeof(int) * 4 * (size_t)N);
     int* pi1 = pc + N;
     int* pi2 = pc + 2 * N;
+    int* drop = pc + 3 * N;   /* facets taken out of the guessed active set (bit i: facet i) */
     double* bak = (double*)malloc(sizeof(double) * (6 * (size_t)N + 2));
     double* lm = bak + 4 * (size_t)N + 2;   /* [N][2] multipliers of the active facets */
     memcpy(bak, w->vrp, sizeof(double) * 2 * N);
     memcpy(bak + 2 * N, w->xi, sizeof(double) * (2 * (size_t)N + 2));
+    for (int k = 0; k < N; ++k) drop[k] = 0;
+    /* pass 0: the guessed active set; pass 1 (only if pass 0 found negative multipliers): the same
+     * set without those facets, from the same iterate */
+    for (int pass = 0; pass < 2; ++pass) {
+    ok = 1;
+    int neg = 0;
     /* 1. active sets, projection onto the active lines, E_k (knot-parallel) */
     for (int k = 0; k < N; ++k) {
         const int m = w->nf[k];
         int c = 0, i1 = 0, i2 = 0;
         for (int i = 0; i < m; ++i) {
-            if (w->lam[k * MF + i] > w->s[k * MF + i]) {
+            if (w->lam[k * MF + i] > w->s[k * MF + i] && !((drop[k] >> i) & 1)) {
                 if (c == 0) i1 = i;
                 else if (c == 1) i2 = i;
                 ++c;
@@ -987,7 +994,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
         } else if (c == 1) {
             const double* a = w->A + (k * M + pi1[k]) * 2;
             l1 = FD2(a[0], g0, a[1], g1) / FD2(a[0], a[0], a[1], a[1]);
-            if (!(l1 >= -tol_d)) ok = 0;
+            if (!(l1 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi1[k]; }
             if (!(fabs(fma(-l1, a[0], g0)) <= tol_d) || !(fabs(fma(-l1, a[1], g1)) <= tol_d)) ok = 0;
         } else {
             const double* a = w->A + (k * M + pi1[k]) * 2;
@@ -995,7 +1002,8 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
             const double idet = 1.0 / fma(a[0], e[1], -(a[1] * e[0]));
             l1 = fma(g0, e[1], -(e[0] * g1)) * idet;
             l2 = fma(a[0], g1, -(g0 * a[1])) * idet;
-            if (!(l1 >= -tol_d) || !(l2 >= -tol_d)) ok = 0;
+            if (!(l1 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi1[k]; }
+            if (!(l2 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi2[k]; }
         }
         lm[2 * k] = l1 > 0.0 ? l1 : 0.0;
         lm[2 * k + 1] = l2 > 0.0 ? l2 : 0.0;
@@ -1004,6 +1012,10 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
             const double* a = w->A + (k * M + i) * 2;
             if (!(FD2(a[0], r0, a[1], r1) - w->b[k * M + i] <= tol_p)) ok = 0;
         }
+    }
+    if (ok || !neg) break;
+    memcpy(w->vrp, bak, sizeof(double) * 2 * N);   /* pass 1 starts from the same iterate */
+    memcpy(w->xi, bak + 2 * N, sizeof(double) * (2 * (size_t)N + 2));
     }
     if (!ok) {
         memcpy(w->vrp, bak, sizeof(double) * 2 * N);
