@@ -55,6 +55,15 @@ extern "C" int blf_debug_fbd_stamps(unsigned long long* out, int reset)
 
 namespace {
 
+// Every kernel in this file runs one 64-lane wavefront per workgroup, and the LDS operations of a
+// wavefront complete in program order, so lanes exchanging data through LDS need only a compiler
+// barrier between the write and the read (no s_barrier, no full s_waitcnt).
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // link record: R 9 | p 3 | w 3 | v 3 | al 3 | a 3 | spatial inertia 10 (m, h, Ibar xx xy xz yy yz zz)
 //              | spatial force 6 (tau_O, f)
 constexpr int kLinkRec = 40;
@@ -197,7 +206,7 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
         md = q > md ? q : md;
     }
     t.maxdepth = __builtin_amdgcn_readfirstlane(md);
-    __syncthreads();
+    wave_sync();
     return t;
 }
 
@@ -253,7 +262,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             b[kAl + i] = 0.0; b[kA + i] = 0.0;
         }
     }
-    __syncthreads();
+    wave_sync();
     FSTAMP_ADD(0, f_t);
     FSTAMP(f_t1);
     // 2. forward kinematics, one tree level at a time: poses, mixed velocities, nu_dot = 0
@@ -301,7 +310,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                 cr[kA + a] = (pr[kA + a] + t3[a]) + t4[a];
             }
         }
-        __syncthreads();
+        wave_sync();
     }
     FSTAMP_ADD(1, f_t1);
     FSTAMP(f_t2);
@@ -388,7 +397,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             sc[13 + a] = sc[3 + a];
         }
     }
-    __syncthreads();
+    wave_sync();
     FSTAMP_ADD(3, f_t3);
     FSTAMP(f_t4);
     // 5. subtree sums of the spatial inertias and (link - contact) forces, from the leaves up:
@@ -416,7 +425,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
 #pragma unroll
             for (int p = 0; p < kComp; ++p) dst[p] = acc[p];
         }
-        __syncthreads();
+        wave_sync();
     }
     FSTAMP_ADD(4, f_t4);
     FSTAMP(f_t5);
@@ -452,7 +461,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         y = (c >= 6 ? tau[c - 6] : 0.0) - (dot3(w, I + 10) + dot3(u, I + 13));
     }
     const unsigned long long myanc = (lane >= 6 && lane < NV) ? S.anc[lane - 5] : 0ull;
-    __syncthreads();
+    wave_sync();
     FSTAMP_ADD(5, f_t5);
     FSTAMP(f_t6);
     // 7. row i of M in registers: M_ij = S_j . F_i when column j moves the subtree of column i
@@ -489,15 +498,15 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             r[k] = lane == k ? piv * isq : (lane > k ? r[k] * isq : r[k]);
             double* col = S.comp + (k & 1) * NV;
             if (lane < NV) col[lane] = r[k];
-            __syncthreads();
-            // The row predicate goes into the multiplier (no branch: a branch would pull each
-            // column read into it and serialise the reads).  j >= NV touches only lanes past the
-            // matrix.
+            wave_sync();
+            // No row predicate: a lane above row j only updates its upper-triangle entry r[j],
+            // which nothing reads (pivots are diagonal, the substitutions and the stored L use
+            // j <= lane), so the update is one LDS broadcast read and one fma per entry.  j >= NV
+            // touches only lanes past the matrix.
 #pragma unroll
             for (int j = k + 1; j < NVMAX; ++j) {
                 const double ljk = col[j < NV ? j : NV - 1];
-                const double f = lane >= j ? r[k] : 0.0;
-                r[j] = r[j] - f * ljk;
+                r[j] = fma(-r[k], ljk, r[j]);   // parity here is 1e-9 relative, not bitwise
             }
         }
     }
@@ -518,7 +527,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
 #pragma unroll
         for (int j = 0; j < NVMAX; ++j)
             if (j < NV && j <= lane) Lm[MS * lane + j] = r[j];
-    __syncthreads();
+    wave_sync();
     double lki = (lane < NV - 1) ? Lm[MS * (NV - 1) + lane] : 0.0;
     for (int k = NV - 1; k >= 0; --k) {
         const double lnext = (k > 0 && lane < k - 1) ? Lm[MS * (k - 1) + lane] : 0.0;   // read ahead
@@ -528,7 +537,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         lki = lnext;
     }
     if (lane < NV) S.rhs[lane] = y;
-    __syncthreads();
+    wave_sync();
     FSTAMP_ADD(8, f_t8);
     FSTAMP_ADD(9, f_t0);
     return ok;
@@ -555,7 +564,7 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
         else v = st.joint_pos[(int64_t)n * q + (i - 18 - n)];
         loc[i] = v;
     }
-    __syncthreads();
+    wave_sync();
     const Topo T = build_topo(m, S);
     const bool ok = fbd_eval<NVMAX>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                     tau + (int64_t)n * q, ct, q, reg, T);
@@ -596,7 +605,7 @@ __global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state 
         else v = st.joint_pos[(int64_t)n * q + (i - 18 - n)];
         loc[i] = v;
     }
-    __syncthreads();
+    wave_sync();
     const Topo T = build_topo(m, S);
     bool ok = true;
     for (int32_t step = 0; step < nsteps; ++step) {
@@ -604,7 +613,7 @@ __global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state 
         ok = fbd_eval<NVMAX>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                              tau + (int64_t)n * q, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
-        __syncthreads();
+        wave_sync();
         // every element moves by its derivative at the start of the step (ForwardEuler.tpp:37-45):
         // positions first (they read the old velocities), then the velocities
         for (int i = lane; i < 12 + n; i += kWave) {
@@ -613,9 +622,9 @@ __global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state 
             else if (i < 12) loc[6 + n + i] = loc[6 + n + i] + dR[i - 3] * h;
             else loc[18 + n + (i - 12)] = loc[18 + n + (i - 12)] + loc[6 + (i - 12)] * h;
         }
-        __syncthreads();
+        wave_sync();
         for (int i = lane; i < NV; i += kWave) loc[i] = loc[i] + S.rhs[i] * h;
-        __syncthreads();
+        wave_sync();
     }
     const double nan = __builtin_nan("");
     for (int i = lane; i < 18 + 2 * n; i += kWave) {
