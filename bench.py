@@ -114,8 +114,9 @@ def main():
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=("c2", "c3", "c5", "rh"), default="c2",
-                    help="c2 (default, the driver's metric): configs[1]; c3: configs[2] pipeline "
+    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c5", "rh"), default="c2",
+                    help="c2 (default, the driver's metric): configs[1]; c1: configs[0] single-solve "
+                         "latency (4 footsteps, N=50) on the GPU and the CPU; c3: configs[2] pipeline "
                          "(hull H-rep + QP + swing splines, B=65536); c5: configs[4] closed loop "
                          "(QP + 30-DoF floating-base dynamics with contacts, B=16384); rh: "
                          "receding-horizon advance() (phase expansion + warm-started QP, B=4096)")
@@ -274,6 +275,8 @@ def other_workload(args):
     N = args.horizon
     if args.workload == "rh":
         return receding_horizon(args, h, dev)
+    if args.workload == "c1":
+        return single_solve_latency(args, h, dev)
     if args.workload == "c3":
         B = 65536
         prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED)
@@ -339,6 +342,54 @@ def other_workload(args):
                 "config": {"workload": f"configs[4] on one GPU: batch={B} robots, horizon-{N} QP "
                                        f"+ {nsteps} Euler steps of the 6+24 DoF dynamics per "
                                        f"period", "batch_per_gpu": B}}
+    print(json.dumps(line), flush=True)
+
+
+def single_solve_latency(args, h, dev):
+    """configs[0]: one TimeVaryingDCMPlanner solve (4 footsteps, 50-knot horizon), the reference's
+    Planners-test case.  Latency of one blf_dcm_mpc_solve (inputs resident, launch to completion,
+    median of 50) next to the CPU restatement on one thread (oracle sequential mode), same
+    problem.  A batch of one leaves 255 of 256 CUs idle: the GPU path is built for batches."""
+    import numpy as np
+    import torch
+    from blf import native
+    from blf import problems as P
+    N = 50
+    prob = P.make_batch(1, horizon=N, n_footsteps=4, seed=P.SEED)
+    d = {k: torch.from_numpy(prob[k]).to(dev) for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
+    A, b, nf = h.assemble_constraints(torch.from_numpy(prob["corners"]).to(dev),
+                                      torch.from_numpy(prob["ncorners"]).to(dev))
+    d.update(A=A, b=b, nfacets=nf)
+    params = native.default_params(N)
+    out = h.dcm_mpc_solve(d, params)
+    torch.cuda.synchronize()
+    lat = []
+    for _ in range(args.warmup + 50):
+        t0 = time.perf_counter()
+        h.dcm_mpc_solve(d, params, out=out)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    gpu_us = float(np.median(lat[args.warmup:])) * 1e6
+    assert int(out["status"][0]) == 0
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    host = dict(prob)
+    for k in ("A", "b", "nfacets"):
+        host[k] = d[k].cpu().numpy()
+    prm = O.default_params(N, sequential=1)
+    O.dcm_mpc_solve(host, params=prm)
+    t1 = time.perf_counter()
+    for _ in range(200):
+        st, _, _, it = O.dcm_mpc_solve(host, params=prm)
+    cpu_us = (time.perf_counter() - t1) / 200 * 1e6
+    line = {"metric": "single DCM-MPC solve latency (configs[0]: 4 footsteps, horizon 50)",
+            "value": gpu_us, "unit": "us", "n_gpus": 1, "higher_is_better": False,
+            "dtype": "f64", "ipm_iters": int(out["iters"][0]), "polished": int(out["polished"][0]),
+            "cpu_baseline": {"value": cpu_us, "unit": "us", "cores": 1, "kind": "port",
+                             "sample": "200 solves of the same problem, oracle/blf_oracle.c "
+                                       "sequential mode, gcc -O2, one thread"},
+            "config": {"workload": "configs[0]: batch=1, 4 footsteps, horizon=50, launch to "
+                                   "completion incl. the host synchronisation"}}
     print(json.dumps(line), flush=True)
 
 
