@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tol-polish", type=float, default=None,
+                    help="override blf_dcm_mpc_default_params' tol_polish (also the CPU baseline's)")
     ap.add_argument("--workload", choices=("c1", "c2", "c3", "c5", "rh"), default="c2",
                     help="c2 (default, the driver's metric): configs[1]; c1: configs[0] single-solve "
                          "latency (4 footsteps, N=50) on the GPU and the CPU; c3: configs[2] pipeline "
@@ -416,6 +418,8 @@ def receding_horizon(args, h, dev):
     omega_full = t("omega")
     M = table["phase_b"].shape[2]
     params = native.default_params(N, max_facets=M)
+    # TimeVaryingDCMPlanner's trigger for warm-started windows (1e-4; the cold default is 3e-4)
+    params.tol_polish = args.tol_polish if args.tol_polish is not None else 1e-4
     stream = torch.cuda.current_stream()
     state = dict(xi0=t("xi_init").clone(), prev=None, s=0)
     bufs = [None, None]

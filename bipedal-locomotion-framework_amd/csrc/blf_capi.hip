@@ -208,7 +208,7 @@ void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon)
     p->tol_mu = 1e-16;
     p->tol_primal = 1e-10;
     p->tol_dual = 1e-9;
-    p->tol_polish = 1e-4;
+    p->tol_polish = 3e-4;
 }
 
 blf_status blf_dcm_phase_expand(blf_handle* handle, const blf_phase_table* ph,

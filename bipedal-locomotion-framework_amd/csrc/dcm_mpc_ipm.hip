@@ -857,8 +857,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         if (init_bad) status = BLF_QP_NUMERICAL;
         STAMP_ADD(12, t_in);
 
-        int drop = 0;         // polish pass 1: facets taken out of the guessed active set (bit i)
-        bool retry = false;   // the next loop top runs polish pass 1
+        int drop = 0;    // polish passes 1, 2: facets taken out of the guessed active set (bit i)
+        int add = 0;     // polish pass 2: facets put into it
+        int pass = 0;    // the polish pass the next loop top runs (uniform)
         for (it = 0; status == 0; ++it) {
             // ---- residuals (knot-parallel) ----
             STAMP(t_r);
@@ -875,21 +876,22 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
             if (P.tol_polish > 0.0 && mu <= P.tol_polish) {
                 // ---- active-set polish (oracle dcm_polish, DESIGN.md 4 "Polish"): one Newton
                 //      step of the QP with the guessed active facets as equalities, certified
-                //      (primal, stationarity, multiplier signs) or undone; facets whose
-                //      multiplier came out negative are dropped and the step retried once ----
+                //      (primal, stationarity, multiplier signs) or undone; a failed pass is
+                //      retried without the negative-multiplier facets, then with the violated
+                //      facets added (oracle dcm_polish) ----
                 STAMP(t_p);
                 const double sr0 = K.r0, sr1 = K.r1, sx0 = K.x0, sx1 = K.x1;
                 int pc = 0, pi1 = 0, pi2 = 0, pk = 0;
                 double E00 = 0.0, E01 = 0.0, E11 = 0.0;
-                bool okp = true, neg = false;
+                bool okp = true, neg = false, viol = false;
                 if (own) {
                     const int kx = opaque(k);
                     const int km = opaque(K.m), mm = opaque_s(mmax);
-                    const int dm = opaque(drop);
+                    const int dm = opaque(drop), am = opaque(add);
 #pragma unroll
                     for (int i = 0; i < kMaxFacets; ++i) {
                         if (i >= mm) break;
-                        if (i < km && K.lam[i] > K.s[i] && !((dm >> i) & 1)) {
+                        if (i < km && ((K.lam[i] > K.s[i] && !((dm >> i) & 1)) || ((am >> i) & 1))) {
                             if (pc == 0) pi1 = i;
                             else if (pc == 1) pi2 = i;
                             ++pc;
@@ -1014,7 +1016,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                             if (i >= mm) break;
                             if (i < km) {
                                 const double2 a = L.A2[i * N + kx];
-                                if (!(FD2(a.x, K.r0, a.y, K.r1) - L.BI[i * N + kx].x <= P.tol_p)) okp = false;
+                                if (!(FD2(a.x, K.r0, a.y, K.r1) - L.BI[i * N + kx].x <= P.tol_p)) {
+                                    okp = false;
+                                    viol = true;
+                                    if (pass >= 1) add |= 1 << i;
+                                }
                             }
                         }
                     }
@@ -1039,16 +1045,18 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 K.r1 = sr1;
                 K.x0 = sx0;
                 K.x1 = sx1;
-                if (!retry && __syncthreads_or(neg)) {
-                    // pass 1: the same iterate, without the facets whose multiplier came out
-                    // negative; it runs this block again from the top of the loop (one copy of
-                    // the polish code) and does not count as an IPM iteration
-                    retry = true;
+                if ((pass == 0 && __syncthreads_or(neg)) || (pass == 1 && __syncthreads_or(viol))) {
+                    // pass 1: the same iterate without the facets whose multiplier came out
+                    // negative; pass 2: pass 1's set plus the facets it left violated.  Each runs
+                    // this block again from the top of the loop (one copy of the polish code) and
+                    // does not count as an IPM iteration.
+                    ++pass;
                     --it;
                     continue;
                 }
-                retry = false;
+                pass = 0;
                 drop = 0;
+                add = 0;
                 // the iterate's gradient and defects again (the polish reused them); the wavefront
                 // boundary values were not touched, so xi_k comes back without a barrier
                 xi_prev(K, lane, xb0, xb1, xk0, xk1);

@@ -93,7 +93,7 @@ public:
     /**
      * Keys (all optional): "horizon" (int), "sampling_time", "gravity", "foot_length",
      * "foot_width", "dcm_weight", "vrp_weight", "terminal_weight" (scalar or 2-vector),
-     * "tolerance" (tol_mu), "polish_tolerance" (tol_polish, default 1e-4; 0: interior point
+     * "tolerance" (tol_mu), "polish_tolerance" (tol_polish, default 1e-4 for the warm-started windows; 0: interior point
      * only), "max_iterations" (int), "warm_start" (bool, default true), "warm_start_floor"
      * (default 1e-3).
      */

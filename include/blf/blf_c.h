@@ -197,7 +197,7 @@ typedef struct blf_dcm_mpc_warm_start {
 } blf_dcm_mpc_warm_start;
 
 /* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-16,
- * tol_primal 1e-10, tol_dual 1e-9, tol_polish 1e-4, max_iter 50, max_facets 8). */
+ * tol_primal 1e-10, tol_dual 1e-9, tol_polish 3e-4, max_iter 50, max_facets 8). */
 void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);
 
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,

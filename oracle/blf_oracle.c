@@ -882,22 +882,24 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
     int* pi1 = pc + N;
     int* pi2 = pc + 2 * N;
     int* drop = pc + 3 * N;   /* facets taken out of the guessed active set (bit i: facet i) */
+    int* add = (int*)calloc((size_t)N, sizeof(int));   /* facets put into it */
     double* bak = (double*)malloc(sizeof(double) * (6 * (size_t)N + 2));
     double* lm = bak + 4 * (size_t)N + 2;   /* [N][2] multipliers of the active facets */
     memcpy(bak, w->vrp, sizeof(double) * 2 * N);
     memcpy(bak + 2 * N, w->xi, sizeof(double) * (2 * (size_t)N + 2));
     for (int k = 0; k < N; ++k) drop[k] = 0;
     /* pass 0: the guessed active set; pass 1 (only if pass 0 found negative multipliers): the same
-     * set without those facets, from the same iterate */
-    for (int pass = 0; pass < 2; ++pass) {
+     * set without those facets; pass 2 (only if pass 1 left facets violated): pass 1's set plus
+     * those facets.  Every pass starts from the same iterate. */
+    for (int pass = 0; pass < 3; ++pass) {
     ok = 1;
-    int neg = 0;
+    int neg = 0, viol = 0;
     /* 1. active sets, projection onto the active lines, E_k (knot-parallel) */
     for (int k = 0; k < N; ++k) {
         const int m = w->nf[k];
         int c = 0, i1 = 0, i2 = 0;
         for (int i = 0; i < m; ++i) {
-            if (w->lam[k * MF + i] > w->s[k * MF + i] && !((drop[k] >> i) & 1)) {
+            if ((w->lam[k * MF + i] > w->s[k * MF + i] && !((drop[k] >> i) & 1)) || ((add[k] >> i) & 1)) {
                 if (c == 0) i1 = i;
                 else if (c == 1) i2 = i;
                 ++c;
@@ -1010,10 +1012,14 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
         const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
         for (int i = 0; i < w->nf[k]; ++i) {
             const double* a = w->A + (k * M + i) * 2;
-            if (!(FD2(a[0], r0, a[1], r1) - w->b[k * M + i] <= tol_p)) ok = 0;
+            if (!(FD2(a[0], r0, a[1], r1) - w->b[k * M + i] <= tol_p)) {
+                ok = 0;
+                viol = 1;
+                if (pass >= 1) add[k] |= 1 << i;
+            }
         }
     }
-    if (ok || !neg) break;
+    if (ok || (pass == 0 && !neg) || (pass == 1 && !viol)) break;
     memcpy(w->vrp, bak, sizeof(double) * 2 * N);   /* pass 1 starts from the same iterate */
     memcpy(w->xi, bak + 2 * N, sizeof(double) * (2 * (size_t)N + 2));
     }
@@ -1028,6 +1034,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
     }
     free(pc);
     free(bak);
+    free(add);
     return ok;
 }
 

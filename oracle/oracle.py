@@ -182,7 +182,7 @@ def default_params(horizon, **kw):
     p.tol_mu = kw.get("tol_mu", 1e-16)
     p.tol_primal = kw.get("tol_primal", 1e-10)
     p.tol_dual = kw.get("tol_dual", 1e-9)
-    p.tol_polish = kw.get("tol_polish", 1e-4)   # blf_dcm_mpc_default_params
+    p.tol_polish = kw.get("tol_polish", 3e-4)   # blf_dcm_mpc_default_params
     return p
 
 
