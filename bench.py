@@ -210,6 +210,13 @@ def main():
         achieved = bpq * B / (kernel_ms * 1e-3) / 1e9
         traffic, traffic_src = profiled_traffic()
         fp64_tf = flops / (kernel_ms * 1e-3) / 1e12
+        # executed fp64 flops of the launch from the committed SQ pass (FMA counts two, 64 lanes
+        # per wave instruction): covers the polish passes and the scans' redundant work, which
+        # the sequential-form count above (IPM iterations only) does not
+        pmc, _ = profiled_summary()
+        f64 = ((pmc or {}).get("valu_issue") or {}).get("fp64_insts_per_launch")
+        fp64_exec_tf = (64.0 * (2.0 * f64["fma"] + f64["mul"] + f64["add"]) / (kernel_ms * 1e-3)
+                        / 1e12) if f64 else None
         line = {
             "metric": "DCM-MPC QP solves/sec (batch, horizon=100) at 1/2/4/8 MI355X",
             "value": total / elapsed,
@@ -233,7 +240,11 @@ def main():
                          "kernel": "dcm_mpc_ipm_kernel<128>", "kernel_ms": kernel_ms,
                          "bytes_per_qp": bpq,
                          "fp64_valu": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
-                                       "frac": fp64_tf / FP64_PEAK_TFLOPS},
+                                       "frac": fp64_tf / FP64_PEAK_TFLOPS,
+                                       "counted": "sequential-form flops of the IPM iterations",
+                                       "executed_tflops": fp64_exec_tf,
+                                       "executed_frac": (fp64_exec_tf / FP64_PEAK_TFLOPS
+                                                         if fp64_exec_tf else None)},
                          "valu_issue": valu_issue(kernel_ms),
                          "mean_ipm_iters": float(iters.float().mean())},
             "gather_ms": gather_ms,

@@ -60,7 +60,7 @@ def run(args, tol_polish):
           f"status!=0: {int((out['status'] != 0).sum())}")
     if stamps is not None:
         stamps(ctypes.cast(buf, ctypes.c_void_p), 0)
-        tot, fac, sol, its = buf[0], buf[1], buf[2], buf[3]
+        tot, fac, sol, its = buf[0], buf[1], buf[2], max(buf[3], 1)
         res, wph, pred, step = buf[4], buf[5], buf[6], buf[7]
         print(f"thread0 cycles per QP: total {tot / 64 / args.reps:.0f}  per iteration: "
               f"residuals {res / its:.0f}, W-phase {wph / its:.0f}, factor {fac / its:.0f}, "
