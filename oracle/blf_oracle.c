@@ -1145,6 +1145,28 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             xi[2 * (k + 1) + 1] = xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
         }
     }
+    if (status == 2) goto done;
+    /* ---- active-set start (DESIGN.md 4 "Polish"): before any IPM iteration, the polish from the
+     *      guess "facets the start point violates" (a warm start: also the facets whose previous
+     *      multiplier exceeds the floor), with up to 6 drop/add passes ---- */
+    if (prm->tol_polish > 0.0) {
+        int* gm = (int*)calloc((size_t)N, sizeof(int));
+        for (int k = 0; k < N; ++k) {
+            const int ws = warm && k + warm->shift < N;
+            for (int i = 0; i < nfacets[k]; ++i) {
+                const double* a = Ain + (k * M + i) * 2;
+                const double sl = bin[k * M + i] - FD2(a[0], vrp[2 * k], a[1], vrp[2 * k + 1]);
+                if (sl < 0.0) gm[k] |= 1 << i;
+                if (ws && warm->lambda[(k + warm->shift) * M + i] > warm->floor) gm[k] |= 1 << i;
+            }
+        }
+        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, 6);
+        free(gm);
+        if (okg) { polished = 1; status = 0; it = 0; goto done; }
+    }
+    /* the interior point method's own start (only when the active-set start did not certify):
+     * the start point was restored exactly */
+
     /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s; warm: s = max(b - A r, floor),
      *      lam = max(lam_warm[src], floor) with the same source knot as the VRP ---- */
     double dres = 0.0;
@@ -1191,27 +1213,6 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             dres = nanmax(dres, fabs(fma(-w->be[k], nu1, w->rh[2 * k + 1])));
         }
     }
-    if (status == 2) goto done;
-    /* ---- active-set start (DESIGN.md 4 "Polish"): before any IPM iteration, the polish from the
-     *      guess "facets the start point violates" (a warm start: also the facets whose previous
-     *      multiplier exceeds the floor), with up to 6 drop/add passes ---- */
-    if (prm->tol_polish > 0.0) {
-        int* gm = (int*)calloc((size_t)N, sizeof(int));
-        for (int k = 0; k < N; ++k) {
-            const int ws = warm && k + warm->shift < N;
-            for (int i = 0; i < nfacets[k]; ++i) {
-                const double* a = Ain + (k * M + i) * 2;
-                const double sl = bin[k * M + i] - FD2(a[0], vrp[2 * k], a[1], vrp[2 * k + 1]);
-                if (sl < 0.0) gm[k] |= 1 << i;
-                if (ws && warm->lambda[(k + warm->shift) * M + i] > warm->floor) gm[k] |= 1 << i;
-            }
-        }
-        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, 6);
-        free(gm);
-        if (okg) { polished = 1; status = 0; it = 0; goto done; }
-        dcm_residuals(w, 1);   /* the start point's gradient and defects again */
-    }
-
     /* mu, pres and dres are known at the top of every iteration without a reduction there: the
      * start computes them, and each step updates them from sums gathered with the step-length
      * maxima (mu: the exact quadratic in the step length; pres, dres: the linear residuals of an
