@@ -193,6 +193,25 @@ struct Reduce {
         }
         return q;
     }
+    // OR of a few flag bits over the workgroup in one exchange (__syncthreads_or costs a
+    // reduction and two barriers per flag).
+    template <int NB>
+    __device__ int or_bits(int f)
+    {
+        int b = 0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) if (__ballot((f >> j) & 1) != 0) b |= 1 << j;
+        if constexpr (NW > 1) {
+            double* r = row();
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) r[4 * w] = (double)b;
+            __syncthreads();
+            b = (int)r[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) b |= (int)r[4 * i];
+        }
+        return b;
+    }
     __device__ double nanmax_(double q)
     {
         q = wave_nanmax(q);
@@ -1039,7 +1058,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                         }
                     }
                 }
-                const bool rejected = __syncthreads_or(!okp);
+                const int fl = R.template or_bits<4>((okp ? 0 : 1) | (neg || viol ? 2 : 0) |
+                                                     (neg ? 4 : 0) | (viol ? 8 : 0));
+                const bool rejected = (fl & 1) != 0;
                 STAMP_ADD(8, t_p);
 #ifdef BLF_STAMPS
                 if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_blf_stamps[9], 1ull);
@@ -1059,9 +1080,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                 K.r1 = sr1;
                 K.x0 = sx0;
                 K.x1 = sx1;
-                const bool more = guess ? (pass + 1 < kGuessPasses && __syncthreads_or(neg || viol))
-                                        : ((pass == 0 && __syncthreads_or(neg)) ||
-                                           (pass == 1 && __syncthreads_or(viol)));
+                const bool more = guess ? (pass + 1 < kGuessPasses && (fl & 2) != 0)
+                                        : ((pass == 0 && (fl & 4) != 0) || (pass == 1 && (fl & 8) != 0));
                 if (more) {
                     // IPM polish, pass 1: the same iterate without the facets whose multiplier came
                     // out negative; pass 2: pass 1's set plus the facets it left violated.  Active-
