@@ -29,7 +29,8 @@ namespace {
 // [0] whole kernel, [1] factorization, [2] predictor solve .. corrector solve, [3] iterations,
 // [4] residuals + reduction, [5] W-phase, [6] predictor solve, [7] corrector step + update,
 // [8] polish attempts (cycles), [9] polish attempts (count), [10] load phase, [11] LQ start step,
-// [12] initial slacks / multipliers / dual residual.
+// [12] initial slacks / multipliers / dual residual, [13] polish: projection + residuals,
+// [14] polish: Riccati sweep, [15] polish: solve.
 __device__ unsigned long long g_blf_stamps[16];
 #define STAMP(t) unsigned long long t = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, t0) \
@@ -955,7 +956,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     double pd, cd;
                     residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
                 }
+                STAMP_ADD(13, t_p);
+                STAMP(t_pr);
                 okp = riccati<NW>(K, P, E00, E01, E11, bnd, N, nwa, k, wv, lane, own) && okp;
+                STAMP_ADD(14, t_pr);
                 pk = opaque(pk);
                 pc = pk & 3;
                 pi1 = (pk >> 2) & 7;
@@ -992,8 +996,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     // the Newton step; then the certificate: costates of the new point from the
                     // solve, nu_k = P_{k+1} dxi_{k+1} + (qx_k + v_{k+1}) (oracle dcm_polish step 6)
                     double dr0, dr1, dx0, dx1, vn0, vn1, dxk0, dxk1;
+                    STAMP(t_ps);
                     solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1,
                               dxk0, dxk1);
+                    STAMP_ADD(15, t_ps);
                     if (own) {
                         K.r0 = K.r0 + dr0;
                         K.r1 = K.r1 + dr1;

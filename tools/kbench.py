@@ -75,6 +75,11 @@ def run(args, tol_polish):
         q = 64 * args.reps
         print(f"start-up per QP: loads {buf[10] / q:.0f}, LQ step {buf[11] / q:.0f}, "
               f"slacks/multipliers/dual residual {buf[12] / q:.0f}")
+        if buf[9]:
+            na = buf[9]
+            print(f"per polish attempt: projection+residuals {buf[13] / na:.0f}, Riccati sweep "
+                  f"{buf[14] / na:.0f}, solve {buf[15] / na:.0f}, h + certificate + vote "
+                  f"{(buf[8] - buf[13] - buf[14] - buf[15]) / na:.0f}")
 
 if __name__ == "__main__":
     main()
