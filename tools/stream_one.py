@@ -40,6 +40,15 @@ def main(which):
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
+    if os.environ.get("STREAM_TIME"):   # event-timed median of 20 launches
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(40)]
+        for i in range(20):
+            ev[2 * i].record()
+            fn()
+            ev[2 * i + 1].record()
+        torch.cuda.synchronize()
+        ms = sorted(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(20))
+        print(f"{which} lib={os.path.basename(native.LIB_PATH)} median {ms[10]:.4f} ms", flush=True)
 
 
 if __name__ == "__main__":
