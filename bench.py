@@ -39,8 +39,12 @@ def profiled_summary():
     written by tools/summarize_profile.py from separate FETCH_SIZE / WRITE_SIZE / SQ passes);
     bench.py cannot read PMC counters itself.  Returns (summary, path) or (None, None)."""
     import glob
-    # newest by name (profiles/rNN_<tag>_summary.json; file times do not survive the copy to a box)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
+    import re
+    # newest by name (profiles/rNN_vMM_<tag>_summary.json; file times do not survive the copy to a
+    # box), numbers compared as numbers so v10 sorts after v9
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")),
+                   key=lambda f: [int(t) if t.isdigit() else t
+                                  for t in re.split(r"(\d+)", os.path.basename(f))])
     if not files:
         return None, None
     with open(files[-1]) as f:

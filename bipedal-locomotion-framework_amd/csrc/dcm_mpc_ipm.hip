@@ -1046,20 +1046,32 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                                 add &= ~(1 << pi2);
                             }
                         }
+                        // primal feasibility of every facet: the rows are read four at a time
+                        // (all lanes, clamped to the staged slots) so the LDS reads overlap
                         const int km = opaque(K.m), mm = opaque_s(mmax);
+                        int vm = 0;
 #pragma unroll
-                        for (int i = 0; i < kMaxFacets; ++i) {
-                            if (i >= mm) break;
-                            if (i < km) {
-                                const double2 a = L.A2[i * N + kx];
-                                if (!(FD2(a.x, K.r0, a.y, K.r1) - L.BI[i * N + kx].x <= P.tol_p)) {
-                                    okp = false;
-                                    viol = true;
-                                    if (pass >= 1 || guess) {
-                                        add |= 1 << i;
-                                        drop &= ~(1 << i);
-                                    }
-                                }
+                        for (int i0 = 0; i0 < kMaxFacets; i0 += 4) {
+                            if (i0 >= mm) break;
+                            double2 av[4];
+                            double bv[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int i = i0 + j < mm ? i0 + j : 0;
+                                av[j] = L.A2[i * N + kx];
+                                bv[j] = L.BI[i * N + kx].x;
+                            }
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (!(FD2(av[j].x, K.r0, av[j].y, K.r1) - bv[j] <= P.tol_p)) vm |= 1 << (i0 + j);
+                        }
+                        vm &= (1 << (km < mm ? km : mm)) - 1;
+                        if (vm) {
+                            okp = false;
+                            viol = true;
+                            if (pass >= 1 || guess) {
+                                add |= vm;
+                                drop &= ~vm;
                             }
                         }
                     }
