@@ -58,7 +58,7 @@ struct KParams {
 constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
 constexpr int kBV = 8;    // v_{64w} (2): backward-scan value at the first knot of wavefront w
 constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last knot of wavefront w
-constexpr int kGuessPasses = 6;   // active-set start: drop/add passes (oracle: dcm_polish max_pass)
+constexpr int kGuessPasses = 8;   // active-set start: drop/add passes (oracle: dcm_polish max_pass)
 constexpr int kBnd = 16;
 struct Lds {
     double2 *A2, *BI;   // facet rows: normal (a_x, a_y); (b, 1/s), 1/s later the multiplier step
@@ -266,6 +266,41 @@ __device__ __forceinline__ double bperm(int addr, double x)
 // VALU op per product pair (the kernel is VALU-issue bound).
 #define FD2(a, b, c, d) fma((a), (b), (c) * (d))
 #define FD3(a, b, c, d, e) fma((a), (b), fma((c), (d), (e)))
+
+// More than two candidate lines in a polish pass (the drop/add moves can add two facets at once):
+// the first pair (i < j in facet order) whose vertex satisfies every facet of the knot — a vertex
+// of the support polygon — is the active pair (oracle dcm_polish).  Returns 2 with pi1, pi2 set,
+// or 3 (no such pair: the pass fails).  Rare, so it reads the rows straight from LDS.
+__device__ __attribute__((noinline)) int vertex_pair(const double2* A2, const double2* BI, int N, int kx,
+                                                     int km, int cm, double tol_p, int& pi1, int& pi2)
+{
+    for (int x = 0; x < km; ++x) {
+        if (!((cm >> x) & 1)) continue;
+        for (int y = x + 1; y < km; ++y) {
+            if (!((cm >> y) & 1)) continue;
+            const double2 a = A2[x * N + kx];
+            const double2 e = A2[y * N + kx];
+            const double ba = BI[x * N + kx].x, be = BI[y * N + kx].x;
+            const double det = fma(a.x, e.y, -(a.y * e.x));
+            const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
+            if (!(det * det > 1e-18 * (aa * ee))) continue;
+            const double idet = 1.0 / det;
+            const double v0 = fma(ba, e.y, -(a.y * be)) * idet;
+            const double v1 = fma(a.x, be, -(ba * e.x)) * idet;
+            bool feas = true;
+            for (int l = 0; l < km; ++l) {
+                const double2 f = A2[l * N + kx];
+                if (!(FD2(f.x, v0, f.y, v1) - BI[l * N + kx].x <= tol_p)) feas = false;
+            }
+            if (feas) {
+                pi1 = x;
+                pi2 = y;
+                return 2;
+            }
+        }
+    }
+    return 3;
+}
 
 // 2x2 compose (row-major): n = a * b;  nc = a * c + e.
 #define COMPOSE(a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, e0, e1)                 \
@@ -915,6 +950,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                     const int kx = opaque(k);
                     const int km = opaque(K.m), mm = opaque_s(mmax);
                     const int dm = opaque(drop), am = opaque(add), gk = opaque(gm);
+                    int cm = 0;   // the pass's active-set candidates (bit i: facet i)
 #pragma unroll
                     for (int i = 0; i < kMaxFacets; ++i) {
                         if (i >= mm) break;
@@ -923,8 +959,10 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                             if (pc == 0) pi1 = i;
                             else if (pc == 1) pi2 = i;
                             ++pc;
+                            cm |= 1 << i;
                         }
                     }
+                    if (pc > 2) pc = vertex_pair(L.A2, L.BI, N, kx, km, cm, P.tol_p, pi1, pi2);
                     okp = pc <= 2;
                     pk = (pc < 3 ? pc : 2) | (pi1 << 2) | (pi2 << 5);
                     const double b2 = K.be * K.be;

@@ -338,6 +338,7 @@ double orc_wave_tree_sum(const double* c, int n)
 }
 
 #define MF 8
+#define ORC_GUESS_PASSES 8   /* active-set start: drop/add passes (kernel: kGuessPasses) */
 #define WV 64
 
 /* Fused forms, used in exactly the places the kernel uses them (csrc/dcm_mpc_ipm.hip):
@@ -874,6 +875,14 @@ static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
  * solved for the active multipliers with residual <= tol_d, and lam >= -tol_d.  Accepted: xi, vrp hold
  * the polished optimum, lam its multipliers (max(lam, 0) on the active facets, 0 on the others)
  * and 1 is returned.  Rejected: xi, vrp are restored, 0 is returned. */
+/* Facet i of knot k is in a polish pass's active set: guessed (the active-set start's guess bits,
+ * or an IPM iterate's lam_i > s_i) and not dropped, or added. */
+static int cand_bit(const dcm_ws* w, const int* guess, const int* drop, const int* add, int k, int i)
+{
+    const int base = guess ? ((guess[k] >> i) & 1) : (w->lam[k * MF + i] > w->s[k * MF + i]);
+    return (base && !((drop[k] >> i) & 1)) || ((add[k] >> i) & 1);
+}
+
 static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, int max_pass)
 {
     const int N = w->N, M = w->M;
@@ -899,14 +908,41 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, i
         const int m = w->nf[k];
         int c = 0, i1 = 0, i2 = 0;
         for (int i = 0; i < m; ++i) {
-            const int base = guess ? ((guess[k] >> i) & 1) : (w->lam[k * MF + i] > w->s[k * MF + i]);
-            if ((base && !((drop[k] >> i) & 1)) || ((add[k] >> i) & 1)) {
+            if (cand_bit(w, guess, drop, add, k, i)) {
                 if (c == 0) i1 = i;
                 else if (c == 1) i2 = i;
                 ++c;
             }
         }
-        if (c > 2) ok = 0;
+        if (c > 2) {
+            /* more than two candidate lines (the drop/add moves can add two facets at once): the
+             * first pair in facet order whose vertex satisfies every facet of the knot (a vertex
+             * of the support polygon) becomes the active pair; none: the pass fails */
+            int found = 0;
+            for (int x = 0; x < m && !found; ++x) {
+                if (!cand_bit(w, guess, drop, add, k, x)) continue;
+                for (int y = x + 1; y < m && !found; ++y) {
+                    if (!cand_bit(w, guess, drop, add, k, y)) continue;
+                    const double* a = w->A + (k * M + x) * 2;
+                    const double* e = w->A + (k * M + y) * 2;
+                    const double ba = w->b[k * M + x], be = w->b[k * M + y];
+                    const double det = fma(a[0], e[1], -(a[1] * e[0]));
+                    const double aa = FD2(a[0], a[0], a[1], a[1]), ee = FD2(e[0], e[0], e[1], e[1]);
+                    if (!(det * det > 1e-18 * (aa * ee))) continue;
+                    const double idet = 1.0 / det;
+                    const double v0 = fma(ba, e[1], -(a[1] * be)) * idet;
+                    const double v1 = fma(a[0], be, -(ba * e[0])) * idet;
+                    int feas = 1;
+                    for (int l = 0; l < m; ++l) {
+                        const double* f = w->A + (k * M + l) * 2;
+                        if (!(FD2(f[0], v0, f[1], v1) - w->b[k * M + l] <= tol_p)) feas = 0;
+                    }
+                    if (feas) { found = 1; i1 = x; i2 = y; }
+                }
+            }
+            if (found) c = 2;
+            else ok = 0;
+        }
         pc[k] = c; pi1[k] = i1; pi2[k] = i2;
         const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
         const double b2 = w->b2[k];
@@ -1148,7 +1184,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     if (status == 2) goto done;
     /* ---- active-set start (DESIGN.md 4 "Polish"): before any IPM iteration, the polish from the
      *      guess "facets the start point violates" (a warm start: also the facets whose previous
-     *      multiplier exceeds the floor), with up to 6 drop/add passes ---- */
+     *      multiplier exceeds the floor), with up to ORC_GUESS_PASSES drop/add passes ---- */
     if (prm->tol_polish > 0.0) {
         int* gm = (int*)calloc((size_t)N, sizeof(int));
         for (int k = 0; k < N; ++k) {
@@ -1160,7 +1196,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
                 if (ws && warm->lambda[(k + warm->shift) * M + i] > warm->floor) gm[k] |= 1 << i;
             }
         }
-        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, 6);
+        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, ORC_GUESS_PASSES);
         free(gm);
         if (okg) { polished = 1; status = 0; it = 0; goto done; }
     }
