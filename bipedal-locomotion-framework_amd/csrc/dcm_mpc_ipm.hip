@@ -19,10 +19,13 @@
 // same combine order, the reductions in the same xor-butterfly order) and the file is built with
 // -ffp-contract=off, so device and oracle iterates agree bit for bit (tests/test_gpu_dcm_mpc.py).
 // DESIGN.md section 4 is the algorithm statement.
-#include "blf_internal.h"
+#include "dcm_qp_common.h"
+
+#include <stdlib.h>
 
 namespace blf {
 namespace {
+using namespace qp;
 
 #ifdef BLF_STAMPS
 // Diagnostic build only (make stamps): per-phase cycle sums of thread 0 for the first 64 QPs.
@@ -40,13 +43,6 @@ __device__ unsigned long long g_blf_stamps[16];
 #define STAMP_ADD(slot, t0)
 #endif
 
-struct KParams {
-    int N, M, max_iter;
-    int ws_shift;        // warm start: knot k starts from knot k + ws_shift (ws_vrp != nullptr)
-    double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_mu, tol_p, tol_d;
-    double tol_polish;   // > 0: try the active-set polish once mu <= tol_polish
-    double ws_floor;     // warm start: s, lambda >= ws_floor
-};
 
 // LDS carve-up (doubles).  The host sizes the launch with the same code (Lds(nullptr, ...)).
 //   A2  [M][N] double2  facet normals, knot-contiguous per facet (conflict-free b128 reads)
@@ -58,7 +54,6 @@ struct KParams {
 constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
 constexpr int kBV = 8;    // v_{64w} (2): backward-scan value at the first knot of wavefront w
 constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last knot of wavefront w
-constexpr int kGuessPasses = 8;   // active-set start: drop/add passes (oracle: dcm_polish max_pass)
 constexpr int kBnd = 16;
 struct Lds {
     double2 *A2, *BI;   // facet rows: normal (a_x, a_y); (b, 1/s), 1/s later the multiplier step
@@ -228,91 +223,6 @@ struct Reduce {
         return q;
     }
 };
-
-// The facet rows never change during a solve, so the compiler would hoist every phase's row loads
-// out of the IPM loop and keep 8 facets x 4 doubles live in VGPRs across it (spilling).  Each phase
-// indexes the rows through an opaque copy of the knot index instead, so they are re-read from LDS.
-__device__ __forceinline__ int opaque(int k)
-{
-    asm volatile("" : "+v"(k));
-    return k;
-}
-
-// The facet-count predicates (i < m_k per lane, i < mmax per QP) never change during a solve, so
-// the compiler would hoist all 8 of each out of the IPM loop as 64-bit lane masks and spill them
-// to VGPR lanes (46 SGPRs; every use then costs two v_readlane).  Each facet loop reads the counts
-// through these opaque copies instead, so the masks are recomputed per phase (one v_cmp each).
-__device__ __forceinline__ int opaque_s(int k)
-{
-    asm volatile("" : "+s"(k));
-    return k;
-}
-
-// Lane shuffles for the scans.  The source-lane address is recomputed from an opaque lane id
-// at every call: hoisted out of the IPM loop, the twelve shift addresses would stay live in
-// VGPRs for the whole kernel.  Out-of-range sources wrap; the scans never use those values.
-__device__ __forceinline__ double bperm(int addr, double x)
-{
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
-    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Fused forms used throughout (and in the same places by oracle/blf_oracle.c):
-//   FD2(a, b, c, d)    = a b + c d      as fma(a, b, c d)
-//   FD3(a, b, c, d, e) = a b + c d + e  as fma(a, b, fma(c, d, e))
-// fma is correctly rounded on both sides, so kernel and oracle stay bit-identical; it saves one
-// VALU op per product pair (the kernel is VALU-issue bound).
-#define FD2(a, b, c, d) fma((a), (b), (c) * (d))
-#define FD3(a, b, c, d, e) fma((a), (b), fma((c), (d), (e)))
-
-// More than two candidate lines in a polish pass (the drop/add moves can add two facets at once):
-// the first pair (i < j in facet order) whose vertex satisfies every facet of the knot — a vertex
-// of the support polygon — is the active pair (oracle dcm_polish).  Returns 2 with pi1, pi2 set,
-// or 3 (no such pair: the pass fails).  Rare, so it reads the rows straight from LDS.
-__device__ __attribute__((noinline)) int vertex_pair(const double2* A2, const double2* BI, int N, int kx,
-                                                     int km, int cm, double tol_p, int& pi1, int& pi2)
-{
-    for (int x = 0; x < km; ++x) {
-        if (!((cm >> x) & 1)) continue;
-        for (int y = x + 1; y < km; ++y) {
-            if (!((cm >> y) & 1)) continue;
-            const double2 a = A2[x * N + kx];
-            const double2 e = A2[y * N + kx];
-            const double ba = BI[x * N + kx].x, be = BI[y * N + kx].x;
-            const double det = fma(a.x, e.y, -(a.y * e.x));
-            const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
-            if (!(det * det > 1e-18 * (aa * ee))) continue;
-            const double idet = 1.0 / det;
-            const double v0 = fma(ba, e.y, -(a.y * be)) * idet;
-            const double v1 = fma(a.x, be, -(ba * e.x)) * idet;
-            bool feas = true;
-            for (int l = 0; l < km; ++l) {
-                const double2 f = A2[l * N + kx];
-                if (!(FD2(f.x, v0, f.y, v1) - BI[l * N + kx].x <= tol_p)) feas = false;
-            }
-            if (feas) {
-                pi1 = x;
-                pi2 = y;
-                return 2;
-            }
-        }
-    }
-    return 3;
-}
-
-// 2x2 compose (row-major): n = a * b;  nc = a * c + e.
-#define COMPOSE(a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, e0, e1)                 \
-    do {                                                                         \
-        const double n0_ = FD2(a0, b0, a1, b2);                                  \
-        const double n1_ = FD2(a0, b1, a1, b3);                                  \
-        const double n2_ = FD2(a2, b0, a3, b2);                                  \
-        const double n3_ = FD2(a2, b1, a3, b3);                                  \
-        const double m0_ = FD3(a0, c0, a1, c1, e0);                              \
-        const double m1_ = FD3(a2, c0, a3, c1, e1);                              \
-        a0 = n0_; a1 = n1_; a2 = n2_; a3 = n3_; e0 = m0_; e1 = m1_;               \
-    } while (0)
 
 // Backward affine recursion v_k = G_k v_{k+1} + c_k, v_N = 0 (oracle scan_backward).  Lanes past
 // the last knot carry the zero element.  Returns v_{k+1} for this lane's knot.
@@ -497,79 +407,6 @@ __device__ __forceinline__ void xi_prev(const Knot& K, int lane, double xb0, dou
     }
 }
 
-// Riccati map element f(P) = H + A^T P (I + G P)^{-1} A (oracle rc_el); knot k: A = alpha_k I,
-// G = E_k, H = Q.  rc_combine(e, q): e <- e o q (q the later knots), the structure-preserving
-// doubling composition — it inverts only I + G H (eigenvalues >= 1).
-struct Rc {
-    double a0, a1, a2, a3, g0, g1, g2, h0, h1, h2;
-};
-
-__device__ __forceinline__ bool rc_combine(Rc& e, const Rc& q)
-{
-    const double T00 = FD3(e.g0, q.h0, e.g1, q.h1, 1.0);
-    const double T01 = FD2(e.g0, q.h1, e.g1, q.h2);
-    const double T10 = FD2(e.g1, q.h0, e.g2, q.h1);
-    const double T11 = FD3(e.g1, q.h1, e.g2, q.h2, 1.0);
-    const double detT = fma(T00, T11, -(T01 * T10));
-    const bool ok = (detT > 0.0) && !__builtin_isinf(detT);
-    const double it = 1.0 / detT;
-    const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
-    const double U00 = FD2(Ti00, e.a0, Ti01, e.a2);
-    const double U01 = FD2(Ti00, e.a1, Ti01, e.a3);
-    const double U10 = FD2(Ti10, e.a0, Ti11, e.a2);
-    const double U11 = FD2(Ti10, e.a1, Ti11, e.a3);
-    const double V00 = FD2(q.a0, Ti00, q.a1, Ti10);
-    const double V01 = FD2(q.a0, Ti01, q.a1, Ti11);
-    const double V10 = FD2(q.a2, Ti00, q.a3, Ti10);
-    const double V11 = FD2(q.a2, Ti01, q.a3, Ti11);
-    const double X00 = FD2(V00, e.g0, V01, e.g1);
-    const double X01 = FD2(V00, e.g1, V01, e.g2);
-    const double X10 = FD2(V10, e.g0, V11, e.g1);
-    const double X11 = FD2(V10, e.g1, V11, e.g2);
-    const double Y00 = FD2(q.h0, e.a0, q.h1, e.a2);
-    const double Y01 = FD2(q.h0, e.a1, q.h1, e.a3);
-    const double Y10 = FD2(q.h1, e.a0, q.h2, e.a2);
-    const double Y11 = FD2(q.h1, e.a1, q.h2, e.a3);
-    Rc r;
-    r.a0 = FD2(q.a0, U00, q.a1, U10);
-    r.a1 = FD2(q.a0, U01, q.a1, U11);
-    r.a2 = FD2(q.a2, U00, q.a3, U10);
-    r.a3 = FD2(q.a2, U01, q.a3, U11);
-    r.g0 = FD3(X00, q.a0, X01, q.a1, q.g0);
-    r.g1 = FD3(X00, q.a2, X01, q.a3, q.g1);
-    r.g2 = FD3(X10, q.a2, X11, q.a3, q.g2);
-    r.h0 = FD3(U00, Y00, U10, Y10, e.h0);
-    r.h1 = FD3(U00, Y01, U10, Y11, e.h1);
-    r.h2 = FD3(U01, Y01, U11, Y11, e.h2);
-    e = r;
-    return ok;
-}
-
-__device__ __forceinline__ bool rc_apply(const Rc& e, double P00, double P01, double P11,
-                                         double& o00, double& o01, double& o11)
-{
-    const double S00 = FD3(e.g0, P00, e.g1, P01, 1.0);
-    const double S01 = FD2(e.g0, P01, e.g1, P11);
-    const double S10 = FD2(e.g1, P00, e.g2, P01);
-    const double S11 = FD3(e.g1, P01, e.g2, P11, 1.0);
-    const double detS = fma(S00, S11, -(S01 * S10));
-    const bool ok = (detS > 0.0) && !__builtin_isinf(detS);
-    const double is = 1.0 / detS;
-    const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
-    const double W00 = FD2(P00, Si00, P01, Si10);
-    const double W01 = FD2(P00, Si01, P01, Si11);
-    const double W10 = FD2(P01, Si00, P11, Si10);
-    const double W11 = FD2(P01, Si01, P11, Si11);
-    const double Z00 = FD2(W00, e.a0, W01, e.a2);
-    const double Z01 = FD2(W00, e.a1, W01, e.a3);
-    const double Z10 = FD2(W10, e.a0, W11, e.a2);
-    const double Z11 = FD2(W10, e.a1, W11, e.a3);
-    o00 = FD3(e.a0, Z00, e.a2, Z10, e.h0);
-    o01 = FD3(e.a0, Z01, e.a2, Z11, e.h1);
-    o11 = FD3(e.a1, Z01, e.a3, Z11, e.h2);
-    return ok;
-}
-
 // Riccati sweep (oracle riccati_sweep) for this lane's E_k.  Leaves P_{k+1} in K.  Returns false
 // on this lane if some (I + G H) or (I + G P) is not positive definite.
 template <int NW>
@@ -744,6 +581,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     const bool own = k < N;
     const bool last = k == N - 1;
     const int64_t p = blockIdx.x;
+    // after the active-set kernel (dcm_mpc_as.hip): only the QPs it handed over
+    if (P.stage2 && status_out[p] != kPending) return;
     constexpr bool warm = WARM;                           // a separate instantiation each way
     const bool ws = warm && k + P.ws_shift < N;           // this knot starts from the warm start
     STAMP(t_start);
@@ -765,7 +604,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         if (bad) K.m = 0;
         K.w = omega[st];
         K.be = P.dt * K.w;
-        const double* r0 = ws ? ws_vrp + 2 * P.ws_shift : vrp_ref;
+        // stage 2: the start point the active-set kernel left in the outputs
+        const double* r0 = P.stage2 ? vrp_out : ws ? ws_vrp + 2 * P.ws_shift : vrp_ref;
         K.r0 = r0[2 * st];
         K.r1 = r0[2 * st + 1];
         const double* Ak = Ain + st * M * 2;
@@ -795,7 +635,17 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     //      trajectory) ----
     // xb = xi_{64 wv}, the left boundary of this wavefront (lane 0 uses it; wavefront 0: xi_init)
     double xb0 = xi00, xb1 = xi01;
-    if (!warm) {
+    if (P.stage2) {   // the start point (the LQ optimum or the warm rollout) from the outputs
+        const double* xo = xi_out + 2 * p * (N + 1);
+        if (own) {
+            K.x0 = xo[2 * (k + 1)];
+            K.x1 = xo[2 * (k + 1) + 1];
+        }
+        if (wv > 0) {
+            xb0 = xo[2 * kWave * wv];
+            xb1 = xo[2 * kWave * wv + 1];
+        }
+    } else if (!warm) {
         if (own) {
             K.x0 = xref[0];
             K.x1 = xref[1];
@@ -833,7 +683,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         // ---- initial point 2: full Newton step of the unconstrained QP (W = 0, lam = 0);
         //      a warm start skips it ----
         STAMP(t_lq);
-        if (!warm) {
+        if (!warm && !P.stage2) {
             xi_prev(K, lane, xb0, xb1, xk0, xk1);
             if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
             ok = factor<NW>(K, P, 0.0, 0.0, 0.0, 0.0, bnd, N, nwa, k, wv, lane, own);
@@ -921,7 +771,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
         int pass = 0;    // the polish pass the next loop top runs (uniform)
         // active-set start (oracle: before its IPM loop): the first polish runs before any IPM
         // iteration from the guess gm, with up to kGuessPasses drop/add passes
-        bool guess = P.tol_polish > 0.0;
+        bool guess = P.tol_polish > 0.0 && !P.stage2;
         for (it = 0; status == 0; ++it) {
             // ---- residuals (knot-parallel) ----
             STAMP(t_r);
@@ -962,7 +812,7 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
                             cm |= 1 << i;
                         }
                     }
-                    if (pc > 2) pc = vertex_pair(L.A2, L.BI, N, kx, km, cm, P.tol_p, pi1, pi2);
+                    if (pc > 2) pc = vertex_pair(L.A2, reinterpret_cast<const double*>(L.BI), 2, N, kx, km, cm, P.tol_p, pi1, pi2);
                     okp = pc <= 2;
                     pk = (pc < 3 ? pc : 2) | (pi1 << 2) | (pi2 << 5);
                     const double b2 = K.be * K.be;
@@ -1431,9 +1281,20 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     kp.tol_polish = prm->tol_polish;
     kp.ws_shift = warm ? warm->shift : 0;
     kp.ws_floor = warm ? warm->floor : 0.0;
+    kp.stage2 = 0;
     if (batch == 0) return BLF_OK;
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     const int N = kp.N;
+    // With the active-set start (tol_polish > 0) and N <= 128, the one-wavefront active-set kernel
+    // solves the QPs its start certifies; this kernel then takes only the rest (stage 2), from
+    // scratch and without the start.  BLF_QP_SINGLE_KERNEL=1 keeps everything in this kernel
+    // (A/B and parity tests: both ways give the same bits).
+    const char* single = getenv("BLF_QP_SINGLE_KERNEL");
+    if (kp.tol_polish > 0.0 && N <= 2 * kWave && !(single && single[0] == '1')) {
+        const blf_status st = launch_dcm_mpc_as(kp, pb, warm, batch, sol, lam_out, s);
+        if (st != BLF_OK) return st;
+        kp.stage2 = 1;
+    }
     if (N <= 64) return launch_nt<64>(kp, pb, warm, batch, sol, lam_out, s);
     if (N <= 128) return launch_nt<128>(kp, pb, warm, batch, sol, lam_out, s);
     if (N <= 256) return launch_nt<256>(kp, pb, warm, batch, sol, lam_out, s);

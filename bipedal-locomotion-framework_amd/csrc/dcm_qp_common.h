@@ -1,0 +1,191 @@
+// dcm_qp_common.h — device pieces shared by the DCM-MPC QP kernels (dcm_mpc_ipm.hip: the
+// general interior point kernel; dcm_mpc_as.hip: the one-wavefront active-set kernel).  Both
+// mirror oracle/blf_oracle.c term for term (same fused forms, same scan combine order), so their
+// results agree with the oracle and with each other bit for bit.
+#pragma once
+#include "blf_internal.h"
+
+namespace blf {
+namespace qp {
+
+constexpr int kGuessPasses = 8;   // active-set start: drop/add passes (oracle: ORC_GUESS_PASSES)
+constexpr int kPending = -1;      // status of a QP the active-set kernel hands to the IPM kernel
+
+struct KParams {
+    int N, M, max_iter;
+    int ws_shift;        // warm start: knot k starts from knot k + ws_shift (ws_vrp != nullptr)
+    double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_mu, tol_p, tol_d;
+    double tol_polish;   // > 0: try the active-set polish once mu <= tol_polish
+    double ws_floor;     // warm start: s, lambda >= ws_floor
+    int stage2;          // IPM kernel after the active-set kernel: only QPs with status kPending,
+                         // and no active-set start (it already failed for them)
+};
+
+// The facet rows never change during a solve, so the compiler would hoist every phase's row loads
+// out of the IPM loop and keep 8 facets x 4 doubles live in VGPRs across it (spilling).  Each phase
+// indexes the rows through an opaque copy of the knot index instead, so they are re-read from LDS.
+__device__ __forceinline__ int opaque(int k)
+{
+    asm volatile("" : "+v"(k));
+    return k;
+}
+
+// The facet-count predicates (i < m_k per lane, i < mmax per QP) never change during a solve, so
+// the compiler would hoist all 8 of each out of the IPM loop as 64-bit lane masks and spill them
+// to VGPR lanes (46 SGPRs; every use then costs two v_readlane).  Each facet loop reads the counts
+// through these opaque copies instead, so the masks are recomputed per phase (one v_cmp each).
+__device__ __forceinline__ int opaque_s(int k)
+{
+    asm volatile("" : "+s"(k));
+    return k;
+}
+
+// Lane shuffles for the scans.  The source-lane address is recomputed from an opaque lane id
+// at every call: hoisted out of the IPM loop, the twelve shift addresses would stay live in
+// VGPRs for the whole kernel.  Out-of-range sources wrap; the scans never use those values.
+__device__ __forceinline__ double bperm(int addr, double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Fused forms used throughout (and in the same places by oracle/blf_oracle.c):
+//   FD2(a, b, c, d)    = a b + c d      as fma(a, b, c d)
+//   FD3(a, b, c, d, e) = a b + c d + e  as fma(a, b, fma(c, d, e))
+// fma is correctly rounded on both sides, so kernel and oracle stay bit-identical; it saves one
+// VALU op per product pair (the kernel is VALU-issue bound).
+#define FD2(a, b, c, d) fma((a), (b), (c) * (d))
+#define FD3(a, b, c, d, e) fma((a), (b), fma((c), (d), (e)))
+
+// More than two candidate lines in a polish pass (the drop/add moves can add two facets at once):
+// the first pair (i < j in facet order) whose vertex satisfies every facet of the knot — a vertex
+// of the support polygon — is the active pair (oracle dcm_polish).  Returns 2 with pi1, pi2 set,
+// or 3 (no such pair: the pass fails).  Rare, so it reads the rows straight from LDS.
+// The offsets are read as Bo[(i N + kx) * bs] (bs = 2: the IPM kernel's (b, 1/s) pairs).
+static __device__ __attribute__((noinline)) int vertex_pair(const double2* A2, const double* Bo, int bs, int N,
+                                                            int kx, int km, int cm, double tol_p, int& pi1,
+                                                            int& pi2)
+{
+    for (int x = 0; x < km; ++x) {
+        if (!((cm >> x) & 1)) continue;
+        for (int y = x + 1; y < km; ++y) {
+            if (!((cm >> y) & 1)) continue;
+            const double2 a = A2[x * N + kx];
+            const double2 e = A2[y * N + kx];
+            const double ba = Bo[(x * N + kx) * bs], be = Bo[(y * N + kx) * bs];
+            const double det = fma(a.x, e.y, -(a.y * e.x));
+            const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
+            if (!(det * det > 1e-18 * (aa * ee))) continue;
+            const double idet = 1.0 / det;
+            const double v0 = fma(ba, e.y, -(a.y * be)) * idet;
+            const double v1 = fma(a.x, be, -(ba * e.x)) * idet;
+            bool feas = true;
+            for (int l = 0; l < km; ++l) {
+                const double2 f = A2[l * N + kx];
+                if (!(FD2(f.x, v0, f.y, v1) - Bo[(l * N + kx) * bs] <= tol_p)) feas = false;
+            }
+            if (feas) {
+                pi1 = x;
+                pi2 = y;
+                return 2;
+            }
+        }
+    }
+    return 3;
+}
+
+// 2x2 compose (row-major): n = a * b;  nc = a * c + e.
+#define COMPOSE(a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, e0, e1)                 \
+    do {                                                                         \
+        const double n0_ = FD2(a0, b0, a1, b2);                                  \
+        const double n1_ = FD2(a0, b1, a1, b3);                                  \
+        const double n2_ = FD2(a2, b0, a3, b2);                                  \
+        const double n3_ = FD2(a2, b1, a3, b3);                                  \
+        const double m0_ = FD3(a0, c0, a1, c1, e0);                              \
+        const double m1_ = FD3(a2, c0, a3, c1, e1);                              \
+        a0 = n0_; a1 = n1_; a2 = n2_; a3 = n3_; e0 = m0_; e1 = m1_;               \
+    } while (0)
+
+// Riccati map element f(P) = H + A^T P (I + G P)^{-1} A (oracle rc_el); knot k: A = alpha_k I,
+// G = E_k, H = Q.  rc_combine(e, q): e <- e o q (q the later knots), the structure-preserving
+// doubling composition — it inverts only I + G H (eigenvalues >= 1).
+struct Rc {
+    double a0, a1, a2, a3, g0, g1, g2, h0, h1, h2;
+};
+
+__device__ __forceinline__ bool rc_combine(Rc& e, const Rc& q)
+{
+    const double T00 = FD3(e.g0, q.h0, e.g1, q.h1, 1.0);
+    const double T01 = FD2(e.g0, q.h1, e.g1, q.h2);
+    const double T10 = FD2(e.g1, q.h0, e.g2, q.h1);
+    const double T11 = FD3(e.g1, q.h1, e.g2, q.h2, 1.0);
+    const double detT = fma(T00, T11, -(T01 * T10));
+    const bool ok = (detT > 0.0) && !__builtin_isinf(detT);
+    const double it = 1.0 / detT;
+    const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
+    const double U00 = FD2(Ti00, e.a0, Ti01, e.a2);
+    const double U01 = FD2(Ti00, e.a1, Ti01, e.a3);
+    const double U10 = FD2(Ti10, e.a0, Ti11, e.a2);
+    const double U11 = FD2(Ti10, e.a1, Ti11, e.a3);
+    const double V00 = FD2(q.a0, Ti00, q.a1, Ti10);
+    const double V01 = FD2(q.a0, Ti01, q.a1, Ti11);
+    const double V10 = FD2(q.a2, Ti00, q.a3, Ti10);
+    const double V11 = FD2(q.a2, Ti01, q.a3, Ti11);
+    const double X00 = FD2(V00, e.g0, V01, e.g1);
+    const double X01 = FD2(V00, e.g1, V01, e.g2);
+    const double X10 = FD2(V10, e.g0, V11, e.g1);
+    const double X11 = FD2(V10, e.g1, V11, e.g2);
+    const double Y00 = FD2(q.h0, e.a0, q.h1, e.a2);
+    const double Y01 = FD2(q.h0, e.a1, q.h1, e.a3);
+    const double Y10 = FD2(q.h1, e.a0, q.h2, e.a2);
+    const double Y11 = FD2(q.h1, e.a1, q.h2, e.a3);
+    Rc r;
+    r.a0 = FD2(q.a0, U00, q.a1, U10);
+    r.a1 = FD2(q.a0, U01, q.a1, U11);
+    r.a2 = FD2(q.a2, U00, q.a3, U10);
+    r.a3 = FD2(q.a2, U01, q.a3, U11);
+    r.g0 = FD3(X00, q.a0, X01, q.a1, q.g0);
+    r.g1 = FD3(X00, q.a2, X01, q.a3, q.g1);
+    r.g2 = FD3(X10, q.a2, X11, q.a3, q.g2);
+    r.h0 = FD3(U00, Y00, U10, Y10, e.h0);
+    r.h1 = FD3(U00, Y01, U10, Y11, e.h1);
+    r.h2 = FD3(U01, Y01, U11, Y11, e.h2);
+    e = r;
+    return ok;
+}
+
+__device__ __forceinline__ bool rc_apply(const Rc& e, double P00, double P01, double P11,
+                                         double& o00, double& o01, double& o11)
+{
+    const double S00 = FD3(e.g0, P00, e.g1, P01, 1.0);
+    const double S01 = FD2(e.g0, P01, e.g1, P11);
+    const double S10 = FD2(e.g1, P00, e.g2, P01);
+    const double S11 = FD3(e.g1, P01, e.g2, P11, 1.0);
+    const double detS = fma(S00, S11, -(S01 * S10));
+    const bool ok = (detS > 0.0) && !__builtin_isinf(detS);
+    const double is = 1.0 / detS;
+    const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
+    const double W00 = FD2(P00, Si00, P01, Si10);
+    const double W01 = FD2(P00, Si01, P01, Si11);
+    const double W10 = FD2(P01, Si00, P11, Si10);
+    const double W11 = FD2(P01, Si01, P11, Si11);
+    const double Z00 = FD2(W00, e.a0, W01, e.a2);
+    const double Z01 = FD2(W00, e.a1, W01, e.a3);
+    const double Z10 = FD2(W10, e.a0, W11, e.a2);
+    const double Z11 = FD2(W10, e.a1, W11, e.a3);
+    o00 = FD3(e.a0, Z00, e.a2, Z10, e.h0);
+    o01 = FD3(e.a0, Z01, e.a2, Z11, e.h1);
+    o11 = FD3(e.a1, Z01, e.a3, Z11, e.h2);
+    return ok;
+}
+
+}  // namespace qp
+
+// dcm_mpc_as.hip: the one-wavefront active-set kernel (N <= 128); QPs it does not certify are left
+// with status qp::kPending for the IPM kernel's stage 2.
+blf_status launch_dcm_mpc_as(const qp::KParams& kp, const blf_dcm_mpc_problem* pb,
+                             const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                             const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s);
+}  // namespace blf

@@ -352,6 +352,7 @@ double orc_wave_tree_sum(const double* c, int n)
 typedef struct {
     int N, M, NW, ntot;
     int scans;                             /* 1: device-order Kogge-Stone scans, 0: sequential */
+    int pairs;                             /* 1: the active-set kernel's pair tree (64 < N <= 128) */
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1;
     const double *omega, *xi_ref, *vrp_ref, *A, *b;
     const int32_t* nf;
@@ -369,6 +370,110 @@ typedef struct {
 
 static double keepmax(double q, double x) { return x > q ? x : q; }
 static double nanmax(double q, double x) { return (x > q || x != x) ? x : q; }
+
+/* ---- the active-set kernel's scan tree (csrc/dcm_mpc_as.hip, 64 < N <= 128): lane l of ONE
+ * wavefront owns the knot pair (2l, 2l + 1); the pair's element is composed in the lane, a
+ * Kogge-Stone scan runs over the 64 lanes, and the pair's inner knot is applied in the lane.
+ * Knots >= N carry the zero element (affine scans) or the identity (Riccati), as in the wavefront
+ * tree above. ---- */
+
+/* 2x2 affine compose: (a, e) <- (a b, a c + e), the COMPOSE of the device */
+static void aff_compose(double* a, double* e, const double* b, const double* c)
+{
+    const double n0 = FD2(a[0], b[0], a[1], b[2]);
+    const double n1 = FD2(a[0], b[1], a[1], b[3]);
+    const double n2 = FD2(a[2], b[0], a[3], b[2]);
+    const double n3 = FD2(a[2], b[1], a[3], b[3]);
+    const double m0 = FD3(a[0], c[0], a[1], c[1], e[0]);
+    const double m1 = FD3(a[2], c[0], a[3], c[1], e[1]);
+    a[0] = n0; a[1] = n1; a[2] = n2; a[3] = n3; e[0] = m0; e[1] = m1;
+}
+
+static void scan_backward_pairs(dcm_ws* w, const double* G, const double* c)
+{
+    const int N = w->N;
+    double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
+    for (int l = 0; l < WV; ++l) {
+        const int k0 = 2 * l, k1 = 2 * l + 1;
+        for (int j = 0; j < 4; ++j) g[l][j] = k0 < N ? G[4 * k0 + j] : 0.0;
+        for (int j = 0; j < 2; ++j) e[l][j] = k0 < N ? c[2 * k0 + j] : 0.0;
+        double b[4], cc[2];
+        for (int j = 0; j < 4; ++j) b[j] = k1 < N ? G[4 * k1 + j] : 0.0;
+        for (int j = 0; j < 2; ++j) cc[j] = k1 < N ? c[2 * k1 + j] : 0.0;
+        aff_compose(g[l], e[l], b, cc);            /* knot 2l after knot 2l + 1 */
+    }
+    for (int dd = 1; dd < WV; dd <<= 1) {
+        for (int l = 0; l < WV; ++l) {
+            memcpy(ng[l], g[l], sizeof(ng[l]));
+            memcpy(ne[l], e[l], sizeof(ne[l]));
+            if (l + dd < WV) aff_compose(ng[l], ne[l], g[l + dd], e[l + dd]);
+        }
+        memcpy(g, ng, sizeof(g));
+        memcpy(e, ne, sizeof(e));
+    }
+    for (int l = 0; l < WV; ++l) {               /* v_{2l} = e_l; v_{2l+1} = G v_{2l+2} + c */
+        const int k0 = 2 * l, k1 = 2 * l + 1;
+        if (k0 < N) { w->v[2 * k0] = e[l][0]; w->v[2 * k0 + 1] = e[l][1]; }
+        if (k1 < N) {
+            const double vb0 = l + 1 < WV ? e[l + 1][0] : 0.0, vb1 = l + 1 < WV ? e[l + 1][1] : 0.0;
+            const double* Gk = G + 4 * k1;
+            w->v[2 * k1] = FD3(Gk[0], vb0, Gk[1], vb1, c[2 * k1]);
+            w->v[2 * k1 + 1] = FD3(Gk[2], vb0, Gk[3], vb1, c[2 * k1 + 1]);
+        }
+    }
+}
+
+static void scan_forward_pairs(dcm_ws* w, const double* F, int transpose, const double* f)
+{
+    const int N = w->N;
+    double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
+    double F0[WV][4], f0[WV][2];
+    for (int l = 0; l < WV; ++l) {
+        const int ks[2] = {2 * l, 2 * l + 1};
+        double Fk[2][4], fk[2][2];
+        for (int q = 0; q < 2; ++q) {
+            const int k = ks[q];
+            if (k < N) {
+                const double* Fp = F + 4 * k;
+                Fk[q][0] = Fp[0];
+                Fk[q][1] = transpose ? Fp[2] : Fp[1];
+                Fk[q][2] = transpose ? Fp[1] : Fp[2];
+                Fk[q][3] = Fp[3];
+                fk[q][0] = f[2 * k];
+                fk[q][1] = f[2 * k + 1];
+            } else {
+                Fk[q][0] = Fk[q][1] = Fk[q][2] = Fk[q][3] = 0.0;
+                fk[q][0] = fk[q][1] = 0.0;
+            }
+        }
+        memcpy(F0[l], Fk[0], sizeof(F0[l]));
+        memcpy(f0[l], fk[0], sizeof(f0[l]));
+        memcpy(g[l], Fk[1], sizeof(g[l]));
+        memcpy(e[l], fk[1], sizeof(e[l]));
+        aff_compose(g[l], e[l], Fk[0], fk[0]);     /* knot 2l + 1 after knot 2l */
+    }
+    for (int dd = 1; dd < WV; dd <<= 1) {
+        for (int l = 0; l < WV; ++l) {
+            memcpy(ng[l], g[l], sizeof(ng[l]));
+            memcpy(ne[l], e[l], sizeof(ne[l]));
+            if (l - dd >= 0) aff_compose(ng[l], ne[l], g[l - dd], e[l - dd]);
+        }
+        memcpy(g, ng, sizeof(g));
+        memcpy(e, ne, sizeof(e));
+    }
+    for (int l = 0; l < WV; ++l) {               /* x_{2l+2} = e_l; x_{2l+1} = F x_{2l} + f */
+        const int k0 = 2 * l, k1 = 2 * l + 1;
+        const double xb0 = l > 0 ? e[l - 1][0] : 0.0, xb1 = l > 0 ? e[l - 1][1] : 0.0;
+        if (k0 < N) {
+            w->x[2 * (k0 + 1)] = FD3(F0[l][0], xb0, F0[l][1], xb1, f0[l][0]);
+            w->x[2 * (k0 + 1) + 1] = FD3(F0[l][2], xb0, F0[l][3], xb1, f0[l][1]);
+        }
+        if (k1 < N) {
+            w->x[2 * (k1 + 1)] = e[l][0];
+            w->x[2 * (k1 + 1) + 1] = e[l][1];
+        }
+    }
+}
 
 /* Backward affine recursion v_k = G_k v_{k+1} + c_k (v_N = 0) the way the device evaluates it:
  * a Kogge-Stone scan over the 64 lanes of each wavefront (lane l combines with lane l + d from
@@ -389,6 +494,7 @@ static void scan_backward(dcm_ws* w, const double* G, const double* c)
         }
         return;
     }
+    if (w->pairs) { scan_backward_pairs(w, G, c); return; }
     for (int wv = w->NW - 1; wv >= 0; --wv) {
         double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
         for (int l = 0; l < WV; ++l) {
@@ -450,6 +556,7 @@ static void scan_forward(dcm_ws* w, const double* F, int transpose, const double
         }
         return;
     }
+    if (w->pairs) { scan_forward_pairs(w, F, transpose, f); return; }
     for (int wv = 0; wv < w->NW; ++wv) {
         double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
         for (int l = 0; l < WV; ++l) {
@@ -630,6 +737,62 @@ static int rc_apply(const rc_el* e, double P00, double P01, double P11, double* 
     return ok;
 }
 
+/* The Riccati map element of knot k (identity for k >= N). */
+static void rc_knot(const dcm_ws* w, int k, rc_el* e)
+{
+    if (k < w->N) {
+        e->a[0] = w->al[k]; e->a[1] = 0.0; e->a[2] = 0.0; e->a[3] = w->al[k];
+        e->g[0] = w->E[3 * k]; e->g[1] = w->E[3 * k + 1]; e->g[2] = w->E[3 * k + 2];
+        e->h[0] = w->Qw0; e->h[1] = 0.0; e->h[2] = w->Qw1;
+    } else {
+        e->a[0] = 1.0; e->a[1] = 0.0; e->a[2] = 0.0; e->a[3] = 1.0;
+        e->g[0] = e->g[1] = e->g[2] = 0.0;
+        e->h[0] = e->h[1] = e->h[2] = 0.0;
+    }
+}
+
+/* riccati_sweep in the active-set kernel's pair tree (lane l: knots 2l, 2l + 1; see
+ * scan_backward_pairs): the pair element e_{2l} o e_{2l+1}, Kogge-Stone over the 64 lanes,
+ * P_{2l} = f(P_N), then P_{2l+1} = f_{2l+1}(P_{2l+2}) in the lane (P_{2l+2} from lane l + 1). */
+static int riccati_sweep_pairs(dcm_ws* w)
+{
+    const int N = w->N;
+    int ok = 1;
+    rc_el e[WV], ne[WV];
+    for (int l = 0; l < WV; ++l) {
+        rc_el e1;
+        rc_knot(w, 2 * l, &e[l]);
+        rc_knot(w, 2 * l + 1, &e1);
+        if (!rc_combine(&e[l], &e1)) ok = 0;
+    }
+    for (int dd = 1; dd < WV; dd <<= 1) {
+        for (int l = 0; l < WV; ++l) {
+            ne[l] = e[l];
+            if (l + dd < WV && !rc_combine(&ne[l], &e[l + dd])) ok = 0;
+        }
+        memcpy(e, ne, sizeof(e));
+    }
+    double P0[WV][3];
+    for (int l = 0; l < WV; ++l)
+        if (!rc_apply(&e[l], w->Pw0, 0.0, w->Pw1, P0[l])) ok = 0;
+    for (int l = 0; l < WV; ++l) {
+        const int k0 = 2 * l, k1 = 2 * l + 1;
+        rc_el e1;
+        rc_knot(w, k1, &e1);
+        double Pn[3] = {w->Pw0, 0.0, w->Pw1};
+        if (l + 1 < WV) { Pn[0] = P0[l + 1][0]; Pn[1] = P0[l + 1][1]; Pn[2] = P0[l + 1][2]; }
+        double P1[3];
+        if (!rc_apply(&e1, Pn[0], Pn[1], Pn[2], P1)) ok = 0;
+        /* P_{k+1} of knot k: knot 2l takes P_{2l+1}, knot 2l + 1 takes P_{2l+2} */
+        if (k0 < N) { w->Pn[3 * k0] = P1[0]; w->Pn[3 * k0 + 1] = P1[1]; w->Pn[3 * k0 + 2] = P1[2]; }
+        if (k1 < N) { w->Pn[3 * k1] = Pn[0]; w->Pn[3 * k1 + 1] = Pn[1]; w->Pn[3 * k1 + 2] = Pn[2]; }
+    }
+    w->Pn[3 * (N - 1)] = w->Pw0;
+    w->Pn[3 * (N - 1) + 1] = 0.0;
+    w->Pn[3 * (N - 1) + 2] = w->Pw1;
+    return ok;
+}
+
 /* Riccati sweep for the per-knot E_k = w->E: P_k for every knot by a Kogge-Stone
  * scan of Riccati map elements over the 64 lanes of each wavefront (lane l composes with lane
  * l + d), then P_k = f_{k..}(P at the next wavefront's first knot, or P_N = diag(Pw)), wavefronts
@@ -652,6 +815,7 @@ static int riccati_sweep(dcm_ws* w)
             Pb0 = out[0]; Pb1 = out[1]; Pb2 = out[2];
         }
     }
+    if (w->scans && w->pairs) return riccati_sweep_pairs(w);
     for (int wv = w->scans ? w->NW - 1 : -1; wv >= 0; --wv) {
         rc_el e[WV], ne[WV];
         for (int l = 0; l < WV; ++l) {
@@ -1097,6 +1261,11 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     dcm_ws* w = &ws;
     w->N = N; w->M = M; w->NW = (N + WV - 1) / WV; w->dt = prm->dt;
     w->scans = prm->sequential ? 0 : 1;
+    /* the start point and the active-set start are evaluated as the device's active-set kernel
+     * evaluates them (one wavefront, knot pairs per lane) when that kernel runs: 64 < N <= 128
+     * with the start enabled (csrc/dcm_mpc_ipm.hip launch_dcm_mpc); the IPM iterations always in
+     * the wavefront tree of the IPM kernel */
+    w->pairs = (prm->tol_polish > 0.0 && N > WV && N <= 2 * WV && !prm->single_kernel) ? 1 : 0;
     w->Qw0 = prm->w_xi[0]; w->Qw1 = prm->w_xi[1];
     w->Rw0 = prm->w_vrp[0]; w->Rw1 = prm->w_vrp[1];
     w->Pw0 = prm->w_terminal[0]; w->Pw1 = prm->w_terminal[1];
@@ -1203,6 +1372,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     /* the interior point method's own start (only when the active-set start did not certify):
      * the start point was restored exactly */
 
+    w->pairs = 0;   /* the IPM kernel's tree from here on */
     /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s; warm: s = max(b - A r, floor),
      *      lam = max(lam_warm[src], floor) with the same source knot as the VRP ---- */
     double dres = 0.0;

@@ -79,6 +79,8 @@ typedef struct orc_dcm_params {
     int32_t horizon, max_facets, max_iter, sequential;
     double dt, w_xi[2], w_vrp[2], w_terminal[2], tol_mu, tol_primal, tol_dual;
     double tol_polish;   /* > 0: try the active-set polish once mu <= tol_polish */
+    int32_t single_kernel;   /* 1: the device's BLF_QP_SINGLE_KERNEL=1 path (IPM kernel alone) */
+    int32_t reserved;
 } orc_dcm_params;
 
 /* Solve one problem (arrays for this problem only, same layout as blf_dcm_mpc_problem).

@@ -22,7 +22,8 @@ class OrcParams(ctypes.Structure):
                 ("dt", ctypes.c_double), ("w_xi", ctypes.c_double * 2),
                 ("w_vrp", ctypes.c_double * 2), ("w_terminal", ctypes.c_double * 2),
                 ("tol_mu", ctypes.c_double), ("tol_primal", ctypes.c_double),
-                ("tol_dual", ctypes.c_double), ("tol_polish", ctypes.c_double)]
+                ("tol_dual", ctypes.c_double), ("tol_polish", ctypes.c_double),
+                ("single_kernel", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 def build():
@@ -183,6 +184,8 @@ def default_params(horizon, **kw):
     p.tol_primal = kw.get("tol_primal", 1e-10)
     p.tol_dual = kw.get("tol_dual", 1e-9)
     p.tol_polish = kw.get("tol_polish", 3e-4)   # blf_dcm_mpc_default_params
+    # 1: evaluate as the device's BLF_QP_SINGLE_KERNEL=1 path (the IPM kernel alone)
+    p.single_kernel = int(kw.get("single_kernel", 0))
     return p
 
 

@@ -234,3 +234,43 @@ def test_dcm_mpc_polish_refusal_matches_oracle_bitwise(handle, oracle):
     np.testing.assert_array_equal(out["iters"].cpu().numpy(), it_o)
     np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi_o)
     np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)
+
+
+@pytest.mark.parametrize("horizon,footsteps", [(100, 6), (50, 4), (128, 8), (65, 4)])
+def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, footsteps, monkeypatch):
+    """The default path for N <= 128 (csrc/dcm_mpc_as.hip: one wavefront per QP, knot pairs per
+    lane, then the IPM kernel's stage 2 on the QPs it hands over) and the IPM kernel alone
+    (BLF_QP_SINGLE_KERNEL=1, the wavefront scan tree) each equal the oracle evaluated the same way
+    bit for bit, cold and warm; the two trees agree to rounding (both are certified optima)."""
+    B = 1024
+    prob = P.make_batch(B, horizon=horizon, n_footsteps=footsteps, seed=5)
+    dev = _gpu_problem(handle, prob)
+    host = dict(prob)
+    for k in ("A", "b", "nfacets"):
+        host[k] = dev[k].cpu().numpy()
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BLF_QP_SINGLE_KERNEL", mode)
+        prm_o = oracle.default_params(horizon, single_kernel=int(mode))
+        out = handle.dcm_mpc_solve(dev, lambda_out=True)
+        torch.cuda.synchronize()
+        cold = {k: v.cpu().numpy().copy() for k, v in out.items()}
+        pol = np.zeros(B, np.int32)
+        st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(host, params=prm_o, threads=8, polished=pol)
+        for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
+                       ("polished", pol)):
+            np.testing.assert_array_equal(cold[k], ref, err_msg=f"cold {k} mode {mode}")
+        warm = dict(vrp=out["vrp"], lam=out["lam"], shift=1, floor=1e-3)
+        outw = handle.dcm_mpc_solve(dev, warm=warm, lambda_out=True)
+        torch.cuda.synchronize()
+        pol = np.zeros(B, np.int32)
+        st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(
+            host, vrp_ws=cold["vrp"], lam_ws=cold["lam"], shift=1, floor=1e-3, params=prm_o,
+            threads=8, polished=pol)
+        for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
+                       ("polished", pol)):
+            np.testing.assert_array_equal(outw[k].cpu().numpy(), ref, err_msg=f"warm {k} mode {mode}")
+        res[mode] = cold
+    assert (res["0"]["status"] == 0).all()
+    assert np.abs(res["0"]["xi"] - res["1"]["xi"]).max() <= 1e-12
+    assert np.abs(res["0"]["vrp"] - res["1"]["vrp"]).max() <= 1e-12
