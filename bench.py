@@ -12,7 +12,8 @@ Prints ONE JSON line on rank 0 (the driver's contract), with two extra objects:
                 per QP and the kernel's average duration measured with HIP
                 events on the launch stream; plus the counted-flop fp64 fraction and the VALU
                 issue fraction (the roof that binds this kernel).
-  cpu_baseline  the CPU oracle (same IPM, C, -O2, one problem per thread) on this host's cores,
+  cpu_baseline  the CPU oracle (same algorithm, C, gcc -O3, one problem per thread)
+                on every CPU this process may use (affinity set capped by the cgroup CPU quota),
                 rank 0 only, on a bounded sample.
 """
 import argparse
@@ -49,7 +50,7 @@ def profiled_summary():
         return None, None
     with open(files[-1]) as f:
         s = json.load(f)
-    if "dcm_mpc_ipm" not in s.get("dominant_kernel", ""):
+    if not any(n in s.get("dominant_kernel", "") for n in ("dcm_mpc_as", "dcm_mpc_ipm")):
         return None, None
     return s, os.path.relpath(files[-1], ROOT)
 
@@ -105,8 +106,31 @@ def cpu_baseline(host, N, seconds, threads):
     return dict(value=solved / el, unit="QP/s", cores=threads, kind="port",
                 sample=f"{solved} solves = {solved // B} passes over the same {B} horizon-{N} QPs "
                        f"in {el:.2f} s wall on {threads} threads (oracle/blf_oracle.c sequential "
-                       f"mode, gcc -O2, one problem per thread)",
-                single_thread_latency_us=round(lat_us, 1))
+                       f"mode, gcc -O3 -mfma, one problem per thread)",
+                single_thread_latency_us=round(lat_us, 1), **host_cpu_info())
+
+
+def cpu_threads():
+    """The CPUs this process can actually run on: the affinity set, capped by the cgroup CPU quota
+    when there is one (a GPU box shows the whole machine in its affinity set, 256 CPUs, but grants
+    one GPU's process a quota of 16; more threads than the quota only time-slice)."""
+    info = host_cpu_info()
+    n = info["affinity_cpus"]
+    if info["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(info["cgroup_cpu_quota"])))
+    return n
+
+
+def host_cpu_info():
+    """What the host offers this process: the affinity set, the cgroup CPU quota (if any) and
+    os.cpu_count(); the CPU baseline runs one thread per CPU of the affinity set."""
+    info = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    return info
 
 
 def main():
@@ -114,7 +138,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="QPs per GPU")
+    ap.add_argument("--batch", type=int, default=4096, help="QPs per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="QPs over all GPUs, split into contiguous per-rank shards (strong scaling; "
+                         "configs[3] is --global-batch 262144 on 8 GPUs)")
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -139,6 +166,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        # checked before any HIP call: a scaling run launched without torch.distributed.run would
+        # otherwise measure one GPU and report it as n_gpus = 1
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 with "
+                 f"python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
+    if args.global_batch is not None:
+        if args.global_batch % world:
+            sys.exit(f"bench.py: --global-batch {args.global_batch} is not divisible by {world} ranks")
+        args.batch = args.global_batch // world
     # RCCL (backend "nccl") over xGMI on a node; BLF_BENCH_BACKEND=gloo rehearses the multi-rank
     # path on a single GPU (every rank then shares device LOCAL_RANK % device_count)
     backend = os.environ.get("BLF_BENCH_BACKEND", "nccl")
@@ -192,9 +228,7 @@ def main():
         elapsed = float(t.item())
 
     iters = out["iters"].to(torch.int64)
-    active = d["nfacets"].to(torch.int64).sum(dim=1)
-    flops = sum(native.flops_per_iter(N, int(a)) * int(i)
-                for a, i in zip(active.cpu().numpy(), iters.cpu().numpy()))
+    polished = out["polished"].to(torch.float64)
 
     # RCCL gather of every rank's solutions to rank 0 (timed separately, not in `value`)
     gather_ms = None
@@ -213,14 +247,14 @@ def main():
         bpq = algorithmic_bytes_per_qp(N, M)
         achieved = bpq * B / (kernel_ms * 1e-3) / 1e9
         traffic, traffic_src = profiled_traffic()
-        fp64_tf = flops / (kernel_ms * 1e-3) / 1e12
-        # executed fp64 flops of the launch from the committed SQ pass (FMA counts two, 64 lanes
-        # per wave instruction): covers the polish passes and the scans' redundant work, which
-        # the sequential-form count above (IPM iterations only) does not
+        # executed fp64 flops of the dominant kernel's launch from the committed SQ pass (FMA
+        # counts two, 64 lanes per wave instruction, masked lanes included): the active-set
+        # passes' scans with their Kogge-Stone redundancy, i.e. what the SIMDs actually did
         pmc, _ = profiled_summary()
         f64 = ((pmc or {}).get("valu_issue") or {}).get("fp64_insts_per_launch")
         fp64_exec_tf = (64.0 * (2.0 * f64["fma"] + f64["mul"] + f64["add"]) / (kernel_ms * 1e-3)
                         / 1e12) if f64 else None
+        vi = valu_issue(kernel_ms)
         line = {
             "metric": "DCM-MPC QP solves/sec (batch, horizon=100) at 1/2/4/8 MI355X",
             "value": total / elapsed,
@@ -230,35 +264,40 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.global_batch is None else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (6-footstep plans, SeedSequence-keyed Philox per problem)",
-            "config": {"workload": f"configs[1]: batch={B} DCM-MPC QPs per GPU, horizon={N}, "
-                                   f"M={M} facet slots, fp64, one workgroup per QP",
-                       "batch_per_gpu": B, "horizon": N, "max_facets": M,
+            "config": {"workload": (f"configs[1]: batch={B} DCM-MPC QPs per GPU, horizon={N}, "
+                                    f"M={M} facet slots, fp64, one wavefront per QP"
+                                    if args.global_batch is None else
+                                    f"configs[3]-style: global batch {args.global_batch} "
+                                    f"DCM-MPC QPs over {world} GPUs ({B} per rank), horizon={N}"),
+                       "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
+                       "max_facets": M,
                        "parallelism": f"shard{world} (independent problems)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "dcm_mpc_ipm_kernel<128>", "kernel_ms": kernel_ms,
+                         "kernel": "dcm_mpc_as_kernel<2> (+ the IPM kernel's stage 2 on the QPs "
+                                   "it hands over, inside the same event pair)",
+                         "kernel_ms": kernel_ms,
                          "bytes_per_qp": bpq,
-                         "fp64_valu": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
-                                       "frac": fp64_tf / FP64_PEAK_TFLOPS,
-                                       "counted": "sequential-form flops of the IPM iterations",
-                                       "executed_tflops": fp64_exec_tf,
+                         # what binds this kernel is neither HBM nor MFMA: VALU issue and the
+                         # latency of the scans' lane-shuffle chains
+                         "binding_roof": {"kind": "valu_issue",
+                                          "frac": vi["frac"] if vi else None},
+                         "valu_issue": vi,
+                         "fp64_valu": {"executed_tflops": fp64_exec_tf,
+                                       "peak_tflops": FP64_PEAK_TFLOPS,
                                        "executed_frac": (fp64_exec_tf / FP64_PEAK_TFLOPS
                                                          if fp64_exec_tf else None)},
-                         "valu_issue": valu_issue(kernel_ms),
-                         "mean_ipm_iters": float(iters.float().mean())},
+                         "mean_ipm_iters": float(iters.float().mean()),
+                         "polished_frac": float(polished.mean())},
             "gather_ms": gather_ms,
         }
         if not args.no_cpu:
-            try:
-                threads = len(os.sched_getaffinity(0))
-            except AttributeError:
-                threads = os.cpu_count() or 1
-            threads = max(1, min(threads, 16))
+            threads = cpu_threads()
             host = dict(prob, A=A.cpu().numpy(), b=b.cpu().numpy(), nfacets=nf.cpu().numpy())
             line["cpu_baseline"] = cpu_baseline(host, N, args.cpu_seconds, threads)
         print(json.dumps(line), flush=True)

@@ -484,12 +484,10 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
             double2 va[U];
             double vb[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = t0 + u * kWave + lane;
-                if (t < nA) {
-                    va[u] = As[t];
-                    vb[u] = bs[t];
-                }
+            for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
+                const int t = min(t0 + u * kWave + lane, nA - 1);
+                va[u] = As[t];
+                vb[u] = bs[t];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {

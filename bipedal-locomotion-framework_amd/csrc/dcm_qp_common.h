@@ -64,7 +64,7 @@ __device__ __forceinline__ double bperm(int addr, double x)
 // of the support polygon — is the active pair (oracle dcm_polish).  Returns 2 with pi1, pi2 set,
 // or 3 (no such pair: the pass fails).  Rare, so it reads the rows straight from LDS.
 // The offsets are read as Bo[(i N + kx) * bs] (bs = 2: the IPM kernel's (b, 1/s) pairs).
-static __device__ __attribute__((noinline)) int vertex_pair(const double2* A2, const double* Bo, int bs, int N,
+static __device__ __forceinline__ int vertex_pair(const double2* A2, const double* Bo, int bs, int N,
                                                             int kx, int km, int cm, double tol_p, int& pi1,
                                                             int& pi2)
 {

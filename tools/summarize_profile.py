@@ -80,6 +80,7 @@ def main():
                     "(Infinity-Cache hits included); gfx950 FETCH_SIZE reads 1/2 of wide "
                     "coalesced stream bytes (MI355X_MICROARCH.md HBM section)"},
         "valu_issue": valu_issue(d, float(stats[dom]["AverageNs"])),
+        "kernel_avg_ns": {k: float(v["AverageNs"]) for k, v in stats.items()},
         "pmc_per_kernel": pmc,
     }
     with open(os.path.join(dst, f"{tag}_summary.json"), "w") as f:
