@@ -151,9 +151,18 @@ def main():
                     help="c2 (default, the driver's metric): configs[1]; c1: configs[0] single-solve "
                          "latency (4 footsteps, N=50) on the GPU and the CPU; c3: configs[2] pipeline "
                          "(hull H-rep + QP + swing splines, B=65536); c5: configs[4] closed loop "
-                         "(QP + 30-DoF floating-base dynamics with contacts, B=16384); rh: "
+                         "(robot DCM -> warm-started QP -> joint references -> 30-DoF floating-"
+                         "base dynamics with contact feet, B=16384 per GPU, multi-rank); rh: "
                          "receding-horizon advance() (phase expansion + warm-started QP, B=4096)")
     args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        # checked before any HIP call: a scaling run launched without torch.distributed.run would
+        # otherwise measure one GPU and report it as n_gpus = 1
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 with "
+                 f"python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
+    if args.workload not in ("c2", "c5") and world > 1:
+        sys.exit(f"bench.py: --workload {args.workload} runs on one GPU")
     if args.workload != "c2":
         return other_workload(args)
 
@@ -166,11 +175,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:
-        # checked before any HIP call: a scaling run launched without torch.distributed.run would
-        # otherwise measure one GPU and report it as n_gpus = 1
-        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 with "
-                 f"python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
     if args.global_batch is not None:
         if args.global_batch % world:
             sys.exit(f"bench.py: --global-batch {args.global_batch} is not divisible by {world} ranks")
@@ -326,6 +330,8 @@ def other_workload(args):
     from blf import native
     from blf import problems as P
     from blf import robot
+    if args.workload == "c5":
+        return closed_loop(args)
     h = native.Handle(0)
     dev = torch.device("cuda", 0)
     N = args.horizon
@@ -359,46 +365,110 @@ def other_workload(args):
                                        f"{B * (N)} support polygons, {kt.shape[0]} swing splines "
                                        f"x 32 queries", "batch_per_gpu": B}}
     else:
-        B = 16384
-        prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED)
-        d = {k: torch.from_numpy(prob[k]).to(dev) for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
-        A, b, nf = h.assemble_constraints(torch.from_numpy(prob["corners"]).to(dev),
-                                          torch.from_numpy(prob["ncorners"]).to(dev))
-        d.update(A=A, b=b, nfacets=nf)
-        params = native.default_params(N)
-        model = robot.humanoid24()
-        dm = h.fb_model(model)
-        st = robot.random_states(model, B, seed=1)
-        state = {k: torch.from_numpy(st[k]).to(dev) for k in native.FB_STATE_KEYS}
-        tau = torch.from_numpy(st["joint_torque"]).to(dev)
-        null = np.zeros((B, 2, 12))
-        null[:, :, 3:] = np.eye(3).reshape(-1)
-        contacts = dict(frame=torch.tensor([0, 1], dtype=torch.int32, device=dev),
-                        params=torch.tensor([[0.12, 0.09, 3.0e4, 300.0]] * 2, dtype=torch.float64,
-                                            device=dev),
-                        null_pose=torch.from_numpy(null).to(dev))
-        period, dT = 0.01, 0.001          # one 10 ms control period of 1 ms Euler steps
-        out = {}
-
-        def step():
-            out["qp"] = h.dcm_mpc_solve(d, params)
-            h.fbd_euler_integrate(dm, state, tau, 0.0, period, dT, contacts=contacts)
-
-        sec = _timed(step, args.steps, args.warmup)
-        nsteps = int(np.ceil(period / dT))
-        t_dyn = _timed(lambda: h.fbd_euler_integrate(dm, state, tau, 0.0, period, dT,
-                                                     contacts=contacts), args.steps, 1)
-        line = {"metric": "closed-loop control periods/sec (DCM-MPC + 30-DoF floating-base "
-                          "dynamics with 2 ContinuousContactModel feet)",
-                "value": B / sec, "unit": "system-periods/s", "n_gpus": 1,
-                "ms_per_step": sec * 1e3, "steps": args.steps, "warmup": args.warmup,
-                "dtype": "f64",
-                "fb_dynamics_evals_per_s": B * nsteps / t_dyn,
-                "fb_dynamics_ms_per_period": t_dyn * 1e3,
-                "config": {"workload": f"configs[4] on one GPU: batch={B} robots, horizon-{N} QP "
-                                       f"+ {nsteps} Euler steps of the 6+24 DoF dynamics per "
-                                       f"period", "batch_per_gpu": B}}
+        return closed_loop(args, h, dev)
     print(json.dumps(line), flush=True)
+
+
+def closed_loop(args):
+    """configs[4]: the closed loop of the DCM-MPC planner and the 30-DoF floating-base robot with
+    two ContinuousContactModel feet (blf/closed_loop.py), B = 16384 robots
+    per GPU, one process per GPU over disjoint robot shards (no data-path collective).  One step =
+    one 20 ms control period of every robot: its DCM -> the plan's xi_init, the warm-started
+    plan window, the plan's first VRP -> joint references, 20 ForwardEuler steps (1 ms) of the
+    dynamics with the joint impedance.  The loop runs from a standing start; warmup periods first,
+    then the timed ones, stream-ordered and synchronised once."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from blf import closed_loop as DL
+    from blf import native
+    from blf import problems as P
+    from blf import robot
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    backend = os.environ.get("BLF_BENCH_BACKEND", "nccl")
+    if world > 1:
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(local)
+    h = native.Handle(local)
+    B = args.batch if args.batch != 4096 else 16384   # configs[4]: 16 384 robots per GPU
+    N, S = args.horizon, args.warmup + args.steps
+    model = robot.humanoid24()
+    plan = P.make_batch(B, horizon=N + S, n_footsteps=8, seed=P.SEED, start=rank * B, first_ds=S + 10)
+    st = robot.standing_states(model, B, seed=1000 + rank)
+    loop = DL.ClosedLoop(h, model, plan, st, horizon=N)
+    for _ in range(args.warmup):
+        loop.period()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    statuses = []
+    for _ in range(args.steps):
+        out = loop.period()
+        statuses.append(out["status"].clone())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=("cuda" if backend == "nccl" else "cpu"))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    finite = all(bool(torch.isfinite(v).all()) for v in loop.state.values())
+    assert finite, "non-finite robot state in the closed loop"
+    stat = torch.bincount(torch.stack(statuses).flatten().to(torch.int64), minlength=4).cpu().numpy()
+    z = loop.state["base_pos"][:, 2]
+    nsteps = int(np.ceil(loop.dt / loop.dT))
+    if rank == 0:
+        line = {"metric": "closed-loop control periods/sec (DCM-MPC + 30-DoF floating-base "
+                          "dynamics with 2 ContinuousContactModel feet, configs[4])",
+                "value": world * B * args.steps / elapsed, "unit": "robot-periods/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "weak", "dtype": "f64", "data": "synthetic (standing start, 8-footstep plans)",
+                "qp_status_counts": {"solved": int(stat[0]), "max_iter": int(stat[1]),
+                                     "numerical": int(stat[2]), "bad_facets": int(stat[3])},
+                "state_finite": finite,
+                "base_height_range": [float(z.min()), float(z.max())],
+                "config": {"workload": f"configs[4]: {B} robots per GPU x {world} GPU(s), 20 ms control "
+                                       f"period = one knot of a horizon-{N} warm-started plan + "
+                                       f"{nsteps} ForwardEuler steps of the 6+24 DoF dynamics",
+                           "batch_per_gpu": B, "parallelism": f"shard{world} (independent robots)"}}
+        if not args.no_cpu:
+            line["cpu_baseline"] = closed_loop_cpu(args, model, N)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def closed_loop_cpu(args, model, N, robots=8, periods=2):
+    """The CPU composition of the same loop (oracle/closed_loop.py: numpy rigid-body terms, the C
+    oracle's QP), a bounded sample: `robots` robots for `periods` periods on one core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import closed_loop as CL
+    from blf import closed_loop as DL
+    from blf import problems as P
+    from blf import robot
+    plan = P.make_batch(robots, horizon=N + periods, n_footsteps=8, seed=P.SEED, first_ds=periods + 10)
+    st = robot.standing_states(model, robots, seed=1000)
+    ref = CL.OracleLoop(model, plan, st, robot.sole_null_poses(model, st),
+                        robot.posture_law_arrays(model), DL.CONTACT_PARAMS, horizon=N)
+    t0 = time.perf_counter()
+    for _ in range(periods):
+        ref.period()
+    el = time.perf_counter() - t0
+    return {"value": robots * periods / el, "unit": "robot-periods/s", "cores": 1, "kind": "port",
+            "sample": f"{robots} robots x {periods} periods in {el:.2f} s on one core "
+                      f"(oracle/closed_loop.py: numpy rigid-body terms + the C oracle's QP)"}
 
 
 def single_solve_latency(args, h, dev):

@@ -1,0 +1,94 @@
+"""BASELINE.json configs[4] on the device: the closed loop of the DCM-MPC planner and the
+30-DoF floating-base robot with two ContinuousContactModel feet.
+
+The reference has no closed-loop driver; a user of it alternates TimeVaryingDCMPlanner::advance()
+(System/Advanceable.h:24-46) with ForwardEuler<FloatingBaseDynamicalSystem>::integrate
+(System/include/BipedalLocomotion/System/ForwardEuler.tpp:18-49 over
+System/src/FloatingBaseSystemDynamics.cpp:102-251, contact wrenches from
+ContactModels/src/ContinuousContactModel.cpp:79-108) and writes the two maps between them.
+One control period of this loop, stream-ordered on the device for a batch of robots:
+
+  1. state -> plan:  xi = c_xy + cdot_xy / omega_0 from the robot's centre of mass
+                     (blf_fb_dcm), the next window's xi_init;
+  2. plan:           the window moved one knot (blf_dcm_phase_expand) and solved warm from the
+                     previous period's solution (blf_dcm_mpc_solve_warm, shift 1);
+  3. plan -> robot:  joint references from the plan's first VRP and the centre of mass, held over
+                     the period (blf_dcm_posture_reference);
+  4. robot:          ForwardEuler<FloatingBaseDynamicalSystem>::integrate over the period with a
+                     joint impedance tracking them as the control input of every step
+                     (blf_fbd_euler_integrate_impedance, contacts at the feet).
+
+The control period is the plan's knot spacing dt (the window moves one knot per period); the
+impedance runs at the integration step dT (1 kHz): a 50 Hz zero-order hold of the joint
+torques does not stabilise the robot's fast modes.  Every piece runs on the device; the host only
+enqueues.
+"""
+import numpy as np
+
+from . import native
+from . import robot as R
+
+# ContinuousContactModel of each sole (length, width, spring_coeff, damper_coeff): the reference
+# test's foot size; stiffness and damping for a 50 kg robot on two 0.12 x 0.09 m soles (about
+# 1 cm of sink) that explicit Euler at dT = 1 ms integrates stably
+CONTACT_PARAMS = (0.12, 0.09, 2.0e6, 2.0e4)
+
+
+class ClosedLoop:
+    """A batch of robots, each closed around its own plan (problems.make_batch with the phase
+    table), on one device.  `states` is a host dict (robot.standing_states), `plan` the host
+    problem dict with a horizon of at least horizon + the number of periods to run."""
+
+    def __init__(self, h, model, plan, states, horizon=100, dT=0.001, law=None,
+                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None):
+        import torch
+        self.h, self.N, self.dT, self.stream = h, horizon, dT, stream
+        dev = torch.device("cuda", h.device)
+        t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
+        self.dt = float(plan["dt"])
+        self.B = plan["omega"].shape[0]
+        self.dm = h.fb_model(model)
+        law = law if law is not None else R.posture_law_arrays(model)
+        self.law = h.posture_law(law["q_nominal"], law["lean"])
+        self.imp = h.joint_impedance(law["kp"], law["kd"])
+        self.state = {k: t(states[k]) for k in native.FB_STATE_KEYS}
+        C = len(model["frame_link"])
+        self.contacts = dict(frame=t(np.arange(C), torch.int32),
+                             params=t(np.tile(np.asarray(contact_params, np.float64), (C, 1))),
+                             null_pose=t(R.sole_null_poses(model, states)))
+        self.table = h.phase_table(t(plan["nphases"], torch.int32), t(plan["phase_begin"]),
+                                   t(plan["phase_end"]), t(plan["phase_corners"]),
+                                   t(plan["phase_ncorners"], torch.int32), ref=t(plan["phase_ref"]))
+        self.omega = t(plan["omega"])
+        self.params = native.default_params(horizon, max_facets=self.table["phase_b"].shape[2])
+        self.params.tol_polish = tol_polish     # TimeVaryingDCMPlanner's warm-start trigger
+        self.com = torch.empty((self.B, 6), dtype=torch.float64, device=dev)
+        self.xi = torch.empty((self.B, 2), dtype=torch.float64, device=dev)
+        self.q_ref = torch.empty((self.B, model["n"]), dtype=torch.float64, device=dev)
+        self.bufs = [None, None]
+        self.prev = None
+        self.s = 0
+
+    def period(self):
+        """One control period (stream-ordered; nothing synchronises).  Returns the plan."""
+        h, s, N = self.h, self.s, self.N
+        if s + N > self.omega.shape[1]:
+            raise ValueError(f"the plan ends at knot {self.omega.shape[1]}; period {s} needs {s + N}")
+        h.fb_dcm(self.dm, self.state, omega=self.omega, column=s, com=self.com, xi=self.xi,
+                 stream=self.stream)
+        w = h.dcm_phase_expand(self.table, s, self.dt, N, stream=self.stream)
+        w.update(xi_init=self.xi, omega=self.omega[:, s:s + N].contiguous())
+        warm = None
+        if self.prev is not None:
+            warm = dict(vrp=self.prev["vrp"], lam=self.prev["lam"], shift=1, floor=1e-3)
+        out = h.dcm_mpc_solve(w, self.params, out=self.bufs[s % 2], warm=warm, lambda_out=True,
+                              stream=self.stream)
+        self.bufs[s % 2] = out
+        h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=self.stream)
+        # integrate(0, dt): the dynamics are time-invariant, and a fixed interval keeps the
+        # FixedStepIntegrator step count (ceil((T - t0) / dT)) the same in every period
+        h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.dt,
+                                        self.dT, contacts=self.contacts, stream=self.stream)
+        self.prev = out
+        self.s = s + 1
+        return out

@@ -26,7 +26,8 @@ EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
             "blf_dcm_phase_expand",
             "blf_dcm_mpc_flops_per_iter",
             "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
-            "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate"]
+            "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate",
+            "blf_fb_dcm", "blf_dcm_posture_reference", "blf_fbd_euler_integrate_impedance"]
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -49,6 +50,16 @@ class FbState(ctypes.Structure):
 
 class FbContacts(ctypes.Structure):
     _fields_ = [("ncontacts", _i32), ("frame", _vp), ("params", _vp), ("null_pose", _vp)]
+
+
+class PostureLaw(ctypes.Structure):
+    """blf_posture_law (include/blf/blf_c.h): the closed loop's plan -> joint reference map."""
+    _fields_ = [("ndof", _i32), ("reserved", _i32), ("q_nominal", _vp), ("lean", _vp)]
+
+
+class JointImpedance(ctypes.Structure):
+    """blf_joint_impedance: tau = kp (q_ref - q) - kd qdot before every Euler step."""
+    _fields_ = [("ndof", _i32), ("reserved", _i32), ("kp", _vp), ("kd", _vp), ("q_ref", _vp)]
 
 
 FB_STATE_KEYS = ("base_vel", "joint_vel", "base_pos", "base_rot", "joint_pos")
@@ -141,6 +152,13 @@ def lib():
         L.blf_fbd_euler_integrate.argtypes = [_vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState),
                                               _vp, ctypes.POINTER(FbContacts), _vp, _i64, _f64,
                                               _f64, _f64, _vp]
+        L.blf_fb_dcm.argtypes = [_vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), _vp, _i64,
+                                 _i64, _vp, _vp, _vp]
+        L.blf_dcm_posture_reference.argtypes = [_vp, ctypes.POINTER(PostureLaw), _vp, _vp, _i64, _i64,
+                                                _vp, _vp]
+        L.blf_fbd_euler_integrate_impedance.argtypes = [
+            _vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), ctypes.POINTER(JointImpedance),
+            ctypes.POINTER(FbContacts), _vp, _i64, _f64, _f64, _f64, _vp]
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         for name in EXPORTED:
             if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
@@ -585,4 +603,88 @@ class Handle:
                                              _ptr(torque, torch.float64, (B, n), "torque"),
                                              ctypes.byref(ct), reg, B, float(t0), float(t1),
                                              float(dT), _stream(stream)))
+        return state
+
+    # ---- config 5: the closed loop's maps ----------------------------------
+    def fb_dcm(self, dm, state, omega=None, column=0, com=None, xi=None, stream=None):
+        """blf_fb_dcm: centre of mass and its velocity com [B,6] of every system and, when omega
+        ([B,K] device tensor) is given, the DCM xi [B,2] = c_xy + cdot_xy / omega[:, column]."""
+        torch = _torch()
+        B, n = state["joint_pos"].shape
+        dev = state["joint_pos"].device
+        com = com if com is not None else torch.empty((B, 6), dtype=torch.float64, device=dev)
+        optr, ostride = None, 0
+        if omega is not None:
+            K = omega.shape[1]
+            _ptr(omega, torch.float64, (B, K), "omega")
+            if not 0 <= column < K:
+                raise ValueError(f"omega column {column} outside [0, {K})")
+            optr, ostride = _vp(omega.data_ptr() + 8 * column), K
+            xi = xi if xi is not None else torch.empty((B, 2), dtype=torch.float64, device=dev)
+        elif xi is not None:
+            raise ValueError("xi requested without omega")
+        _check(lib().blf_fb_dcm(self._h, ctypes.byref(dm.c), ctypes.byref(self._fb_state(state, B, n)),
+                                optr, ostride, B, _ptr(com, torch.float64, (B, 6), "com"),
+                                _ptr(xi, torch.float64, (B, 2), "xi") if xi is not None else None,
+                                _stream(stream)))
+        return com, xi
+
+    def posture_law(self, q_nominal, lean):
+        """Upload a blf_posture_law: q_nominal [n], lean [n,2] (host arrays)."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+
+        class _L:
+            pass
+        law = _L()
+        f64 = lambda a: torch.as_tensor(a, dtype=torch.float64).contiguous().to(dev)
+        law.t = dict(q_nominal=f64(q_nominal), lean=f64(lean))
+        n = law.t["q_nominal"].shape[0]
+        if law.t["lean"].shape != (n, 2):
+            raise ValueError("posture law: q_nominal [n] and lean [n,2]")
+        c = PostureLaw()
+        c.ndof = n
+        c.q_nominal, c.lean = _vp(law.t["q_nominal"].data_ptr()), _vp(law.t["lean"].data_ptr())
+        law.c = c
+        return law
+
+    def posture_reference(self, law, com, vrp, q_ref=None, stream=None):
+        """blf_dcm_posture_reference: joint references [B,n] from the plan's first VRP (vrp
+        [B,N,2], a blf_dcm_mpc_solve output) and the centre of mass com [B,6] (fb_dcm)."""
+        torch = _torch()
+        B, N = vrp.shape[0], vrp.shape[1]
+        n = law.c.ndof
+        q_ref = q_ref if q_ref is not None else torch.empty((B, n), dtype=torch.float64,
+                                                            device=vrp.device)
+        _check(lib().blf_dcm_posture_reference(self._h, ctypes.byref(law.c),
+                                               _ptr(com, torch.float64, (B, 6), "com"),
+                                               _ptr(vrp, torch.float64, (B, N, 2), "vrp"), 2 * N, B,
+                                               _ptr(q_ref, torch.float64, (B, n), "q_ref"),
+                                               _stream(stream)))
+        return q_ref
+
+    def joint_impedance(self, kp, kd):
+        """Device copies of the impedance gains kp, kd [n] (host arrays)."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        f64 = lambda a: torch.as_tensor(a, dtype=torch.float64).contiguous().to(dev)
+        return dict(kp=f64(kp), kd=f64(kd))
+
+    def fbd_euler_integrate_impedance(self, dm, state, impedance, q_ref, t0, t1, dT, contacts=None,
+                                      mass_reg=None, stream=None):
+        """blf_fbd_euler_integrate_impedance in place on `state`: the control input of every
+        Euler step is tau = kp (q_ref - q) - kd qdot (impedance: joint_impedance())."""
+        torch = _torch()
+        B, n = state["joint_pos"].shape
+        NV = n + 6
+        reg = _ptr(mass_reg, torch.float64, (NV, NV), "mass_reg") if mass_reg is not None else None
+        imp = JointImpedance()
+        imp.ndof = n
+        imp.kp = _ptr(impedance["kp"], torch.float64, (n,), "kp")
+        imp.kd = _ptr(impedance["kd"], torch.float64, (n,), "kd")
+        imp.q_ref = _ptr(q_ref, torch.float64, (B, n), "q_ref")
+        _check(lib().blf_fbd_euler_integrate_impedance(
+            self._h, ctypes.byref(dm.c), ctypes.byref(self._fb_state(state, B, n)), ctypes.byref(imp),
+            ctypes.byref(self._fb_contacts(contacts, B)), reg, B, float(t0), float(t1), float(dT),
+            _stream(stream)))
         return state

@@ -19,12 +19,14 @@ GRAVITY = 9.81
 SEED = 20201015
 
 
-def contact_schedule(n_footsteps, horizon):
+def contact_schedule(n_footsteps, horizon, first_ds=DS_KNOTS):
     """Knot-index schedule of the plan: returns {foot: [(act_knot, deact_knot, pose_slot)]}.
 
     Footsteps 0 and 1 are the initial left/right stance (active from knot 0); step j >= 0 swings
-    the right foot for even j, the left foot for odd j: lift at 10 + 40 j, land at 40 + 40 j.
-    The last contact of each foot stays active until past the horizon.
+    the right foot for even j, the left foot for odd j: lift at first_ds + 40 j, land at
+    first_ds + 30 + 40 j (first_ds = 10: the standard 0.2 s double support; longer: the robot
+    stands first, as the config-5 closed loop does).  The last contact of each foot stays active
+    until past the horizon.
     """
     assert n_footsteps >= 2
     lists = {"left": [], "right": []}
@@ -33,7 +35,8 @@ def contact_schedule(n_footsteps, horizon):
     nxt = 2
     for j in range(n_footsteps - 2):
         foot = "right" if j % 2 == 0 else "left"
-        lift, land = DS_KNOTS + (DS_KNOTS + SS_KNOTS) * j, (DS_KNOTS + SS_KNOTS) * (j + 1)
+        lift = first_ds + (DS_KNOTS + SS_KNOTS) * j
+        land = lift + SS_KNOTS
         lists[foot].append((act[foot], lift, slot[foot]))
         act[foot], slot[foot] = land, nxt
         nxt += 1
@@ -92,10 +95,11 @@ def rectangle_corners(pose):
     return np.stack(out, axis=-2)
 
 
-def make_batch(batch, horizon=100, n_footsteps=6, dt=0.02, seed=SEED, start=0):
+def make_batch(batch, horizon=100, n_footsteps=6, dt=0.02, seed=SEED, start=0, first_ds=DS_KNOTS):
     """Problems [start, start+batch) of the synthetic workload with the given seed.
 
     Problem i's random draws depend only on (seed, start + i), so shards are reproducible.
+    first_ds: knots of the initial double support (contact_schedule).
     """
     F = n_footsteps
     rows = np.arange(start, start + batch, dtype=np.uint64)
@@ -115,7 +119,7 @@ def make_batch(batch, horizon=100, n_footsteps=6, dt=0.02, seed=SEED, start=0):
         side = -1.0 if j % 2 == 0 else 1.0                       # right foot first
         poses[:, j + 2] = np.stack([x, side * 0.10 + 0.02 * u[:, j + 2, 0], 0.1 * u[:, j + 2, 1]], -1)
 
-    lists = contact_schedule(F, horizon)
+    lists = contact_schedule(F, horizon, first_ds)
     phases = phases_from_schedule(lists, dt)
     corners_all = rectangle_corners(poses)                      # [B, F, 4, 2]
     foot_names = ["left", "right"]

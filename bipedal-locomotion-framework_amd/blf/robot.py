@@ -98,3 +98,110 @@ def random_states(model, batch, seed=0, spread=0.3):
         joint_pos=rng.uniform(-spread, spread, (batch, n)),
         joint_torque=rng.normal(size=(batch, n)) * 5.0,
     )
+
+
+# ---- config 5 closed loop: a standing start (synthetic input generation, host side) -----------
+def sole_offsets(model):
+    """Positions of the sole frames relative to the base origin at the nominal posture (all joints
+    0, base orientation identity): plain forward kinematics of the tree's fixed transforms."""
+    n = model["n"]
+    Rl = [np.eye(3)] + [None] * n
+    pl = [np.zeros(3)] + [None] * n
+    for j in range(n):
+        P = model["parent"][j]
+        Rl[j + 1] = Rl[P] @ model["joint_rot"][j]
+        pl[j + 1] = pl[P] + Rl[P] @ model["joint_origin"][j]
+    out = []
+    for f in range(len(model["frame_link"])):
+        l = model["frame_link"][f]
+        out.append(pl[l] + Rl[l] @ model["frame_pose"][f, :3])
+    return np.array(out)
+
+
+def standing_states(model, batch, seed=0, spread=0.05, vel=0.02):
+    """Batch of states near the nominal standing posture: base upright at the height that puts the
+    soles on z = 0 with straight legs, the torso, arm and neck joints within +-spread rad of 0,
+    small velocities.  (Random leg joints would start the soles off the ground or in it: the
+    contact springs then kick the robot at the first step.)"""
+    rng = np.random.default_rng(seed)
+    n = model["n"]
+    h = -sole_offsets(model)[:, 2].mean()
+    legs = np.array([nm[0] in "lr" and nm[1] == "_" and nm[2:].split("_")[0] in ("hip", "knee", "ankle")
+                     for nm in model["names"][1:]])
+    q = rng.uniform(-spread, spread, (batch, n))
+    q[:, legs] = 0.0
+    return dict(
+        base_vel=rng.normal(size=(batch, 6)) * vel,
+        joint_vel=rng.normal(size=(batch, n)) * vel,
+        base_pos=np.column_stack([rng.normal(size=(batch, 2)) * 0.01, np.full(batch, h)]),
+        base_rot=np.broadcast_to(np.eye(3), (batch, 3, 3)).copy(),
+        joint_pos=q,
+    )
+
+
+def sole_null_poses(model, states):
+    """ContinuousContactModel null-force transforms [B][F][12] of the sole frames: each foot's
+    nominal sole position under the base on the ground (z = 0), orientation identity."""
+    off = sole_offsets(model)
+    B, F = states["base_pos"].shape[0], off.shape[0]
+    null = np.zeros((B, F, 12))
+    null[:, :, 0] = states["base_pos"][:, None, 0] + off[None, :, 0]
+    null[:, :, 1] = states["base_pos"][:, None, 1] + off[None, :, 1]
+    null[:, :, 3:] = np.eye(3).reshape(-1)
+    return null
+
+
+def joint_inertias(model):
+    """Composite inertia of every joint's subtree about the joint axis at the nominal posture
+    (joints 0, base identity): sum over the subtree's links of z^T R I_c R^T z + m |z x (c - o)|^2."""
+    n = model["n"]
+    Rl = [np.eye(3)] + [None] * n
+    pl = [np.zeros(3)] + [None] * n
+    z, o = np.zeros((n, 3)), np.zeros((n, 3))
+    for j in range(n):
+        P = model["parent"][j]
+        Rl[j + 1] = Rl[P] @ model["joint_rot"][j]
+        pl[j + 1] = pl[P] + Rl[P] @ model["joint_origin"][j]
+        z[j], o[j] = Rl[j + 1] @ model["joint_axis"][j], pl[j + 1]
+    anc = [set() for _ in range(n + 1)]
+    for j in range(n):
+        anc[j + 1] = anc[model["parent"][j]] | {j}
+    I = np.zeros(n)
+    for l in range(n + 1):
+        c = pl[l] + Rl[l] @ model["link_com"][l]
+        Iw = Rl[l] @ model["link_inertia"][l] @ Rl[l].T
+        for j in anc[l]:
+            r = np.cross(z[j], c - o[j])
+            I[j] += z[j] @ Iw @ z[j] + model["link_mass"][l] * (r @ r)
+    return I
+
+
+def posture_law_arrays(model, freq=20.0, zeta=1.0, ankle_inertia=0.2, hip_lean=0.0, gravity=9.81):
+    """The closed loop's plan -> robot map: joint references (blf_dcm_posture_reference) tracked
+    by a joint impedance (blf_fbd_euler_integrate_impedance), PD to the zero posture with
+    per-joint gains for one natural frequency (kp = freq^2 I_j, I_j the joint's composite
+    inertia; kd = 2 zeta sqrt(kp I_j), damped for the joint's own subtree, so explicit Euler
+    sees a bounded freq * dT on every joint).  The plan enters through the ankles: the ankle
+    pitch / roll references move by m g / (2 kp_ankle) rad per metre of (r0 - c), the offset at
+    which each foot's ankle impedance exerts the torque m g / 2 (r0 - c) that moves the centre of
+    pressure from under the centre of mass to the planned VRP; the hips can counter-lean the
+    trunk (hip_lean rad per metre).  The ankles carry the body in stance, so their inertia is
+    floored at `ankle_inertia` (the free foot alone would give them far too weak a posture)."""
+    n = model["n"]
+    names = model["names"][1:]   # joint j moves link j + 1
+    I = joint_inertias(model)
+    Ik = I.copy()
+    for side in ("l", "r"):
+        for jn in ("ankle_pitch", "ankle_roll"):
+            j = names.index(f"{side}_{jn}")
+            Ik[j] = max(I[j], ankle_inertia)
+    kp = freq * freq * Ik
+    mg2 = 0.5 * model["link_mass"].sum() * gravity
+    L = np.zeros((n, 2))
+    for side in ("l", "r"):
+        jp, jr = names.index(f"{side}_ankle_pitch"), names.index(f"{side}_ankle_roll")
+        L[jp, 0] = mg2 / kp[jp]
+        L[jr, 1] = -mg2 / kp[jr]
+        L[names.index(f"{side}_hip_pitch"), 0] = -hip_lean
+        L[names.index(f"{side}_hip_roll"), 1] = hip_lean
+    return dict(q_nominal=np.zeros(n), lean=L, kp=kp, kd=2.0 * zeta * np.sqrt(kp * I))

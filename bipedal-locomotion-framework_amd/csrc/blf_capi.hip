@@ -400,6 +400,66 @@ blf_status blf_fbd_dynamics(blf_handle* handle, const blf_fb_model* model,
                                (hipStream_t)stream);
 }
 
+blf_status blf_fb_dcm(blf_handle* handle, const blf_fb_model* model, const blf_fb_state* state,
+                      const double* omega0, int64_t omega0_stride, int64_t batch, double* com,
+                      double* xi, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_fb_dcm: null handle");
+    BLF_REQUIRE(model != nullptr && state != nullptr, "blf_fb_dcm: null model / state");
+    BLF_REQUIRE(model->ndof >= 1 && model->ndof <= BLF_FBD_MAX_DOFS, "blf_fb_dcm: ndof=%d outside [1, %d]",
+                model->ndof, BLF_FBD_MAX_DOFS);
+    BLF_REQUIRE(batch >= 0, "blf_fb_dcm: negative batch");
+    BLF_REQUIRE(model->parent && model->joint_origin && model->joint_rot && model->joint_axis &&
+                    model->link_mass && model->link_com && model->link_inertia,
+                "blf_fb_dcm: null model array");
+    BLF_REQUIRE(batch == 0 || (state->base_vel && state->joint_vel && state->base_pos &&
+                               state->base_rot && state->joint_pos && com),
+                "blf_fb_dcm: null state / output buffer");
+    BLF_REQUIRE(xi == nullptr || omega0 != nullptr, "blf_fb_dcm: xi requested without omega0");
+    BLF_REQUIRE(omega0_stride >= 0, "blf_fb_dcm: negative omega0 stride");
+    return launch_fb_dcm(model, state, omega0, omega0_stride, batch, com, xi, (hipStream_t)stream);
+}
+
+blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* law,
+                                     const double* com, const double* vrp, int64_t vrp_stride,
+                                     int64_t batch, double* q_ref, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_dcm_posture_reference: null handle");
+    BLF_REQUIRE(law != nullptr, "blf_dcm_posture_reference: null law");
+    BLF_REQUIRE(law->ndof >= 1 && law->ndof <= BLF_FBD_MAX_DOFS,
+                "blf_dcm_posture_reference: ndof=%d outside [1, %d]", law->ndof, BLF_FBD_MAX_DOFS);
+    BLF_REQUIRE(law->q_nominal && law->lean, "blf_dcm_posture_reference: null law array");
+    BLF_REQUIRE(batch >= 0 && vrp_stride >= 2, "blf_dcm_posture_reference: bad batch / vrp stride");
+    BLF_REQUIRE(batch == 0 || (com && vrp && q_ref), "blf_dcm_posture_reference: null buffer");
+    return launch_posture_reference(law, com, vrp, vrp_stride, batch, q_ref, (hipStream_t)stream);
+}
+
+blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_model* model,
+                                             const blf_fb_state* state,
+                                             const blf_joint_impedance* impedance,
+                                             const blf_fb_contacts* contacts,
+                                             const double* mass_reg, int64_t batch,
+                                             double initial_time, double final_time, double dT,
+                                             void* stream)
+{
+    BLF_REQUIRE(impedance != nullptr, "blf_fbd_euler_integrate_impedance: null impedance");
+    BLF_REQUIRE(impedance->kp && impedance->kd && (batch == 0 || impedance->q_ref),
+                "blf_fbd_euler_integrate_impedance: null impedance array");
+    BLF_REQUIRE(model != nullptr && impedance->ndof == model->ndof,
+                "blf_fbd_euler_integrate_impedance: impedance ndof %d != model ndof %d",
+                impedance->ndof, model ? model->ndof : -1);
+    // the constant-torque checks with a stand-in torque pointer (the impedance replaces it)
+    blf_status st = check_fbd("blf_fbd_euler_integrate_impedance", handle, model, state,
+                              impedance->kp, contacts, batch);
+    if (st != BLF_OK) return st;
+    int iterations = 0;
+    double dT_last = 0.0;
+    st = step_schedule(initial_time, final_time, dT, &iterations, &dT_last);
+    if (st != BLF_OK) return st;
+    return launch_fbd_euler(model, state, nullptr, contacts, mass_reg, batch, iterations, dT,
+                            dT_last, (hipStream_t)stream, impedance);
+}
+
 blf_status blf_fbd_euler_integrate(blf_handle* handle, const blf_fb_model* model,
                                    const blf_fb_state* state, const double* joint_torque,
                                    const blf_fb_contacts* contacts, const double* mass_reg,

@@ -68,8 +68,13 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
                                const blf_fb_state* out, hipStream_t s);
 blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
-                            int32_t nsteps, double dT, double dT_last, hipStream_t s);
+                            int32_t nsteps, double dT, double dT_last, hipStream_t s,
+                            const blf_joint_impedance* impedance = nullptr);
 size_t fbd_lds_bytes(int n, int C);
+blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const double* omega0,
+                         int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s);
+blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
+                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s);
 blf_status launch_fbk_euler(int n, double rho, double* pos, double* rot, double* joints,
                             const double* twist, const double* joint_vel, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s);

@@ -72,7 +72,7 @@ constexpr int kComp = 16;   // subtree sum: spatial inertia 10 | spatial force 6
 constexpr int kCs = 16;     // contact scratch: point 3 | wrench 6 | link 1 | spatial wrench 6
 
 struct Smem {
-    double *link, *jrot, *jz, *jo, *comp, *sax, *rhs, *cscr, *st;
+    double *link, *jrot, *jz, *jo, *comp, *sax, *rhs, *cscr, *st, *tq;
     unsigned long long* anc;
     int ms;   // row stride of L (odd: the per-lane row accesses do not conflict)
     size_t total;
@@ -100,6 +100,7 @@ struct Smem {
         rhs = take((size_t)NV);
         cscr = take((size_t)kCs * (C > 0 ? C : 1));
         st = take(18 + 2 * (size_t)n + (size_t)NV + 9);   // Euler state (6 + n + 3 + 9 + n) + acc + dR
+        tq = take((size_t)n);                              // the joint impedance's torques
         anc = reinterpret_cast<unsigned long long*>(take((size_t)L));
         total = o;
     }
@@ -210,25 +211,18 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
     return t;
 }
 
-// One evaluation of the dynamics for the system whose state sits in LDS (bv, jv, bp, bR, jp).
-// Leaves the generalized acceleration in S.rhs and returns false if the factorization failed.
-// NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
-// registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
-// steps 6-9.
-template <int NVMAX>
-__device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
-                                         const double* jvel, const double* bp, const double* bR,
-                                         const double* jp, const double* tau, const Contacts& ct,
-                                         int64_t sys, const double* reg, const Topo& T)
+// Steps 1-2 of fbd_eval: per-joint rotations and forward kinematics (poses, mixed velocities,
+// nu_dot = 0 accelerations) of every link into the link records.
+__device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, const double* bv,
+                                               const double* jvel, const double* bp, const double* bR,
+                                               const double* jp, const Topo& T)
 {
-    const int n = m.n, L = n + 1, NV = n + 6, MS = S.ms;
+    const int n = m.n;
     const int lane = threadIdx.x;
     const bool jl = lane < n;   // n <= 48 < 64: one joint per lane
-    FSTAMP(f_t0);
-    FSTAMP(f_t);
-    // 1. per-joint rotation E_j Rot(a_j, s_j) (Rodrigues) and E_j a_j, lane per joint
     const int depth = T.depth, P = T.P, maxdepth = T.maxdepth;
     const double sd = jl ? jvel[lane] : 0.0;
+    // 1. per-joint rotation E_j Rot(a_j, s_j) (Rodrigues) and E_j a_j, lane per joint
     if (jl) {
         const int j = lane;
         const double* a = m.jaxis + 3 * j;
@@ -263,8 +257,6 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         }
     }
     wave_sync();
-    FSTAMP_ADD(0, f_t);
-    FSTAMP(f_t1);
     // 2. forward kinematics, one tree level at a time: poses, mixed velocities, nu_dot = 0
     //    accelerations of every joint whose parent link is done
     for (int lev = 0; lev <= maxdepth; ++lev) {
@@ -312,6 +304,26 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         }
         wave_sync();
     }
+}
+
+// One evaluation of the dynamics for the system whose state sits in LDS (bv, jv, bp, bR, jp).
+// Leaves the generalized acceleration in S.rhs and returns false if the factorization failed.
+// NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
+// registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
+// steps 6-9.
+template <int NVMAX>
+__device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
+                                         const double* jvel, const double* bp, const double* bR,
+                                         const double* jp, const double* tau, const Contacts& ct,
+                                         int64_t sys, const double* reg, const Topo& T)
+{
+    const int n = m.n, L = n + 1, NV = n + 6, MS = S.ms;
+    const int lane = threadIdx.x;
+    const bool jl = lane < n;   // n <= 48 < 64: one joint per lane
+    const int depth = T.depth, maxdepth = T.maxdepth;
+    FSTAMP(f_t0);
+    FSTAMP(f_t1);
+    fbd_kinematics(m, S, bv, jvel, bp, bR, jp, T);
     FSTAMP_ADD(1, f_t1);
     FSTAMP(f_t2);
     // 3. per link: COM, world inertia, Newton-Euler force / moment, and the spatial inertia and
@@ -583,11 +595,18 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
     for (int j = lane; j < n; j += kWave) out.joint_pos[(int64_t)n * q + j] = loc[6 + j];
 }
 
+// The joint impedance of blf_fbd_euler_integrate_impedance: tau = kp (q_ref - q) - kd qdot, set as
+// the control input before every Euler step (kp == nullptr: the constant torques `tau`).
+struct Impedance {
+    const double *kp, *kd, *qref;
+};
+
 template <int NVMAX>
 __global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state st,
                                                        const double* __restrict__ tau,
                                                        Contacts ct, const double* reg,
-                                                       int32_t nsteps, double dT, double dT_last)
+                                                       int32_t nsteps, double dT, double dT_last,
+                                                       Impedance imp)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int n = m.n, NV = n + 6;
@@ -608,10 +627,17 @@ __global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state 
     wave_sync();
     const Topo T = build_topo(m, S);
     bool ok = true;
+    const double* tq = tau + (int64_t)n * q;
     for (int32_t step = 0; step < nsteps; ++step) {
         const double h = step + 1 < nsteps ? dT : dT_last;
+        if (imp.kp) {   // the control input of this step from its start state
+            for (int j = lane; j < n; j += kWave)
+                S.tq[j] = imp.kp[j] * (imp.qref[(int64_t)n * q + j] - loc[18 + n + j]) - imp.kd[j] * loc[6 + j];
+            wave_sync();
+            tq = S.tq;
+        }
         ok = fbd_eval<NVMAX>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
-                             tau + (int64_t)n * q, ct, q, reg, T) && ok;
+                             tq, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         wave_sync();
         // every element moves by its derivative at the start of the step (ForwardEuler.tpp:37-45):
@@ -635,6 +661,85 @@ __global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state 
         else if (i < 18 + n) st.base_rot[9 * q + (i - 9 - n)] = v;
         else st.joint_pos[(int64_t)n * q + (i - 18 - n)] = v;
     }
+}
+
+// The closed loop's state -> plan map: the centre of mass, its velocity
+// and the DCM of every system,
+//   c = sum_l m_l (p_l + R_l com_l) / m,   cdot = sum_l m_l (v_l + w_l x R_l com_l) / m,
+//   xi = c_xy + cdot_xy / omega_0
+// (the LIP's divergent component with the plan's first-knot omega).  One wavefront per system:
+// the forward kinematics of fbd_eval, then lane per link and one wave sum per quantity.
+__global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, const double* __restrict__ omega0,
+                                                    int64_t ostride, double* __restrict__ com,
+                                                    double* __restrict__ xi)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int n = m.n, L = n + 1;
+    const Smem S(smem, n, 0);
+    const int64_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    double* loc = S.st;   // bv 6 | jv n | bp 3 | bR 9 | jp n
+    for (int i = lane; i < 18 + 2 * n; i += kWave) {
+        double v;
+        if (i < 6) v = st.base_vel[6 * q + i];
+        else if (i < 6 + n) v = st.joint_vel[(int64_t)n * q + (i - 6)];
+        else if (i < 9 + n) v = st.base_pos[3 * q + (i - 6 - n)];
+        else if (i < 18 + n) v = st.base_rot[9 * q + (i - 9 - n)];
+        else v = st.joint_pos[(int64_t)n * q + (i - 18 - n)];
+        loc[i] = v;
+    }
+    wave_sync();
+    const Topo T = build_topo(m, S);
+    fbd_kinematics(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n, T);
+    wave_sync();
+    double a[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // m c (3), m cdot (3), m
+    if (lane < L) {
+        const double* k = S.link + kLinkRec * lane;
+        const double* R = k + kR;
+        const double* cl = m.com + 3 * lane;
+        double rc[3], t[3];
+        for (int i = 0; i < 3; ++i) rc[i] = (R[3 * i] * cl[0] + R[3 * i + 1] * cl[1]) + R[3 * i + 2] * cl[2];
+        cross3(k + kW, rc, t);
+        const double ms = m.mass[lane];
+        for (int i = 0; i < 3; ++i) {
+            a[i] = ms * (k[kP + i] + rc[i]);
+            a[3 + i] = ms * (k[kV + i] + t[i]);
+        }
+        a[6] = ms;
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) a[i] = wave_sum(a[i]);
+    if (lane == 0) {
+        double o[6];
+        for (int i = 0; i < 6; ++i) o[i] = a[i] / a[6];
+        for (int i = 0; i < 6; ++i) com[6 * q + i] = o[i];
+        if (xi) {
+            const double w0 = omega0[q * ostride];
+            xi[2 * q] = o[0] + o[3] / w0;
+            xi[2 * q + 1] = o[1] + o[4] / w0;
+        }
+    }
+}
+
+// The closed loop's plan -> robot map: the joint references held over one
+// control period,
+//   q_ref_j = q_nom_j + lean_j0 (r0_x - c_x) + lean_j1 (r0_y - c_y)
+// with r0 the plan's first VRP and c the centre of mass; the joint impedance of
+// fbd_euler_kernel tracks them.  Element per (system, joint).
+__global__ __launch_bounds__(256) void posture_reference_kernel(int n, const double* __restrict__ qnom,
+                                                                const double* __restrict__ lean,
+                                                                const double* __restrict__ com,
+                                                                const double* __restrict__ vrp,
+                                                                int64_t vstride, int64_t total,
+                                                                double* __restrict__ qref)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const int64_t q = e / n;
+    const int j = (int)(e - q * n);
+    const double ex = vrp[q * vstride] - com[6 * q];
+    const double ey = vrp[q * vstride + 1] - com[6 * q + 1];
+    qref[e] = (qnom[j] + lean[2 * j] * ex) + lean[2 * j + 1] * ey;
 }
 
 Model to_model(const blf_fb_model* md)
@@ -690,18 +795,42 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 
 blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
-                            int32_t nsteps, double dT, double dT_last, hipStream_t s)
+                            int32_t nsteps, double dT, double dT_last, hipStream_t s,
+                            const blf_joint_impedance* impedance)
 {
     if (batch == 0) return BLF_OK;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
+    Impedance imp{nullptr, nullptr, nullptr};
+    if (impedance) imp = Impedance{impedance->kp, impedance->kd, impedance->q_ref};
     if (md->ndof + 6 <= 32)
         hipLaunchKernelGGL(fbd_euler_kernel<32>, dim3((unsigned)batch), dim3(kWave), lds, s,
-                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last);
+                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp);
     else
         hipLaunchKernelGGL(fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6>, dim3((unsigned)batch),
-                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last);
+                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last,
+                           imp);
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
+}
+
+blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const double* omega0,
+                         int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s)
+{
+    if (batch == 0) return BLF_OK;
+    const size_t lds = fbd_lds_bytes(md->ndof, 0);
+    hipLaunchKernelGGL(fb_dcm_kernel, dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st,
+                       omega0, ostride, com, xi);
+    return check_hip(hipGetLastError(), "fb_dcm_kernel launch");
+}
+
+blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
+                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s)
+{
+    const int64_t total = batch * law->ndof;
+    if (total == 0) return BLF_OK;
+    hipLaunchKernelGGL(posture_reference_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       law->ndof, law->q_nominal, law->lean, com, vrp, vstride, total, qref);
+    return check_hip(hipGetLastError(), "posture_reference_kernel launch");
 }
 
 }  // namespace blf

@@ -35,6 +35,11 @@
  *   blf_fbd_euler_integrate   ForwardEuler<FloatingBaseDynamicalSystem>::integrate
  *   blf_dcm_phase_expand      Planners/src/ContactPhaseList.cpp:16-84 phases looked up per knot with the
  *                             getPresentContact rule (ContactList.cpp:190-202), SURVEY.md 8(f) item 2
+ *   blf_fb_dcm / blf_dcm_posture_reference  the state -> plan and plan -> input maps a user
+ *                             writes around Advanceable::advance() and ForwardEuler::integrate in a
+ *                             closed loop (config 5); no reference counterpart
+ *   blf_fbd_euler_integrate_impedance  blf_fbd_euler_integrate with a joint impedance as the
+ *                             control input of every step (the user's per-step setControlInput)
  *   blf_dcm_mpc_solve[_warm]  ABSENT in the reference (TimeVaryingDCMPlanner QP),
  *                             driven through System/Advanceable.h:24-46 (advance()) by the C++ host
  *                             adapter blf::Planners::TimeVaryingDCMPlanner
@@ -345,6 +350,55 @@ blf_status blf_fbd_euler_integrate(blf_handle* handle, const blf_fb_model* model
                                    const blf_fb_contacts* contacts, const double* mass_reg,
                                    int64_t batch, double initial_time, double final_time,
                                    double dT, void* stream);
+
+/* ---- 9. Closed loop (BASELINE.json configs[4]): the maps between the robot and the planner ----
+ * The reference has no closed-loop API: a user drives TimeVaryingDCMPlanner::advance()
+ * (System/Advanceable.h:24-46) and ForwardEuler<FloatingBaseDynamicalSystem>::integrate
+ * (ForwardEuler.tpp:18-49 over FloatingBaseSystemDynamics.cpp:102-251) in turn and maps the robot
+ * state to the plan's initial DCM and the plan to the robot's input.  These two entry points are
+ * those maps:
+ *
+ * blf_fb_dcm: state -> centre of mass c, its velocity cdot and the DCM
+ *   c = sum_l m_l (p_l + R_l com_l) / m,  cdot = sum_l m_l (v_l + w_l x R_l com_l) / m,
+ *   xi = c_xy + cdot_xy / omega0[b * omega0_stride]  (the plan's first-knot omega).
+ *   com [B][6] = (c, cdot); xi [B][2] (may be the next solve's xi_init) or NULL.            */
+blf_status blf_fb_dcm(blf_handle* handle, const blf_fb_model* model, const blf_fb_state* state,
+                      const double* omega0, int64_t omega0_stride, int64_t batch, double* com,
+                      double* xi, void* stream);
+
+/* blf_dcm_posture_reference: plan -> joint references, held over the control period:
+ *   q_ref[b][j] = q_nominal_j + lean_j0 (r0_x - c_x) + lean_j1 (r0_y - c_y)
+ *   with r0 = vrp[b * vrp_stride + (0, 1)] (the plan's first VRP) and c = com[b][0..1].  The joint
+ *   impedance of blf_fbd_euler_integrate_impedance tracks them.                               */
+typedef struct blf_posture_law {
+    int32_t ndof;                 /* n                                                       */
+    int32_t reserved;
+    const double* q_nominal;      /* [n]                                                     */
+    const double* lean;           /* [n][2] joint offset per metre of (r0 - c)              */
+} blf_posture_law;
+blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* law,
+                                     const double* com, const double* vrp, int64_t vrp_stride,
+                                     int64_t batch, double* q_ref, void* stream);
+
+/* blf_fbd_euler_integrate_impedance: ForwardEuler<FloatingBaseDynamicalSystem>::integrate(t0, T)
+ * (the schedule of blf_fbd_euler_integrate) with the control input set before EVERY step from a
+ * joint impedance, tau = kp (q_ref - q) - kd qdot at the step's start state: the reference loop
+ * `system->setControlInput(tau(x)); integrator.integrate(t_i, t_i + dT_i)` a user writes for a
+ * joint-level controller faster than the planner, in one launch.                             */
+typedef struct blf_joint_impedance {
+    int32_t ndof;                 /* n, must match the model                                 */
+    int32_t reserved;
+    const double* kp;             /* [n]                                                     */
+    const double* kd;             /* [n]                                                     */
+    const double* q_ref;          /* [B][n]                                                  */
+} blf_joint_impedance;
+blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_model* model,
+                                             const blf_fb_state* state,
+                                             const blf_joint_impedance* impedance,
+                                             const blf_fb_contacts* contacts,
+                                             const double* mass_reg, int64_t batch,
+                                             double initial_time, double final_time, double dT,
+                                             void* stream);
 
 /* Algorithmic flop count of one IPM iteration of one problem (what the fp64 roofline field
  * of bench.py is computed from); `active_facets` = sum_k nfacets[k]. */
