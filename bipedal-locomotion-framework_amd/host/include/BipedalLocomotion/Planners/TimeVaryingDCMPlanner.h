@@ -30,6 +30,7 @@
 #include <BipedalLocomotion/ParametersHandler/IParametersHandler.h>
 #include <BipedalLocomotion/Planners/ContactPhaseList.h>
 #include <BipedalLocomotion/System/Advanceable.h>
+#include <BipedalLocomotion/System/VariablesHandler.h>
 #include <blf/device.h>
 
 namespace BipedalLocomotion
@@ -46,6 +47,9 @@ struct DCMPlanBatch
     std::vector<double> vrp;          /**< [batch][horizon][2]   */
     std::vector<int32_t> status;      /**< [batch] BLF_QP_*      */
     std::vector<int32_t> iterations;  /**< [batch]               */
+    /** [batch][n] each problem's QP variables in the planner's VariablesHandler layout
+     * (TimeVaryingDCMPlanner::variablesHandler(): "dcm" then "vrp", n = 4 horizon + 2). */
+    std::vector<double> variables;
 };
 
 class TimeVaryingDCMPlanner : public System::Advanceable<DCMPlanBatch>
@@ -64,7 +68,9 @@ class TimeVaryingDCMPlanner : public System::Advanceable<DCMPlanBatch>
     // host view of the phase table: the span each problem's window must stay in
     int m_maxPhases{0};
     std::vector<double> m_planBegin, m_planEnd;   /**< [batch] first begin, last end */
-    std::vector<double> m_badBegin, m_badEnd;     /**< [batch] first phase without support */
+    /** [batch] the [begin, end) of every phase without an active contact */
+    std::vector<std::vector<std::pair<double, double>>> m_unsupported;
+    System::VariablesHandler m_variables;         /**< the QP layout: "dcm", "vrp" */
 
     bool m_tableDirty{true}, m_omegaDirty{true}, m_xi0Dirty{true};
     bool m_haveWarm{false};
@@ -109,8 +115,16 @@ public:
 
     const DCMPlanBatch& get() const final;
     bool isValid() const final;
+    /** Expand the window, solve every problem's QP (warm-started) and move the window one knot.
+     * True when the solve was enqueued: a problem whose QP ended at the iteration cap still
+     * hands its iterate (xi_1, multipliers) to the next window's warm start; isValid() tells
+     * whether every problem of the current plan is solved (status BLF_QP_SOLVED). */
     bool advance() final;
 
+    /** The QP's variable layout (System/src/VariablesHandler.cpp:13-48):
+     * "dcm" -> (0, 2 (N + 1)) and "vrp" -> (2 (N + 1), 2 N), registered by initialize(); the
+     * plan's `variables` rows are laid out by it. */
+    const System::VariablesHandler& variablesHandler() const { return m_variables; }
     const blf_dcm_mpc_params& parameters() const { return m_params; }
     int currentKnot() const { return m_start; }
     /** Device pointers of the latest plan (valid until the next advance() or destruction). */

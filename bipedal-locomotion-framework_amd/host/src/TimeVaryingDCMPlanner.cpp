@@ -4,6 +4,7 @@
  * blf_hull2d_hrep (once per plan) -> blf_dcm_phase_expand -> blf_dcm_mpc_solve_warm (per
  * advance()).
  */
+#include <algorithm>
 #include <cmath>
 #include <iostream>
 #include <limits>
@@ -83,6 +84,11 @@ bool TimeVaryingDCMPlanner::initialize(std::weak_ptr<ParametersHandler::IParamet
                   << std::endl;
         return false;
     }
+    // the QP's variable layout: the DCM knots, then the VRPs
+    m_variables = System::VariablesHandler();
+    if (!m_variables.addVariable("dcm", 2 * static_cast<std::size_t>(horizon + 1)) ||
+        !m_variables.addVariable("vrp", 2 * static_cast<std::size_t>(horizon)))
+        return false;
     m_start = 0;
     m_solved = false;
     m_haveWarm = false;
@@ -144,8 +150,7 @@ bool TimeVaryingDCMPlanner::buildPhaseTable(blf_handle* h)
     const double inf = std::numeric_limits<double>::infinity();
     m_planBegin.assign(B, inf);
     m_planEnd.assign(B, -inf);
-    m_badBegin.assign(B, inf);
-    m_badEnd.assign(B, -inf);
+    m_unsupported.assign(B, {});
     for (int b = 0; b < B; ++b)
     {
         const ContactPhaseList& plan = m_plans[b];
@@ -158,6 +163,13 @@ bool TimeVaryingDCMPlanner::buildPhaseTable(blf_handle* h)
             // deterministic corner order: active contacts sorted by list name
             std::map<std::string, ContactList::const_iterator> active(
                 plan[p].activeContacts.begin(), plan[p].activeContacts.end());
+            if (active.size() > static_cast<std::size_t>(kCorners / 4))
+            {   // the support polygon holds two rectangular feet (8 corners) at most
+                std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b << ": phase " << p
+                          << " has " << active.size() << " active contacts; at most "
+                          << kCorners / 4 << " are supported." << std::endl;
+                return false;
+            }
             int c = 0;
             double sx = 0.0, sy = 0.0;
             for (const auto& entry : active)
@@ -179,11 +191,8 @@ bool TimeVaryingDCMPlanner::buildPhaseTable(blf_handle* h)
                 ref[2 * row] = sx / c;
                 ref[2 * row + 1] = sy / c;
             }
-            else if (m_badBegin[b] == inf)
-            {   // no support polygon: a window touching this phase cannot be planned
-                m_badBegin[b] = plan[p].beginTime;
-                m_badEnd[b] = plan[p].endTime;
-            }
+            else   // no support polygon: a window touching this phase cannot be planned
+                m_unsupported[b].emplace_back(plan[p].beginTime, plan[p].endTime);
             if (p == 0) m_planBegin[b] = plan[p].beginTime;
             m_planEnd[b] = plan[p].endTime;
         }
@@ -216,12 +225,13 @@ bool TimeVaryingDCMPlanner::checkWindow() const
                       << t0 << ", " << t1 << "] leaves the contact phases." << std::endl;
             return false;
         }
-        if (m_badBegin[b] <= t1 && t0 < m_badEnd[b])
-        {
-            std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b
-                      << ": no active contact in a phase of the window." << std::endl;
-            return false;
-        }
+        for (const auto& bad : m_unsupported[b])
+            if (bad.first <= t1 && t0 < bad.second)
+            {
+                std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b
+                          << ": no active contact in a phase of the window." << std::endl;
+                return false;
+            }
     }
     return true;
 }
@@ -324,6 +334,19 @@ void TimeVaryingDCMPlanner::download() const
     if (ok)
     {
         for (int b = 0; b < B; ++b) ok = ok && m_output.status[b] == BLF_QP_SOLVED;
+        // each problem's QP variables in the VariablesHandler layout
+        const System::IndexRange dcm = m_variables.getVariable("dcm");
+        const System::IndexRange vrp = m_variables.getVariable("vrp");
+        const std::size_t n = m_variables.getNumberOfVariables();
+        m_output.variables.assign(static_cast<std::size_t>(B) * n, 0.0);
+        for (int b = 0; b < B; ++b)
+        {
+            double* row = m_output.variables.data() + static_cast<std::size_t>(b) * n;
+            std::copy_n(m_output.dcm.data() + static_cast<std::size_t>(b) * dcm.size, dcm.size,
+                        row + dcm.offset);
+            std::copy_n(m_output.vrp.data() + static_cast<std::size_t>(b) * vrp.size, vrp.size,
+                        row + vrp.offset);
+        }
     }
     else
     {

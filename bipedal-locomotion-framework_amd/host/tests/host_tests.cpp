@@ -390,6 +390,25 @@ static void testPlanner()
     }
     REQUIRE(itWarm < 0.8 * itCold);
     REQUIRE(maxDiff < 1e-6);
+    // the QP layout contract (VariablesHandlerTest.cpp:15-35): "dcm" then
+    // "vrp", and the plan's variable rows read through it equal the dcm / vrp arrays
+    {
+        const VariablesHandler& vh = warmPlanner.variablesHandler();
+        const IndexRange dcm = vh.getVariable("dcm"), vrp = vh.getVariable("vrp");
+        REQUIRE(dcm.offset == 0 && dcm.size == 2 * 101);
+        REQUIRE(vrp.offset == 2 * 101 && vrp.size == 2 * 100);
+        REQUIRE(vh.getNumberOfVariables() == 4 * 100 + 2);
+        REQUIRE_FALSE(vh.getVariable("com").isValid());
+        const DCMPlanBatch& a = warmPlanner.get();
+        const std::size_t n = vh.getNumberOfVariables();
+        REQUIRE(a.variables.size() == 16 * n);
+        bool same = true;
+        for (int b = 0; b < 16; ++b)
+            for (std::ptrdiff_t i = 0; i < vrp.size; ++i)
+                same = same && a.variables[b * n + vrp.offset + i] == a.vrp[b * vrp.size + i] &&
+                       (i >= dcm.size || a.variables[b * n + dcm.offset + i] == a.dcm[b * dcm.size + i]);
+        REQUIRE(same);
+    }
     // a window that runs past the plan's last phase is refused
     TimeVaryingDCMPlanner shortPlanner;
     auto longH = std::make_shared<ParametersHandler::StdImplementation>();
