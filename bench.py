@@ -342,17 +342,22 @@ def other_workload(args):
     if args.workload == "c3":
         B = 65536
         prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED)
-        d = {k: torch.from_numpy(prob[k]).to(dev) for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
-        corners = torch.from_numpy(prob["corners"]).to(dev)
-        ncorners = torch.from_numpy(prob["ncorners"]).to(dev)
+        t = lambda k: torch.from_numpy(prob[k]).to(dev)
+        d = {k: t(k) for k in ("xi_init", "omega")}
         kt, kp, tq = (torch.from_numpy(a).to(dev) for a in P.swing_splines(prob, queries=32))
         params = native.default_params(N)
         out = {}
+        Pn = prob["phase_begin"].shape[1]
 
         def step():
-            A, b, nf = h.assemble_constraints(corners, ncorners)
-            d.update(A=A, b=b, nfacets=nf)
-            out["qp"] = h.dcm_mpc_solve(d, params)
+            # ConvexHullHelper on every phase's support polygon (blf_hull2d_hrep), the knots'
+            # constraints and references from the phase table (blf_dcm_phase_expand), the QPs,
+            # then the swing-foot splines
+            table = h.phase_table(t("nphases"), t("phase_begin"), t("phase_end"), t("phase_corners"),
+                                  t("phase_ncorners"), ref=t("phase_ref"))
+            w = h.dcm_phase_expand(table, 0, prob["dt"], N)
+            w.update(d)
+            out["qp"] = h.dcm_mpc_solve(w, params)
             coeffs = h.quintic_fit(kt, kp)
             out["sp"] = h.quintic_eval(kt, coeffs, tq)
 
@@ -361,9 +366,12 @@ def other_workload(args):
         line = {"metric": "DCM-MPC pipeline solves/sec (hull H-rep + QP + swing splines)",
                 "value": B / sec, "unit": "QP/s", "n_gpus": 1, "ms_per_step": sec * 1e3,
                 "steps": args.steps, "warmup": args.warmup, "dtype": "f64",
-                "config": {"workload": f"configs[2]: batch={B}, horizon={N}, "
-                                       f"{B * (N)} support polygons, {kt.shape[0]} swing splines "
-                                       f"x 32 queries", "batch_per_gpu": B}}
+                "config": {"workload": f"configs[2]: batch={B}, horizon={N}, {B * Pn} phase "
+                                       f"support polygons (hull H-rep) expanded to the knots, "
+                                       f"{kt.shape[0]} swing splines x 32 queries",
+                           "batch_per_gpu": B}}
+        if not args.no_cpu:
+            line["cpu_baseline"] = pipeline_cpu(N)
     else:
         return closed_loop(args, h, dev)
     print(json.dumps(line), flush=True)
@@ -448,6 +456,39 @@ def closed_loop(args):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pipeline_cpu(N, B=2048):
+    """configs[2] on the CPU, a bounded sample of B problems: the oracle's hull of every phase
+    polygon, its phase expansion, the QPs (sequential recursions, one problem per thread on the
+    CPUs the process may use) and the swing splines, the same stages as the device step."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    import closed_loop as CL
+    from blf import problems as P
+    prob = P.make_batch(B, horizon=N, n_footsteps=6, seed=P.SEED)
+    kt, kp, tq = P.swing_splines(prob, queries=32)
+    threads = cpu_threads()
+    prm = O.default_params(N, sequential=1)
+    t0 = time.perf_counter()
+    table = CL.phase_table(prob)
+    w = O.dcm_phase_expand(table, 0, prob["dt"], N)
+    w.update(xi_init=prob["xi_init"], omega=prob["omega"])
+    t1 = time.perf_counter()
+    st, _, _, _ = O.dcm_mpc_solve_batch(w, params=prm, threads=threads)
+    t2 = time.perf_counter()
+    for s in range(kt.shape[0]):
+        O.quintic_eval(kt[s], O.quintic_fit(kt[s], kp[s]), tq[s])
+    t3 = time.perf_counter()
+    assert (st == 0).all()
+    el = t3 - t0
+    return {"value": B / el, "unit": "QP/s", "cores": threads, "kind": "port",
+            "sample": f"{B} problems: phase hulls + expansion {t1 - t0:.3f} s (1 thread), QPs "
+                      f"{t2 - t1:.3f} s ({threads} threads, oracle sequential mode), "
+                      f"{kt.shape[0]} splines x 32 queries {t3 - t2:.3f} s (1 thread); the hull "
+                      f"and spline stages call the oracle per polygon / spline from Python, so "
+                      f"they include the ctypes call overhead"}
 
 
 def closed_loop_cpu(args, model, N, robots=8, periods=2):
