@@ -21,6 +21,23 @@ namespace blf {
 namespace {
 using namespace qp;
 
+#ifdef BLF_STAMPS
+// Diagnostic build only (make stamps): per-phase cycle sums of lane 0 for the first 64 QPs.
+// [0] whole kernel, [1] slab staging + knot loads, [2] LQ step, [3] guess, [4] pass: setup +
+// residuals, [5] pass: Riccati sweep, [6] pass: h, [7] pass: solve, [8] pass: certificate,
+// [9] pass: vote + restore, [10] passes (count), [11] outputs.
+__device__ unsigned long long g_as_stamps[16];
+#define AS_STAMP(t) unsigned long long t = __builtin_amdgcn_s_memtime()
+#define AS_STAMP_ADD(slot, t0) \
+    do { if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_as_stamps[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
+#define AS_COUNT(slot) \
+    do { if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_as_stamps[slot], 1ull); } while (0)
+#else
+#define AS_STAMP(t)
+#define AS_STAMP_ADD(slot, t0)
+#define AS_COUNT(slot)
+#endif
+
 // Per-knot state of the active-set passes.
 struct AKnot {
     int m;                          // facet count
@@ -290,54 +307,55 @@ __device__ __forceinline__ void as_solve(const AKnot (&K)[KPL], const double (&g
 
 // Candidate facets of a pass -> (pc, pi1, pi2) packed as pc | pi1 << 2 | pi2 << 5, the VRP moved
 // onto the active lines and E_k (IPM kernel polish block, "active sets, projection").
+// Branch-free: the two knots of a lane, and the lanes of a wavefront, have every mix of 0, 1 and 2
+// active lines, so per-case branches serialised all three bodies and their divisions.  Each knot
+// instead evaluates exactly two quotients whose operands its case selects (c = 0: b2 / Rw0,
+// b2 / Rw1; c = 1: (a r - b) / |a|^2, b2 / (Rw0 a_y^2 + Rw1 a_x^2); c = 2: 1 / det) — the same
+// operations as the per-case form of the oracle, so the results are bit-identical.
 __device__ __forceinline__ void as_pass_setup(AKnot& K, const KParams& P, const double2* A2, const double* Bv,
                                               int S, int col, double sr0, double sr1, int& pk, double (&E)[3],
                                               bool& okp)
 {
     const int cx = opaque(col);
     const int km = opaque(K.m);
-    int pc = 0, pi1 = 0, pi2 = 0, cm = 0;
-    for (int i = 0; i < km; ++i) {
-        if ((((K.gm >> i) & 1) && !((K.drop >> i) & 1)) || ((K.add >> i) & 1)) {
-            if (pc == 0) pi1 = i;
-            else if (pc == 1) pi2 = i;
-            ++pc;
-            cm |= 1 << i;
-        }
-    }
+    // candidates: guessed and not dropped, or added (bit i, i < m); the first two in facet order
+    const int cm = ((K.gm & ~K.drop) | K.add) & ((1 << km) - 1);
+    int pc = __builtin_popcount(cm);
+    const int cm2 = cm & (cm - 1);
+    int pi1 = cm ? __builtin_ctz(cm) : 0;
+    int pi2 = cm2 ? __builtin_ctz(cm2) : 0;
     if (pc > 2) pc = vertex_pair(A2, Bv, 1, S, cx, km, cm, P.tol_p, pi1, pi2);
     if (pc > 2) okp = false;
-    pk = (pc < 3 ? pc : 2) | (pi1 << 2) | (pi2 << 5);
+    const int c = pc < 3 ? pc : 2;
+    pk = c | (pi1 << 2) | (pi2 << 5);
     const double b2 = K.be * K.be;
-    E[0] = E[1] = E[2] = 0.0;
-    if (pc == 0) {
-        E[0] = b2 / P.Rw0;
-        E[2] = b2 / P.Rw1;
-    } else if (pc == 1) {
-        const double2 a = A2[pi1 * S + cx];
-        const double aa = FD2(a.x, a.x, a.y, a.y);
-        const double t = (FD2(a.x, sr0, a.y, sr1) - Bv[pi1 * S + cx]) / aa;
-        K.r0 = fma(-t, a.x, sr0);
-        K.r1 = fma(-t, a.y, sr1);
-        const double u = a.y * a.y, v = a.x * a.x, q = a.x * a.y;
-        const double ie = b2 / FD2(P.Rw0, u, P.Rw1, v);
-        E[0] = u * ie;
-        E[1] = -(q * ie);
-        E[2] = v * ie;
-    } else {
-        const double2 a = A2[pi1 * S + cx];
-        const double2 e = A2[pi2 * S + cx];
-        const double ba = Bv[pi1 * S + cx], be = Bv[pi2 * S + cx];
-        const double det = fma(a.x, e.y, -(a.y * e.x));
-        const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
-        if (!(det * det > 1e-18 * (aa * ee))) okp = false;
-        const double idet = 1.0 / det;
-        K.r0 = fma(ba, e.y, -(a.y * be)) * idet;
-        K.r1 = fma(a.x, be, -(ba * e.x)) * idet;
+    const double2 a = A2[pi1 * S + cx];
+    const double2 e = A2[pi2 * S + cx];
+    const double ba = Bv[pi1 * S + cx], be = Bv[pi2 * S + cx];
+    const double aa = FD2(a.x, a.x, a.y, a.y);
+    const double u = a.y * a.y, v = a.x * a.x, q = a.x * a.y;
+    const double det = fma(a.x, e.y, -(a.y * e.x));
+    const double n1 = c == 0 ? b2 : c == 1 ? FD2(a.x, sr0, a.y, sr1) - ba : 1.0;
+    const double d1 = c == 0 ? P.Rw0 : c == 1 ? aa : det;
+    const double d2 = c == 0 ? P.Rw1 : c == 1 ? FD2(P.Rw0, u, P.Rw1, v) : 1.0;
+    const double q1 = n1 / d1;   // c = 0: E00; c = 1: t; c = 2: 1 / det
+    const double q2 = b2 / d2;   // c = 0: E11; c = 1: ie
+    if (c == 2) {
+        const double ee = FD2(e.x, e.x, e.y, e.y);
+        if (!(det * det > 1e-18 * (aa * ee))) okp = false;   // (nearly) parallel active facets
     }
+    const double p0 = c == 1 ? fma(-q1, a.x, sr0) : fma(ba, e.y, -(a.y * be)) * q1;
+    const double p1 = c == 1 ? fma(-q1, a.y, sr1) : fma(a.x, be, -(ba * e.x)) * q1;
+    K.r0 = c == 0 ? K.r0 : p0;
+    K.r1 = c == 0 ? K.r1 : p1;
+    E[0] = c == 0 ? q1 : c == 1 ? u * q2 : 0.0;
+    E[1] = c == 1 ? -(q * q2) : 0.0;
+    E[2] = c == 0 ? q2 : c == 1 ? v * q2 : 0.0;
 }
 
-// h_k = H_k^{-1} of the knot's active subspace after the Riccati sweep (IPM kernel polish block).
+// h_k = H_k^{-1} of the knot's active subspace after the Riccati sweep (IPM kernel polish block):
+// c = 0: B^{-1}; c = 1: t t^T / (t^T B t), t = (-a_y, a_x); c = 2: 0.  One quotient per knot,
+// operands selected by the case (bit-identical to the per-case form).
 __device__ __forceinline__ void as_pass_h(AKnot& K, const KParams& P, const double2* A2, int S, int col, int pk,
                                           bool& okp)
 {
@@ -346,31 +364,21 @@ __device__ __forceinline__ void as_pass_h(AKnot& K, const KParams& P, const doub
     const double B00 = fma(b2, K.P00, P.Rw0);
     const double B01 = b2 * K.P01;
     const double B11 = fma(b2, K.P11, P.Rw1);
-    if (pc == 0) {
-        const double det = fma(B00, B11, -(B01 * B01));
-        if (!(det > 0.0) || __builtin_isinf(det)) okp = false;
-        const double idet = 1.0 / det;
-        K.h00 = B11 * idet;
-        K.h01 = -(B01 * idet);
-        K.h11 = B00 * idet;
-    } else if (pc == 1) {
-        const double2 a = A2[pi1 * S + opaque(col)];
-        const double u = a.y * a.y, v = a.x * a.x, q = a.x * a.y;
-        const double tbt = FD3(B00, u, B11, v, -2.0 * (B01 * q));
-        if (!(tbt > 0.0) || __builtin_isinf(tbt)) okp = false;
-        const double itb = 1.0 / tbt;
-        K.h00 = u * itb;
-        K.h01 = -(q * itb);
-        K.h11 = v * itb;
-    } else {
-        K.h00 = 0.0;
-        K.h01 = 0.0;
-        K.h11 = 0.0;
-    }
+    const double2 a = A2[pi1 * S + opaque(col)];
+    const double u = a.y * a.y, v = a.x * a.x, q = a.x * a.y;
+    const double detB = fma(B00, B11, -(B01 * B01));
+    const double tbt = FD3(B00, u, B11, v, -2.0 * (B01 * q));
+    const double den = pc == 0 ? detB : pc == 1 ? tbt : 1.0;
+    if (pc < 2 && (!(den > 0.0) || __builtin_isinf(den))) okp = false;
+    const double id = 1.0 / den;
+    K.h00 = pc == 0 ? B11 * id : pc == 1 ? u * id : 0.0;
+    K.h01 = pc == 0 ? -(B01 * id) : pc == 1 ? -(q * id) : 0.0;
+    K.h11 = pc == 0 ? B00 * id : pc == 1 ? v * id : 0.0;
 }
 
 // The certificate of one knot after the step (IPM kernel polish block): stationarity with the
 // solve's costates, multiplier signs, primal feasibility of every facet; drop / add bookkeeping.
+// One quotient per knot (c = 1: (a g) / |a|^2; c = 2: 1 / det), operands selected by the case.
 __device__ __forceinline__ void as_certify(AKnot& K, const KParams& P, const double2* A2, const double* Bv,
                                            int S, int col, int pk, double dx0, double dx1, double vn0,
                                            double vn1, double& l1o, double& l2o, bool& okp, bool& neg,
@@ -386,41 +394,25 @@ __device__ __forceinline__ void as_certify(AKnot& K, const KParams& P, const dou
     const double rh1 = P.Rw1 * (K.r1 - K.rr1);
     const double g0 = fma(K.be, nu0, -rh0);
     const double g1 = fma(K.be, nu1, -rh1);
-    l1o = l2o = 0.0;
-    if (pc == 0) {
-        if (!(fabs(g0) <= P.tol_d) || !(fabs(g1) <= P.tol_d)) okp = false;
-    } else if (pc == 1) {
-        const double2 a = A2[pi1 * S + cx];
-        const double l1 = FD2(a.x, g0, a.y, g1) / FD2(a.x, a.x, a.y, a.y);
-        l1o = l1;
-        if (!(l1 >= -P.tol_d)) {
-            okp = false;
-            neg = true;
-            K.drop |= 1 << pi1;
-            K.add &= ~(1 << pi1);
-        }
-        if (!(fabs(fma(-l1, a.x, g0)) <= P.tol_d) || !(fabs(fma(-l1, a.y, g1)) <= P.tol_d)) okp = false;
-    } else {
-        const double2 a = A2[pi1 * S + cx];
-        const double2 e = A2[pi2 * S + cx];
-        const double idet = 1.0 / fma(a.x, e.y, -(a.y * e.x));
-        const double l1 = fma(g0, e.y, -(e.x * g1)) * idet;
-        const double l2 = fma(a.x, g1, -(g0 * a.y)) * idet;
-        l1o = l1;
-        l2o = l2;
-        if (!(l1 >= -P.tol_d)) {
-            okp = false;
-            neg = true;
-            K.drop |= 1 << pi1;
-            K.add &= ~(1 << pi1);
-        }
-        if (!(l2 >= -P.tol_d)) {
-            okp = false;
-            neg = true;
-            K.drop |= 1 << pi2;
-            K.add &= ~(1 << pi2);
-        }
-    }
+    const double2 a = A2[pi1 * S + cx];
+    const double2 e = A2[pi2 * S + cx];
+    const double n = pc == 1 ? FD2(a.x, g0, a.y, g1) : 1.0;
+    const double d = pc == 1 ? FD2(a.x, a.x, a.y, a.y) : fma(a.x, e.y, -(a.y * e.x));
+    const double qd = n / d;
+    const double l1 = pc == 1 ? qd : pc == 2 ? fma(g0, e.y, -(e.x * g1)) * qd : 0.0;
+    const double l2 = pc == 2 ? fma(a.x, g1, -(g0 * a.y)) * qd : 0.0;
+    l1o = l1;
+    l2o = l2;
+    bool bad = false;
+    if (pc == 0) bad = !(fabs(g0) <= P.tol_d) || !(fabs(g1) <= P.tol_d);
+    if (pc == 1) bad = !(fabs(fma(-l1, a.x, g0)) <= P.tol_d) || !(fabs(fma(-l1, a.y, g1)) <= P.tol_d);
+    const bool n1 = pc >= 1 && !(l1 >= -P.tol_d);
+    const bool n2 = pc == 2 && !(l2 >= -P.tol_d);
+    const int dm = (n1 ? 1 << pi1 : 0) | (n2 ? 1 << pi2 : 0);
+    if (bad || dm) okp = false;
+    if (dm) neg = true;
+    K.drop |= dm;
+    K.add &= ~dm;
     // primal feasibility of every facet, rows read four at a time
     const int km = opaque(K.m);
     int vm = 0;
@@ -466,38 +458,24 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
     double* Bv = smem + 2 * (size_t)M * S;              // [M][S] offsets
     const int lane = threadIdx.x;
     const int64_t p = blockIdx.x;
+    AS_STAMP(t_start);
 
     // ---- the QP's facet slabs A [N][M][2], b [N][M] into LDS: coalesced (consecutive lanes on
-    //      consecutive 16 B, U loads of a lane in flight before its LDS stores) ----
+    //      consecutive 16 B).  Every load of the start-up is issued before the first wait: the
+    //      slab loads (one round, U per lane covers N M <= 128 x 8), then the knots' own loads,
+    //      then the LDS stores, which wait for the slab loads only. ----
+    const int nA = N * M;
+    constexpr int U = (2 * kWave * kMaxFacets) / kWave;   // 16: nA <= 1024 in one round
+    double2 va[U];
+    double vb[U];
     {
-        const int nA = N * M;
         const double2* As = reinterpret_cast<const double2*>(Ain) + p * nA;
         const double* bs = bin + p * nA;
-        const bool pow2 = (M & (M - 1)) == 0;
-        const int sh = __builtin_ctz(M);
-        auto at = [&](int t) {
-            const int k = pow2 ? t >> sh : t / M, i = t - k * M;
-            return i * S + (k % KPL) * NH + k / KPL;
-        };
-        constexpr int U = 8;
-        for (int t0 = 0; t0 < nA; t0 += U * kWave) {
-            double2 va[U];
-            double vb[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
-                const int t = min(t0 + u * kWave + lane, nA - 1);
-                va[u] = As[t];
-                vb[u] = bs[t];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = t0 + u * kWave + lane;
-                if (t < nA) {
-                    const int o = at(t);
-                    A2[o] = va[u];
-                    Bv[o] = vb[u];
-                }
-            }
+        for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
+            const int t = min(u * kWave + lane, nA - 1);
+            va[u] = As[t];
+            vb[u] = bs[t];
         }
     }
 
@@ -519,12 +497,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
         if (k < N) {
             const int64_t st = p * N + k;
             Kj.m = nfacets[st];
-            if (Kj.m < 0 || Kj.m > M) {
-                bad = true;
-                Kj.m = 0;
-            }
             Kj.w = omega[st];
-            Kj.be = P.dt * Kj.w;
             const bool ws = warm && k + P.ws_shift < N;
             const double* r0 = ws ? ws_vrp + 2 * P.ws_shift : vrp_ref;
             Kj.r0 = r0[2 * st];
@@ -535,10 +508,37 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
             Kj.xr0 = xi_ref[2 * sx];
             Kj.xr1 = xi_ref[2 * sx + 1];
         }
+    }
+    {
+        const bool pow2 = (M & (M - 1)) == 0;
+        const int sh = __builtin_ctz(M);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = u * kWave + lane;
+            if (t < nA) {
+                const int k = pow2 ? t >> sh : t / M, i = t - k * M;
+                const int o = i * S + (k % KPL) * NH + k / KPL;
+                A2[o] = va[u];
+                Bv[o] = vb[u];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        AKnot& Kj = K[j];
+        if (KPL * lane + j < N) {
+            if (Kj.m < 0 || Kj.m > M) {
+                bad = true;
+                Kj.m = 0;
+            }
+            Kj.be = P.dt * Kj.w;
+        }
         Kj.al = 1.0 + Kj.be;
     }
     const bool any_bad = __ballot(bad) != 0;
     __syncthreads();   // the LDS slabs (one wavefront: a wait for the stores)
+    AS_STAMP_ADD(1, t_start);
+    AS_STAMP(t_lq);
 
     // ---- initial point: a warm start rolls xi out from its VRPs (forward scan of
     //      xi_{k+1} = alpha_k xi_k - beta_k r_k); a cold start takes xi_ref, then the LQ step ----
@@ -652,7 +652,9 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
         }
     }
 
+    AS_STAMP_ADD(2, t_lq);
     if (status == 0) {
+        AS_STAMP(t_g);
         // ---- the guess: facets the start point violates (warm: also those whose previous
         //      multiplier exceeds the floor) ----
 #pragma unroll
@@ -677,7 +679,10 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
         // ---- active-set passes (oracle dcm_polish with the guess) ----
         double xk[KPL][2];
         as_xi_prev<KPL>(K, lane, xi00, xi01, xk);
+        AS_STAMP_ADD(3, t_g);
         for (int pass = 0; pass < kGuessPasses; ++pass) {
+            AS_COUNT(10);
+            AS_STAMP(t_s);
             double sv[KPL][4];
             double E[KPL][3];
             bool okp = true;
@@ -692,10 +697,15 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
                     as_residuals(K[j], P, k == N - 1, xk[j][0], xk[j][1]);
                 }
             }
+            AS_STAMP_ADD(4, t_s);
+            AS_STAMP(t_r);
             okp = as_riccati<KPL>(K, P, E, N, lane) && okp;
+            AS_STAMP_ADD(5, t_r);
+            AS_STAMP(t_h);
 #pragma unroll
             for (int j = 0; j < KPL; ++j)
                 if (KPL * lane + j < N) as_pass_h(K[j], P, A2, S, j * NH + lane, opaque(pk[j]), okp);
+            AS_STAMP_ADD(6, t_h);
             // the Newton step, then the certificate (costates of the new point from the solve)
             bool neg = false, viol = false;
             {
@@ -705,7 +715,10 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
                     g[j][0] = K[j].rh0;
                     g[j][1] = K[j].rh1;
                 }
+                AS_STAMP(t_v);
                 as_solve<KPL>(K, g, N, lane, dr, dx, vn);
+                AS_STAMP_ADD(7, t_v);
+                AS_STAMP(t_c);
 #pragma unroll
                 for (int j = 0; j < KPL; ++j) {
                     pl[j][0] = pl[j][1] = 0.0;
@@ -718,9 +731,12 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
                                    vn[j][0], vn[j][1], pl[j][0], pl[j][1], okp, neg, viol);
                     }
                 }
+                AS_STAMP_ADD(8, t_c);
             }
+            AS_STAMP(t_o);
             if (__ballot(!okp) == 0) {
                 certified = true;
+                AS_STAMP_ADD(9, t_o);
                 break;
             }
             const bool more = __ballot(neg || viol) != 0;
@@ -731,9 +747,11 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
                 K[j].x0 = sv[j][2];
                 K[j].x1 = sv[j][3];
             }
+            AS_STAMP_ADD(9, t_o);
             if (!more) break;
         }
     }
+    AS_STAMP(t_out);
 
     // ---- outputs: the solution (certified), the oracle's outputs of a bad or failed start
     //      (status 3 / 2), or the start point for the IPM kernel's stage 2 (kPending) ----
@@ -767,6 +785,8 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_as_kernel(
             if (polished_out) polished_out[p] = certified ? 1 : 0;
         }
     }
+    AS_STAMP_ADD(11, t_out);
+    AS_STAMP_ADD(0, t_start);
 }
 
 template <int KPL>
@@ -785,6 +805,20 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
 }
 
 }  // namespace
+
+#ifdef BLF_STAMPS
+extern "C" int blf_debug_as_stamps(unsigned long long* out, int reset)
+{
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_as_stamps), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < 16; ++i) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_as_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 // Active-set kernel of a launch_dcm_mpc call (N <= 128, tol_polish > 0): every QP either solved
 // (status 0, polished) or marked kPending for the IPM kernel's stage 2.

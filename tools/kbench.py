@@ -47,6 +47,11 @@ def run(args, tol_polish):
     if stamps is not None:
         stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         stamps(ctypes.cast(buf, ctypes.c_void_p), 1)
+    as_stamps = getattr(L, "blf_debug_as_stamps", None) if hasattr(L, "blf_debug_as_stamps") else None
+    abuf = (ctypes.c_ulonglong * 16)()
+    if as_stamps is not None:
+        as_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        as_stamps(ctypes.cast(abuf, ctypes.c_void_p), 1)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.reps):
@@ -58,8 +63,17 @@ def run(args, tol_polish):
           f"{ms:.3f} ms/solve, polished {out['polished'].float().mean().item():.3f}, "
           f"{args.batch / ms * 1e3:.0f} QP/s, mean iters {out['iters'].float().mean().item():.2f}, "
           f"status!=0: {int((out['status'] != 0).sum())}")
-    if stamps is not None:
-        stamps(ctypes.cast(buf, ctypes.c_void_p), 0)
+    if as_stamps is not None:
+        as_stamps(ctypes.cast(abuf, ctypes.c_void_p), 0)
+        q = 64 * args.reps
+        npass = max(abuf[10], 1)
+        print(f"active-set kernel, lane 0 cycles per QP: total {abuf[0] / q:.0f}, staging + knot loads "
+              f"{abuf[1] / q:.0f}, LQ step {abuf[2] / q:.0f}, guess {abuf[3] / q:.0f}, outputs "
+              f"{abuf[11] / q:.0f}, passes {abuf[10] / q:.2f} per QP")
+        print(f"per pass: setup + residuals {abuf[4] / npass:.0f}, Riccati sweep {abuf[5] / npass:.0f}, "
+              f"h {abuf[6] / npass:.0f}, solve {abuf[7] / npass:.0f}, certificate {abuf[8] / npass:.0f}, "
+              f"vote + restore {abuf[9] / npass:.0f}")
+    if stamps is not None and not stamps(ctypes.cast(buf, ctypes.c_void_p), 0) and buf[0]:
         tot, fac, sol, its = buf[0], buf[1], buf[2], max(buf[3], 1)
         res, wph, pred, step = buf[4], buf[5], buf[6], buf[7]
         print(f"thread0 cycles per QP: total {tot / 64 / args.reps:.0f}  per iteration: "
