@@ -1282,6 +1282,12 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     kp.ws_shift = warm ? warm->shift : 0;
     kp.ws_floor = warm ? warm->floor : 0.0;
     kp.stage2 = 0;
+    kp.f_dt = (float)kp.dt;
+    kp.f_Qw0 = (float)kp.Qw0; kp.f_Qw1 = (float)kp.Qw1;
+    kp.f_Rw0 = (float)kp.Rw0; kp.f_Rw1 = (float)kp.Rw1;
+    kp.f_Pw0 = (float)kp.Pw0; kp.f_Pw1 = (float)kp.Pw1;
+    kp.f_tol_p = kSearchTolP;
+    kp.f_tol_d = kSearchTolD;
     if (batch == 0) return BLF_OK;
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     const int N = kp.N;

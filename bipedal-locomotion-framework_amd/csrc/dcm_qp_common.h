@@ -19,7 +19,18 @@ struct KParams {
     double ws_floor;     // warm start: s, lambda >= ws_floor
     int stage2;          // IPM kernel after the active-set kernel: only QPs with status kPending,
                          // and no active-set start (it already failed for them)
+    // The active-set kernel's fp32 search (cold starts): the parameters rounded to float, and the
+    // search's own certificate tolerances (kSearchTolP / kSearchTolD)
+    float f_dt, f_Qw0, f_Qw1, f_Rw0, f_Rw1, f_Pw0, f_Pw1, f_tol_p, f_tol_d;
 };
+
+// Tolerances of the fp32 active-set search (oracle ORC_SEARCH_TOL_P / _D): the search only
+// proposes the active set that the fp64 passes then certify at tol_primal / tol_dual.
+constexpr float kSearchTolP = 1e-5f;
+constexpr float kSearchTolD = 1e-4f;
+// The fp64 passes' guess after the search: the facets whose slack at the float point is below
+// this (oracle ORC_GUESS_SLACK).
+constexpr double kGuessSlack = 1e-5;
 
 // The facet rows never change during a solve, so the compiler would hoist every phase's row loads
 // out of the IPM loop and keep 8 facets x 4 doubles live in VGPRs across it (spilling).  Each phase
@@ -49,6 +60,11 @@ __device__ __forceinline__ double bperm(int addr, double x)
     const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
     const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ float bperm(int addr, float x)
+{
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(x)));
 }
 
 // Fused forms used throughout (and in the same places by oracle/blf_oracle.c):
@@ -111,37 +127,43 @@ static __device__ __forceinline__ int vertex_pair(const double2* A2, const doubl
 // Riccati map element f(P) = H + A^T P (I + G P)^{-1} A (oracle rc_el); knot k: A = alpha_k I,
 // G = E_k, H = Q.  rc_combine(e, q): e <- e o q (q the later knots), the structure-preserving
 // doubling composition — it inverts only I + G H (eigenvalues >= 1).
-struct Rc {
-    double a0, a1, a2, a3, g0, g1, g2, h0, h1, h2;
+// Templated on the scalar type: double everywhere, float in the active-set kernel's fp32 search
+// (the same operations in the same order, so oracle/blf_oracle_as32.c restates them bit for bit).
+template <class T>
+struct RcT {
+    T a0, a1, a2, a3, g0, g1, g2, h0, h1, h2;
 };
+using Rc = RcT<double>;
 
-__device__ __forceinline__ bool rc_combine(Rc& e, const Rc& q)
+template <class T>
+__device__ __forceinline__ bool rc_combine(RcT<T>& e, const RcT<T>& q)
 {
-    const double T00 = FD3(e.g0, q.h0, e.g1, q.h1, 1.0);
-    const double T01 = FD2(e.g0, q.h1, e.g1, q.h2);
-    const double T10 = FD2(e.g1, q.h0, e.g2, q.h1);
-    const double T11 = FD3(e.g1, q.h1, e.g2, q.h2, 1.0);
-    const double detT = fma(T00, T11, -(T01 * T10));
-    const bool ok = (detT > 0.0) && !__builtin_isinf(detT);
-    const double it = 1.0 / detT;
-    const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
-    const double U00 = FD2(Ti00, e.a0, Ti01, e.a2);
-    const double U01 = FD2(Ti00, e.a1, Ti01, e.a3);
-    const double U10 = FD2(Ti10, e.a0, Ti11, e.a2);
-    const double U11 = FD2(Ti10, e.a1, Ti11, e.a3);
-    const double V00 = FD2(q.a0, Ti00, q.a1, Ti10);
-    const double V01 = FD2(q.a0, Ti01, q.a1, Ti11);
-    const double V10 = FD2(q.a2, Ti00, q.a3, Ti10);
-    const double V11 = FD2(q.a2, Ti01, q.a3, Ti11);
-    const double X00 = FD2(V00, e.g0, V01, e.g1);
-    const double X01 = FD2(V00, e.g1, V01, e.g2);
-    const double X10 = FD2(V10, e.g0, V11, e.g1);
-    const double X11 = FD2(V10, e.g1, V11, e.g2);
-    const double Y00 = FD2(q.h0, e.a0, q.h1, e.a2);
-    const double Y01 = FD2(q.h0, e.a1, q.h1, e.a3);
-    const double Y10 = FD2(q.h1, e.a0, q.h2, e.a2);
-    const double Y11 = FD2(q.h1, e.a1, q.h2, e.a3);
-    Rc r;
+    const T one = T(1);
+    const T T00 = FD3(e.g0, q.h0, e.g1, q.h1, one);
+    const T T01 = FD2(e.g0, q.h1, e.g1, q.h2);
+    const T T10 = FD2(e.g1, q.h0, e.g2, q.h1);
+    const T T11 = FD3(e.g1, q.h1, e.g2, q.h2, one);
+    const T detT = fma(T00, T11, -(T01 * T10));
+    const bool ok = (detT > T(0)) && !__builtin_isinf(detT);
+    const T it = one / detT;
+    const T Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
+    const T U00 = FD2(Ti00, e.a0, Ti01, e.a2);
+    const T U01 = FD2(Ti00, e.a1, Ti01, e.a3);
+    const T U10 = FD2(Ti10, e.a0, Ti11, e.a2);
+    const T U11 = FD2(Ti10, e.a1, Ti11, e.a3);
+    const T V00 = FD2(q.a0, Ti00, q.a1, Ti10);
+    const T V01 = FD2(q.a0, Ti01, q.a1, Ti11);
+    const T V10 = FD2(q.a2, Ti00, q.a3, Ti10);
+    const T V11 = FD2(q.a2, Ti01, q.a3, Ti11);
+    const T X00 = FD2(V00, e.g0, V01, e.g1);
+    const T X01 = FD2(V00, e.g1, V01, e.g2);
+    const T X10 = FD2(V10, e.g0, V11, e.g1);
+    const T X11 = FD2(V10, e.g1, V11, e.g2);
+    const T Y00 = FD2(q.h0, e.a0, q.h1, e.a2);
+    const T Y01 = FD2(q.h0, e.a1, q.h1, e.a3);
+    const T Y10 = FD2(q.h1, e.a0, q.h2, e.a2);
+    const T Y11 = FD2(q.h1, e.a1, q.h2, e.a3);
+    RcT<T> r;
     r.a0 = FD2(q.a0, U00, q.a1, U10);
     r.a1 = FD2(q.a0, U01, q.a1, U11);
     r.a2 = FD2(q.a2, U00, q.a3, U10);
@@ -156,25 +178,26 @@ __device__ __forceinline__ bool rc_combine(Rc& e, const Rc& q)
     return ok;
 }
 
-__device__ __forceinline__ bool rc_apply(const Rc& e, double P00, double P01, double P11,
-                                         double& o00, double& o01, double& o11)
+template <class T>
+__device__ __forceinline__ bool rc_apply(const RcT<T>& e, T P00, T P01, T P11, T& o00, T& o01, T& o11)
 {
-    const double S00 = FD3(e.g0, P00, e.g1, P01, 1.0);
-    const double S01 = FD2(e.g0, P01, e.g1, P11);
-    const double S10 = FD2(e.g1, P00, e.g2, P01);
-    const double S11 = FD3(e.g1, P01, e.g2, P11, 1.0);
-    const double detS = fma(S00, S11, -(S01 * S10));
-    const bool ok = (detS > 0.0) && !__builtin_isinf(detS);
-    const double is = 1.0 / detS;
-    const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
-    const double W00 = FD2(P00, Si00, P01, Si10);
-    const double W01 = FD2(P00, Si01, P01, Si11);
-    const double W10 = FD2(P01, Si00, P11, Si10);
-    const double W11 = FD2(P01, Si01, P11, Si11);
-    const double Z00 = FD2(W00, e.a0, W01, e.a2);
-    const double Z01 = FD2(W00, e.a1, W01, e.a3);
-    const double Z10 = FD2(W10, e.a0, W11, e.a2);
-    const double Z11 = FD2(W10, e.a1, W11, e.a3);
+    const T one = T(1);
+    const T S00 = FD3(e.g0, P00, e.g1, P01, one);
+    const T S01 = FD2(e.g0, P01, e.g1, P11);
+    const T S10 = FD2(e.g1, P00, e.g2, P01);
+    const T S11 = FD3(e.g1, P01, e.g2, P11, one);
+    const T detS = fma(S00, S11, -(S01 * S10));
+    const bool ok = (detS > T(0)) && !__builtin_isinf(detS);
+    const T is = one / detS;
+    const T Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
+    const T W00 = FD2(P00, Si00, P01, Si10);
+    const T W01 = FD2(P00, Si01, P01, Si11);
+    const T W10 = FD2(P01, Si00, P11, Si10);
+    const T W11 = FD2(P01, Si01, P11, Si11);
+    const T Z00 = FD2(W00, e.a0, W01, e.a2);
+    const T Z01 = FD2(W00, e.a1, W01, e.a3);
+    const T Z10 = FD2(W10, e.a0, W11, e.a2);
+    const T Z11 = FD2(W10, e.a1, W11, e.a3);
     o00 = FD3(e.a0, Z00, e.a2, Z10, e.h0);
     o01 = FD3(e.a0, Z01, e.a2, Z11, e.h1);
     o11 = FD3(e.a1, Z01, e.a3, Z11, e.h2);

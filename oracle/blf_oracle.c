@@ -339,6 +339,7 @@ double orc_wave_tree_sum(const double* c, int n)
 
 #define MF 8
 #define ORC_GUESS_PASSES 8   /* active-set start: drop/add passes (kernel: kGuessPasses) */
+#define ORC_GUESS_SLACK 1e-5  /* the fp64 passes' guess after the fp32 search (kernel: kGuessSlack) */
 #define WV 64
 
 /* Fused forms, used in exactly the places the kernel uses them (csrc/dcm_mpc_ipm.hip):
@@ -1329,6 +1330,45 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         for (int k = 1; k <= N; ++k) { xi[2 * k] = xi_ref[2 * k]; xi[2 * k + 1] = xi_ref[2 * k + 1]; }
     }
     if (status == 3) goto done;
+    /* ---- the active-set kernel's cold start (csrc/dcm_mpc_as.hip): the active
+     *      set searched in fp32 (blf_oracle_as32.c, kernel A: float LQ optimum, guess, drop/add
+     *      passes), then the fp64 passes (kernel B) from the float point with the facets active
+     *      there as the guess;
+     *      when they do not certify, the IPM's start from the fp64 LQ optimum below ---- */
+    if (!warm && prm->tol_polish > 0.0 && N <= 2 * WV && !prm->single_kernel) {
+        double* r32 = (double*)malloc(sizeof(double) * 4 * (size_t)N);
+        double* x32 = r32 + 2 * N;
+        int* g32 = (int*)malloc(sizeof(int) * (size_t)N);
+        orc_as32_search(prm, prm->sequential, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets,
+                        r32, x32, g32);
+        for (int k = 0; k < N; ++k) {
+            vrp[2 * k] = r32[2 * k];
+            vrp[2 * k + 1] = r32[2 * k + 1];
+            xi[2 * (k + 1)] = x32[2 * k];
+            xi[2 * (k + 1) + 1] = x32[2 * k + 1];
+        }
+        /* the fp64 passes' guess: the facets whose slack at the float point is below
+         * ORC_GUESS_SLACK (kernel kGuessSlack) */
+        for (int k = 0; k < N; ++k) {
+            int gk = 0;
+            for (int i = 0; i < nfacets[k]; ++i) {
+                const double* a = Ain + (k * M + i) * 2;
+                const double sl = bin[k * M + i] - FD2(a[0], vrp[2 * k], a[1], vrp[2 * k + 1]);
+                if (sl < ORC_GUESS_SLACK) gk |= 1 << i;
+            }
+            g32[k] = gk;
+        }
+        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, g32, ORC_GUESS_PASSES);
+        free(r32);
+        free(g32);
+        if (okg) { polished = 1; status = 0; it = 0; goto done; }
+        for (int k = 0; k < N; ++k) {
+            vrp[2 * k] = vrp_ref[2 * k];
+            vrp[2 * k + 1] = vrp_ref[2 * k + 1];
+            xi[2 * (k + 1)] = xi_ref[2 * (k + 1)];
+            xi[2 * (k + 1) + 1] = xi_ref[2 * (k + 1) + 1];
+        }
+    }
     /* ---- initial point 2: one full Newton step of the QP without the polygon constraints
      *      (W = 0, lam = 0): the unconstrained LQ optimum.  For the unstable DCM the rollout is far
      *      from dual feasible (costates grow like alpha^N); this step makes the linear residuals
@@ -1353,8 +1393,9 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     if (status == 2) goto done;
     /* ---- active-set start (DESIGN.md 4 "Polish"): before any IPM iteration, the polish from the
      *      guess "facets the start point violates" (a warm start: also the facets whose previous
-     *      multiplier exceeds the floor), with up to ORC_GUESS_PASSES drop/add passes ---- */
-    if (prm->tol_polish > 0.0) {
+     *      multiplier exceeds the floor), with up to ORC_GUESS_PASSES drop/add passes (the cold
+     *      starts of the active-set kernel already ran theirs above) ---- */
+    if (prm->tol_polish > 0.0 && (warm || N > 2 * WV || prm->single_kernel)) {
         int* gm = (int*)calloc((size_t)N, sizeof(int));
         for (int k = 0; k < N; ++k) {
             const int ws = warm && k + warm->shift < N;

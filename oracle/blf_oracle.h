@@ -90,6 +90,15 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                       const double* b, const int32_t* nfacets, double* xi, double* vrp,
                       int32_t* iters);
 
+/* The fp32 active-set search of a cold start as the device's active-set kernel runs it
+ * (blf_oracle_as32.c): returns the float point (r [N][2], xi_{k+1} [N][2], as
+ * doubles) and the search's active set (guess bits per knot) the fp64 passes start from.
+ * sequential = 1: plain recursions instead of the kernel's scan tree (CPU baseline). */
+void orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_init,
+                     const double* omega, const double* xi_ref, const double* vrp_ref,
+                     const double* A, const double* b, const int32_t* nfacets, double* r_out,
+                     double* x_out, int32_t* guess);
+
 /* Warm start of a receding-horizon re-solve ("Warm start"): knot k
  * starts from knot src = min(k + shift, N - 1) of a previous solution: r_k = vrp[src],
  * s = max(b - A r, floor), lam = max(lambda[src], floor); the LQ start step is skipped. */

@@ -48,7 +48,7 @@ def run(args, tol_polish):
         stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         stamps(ctypes.cast(buf, ctypes.c_void_p), 1)
     as_stamps = getattr(L, "blf_debug_as_stamps", None) if hasattr(L, "blf_debug_as_stamps") else None
-    abuf = (ctypes.c_ulonglong * 16)()
+    abuf = (ctypes.c_ulonglong * 32)()
     if as_stamps is not None:
         as_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         as_stamps(ctypes.cast(abuf, ctypes.c_void_p), 1)
@@ -70,9 +70,36 @@ def run(args, tol_polish):
         print(f"active-set kernel, lane 0 cycles per QP: total {abuf[0] / q:.0f}, staging + knot loads "
               f"{abuf[1] / q:.0f}, LQ step {abuf[2] / q:.0f}, guess {abuf[3] / q:.0f}, outputs "
               f"{abuf[11] / q:.0f}, passes {abuf[10] / q:.2f} per QP")
-        print(f"per pass: setup + residuals {abuf[4] / npass:.0f}, Riccati sweep {abuf[5] / npass:.0f}, "
+        print(f"per fp64 pass: setup + residuals {abuf[4] / npass:.0f}, Riccati sweep {abuf[5] / npass:.0f}, "
               f"h {abuf[6] / npass:.0f}, solve {abuf[7] / npass:.0f}, certificate {abuf[8] / npass:.0f}, "
               f"vote + restore {abuf[9] / npass:.0f}")
+        if abuf[12]:
+            n32 = abuf[12]
+            print(f"fp32 passes: {abuf[13] / q:.0f} cycles per QP, {n32 / q:.2f} passes; fp64 passes "
+                  f"{abuf[14] / q:.0f} cycles per QP; kernel B total {abuf[15] / q:.0f}")
+            print(f"per fp32 pass: setup + residuals {abuf[16] / n32:.0f}, Riccati sweep {abuf[17] / n32:.0f}, "
+                  f"h {abuf[18] / n32:.0f}, solve {abuf[19] / n32:.0f}, certificate {abuf[20] / n32:.0f}, "
+                  f"vote + restore {abuf[21] / n32:.0f}")
+    for tl_name in ("blf_debug_as32_timeline", "blf_debug_as_timeline"):
+        tl = getattr(L, tl_name, None) if hasattr(L, tl_name) else None
+        if tl is None:
+            continue
+        import numpy as np
+        n = min(args.batch, 65536)
+        t = np.zeros((n, 4), dtype=np.uint64)
+        tl.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        tl(t.ctypes.data, n)
+        rt0, rt1 = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64)
+        base = rt0.min()
+        s0, s1 = (rt0 - base) / 100.0, (rt1 - base) / 100.0   # us
+        clk = (t[:, 3].astype(np.int64) - t[:, 2].astype(np.int64)) / ((rt1 - rt0) / 100.0) / 1e3   # GHz
+        life = s1 - s0
+        print(f"{tl_name} (last launch, {n} QPs): span {s1.max():.1f} us, wave lifetime mean {life.mean():.1f} "
+              f"min {life.min():.1f} max {life.max():.1f} us, shader clock median {np.median(clk):.2f} GHz")
+        edges = np.linspace(0, s1.max(), 21)
+        res = [int(((s0 <= e) & (s1 > e)).sum()) for e in edges[:-1]]
+        print("resident waves at 20 instants:", res)
+        print("start times quantiles (us):", np.round(np.quantile(s0, [0, .1, .25, .5, .75, .9, 1]), 1).tolist())
     if stamps is not None and not stamps(ctypes.cast(buf, ctypes.c_void_p), 0) and buf[0]:
         tot, fac, sol, its = buf[0], buf[1], buf[2], max(buf[3], 1)
         res, wph, pred, step = buf[4], buf[5], buf[6], buf[7]
