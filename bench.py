@@ -8,10 +8,11 @@ shard of independent problems — no data-path collective (scaling "weak"); the 
 solutions to rank 0 is timed separately and reported as gather_ms.
 
 Prints ONE JSON line on rank 0 (the driver's contract), with two extra objects:
-  roofline      HBM roofline of the dominant kernel (dcm_mpc_ipm), from the algorithmic bytes
-                per QP and the kernel's average duration measured with HIP
-                events on the launch stream; plus the counted-flop fp64 fraction and the VALU
-                issue fraction (the roof that binds this kernel).
+  roofline      HBM roofline of the dominant kernel (dcm_mpc_cold_kernel: the fp32 active-set
+                search and the fp64 certified passes), from the algorithmic bytes per QP
+                 and the kernel's average duration measured with HIP events
+                on the launch stream; plus the executed fp64 fraction and the VALU issue fraction
+                (the roof that binds this kernel).
   cpu_baseline  the CPU oracle (same algorithm, C, gcc -O3, one problem per thread)
                 on every CPU this process may use (affinity set capped by the cgroup CPU quota),
                 rank 0 only, on a bounded sample.
@@ -64,20 +65,25 @@ def profiled_traffic():
     return t["total_bytes_corrected"], path
 
 
-SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4
+SIMDS, CLOCK_HZ = 1024, 2.4e9
+F64_CYCLES, VALU32_CYCLES = 4, 2   # wave64 on a SIMD-32: fp64 at 16 lanes / cycle, 32-bit at 32
 
 
 def valu_issue(kernel_ms):
     """The roof that binds the QP kernel: VALU issue.  VALU wave-instructions per launch from the
-    committed SQ_INSTS_VALU pass, x 4 SIMD cycles each, over the chip's SIMD cycles in the kernel
-    time measured here (1024 SIMDs at the 2.4 GHz peak clock)."""
+    committed SQ_INSTS_VALU pass (fp64 FMA / MUL / ADD counted at 4 SIMD cycles, every other VALU
+    instruction at 2), over the chip's SIMD cycles in the kernel time measured here (1024 SIMDs at
+    the 2.4 GHz peak clock)."""
     s, path = profiled_summary()
     v = s.get("valu_issue") if s else None
     if not v:
         return None
     n = v["valu_insts_per_launch"]
-    return {"valu_insts_per_launch": n,
-            "frac": n * VALU_CYCLES / (SIMDS * CLOCK_HZ * kernel_ms * 1e-3),
+    f = v.get("fp64_insts_per_launch")
+    n64 = (f["fma"] + f["mul"] + f["add"]) if f else n
+    cycles = F64_CYCLES * n64 + VALU32_CYCLES * (n - n64)
+    return {"valu_insts_per_launch": n, "fp64_insts_per_launch": n64,
+            "frac": cycles / (SIMDS * CLOCK_HZ * kernel_ms * 1e-3),
             "source": path}
 
 
@@ -271,6 +277,8 @@ def main():
             "scaling": "weak" if args.global_batch is None else "strong",
             "vs_baseline": None,
             "dtype": "f64",
+            "arith": "fp32 active-set search, fp64 certified equality-constrained solve (the "
+                     "returned optimum is fp64)",
             "data": "synthetic (6-footstep plans, SeedSequence-keyed Philox per problem)",
             "config": {"workload": (f"configs[1]: batch={B} DCM-MPC QPs per GPU, horizon={N}, "
                                     f"M={M} facet slots, fp64, one wavefront per QP"
@@ -283,8 +291,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "dcm_mpc_as_kernel<2> (+ the IPM kernel's stage 2 on the QPs "
-                                   "it hands over, inside the same event pair)",
+                         "kernel": "dcm_mpc_cold_kernel<2> (fp32 active-set search + fp64 "
+                                   "certified passes; + the IPM kernel's stage 2 on the QPs it hands "
+                                   "over, inside the same event pair)",
                          "kernel_ms": kernel_ms,
                          "bytes_per_qp": bpq,
                          # what binds this kernel is neither HBM nor MFMA: VALU issue and the

@@ -28,21 +28,23 @@ def counters(path):
 
 SIMDS = 1024          # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9      # peak engine clock
-VALU_CYCLES = 4       # a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles
 
 
 def valu_issue(d, avg_ns):
     """The roof that binds the QP kernel: VALU issue.  SQ_INSTS_VALU counts wave-instructions per
-    dispatch; each takes 4 SIMD cycles; the chip offers SIMDS x clock x time SIMD cycles."""
+    dispatch; an fp64 FMA / MUL / ADD takes 4 SIMD cycles (16 lanes per cycle), every other VALU
+    instruction 2 (SIMD-32); the chip offers SIMDS x clock x time SIMD cycles."""
     n = d.get("SQ_INSTS_VALU", {}).get("mean_per_dispatch")
     if n is None:
         return None
-    out = {"valu_insts_per_launch": n,
-           "valu_cycles_per_launch": n * VALU_CYCLES,
-           "chip_simd_cycles_per_launch": SIMDS * CLOCK_HZ * avg_ns * 1e-9,
-           "frac": n * VALU_CYCLES / (SIMDS * CLOCK_HZ * avg_ns * 1e-9)}
     f64 = [d.get(c, {}).get("mean_per_dispatch") for c in
            ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")]
+    n64 = sum(f64) if None not in f64 else n
+    cycles = 4 * n64 + 2 * (n - n64)
+    out = {"valu_insts_per_launch": n,
+           "valu_cycles_per_launch": cycles,
+           "chip_simd_cycles_per_launch": SIMDS * CLOCK_HZ * avg_ns * 1e-9,
+           "frac": cycles / (SIMDS * CLOCK_HZ * avg_ns * 1e-9)}
     if None not in f64:
         out["fp64_insts_per_launch"] = {"fma": f64[0], "mul": f64[1], "add": f64[2]}
     return out
