@@ -90,6 +90,19 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                       const double* b, const int32_t* nfacets, double* xi, double* vrp,
                       int32_t* iters);
 
+/* Batched, multi-threaded drivers (blf_oracle_batch.c; bench.py CPU baselines): the per-item
+ * entry points above over `count` items on `threads` POSIX threads. */
+void orc_hull2d_hrep_batch(int64_t count, int P, int M, const double* pts, const int32_t* npts,
+                           double* A, double* b, int32_t* nf, int threads);
+void orc_dcm_phase_expand_batch(int64_t B, int P, int M, const int32_t* nphases, const double* begin,
+                                const double* end, const double* pA, const double* pb,
+                                const int32_t* pnf, const double* pref, int64_t start, double dt,
+                                int N, double* A, double* b, int32_t* nfacets, double* xi_ref,
+                                double* vrp_ref, int threads);
+void orc_quintic_batch(int64_t S, int K1, int dim, int Q, const double* knots_t,
+                       const double* knots_pva, const double* tq, double* coeffs, double* pva,
+                       int32_t* idx, int threads);
+
 /* The fp32 active-set search of a cold start as the device's active-set kernel runs it
  * (blf_oracle_as32.c): returns the float point (r [N][2], xi_{k+1} [N][2], as
  * doubles) and the search's active set (guess bits per knot) the fp64 passes start from.

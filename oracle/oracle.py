@@ -66,6 +66,14 @@ def lib():
         L.orc_dcm_phase_expand.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp,
                                            _dp, _dp, _ip, _dp, ctypes.c_int64, ctypes.c_double,
                                            ctypes.c_int, _dp, _dp, _ip, _dp, _dp]
+        L.orc_hull2d_hrep_batch.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _dp, _ip,
+                                            _dp, _dp, _ip, ctypes.c_int]
+        L.orc_dcm_phase_expand_batch.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _ip,
+                                                 _dp, _dp, _dp, _dp, _ip, _dp, ctypes.c_int64,
+                                                 ctypes.c_double, ctypes.c_int, _dp, _dp, _ip, _dp,
+                                                 _dp, ctypes.c_int]
+        L.orc_quintic_batch.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        _dp, _dp, _dp, _dp, _dp, _ip, ctypes.c_int]
         L.orc_wave_tree_sum.restype = ctypes.c_double
         L.orc_wave_tree_sum.argtypes = [_dp, ctypes.c_int]
         L.orc_contact_eval.argtypes = [_dp] * 8
@@ -260,6 +268,47 @@ def dcm_phase_expand(table, start, dt, horizon):
             int(start), float(dt), N, _d(out["A"][q]), _d(out["b"][q]), _i(out["nfacets"][q]),
             _d(out["xi_ref"][q]), _d(out["vrp_ref"][q]))
     return out
+
+
+def hull2d_hrep_batch(pts, npts, max_facets=8, threads=1):
+    """orc_hull2d_hrep over pts [count, P, 2] (npts [count] valid points each), threaded."""
+    pts, npts = _f64(pts), np.ascontiguousarray(npts, dtype=np.int32)
+    n, P = pts.shape[0], pts.shape[1]
+    A = np.zeros((n, max_facets, 2))
+    b = np.zeros((n, max_facets))
+    nf = np.zeros(n, dtype=np.int32)
+    lib().orc_hull2d_hrep_batch(n, P, max_facets, _d(pts), _i(npts), _d(A), _d(b), _i(nf), int(threads))
+    return A, b, nf
+
+
+def dcm_phase_expand_batch(table, start, dt, horizon, threads=1):
+    """dcm_phase_expand with the C batch driver (threaded)."""
+    B, P = table["phase_begin"].shape
+    M = table["phase_b"].shape[2]
+    N = horizon
+    out = dict(A=np.zeros((B, N, M, 2)), b=np.zeros((B, N, M)),
+               nfacets=np.zeros((B, N), dtype=np.int32), xi_ref=np.zeros((B, N + 1, 2)),
+               vrp_ref=np.zeros((B, N, 2)))
+    c = lambda k, dt_=np.float64: np.ascontiguousarray(table[k], dtype=dt_)
+    lib().orc_dcm_phase_expand_batch(
+        B, P, M, _i(c("nphases", np.int32)), _d(c("phase_begin")), _d(c("phase_end")),
+        _d(c("phase_A")), _d(c("phase_b")), _i(c("phase_nf", np.int32)), _d(c("phase_ref")),
+        int(start), float(dt), N, _d(out["A"]), _d(out["b"]), _i(out["nfacets"]), _d(out["xi_ref"]),
+        _d(out["vrp_ref"]), int(threads))
+    return out
+
+
+def quintic_batch(knots_t, knots_pva, tq, threads=1):
+    """Fit and evaluate S quintic splines (knots_t [S, K1], knots_pva [S, K1, 3, D], tq [S, Q])."""
+    knots_t, knots_pva, tq = _f64(knots_t), _f64(knots_pva), _f64(tq)
+    S, K1 = knots_t.shape
+    D, Q = knots_pva.shape[3], tq.shape[1]
+    coeffs = np.zeros((S, K1 - 1, D, 6))
+    pva = np.zeros((S, Q, 3, D))
+    idx = np.zeros((S, Q), dtype=np.int32)
+    lib().orc_quintic_batch(S, K1, D, Q, _d(knots_t), _d(knots_pva), _d(tq), _d(coeffs), _d(pva),
+                            _i(idx), int(threads))
+    return coeffs, pva, idx
 
 
 def wave_tree_sum(c):

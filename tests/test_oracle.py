@@ -274,3 +274,31 @@ def test_dcm_mpc_active_set_start_solves_most_problems_without_iterations():
     for i in range(0, 256, 32):
         xd, rd = certify(prob, i, xi[i], vrp[i])
         assert np.abs(rd - vrp[i]).max() < 1e-12 and np.abs(xd - xi[i]).max() < 1e-12
+
+
+def test_oracle_batch_drivers_match_single_item_calls():
+    """The threaded C batch drivers (bench.py CPU baselines) return exactly what the per-item
+    entry points return."""
+    import numpy as np
+    from blf import problems as P
+    import closed_loop as CL
+    prob = P.make_batch(16, horizon=40, n_footsteps=4, seed=9)
+    B, Pn, C = prob["phase_corners"].shape[:3]
+    A, b, nf = O.hull2d_hrep_batch(prob["phase_corners"].reshape(B * Pn, C, 2),
+                                   prob["phase_ncorners"].reshape(B * Pn), 8, threads=3)
+    tab = CL.phase_table(prob)
+    np.testing.assert_array_equal(A.reshape(B, Pn, 8, 2), tab["phase_A"])
+    np.testing.assert_array_equal(b.reshape(B, Pn, 8), tab["phase_b"])
+    np.testing.assert_array_equal(nf.reshape(B, Pn), tab["phase_nf"])
+    w1 = O.dcm_phase_expand(tab, 3, prob["dt"], 40)
+    w2 = O.dcm_phase_expand_batch(tab, 3, prob["dt"], 40, threads=3)
+    for k in w1:
+        np.testing.assert_array_equal(w1[k], w2[k])
+    kt, kp, tq = P.swing_splines(prob, queries=8)
+    co, pva, idx = O.quintic_batch(kt, kp, tq, threads=3)
+    for s in (0, kt.shape[0] - 1):
+        c1 = O.quintic_fit(kt[s], kp[s])
+        p1, i1 = O.quintic_eval(kt[s], c1, tq[s])
+        np.testing.assert_array_equal(co[s], c1)
+        np.testing.assert_array_equal(pva[s], p1)
+        np.testing.assert_array_equal(idx[s], i1)
