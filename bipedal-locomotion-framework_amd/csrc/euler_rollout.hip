@@ -162,7 +162,7 @@ __device__ __forceinline__ void roll_store_full(double* __restrict__ xi_out, con
 #pragma unroll
     for (int u = 0; u < KC; ++u) {
         const int j = u * 64 + lane, r = j / KC, c2 = j % KC;
-        *reinterpret_cast<double2*>(xi_out + (p0 + r) * 2 * (N + 1) + 2 * (kb + 1) + 2 * c2) = v[u];
+        st_stream(reinterpret_cast<double2*>(xi_out + (p0 + r) * 2 * (N + 1) + 2 * (kb + 1) + 2 * c2), v[u]);
     }
 }
 

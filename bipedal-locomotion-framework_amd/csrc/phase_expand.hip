@@ -16,6 +16,7 @@
 // 16-B A rows, 8-B offsets, facet counts and 16-B references.  HBM-bound: the bytes written are
 // the per-knot arrays of the QP.
 #include "blf_internal.h"
+#include "slab.h"
 
 namespace blf {
 namespace {
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
     for (int j = tid; j < nm; j += kExpandBlock) {
         const int k = j / M, i = j - k * M;
         const int ph = sPh[k];
-        oA[j] = ph >= 0 ? sA[ph * M + i] : make_double2(0.0, 0.0);
+        st_stream(oA + j, ph >= 0 ? sA[ph * M + i] : make_double2(0.0, 0.0));
         oB[j] = ph >= 0 ? sB[ph * M + i] : 0.0;
     }
     double2* oX = reinterpret_cast<double2*>(xi_ref) + q * (N + 1);
@@ -96,9 +97,9 @@ __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
     for (int k = tid; k <= N; k += kExpandBlock) {
         const int ph = sPh[k];
         const double2 ref = ph >= 0 ? sRef[ph] : make_double2(0.0, 0.0);
-        oX[k] = ref;
+        st_stream(oX + k, ref);
         if (k < N) {
-            oR[k] = ref;
+            st_stream(oR + k, ref);
             oN[k] = ph >= 0 ? sNf[ph] : -1;
         }
     }

@@ -326,6 +326,7 @@ __global__ __launch_bounds__(256) void quintic_fit_kernel(const double* __restri
 // written with coalesced 16-B stores (slab.h)
 constexpr int kEvalBlock = 256;
 
+template <bool VEC>
 __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* __restrict__ kt,
                                                                   const double* __restrict__ coeffs,
                                                                   int32_t K1, int32_t D, int64_t S,
@@ -340,7 +341,9 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
     const int64_t gid = g0 + threadIdx.x;
     const int rows = (int)((S * Q - g0) < kEvalBlock ? (S * Q - g0) : kEvalBlock);
     if (gid < S * Q) {
-        const int64_t sp = gid / Q;
+        // 32-bit division when the launch fits (every bench / test shape): the 64-bit one is a
+        // long VALU sequence per lane
+        const int64_t sp = (S * Q < 0x7fffffffLL) ? (int64_t)((uint32_t)gid / (uint32_t)Q) : gid / Q;
         const double* t = kt + sp * K1;
         const double tt = tq[gid];
         // last j with t_j <= t: a forward pass keeps the knot loads independent of each other
@@ -352,8 +355,17 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
         const double tau = tt - t[seg];
         double* o = s_out + threadIdx.x * SW;
         for (int d = 0; d < D; ++d) {
-            const double* c = coeffs + ((sp * K + seg) * D + d) * 6;
-            const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5];
+            // the segment's 6 coefficients are 48 contiguous bytes: three 16-B loads when the
+            // array is 16-B aligned (VEC), six 8-B loads otherwise
+            const double* cp = coeffs + ((sp * K + seg) * D + d) * 6;
+            double c0, c1, c2, c3, c4, c5;
+            if (VEC) {
+                const double2* c = reinterpret_cast<const double2*>(cp);
+                const double2 ca = c[0], cb = c[1], cc = c[2];
+                c0 = ca.x; c1 = ca.y; c2 = cb.x; c3 = cb.y; c4 = cc.x; c5 = cc.y;
+            } else {
+                c0 = cp[0]; c1 = cp[1]; c2 = cp[2]; c3 = cp[3]; c4 = cp[4]; c5 = cp[5];
+            }
             const double p = c0 + tau * (c1 + tau * (c2 + tau * (c3 + tau * (c4 + tau * c5))));
             const double v = c1 + tau * (2.0 * c2 + tau * (3.0 * c3 + tau * (4.0 * c4 + tau * (5.0 * c5))));
             const double a = 2.0 * c2 + tau * (6.0 * c3 + tau * (12.0 * c4 + tau * (20.0 * c5)));
@@ -412,8 +424,9 @@ blf_status launch_quintic_eval(const double* kt, const double* coeffs, int32_t K
 {
     const int64_t n = S * Q;
     if (n == 0) return BLF_OK;
-    hipLaunchKernelGGL(quintic_eval_kernel, dim3((unsigned)ceil_div(n, kEvalBlock)),
-                       dim3(kEvalBlock), 0, s, kt, coeffs, K1, D, S, tq, Q, pva, idx);
+    auto kern = (((uintptr_t)coeffs & 15) == 0) ? quintic_eval_kernel<true> : quintic_eval_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(n, kEvalBlock)), dim3(kEvalBlock), 0, s, kt,
+                       coeffs, K1, D, S, tq, Q, pva, idx);
     return check_hip(hipGetLastError(), "quintic_eval_kernel launch");
 }
 
