@@ -5,10 +5,11 @@
 //    ForwardEuler.tpp:18-49, src/System/src/LinearTimeInvariantSystem.cpp:71).  The step
 //    schedule (count and the stale-time last step) is computed once on the host (blf_capi.hip)
 //    and is identical for every system of the batch.  One lane per system.
-//  * dcm_rollout_kernel: the DCM instance, one reference Euler step per knot with
-//    A = omega_k I, B = -omega_k I.  One lane per problem; each workgroup stages its 64 problems'
-//    omega / vrp rows through LDS in chunks of knots so that the HBM reads and the xi writes are
-//    coalesced (problem-major layout).
+//  * dcm_rollout_rows_kernel / dcm_rollout_kernel: the DCM instance, one reference Euler step
+//    per knot with A = omega_k I, B = -omega_k I.  Horizons up to 160: a wave takes 8 problems'
+//    whole rows (contiguous in HBM) through LDS, two lanes per problem; longer horizons: one lane
+//    per problem, 64 problems' rows staged in chunks of knots (problem-major layout, DESIGN.md
+//    section 3).
 // Built with -ffp-contract=off: bit-identical to oracle/blf_oracle.c.
 #include "blf_internal.h"
 #include "slab.h"
@@ -224,6 +225,109 @@ __global__ __launch_bounds__(64) void dcm_rollout_kernel(const double* __restric
     }
 }
 
+// Whole rows, PPW problems per wave (horizons up to kRollRowsMaxN).  The tile's omega, vrp and xi
+// rows are contiguous regions of HBM, so the wave reads and writes them as plain 16-B streams
+// with whole 128-B lines; chunks of knots across 64 problems (the kernel above) cut every row
+// at chunk edges, which re-fetches the lines they split and writes partial lines (1.19x the
+// algorithmic bytes fetched).  Two lanes per problem, one per component of xi (the components
+// share omega and nothing else).  LDS: omega rows, and vrp rows shifted by one knot with xi0 in
+// front, overwritten in place by xi_{k+1} (r_k is read just before xi_{k+1} replaces it), so the
+// xi row leaves exactly as it is laid out in xi_out.
+constexpr int kRollRowsMaxN = 160;
+
+template <int PPW>
+__global__ __launch_bounds__(64) void dcm_rollout_rows_kernel(const double* __restrict__ xi0,
+                                                              const double* __restrict__ omega,
+                                                              const double* __restrict__ vrp,
+                                                              int32_t N, double dt,
+                                                              double* __restrict__ xi_out,
+                                                              int64_t batch)
+{
+    extern __shared__ double s_rows[];
+    const int SWo = odd_stride(N), SWx = odd_stride(2 * (N + 1));
+    double* s_om = s_rows;              // [PPW][SWo]
+    double* s_x = s_rows + PPW * SWo;   // [PPW][SWx]: xi0, r_0 .. r_{N-1} -> xi0 .. xi_N
+    const int lane = threadIdx.x;
+    const int64_t p0 = (int64_t)blockIdx.x * PPW;
+    const int np = (int)((batch - p0) < PPW ? (batch - p0) : PPW);
+    const double* go = omega + p0 * N;
+    const double* gr = vrp + p0 * 2 * N;
+    const int no = np * N / 2, nr = np * N;   // 16-B pairs of the tile's omega / vrp regions
+    if (lane < 2 * np) s_x[(lane >> 1) * SWx + (lane & 1)] = xi0[2 * p0 + lane];
+    constexpr int UO = PPW, UR = 2 * PPW;   // N <= 128
+    if (((N & 1) | (((uintptr_t)go | (uintptr_t)gr) & 15)) == 0 && no <= UO * 64 && nr <= UR * 64) {
+        // both regions' loads in flight before the first LDS write
+        double2 vo[UO], vr[UR];
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int j = u * 64 + lane;
+            if (j < no) vo[u] = reinterpret_cast<const double2*>(go)[j];
+        }
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int j = u * 64 + lane;
+            if (j < nr) vr[u] = reinterpret_cast<const double2*>(gr)[j];
+        }
+        const SlabIdx io(N), ir(2 * N);
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int e = 2 * (u * 64 + lane);
+            if (e < 2 * no) {   // N even: a pair never straddles two rows
+                const int r = io.row(e);
+                s_om[r * SWo + e - r * N] = vo[u].x;
+                s_om[r * SWo + e - r * N + 1] = vo[u].y;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int e = 2 * (u * 64 + lane);
+            if (e < 2 * nr) {
+                const int r = ir.row(e);
+                s_x[2 + r * SWx + e - r * 2 * N] = vr[u].x;
+                s_x[2 + r * SWx + e - r * 2 * N + 1] = vr[u].y;
+            }
+        }
+    } else {
+        slab_load<64, 8>(s_om, SWo, go, N, np, N);
+        slab_load<64, 16>(s_x + 2, SWx, gr, 2 * N, np, 2 * N);
+    }
+    __syncthreads();
+    if (lane < 2 * np) {
+        const double* om = s_om + (lane >> 1) * SWo;
+        double* xr = s_x + (lane >> 1) * SWx + (lane & 1);
+        double x = xr[0];
+        int k = 0;
+        for (; k + 4 <= N; k += 4) {   // the LDS reads of four knots ahead of their recurrence
+            double w[4], r[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                w[g] = om[k + g];
+                r[g] = xr[2 * (k + g + 1)];
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const double dx = w[g] * x + (-w[g]) * r[g];
+                x = x + dx * dt;
+                xr[2 * (k + g + 1)] = x;
+            }
+        }
+        for (; k < N; ++k) {
+            const double w = om[k];
+            const double dx = w * x + (-w) * xr[2 * (k + 1)];
+            x = x + dx * dt;
+            xr[2 * (k + 1)] = x;
+        }
+    }
+    __syncthreads();
+    slab_store<64, 16>(xi_out + p0 * 2 * (N + 1), 2 * (N + 1), s_x, SWx, np, 2 * (N + 1));
+}
+
+#ifndef BLF_ROLL_PPW
+#define BLF_ROLL_PPW 8
+#endif
+constexpr int kRollPPW = BLF_ROLL_PPW;
+inline int odd_stride_host(int w) { return w | 1; }
+
 }  // namespace
 
 blf_status launch_lti_euler(int n, int m, const double* A, const double* Bm, int shared,
@@ -252,6 +356,12 @@ blf_status launch_dcm_rollout(const double* xi0, const double* omega, const doub
                               hipStream_t s)
 {
     if (batch == 0) return BLF_OK;
+    if (N <= kRollRowsMaxN) {
+        const size_t lds = (size_t)kRollPPW * (odd_stride_host(N) + odd_stride_host(2 * (N + 1))) * 8;
+        hipLaunchKernelGGL(dcm_rollout_rows_kernel<kRollPPW>, dim3((unsigned)ceil_div(batch, kRollPPW)),
+                           dim3(64), lds, s, xi0, omega, vrp, N, dt, xi_out, batch);
+        return check_hip(hipGetLastError(), "dcm_rollout_rows_kernel launch");
+    }
     const int64_t blocks = ceil_div(batch, 64);
     const bool vec = (N % 2 == 0) && ((((uintptr_t)omega | (uintptr_t)vrp | (uintptr_t)xi_out) & 15) == 0);
     if (vec)
