@@ -23,7 +23,7 @@ EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_quintic_fit", "blf_quintic_eval",
             "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_solve_warm",
-            "blf_dcm_phase_expand",
+            "blf_dcm_phase_expand", "blf_dcm_mpc_solve_phased",
             "blf_dcm_mpc_flops_per_iter",
             "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
             "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate",
@@ -91,6 +91,11 @@ class PhaseTable(ctypes.Structure):
                 ("end", _vp), ("A", _vp), ("b", _vp), ("nfacets", _vp), ("ref", _vp)]
 
 
+class DcmMpcWindow(ctypes.Structure):
+    _fields_ = [("omega", _vp), ("xi_ref", _vp), ("vrp_ref", _vp), ("A", _vp), ("b", _vp),
+                ("nfacets", _vp)]
+
+
 class DcmMpcWarmStart(ctypes.Structure):
     _fields_ = [("vrp", _vp), ("lambda_", _vp), ("shift", _i32), ("reserved", _i32),
                 ("floor", _f64)]
@@ -138,6 +143,11 @@ def lib():
                                              ctypes.POINTER(DcmMpcSolution), _vp, _vp]
         L.blf_dcm_phase_expand.argtypes = [_vp, ctypes.POINTER(PhaseTable), _i64, _f64, _i32,
                                            _i64, _vp, _vp, _vp, _vp, _vp, _vp]
+        L.blf_dcm_mpc_solve_phased.argtypes = [_vp, ctypes.POINTER(DcmMpcParams),
+                                               ctypes.POINTER(PhaseTable), _i64, _vp, _vp, _i64,
+                                               ctypes.POINTER(DcmMpcWarmStart), _i64,
+                                               ctypes.POINTER(DcmMpcWindow),
+                                               ctypes.POINTER(DcmMpcSolution), _vp, _vp]
         L.blf_dcm_mpc_flops_per_iter.argtypes = [_i32, _i64]
         L.blf_contact_model_eval.argtypes = [_vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                              _vp, _vp]
@@ -441,6 +451,82 @@ class Handle:
             _ptr(out["nfacets"], torch.int32, (B, N), "nfacets"),
             _ptr(out["xi_ref"], torch.float64, (B, N + 1, 2), "xi_ref"),
             _ptr(out["vrp_ref"], torch.float64, (B, N, 2), "vrp_ref"), _stream(stream)))
+        return out
+
+    def _phase_table_struct(self, table):
+        torch = _torch()
+        B, P = table["phase_begin"].shape
+        M = table["phase_b"].shape[2]
+        return PhaseTable(P, M, _ptr(table["nphases"], torch.int32, (B,), "nphases"),
+                          _ptr(table["phase_begin"], torch.float64, (B, P), "phase_begin"),
+                          _ptr(table["phase_end"], torch.float64, (B, P), "phase_end"),
+                          _ptr(table["phase_A"], torch.float64, (B, P, M, 2), "phase_A"),
+                          _ptr(table["phase_b"], torch.float64, (B, P, M), "phase_b"),
+                          _ptr(table["phase_nf"], torch.int32, (B, P), "phase_nf"),
+                          _ptr(table["phase_ref"], torch.float64, (B, P, 2), "phase_ref"))
+
+    def dcm_mpc_solve_phased(self, table, start, xi_init, omega, params=None, warm=None,
+                             out=None, window=None, lambda_out=False, stream=None):
+        """blf_dcm_mpc_solve_phased: dcm_phase_expand(table, start, params.dt, N) followed by
+        dcm_mpc_solve on that window, fused (same results bit for bit, N <= 128).
+        omega [B, N] or a row-strided view [B, N] of a longer [B, L] array (stride(1) == 1).
+        window: scratch dict (omega, xi_ref, vrp_ref, A, b, nfacets) of the window's shapes, kept
+        in out["window"] (allocated once when absent)."""
+        torch = _torch()
+        B, N = omega.shape
+        M = table["phase_b"].shape[2]
+        p = params if params is not None else default_params(N, max_facets=M)
+        if p.horizon != N or p.max_facets != M:
+            raise ValueError("params.horizon / max_facets do not match omega / the phase table")
+        if omega.device.type != "cuda" or omega.dtype != torch.float64 or omega.stride(1) != 1:
+            raise ValueError("omega must be a float64 device tensor with unit column stride")
+        ostride = omega.stride(0) if B > 1 else N
+        dev = omega.device
+        if out is None:
+            out = dict(xi=torch.empty((B, N + 1, 2), dtype=torch.float64, device=dev),
+                       vrp=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+                       status=torch.empty((B,), dtype=torch.int32, device=dev),
+                       iters=torch.empty((B,), dtype=torch.int32, device=dev),
+                       polished=torch.empty((B,), dtype=torch.int32, device=dev))
+        if window is None:
+            window = out.get("window")
+        if window is None:
+            window = dict(omega=torch.empty((B, N), dtype=torch.float64, device=dev),
+                          xi_ref=torch.empty((B, N + 1, 2), dtype=torch.float64, device=dev),
+                          vrp_ref=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+                          A=torch.empty((B, N, M, 2), dtype=torch.float64, device=dev),
+                          b=torch.empty((B, N, M), dtype=torch.float64, device=dev),
+                          nfacets=torch.empty((B, N), dtype=torch.int32, device=dev))
+            out["window"] = window
+        win = DcmMpcWindow(_ptr(window["omega"], torch.float64, (B, N), "window omega"),
+                           _ptr(window["xi_ref"], torch.float64, (B, N + 1, 2), "window xi_ref"),
+                           _ptr(window["vrp_ref"], torch.float64, (B, N, 2), "window vrp_ref"),
+                           _ptr(window["A"], torch.float64, (B, N, M, 2), "window A"),
+                           _ptr(window["b"], torch.float64, (B, N, M), "window b"),
+                           _ptr(window["nfacets"], torch.int32, (B, N), "window nfacets"))
+        tb = self._phase_table_struct(table)
+        so = DcmMpcSolution(
+            _ptr(out["xi"], torch.float64, (B, N + 1, 2), "xi"),
+            _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
+            _ptr(out["status"], torch.int32, (B,), "status"),
+            _ptr(out["iters"], torch.int32, (B,), "iters"),
+            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
+        ws = None
+        if warm is not None:
+            ws = DcmMpcWarmStart(_ptr(warm["vrp"], torch.float64, (B, N, 2), "warm vrp"),
+                                 _ptr(warm["lam"], torch.float64, (B, N, M), "warm lam"),
+                                 int(warm.get("shift", 1)), 0, float(warm.get("floor", 1e-2)))
+        lam_ptr = None
+        if lambda_out:
+            if "lam" not in out:
+                out["lam"] = torch.empty((B, N, M), dtype=torch.float64, device=dev)
+            lam_ptr = _ptr(out["lam"], torch.float64, (B, N, M), "lam")
+        self._keep = (tb, so, ws, win)
+        _check(lib().blf_dcm_mpc_solve_phased(
+            self._h, ctypes.byref(p), ctypes.byref(tb), int(start),
+            _ptr(xi_init, torch.float64, (B, 2), "xi_init"), _vp(omega.data_ptr()), ostride,
+            ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(win), ctypes.byref(so),
+            lam_ptr, _stream(stream)))
         return out
 
     # --- C3 pipeline: corner sets -> polygons (device hull) -> QP arrays ---

@@ -268,6 +268,61 @@ blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* 
     return launch_dcm_mpc(params, problem, warm, batch, solution, lambda_out, (hipStream_t)stream);
 }
 
+blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                    const blf_phase_table* ph, int64_t start_knot,
+                                    const double* xi_init, const double* omega,
+                                    int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
+                                    int64_t batch, const blf_dcm_mpc_window* win,
+                                    const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                    void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve_phased: null handle");
+    BLF_REQUIRE(params && ph && win && solution, "blf_dcm_mpc_solve_phased: null argument");
+    BLF_REQUIRE(ph->max_phases >= 1, "blf_dcm_mpc_solve_phased: max_phases %d < 1", ph->max_phases);
+    BLF_REQUIRE(ph->max_facets == params->max_facets,
+                "blf_dcm_mpc_solve_phased: phase table max_facets %d != params max_facets %d",
+                ph->max_facets, params->max_facets);
+    BLF_REQUIRE(start_knot >= 0, "blf_dcm_mpc_solve_phased: start_knot < 0");
+    BLF_REQUIRE(omega_stride >= params->horizon, "blf_dcm_mpc_solve_phased: omega_stride %lld < horizon %d",
+                (long long)omega_stride, params->horizon);
+    BLF_REQUIRE(batch == 0 || (ph->nphases && ph->begin && ph->end && ph->A && ph->b && ph->nfacets &&
+                               ph->ref && win->omega && win->xi_ref && win->vrp_ref && win->A &&
+                               win->b && win->nfacets),
+                "blf_dcm_mpc_solve_phased: null buffer");
+    // the QP arguments as blf_dcm_mpc_solve_warm checks them (the window scratch stands in for the
+    // per-knot arrays, which this call does not read)
+    const blf_dcm_mpc_problem pb{xi_init, omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
+    if (batch > 0) {
+        BLF_REQUIRE(params->horizon >= 1 && params->horizon <= 128,
+                    "blf_dcm_mpc_solve_phased: horizon %d outside [1, 128]", params->horizon);
+        BLF_REQUIRE(params->tol_polish > 0, "blf_dcm_mpc_solve_phased: tol_polish must be > 0");
+    }
+    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacets,
+                "blf_dcm_mpc_solve_phased: max_facets %d outside [1, %d]", params->max_facets, kMaxFacets);
+    BLF_REQUIRE(params->max_iter >= 0, "blf_dcm_mpc_solve_phased: max_iter < 0");
+    BLF_REQUIRE(params->reserved == 0, "blf_dcm_mpc_solve_phased: reserved must be 0");
+    BLF_REQUIRE(params->dt > 0 && std::isfinite(params->dt), "blf_dcm_mpc_solve_phased: dt must be finite and > 0");
+    BLF_REQUIRE(params->w_vrp[0] > 0 && params->w_vrp[1] > 0 && params->w_xi[0] >= 0 &&
+                    params->w_xi[1] >= 0 && params->w_terminal[0] >= 0 && params->w_terminal[1] >= 0,
+                "blf_dcm_mpc_solve_phased: weights must be R > 0, Q >= 0, P >= 0");
+    BLF_REQUIRE(batch >= 0, "blf_dcm_mpc_solve_phased: negative batch");
+    BLF_REQUIRE(batch == 0 || (pb.xi_init && pb.omega && solution->xi && solution->vrp &&
+                               solution->status && solution->iters),
+                "blf_dcm_mpc_solve_phased: null buffer");
+    if (warm) {
+        BLF_REQUIRE(batch == 0 || (warm->vrp && warm->lambda),
+                    "blf_dcm_mpc_solve_phased: null warm-start buffer");
+        BLF_REQUIRE(warm->shift >= 0, "blf_dcm_mpc_solve_phased: shift %d < 0", warm->shift);
+        BLF_REQUIRE(warm->reserved == 0, "blf_dcm_mpc_solve_phased: reserved must be 0");
+        BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
+                    "blf_dcm_mpc_solve_phased: floor must be finite and > 0");
+        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out,
+                    "blf_dcm_mpc_solve_phased: warm-start buffers must not alias the outputs");
+    }
+    return launch_dcm_mpc_phased(params, ph, start_knot, xi_init, omega, omega_stride, warm, batch,
+                                 win, solution, lambda_out, (hipStream_t)stream);
+}
+
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
                              const blf_dcm_mpc_problem* problem, int64_t batch,
                              const blf_dcm_mpc_solution* solution, void* stream)

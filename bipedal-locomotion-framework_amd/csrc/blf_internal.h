@@ -52,6 +52,11 @@ blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* 
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
                           const blf_dcm_mpc_warm_start* warm, int64_t batch,
                           const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);
+blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_table* ph,
+                                 int64_t start_knot, const double* xi_init, const double* omega,
+                                 int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
+                                 int64_t batch, const blf_dcm_mpc_window* win,
+                                 const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);
 blf_status launch_contact_eval(const double* prm, int shared, const double* twist,
                                const double* pose, const double* null_pose, int64_t batch,
                                double* wrench, double* autonomous, double* control,

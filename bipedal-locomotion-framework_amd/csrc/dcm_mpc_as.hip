@@ -751,6 +751,133 @@ __device__ __forceinline__ void stage_rows(const double* Ain, const double* bin,
     }
 }
 
+// ---- the phase-indexed input (blf_dcm_mpc_solve_phased) ----
+// The window is expanded from the plan's phase table straight into the kernel's LDS, as
+// phase_expand_kernel would write it to HBM: the same knot -> phase rule (phase_of), the phase's
+// rows verbatim, nfacets = -1 and zero rows / references outside every phase.  LDS after the
+// facet rows: the problem's phase begin / end times [2][P] doubles, the knot phases [N+1] int32.
+__host__ __device__ inline size_t ph_lds_bytes(int P, int N)
+{
+    return sizeof(double) * 2 * (size_t)P + sizeof(int32_t) * (size_t)(N + 1);
+}
+
+__device__ __forceinline__ void ph_stage_phases(const PhaseSrc& ps, int64_t p, int N, double dt, int lane,
+                                                double* sBE, int32_t* sPh)
+{
+    int np = ps.nphases[p];
+    np = np < 0 ? 0 : (np > ps.P ? ps.P : np);
+    for (int j = lane; j < np; j += kWave) {
+        sBE[j] = ps.begin[p * ps.P + j];
+        sBE[ps.P + j] = ps.end[p * ps.P + j];
+    }
+    __syncthreads();
+    for (int k = lane; k <= N; k += kWave)
+        sPh[k] = phase_of(sBE, sBE + ps.P, np, (double)(ps.start + k) * dt);
+    __syncthreads();
+}
+
+// stage_rows from the phase table: slot (k, i) = row i of knot k's phase (zeros outside every
+// phase).  The table rows are a few KB per problem, read through the caches.
+template <int KPL, int U>
+__device__ __forceinline__ void stage_rows_ph(const PhaseSrc& ps, const int32_t* sPh, int64_t p, int N, int M,
+                                              int S, int NH, int lane, double* A2v, double* Bv)
+{
+    const int nA = N * M;
+    const double2* As = reinterpret_cast<const double2*>(ps.A) + p * ps.P * M;
+    const double* bs = ps.b + p * ps.P * M;
+    const bool pow2 = (M & (M - 1)) == 0;
+    const int sh = __builtin_ctz(M);
+    double2 va[U];
+    double vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
+        const int t = min(u * kWave + lane, nA - 1);
+        const int k = pow2 ? t >> sh : t / M, i = t - k * M;
+        const int ph = sPh[k];
+        const int src = (ph < 0 ? 0 : ph) * M + i;
+        const double2 a = As[src];
+        const double b = bs[src];
+        va[u] = ph < 0 ? make_double2(0.0, 0.0) : a;
+        vb[u] = ph < 0 ? 0.0 : b;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = u * kWave + lane;
+        if (t < nA) {
+            const int k = pow2 ? t >> sh : t / M, i = t - k * M;
+            const int o = i * S + (k % KPL) * NH + k / KPL;
+            A2v[2 * o] = va[u].x;
+            A2v[2 * o + 1] = va[u].y;
+            Bv[o] = vb[u];
+        }
+    }
+}
+
+// A knot's own inputs: facet count, omega, references (vrp_ref_k, xi_ref_{k+1}).
+struct KnotIn {
+    int m;
+    double w, rr0, rr1, xr0, xr1;
+};
+
+template <bool PH>
+__device__ __forceinline__ KnotIn knot_in(int64_t p, int k, int N, const double* omega, const double* xi_ref,
+                                          const double* vrp_ref, const int32_t* nfacets, const PhaseSrc& ps,
+                                          const int32_t* sPh)
+{
+    KnotIn r;
+    if (PH) {
+        const int ph = sPh[k], ph1 = sPh[k + 1];
+        const int64_t t0 = p * ps.P + (ph < 0 ? 0 : ph), t1 = p * ps.P + (ph1 < 0 ? 0 : ph1);
+        const int m = ps.nf[t0];
+        const double a0 = ps.ref[2 * t0], a1 = ps.ref[2 * t0 + 1];
+        const double c0 = ps.ref[2 * t1], c1 = ps.ref[2 * t1 + 1];
+        r.m = ph < 0 ? -1 : m;
+        r.w = omega[p * ps.ostride + k];
+        r.rr0 = ph < 0 ? 0.0 : a0;
+        r.rr1 = ph < 0 ? 0.0 : a1;
+        r.xr0 = ph1 < 0 ? 0.0 : c0;
+        r.xr1 = ph1 < 0 ? 0.0 : c1;
+    } else {
+        const int64_t st = p * N + k, sx = p * (N + 1) + (k + 1);
+        r.m = nfacets[st];
+        r.w = omega[st];
+        r.rr0 = vrp_ref[2 * st];
+        r.rr1 = vrp_ref[2 * st + 1];
+        r.xr0 = xi_ref[2 * sx];
+        r.xr1 = xi_ref[2 * sx + 1];
+    }
+    return r;
+}
+
+// A QP handed to the IPM kernel (status kPending) under the phase-indexed input: its expanded
+// window into the caller's scratch, which stage 2 reads as a blf_dcm_mpc_problem.
+template <int KPL>
+__device__ void ph_write_window(const PhaseSrc& ps, const int32_t* sPh, const double* omega, const double* A2v,
+                                const double* Bv, int64_t p, int N, int M, int S, int NH, int lane)
+{
+    const int nA = N * M;
+    for (int t = lane; t < nA; t += kWave) {
+        const int k = t / M, i = t - k * M;
+        const int o = i * S + (k % KPL) * NH + k / KPL;
+        ps.wA[2 * (p * nA + t)] = A2v[2 * o];
+        ps.wA[2 * (p * nA + t) + 1] = A2v[2 * o + 1];
+        ps.wb[p * nA + t] = Bv[o];
+    }
+    for (int k = lane; k <= N; k += kWave) {
+        const int ph = sPh[k];
+        const int64_t tp = p * ps.P + (ph < 0 ? 0 : ph);
+        const double r0 = ph < 0 ? 0.0 : ps.ref[2 * tp], r1 = ph < 0 ? 0.0 : ps.ref[2 * tp + 1];
+        ps.wxr[2 * (p * (N + 1) + k)] = r0;
+        ps.wxr[2 * (p * (N + 1) + k) + 1] = r1;
+        if (k < N) {
+            ps.wrr[2 * (p * N + k)] = r0;
+            ps.wrr[2 * (p * N + k) + 1] = r1;
+            ps.wnf[p * N + k] = ph < 0 ? -1 : ps.nf[tp];
+            ps.wom[p * N + k] = omega[p * ps.ostride + k];
+        }
+    }
+}
+
 // Outputs of one QP: the solution (certified), the oracle's outputs of a bad start or a failed LQ
 // factorization (status 3 / 2), or the start point for the IPM kernel's stage 2 (kPending).
 template <int KPL, bool LAMOUT>
@@ -800,14 +927,14 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
 // when none certifies, the fp64 LQ optimum from (xi_ref, vrp_ref) becomes the IPM's start point.
 // Measured alternatives: float rows in LDS with phase B reading fp64 rows from
 // global memory, at 2 / 3 / 4 waves per SIMD, and phase A as a kernel of its own — all slower.
-template <int KPL, bool LAMOUT>
+template <int KPL, bool LAMOUT, bool PH>
 __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
     const double* __restrict__ Ain, const double* __restrict__ bin,
     const int32_t* __restrict__ nfacets, double* __restrict__ xi_out, double* __restrict__ vrp_out,
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
-    double* __restrict__ lam_out)
+    double* __restrict__ lam_out, PhaseSrc ps)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
@@ -825,7 +952,14 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
 
     const int nA = N * M;
     constexpr int U = 2 * kMaxFacets;   // one round of 16 covers N M <= 1024
-    stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, 0, nA, A2d, Bv);
+    double* sBE = smem + 3 * (size_t)M * S;                            // PH: [2][P]
+    int32_t* sPh = reinterpret_cast<int32_t*>(sBE + 2 * (size_t)ps.P);  // PH: [N+1]
+    if (PH) {
+        ph_stage_phases(ps, p, N, P.dt, lane, sBE, sPh);
+        stage_rows_ph<KPL, U>(ps, sPh, p, N, M, S, NH, lane, A2d, Bv);
+    } else {
+        stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, 0, nA, A2d, Bv);
+    }
     const LdsRows<double> R{reinterpret_cast<const double2*>(A2d), Bv, S, NH};
 
     // ---- phase A: the float search (facet counts clamped; a bad count is reported below) ----
@@ -841,16 +975,14 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
         Fj.rh0 = Fj.rh1 = Fj.d0 = Fj.d1 = Fj.qx0 = Fj.qx1 = 0.0f;
         Fj.P00 = Fj.P01 = Fj.P11 = Fj.h00 = Fj.h01 = Fj.h11 = 0.0f;
         if (k < N) {
-            const int64_t st = p * N + k;
-            const int m = nfacets[st];
-            Fj.m = m < 0 ? 0 : m > M ? M : m;
-            Fj.w = float(omega[st]);
+            const KnotIn in = knot_in<PH>(p, k, N, omega, xi_ref, vrp_ref, nfacets, ps, sPh);
+            Fj.m = in.m < 0 ? 0 : in.m > M ? M : in.m;
+            Fj.w = float(in.w);
             Fj.be = Pf.dt * Fj.w;
-            Fj.rr0 = float(vrp_ref[2 * st]);
-            Fj.rr1 = float(vrp_ref[2 * st + 1]);
-            const int64_t sx = p * (N + 1) + (k + 1);
-            Fj.xr0 = float(xi_ref[2 * sx]);
-            Fj.xr1 = float(xi_ref[2 * sx + 1]);
+            Fj.rr0 = float(in.rr0);
+            Fj.rr1 = float(in.rr1);
+            Fj.xr0 = float(in.xr0);
+            Fj.xr1 = float(in.xr1);
         }
         Fj.al = 1.0f + Fj.be;
         Fj.r0 = Fj.rr0; Fj.r1 = Fj.rr1;
@@ -891,14 +1023,13 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
         Kj.P00 = Kj.P01 = Kj.P11 = Kj.h00 = Kj.h01 = Kj.h11 = 0.0;
         Kj.rr0 = Kj.rr1 = Kj.xr0 = Kj.xr1 = 0.0;
         if (k < N) {
-            const int64_t st = p * N + k;
-            Kj.m = nfacets[st];
-            Kj.w = omega[st];
-            Kj.rr0 = vrp_ref[2 * st];
-            Kj.rr1 = vrp_ref[2 * st + 1];
-            const int64_t sx = p * (N + 1) + (k + 1);
-            Kj.xr0 = xi_ref[2 * sx];
-            Kj.xr1 = xi_ref[2 * sx + 1];
+            const KnotIn in = knot_in<PH>(p, k, N, omega, xi_ref, vrp_ref, nfacets, ps, sPh);
+            Kj.m = in.m;
+            Kj.w = in.w;
+            Kj.rr0 = in.rr0;
+            Kj.rr1 = in.rr1;
+            Kj.xr0 = in.xr0;
+            Kj.xr1 = in.xr1;
             if (Kj.m < 0 || Kj.m > M) {
                 bad = true;
                 Kj.m = 0;
@@ -950,6 +1081,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
     AS_STAMP_ADD(14, t_b);
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
                                   status_out, iters_out, polished_out, lam_out);
+    if (PH && !certified && status == 0) ph_write_window<KPL>(ps, sPh, omega, A2d, Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(0, t_start);
 #ifdef BLF_STAMPS
     if (threadIdx.x == 0 && blockIdx.x < 65536) {
@@ -965,7 +1097,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
 // One wavefront per QP, fp64 facet rows in LDS.  From the shifted previous solution (xi rolled
 // out from its VRPs), guess = the facets the rollout violates plus those whose previous multiplier
 // exceeds the floor, then the fp64 passes (1.7 per window on average: no float search first).
-template <int KPL, bool LAMOUT>
+template <int KPL, bool LAMOUT, bool PH>
 __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -973,7 +1105,8 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     const int32_t* __restrict__ nfacets, const double* __restrict__ ws_vrp,
     const double* __restrict__ ws_lam, double* __restrict__ xi_out, double* __restrict__ vrp_out,
     int32_t* __restrict__ status_out,
-    int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out)
+    int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out,
+    PhaseSrc ps)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
@@ -994,9 +1127,15 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     //      then the LDS stores, which wait for the slab loads only ----
     const int nA = N * M;
     constexpr int U = (2 * kWave * kMaxFacets) / kWave;   // 16: nA <= 1024 in one round
-    double2 va[U];
-    double vb[U];
-    {
+    double* sBE = smem + 3 * (size_t)M * S;                            // PH: [2][P]
+    int32_t* sPh = reinterpret_cast<int32_t*>(sBE + 2 * (size_t)ps.P);  // PH: [N+1]
+    if (PH) {   // the rows from the phase table (the knots' loads then follow the LDS stores)
+        ph_stage_phases(ps, p, N, P.dt, lane, sBE, sPh);
+        stage_rows_ph<KPL, U>(ps, sPh, p, N, M, S, NH, lane, reinterpret_cast<double*>(A2), Bv);
+    }
+    double2 va[PH ? 1 : U];
+    double vb[PH ? 1 : U];
+    if (!PH) {
         const double2* As = reinterpret_cast<const double2*>(Ain) + p * nA;
         const double* bs = bin + p * nA;
 #pragma unroll
@@ -1023,20 +1162,19 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
         Kj.rr0 = Kj.rr1 = Kj.xr0 = Kj.xr1 = 0.0;
         if (k < N) {
             const int64_t st = p * N + k;
-            Kj.m = nfacets[st];
-            Kj.w = omega[st];
+            const KnotIn in = knot_in<PH>(p, k, N, omega, xi_ref, vrp_ref, nfacets, ps, sPh);
+            Kj.m = in.m;
+            Kj.w = in.w;
             const bool ws = k + P.ws_shift < N;
-            const double* r0 = ws ? ws_vrp + 2 * P.ws_shift : vrp_ref;
-            Kj.r0 = r0[2 * st];
-            Kj.r1 = r0[2 * st + 1];
-            Kj.rr0 = vrp_ref[2 * st];
-            Kj.rr1 = vrp_ref[2 * st + 1];
-            const int64_t sx = p * (N + 1) + (k + 1);
-            Kj.xr0 = xi_ref[2 * sx];
-            Kj.xr1 = xi_ref[2 * sx + 1];
+            Kj.r0 = ws ? ws_vrp[2 * (st + P.ws_shift)] : in.rr0;
+            Kj.r1 = ws ? ws_vrp[2 * (st + P.ws_shift) + 1] : in.rr1;
+            Kj.rr0 = in.rr0;
+            Kj.rr1 = in.rr1;
+            Kj.xr0 = in.xr0;
+            Kj.xr1 = in.xr1;
         }
     }
-    {
+    if (!PH) {
         const bool pow2 = (M & (M - 1)) == 0;
         const int sh = __builtin_ctz(M);
 #pragma unroll
@@ -1125,6 +1263,8 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
 
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
                                   status_out, iters_out, polished_out, lam_out);
+    if (PH && !certified && status == 0)
+        ph_write_window<KPL>(ps, sPh, omega, reinterpret_cast<const double*>(A2), Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(11, t_out);
     AS_STAMP_ADD(15, t_start);
 #ifdef BLF_STAMPS
@@ -1139,23 +1279,31 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
 
 template <int KPL>
 blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const blf_dcm_mpc_warm_start* warm,
-                      int64_t batch, const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+                      int64_t batch, const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
+                      const PhaseSrc* ps)
 {
 #ifndef AS_EXTRA_LDS
 #define AS_EXTRA_LDS 0
 #endif
     const size_t slots = (size_t)kp.M * (KPL * ((kp.N + KPL - 1) / KPL));
+    const PhaseSrc none{};
+    const PhaseSrc& src = ps ? *ps : none;
+    const size_t lds = 3 * sizeof(double) * slots + (ps ? ph_lds_bytes(ps->P, kp.N) : 0) + AS_EXTRA_LDS;
+    if (lds > 64 * 1024)
+        return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: %zu B of LDS (%d phases)", lds, ps ? ps->P : 0);
     if (warm == nullptr) {
-        auto kern = lam_out ? dcm_mpc_cold_kernel<KPL, true> : dcm_mpc_cold_kernel<KPL, false>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), 3 * sizeof(double) * slots + AS_EXTRA_LDS, s, kp,
+        auto kern = ps ? (lam_out ? dcm_mpc_cold_kernel<KPL, true, true> : dcm_mpc_cold_kernel<KPL, false, true>)
+                       : (lam_out ? dcm_mpc_cold_kernel<KPL, true, false> : dcm_mpc_cold_kernel<KPL, false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds, s, kp,
                            pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, sol->xi,
-                           sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
+                           sol->vrp, sol->status, sol->iters, sol->polished, lam_out, src);
         return check_hip(hipGetLastError(), "dcm_mpc_cold_kernel launch");
     }
-    auto kern = lam_out ? dcm_mpc_warm_kernel<KPL, true> : dcm_mpc_warm_kernel<KPL, false>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), 3 * sizeof(double) * slots + AS_EXTRA_LDS, s, kp,
+    auto kern = ps ? (lam_out ? dcm_mpc_warm_kernel<KPL, true, true> : dcm_mpc_warm_kernel<KPL, false, true>)
+                   : (lam_out ? dcm_mpc_warm_kernel<KPL, true, false> : dcm_mpc_warm_kernel<KPL, false, false>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, warm->vrp,
-                       warm->lambda, sol->xi, sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
+                       warm->lambda, sol->xi, sol->vrp, sol->status, sol->iters, sol->polished, lam_out, src);
     return check_hip(hipGetLastError(), "dcm_mpc_warm_kernel launch");
 }
 
@@ -1189,10 +1337,11 @@ extern "C" int blf_debug_as_stamps(unsigned long long* out, int reset)
 // (status 0, polished) or marked kPending for the IPM kernel's stage 2.
 blf_status launch_dcm_mpc_as(const qp::KParams& kp, const blf_dcm_mpc_problem* pb,
                              const blf_dcm_mpc_warm_start* warm, int64_t batch,
-                             const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+                             const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
+                             const qp::PhaseSrc* ps)
 {
-    if (kp.N <= kWave) return launch_kpl<1>(kp, pb, warm, batch, sol, lam_out, s);
-    if (kp.N <= 2 * kWave) return launch_kpl<2>(kp, pb, warm, batch, sol, lam_out, s);
+    if (kp.N <= kWave) return launch_kpl<1>(kp, pb, warm, batch, sol, lam_out, s, ps);
+    if (kp.N <= 2 * kWave) return launch_kpl<2>(kp, pb, warm, batch, sol, lam_out, s, ps);
     return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: horizon %d > 128", kp.N);
 }
 

@@ -1263,9 +1263,8 @@ extern "C" int blf_debug_stamps(unsigned long long* out, int reset)
 }
 #endif
 
-blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
-                          const blf_dcm_mpc_warm_start* warm, int64_t batch,
-                          const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+namespace {
+KParams make_kparams(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_warm_start* warm)
 {
     KParams kp;
     kp.N = prm->horizon;
@@ -1288,6 +1287,27 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     kp.f_Pw0 = (float)kp.Pw0; kp.f_Pw1 = (float)kp.Pw1;
     kp.f_tol_p = kSearchTolP;
     kp.f_tol_d = kSearchTolD;
+    return kp;
+}
+
+blf_status launch_ipm(const KParams& kp, const blf_dcm_mpc_problem* pb, const blf_dcm_mpc_warm_start* warm,
+                      int64_t batch, const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+{
+    const int N = kp.N;
+    if (N <= 64) return launch_nt<64>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 128) return launch_nt<128>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 256) return launch_nt<256>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 512) return launch_nt<512>(kp, pb, warm, batch, sol, lam_out, s);
+    if (N <= 1024) return launch_nt<1024>(kp, pb, warm, batch, sol, lam_out, s);
+    return set_error(BLF_ERR_UNSUPPORTED, "horizon %d > 1024", N);
+}
+}  // namespace
+
+blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
+                          const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                          const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+{
+    KParams kp = make_kparams(prm, warm);
     if (batch == 0) return BLF_OK;
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     const int N = kp.N;
@@ -1301,12 +1321,48 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
         if (st != BLF_OK) return st;
         kp.stage2 = 1;
     }
-    if (N <= 64) return launch_nt<64>(kp, pb, warm, batch, sol, lam_out, s);
-    if (N <= 128) return launch_nt<128>(kp, pb, warm, batch, sol, lam_out, s);
-    if (N <= 256) return launch_nt<256>(kp, pb, warm, batch, sol, lam_out, s);
-    if (N <= 512) return launch_nt<512>(kp, pb, warm, batch, sol, lam_out, s);
-    if (N <= 1024) return launch_nt<1024>(kp, pb, warm, batch, sol, lam_out, s);
-    return set_error(BLF_ERR_UNSUPPORTED, "horizon %d > 1024", N);
+    return launch_ipm(kp, pb, warm, batch, sol, lam_out, s);
+}
+
+// blf_dcm_mpc_solve_phased: the active-set kernels read the window from the phase table (PhaseSrc);
+// the QPs they hand over (kPending) leave their expanded window in the caller's scratch, from
+// which the IPM kernel's stage 2 continues exactly as after blf_dcm_phase_expand + solve.
+blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_table* ph,
+                                 int64_t start_knot, const double* xi_init, const double* omega,
+                                 int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
+                                 int64_t batch, const blf_dcm_mpc_window* win,
+                                 const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+{
+    KParams kp = make_kparams(prm, warm);
+    if (batch == 0) return BLF_OK;
+    if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
+    if (kp.N > 2 * kWave || !(kp.tol_polish > 0.0))
+        return set_error(BLF_ERR_UNSUPPORTED,
+                         "phase-indexed solve: horizon %d > 128 or tol_polish = 0 (use blf_dcm_phase_expand "
+                         "+ blf_dcm_mpc_solve_warm)", kp.N);
+    PhaseSrc ps{};
+    ps.P = ph->max_phases;
+    ps.nphases = ph->nphases;
+    ps.begin = ph->begin;
+    ps.end = ph->end;
+    ps.A = ph->A;
+    ps.b = ph->b;
+    ps.nf = ph->nfacets;
+    ps.ref = ph->ref;
+    ps.start = start_knot;
+    ps.ostride = omega_stride;
+    ps.wom = win->omega;
+    ps.wxr = win->xi_ref;
+    ps.wrr = win->vrp_ref;
+    ps.wA = win->A;
+    ps.wb = win->b;
+    ps.wnf = win->nfacets;
+    const blf_dcm_mpc_problem pin{xi_init, omega, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const blf_status st = launch_dcm_mpc_as(kp, &pin, warm, batch, sol, lam_out, s, &ps);
+    if (st != BLF_OK) return st;
+    kp.stage2 = 1;
+    const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
+    return launch_ipm(kp, &pw, warm, batch, sol, lam_out, s);
 }
 
 }  // namespace blf

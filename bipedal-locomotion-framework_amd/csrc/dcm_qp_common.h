@@ -204,11 +204,44 @@ __device__ __forceinline__ bool rc_apply(const RcT<T>& e, T P00, T P01, T P11, T
     return ok;
 }
 
+// The phase-indexed input of blf_dcm_mpc_solve_phased: the plan's phase table (blf_phase_table)
+// in place of the window's per-knot arrays, and the window scratch a QP handed to the IPM kernel
+// is expanded into (blf_dcm_mpc_window).
+struct PhaseSrc {
+    int32_t P;                         // phases per problem (table stride)
+    const int32_t* nphases;            // [B]
+    const double *begin, *end;         // [B][P]
+    const double *A, *b;               // [B][P][M][2], [B][P][M]
+    const int32_t* nf;                 // [B][P]
+    const double* ref;                 // [B][P][2]
+    int64_t start;                     // window start knot: t_k = (start + k) dt
+    int64_t ostride;                   // omega row stride of the window
+    double *wom, *wxr, *wrr, *wA, *wb; // window scratch (stage 2)
+    int32_t* wnf;
+};
+
 }  // namespace qp
 
+// The knot -> phase rule of blf_dcm_phase_expand (phase_expand.hip and the fused phase-indexed
+// solve share it, so both expand a window identically): p = the last phase with begin_p <= t, by
+// this binary search over the phases in table order; the knot is in p iff t < end_p, else -1.
+__device__ __forceinline__ int phase_of(const double* begin, const double* end, int n, double t)
+{
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (begin[mid] <= t) lo = mid + 1;
+        else hi = mid;
+    }
+    const int p = lo - 1;
+    return (p >= 0 && t < end[p]) ? p : -1;
+}
+
 // dcm_mpc_as.hip: the one-wavefront active-set kernel (N <= 128); QPs it does not certify are left
-// with status qp::kPending for the IPM kernel's stage 2.
+// with status qp::kPending for the IPM kernel's stage 2.  ps != nullptr: the phase-indexed input
+// (pb->xi_init and pb->omega are used, the other per-knot arrays are not).
 blf_status launch_dcm_mpc_as(const qp::KParams& kp, const blf_dcm_mpc_problem* pb,
                              const blf_dcm_mpc_warm_start* warm, int64_t batch,
-                             const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s);
+                             const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
+                             const qp::PhaseSrc* ps = nullptr);
 }  // namespace blf

@@ -15,25 +15,13 @@
 // in LDS); then the workgroup writes the window's arrays with consecutive threads on consecutive
 // 16-B A rows, 8-B offsets, facet counts and 16-B references.  HBM-bound: the bytes written are
 // the per-knot arrays of the QP.
-#include "blf_internal.h"
+#include "dcm_qp_common.h"   // phase_of
 #include "slab.h"
 
 namespace blf {
 namespace {
 
 constexpr int kExpandBlock = 256;
-
-__device__ __forceinline__ int phase_of(const double* begin, const double* end, int n, double t)
-{
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (begin[mid] <= t) lo = mid + 1;
-        else hi = mid;
-    }
-    const int p = lo - 1;
-    return (p >= 0 && t < end[p]) ? p : -1;
-}
 
 // Dynamic LDS (doubles first, 16-B aligned): A [P][M] double2, ref [P] double2, b [P][M],
 // begin [P], end [P], then nf [P] and the knot phases [N+1] as int32.

@@ -22,6 +22,10 @@ namespace blf {
 namespace {
 
 constexpr int kHullBlock = 64;
+#ifndef BLF_HULL_U
+#define BLF_HULL_U 4
+#endif
+constexpr int HU = BLF_HULL_U;   // facet pairs per lane in flight (phase 2)
 
 __device__ __forceinline__ double cross3(double ox, double oy, double ax, double ay, double bx,
                                          double by)
@@ -235,9 +239,11 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     double* bb = bout + p0 * M;
     const bool vecA = ((uintptr_t)Ab & 15) == 0;
     const SlabIdx im(M);
-    for (int e = t; e < npair; e += kHullBlock) {
+    auto facet = [&](int e, double& nx, double& ny, double& bj) {
         const int r = im.row(e), j = e - r * M;
-        double nx = 0.0, ny = 0.0, bj = 0.0;
+        nx = 0.0;
+        ny = 0.0;
+        bj = 0.0;
         if (j < s_nf[r]) {
             int a, b;
             if (PK) {
@@ -256,6 +262,8 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
             ny = (-ex) / len;
             bj = nx * v0x + ny * v0y;
         }
+    };
+    auto put = [&](int e, double nx, double ny, double bj) {
         if (vecA) {
             *reinterpret_cast<double2*>(Ab + 2 * e) = make_double2(nx, ny);
         } else {
@@ -263,6 +271,21 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
             Ab[2 * e + 1] = ny;
         }
         bb[e] = bj;
+    };
+    int e = t;
+    // HU pairs per lane at a time: their LDS reads, square roots and divisions are independent,
+    // so they overlap instead of serialising one pair's latency chain after another
+    for (; e + (HU - 1) * kHullBlock < npair; e += HU * kHullBlock) {
+        double nx[HU], ny[HU], bj[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) facet(e + u * kHullBlock, nx[u], ny[u], bj[u]);
+#pragma unroll
+        for (int u = 0; u < HU; ++u) put(e + u * kHullBlock, nx[u], ny[u], bj[u]);
+    }
+    for (; e < npair; e += kHullBlock) {
+        double nx, ny, bj;
+        facet(e, nx, ny, bj);
+        put(e, nx, ny, bj);
     }
 }
 
@@ -345,12 +368,23 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
         // long VALU sequence per lane
         const int64_t sp = (S * Q < 0x7fffffffLL) ? (int64_t)((uint32_t)gid / (uint32_t)Q) : gid / Q;
         const double* t = kt + sp * K1;
-        const double tt = tq[gid];
+        // the query times and knot indices are streamed once: non-temporal
+        const double tt = __builtin_nontemporal_load(tq + gid);
         // last j with t_j <= t: a forward pass keeps the knot loads independent of each other
+        // (up to 8 knots all issued before the first comparison)
         int raw = -1;
-        for (int j = 0; j < K1; ++j)
-            if (t[j] <= tt) raw = j;
-        idx[gid] = raw;
+        if (K1 <= 8) {
+            double tk[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) tk[j] = j < K1 ? t[j] : 0.0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < K1 && tk[j] <= tt) raw = j;
+        } else {
+            for (int j = 0; j < K1; ++j)
+                if (t[j] <= tt) raw = j;
+        }
+        __builtin_nontemporal_store(raw, idx + gid);
         const int seg = raw < 0 ? 0 : (raw > K - 1 ? K - 1 : raw);
         const double tau = tt - t[seg];
         double* o = s_out + threadIdx.x * SW;
@@ -375,7 +409,7 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
         }
     }
     __syncthreads();
-    slab_store<kEvalBlock, 4>(pva + g0 * W, W, s_out, SW, rows, W);
+    slab_store<kEvalBlock, 6>(pva + g0 * W, W, s_out, SW, rows, W);   // 9 doubles x 256: one batch
 }
 
 }  // namespace

@@ -85,7 +85,7 @@ class TimeVaryingDCMPlanner : public System::Advanceable<DCMPlanBatch>
     // device-resident state
     blf::DeviceBuffer<double> m_dPhBegin, m_dPhEnd, m_dPhCorners, m_dPhRef, m_dPhA, m_dPhB;
     blf::DeviceBuffer<int32_t> m_dNPhases, m_dPhNCorners, m_dPhNf;
-    blf::DeviceBuffer<double> m_dXi0, m_dOmega, m_dXiRef, m_dVrpRef, m_dA, m_dB;
+    blf::DeviceBuffer<double> m_dXi0, m_dOmega, m_dXiRef, m_dVrpRef, m_dA, m_dB, m_dWinOmega;
     blf::DeviceBuffer<double> m_dXi, m_dVrp[2], m_dLam[2];
     blf::DeviceBuffer<int32_t> m_dNf, m_dStatus, m_dIters;
 

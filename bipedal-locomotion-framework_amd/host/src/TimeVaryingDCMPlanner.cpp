@@ -1,8 +1,8 @@
 /**
  * @file TimeVaryingDCMPlanner.cpp
  * Host bookkeeping (phases -> active-contact corners, once per plan) around the device pipeline
- * blf_hull2d_hrep (once per plan) -> blf_dcm_phase_expand -> blf_dcm_mpc_solve_warm (per
- * advance()).
+ * blf_hull2d_hrep (once per plan) -> blf_dcm_mpc_solve_phased (per advance(); horizons above 128:
+ * blf_dcm_phase_expand -> blf_dcm_mpc_solve_warm).
  */
 #include <algorithm>
 #include <cmath>
@@ -279,34 +279,49 @@ bool TimeVaryingDCMPlanner::advance()
         m_xi0Dirty = false;
     }
 
-    // 2. the window's per-knot arrays from the phase table
+    // 2. the window's QPs, warm-started from the previous solution shifted by one knot.  Horizons
+    //    up to 128 read the window straight from the phase table (blf_dcm_mpc_solve_phased: the
+    //    expansion happens in the solver's LDS; the per-knot arrays are only scratch for problems
+    //    the interior point method finishes); longer ones expand the window through HBM first.
     if (!m_dA.resize(BN * M * 2) || !m_dB.resize(BN * M) || !m_dNf.resize(BN) ||
         !m_dXiRef.resize(static_cast<std::size_t>(B) * (N + 1) * 2) || !m_dVrpRef.resize(BN * 2))
         return false;
     blf_phase_table table{m_maxPhases,     M,             m_dNPhases.data(), m_dPhBegin.data(),
                           m_dPhEnd.data(), m_dPhA.data(), m_dPhB.data(),     m_dPhNf.data(),
                           m_dPhRef.data()};
-    if (!blf::report(blf_dcm_phase_expand(h, &table, m_start, m_params.dt, N, B, m_dA.data(),
-                                          m_dB.data(), m_dNf.data(), m_dXiRef.data(),
-                                          m_dVrpRef.data(), nullptr),
-                     "TimeVaryingDCMPlanner::advance"))
-        return false;
-
-    // 3. the QPs, warm-started from the previous solution shifted by one knot
     const int nxt = m_solved ? 1 - m_cur : m_cur;
     if (!m_dXi.resize(static_cast<std::size_t>(B) * (N + 1) * 2) ||
         !m_dVrp[nxt].resize(BN * 2) || !m_dLam[nxt].resize(BN * M) || !m_dStatus.resize(B) ||
         !m_dIters.resize(B))
         return false;
-    blf_dcm_mpc_problem prob{m_dXi0.data(), m_dOmega.data(), m_dXiRef.data(), m_dVrpRef.data(),
-                             m_dA.data(),   m_dB.data(),     m_dNf.data()};
     blf_dcm_mpc_solution sol{m_dXi.data(), m_dVrp[nxt].data(), m_dStatus.data(), m_dIters.data()};
     blf_dcm_mpc_warm_start warm{m_dVrp[m_cur].data(), m_dLam[m_cur].data(), 1, 0, m_warmFloor};
     const bool useWarm = m_warmStart && m_haveWarm && m_solved;
-    if (!blf::report(blf_dcm_mpc_solve_warm(h, &m_params, &prob, useWarm ? &warm : nullptr, B,
-                                            &sol, m_dLam[nxt].data(), nullptr),
-                     "TimeVaryingDCMPlanner::advance"))
-        return false;
+    if (N <= 128 && m_params.tol_polish > 0)
+    {
+        if (!m_dWinOmega.resize(BN)) return false;
+        blf_dcm_mpc_window win{m_dWinOmega.data(), m_dXiRef.data(), m_dVrpRef.data(),
+                               m_dA.data(),        m_dB.data(),     m_dNf.data()};
+        if (!blf::report(blf_dcm_mpc_solve_phased(h, &m_params, &table, m_start, m_dXi0.data(),
+                                                  m_dOmega.data(), N, useWarm ? &warm : nullptr,
+                                                  B, &win, &sol, m_dLam[nxt].data(), nullptr),
+                         "TimeVaryingDCMPlanner::advance"))
+            return false;
+    }
+    else
+    {
+        if (!blf::report(blf_dcm_phase_expand(h, &table, m_start, m_params.dt, N, B, m_dA.data(),
+                                              m_dB.data(), m_dNf.data(), m_dXiRef.data(),
+                                              m_dVrpRef.data(), nullptr),
+                         "TimeVaryingDCMPlanner::advance"))
+            return false;
+        blf_dcm_mpc_problem prob{m_dXi0.data(), m_dOmega.data(), m_dXiRef.data(), m_dVrpRef.data(),
+                                 m_dA.data(),   m_dB.data(),     m_dNf.data()};
+        if (!blf::report(blf_dcm_mpc_solve_warm(h, &m_params, &prob, useWarm ? &warm : nullptr, B,
+                                                &sol, m_dLam[nxt].data(), nullptr),
+                         "TimeVaryingDCMPlanner::advance"))
+            return false;
+    }
 
     // 4. the planned xi_1 is the next window's initial DCM; move the window
     if (!blf::copyRows(m_dXi0.data(), 2 * sizeof(double), m_dXi.data() + 2,

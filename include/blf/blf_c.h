@@ -35,6 +35,8 @@
  *   blf_fbd_euler_integrate   ForwardEuler<FloatingBaseDynamicalSystem>::integrate
  *   blf_dcm_phase_expand      Planners/src/ContactPhaseList.cpp:16-84 phases looked up per knot with the
  *                             getPresentContact rule (ContactList.cpp:190-202), SURVEY.md 8(f) item 2
+ *   blf_dcm_mpc_solve_phased  blf_dcm_phase_expand + blf_dcm_mpc_solve_warm fused: one
+ *                             Advanceable::advance() (System/Advanceable.h:24-46) of the planner
  *   blf_fb_dcm / blf_dcm_posture_reference  the state -> plan and plan -> input maps a user
  *                             writes around Advanceable::advance() and ForwardEuler::integrate in a
  *                             closed loop (config 5); no reference counterpart
@@ -246,6 +248,36 @@ blf_status blf_dcm_phase_expand(blf_handle* handle, const blf_phase_table* phase
                                 int64_t start_knot, double dt, int32_t horizon, int64_t batch,
                                 double* A, double* b, int32_t* nfacets, double* xi_ref,
                                 double* vrp_ref, void* stream);
+
+/* ---- 5c. Phase-indexed solve: one advance() of the receding horizon in one call ---------------
+ * blf_dcm_phase_expand(phases, start_knot, params->dt, params->horizon) followed by
+ * blf_dcm_mpc_solve_warm on the expanded window, with the same results bit for bit, for horizons
+ * up to 128 (larger: BLF_ERR_UNSUPPORTED; use the two calls).  The window's rows are expanded from
+ * the phase table into the solver's on-chip memory instead of through HBM: a problem reads its
+ * phase table (a few KB) instead of the window's per-knot arrays (~19 KB at N = 100, M = 8).
+ * phases->max_facets must equal params->max_facets.  omega: row q (the window's N values) at
+ * omega + q * omega_stride (omega_stride >= N; e.g. the plan's omega shifted by start_knot, no
+ * copy).  xi_init, warm, solution and lambda_out as blf_dcm_mpc_solve_warm.
+ * window: blf_dcm_phase_expand's output arrays plus the window's omega (omega [B][N]), used as
+ * scratch: a problem the active-set passes do not certify continues in the interior point method,
+ * which reads its expanded window from there.  Only such problems' rows are written (none, with
+ * the default parameters, in every workload measured); the contents are unspecified otherwise. */
+typedef struct blf_dcm_mpc_window {
+    double* omega;             /* [B][N]                                                     */
+    double* xi_ref;            /* [B][N+1][2]                                                */
+    double* vrp_ref;           /* [B][N][2]                                                  */
+    double* A;                 /* [B][N][M][2]                                               */
+    double* b;                 /* [B][N][M]                                                  */
+    int32_t* nfacets;          /* [B][N]                                                     */
+} blf_dcm_mpc_window;
+
+blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                    const blf_phase_table* phases, int64_t start_knot,
+                                    const double* xi_init, const double* omega,
+                                    int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
+                                    int64_t batch, const blf_dcm_mpc_window* window,
+                                    const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                    void* stream);
 
 /* ---- 6. Contact model (ContinuousContactModel), batched ------------------------------------
  * Rectangular L x W patch, spring k, damper b (ContinuousContactModel.h:22-57).
