@@ -153,6 +153,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--tol-polish", type=float, default=None,
                     help="override blf_dcm_mpc_default_params' tol_polish (also the CPU baseline's)")
+    ap.add_argument("--expand-path", action="store_true",
+                    help="rh / c3 / c5: expand the window through HBM (blf_dcm_phase_expand) and "
+                         "solve it (the two calls blf_dcm_mpc_solve_phased fuses; A/B only)")
     ap.add_argument("--workload", choices=("c1", "c2", "c3", "c5", "rh"), default="c2",
                     help="c2 (default, the driver's metric): configs[1]; c1: configs[0] single-solve "
                          "latency (4 footsteps, N=50) on the GPU and the CPU; c3: configs[2] pipeline "
@@ -364,14 +367,19 @@ def other_workload(args):
         Pn = prob["phase_begin"].shape[1]
 
         def step():
-            # ConvexHullHelper on every phase's support polygon (blf_hull2d_hrep), the knots'
-            # constraints and references from the phase table (blf_dcm_phase_expand), the QPs,
+            # ConvexHullHelper on every phase's support polygon (blf_hull2d_hrep), the QPs read
+            # their knots' constraints and references from that phase table
+            # (blf_dcm_mpc_solve_phased; --expand-path: blf_dcm_phase_expand + blf_dcm_mpc_solve),
             # then the swing-foot splines
             table = h.phase_table(t("nphases"), t("phase_begin"), t("phase_end"), t("phase_corners"),
                                   t("phase_ncorners"), ref=t("phase_ref"))
-            w = h.dcm_phase_expand(table, 0, prob["dt"], N)
-            w.update(d)
-            out["qp"] = h.dcm_mpc_solve(w, params)
+            if args.expand_path:
+                w = h.dcm_phase_expand(table, 0, prob["dt"], N)
+                w.update(d)
+                out["qp"] = h.dcm_mpc_solve(w, params)
+            else:
+                out["qp"] = h.dcm_mpc_solve_phased(table, 0, d["xi_init"], d["omega"], params,
+                                                   out=out.get("qp"))
             coeffs = h.quintic_fit(kt, kp)
             out["sp"] = h.quintic_eval(kt, coeffs, tq)
 
@@ -381,7 +389,8 @@ def other_workload(args):
                 "value": B / sec, "unit": "QP/s", "n_gpus": 1, "ms_per_step": sec * 1e3,
                 "steps": args.steps, "warmup": args.warmup, "dtype": "f64",
                 "config": {"workload": f"configs[2]: batch={B}, horizon={N}, {B * Pn} phase "
-                                       f"support polygons (hull H-rep) expanded to the knots, "
+                                       f"support polygons (hull H-rep) "
+                                       f"{'expanded to the knots in HBM' if args.expand_path else 'read by the QP kernel (phase-indexed)'}, "
                                        f"{kt.shape[0]} swing splines x 32 queries",
                            "batch_per_gpu": B}}
         if not args.no_cpu:
@@ -424,6 +433,7 @@ def closed_loop(args):
     plan = P.make_batch(B, horizon=N + S, n_footsteps=8, seed=P.SEED, start=rank * B, first_ds=S + 10)
     st = robot.standing_states(model, B, seed=1000 + rank)
     loop = DL.ClosedLoop(h, model, plan, st, horizon=N)
+    loop.expand_path = args.expand_path
     for _ in range(args.warmup):
         loop.period()
     torch.cuda.synchronize()
@@ -626,17 +636,24 @@ def receding_horizon(args, h, dev):
         if timed:
             evs.append(ev)
             ev[0].record(stream)
-        w = h.dcm_phase_expand(table, s, prob["dt"], N)
-        if timed:
-            ev[1].record(stream)
-        w.update(xi_init=state["xi0"], omega=omega_full[:, s:s + N].contiguous())
         cur = s % 2
         warm = None
         if state["prev"] is not None:
             warm = dict(vrp=state["prev"]["vrp"], lam=state["prev"]["lam"], shift=1, floor=1e-3)
-        if timed:
-            ev[2].record(stream)
-        out = h.dcm_mpc_solve(w, params, out=bufs[cur], warm=warm, lambda_out=True)
+        if args.expand_path:
+            w = h.dcm_phase_expand(table, s, prob["dt"], N)
+            if timed:
+                ev[1].record(stream)
+            w.update(xi_init=state["xi0"], omega=omega_full[:, s:s + N].contiguous())
+            if timed:
+                ev[2].record(stream)
+            out = h.dcm_mpc_solve(w, params, out=bufs[cur], warm=warm, lambda_out=True)
+        else:   # one call: the window read from the phase table, omega as a strided view
+            if timed:
+                ev[1].record(stream)
+                ev[2].record(stream)
+            out = h.dcm_mpc_solve_phased(table, s, state["xi0"], omega_full[:, s:s + N], params,
+                                         warm=warm, out=bufs[cur], lambda_out=True)
         if timed:
             ev[3].record(stream)
         bufs[cur] = out
@@ -660,19 +677,22 @@ def receding_horizon(args, h, dev):
     assert int((state["prev"]["status"] != 0).sum()) == 0, "unsolved QPs in a window"
     it = torch.stack(iters[args.warmup:]).float()
     Pn = table["phase_begin"].shape[1]
-    ex_ms = sorted(expand_ms)[len(expand_ms) // 2]
-    ex_gbs = phase_expand_bytes(Pn, N, M) * B / (ex_ms * 1e-3) / 1e9
     line = {"metric": "receding-horizon DCM-MPC advance()/sec (phase expansion + warm-started QP)",
             "value": B / sec, "unit": "QP/s", "n_gpus": 1, "ms_per_step": sec * 1e3,
             "steps": args.steps, "warmup": args.warmup, "dtype": "f64",
             "mean_ipm_iters_warm": float(it.mean()),
             "solve_ms_median": sorted(solve_ms)[len(solve_ms) // 2],
-            "phase_expand": {"kernel_ms_median": ex_ms, "bytes_per_problem":
-                             phase_expand_bytes(Pn, N, M), "achieved_gbs": ex_gbs,
-                             "frac_hbm": ex_gbs / HBM_PEAK_GBS},
+            "path": "blf_dcm_phase_expand + blf_dcm_mpc_solve_warm" if args.expand_path else
+                    "blf_dcm_mpc_solve_phased (window read from the phase table in the QP kernel)",
             "config": {"workload": f"batch={B} plans (8 footsteps, {Pn} phases), horizon={N}, "
                                    f"window moved one knot per step, warm start shift 1 floor 1e-3",
                        "batch_per_gpu": B}}
+    if args.expand_path:
+        ex_ms = sorted(expand_ms)[len(expand_ms) // 2]
+        ex_gbs = phase_expand_bytes(Pn, N, M) * B / (ex_ms * 1e-3) / 1e9
+        line["phase_expand"] = {"kernel_ms_median": ex_ms, "bytes_per_problem":
+                                phase_expand_bytes(Pn, N, M), "achieved_gbs": ex_gbs,
+                                "frac_hbm": ex_gbs / HBM_PEAK_GBS}
     print(json.dumps(line), flush=True)
 
 

@@ -10,7 +10,7 @@ One control period of this loop, stream-ordered on the device for a batch of rob
 
   1. state -> plan:  xi = c_xy + cdot_xy / omega_0 from the robot's centre of mass
                      (blf_fb_dcm), the next window's xi_init;
-  2. plan:           the window moved one knot (blf_dcm_phase_expand) and solved warm from the
+  2. plan:           the window moved one knot (blf_dcm_mpc_solve_phased) and solved warm from the
                      previous period's solution (blf_dcm_mpc_solve_warm, shift 1);
   3. plan -> robot:  joint references from the plan's first VRP and the centre of mass, held over
                      the period (blf_dcm_posture_reference);
@@ -62,12 +62,14 @@ class ClosedLoop:
         self.omega = t(plan["omega"])
         self.params = native.default_params(horizon, max_facets=self.table["phase_b"].shape[2])
         self.params.tol_polish = tol_polish     # TimeVaryingDCMPlanner's warm-start trigger
+        self.params.dt = self.dt                # the knots of the plan are the QP's knots
         self.com = torch.empty((self.B, 6), dtype=torch.float64, device=dev)
         self.xi = torch.empty((self.B, 2), dtype=torch.float64, device=dev)
         self.q_ref = torch.empty((self.B, model["n"]), dtype=torch.float64, device=dev)
         self.bufs = [None, None]
         self.prev = None
         self.s = 0
+        self.expand_path = False   # True: blf_dcm_phase_expand + blf_dcm_mpc_solve (A/B)
 
     def period(self):
         """One control period (stream-ordered; nothing synchronises).  Returns the plan."""
@@ -76,13 +78,18 @@ class ClosedLoop:
             raise ValueError(f"the plan ends at knot {self.omega.shape[1]}; period {s} needs {s + N}")
         h.fb_dcm(self.dm, self.state, omega=self.omega, column=s, com=self.com, xi=self.xi,
                  stream=self.stream)
-        w = h.dcm_phase_expand(self.table, s, self.dt, N, stream=self.stream)
-        w.update(xi_init=self.xi, omega=self.omega[:, s:s + N].contiguous())
         warm = None
         if self.prev is not None:
             warm = dict(vrp=self.prev["vrp"], lam=self.prev["lam"], shift=1, floor=1e-3)
-        out = h.dcm_mpc_solve(w, self.params, out=self.bufs[s % 2], warm=warm, lambda_out=True,
-                              stream=self.stream)
+        if N <= 128 and not self.expand_path:   # the window read from the phase table
+            out = h.dcm_mpc_solve_phased(self.table, s, self.xi, self.omega[:, s:s + N],
+                                         self.params, warm=warm, out=self.bufs[s % 2],
+                                         lambda_out=True, stream=self.stream)
+        else:
+            w = h.dcm_phase_expand(self.table, s, self.dt, N, stream=self.stream)
+            w.update(xi_init=self.xi, omega=self.omega[:, s:s + N].contiguous())
+            out = h.dcm_mpc_solve(w, self.params, out=self.bufs[s % 2], warm=warm,
+                                  lambda_out=True, stream=self.stream)
         self.bufs[s % 2] = out
         h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=self.stream)
         # integrate(0, dt): the dynamics are time-invariant, and a fixed interval keeps the
