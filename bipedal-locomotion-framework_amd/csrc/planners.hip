@@ -23,7 +23,7 @@ namespace {
 
 constexpr int kHullBlock = 64;
 #ifndef BLF_HULL_U
-#define BLF_HULL_U 4
+#define BLF_HULL_U 8
 #endif
 constexpr int HU = BLF_HULL_U;   // facet pairs per lane in flight (phase 2)
 
