@@ -53,7 +53,7 @@ def main():
     xi0, om, vrp = rnd(B, 2), rnd(B, N) * 4 + 3, rnd(B, N, 2)
     out = torch.empty(B, N + 1, 2, dtype=torch.float64, device=dev)
     ms = timed(lambda: h.dcm_euler_rollout(xi0, om, vrp, 0.02, out=out))
-    report("dcm_rollout_kernel", B * (N * 40 + 16 + 16), ms, B * N, "problem-knots")
+    report("dcm_rollout_rows_kernel", B * (N * 40 + 16 + 16), ms, B * N, "problem-knots")
     del xi0, om, vrp, out
     # hull2d_hrep: 8 points per polygon, M = 8 rows
     P, M = 2 * 1024 * 1024, 8
