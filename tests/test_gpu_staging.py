@@ -149,3 +149,16 @@ def test_hull2d_ties_duplicates_nonfinite(handle, oracle):
         assert nf[i] == mo, i
         np.testing.assert_array_equal(A[i], Ao)
         np.testing.assert_array_equal(b[i], bo)
+
+
+@pytest.mark.parametrize("B,misalign", [(65, False), (130, True), (1, True), (64, False)])
+def test_contact_eval_tiles_and_alignment(handle, oracle, B, misalign):
+    """contact_eval_kernel's 64-contact LDS tiles: partial tiles, and inputs only 8-B aligned (the
+    three 16-B input streams fall back to slab_load)."""
+    from test_gpu_contact import contact_batch
+    prm, twist, pose, null = contact_batch(B, seed=B + 7)
+    out = handle.contact_model_eval(_d(prm, misalign=misalign), _d(twist, misalign=misalign),
+                                    _d(pose, misalign=misalign), _d(null, misalign=misalign))
+    ref = oracle.contact_eval_batch(prm, twist, pose, null)
+    for name, r in zip(("wrench", "autonomous", "control", "regressor"), ref):
+        np.testing.assert_array_equal(out[name].cpu().numpy(), r, err_msg=name)
