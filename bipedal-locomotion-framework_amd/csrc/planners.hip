@@ -348,6 +348,10 @@ __global__ __launch_bounds__(256) void quintic_fit_kernel(const double* __restri
 // one lane per (spline, query); the workgroup's [256][3][D] output slab is staged in LDS and
 // written with coalesced 16-B stores (slab.h)
 constexpr int kEvalBlock = 256;
+#ifndef BLF_Q_STAGE
+#define BLF_Q_STAGE 512
+#endif
+constexpr int kEvalStage = BLF_Q_STAGE;   // doubles of staged spline data per workgroup (4 KB)
 
 template <bool VEC>
 __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* __restrict__ kt,
@@ -358,18 +362,36 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
                                                                   int32_t* __restrict__ idx)
 {
     __shared__ double s_out[kEvalBlock * 9];
+    __shared__ __attribute__((aligned(16))) double s_spl[kEvalStage];   // the splines' knots + coefficients
     const int K = K1 - 1;
     const int W = 3 * D, SW = odd_stride(W);
     const int64_t g0 = (int64_t)blockIdx.x * kEvalBlock;
     const int64_t gid = g0 + threadIdx.x;
     const int rows = (int)((S * Q - g0) < kEvalBlock ? (S * Q - g0) : kEvalBlock);
+    // 32-bit division when the launch fits (every bench / test shape): the 64-bit one is a long
+    // VALU sequence per lane
+    const bool small = S * Q < 0x7fffffffLL;
+    auto spline_of = [&](int64_t g) { return small ? (int64_t)((uint32_t)g / (uint32_t)Q) : g / Q; };
+    // The workgroup's queries belong to a few consecutive splines (8-9 at 32 queries each), whose
+    // knots and coefficients are contiguous: staged once into LDS (coalesced, in flight together
+    // with the query times) instead of every lane gathering its segment from L2 after its knot
+    // search.  Larger spans read global memory as before.
+    const int64_t sp0 = spline_of(g0);
+    const int nsp = (int)(spline_of(g0 + rows - 1) - sp0 + 1);
+    const int ncf = nsp * K * D * 6, nkt = nsp * K1;
+    const bool staged = VEC && ncf + nkt <= kEvalStage;
+    double tt = 0.0;
+    if (gid < S * Q) tt = __builtin_nontemporal_load(tq + gid);   // streamed once
+    if (staged) {
+        const double2* gc = reinterpret_cast<const double2*>(coeffs + sp0 * K * D * 6);
+        double2* sc = reinterpret_cast<double2*>(s_spl + nkt + (nkt & 1));
+        for (int j = threadIdx.x; j < ncf / 2; j += kEvalBlock) sc[j] = gc[j];
+        for (int j = threadIdx.x; j < nkt; j += kEvalBlock) s_spl[j] = kt[sp0 * K1 + j];
+        __syncthreads();
+    }
     if (gid < S * Q) {
-        // 32-bit division when the launch fits (every bench / test shape): the 64-bit one is a
-        // long VALU sequence per lane
-        const int64_t sp = (S * Q < 0x7fffffffLL) ? (int64_t)((uint32_t)gid / (uint32_t)Q) : gid / Q;
-        const double* t = kt + sp * K1;
-        // the query times and knot indices are streamed once: non-temporal
-        const double tt = __builtin_nontemporal_load(tq + gid);
+        const int64_t sp = spline_of(gid);
+        const double* t = staged ? s_spl + (sp - sp0) * K1 : kt + sp * K1;
         // last j with t_j <= t: a forward pass keeps the knot loads independent of each other
         // (up to 8 knots all issued before the first comparison)
         int raw = -1;
@@ -388,10 +410,12 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
         const int seg = raw < 0 ? 0 : (raw > K - 1 ? K - 1 : raw);
         const double tau = tt - t[seg];
         double* o = s_out + threadIdx.x * SW;
+        const double* cbase = staged ? s_spl + nkt + (nkt & 1) + ((sp - sp0) * K + seg) * D * 6
+                                     : coeffs + (sp * K + seg) * D * 6;
         for (int d = 0; d < D; ++d) {
             // the segment's 6 coefficients are 48 contiguous bytes: three 16-B loads when the
             // array is 16-B aligned (VEC), six 8-B loads otherwise
-            const double* cp = coeffs + ((sp * K + seg) * D + d) * 6;
+            const double* cp = cbase + d * 6;
             double c0, c1, c2, c3, c4, c5;
             if (VEC) {
                 const double2* c = reinterpret_cast<const double2*>(cp);

@@ -74,18 +74,20 @@ def test_hull2d_sizes_and_tiles(handle, oracle, B, P_, M):
         np.testing.assert_array_equal(b[i], bo)
 
 
-@pytest.mark.parametrize("D,Q,S", [(1, 7, 33), (2, 40, 10), (3, 1, 300), (3, 256, 3)])
-def test_quintic_eval_dims_and_tiles(handle, oracle, D, Q, S):
-    rng = np.random.default_rng(D * 100 + Q)
-    K1 = 4
+@pytest.mark.parametrize("D,Q,S,K1", [(1, 7, 33, 4), (2, 40, 10, 4), (3, 1, 300, 4), (3, 256, 3, 4),
+                                      (3, 32, 40, 3), (2, 32, 17, 11), (3, 5, 60, 2)])
+def test_quintic_eval_dims_and_tiles(handle, oracle, D, Q, S, K1):
+    """Workgroups whose splines' knots and coefficients fit the LDS stage (<= 512 doubles) read
+    them from there, the others from global memory; both bit-exact against the oracle."""
+    rng = np.random.default_rng(D * 100 + Q + K1)
     kt = np.cumsum(rng.uniform(0.1, 0.5, (S, K1)), axis=1)
     kp = rng.normal(size=(S, K1, 3, D))
     tq = kt[:, :1] - 0.05 + (kt[:, -1:] - kt[:, :1] + 0.1) * rng.uniform(size=(S, Q))
-    tq[:, 0] = kt[:, 2]       # exactly on a knot
+    tq[:, 0] = kt[:, min(2, K1 - 1)]       # exactly on a knot
     coeffs = handle.quintic_fit(_d(kt), _d(kp))
     pva, idx = handle.quintic_eval(_d(kt), coeffs, _d(tq))
     cg, pg, ig = coeffs.cpu().numpy(), pva.cpu().numpy(), idx.cpu().numpy()
-    for s in sorted({0, S // 2, S - 1}):
+    for s in range(S):
         po, io = oracle.quintic_eval(kt[s], cg[s], tq[s])
         np.testing.assert_array_equal(ig[s], io)
         np.testing.assert_array_equal(pg[s], po)
