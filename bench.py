@@ -51,7 +51,7 @@ def profiled_summary():
         return None, None
     with open(files[-1]) as f:
         s = json.load(f)
-    if not any(n in s.get("dominant_kernel", "") for n in ("dcm_mpc_as", "dcm_mpc_ipm")):
+    if "dcm_mpc_" not in s.get("dominant_kernel", ""):   # the QP kernels (cold / warm / ipm)
         return None, None
     return s, os.path.relpath(files[-1], ROOT)
 
