@@ -173,6 +173,37 @@ int orc_fbk_euler_integrate(int n, double rho, double* pos, double* rot, double*
                             const double* twist, const double* joint_vel, double t0, double t1,
                             double dT);
 
+/* FloatingBaseDynamicalSystem::dynamics and its ForwardEuler with a joint impedance
+ * (blf_oracle_fbd.c; the C restatement of oracle/fb_dynamics.py).  n <= 40 joints. */
+typedef struct orc_fb_model {
+    int n;
+    const int32_t* parent;
+    const double* joint_origin;
+    const double* joint_rot;
+    const double* joint_axis;
+    const double* link_mass;
+    const double* link_com;
+    const double* link_inertia;
+    const int32_t* frame_link;
+    const double* frame_pose;
+    double gravity[3];
+    double rho;
+} orc_fb_model;
+int orc_fbd_dynamics(const orc_fb_model* m, const double* bpos, const double* brot, const double* q,
+                     const double* bvel, const double* qd, const double* tau, int ncontacts,
+                     const double* cparams, const double* null_poses, double* base_acc, double* joint_acc,
+                     double* dpos, double* drot, double* dq);
+int orc_fbd_euler_impedance(const orc_fb_model* m, double* bpos, double* brot, double* q, double* bvel,
+                            double* qd, const double* q_ref, const double* kp, const double* kd,
+                            int ncontacts, const double* cparams, const double* null_poses, double t0,
+                            double t1, double dT);
+int orc_fbd_euler_impedance_batch(const orc_fb_model* m, int64_t B, double* bpos, double* brot, double* q,
+                                  double* bvel, double* qd, const double* q_ref, const double* kp,
+                                  const double* kd, int ncontacts, const double* cparams,
+                                  const double* null_poses, double t0, double t1, double dT, int threads);
+void orc_fbd_com_batch(const orc_fb_model* m, int64_t B, const double* bpos, const double* brot,
+                       const double* q, const double* bvel, const double* qd, double* com);
+
 #ifdef __cplusplus
 }
 #endif

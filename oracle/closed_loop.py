@@ -91,7 +91,11 @@ class OracleLoop:
     """blf.closed_loop.ClosedLoop restated on the CPU (same inputs, same sequence)."""
 
     def __init__(self, model, plan, states, null_pose, law, contact_params, horizon=100, dT=0.001,
-                 tol_polish=1e-4):
+                 tol_polish=1e-4, compiled=False, threads=8):
+        """compiled: the rigid-body maps (centre of mass, the impedance-driven Euler steps) run the
+        C restatement (blf_oracle_fbd.c) on `threads` threads instead of numpy (bench.py's
+        configs[4] CPU baseline); the QP is the C oracle either way."""
+        self.compiled, self.threads = compiled, threads
         self.model, self.N, self.dT = model, horizon, dT
         self.dt = float(plan["dt"])
         self.law = law
@@ -109,16 +113,25 @@ class OracleLoop:
     def period(self):
         s, N = self.s, self.N
         omega = np.ascontiguousarray(self.omega[:, s:s + N])
-        com, xi = dcm_from_state(self.model, self.state, omega[:, 0])
+        if self.compiled:
+            com = O.fbd_com_batch(self.model, self.state)
+            xi = com[:, :2] + com[:, 3:5] / omega[:, 0][:, None]
+        else:
+            com, xi = dcm_from_state(self.model, self.state, omega[:, 0])
         w = O.dcm_phase_expand(self.table, s, self.dt, N)
         w.update(xi_init=xi, omega=omega)
         pv, pl = (None, None) if self.prev is None else (self.prev["vrp"], self.prev["lam"])
         pol = np.zeros(xi.shape[0], np.int32)
         st, xo, vrp, it, lam = O.dcm_mpc_solve_batch_warm(w, vrp_ws=pv, lam_ws=pl, shift=1, floor=1e-3,
-                                                          params=self.params, threads=8, polished=pol)
+                                                          params=self.params, threads=self.threads,
+                                                          polished=pol)
         q_ref = posture_reference(self.law, com, vrp)
         C = len(self.model["frame_link"])
-        for i in range(xi.shape[0]):
+        if self.compiled:
+            self.state = O.fbd_euler_impedance_batch(self.model, self.state, q_ref, self.law["kp"],
+                                                     self.law["kd"], self.cparams, self.null, 0.0,
+                                                     self.dt, self.dT, threads=self.threads)
+        for i in range(0 if self.compiled else xi.shape[0]):
             si = euler_integrate_impedance(self.model, self.state, i, q_ref[i], self.law["kp"],
                                            self.law["kd"], 0.0, self.dt, self.dT,
                                            contacts=list(range(C)), contact_params=self.cparams,

@@ -16,6 +16,13 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
 
 
+class OrcFbModel(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("parent", _ip), ("joint_origin", _dp), ("joint_rot", _dp),
+                ("joint_axis", _dp), ("link_mass", _dp), ("link_com", _dp), ("link_inertia", _dp),
+                ("frame_link", _ip), ("frame_pose", _dp), ("gravity", ctypes.c_double * 3),
+                ("rho", ctypes.c_double)]
+
+
 class OrcParams(ctypes.Structure):
     _fields_ = [("horizon", ctypes.c_int32), ("max_facets", ctypes.c_int32),
                 ("max_iter", ctypes.c_int32), ("sequential", ctypes.c_int32),
@@ -85,6 +92,12 @@ def lib():
         L.orc_fbk_euler_integrate.argtypes = [ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp,
                                               _dp, ctypes.c_double, ctypes.c_double,
                                               ctypes.c_double]
+        L.orc_fbd_euler_impedance_batch.restype = ctypes.c_int
+        L.orc_fbd_euler_impedance_batch.argtypes = [
+            ctypes.POINTER(OrcFbModel), ctypes.c_int64, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp,
+            ctypes.c_int, _dp, _dp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int]
+        L.orc_fbd_com_batch.argtypes = [ctypes.POINTER(OrcFbModel), ctypes.c_int64, _dp, _dp, _dp,
+                                        _dp, _dp, _dp]
         _LIB = L
     return _LIB
 
@@ -380,3 +393,55 @@ def fbk_euler_integrate(rho, pos, rot, joints, twist, joint_vel, t0, t1, dT):
     st = lib().orc_fbk_euler_integrate(n, rho, _d(pos), _d(rot), _d(jz), _d(twist), _d(jv),
                                        t0, t1, dT)
     return st, pos, rot.reshape(3, 3), joints
+
+
+def fbd_euler_impedance_batch(model, states, q_ref, kp, kd, contact_params, null_poses, t0, t1, dT,
+                              rho=0.01, gravity=(0.0, 0.0, -9.81), threads=1):
+    """C restatement (blf_oracle_fbd.c) of fb_dynamics / closed_loop.euler_integrate_impedance for
+    B robots: states dict of [B,...] arrays (base_pos, base_rot [B,3,3], joint_pos, base_vel,
+    joint_vel), q_ref [B,n], kp / kd [n], contact_params [C,4], null_poses [B,C,12].  Returns the
+    integrated states (new arrays)."""
+    keep = []
+
+    def arr(a, dt=np.float64):
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a
+    mdl = _fb_model(model, keep, rho, gravity)
+    out = {k: np.array(states[k], dtype=np.float64, copy=True)
+           for k in ("base_pos", "base_rot", "joint_pos", "base_vel", "joint_vel")}
+    B = out["base_pos"].shape[0]
+    cp, npz = arr(contact_params), arr(null_poses)
+    rc = lib().orc_fbd_euler_impedance_batch(
+        ctypes.byref(mdl), B, _d(out["base_pos"]), _d(out["base_rot"]), _d(out["joint_pos"]),
+        _d(out["base_vel"]), _d(out["joint_vel"]), _d(arr(q_ref)), _d(arr(kp)), _d(arr(kd)),
+        int(cp.shape[0]), _d(cp), _d(npz), t0, t1, dT, threads)
+    if rc:
+        raise RuntimeError(f"orc_fbd_euler_impedance_batch failed ({rc})")
+    return out
+
+
+def _fb_model(model, keep, rho=0.01, gravity=(0.0, 0.0, -9.81)):
+    def arr(a, dt=np.float64):
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a
+    return OrcFbModel(int(model["n"]), _i(arr(model["parent"], np.int32)),
+                      _d(arr(model["joint_origin"])), _d(arr(model["joint_rot"])),
+                      _d(arr(model["joint_axis"])), _d(arr(model["link_mass"])),
+                      _d(arr(model["link_com"])), _d(arr(model["link_inertia"])),
+                      _i(arr(model["frame_link"], np.int32)), _d(arr(model["frame_pose"])),
+                      (ctypes.c_double * 3)(*gravity), rho)
+
+
+def fbd_com_batch(model, states):
+    """C restatement of closed_loop.com_state for B robots: com [B,6] = (c, cdot)."""
+    keep = []
+    mdl = _fb_model(model, keep)
+    st = {k: np.ascontiguousarray(states[k], dtype=np.float64)
+          for k in ("base_pos", "base_rot", "joint_pos", "base_vel", "joint_vel")}
+    B = st["base_pos"].shape[0]
+    com = np.zeros((B, 6))
+    lib().orc_fbd_com_batch(ctypes.byref(mdl), B, _d(st["base_pos"]), _d(st["base_rot"]),
+                            _d(st["joint_pos"]), _d(st["base_vel"]), _d(st["joint_vel"]), _d(com))
+    return com

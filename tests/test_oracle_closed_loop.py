@@ -65,3 +65,48 @@ def test_standing_start_puts_the_soles_on_the_ground():
             assert abs(pf[2]) < 3e-3
     null = R.sole_null_poses(MODEL, st)
     assert null.shape == (3, 2, 12) and (null[:, :, 2] == 0).all()
+
+
+def test_c_fbd_restatement_matches_numpy():
+    """oracle/blf_oracle_fbd.c (the configs[4] CPU baseline's dynamics) against the numpy
+    restatement: 20 impedance-driven Euler steps with both soles in contact, to 1e-10."""
+    import oracle as O
+    from blf import closed_loop as DL
+    B = 4
+    st = R.standing_states(MODEL, B, seed=5)
+    st.pop("joint_torque", None)
+    law = R.posture_law_arrays(MODEL)
+    q_ref = np.random.default_rng(3).normal(size=(B, MODEL["n"])) * 0.02
+    null = R.sole_null_poses(MODEL, st)
+    cp = np.tile(np.asarray(DL.CONTACT_PARAMS), (2, 1))
+    got = O.fbd_euler_impedance_batch(MODEL, st, q_ref, law["kp"], law["kd"], cp, null, 0.0, 0.02,
+                                      0.001, threads=2)
+    for i in range(B):
+        ref = CL.euler_integrate_impedance(MODEL, st, i, q_ref[i], law["kp"], law["kd"], 0.0, 0.02,
+                                           0.001, contacts=[0, 1], contact_params=cp,
+                                           null_poses=null[i])
+        for k in ref:
+            if k == "joint_torque":
+                continue
+            err = np.abs(got[k][i] - ref[k]).max() / max(1.0, np.abs(ref[k]).max())
+            assert err <= 1e-10, (i, k, err)
+
+
+def test_compiled_oracle_loop_matches_numpy_loop():
+    """OracleLoop(compiled=True) (C centre of mass and dynamics, the configs[4] CPU baseline) runs
+    the same periods as the numpy composition, to 1e-9."""
+    from blf import closed_loop as DL
+    from blf import problems as P
+    N, B = 30, 3
+    plan = P.make_batch(B, horizon=N + 2, n_footsteps=4, seed=11, first_ds=12)
+    st = R.standing_states(MODEL, B, seed=4)
+    args = (MODEL, plan, st, R.sole_null_poses(MODEL, st), R.posture_law_arrays(MODEL),
+            DL.CONTACT_PARAMS)
+    a = CL.OracleLoop(*args, horizon=N)
+    b = CL.OracleLoop(*args, horizon=N, compiled=True, threads=2)
+    for _ in range(2):
+        ra, rb = a.period(), b.period()
+        np.testing.assert_array_equal(ra["status"], rb["status"])
+        np.testing.assert_allclose(rb["xi_init"], ra["xi_init"], rtol=0, atol=1e-9)
+        for k in a.state:
+            np.testing.assert_allclose(b.state[k], a.state[k], rtol=0, atol=1e-9)
