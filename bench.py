@@ -526,6 +526,47 @@ def pipeline_cpu(N, B=4096):
                       f"(oracle C batch drivers)"}
 
 
+def receding_cpu(N, tol_polish, B=4096, windows=20):
+    """The receding horizon on the CPU, a bounded sample: B plans advanced `windows` windows, each
+    window expanded from the phase table and solved warm from the previous one (the oracle's C
+    batch drivers on every thread this process may use, sequential recursions per problem)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from blf import problems as P
+    prob = P.make_batch(B, horizon=N + windows + 1, n_footsteps=8, seed=P.SEED)
+    threads = cpu_threads()
+    prm = O.default_params(N, sequential=1, tol_polish=tol_polish)
+    Bq, Pn, C = prob["phase_corners"].shape[:3]
+    A, b, nf = O.hull2d_hrep_batch(prob["phase_corners"].reshape(Bq * Pn, C, 2),
+                                   prob["phase_ncorners"].reshape(Bq * Pn), 8, threads=threads)
+    table = dict(nphases=prob["nphases"], phase_begin=prob["phase_begin"],
+                 phase_end=prob["phase_end"], phase_A=A.reshape(Bq, Pn, 8, 2),
+                 phase_b=b.reshape(Bq, Pn, 8), phase_nf=nf.reshape(Bq, Pn),
+                 phase_ref=prob["phase_ref"])
+    xi0, prev = prob["xi_init"], None
+
+    def window(s):
+        nonlocal xi0, prev
+        w = O.dcm_phase_expand_batch(table, s, prob["dt"], N, threads=threads)
+        w.update(xi_init=xi0, omega=np.ascontiguousarray(prob["omega"][:, s:s + N]))
+        pv, pl = (None, None) if prev is None else prev
+        st, xi, vrp, _, lam = O.dcm_mpc_solve_batch_warm(w, vrp_ws=pv, lam_ws=pl, shift=1,
+                                                         floor=1e-3, params=prm, threads=threads)
+        prev, xi0 = (vrp, lam), np.ascontiguousarray(xi[:, 1])
+        return st
+
+    window(0)   # the cold first window, untimed (the device bench also times warm windows only)
+    t0 = time.perf_counter()
+    for s in range(1, windows + 1):
+        st = window(s)
+    el = time.perf_counter() - t0
+    return {"value": B * windows / el, "unit": "QP/s", "cores": threads, "kind": "port",
+            "sample": f"{B} plans x {windows} warm windows in {el:.2f} s on {threads} threads "
+                      f"(phase expansion + warm solve per window, oracle C batch drivers, "
+                      f"sequential mode), {int((st != 0).sum())} unsolved in the last window"}
+
+
 def closed_loop_cpu(args, model, N, periods=3):
     """The CPU composition of the same loop, compiled: oracle/closed_loop.py OracleLoop with the C
     restatements of the centre of mass and of the impedance-driven floating-base dynamics
@@ -697,6 +738,8 @@ def receding_horizon(args, h, dev):
             "config": {"workload": f"batch={B} plans (8 footsteps, {Pn} phases), horizon={N}, "
                                    f"window moved one knot per step, warm start shift 1 floor 1e-3",
                        "batch_per_gpu": B}}
+    if not args.no_cpu:
+        line["cpu_baseline"] = receding_cpu(N, params.tol_polish)
     if args.expand_path:
         ex_ms = sorted(expand_ms)[len(expand_ms) // 2]
         ex_gbs = phase_expand_bytes(Pn, N, M) * B / (ex_ms * 1e-3) / 1e9
