@@ -72,37 +72,53 @@ constexpr int kComp = 16;   // subtree sum: spatial inertia 10 | spatial force 6
 constexpr int kCs = 16;     // contact scratch: point 3 | wrench 6 | link 1 | spatial wrench 6
 
 struct Smem {
-    double *link, *jrot, *jz, *jo, *comp, *sax, *rhs, *cscr, *st, *tq;
-    unsigned long long* anc;
+    // one base pointer (per system: the two halves of a wavefront have their own) and wave-uniform
+    // offsets, so the per-half base costs one address, not one per array
+    double* base;
+    int o_link, o_jrot, o_jz, o_jo, o_comp, o_sax, o_rhs, o_cscr, o_st, o_tq, o_anc;
     int ms;   // row stride of L (odd: the per-lane row accesses do not conflict)
     size_t total;
-    __host__ __device__ Smem(double* base, int n, int C)
+    __host__ __device__ Smem(double* b, int n, int C) : base(b)
     {
         const int L = n + 1, NV = n + 6;
         ms = NV | 1;
         size_t o = 0;
         auto take = [&](size_t k) {
-            double* p = base ? base + o : nullptr;
+            const int at = (int)o;
             o += (k + 1) & ~size_t(1);
-            return p;
+            return at;
         };
         // link records; after the mass matrix is assembled the same space holds L (NV rows)
         const size_t lk = (size_t)kLinkRec * L, lm = (size_t)NV * ms;
-        link = take(lk > lm ? lk : lm);
-        jrot = take(12 * (size_t)n);           // E_j Rot(a_j, s_j) (9) | E_j a_j (3)
-        jz = take(3 * (size_t)n);
-        jo = take(3 * (size_t)n);
+        o_link = take(lk > lm ? lk : lm);
+        o_jrot = take(12 * (size_t)n);           // E_j Rot(a_j, s_j) (9) | E_j a_j (3)
+        o_jz = take(3 * (size_t)n);
+        o_jo = take(3 * (size_t)n);
         // subtree sums [j] (joint j's subtree) and [n] (every link); later the pivot-column
         // buffers of the factorization (2 NV)
         const size_t cp = (size_t)kComp * (n + 1);
-        comp = take(cp > 2 * (size_t)NV ? cp : 2 * (size_t)NV);
-        sax = take(6 * (size_t)NV);
-        rhs = take((size_t)NV);
-        cscr = take((size_t)kCs * (C > 0 ? C : 1));
-        st = take(18 + 2 * (size_t)n + (size_t)NV + 9);   // Euler state (6 + n + 3 + 9 + n) + acc + dR
-        tq = take((size_t)n);                              // the joint impedance's torques
-        anc = reinterpret_cast<unsigned long long*>(take((size_t)L));
+        o_comp = take(cp > 2 * (size_t)NV ? cp : 2 * (size_t)NV);
+        o_sax = take(6 * (size_t)NV);
+        o_rhs = take((size_t)NV);
+        o_cscr = take((size_t)kCs * (C > 0 ? C : 1));
+        o_st = take(18 + 2 * (size_t)n + (size_t)NV + 9);   // Euler state (6 + n + 3 + 9 + n) + acc + dR
+        o_tq = take((size_t)n);                              // the joint impedance's torques
+        o_anc = take((size_t)L);
         total = o;
+    }
+    __device__ __forceinline__ double* link() const { return base + o_link; }
+    __device__ __forceinline__ double* jrot() const { return base + o_jrot; }
+    __device__ __forceinline__ double* jz() const { return base + o_jz; }
+    __device__ __forceinline__ double* jo() const { return base + o_jo; }
+    __device__ __forceinline__ double* comp() const { return base + o_comp; }
+    __device__ __forceinline__ double* sax() const { return base + o_sax; }
+    __device__ __forceinline__ double* rhs() const { return base + o_rhs; }
+    __device__ __forceinline__ double* cscr() const { return base + o_cscr; }
+    __device__ __forceinline__ double* st() const { return base + o_st; }
+    __device__ __forceinline__ double* tq() const { return base + o_tq; }
+    __device__ __forceinline__ unsigned long long* anc() const
+    {
+        return reinterpret_cast<unsigned long long*>(base + o_anc);
     }
 };
 
@@ -149,6 +165,31 @@ __device__ __forceinline__ double bcast(double v, int src)
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Systems per wavefront.  A model with NV = n + 6 <= 32 fits half a wavefront (lane hl < 32 owns
+// joint / row hl), so one wavefront integrates two systems side by side, one per half (HW = 32
+// lanes per system); larger models take the whole wavefront (HW = 64).  Every loop, mask and
+// broadcast below is per half; both halves run the same model, so their control flow is the same.
+template <int HW>
+struct Half {
+    int hl, half;   // lane within the system's half, and which half
+    __device__ __forceinline__ Half() : hl(threadIdx.x & (HW - 1)), half(HW == 64 ? 0 : (int)threadIdx.x / HW) {}
+    // a ballot restricted to this half (bit i = lane i of the half)
+    __device__ __forceinline__ unsigned long long ballot(bool p) const
+    {
+        const unsigned long long b = __ballot(p);
+        return HW == 64 ? b : (b >> (HW * half)) & ((1ull << HW) - 1);
+    }
+    // v of lane `src` of this half
+    __device__ __forceinline__ int shfl(int v, int src) const { return __shfl(v, HW * half + src, kWave); }
+    // v of lane k of this half, as a broadcast (v_readlane; two of them and a select for halves)
+    __device__ __forceinline__ double bcast_k(double v, int k) const
+    {
+        if (HW == 64) return bcast(v, k);
+        const double a = bcast(v, k), b = bcast(v, HW + k);
+        return half ? b : a;
+    }
+};
+
 // r[lane] of a register row (the diagonal entry of the lane's own row), compile-time indexed.
 template <int NVMAX>
 __device__ __forceinline__ double bcast_own_diag(const double* r, int lane)
@@ -169,9 +210,11 @@ struct Topo {
     unsigned long long cmask, bmask;
 };
 
+template <int HW>
 __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
 {
-    const int n = m.n, lane = threadIdx.x;
+    const Half<HW> H;
+    const int n = m.n, lane = H.hl;
     const bool jl = lane < n;
     Topo t;
     t.P = jl ? m.parent[lane] : 0;
@@ -183,8 +226,8 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
     int depth = 0, Q = t.P;
     for (int it = 0; it < n; ++it) {
         const bool up = jl && Q > 0;
-        if (!__ballot(up)) break;
-        const int q = __shfl(t.P, up ? Q - 1 : 0, kWave);
+        if (!__ballot(up)) break;   // both halves hold the same model
+        const int q = H.shfl(t.P, up ? Q - 1 : 0);
         if (up) {
             ++depth;
             an |= 1ull << (Q - 1);
@@ -192,17 +235,17 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
         }
     }
     t.depth = depth;
-    if (jl) S.anc[lane + 1] = an;
-    if (lane == 0) S.anc[0] = 0ull;
+    if (jl) S.anc()[lane + 1] = an;
+    if (lane == 0) S.anc()[0] = 0ull;
     t.cmask = 0ull;
     for (int j = 0; j < n; ++j) {
-        const unsigned long long b = __ballot(jl && t.P == j + 1);
+        const unsigned long long b = H.ballot(jl && t.P == j + 1);
         if (lane == j) t.cmask = b;
     }
-    t.bmask = __ballot(jl && t.P == 0);
+    t.bmask = H.ballot(jl && t.P == 0);
     int md = depth;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = HW / 2; off >= 1; off >>= 1) {
         const int q = __shfl_xor(md, off, kWave);
         md = q > md ? q : md;
     }
@@ -213,12 +256,13 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
 
 // Steps 1-2 of fbd_eval: per-joint rotations and forward kinematics (poses, mixed velocities,
 // nu_dot = 0 accelerations) of every link into the link records.
+template <int HW>
 __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, const double* bv,
                                                const double* jvel, const double* bp, const double* bR,
                                                const double* jp, const Topo& T)
 {
     const int n = m.n;
-    const int lane = threadIdx.x;
+    const int lane = Half<HW>().hl;
     const bool jl = lane < n;   // n <= 48 < 64: one joint per lane
     const int depth = T.depth, P = T.P, maxdepth = T.maxdepth;
     const double sd = jl ? jvel[lane] : 0.0;
@@ -239,7 +283,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
                 const double K2 = (K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c]) + K[3 * r + 2] * K[6 + c];
                 Rr[3 * r + c] = ((r == c ? 1.0 : 0.0) + sn * K[3 * r + c]) + c1 * K2;
             }
-        double* out = S.jrot + 12 * j;
+        double* out = S.jrot() + 12 * j;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
 #pragma unroll
@@ -249,7 +293,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
         }
     }
     if (lane == 0) {
-        double* b = S.link;
+        double* b = S.link();
         for (int i = 0; i < 9; ++i) b[kR + i] = bR[i];
         for (int i = 0; i < 3; ++i) {
             b[kP + i] = bp[i]; b[kV + i] = bv[i]; b[kW + i] = bv[3 + i];
@@ -265,11 +309,11 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
             // the parent link's record and this joint's rotation into registers first (the child
             // record's stores could otherwise alias them and delay the loads)
             double pr[24], Ej[12];
-            const double* prs = S.link + kLinkRec * P;
+            const double* prs = S.link() + kLinkRec * P;
 #pragma unroll
             for (int i = 0; i < 24; ++i) pr[i] = prs[i];
 #pragma unroll
-            for (int i = 0; i < 12; ++i) Ej[i] = S.jrot[12 * j + i];
+            for (int i = 0; i < 12; ++i) Ej[i] = S.jrot()[12 * j + i];
             const double o[3] = {T.o0, T.o1, T.o2};
             const double* RP = pr + kR;
             double cR[9], r[3], z[3];
@@ -287,15 +331,15 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
             cross3(pr + kW, zs, t2);           // w_P x z sd
             cross3(pr + kAl, r, t3);           // al_P x r
             cross3(pr + kW, t1, t4);           // w_P x (w_P x r)
-            double* cr = S.link + kLinkRec * (j + 1);
+            double* cr = S.link() + kLinkRec * (j + 1);
 #pragma unroll
             for (int i = 0; i < 9; ++i) cr[kR + i] = cR[i];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 const double pc = pr[kP + a] + r[a];
                 cr[kP + a] = pc;
-                S.jz[3 * j + a] = z[a];
-                S.jo[3 * j + a] = pc;
+                S.jz()[3 * j + a] = z[a];
+                S.jo()[3 * j + a] = pc;
                 cr[kW + a] = pr[kW + a] + zs[a];
                 cr[kV + a] = pr[kV + a] + t1[a];
                 cr[kAl + a] = pr[kAl + a] + t2[a];
@@ -307,29 +351,31 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
 }
 
 // One evaluation of the dynamics for the system whose state sits in LDS (bv, jv, bp, bR, jp).
-// Leaves the generalized acceleration in S.rhs and returns false if the factorization failed.
+// Leaves the generalized acceleration in S.rhs() and returns false if the factorization failed.
 // NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
 // registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
 // steps 6-9.
-template <int NVMAX>
+template <int NVMAX, int HW>
 __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
                                          const double* jvel, const double* bp, const double* bR,
                                          const double* jp, const double* tau, const Contacts& ct,
                                          int64_t sys, const double* reg, const Topo& T)
 {
+    static_assert(NVMAX <= HW, "a system's rows must fit its lanes");
+    const Half<HW> H;
     const int n = m.n, L = n + 1, NV = n + 6, MS = S.ms;
-    const int lane = threadIdx.x;
+    const int lane = H.hl;
     const bool jl = lane < n;   // n <= 48 < 64: one joint per lane
     const int depth = T.depth, maxdepth = T.maxdepth;
     FSTAMP(f_t0);
     FSTAMP(f_t1);
-    fbd_kinematics(m, S, bv, jvel, bp, bR, jp, T);
+    fbd_kinematics<HW>(m, S, bv, jvel, bp, bR, jp, T);
     FSTAMP_ADD(1, f_t1);
     FSTAMP(f_t2);
     // 3. per link: COM, world inertia, Newton-Euler force / moment, and the spatial inertia and
     //    force about the world origin (lane per link)
-    for (int l = lane; l < L; l += kWave) {
-        double* k = S.link + kLinkRec * l;
+    for (int l = lane; l < L; l += HW) {
+        double* k = S.link() + kLinkRec * l;
         const double* R = k + kR;
         const double* cl = m.com + 3 * l;
         const double* Ic = m.inertia + 9 * l;
@@ -380,10 +426,10 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     FSTAMP_ADD(2, f_t2);
     FSTAMP(f_t3);
     // 4. contacts: frame state + ContinuousContactModel wrench, and the wrench about the origin
-    for (int c = lane; c < ct.C; c += kWave) {
+    for (int c = lane; c < ct.C; c += HW) {
         const int f = ct.frame[c];
         const int l = m.flink[f];
-        const double* k = S.link + kLinkRec * l;
+        const double* k = S.link() + kLinkRec * l;
         const double* fp = m.fpose + 12 * f;
         const double* R = k + kR;
         double pose[12], tw[6], d[3], t1[3];
@@ -398,7 +444,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             tw[a] = k[kV + a] + t1[a];
             tw[3 + a] = k[kW + a];
         }
-        double* sc = S.cscr + kCs * c;
+        double* sc = S.cscr() + kCs * c;
         contact_wrench(ct.params + 4 * c, tw, pose, ct.null_pose + (sys * ct.C + c) * 12, sc + 3);
         sc[0] = pose[0]; sc[1] = pose[1]; sc[2] = pose[2];
         sc[9] = (double)l;
@@ -421,19 +467,19 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             const unsigned long long ch = lev >= 0 ? T.cmask : T.bmask;
             double acc[kComp];
 #pragma unroll
-            for (int p = 0; p < kComp; ++p) acc[p] = S.link[kLinkRec * l + kSI + p];
+            for (int p = 0; p < kComp; ++p) acc[p] = S.link()[kLinkRec * l + kSI + p];
             for (int c = 0; c < ct.C; ++c) {
-                const double* sc = S.cscr + kCs * c;
+                const double* sc = S.cscr() + kCs * c;
                 if ((int)sc[9] == l)
 #pragma unroll
                     for (int p = 10; p < kComp; ++p) acc[p] = acc[p] - sc[p];
             }
             for (unsigned long long b = ch; b; b &= b - 1) {
-                const double* cs = S.comp + kComp * __builtin_ctzll(b);
+                const double* cs = S.comp() + kComp * __builtin_ctzll(b);
 #pragma unroll
                 for (int p = 0; p < kComp; ++p) acc[p] = acc[p] + cs[p];
             }
-            double* dst = S.comp + kComp * (lev >= 0 ? lane : n);
+            double* dst = S.comp() + kComp * (lev >= 0 ? lane : n);
 #pragma unroll
             for (int p = 0; p < kComp; ++p) dst[p] = acc[p];
         }
@@ -443,7 +489,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     FSTAMP(f_t5);
     // 6. lane c: column axis S_c = (w, u) (to LDS), F_c = Ic S_c with Ic the subtree sum the
     //    column moves (registers), rhs_c = [tau] - S_c^T (subtree force)
-    const double* pB = S.link + kP;
+    const double* pB = S.link() + kP;
     double y = 0.0, Fc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     if (lane < NV) {
         const int c = lane;
@@ -455,15 +501,15 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             cross3(pB, w, u);
         } else {
             const int j = c - 6;
-            for (int a = 0; a < 3; ++a) w[a] = S.jz[3 * j + a];
-            cross3(S.jo + 3 * j, w, u);
+            for (int a = 0; a < 3; ++a) w[a] = S.jz()[3 * j + a];
+            cross3(S.jo() + 3 * j, w, u);
         }
-        const double* I = S.comp + kComp * (c < 6 ? n : c - 6);
+        const double* I = S.comp() + kComp * (c < 6 ? n : c - 6);
         double Iwv[3], hu[3], wh[3];
         sym_mv(I + 4, w, Iwv);
         cross3(I + 1, u, hu);
         cross3(w, I + 1, wh);
-        double* sa = S.sax + 6 * c;
+        double* sa = S.sax() + 6 * c;
         for (int a = 0; a < 3; ++a) {
             sa[a] = w[a];
             sa[3 + a] = u[a];
@@ -472,7 +518,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         }
         y = (c >= 6 ? tau[c - 6] : 0.0) - (dot3(w, I + 10) + dot3(u, I + 13));
     }
-    const unsigned long long myanc = (lane >= 6 && lane < NV) ? S.anc[lane - 5] : 0ull;
+    const unsigned long long myanc = (lane >= 6 && lane < NV) ? S.anc()[lane - 5] : 0ull;
     wave_sync();
     FSTAMP_ADD(5, f_t5);
     FSTAMP(f_t6);
@@ -483,7 +529,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     double r[NVMAX];
 #pragma unroll
     for (int j = 0; j < NVMAX; ++j) {
-        const double* sa = S.sax + 6 * (j < NV ? j : NV - 1);   // every lane reads the same S_j
+        const double* sa = S.sax() + 6 * (j < NV ? j : NV - 1);   // every lane reads the same S_j
         const double v = dot3(sa, Fc) + dot3(sa + 3, Fc + 3);
         const bool vis = j <= lane && lane < NV && (j < 6 || ((myanc >> (j - 6)) & 1ull));
         r[j] = vis ? v : 0.0;
@@ -501,14 +547,14 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
 #pragma unroll
     for (int k = 0; k < NVMAX; ++k) {
         if (k < NV) {
-            const double piv = bcast(r[k], k);
+            const double piv = H.bcast_k(r[k], k);
             ok = ok && (piv > 0.0);
             // 1 / sqrt(piv): v_rsq_f64 and one Newton step (the factorization's accuracy is that
             // of its rounding errors; parity with the oracle is at 1e-9)
             double isq = __builtin_amdgcn_rsq(piv);
             isq = isq * (1.5 - (0.5 * piv) * (isq * isq));
             r[k] = lane == k ? piv * isq : (lane > k ? r[k] * isq : r[k]);
-            double* col = S.comp + (k & 1) * NV;
+            double* col = S.comp() + (k & 1) * NV;
             if (lane < NV) col[lane] = r[k];
             wave_sync();
             // No row predicate: a lane above row j only updates its upper-triangle entry r[j],
@@ -530,11 +576,11 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
 #pragma unroll
     for (int k = 0; k < NVMAX; ++k) {   // k >= NV changes only lanes past the matrix
         y = lane == k ? y * idg : y;
-        const double xk = bcast(y, k);
+        const double xk = H.bcast_k(y, k);
         const double f = lane > k ? r[k] : 0.0;
         y = y - f * xk;
     }
-    double* Lm = S.link;
+    double* Lm = S.link();
     if (lane < NV)
 #pragma unroll
         for (int j = 0; j < NVMAX; ++j)
@@ -544,30 +590,35 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     for (int k = NV - 1; k >= 0; --k) {
         const double lnext = (k > 0 && lane < k - 1) ? Lm[MS * (k - 1) + lane] : 0.0;   // read ahead
         if (lane == k) y = y * idg;
-        const double xk = bcast(y, k);
+        const double xk = H.bcast_k(y, k);
         if (lane < k) y = y - lki * xk;
         lki = lnext;
     }
-    if (lane < NV) S.rhs[lane] = y;
+    if (lane < NV) S.rhs()[lane] = y;
     wave_sync();
     FSTAMP_ADD(8, f_t8);
     FSTAMP_ADD(9, f_t0);
     return ok;
 }
 
-template <int NVMAX>
+template <int NVMAX, int HW>
 __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state st,
                                                           const double* __restrict__ tau,
                                                           Contacts ct, const double* reg,
-                                                          blf_fb_state out)
+                                                          blf_fb_state out, int64_t batch)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    const Half<HW> H;
     const int n = m.n, NV = n + 6;
-    const Smem S(smem, n, ct.C);
-    const int64_t q = blockIdx.x;
-    const int lane = threadIdx.x;
-    double* loc = S.st;   // bv 6 | jv n | bp 3 | bR 9 | jp n
-    for (int i = lane; i < 18 + 2 * n; i += kWave) {
+    const Smem S(smem + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
+    // system of this half; a missing second system of the last wavefront recomputes the last one
+    // and writes nothing
+    const int64_t q0 = (int64_t)blockIdx.x * (kWave / HW) + H.half;
+    const bool active = q0 < batch;
+    const int64_t q = active ? q0 : batch - 1;
+    const int lane = H.hl;
+    double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n
+    for (int i = lane; i < 18 + 2 * n; i += HW) {
         double v;
         if (i < 6) v = st.base_vel[6 * q + i];
         else if (i < 6 + n) v = st.joint_vel[(int64_t)n * q + (i - 6)];
@@ -577,12 +628,13 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
         loc[i] = v;
     }
     wave_sync();
-    const Topo T = build_topo(m, S);
-    const bool ok = fbd_eval<NVMAX>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
-                                    tau + (int64_t)n * q, ct, q, reg, T);
+    const Topo T = build_topo<HW>(m, S);
+    const bool ok = fbd_eval<NVMAX, HW>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+                                        tau + (int64_t)n * q, ct, q, reg, T);
+    if (!active) return;
     const double nan = __builtin_nan("");
-    for (int c = lane; c < NV; c += kWave) {
-        const double a = ok ? S.rhs[c] : nan;
+    for (int c = lane; c < NV; c += HW) {
+        const double a = ok ? S.rhs()[c] : nan;
         if (c < 6) out.base_vel[6 * q + c] = a;
         else out.joint_vel[(int64_t)n * q + (c - 6)] = a;
     }
@@ -592,7 +644,7 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
         for (int i = 0; i < 3; ++i) out.base_pos[3 * q + i] = loc[i];
         for (int i = 0; i < 9; ++i) out.base_rot[9 * q + i] = dR[i];
     }
-    for (int j = lane; j < n; j += kWave) out.joint_pos[(int64_t)n * q + j] = loc[6 + j];
+    for (int j = lane; j < n; j += HW) out.joint_pos[(int64_t)n * q + j] = loc[6 + j];
 }
 
 // The joint impedance of blf_fbd_euler_integrate_impedance: tau = kp (q_ref - q) - kd qdot, set as
@@ -601,21 +653,27 @@ struct Impedance {
     const double *kp, *kd, *qref;
 };
 
-template <int NVMAX>
-__global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state st,
-                                                       const double* __restrict__ tau,
-                                                       Contacts ct, const double* reg,
-                                                       int32_t nsteps, double dT, double dT_last,
-                                                       Impedance imp)
+template <int NVMAX, int HW>
+// Two systems per wavefront (HW = 32) keep more state live per wave: capping it at 256 VGPRs for
+// two waves per SIMD spills (9.40 ms per c5 period), one wave per SIMD does not (8.29 ms, against
+// 9.29 ms with one system per wavefront at two waves per SIMD; tools/ab_c5.sh).
+__global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m, blf_fb_state st,
+                                                          const double* __restrict__ tau,
+                                                          Contacts ct, const double* reg,
+                                                          int32_t nsteps, double dT, double dT_last,
+                                                          Impedance imp, int64_t batch)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    const Half<HW> H;
     const int n = m.n, NV = n + 6;
-    const Smem S(smem, n, ct.C);
-    const int64_t q = blockIdx.x;
-    const int lane = threadIdx.x;
-    double* loc = S.st;   // bv 6 | jv n | bp 3 | bR 9 | jp n | dR 9
+    const Smem S(smem + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
+    const int64_t q0 = (int64_t)blockIdx.x * (kWave / HW) + H.half;
+    const bool active = q0 < batch;   // see fbd_dynamics_kernel
+    const int64_t q = active ? q0 : batch - 1;
+    const int lane = H.hl;
+    double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n | dR 9
     double* dR = loc + 18 + 2 * n;
-    for (int i = lane; i < 18 + 2 * n; i += kWave) {
+    for (int i = lane; i < 18 + 2 * n; i += HW) {
         double v;
         if (i < 6) v = st.base_vel[6 * q + i];
         else if (i < 6 + n) v = st.joint_vel[(int64_t)n * q + (i - 6)];
@@ -625,35 +683,36 @@ __global__ __launch_bounds__(64, 2) void fbd_euler_kernel(Model m, blf_fb_state 
         loc[i] = v;
     }
     wave_sync();
-    const Topo T = build_topo(m, S);
+    const Topo T = build_topo<HW>(m, S);
     bool ok = true;
     const double* tq = tau + (int64_t)n * q;
     for (int32_t step = 0; step < nsteps; ++step) {
         const double h = step + 1 < nsteps ? dT : dT_last;
         if (imp.kp) {   // the control input of this step from its start state
-            for (int j = lane; j < n; j += kWave)
-                S.tq[j] = imp.kp[j] * (imp.qref[(int64_t)n * q + j] - loc[18 + n + j]) - imp.kd[j] * loc[6 + j];
+            for (int j = lane; j < n; j += HW)
+                S.tq()[j] = imp.kp[j] * (imp.qref[(int64_t)n * q + j] - loc[18 + n + j]) - imp.kd[j] * loc[6 + j];
             wave_sync();
-            tq = S.tq;
+            tq = S.tq();
         }
-        ok = fbd_eval<NVMAX>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
-                             tq, ct, q, reg, T) && ok;
+        ok = fbd_eval<NVMAX, HW>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+                                 tq, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         wave_sync();
         // every element moves by its derivative at the start of the step (ForwardEuler.tpp:37-45):
         // positions first (they read the old velocities), then the velocities
-        for (int i = lane; i < 12 + n; i += kWave) {
+        for (int i = lane; i < 12 + n; i += HW) {
             // base position (3), base rotation (9), joint positions (n)
             if (i < 3) loc[6 + n + i] = loc[6 + n + i] + loc[i] * h;
             else if (i < 12) loc[6 + n + i] = loc[6 + n + i] + dR[i - 3] * h;
             else loc[18 + n + (i - 12)] = loc[18 + n + (i - 12)] + loc[6 + (i - 12)] * h;
         }
         wave_sync();
-        for (int i = lane; i < NV; i += kWave) loc[i] = loc[i] + S.rhs[i] * h;
+        for (int i = lane; i < NV; i += HW) loc[i] = loc[i] + S.rhs()[i] * h;
         wave_sync();
     }
+    if (!active) return;
     const double nan = __builtin_nan("");
-    for (int i = lane; i < 18 + 2 * n; i += kWave) {
+    for (int i = lane; i < 18 + 2 * n; i += HW) {
         const double v = ok ? loc[i] : nan;
         if (i < 6) st.base_vel[6 * q + i] = v;
         else if (i < 6 + n) st.joint_vel[(int64_t)n * q + (i - 6)] = v;
@@ -678,7 +737,7 @@ __global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, co
     const Smem S(smem, n, 0);
     const int64_t q = blockIdx.x;
     const int lane = threadIdx.x;
-    double* loc = S.st;   // bv 6 | jv n | bp 3 | bR 9 | jp n
+    double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n
     for (int i = lane; i < 18 + 2 * n; i += kWave) {
         double v;
         if (i < 6) v = st.base_vel[6 * q + i];
@@ -689,12 +748,12 @@ __global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, co
         loc[i] = v;
     }
     wave_sync();
-    const Topo T = build_topo(m, S);
-    fbd_kinematics(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n, T);
+    const Topo T = build_topo<kWave>(m, S);
+    fbd_kinematics<kWave>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n, T);
     wave_sync();
     double a[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // m c (3), m cdot (3), m
     if (lane < L) {
-        const double* k = S.link + kLinkRec * lane;
+        const double* k = S.link() + kLinkRec * lane;
         const double* R = k + kR;
         const double* cl = m.com + 3 * lane;
         double rc[3], t[3];
@@ -784,12 +843,12 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
     if (batch == 0) return BLF_OK;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
-    if (md->ndof + 6 <= 32)
-        hipLaunchKernelGGL(fbd_dynamics_kernel<32>, dim3((unsigned)batch), dim3(kWave), lds, s,
-                           to_model(md), *st, tau, c, reg, *out);
+    if (md->ndof + 6 <= 32)   // two systems per wavefront
+        hipLaunchKernelGGL((fbd_dynamics_kernel<32, 32>), dim3((unsigned)ceil_div(batch, 2)), dim3(kWave),
+                           2 * lds, s, to_model(md), *st, tau, c, reg, *out, batch);
     else
-        hipLaunchKernelGGL(fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6>, dim3((unsigned)batch),
-                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, *out);
+        hipLaunchKernelGGL((fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6, kWave>), dim3((unsigned)batch),
+                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, *out, batch);
     return check_hip(hipGetLastError(), "fbd_dynamics_kernel launch");
 }
 
@@ -803,13 +862,13 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     Impedance imp{nullptr, nullptr, nullptr};
     if (impedance) imp = Impedance{impedance->kp, impedance->kd, impedance->q_ref};
-    if (md->ndof + 6 <= 32)
-        hipLaunchKernelGGL(fbd_euler_kernel<32>, dim3((unsigned)batch), dim3(kWave), lds, s,
-                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp);
+    if (md->ndof + 6 <= 32)   // two systems per wavefront
+        hipLaunchKernelGGL((fbd_euler_kernel<32, 32>), dim3((unsigned)ceil_div(batch, 2)), dim3(kWave),
+                           2 * lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp, batch);
     else
-        hipLaunchKernelGGL(fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6>, dim3((unsigned)batch),
+        hipLaunchKernelGGL((fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave>), dim3((unsigned)batch),
                            dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last,
-                           imp);
+                           imp, batch);
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
 }
 

@@ -111,3 +111,29 @@ def test_fbd_errors(handle):
         with pytest.raises(native.BlfError) as e:
             handle.fbd_euler_integrate(dm, dst, tau, t0, t1, dT)
         assert e.value.code == code
+
+
+@pytest.mark.parametrize("B", [1, 3, 5])
+def test_fbd_two_systems_per_wavefront_odd_batches(handle, B):
+    """30-DoF systems run two per wavefront (one per half): odd batches leave the last wavefront
+    half empty; it must compute nothing visible (a sentinel row past the batch stays untouched)."""
+    st = robot.random_states(MODEL, B + 1, seed=40 + B)
+    host, dev = contacts_for(B + 1, seed=3)
+    dm = handle.fb_model(MODEL)
+    full = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    view = {k: v[:B] for k, v in full.items()}
+    sentinel = {k: v[B].clone() for k, v in full.items()}
+    cdev = dict(dev, null_pose=dev["null_pose"][:B])
+    out = handle.fbd_dynamics(dm, view, _d(st["joint_torque"][:B]), contacts=cdev)
+    handle.fbd_euler_integrate(dm, view, _d(st["joint_torque"][:B]), 0.0, 0.003, 0.001, contacts=cdev)
+    torch.cuda.synchronize()
+    for k in native.FB_STATE_KEYS:
+        assert torch.equal(full[k][B], sentinel[k]), k
+    acc = out["joint_vel"].cpu().numpy()
+    got = {k: v.cpu().numpy() for k, v in view.items()}
+    for i in range(B):
+        kw = dict(contacts=host["frame"], contact_params=host["params"], null_poses=host["null_pose"][i])
+        assert rel_err(acc[i], F.dynamics(MODEL, st, i, **kw)[1]) < TOL
+        ref = F.euler_integrate(MODEL, st, i, 0.0, 0.003, 0.001, **kw)
+        for k in native.FB_STATE_KEYS:
+            assert rel_err(got[k][i], ref[k]) < TOL, (i, k)
