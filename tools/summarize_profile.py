@@ -17,6 +17,51 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def occupancy(d, avg_ns):
+    """Achieved residency of the dominant kernel: SQ_WAVE_CYCLES (counted in units of 4 cycles on
+    gfx9) over the chip's SIMD cycles in the kernel time, i.e. waves resident per SIMD on
+    average, next to the compile-time limit (tools/kernel_resources)."""
+    wc = d.get("SQ_WAVE_CYCLES", {}).get("mean_per_dispatch")
+    if wc is None:
+        return None
+    return {"waves_per_simd_achieved": 4.0 * wc / (SIMDS * CLOCK_HZ * avg_ns * 1e-9),
+            "note": "SQ_WAVE_CYCLES x 4 / (1024 SIMDs x 2.4 GHz x kernel time); the tail of the "
+                    "last round of workgroups lowers the average"}
+
+
+def resources():
+    """Compile-time VGPRs / spills / occupancy of the QP kernels (hipcc -Rpass-analysis)."""
+    import re
+    import subprocess
+    src = os.path.join(ROOT, "bipedal-locomotion-framework_amd", "csrc", "dcm_mpc_as.hip")
+    try:
+        out = subprocess.run(
+            ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+             "-ffp-contract=off", "-I" + os.path.join(ROOT, "include"),
+             "-I" + os.path.dirname(src), "-c", src, "-o", os.devnull, "--cuda-device-only",
+             "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=600).stderr
+    except (OSError, subprocess.SubprocessError):
+        return None
+    res, cur = {}, None
+    for line in out.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            res[cur] = {}
+            continue
+        m = re.search(r"remark:\s+(VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|"
+                      r"VGPRs Spill|LDS Size \[bytes/block\]): (\d+)", line)
+        if m and cur:
+            key = {"VGPRs Spill": "vgpr_spill", "ScratchSize [bytes/lane]": "scratch_bytes_per_lane",
+                   "Occupancy [waves/SIMD]": "occupancy_waves_per_simd",
+                   "LDS Size [bytes/block]": "static_lds_bytes"}.get(m.group(1), m.group(1).lower())
+            res[cur][key] = int(m.group(2))
+    keep = {k: v for k, v in res.items() if "dcm_mpc_cold_kernelILi2ELb0ELb0E" in k
+            or "dcm_mpc_warm_kernelILi2ELb1ELb0E" in k}
+    return {("dcm_mpc_cold_kernel<2> (c2)" if "cold" in k else "dcm_mpc_warm_kernel<2> (rh)"): v
+            for k, v in keep.items()}
+
+
 def counters(path):
     out = collections.defaultdict(lambda: collections.defaultdict(list))
     if not os.path.exists(path):
@@ -82,6 +127,8 @@ def main():
                     "(Infinity-Cache hits included); gfx950 FETCH_SIZE reads 1/2 of wide "
                     "coalesced stream bytes (MI355X_MICROARCH.md HBM section)"},
         "valu_issue": valu_issue(d, float(stats[dom]["AverageNs"])),
+        "occupancy": occupancy(d, float(stats[dom]["AverageNs"])),
+        "kernel_resources": resources(),
         "kernel_avg_ns": {k: float(v["AverageNs"]) for k, v in stats.items()},
         "pmc_per_kernel": pmc,
     }
