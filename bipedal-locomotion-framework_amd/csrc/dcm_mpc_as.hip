@@ -125,20 +125,45 @@ __device__ __forceinline__ Row<T> normal(const LdsRows<V>& R, int i, int col)
 // identity (Riccati).
 
 // Backward affine scan v_k = G_k v_{k+1} + c_k, v_N = 0.  Returns v_{k+1} per slot.
+// pad (KPL = 2, N <= 126): lane 63 holds no knot, so it carries the zero element (affine scans) or
+// the identity (Riccati) at every level.  A lane whose partner would lie past the wavefront then
+// combines with lane 63 instead of being masked: the combine leaves its vector part unchanged
+// (signed zeros aside; the oracle's pair tree does the same), and the level needs no exec mask,
+// no branch and no write-back of temporaries (0.141 -> 0.133 ms at B = 4096).
+__device__ __forceinline__ bool as_pad(int KPL, int N) { return KPL == 2 && N <= 2 * kWave - 2; }
+
+// The kernels are instantiated per as_pad value (PAD) and tell the compiler which one holds, so
+// every scan's pad test folds and only one of its two loops is emitted.
+template <int KPL, bool PAD>
+__device__ __forceinline__ void assume_pad(int N)
+{
+    if (KPL == 2) __builtin_assume(PAD == (N <= 2 * kWave - 2));
+}
+
 template <int KPL, class T>
 __device__ __forceinline__ void as_scan_backward(const T (&G)[KPL][4], const T (&c)[KPL][2], int lane,
-                                                 T (&vn)[KPL][2])
+                                                 T (&vn)[KPL][2], bool pad)
 {
     T g0 = G[0][0], g1 = G[0][1], g2 = G[0][2], g3 = G[0][3], e0 = c[0][0], e1 = c[0][1];
     if constexpr (KPL == 2)   // knot 2l after knot 2l + 1
         COMPOSE(g0, g1, g2, g3, G[1][0], G[1][1], G[1][2], G[1][3], c[1][0], c[1][1], e0, e1);
     const int ln = opaque(lane);
+    if (KPL == 2 && pad) {
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const int ad = ((ln + d) & (kWave - 1)) << 2;
-        const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
-        const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
-        if (ln + d < kWave) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int ad = min(ln + d, kWave - 1) << 2;
+            const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
+            const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
+            COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
+    } else {
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int ad = ((ln + d) & (kWave - 1)) << 2;
+            const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
+            const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
+            if (ln + d < kWave) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
     }
     // e = v at this lane's first knot; the next lane's = v past this lane's last knot
     const int a1 = ((ln + 1) & (kWave - 1)) << 2;
@@ -161,19 +186,29 @@ __device__ __forceinline__ void as_scan_backward(const T (&G)[KPL][4], const T (
 // Forward affine scan x_{k+1} = F_k x_k + f_k, x_0 = 0.  Returns x_{k+1} and x_k per slot.
 template <int KPL, class T>
 __device__ __forceinline__ void as_scan_forward(const T (&F)[KPL][4], const T (&f)[KPL][2], int lane,
-                                                T (&x)[KPL][2], T (&xk)[KPL][2])
+                                                T (&x)[KPL][2], T (&xk)[KPL][2], bool pad)
 {
     constexpr int L = KPL - 1;   // the lane's last knot
     T g0 = F[L][0], g1 = F[L][1], g2 = F[L][2], g3 = F[L][3], e0 = f[L][0], e1 = f[L][1];
     if constexpr (KPL == 2)   // knot 2l + 1 after knot 2l
         COMPOSE(g0, g1, g2, g3, F[0][0], F[0][1], F[0][2], F[0][3], f[0][0], f[0][1], e0, e1);
     const int ln = opaque(lane);
+    if (KPL == 2 && pad) {   // lanes before the first partner take lane 63's zero element (as_pad)
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const int ad = ((ln - d) & (kWave - 1)) << 2;
-        const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
-        const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
-        if (ln >= d) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int ad = (ln >= d ? ln - d : kWave - 1) << 2;
+            const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
+            const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
+            COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
+    } else {
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int ad = ((ln - d) & (kWave - 1)) << 2;
+            const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
+            const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
+            if (ln >= d) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
     }
     // e = x past this lane's last knot; the previous lane's = x at this lane's first knot
     const int a1 = ((ln - 1) & (kWave - 1)) << 2;
@@ -259,14 +294,25 @@ __device__ __forceinline__ bool as_riccati(AKnotT<T> (&K)[KPL], const PT<T>& P, 
         ok = rc_combine(e, e1) && ok;
     }
     const int ln = opaque(lane);
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const int ad = ((ln + d) & (kWave - 1)) << 2;
-        RcT<T> q;
+    auto level = [&](int ad, RcT<T>& q) {
         q.a0 = bperm(ad, e.a0); q.a1 = bperm(ad, e.a1); q.a2 = bperm(ad, e.a2); q.a3 = bperm(ad, e.a3);
         q.g0 = bperm(ad, e.g0); q.g1 = bperm(ad, e.g1); q.g2 = bperm(ad, e.g2);
         q.h0 = bperm(ad, e.h0); q.h1 = bperm(ad, e.h1); q.h2 = bperm(ad, e.h2);
-        if (ln + d < kWave) ok = rc_combine(e, q) && ok;
+    };
+    if (as_pad(KPL, N)) {   // past the wavefront: lane 63's identity (as_pad)
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            RcT<T> q;
+            level(min(ln + d, kWave - 1) << 2, q);
+            ok = rc_combine(e, q) && ok;
+        }
+    } else {
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            RcT<T> q;
+            level(((ln + d) & (kWave - 1)) << 2, q);
+            if (ln + d < kWave) ok = rc_combine(e, q) && ok;
+        }
     }
     // P at this lane's first knot; the next lane's (terminal past the last lane)
     T P00, P01, P11;
@@ -337,7 +383,7 @@ __device__ __forceinline__ void as_solve(const AKnotT<T> (&K)[KPL], const T (&g)
     for (int j = 0; j < KPL; ++j) {
         Gt[j][0] = G[j][0]; Gt[j][1] = G[j][2]; Gt[j][2] = G[j][1]; Gt[j][3] = G[j][3];
     }
-    as_scan_backward<KPL, T>(G, c, lane, vn);
+    as_scan_backward<KPL, T>(G, c, lane, vn, as_pad(KPL, N));
     T k[KPL][2], f[KPL][2];
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
@@ -355,7 +401,7 @@ __device__ __forceinline__ void as_solve(const AKnotT<T> (&K)[KPL], const T (&g)
         }
     }
     T xk[KPL][2];
-    as_scan_forward<KPL, T>(Gt, f, lane, dx, xk);
+    as_scan_forward<KPL, T>(Gt, f, lane, dx, xk, as_pad(KPL, N));
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
         const AKnotT<T>& Kj = K[j];
@@ -927,7 +973,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
 // when none certifies, the fp64 LQ optimum from (xi_ref, vrp_ref) becomes the IPM's start point.
 // Measured alternatives: float rows in LDS with phase B reading fp64 rows from
 // global memory, at 2 / 3 / 4 waves per SIMD, and phase A as a kernel of its own — all slower.
-template <int KPL, bool LAMOUT, bool PH>
+template <int KPL, bool LAMOUT, bool PH, bool PAD>
 __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -938,6 +984,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
+    assume_pad<KPL, PAD>(N);
     const int NH = (N + KPL - 1) / KPL;
     const int S = KPL * NH;
     double* A2d = smem;                               // [M][S] double2 normals
@@ -1097,7 +1144,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
 // One wavefront per QP, fp64 facet rows in LDS.  From the shifted previous solution (xi rolled
 // out from its VRPs), guess = the facets the rollout violates plus those whose previous multiplier
 // exceeds the floor, then the fp64 passes (1.7 per window on average: no float search first).
-template <int KPL, bool LAMOUT, bool PH>
+template <int KPL, bool LAMOUT, bool PH, bool PAD>
 __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1110,6 +1157,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
+    assume_pad<KPL, PAD>(N);
     const int NH = (N + KPL - 1) / KPL;   // lanes holding knots
     const int S = KPL * NH;               // LDS row stride: facet i of slot j, lane l at i S + j NH + l
     double2* A2 = reinterpret_cast<double2*>(smem);   // [M][S] facet normals
@@ -1235,7 +1283,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
             const double ga = k < N ? K[j].al : 0.0;
             g[j][0] = ga; g[j][1] = 0.0; g[j][2] = 0.0; g[j][3] = ga;
         }
-        as_scan_forward<KPL, double>(g, f, lane, x, xk);
+        as_scan_forward<KPL, double>(g, f, lane, x, xk, as_pad(KPL, N));
 #pragma unroll
         for (int j = 0; j < KPL; ++j) {
             K[j].x0 = x[j][0];
@@ -1291,16 +1339,25 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     const size_t lds = 3 * sizeof(double) * slots + (ps ? ph_lds_bytes(ps->P, kp.N) : 0) + AS_EXTRA_LDS;
     if (lds > 64 * 1024)
         return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: %zu B of LDS (%d phases)", lds, ps ? ps->P : 0);
+    const bool pad = KPL == 2 && kp.N <= 2 * kWave - 2;
     if (warm == nullptr) {
-        auto kern = ps ? (lam_out ? dcm_mpc_cold_kernel<KPL, true, true> : dcm_mpc_cold_kernel<KPL, false, true>)
-                       : (lam_out ? dcm_mpc_cold_kernel<KPL, true, false> : dcm_mpc_cold_kernel<KPL, false, false>);
+#define AS_COLD(L, H, D) dcm_mpc_cold_kernel<KPL, L, H, D>
+        auto kern = pad ? (ps ? (lam_out ? AS_COLD(true, true, true) : AS_COLD(false, true, true))
+                              : (lam_out ? AS_COLD(true, false, true) : AS_COLD(false, false, true)))
+                        : (ps ? (lam_out ? AS_COLD(true, true, false) : AS_COLD(false, true, false))
+                              : (lam_out ? AS_COLD(true, false, false) : AS_COLD(false, false, false)));
+#undef AS_COLD
         hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds, s, kp,
                            pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, sol->xi,
                            sol->vrp, sol->status, sol->iters, sol->polished, lam_out, src);
         return check_hip(hipGetLastError(), "dcm_mpc_cold_kernel launch");
     }
-    auto kern = ps ? (lam_out ? dcm_mpc_warm_kernel<KPL, true, true> : dcm_mpc_warm_kernel<KPL, false, true>)
-                   : (lam_out ? dcm_mpc_warm_kernel<KPL, true, false> : dcm_mpc_warm_kernel<KPL, false, false>);
+#define AS_WARM(L, H, D) dcm_mpc_warm_kernel<KPL, L, H, D>
+    auto kern = pad ? (ps ? (lam_out ? AS_WARM(true, true, true) : AS_WARM(false, true, true))
+                          : (lam_out ? AS_WARM(true, false, true) : AS_WARM(false, false, true)))
+                    : (ps ? (lam_out ? AS_WARM(true, true, false) : AS_WARM(false, true, false))
+                          : (lam_out ? AS_WARM(true, false, false) : AS_WARM(false, false, false)));
+#undef AS_WARM
     hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, warm->vrp,
                        warm->lambda, sol->xi, sol->vrp, sol->status, sol->iters, sol->polished, lam_out, src);

@@ -403,11 +403,13 @@ static void scan_backward_pairs(dcm_ws* w, const double* G, const double* c)
         for (int j = 0; j < 2; ++j) cc[j] = k1 < N ? c[2 * k1 + j] : 0.0;
         aff_compose(g[l], e[l], b, cc);            /* knot 2l after knot 2l + 1 */
     }
+    const int pad = N <= 2 * WV - 2;   /* lane WV - 1 holds no knot: its zero element (kernel as_pad) */
     for (int dd = 1; dd < WV; dd <<= 1) {
         for (int l = 0; l < WV; ++l) {
             memcpy(ng[l], g[l], sizeof(ng[l]));
             memcpy(ne[l], e[l], sizeof(ne[l]));
             if (l + dd < WV) aff_compose(ng[l], ne[l], g[l + dd], e[l + dd]);
+            else if (pad) aff_compose(ng[l], ne[l], g[WV - 1], e[WV - 1]);
         }
         memcpy(g, ng, sizeof(g));
         memcpy(e, ne, sizeof(e));
@@ -453,11 +455,13 @@ static void scan_forward_pairs(dcm_ws* w, const double* F, int transpose, const 
         memcpy(e[l], fk[1], sizeof(e[l]));
         aff_compose(g[l], e[l], Fk[0], fk[0]);     /* knot 2l + 1 after knot 2l */
     }
+    const int pad = N <= 2 * WV - 2;   /* lanes before their partner take lane WV - 1's zero element */
     for (int dd = 1; dd < WV; dd <<= 1) {
         for (int l = 0; l < WV; ++l) {
             memcpy(ng[l], g[l], sizeof(ng[l]));
             memcpy(ne[l], e[l], sizeof(ne[l]));
             if (l - dd >= 0) aff_compose(ng[l], ne[l], g[l - dd], e[l - dd]);
+            else if (pad) aff_compose(ng[l], ne[l], g[WV - 1], e[WV - 1]);
         }
         memcpy(g, ng, sizeof(g));
         memcpy(e, ne, sizeof(e));
@@ -766,10 +770,15 @@ static int riccati_sweep_pairs(dcm_ws* w)
         rc_knot(w, 2 * l + 1, &e1);
         if (!rc_combine(&e[l], &e1)) ok = 0;
     }
+    const int pad = N <= 2 * WV - 2;   /* lane WV - 1 holds no knot: the identity (kernel as_pad) */
     for (int dd = 1; dd < WV; dd <<= 1) {
         for (int l = 0; l < WV; ++l) {
             ne[l] = e[l];
-            if (l + dd < WV && !rc_combine(&ne[l], &e[l + dd])) ok = 0;
+            if (l + dd < WV) {
+                if (!rc_combine(&ne[l], &e[l + dd])) ok = 0;
+            } else if (pad && !rc_combine(&ne[l], &e[WV - 1])) {
+                ok = 0;
+            }
         }
         memcpy(e, ne, sizeof(e));
     }

@@ -157,10 +157,15 @@ static int riccati32(s32* s, const float (*E)[3])
             if (!rcf_combine(&e[l], &e1)) ok = 0;
         }
     }
+    const int pad = KPL == 2 && N <= 2 * WV - 2;   /* the kernel's as_pad: lane WV - 1's identity */
     for (int d = 1; d < WV; d <<= 1) {
         for (int l = 0; l < WV; ++l) {
             ne[l] = e[l];
-            if (l + d < WV && !rcf_combine(&ne[l], &e[l + d])) ok = 0;
+            if (l + d < WV) {
+                if (!rcf_combine(&ne[l], &e[l + d])) ok = 0;
+            } else if (pad && !rcf_combine(&ne[l], &e[WV - 1])) {
+                ok = 0;
+            }
         }
         memcpy(e, ne, sizeof(e));
     }
@@ -216,11 +221,13 @@ static void scan_backward32(const s32* s, float (*G)[4], float (*c)[2], float (*
         memcpy(e[l], c[KPL * l], sizeof(e[l]));
         if (KPL == 2) compose(g[l], e[l], G[2 * l + 1], c[2 * l + 1]);
     }
+    const int pad = KPL == 2 && N <= 2 * WV - 2;   /* lane WV - 1's zero element (kernel as_pad) */
     for (int d = 1; d < WV; d <<= 1) {
         for (int l = 0; l < WV; ++l) {
             memcpy(ng[l], g[l], sizeof(ng[l]));
             memcpy(ne[l], e[l], sizeof(ne[l]));
             if (l + d < WV) compose(ng[l], ne[l], g[l + d], e[l + d]);
+            else if (pad) compose(ng[l], ne[l], g[WV - 1], e[WV - 1]);
         }
         memcpy(g, ng, sizeof(g));
         memcpy(e, ne, sizeof(e));
@@ -262,11 +269,13 @@ static void scan_forward32(const s32* s, float (*F)[4], float (*f)[2], float (*x
         memcpy(e[l], f[KPL * l + L], sizeof(e[l]));
         if (KPL == 2) compose(g[l], e[l], F[2 * l], f[2 * l]);
     }
+    const int pad = KPL == 2 && N <= 2 * WV - 2;   /* lane WV - 1's zero element (kernel as_pad) */
     for (int d = 1; d < WV; d <<= 1) {
         for (int l = 0; l < WV; ++l) {
             memcpy(ng[l], g[l], sizeof(ng[l]));
             memcpy(ne[l], e[l], sizeof(ne[l]));
             if (l >= d) compose(ng[l], ne[l], g[l - d], e[l - d]);
+            else if (pad) compose(ng[l], ne[l], g[WV - 1], e[WV - 1]);
         }
         memcpy(g, ng, sizeof(g));
         memcpy(e, ne, sizeof(e));

@@ -121,7 +121,7 @@ def _bitwise_vs_oracle(handle, oracle, host, params=None, oparams=None):
     return st_o, it_o
 
 
-@pytest.mark.parametrize("horizon", [63, 64, 65, 127, 128, 129, 200, 256, 300])
+@pytest.mark.parametrize("horizon", [63, 64, 65, 126, 127, 128, 129, 200, 256, 300])
 def test_dcm_mpc_wavefront_boundaries(handle, oracle, horizon):
     """Horizons around the 64-knot wavefront boundaries and multi-wavefront workgroups (the
     scans' cross-wavefront steps, padding wavefronts of the 256 / 512-thread variants)."""
@@ -236,7 +236,7 @@ def test_dcm_mpc_polish_refusal_matches_oracle_bitwise(handle, oracle):
     np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)
 
 
-@pytest.mark.parametrize("horizon,footsteps", [(100, 6), (50, 4), (128, 8), (65, 4)])
+@pytest.mark.parametrize("horizon,footsteps", [(100, 6), (50, 4), (128, 8), (126, 8), (65, 4)])
 def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, footsteps, monkeypatch):
     """The default path for N <= 128 (csrc/dcm_mpc_as.hip: one wavefront per QP, knot pairs per
     lane, then the IPM kernel's stage 2 on the QPs it hands over) and the IPM kernel alone
