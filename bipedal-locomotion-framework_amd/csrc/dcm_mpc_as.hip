@@ -149,16 +149,26 @@ __device__ __forceinline__ void as_scan_backward(const T (&G)[KPL][4], const T (
         COMPOSE(g0, g1, g2, g3, G[1][0], G[1][1], G[1][2], G[1][3], c[1][0], c[1][1], e0, e1);
     const int ln = opaque(lane);
     if (KPL == 2 && pad) {
+        {   // d = 1 (DPP)
+            const T p0 = dpp1<kNextKeep>(g0), p1 = dpp1<kNextKeep>(g1), p2 = dpp1<kNextKeep>(g2);
+            const T p3 = dpp1<kNextKeep>(g3), q0 = dpp1<kNextKeep>(e0), q1 = dpp1<kNextKeep>(e1);
+            COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
 #pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
+        for (int d = 2; d < kWave; d <<= 1) {
             const int ad = min(ln + d, kWave - 1) << 2;
             const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
             const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
             COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
         }
     } else {
+        {
+            const T p0 = dpp1<kNextWrap>(g0), p1 = dpp1<kNextWrap>(g1), p2 = dpp1<kNextWrap>(g2);
+            const T p3 = dpp1<kNextWrap>(g3), q0 = dpp1<kNextWrap>(e0), q1 = dpp1<kNextWrap>(e1);
+            if (ln + 1 < kWave) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
 #pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
+        for (int d = 2; d < kWave; d <<= 1) {
             const int ad = ((ln + d) & (kWave - 1)) << 2;
             const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
             const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
@@ -166,8 +176,7 @@ __device__ __forceinline__ void as_scan_backward(const T (&G)[KPL][4], const T (
         }
     }
     // e = v at this lane's first knot; the next lane's = v past this lane's last knot
-    const int a1 = ((ln + 1) & (kWave - 1)) << 2;
-    T vb0 = bperm(a1, e0), vb1 = bperm(a1, e1);
+    T vb0 = dpp1<kNextWrap>(e0), vb1 = dpp1<kNextWrap>(e1);
     if (lane == kWave - 1) {
         vb0 = T(0);
         vb1 = T(0);
@@ -194,16 +203,26 @@ __device__ __forceinline__ void as_scan_forward(const T (&F)[KPL][4], const T (&
         COMPOSE(g0, g1, g2, g3, F[0][0], F[0][1], F[0][2], F[0][3], f[0][0], f[0][1], e0, e1);
     const int ln = opaque(lane);
     if (KPL == 2 && pad) {   // lanes before the first partner take lane 63's zero element (as_pad)
+        {   // d = 1 (DPP; lane 0 takes lane 63's)
+            const T p0 = dpp1<kPrevWrap>(g0), p1 = dpp1<kPrevWrap>(g1), p2 = dpp1<kPrevWrap>(g2);
+            const T p3 = dpp1<kPrevWrap>(g3), q0 = dpp1<kPrevWrap>(e0), q1 = dpp1<kPrevWrap>(e1);
+            COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
 #pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
+        for (int d = 2; d < kWave; d <<= 1) {
             const int ad = (ln >= d ? ln - d : kWave - 1) << 2;
             const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
             const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
             COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
         }
     } else {
+        {
+            const T p0 = dpp1<kPrevWrap>(g0), p1 = dpp1<kPrevWrap>(g1), p2 = dpp1<kPrevWrap>(g2);
+            const T p3 = dpp1<kPrevWrap>(g3), q0 = dpp1<kPrevWrap>(e0), q1 = dpp1<kPrevWrap>(e1);
+            if (ln >= 1) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+        }
 #pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
+        for (int d = 2; d < kWave; d <<= 1) {
             const int ad = ((ln - d) & (kWave - 1)) << 2;
             const T p0 = bperm(ad, g0), p1 = bperm(ad, g1), p2 = bperm(ad, g2), p3 = bperm(ad, g3);
             const T q0 = bperm(ad, e0), q1 = bperm(ad, e1);
@@ -211,8 +230,7 @@ __device__ __forceinline__ void as_scan_forward(const T (&F)[KPL][4], const T (&
         }
     }
     // e = x past this lane's last knot; the previous lane's = x at this lane's first knot
-    const int a1 = ((ln - 1) & (kWave - 1)) << 2;
-    T xb0 = bperm(a1, e0), xb1 = bperm(a1, e1);
+    T xb0 = dpp1<kPrevWrap>(e0), xb1 = dpp1<kPrevWrap>(e1);
     if (lane == 0) {
         xb0 = T(0);
         xb1 = T(0);
@@ -236,8 +254,8 @@ template <int KPL, class T>
 __device__ __forceinline__ void as_xi_prev(const AKnotT<T> (&K)[KPL], int lane, T xi00, T xi01, T (&xk)[KPL][2])
 {
     constexpr int L = KPL - 1;
-    xk[0][0] = __shfl_up(K[L].x0, 1, kWave);
-    xk[0][1] = __shfl_up(K[L].x1, 1, kWave);
+    xk[0][0] = dpp1<kPrevWrap>(K[L].x0);
+    xk[0][1] = dpp1<kPrevWrap>(K[L].x1);
     if (lane == 0) {
         xk[0][0] = xi00;
         xk[0][1] = xi01;
@@ -299,16 +317,39 @@ __device__ __forceinline__ bool as_riccati(AKnotT<T> (&K)[KPL], const PT<T>& P, 
         q.g0 = bperm(ad, e.g0); q.g1 = bperm(ad, e.g1); q.g2 = bperm(ad, e.g2);
         q.h0 = bperm(ad, e.h0); q.h1 = bperm(ad, e.h1); q.h2 = bperm(ad, e.h2);
     };
+    auto level1 = [&](RcT<T>& q) {   // d = 1 (DPP; as_pad: lane 63 keeps its own identity)
+        if (as_pad(KPL, N)) {
+            q.a0 = dpp1<kNextKeep>(e.a0); q.a1 = dpp1<kNextKeep>(e.a1);
+            q.a2 = dpp1<kNextKeep>(e.a2); q.a3 = dpp1<kNextKeep>(e.a3);
+            q.g0 = dpp1<kNextKeep>(e.g0); q.g1 = dpp1<kNextKeep>(e.g1); q.g2 = dpp1<kNextKeep>(e.g2);
+            q.h0 = dpp1<kNextKeep>(e.h0); q.h1 = dpp1<kNextKeep>(e.h1); q.h2 = dpp1<kNextKeep>(e.h2);
+        } else {
+            q.a0 = dpp1<kNextWrap>(e.a0); q.a1 = dpp1<kNextWrap>(e.a1);
+            q.a2 = dpp1<kNextWrap>(e.a2); q.a3 = dpp1<kNextWrap>(e.a3);
+            q.g0 = dpp1<kNextWrap>(e.g0); q.g1 = dpp1<kNextWrap>(e.g1); q.g2 = dpp1<kNextWrap>(e.g2);
+            q.h0 = dpp1<kNextWrap>(e.h0); q.h1 = dpp1<kNextWrap>(e.h1); q.h2 = dpp1<kNextWrap>(e.h2);
+        }
+    };
     if (as_pad(KPL, N)) {   // past the wavefront: lane 63's identity (as_pad)
+        {
+            RcT<T> q;
+            level1(q);
+            ok = rc_combine(e, q) && ok;
+        }
 #pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
+        for (int d = 2; d < kWave; d <<= 1) {
             RcT<T> q;
             level(min(ln + d, kWave - 1) << 2, q);
             ok = rc_combine(e, q) && ok;
         }
     } else {
+        {
+            RcT<T> q;
+            level1(q);
+            if (ln + 1 < kWave) ok = rc_combine(e, q) && ok;
+        }
 #pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
+        for (int d = 2; d < kWave; d <<= 1) {
             RcT<T> q;
             level(((ln + d) & (kWave - 1)) << 2, q);
             if (ln + d < kWave) ok = rc_combine(e, q) && ok;
@@ -317,8 +358,7 @@ __device__ __forceinline__ bool as_riccati(AKnotT<T> (&K)[KPL], const PT<T>& P, 
     // P at this lane's first knot; the next lane's (terminal past the last lane)
     T P00, P01, P11;
     ok = rc_apply(e, P.Pw0, T(0), P.Pw1, P00, P01, P11) && ok;
-    const int a1 = ((ln + 1) & (kWave - 1)) << 2;
-    T Pn00 = bperm(a1, P00), Pn01 = bperm(a1, P01), Pn11 = bperm(a1, P11);
+    T Pn00 = dpp1<kNextWrap>(P00), Pn01 = dpp1<kNextWrap>(P01), Pn11 = dpp1<kNextWrap>(P11);
     if (lane == kWave - 1) {
         Pn00 = P.Pw0;
         Pn01 = T(0);

@@ -67,6 +67,37 @@ __device__ __forceinline__ float bperm(int addr, float x)
     return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(x)));
 }
 
+// One-lane shifts across the wavefront through DPP (a VALU move, no LDS round trip), for the
+// scans' distance-1 level and their final hand-over to the neighbour lane.  They return exactly
+// what bperm returns at the addresses they replace:
+//   kNextKeep (wave_shl:1): lane l takes lane l + 1's value, lane 63 keeps its own (min(l + 1, 63));
+//   kNextWrap (wave_rol:1): lane l takes lane (l + 1) mod 64's;
+//   kPrevWrap (wave_ror:1): lane l takes lane (l - 1) mod 64's.
+// update_dpp's "old" operand is the lane's own value and bound_ctrl is off, so the lane with no
+// source (wave_shl's lane 63) keeps it.
+enum : int { kNextKeep = 0x130, kNextWrap = 0x134, kPrevWrap = 0x13C };
+
+template <int CTRL>
+__device__ __forceinline__ int dpp1(int x)
+{
+    return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp1(double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = dpp1<CTRL>((int)b);
+    const int hi = dpp1<CTRL>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp1(float x)
+{
+    return __int_as_float(dpp1<CTRL>(__float_as_int(x)));
+}
+
 // Fused forms used throughout (and in the same places by oracle/blf_oracle.c):
 //   FD2(a, b, c, d)    = a b + c d      as fma(a, b, c d)
 //   FD3(a, b, c, d, e) = a b + c d + e  as fma(a, b, fma(c, d, e))
