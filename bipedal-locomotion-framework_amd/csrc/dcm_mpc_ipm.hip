@@ -232,8 +232,14 @@ __device__ __forceinline__ void scan_backward(double g0, double g1, double g2, d
                                               double& vn0, double& vn1)
 {
     const int ln = opaque(lane);
+    {   // d = 1 through DPP (dcm_qp_common.h)
+        const double p0 = dpp1<kNextWrap>(g0), p1 = dpp1<kNextWrap>(g1);
+        const double p2 = dpp1<kNextWrap>(g2), p3 = dpp1<kNextWrap>(g3);
+        const double q0 = dpp1<kNextWrap>(c0), q1 = dpp1<kNextWrap>(c1);
+        if (ln + 1 < kWave) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
+    }
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
+    for (int d = 2; d < kWave; d <<= 1) {
         const int ad = ((ln + d) & (kWave - 1)) << 2;
         const double p0 = bperm(ad, g0), p1 = bperm(ad, g1);
         const double p2 = bperm(ad, g2), p3 = bperm(ad, g3);
@@ -254,9 +260,8 @@ __device__ __forceinline__ void scan_backward(double g0, double g1, double g2, d
             if (w > 0) __syncthreads();
         }
     }
-    const int a1 = ((ln + 1) & (kWave - 1)) << 2;
-    vn0 = bperm(a1, v0);
-    vn1 = bperm(a1, v1);
+    vn0 = dpp1<kNextWrap>(v0);
+    vn1 = dpp1<kNextWrap>(v1);
     if (lane == kWave - 1) {
         vn0 = 0.0;
         vn1 = 0.0;
@@ -275,8 +280,14 @@ __device__ __forceinline__ void scan_forward(double g0, double g1, double g2, do
                                              double& x1, double& xk0, double& xk1)
 {
     const int ln = opaque(lane);
+    {   // d = 1 through DPP
+        const double p0 = dpp1<kPrevWrap>(g0), p1 = dpp1<kPrevWrap>(g1);
+        const double p2 = dpp1<kPrevWrap>(g2), p3 = dpp1<kPrevWrap>(g3);
+        const double q0 = dpp1<kPrevWrap>(c0), q1 = dpp1<kPrevWrap>(c1);
+        if (ln >= 1) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, c0, c1);
+    }
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
+    for (int d = 2; d < kWave; d <<= 1) {
         const int ad = ((ln - d) & (kWave - 1)) << 2;
         const double p0 = bperm(ad, g0), p1 = bperm(ad, g1);
         const double p2 = bperm(ad, g2), p3 = bperm(ad, g3);
@@ -298,9 +309,8 @@ __device__ __forceinline__ void scan_forward(double g0, double g1, double g2, do
             if (w < nwa - 1) __syncthreads();
         }
     }
-    const int a1 = ((ln - 1) & (kWave - 1)) << 2;
-    xk0 = bperm(a1, x0);
-    xk1 = bperm(a1, x1);
+    xk0 = dpp1<kPrevWrap>(x0);
+    xk1 = dpp1<kPrevWrap>(x1);
     if (lane == 0) {
         xk0 = 0.0;
         xk1 = 0.0;
@@ -399,8 +409,8 @@ __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P
 __device__ __forceinline__ void xi_prev(const Knot& K, int lane, double xb0, double xb1, double& xk0,
                                         double& xk1)
 {
-    xk0 = __shfl_up(K.x0, 1, kWave);
-    xk1 = __shfl_up(K.x1, 1, kWave);
+    xk0 = dpp1<kPrevWrap>(K.x0);
+    xk1 = dpp1<kPrevWrap>(K.x1);
     if (lane == 0) {
         xk0 = xb0;
         xk1 = xb1;
@@ -428,8 +438,16 @@ __device__ __forceinline__ bool riccati(Knot& K, const KParams& P, double E00, d
         e.h0 = e.h1 = e.h2 = 0.0;
     }
     const int ln = opaque(lane);
+    {   // d = 1 through DPP
+        Rc q;
+        q.a0 = dpp1<kNextWrap>(e.a0); q.a1 = dpp1<kNextWrap>(e.a1);
+        q.a2 = dpp1<kNextWrap>(e.a2); q.a3 = dpp1<kNextWrap>(e.a3);
+        q.g0 = dpp1<kNextWrap>(e.g0); q.g1 = dpp1<kNextWrap>(e.g1); q.g2 = dpp1<kNextWrap>(e.g2);
+        q.h0 = dpp1<kNextWrap>(e.h0); q.h1 = dpp1<kNextWrap>(e.h1); q.h2 = dpp1<kNextWrap>(e.h2);
+        if (ln + 1 < kWave) ok = rc_combine(e, q) && ok;
+    }
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
+    for (int d = 2; d < kWave; d <<= 1) {
         const int ad = ((ln + d) & (kWave - 1)) << 2;
         Rc q;
         q.a0 = bperm(ad, e.a0); q.a1 = bperm(ad, e.a1); q.a2 = bperm(ad, e.a2); q.a3 = bperm(ad, e.a3);
@@ -456,10 +474,9 @@ __device__ __forceinline__ bool riccati(Knot& K, const KParams& P, double E00, d
         if (w > 0) __syncthreads();
     }
     // lane k takes P_{k+1} from lane k+1
-    const int a1 = ((ln + 1) & (kWave - 1)) << 2;
-    double P00 = bperm(a1, Pk00);
-    double P01 = bperm(a1, Pk01);
-    double P11 = bperm(a1, Pk11);
+    double P00 = dpp1<kNextWrap>(Pk00);
+    double P01 = dpp1<kNextWrap>(Pk01);
+    double P11 = dpp1<kNextWrap>(Pk11);
     if (lane == kWave - 1 && NW > 1 && wv < nwa - 1) {
         P00 = bnd[kBnd * (wv + 1) + kBP];
         P01 = bnd[kBnd * (wv + 1) + kBP + 1];
