@@ -1,5 +1,5 @@
 """Run one streaming kernel a few times (for rocprofv3 counter passes):
-  python tools/stream_one.py rollout|hull|quintic|contact"""
+  python tools/stream_one.py rollout|hull|quintic|contact|fbk|fbk_euler"""
 import os
 import sys
 
@@ -32,6 +32,14 @@ def main(which):
         co = h.quintic_fit(kt, rnd(S, 3, 3, 3))
         tq = (kt[:, :1] + (kt[:, 2:] - kt[:, :1]) * rnd(S, Q)).contiguous()
         fn = lambda: h.quintic_eval(kt, co, tq)
+    elif which in ("fbk", "fbk_euler"):
+        B, n = 2 * 1024 * 1024, 24
+        R = torch.linalg.qr(torch.randn(B, 3, 3, dtype=torch.float64, device=dev))[0].contiguous()
+        tw, sd, pos, q = rnd(B, 6), rnd(B, n), rnd(B, 3), rnd(B, n)
+        if which == "fbk":
+            fn = lambda: h.fbk_dynamics(0.01, R, tw, sd)
+        else:
+            fn = lambda: h.fbk_euler_integrate(0.01, pos, R, q, tw, sd, 0.0, 0.01, 0.01)
     else:
         C = 4 * 1024 * 1024
         prm = torch.tensor([0.12, 0.09, 2000.0, 100.0], dtype=torch.float64, device=dev)
