@@ -623,6 +623,18 @@ def single_solve_latency(args, h, dev):
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t0)
     gpu_us = float(np.median(lat[args.warmup:])) * 1e6
+    # the same call timed on the device (HIP events on the stream the solve is enqueued on): the
+    # kernels alone, without the host's argument marshalling, launch and synchronisation.  A spin
+    # kernel ahead of the start event keeps the device busy while the host enqueues the solve, so
+    # the start event is reached only when the solve's kernels are already queued behind it.
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(100)]
+    for i in range(50):
+        torch.cuda._sleep(1 << 20)
+        ev[2 * i].record()
+        h.dcm_mpc_solve(d, params, out=out)
+        ev[2 * i + 1].record()
+        torch.cuda.synchronize()
+    dev_us = float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(50)])) * 1e3
     assert int(out["status"][0]) == 0
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -642,6 +654,7 @@ def single_solve_latency(args, h, dev):
     line = {"metric": "single DCM-MPC solve latency (configs[0]: 4 footsteps, horizon 50)",
             "value": gpu_us, "unit": "us", "n_gpus": 1, "higher_is_better": False,
             "dtype": "f64", "ipm_iters": int(out["iters"][0]), "polished": int(out["polished"][0]),
+            "device_us": dev_us,
             "cpu_baseline": {"value": cpu_us, "unit": "us", "cores": 1, "kind": "port",
                              "sample": "200 solves of the same problem in one C batch call, "
                                        "oracle/blf_oracle.c sequential mode, gcc -O3, one thread"},
