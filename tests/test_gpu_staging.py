@@ -144,10 +144,29 @@ def test_hull2d_ties_duplicates_nonfinite(handle, oracle):
     pts[3::11, 2, 0] = np.nan
     pts[4::13, 1, 1] = np.inf
     pts[5::17, 0, 0] = -np.inf
+    pts[6::19, 0] = (0.0, 1.0)                              # signed-zero tie: equal keys,
+    pts[6::19, 1] = (-0.0, 1.0)                             # different bits
     A, b, nf = handle.hull2d_hrep(_d(pts), _d(npts, torch.int32), 8)
     A, b, nf = A.cpu().numpy(), b.cpu().numpy(), nf.cpu().numpy()
     for i in range(B):
         Ao, bo, mo = oracle.hull2d_hrep(pts[i, :npts[i]], 8)
+        assert nf[i] == mo, i
+        np.testing.assert_array_equal(A[i], Ao)
+        np.testing.assert_array_equal(b[i], bo)
+
+
+@pytest.mark.parametrize("B,P_,M,nonfinite", [(64, 8, 8, False), (200, 8, 8, True), (130, 5, 6, False),
+                                               (33, 3, 3, True)])
+def test_hull2d_register_path_misaligned(handle, oracle, B, P_, M, nonfinite):
+    """Input points only 8-B aligned, partial workgroups (B = 33, 130), and waves in which one
+    polygon with a NaN coordinate takes the insertion sort next to sorting-network polygons."""
+    pts, npts = _polygons(B, P_, seed=B * 3 + P_)
+    if nonfinite:
+        pts[B // 2, 1, 0] = np.nan
+    A, b, nf = handle.hull2d_hrep(_d(pts, misalign=True), _d(npts, torch.int32), M)
+    A, b, nf = A.cpu().numpy(), b.cpu().numpy(), nf.cpu().numpy()
+    for i in range(B):
+        Ao, bo, mo = oracle.hull2d_hrep(pts[i, :npts[i]], M)
         assert nf[i] == mo, i
         np.testing.assert_array_equal(A[i], Ao)
         np.testing.assert_array_equal(b[i], bo)
