@@ -21,7 +21,7 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 # every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
-            "blf_hull2d_contains", "blf_quintic_fit", "blf_quintic_eval",
+            "blf_hull2d_contains", "blf_hull3d_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
             "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_solve_warm",
             "blf_dcm_phase_expand", "blf_dcm_mpc_solve_phased",
             "blf_dcm_mpc_flops_per_iter",
@@ -130,6 +130,8 @@ def lib():
         L.blf_dcm_euler_rollout.argtypes = [_vp, _vp, _vp, _vp, _i32, _f64, _vp, _i64, _vp]
         L.blf_hull2d_hrep.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
         L.blf_hull2d_contains.argtypes = [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp]
+        L.blf_hull3d_hrep.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
+        L.blf_halfspace_contains.argtypes = [_vp, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp]
         L.blf_quintic_fit.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp]
         L.blf_quintic_eval.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _i32, _vp, _vp, _vp]
         L.blf_dcm_mpc_default_params.argtypes = [ctypes.POINTER(DcmMpcParams), _i32]
@@ -322,6 +324,33 @@ class Handle:
         _check(lib().blf_hull2d_contains(
             self._h, _ptr(A, torch.float64, (B, M, 2), "A"), _ptr(b, torch.float64, (B, M), "b"),
             _ptr(nf, torch.int32, (B,), "nfacets"), M, _ptr(query, torch.float64, (B, 2), "query"),
+            B, _ptr(inside, torch.int32, (B,), "inside"), _stream(stream)))
+        return inside
+
+    def hull3d_hrep(self, pts, npts, max_facets=32, out=None, stream=None):
+        """blf_hull3d_hrep: pts [B, P, 3], npts [B] -> A [B, max_facets, 3], b, nfacets."""
+        torch = _torch()
+        B, P = pts.shape[0], pts.shape[1]
+        if out is None:
+            out = (torch.empty((B, max_facets, 3), dtype=torch.float64, device=pts.device),
+                   torch.empty((B, max_facets), dtype=torch.float64, device=pts.device),
+                   torch.empty((B,), dtype=torch.int32, device=pts.device))
+        A, b, nf = out
+        _check(lib().blf_hull3d_hrep(
+            self._h, _ptr(pts, torch.float64, (B, P, 3), "pts"), _ptr(npts, torch.int32, (B,), "npts"),
+            P, max_facets, B, _ptr(A, torch.float64, (B, max_facets, 3), "A"),
+            _ptr(b, torch.float64, (B, max_facets), "b"), _ptr(nf, torch.int32, (B,), "nfacets"),
+            _stream(stream)))
+        return A, b, nf
+
+    def halfspace_contains(self, A, b, nf, query, stream=None):
+        """blf_halfspace_contains: A [B, M, dim], b [B, M], nf [B], query [B, dim] -> inside [B]."""
+        torch = _torch()
+        B, M, D = A.shape
+        inside = torch.empty((B,), dtype=torch.int32, device=A.device)
+        _check(lib().blf_halfspace_contains(
+            self._h, _ptr(A, torch.float64, (B, M, D), "A"), _ptr(b, torch.float64, (B, M), "b"),
+            _ptr(nf, torch.int32, (B,), "nfacets"), D, M, _ptr(query, torch.float64, (B, D), "query"),
             B, _ptr(inside, torch.int32, (B,), "inside"), _stream(stream)))
         return inside
 

@@ -167,6 +167,35 @@ blf_status blf_hull2d_contains(blf_handle* handle, const double* A, const double
                                   (hipStream_t)stream);
 }
 
+blf_status blf_hull3d_hrep(blf_handle* handle, const double* pts, const int32_t* npts,
+                           int32_t max_points, int32_t max_facets, int64_t batch, double* A,
+                           double* b, int32_t* nfacets, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_hull3d_hrep: null handle");
+    BLF_REQUIRE(max_points >= 1 && max_points <= BLF_HULL_MAX_POINTS,
+                "blf_hull3d_hrep: max_points %d outside [1, %d]", max_points, BLF_HULL_MAX_POINTS);
+    BLF_REQUIRE(max_facets >= 1 && max_facets <= BLF_HULL3D_MAX_FACETS,
+                "blf_hull3d_hrep: max_facets %d outside [1, %d]", max_facets, BLF_HULL3D_MAX_FACETS);
+    BLF_REQUIRE(batch >= 0, "blf_hull3d_hrep: negative batch");
+    BLF_REQUIRE(batch == 0 || (pts && npts && A && b && nfacets), "blf_hull3d_hrep: null buffer");
+    return launch_hull3d(pts, npts, max_points, max_facets, batch, A, b, nfacets,
+                         (hipStream_t)stream);
+}
+
+blf_status blf_halfspace_contains(blf_handle* handle, const double* A, const double* b,
+                                  const int32_t* nfacets, int32_t dim, int32_t max_facets,
+                                  const double* query, int64_t batch, int32_t* inside, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_halfspace_contains: null handle");
+    BLF_REQUIRE(dim >= 1, "blf_halfspace_contains: dim %d", dim);
+    BLF_REQUIRE(max_facets >= 1, "blf_halfspace_contains: max_facets %d", max_facets);
+    BLF_REQUIRE(batch >= 0, "blf_halfspace_contains: negative batch");
+    BLF_REQUIRE(batch == 0 || (A && b && nfacets && query && inside),
+                "blf_halfspace_contains: null buffer");
+    return launch_halfspace_contains(A, b, nfacets, dim, max_facets, query, batch, inside,
+                                     (hipStream_t)stream);
+}
+
 blf_status blf_quintic_fit(blf_handle* handle, const double* knots_t, const double* knots_pva,
                            int32_t nknots, int32_t dim, int64_t nsplines, double* coeffs,
                            void* stream)

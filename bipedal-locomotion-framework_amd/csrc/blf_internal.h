@@ -35,6 +35,11 @@ blf_status launch_dcm_rollout(const double* xi0, const double* omega, const doub
                               hipStream_t s);
 blf_status launch_hull2d(const double* pts, const int32_t* npts, int32_t P, int32_t M,
                          int64_t batch, double* A, double* b, int32_t* nf, hipStream_t s);
+blf_status launch_hull3d(const double* pts, const int32_t* npts, int32_t P, int32_t M,
+                         int64_t batch, double* A, double* b, int32_t* nf, hipStream_t s);
+blf_status launch_halfspace_contains(const double* A, const double* b, const int32_t* nf,
+                                     int32_t dim, int32_t M, const double* q, int64_t batch,
+                                     int32_t* inside, hipStream_t s);
 blf_status launch_hull2d_contains(const double* A, const double* b, const int32_t* nf, int32_t M,
                                   const double* q, int64_t batch, int32_t* inside,
                                   hipStream_t s);

@@ -307,6 +307,114 @@ __global__ __launch_bounds__(256) void hull2d_contains_kernel(const double* __re
     inside[q] = in;
 }
 
+// 3-D hull (ConvexHullHelper::buildConvexHull on 3 x p points; the reference's own test,
+// ConvexHullHelperTest.cpp:15-63, is 3-D): one lane per point set, the supporting planes through
+// every triple in lexicographic order, deduplicated -- oracle orc_hull3d_hrep states the rule and
+// runs the same operations in the same order.  Off the planning path (the support polygons are
+// 2-D), so it stays a plain lane-per-set kernel reading its points through L1/L2.
+__global__ __launch_bounds__(64) void hull3d_kernel(const double* __restrict__ pts,
+                                                    const int32_t* __restrict__ npts, int32_t P,
+                                                    int32_t M, int64_t batch,
+                                                    double* __restrict__ Aout,
+                                                    double* __restrict__ bout,
+                                                    int32_t* __restrict__ nfout)
+{
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= batch) return;
+    const double* q = pts + s * 3 * P;
+    double* A = Aout + s * 3 * M;
+    double* b = bout + s * M;
+    for (int e = 0; e < 3 * M; ++e) A[e] = 0.0;
+    for (int e = 0; e < M; ++e) b[e] = 0.0;
+    const int n = npts[s];
+    if (n < 4 || n > P) {
+        nfout[s] = -1;
+        return;
+    }
+    double scale = 0.0;
+    for (int e = 0; e < 3 * n; ++e) {
+        const double a = fabs(q[e]);
+        if (a > scale) scale = a;
+    }
+    const double tol = 1e-12 * (1.0 + scale);
+    const double btol = 1e-9 * (1.0 + scale);
+    int count = 0;
+    bool overflow = false;
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j)
+            for (int k = j + 1; k < n; ++k) {
+                const double pix = q[3 * i], piy = q[3 * i + 1], piz = q[3 * i + 2];
+                const double ux = q[3 * j] - pix, uy = q[3 * j + 1] - piy, uz = q[3 * j + 2] - piz;
+                const double vx = q[3 * k] - pix, vy = q[3 * k + 1] - piy, vz = q[3 * k + 2] - piz;
+                const double cx = uy * vz - uz * vy;
+                const double cy = uz * vx - ux * vz;
+                const double cz = ux * vy - uy * vx;
+                const double len = sqrt(cx * cx + cy * cy + cz * cz);
+                if (!(len > 0.0)) continue;
+                double nx = cx / len, ny = cy / len, nz = cz / len;
+                bool pos = false, neg = false;
+                for (int l = 0; l < n; ++l) {
+                    const double d = nx * (q[3 * l] - pix) + ny * (q[3 * l + 1] - piy) +
+                                     nz * (q[3 * l + 2] - piz);
+                    pos = pos || d > tol;
+                    neg = neg || d < -tol;
+                }
+                if ((pos && neg) || !(pos || neg)) continue;
+                if (pos) {
+                    nx = -nx;
+                    ny = -ny;
+                    nz = -nz;
+                }
+                double bm = -__builtin_inf();
+                for (int l = 0; l < n; ++l) {
+                    const double v = nx * q[3 * l] + ny * q[3 * l + 1] + nz * q[3 * l + 2];
+                    if (v > bm) bm = v;
+                }
+                bool dup = false;
+                for (int e = 0; e < count && e < M; ++e)
+                    dup = dup || (fabs(A[3 * e] - nx) <= 1e-9 && fabs(A[3 * e + 1] - ny) <= 1e-9 &&
+                                  fabs(A[3 * e + 2] - nz) <= 1e-9 && fabs(b[e] - bm) <= btol);
+                if (dup) continue;
+                if (count < M) {
+                    A[3 * count] = nx;
+                    A[3 * count + 1] = ny;
+                    A[3 * count + 2] = nz;
+                    b[count] = bm;
+                } else {
+                    overflow = true;
+                }
+                ++count;
+            }
+    if (overflow || count < 4) {
+        for (int e = 0; e < 3 * M; ++e) A[e] = 0.0;
+        for (int e = 0; e < M; ++e) b[e] = 0.0;
+        count = -1;
+    }
+    nfout[s] = count;
+}
+
+// doesPointBelongToConvexHull in any dimension (ConvexHullHelper.cpp:101-117): strict `>` rejects.
+__global__ __launch_bounds__(256) void halfspace_contains_kernel(const double* __restrict__ A,
+                                                                 const double* __restrict__ b,
+                                                                 const int32_t* __restrict__ nf,
+                                                                 int32_t dim, int32_t M,
+                                                                 const double* __restrict__ query,
+                                                                 int64_t batch,
+                                                                 int32_t* __restrict__ inside)
+{
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= batch) return;
+    const int m = nf[s];
+    int in = m >= 0 ? 1 : 0;
+    const double* p = query + s * dim;
+    for (int i = 0; i < m; ++i) {
+        double v = 0.0;
+        for (int c = 0; c < dim; ++c) v = v + A[(s * M + i) * dim + c] * p[c];
+        if (v > b[s * M + i]) in = 0;
+    }
+    inside[s] = in;
+}
+
 // one lane per (spline, segment, axis)
 __global__ __launch_bounds__(256) void quintic_fit_kernel(const double* __restrict__ kt,
                                                           const double* __restrict__ kp,
@@ -464,6 +572,25 @@ blf_status launch_hull2d_contains(const double* A, const double* b, const int32_
     hipLaunchKernelGGL(hull2d_contains_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256), 0,
                        s, A, b, nf, M, q, batch, inside);
     return check_hip(hipGetLastError(), "hull2d_contains_kernel launch");
+}
+
+blf_status launch_hull3d(const double* pts, const int32_t* npts, int32_t P, int32_t M,
+                         int64_t batch, double* A, double* b, int32_t* nf, hipStream_t s)
+{
+    if (batch == 0) return BLF_OK;
+    hipLaunchKernelGGL(hull3d_kernel, dim3((unsigned)ceil_div(batch, 64)), dim3(64), 0, s, pts, npts,
+                       P, M, batch, A, b, nf);
+    return check_hip(hipGetLastError(), "hull3d_kernel launch");
+}
+
+blf_status launch_halfspace_contains(const double* A, const double* b, const int32_t* nf,
+                                     int32_t dim, int32_t M, const double* q, int64_t batch,
+                                     int32_t* inside, hipStream_t s)
+{
+    if (batch == 0) return BLF_OK;
+    hipLaunchKernelGGL(halfspace_contains_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256),
+                       0, s, A, b, nf, dim, M, q, batch, inside);
+    return check_hip(hipGetLastError(), "halfspace_contains_kernel launch");
 }
 
 blf_status launch_quintic_fit(const double* kt, const double* kp, int32_t K1, int32_t D,

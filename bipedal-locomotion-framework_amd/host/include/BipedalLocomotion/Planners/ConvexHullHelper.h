@@ -1,13 +1,15 @@
 /**
  * @file ConvexHullHelper.h
  * Drop-in for src/Planners/include/BipedalLocomotion/Planners/ConvexHullHelper.h:32-81
- * (src/Planners/src/ConvexHullHelper.cpp:35-117) for the planners' 2-D support polygons.
- * buildConvexHull runs blf_hull2d_hrep on the device (2 x p points, p <= 16); getA()/getB() return
- * the H-representation A x <= b (unit outward normals, merged collinear facets, counter-clockwise
- * order — Qhull's facet order is internal to Qhull, so only the facet SET is comparable);
- * doesPointBelongToConvexHull runs blf_hull2d_contains (strict `>` rejects, no tolerance).
- * Inputs with a row count other than 2 are rejected with false: 3-D hulls are not on the
- * accelerated path (scope).
+ * (src/Planners/src/ConvexHullHelper.cpp:35-117).
+ * buildConvexHull runs blf_hull2d_hrep on the device for 2 x p points (the planners' support
+ * polygons) and blf_hull3d_hrep for 3 x p points (p <= 16; the reference's own test,
+ * ConvexHullHelperTest.cpp:15-63, is 3-D); getA()/getB() return the H-representation A x <= b
+ * (unit outward normals; 2-D: merged collinear facets, counter-clockwise; 3-D: one row per
+ * distinct supporting plane, where Qhull "Qt" may give a split face twice — Qhull's facet order is
+ * internal to Qhull, so only the SET of planes is comparable).  doesPointBelongToConvexHull runs
+ * blf_hull2d_contains / blf_halfspace_contains (strict `>` rejects, no tolerance).  Other row
+ * counts are rejected with false.
  */
 #ifndef BLF_BIPEDAL_LOCOMOTION_PLANNERS_CONVEX_HULL_HELPER_H
 #define BLF_BIPEDAL_LOCOMOTION_PLANNERS_CONVEX_HULL_HELPER_H
@@ -29,9 +31,10 @@ class ConvexHullHelper
     blf::VectorXd m_b;
     blf::DeviceBuffer<double> m_dPts, m_dA, m_dB, m_dQ;
     blf::DeviceBuffer<int32_t> m_dN, m_dInside;
+    bool buildConvexHull3(const blf::MatrixXd& points);
 
 public:
-    /** points: 2 x p (one point per column).  Any matrix type with rows(), cols(), (i, j). */
+    /** points: 2 x p or 3 x p (one point per column).  Any matrix type with rows(), cols(), (i, j). */
     template <class Mat> bool buildConvexHull(const Mat& points)
     {
         return buildConvexHull(blf::MatrixXd::from(points));

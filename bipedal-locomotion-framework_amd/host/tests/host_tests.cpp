@@ -264,9 +264,42 @@ static void testConvexHull()
     REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.0, 0.0 - 1.0}));
     REQUIRE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.1, 0.0}));
     REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.1, 0.0, 0.0}));   // wrong size
-    // 3-D input (ConvexHullHelperTest.cpp's points) is outside the accelerated path
-    blf::MatrixXd p3(3, 8);
-    REQUIRE_FALSE(helper.buildConvexHull(p3));
+    // 4-D input is refused
+    blf::MatrixXd p4(4, 8);
+    REQUIRE_FALSE(helper.buildConvexHull(p4));
+}
+
+// ---- ConvexHullHelper (device, 3-D): the reference's own test, ConvexHullHelperTest.cpp:15-63 --
+static void testConvexHull3()
+{
+    ConvexHullHelper helper;
+    blf::MatrixXd p(3, 8);
+    const double c[8][3] = {{0.6269, 0.7207, 0.3000}, {0.5538, 0.6526, 0.3000},
+                            {0.6901, 0.5062, 0.3000}, {0.7633, 0.5744, 0.3000},
+                            {0.8927, 0.7319, 0.2400}, {0.8101, 0.6754, 0.2400},
+                            {0.9231, 0.5103, 0.2400}, {1.0056, 0.5668, 0.2400}};
+    for (int j = 0; j < 8; ++j)
+        for (int r = 0; r < 3; ++r) p(r, j) = c[j][r];
+    REQUIRE(helper.buildConvexHull(p));
+    // check if the points belong to convex hull
+    for (int col = 0; col < 8; ++col)
+        REQUIRE(helper.doesPointBelongToConvexHull(blf::VectorXd{p(0, col), p(1, col), p(2, col)}));
+    // p = [0 0 0] does not belong to the convex hull
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.0, 0.0, 0.0}));
+    // the Qhull fixture's 10 distinct planes (tests/golden/hull3d.json), unit normals
+    REQUIRE(helper.getA().rows() == 10 && helper.getA().cols() == 3);
+    for (std::size_t i = 0; i < helper.getA().rows(); ++i)
+    {
+        const double n2 = helper.getA()(i, 0) * helper.getA()(i, 0) +
+                          helper.getA()(i, 1) * helper.getA()(i, 1) +
+                          helper.getA()(i, 2) * helper.getA()(i, 2);
+        REQUIRE(std::abs(n2 - 1.0) < 1e-12);
+    }
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.7, 0.6}));   // wrong size
+    // a flat set has no 3-D hull
+    blf::MatrixXd flat(3, 4);
+    for (int j = 0; j < 4; ++j) { flat(0, j) = j & 1; flat(1, j) = j >> 1; flat(2, j) = 0.5; }
+    REQUIRE_FALSE(helper.buildConvexHull(flat));
 }
 
 // ---- QuinticSpline (device) -------------------------------------------------------------------
@@ -767,6 +800,7 @@ int main(int argc, char** argv)
         {"ParametersHandler (config.ini)", false, testParametersHandler},
         {"Integrator - Linear system", true, testIntegratorLTI},
         {"Convex Hull helper (2-D)", true, testConvexHull},
+        {"Convex Hull helper (3-D, ConvexHullHelperTest.cpp)", true, testConvexHull3},
         {"QuinticSpline", true, testQuinticSpline},
         {"TimeVaryingDCMPlanner advance", true, testPlanner},
         {"Continuous Contact", true, testContinuousContact},

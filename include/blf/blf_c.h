@@ -18,6 +18,9 @@
  *                             A = omega_k I, B = -omega_k I (LinearTimeInvariantSystem.cpp:13-38, :71)
  *   blf_hull2d_hrep           Planners/src/ConvexHullHelper.cpp:35-99 (buildConvexHull/getA/getB)
  *   blf_hull2d_contains       Planners/src/ConvexHullHelper.cpp:101-117 (doesPointBelongToConvexHull)
+ *   blf_hull3d_hrep           ConvexHullHelper.cpp:35-99 on 3 x p points (Planners/tests/
+ *                             ConvexHullHelperTest.cpp:15-63 is 3-D)
+ *   blf_halfspace_contains    ConvexHullHelper.cpp:101-117 in any dimension
  *   blf_quintic_fit/_eval     ABSENT in the reference (QuinticSpline); knot rule
  *                             of Planners/src/ContactList.cpp:190-202 (getPresentContact, `<=`)
  *   blf_contact_model_eval    ContactModels/src/ContinuousContactModel.cpp:79-171, 223-254 behind the
@@ -127,6 +130,26 @@ blf_status blf_hull2d_hrep(blf_handle* handle, const double* pts, const int32_t*
 blf_status blf_hull2d_contains(blf_handle* handle, const double* A, const double* b,
                                const int32_t* nfacets, int32_t max_facets, const double* query,
                                int64_t batch, int32_t* inside, void* stream);
+
+/* 3-D H-representation (ConvexHullHelper on 3 x p points).  pts: [B][P][3] (P <=
+ * BLF_HULL_MAX_POINTS), npts: [B].  Output padded to max_facets rows: A: [B][max_facets][3] unit
+ * outward normals, b: [B][max_facets] (inside: A x <= b), nfacets: [B].  The rows are the distinct
+ * supporting planes of the set (a face Qhull "Qt" splits into triangles is one row here; compare
+ * as sets of planes), b = the largest n . p over the input points, so every input point is
+ * inside exactly.  nfacets = -1 for fewer than 4 points, a flat set, or more than max_facets
+ * planes.  Rule and tolerances: oracle orc_hull3d_hrep.                                       */
+#define BLF_HULL3D_MAX_FACETS 64
+blf_status blf_hull3d_hrep(blf_handle* handle, const double* pts, const int32_t* npts,
+                           int32_t max_points, int32_t max_facets, int64_t batch,
+                           double* A, double* b, int32_t* nfacets, void* stream);
+
+/* doesPointBelongToConvexHull in `dim` dimensions: A: [B][max_facets][dim], b: [B][max_facets],
+ * query: [B][dim]; inside[q] = 1 iff no row i < nfacets has (A p)_i > b_i (sum in column order
+ * from 0.0).  nfacets < 0 gives 0.                                                            */
+blf_status blf_halfspace_contains(blf_handle* handle, const double* A, const double* b,
+                                  const int32_t* nfacets, int32_t dim, int32_t max_facets,
+                                  const double* query, int64_t batch, int32_t* inside,
+                                  void* stream);
 
 /* ---- 4. Quintic spline (swing foot) -------------------------------------------------------
  * A spline has K+1 knots t_0 < ... < t_K, and per knot and per axis (D axes, D <= 3) the

@@ -214,6 +214,100 @@ int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, doub
     return nv;
 }
 
+/* 3-D H-representation (ConvexHullHelper::buildConvexHull on a 3 x p matrix,
+ * ConvexHullHelper.cpp:35-99; the reference's own test is 3-D, ConvexHullHelperTest.cpp:15-63).
+ * The facets are the distinct supporting planes through three input points: for i < j < k in
+ * lexicographic order, c = (p_j - p_i) x (p_k - p_i), n = c / |c|, d_l = n . (p_l - p_i); the plane
+ * supports the set when no d_l exceeds tol on one side (tol = 1e-12 (1 + max |coordinate|)); its
+ * outward normal is n when no d_l > tol, else -n; b = max_l n . p_l, so every input point satisfies
+ * A p <= b exactly (the reference test's membership checks).  A plane within 1e-9 (normal,
+ * infinity norm) and 1e-9 (1 + scale) (offset) of an earlier one is the same facet (Qhull "Qt"
+ * triangulates a face into several facets with one plane; compare as sets of planes).  Returns
+ * -1 for fewer than 4 points, a flat set (every triple has all points within tol of its plane),
+ * or more than max_facets planes.  The kernel (hull3d_kernel) runs these operations in this order
+ * (-ffp-contract=off), so the two agree bit for bit. */
+int orc_hull3d_hrep(const double* pts, int npts, int max_facets, double* A, double* b)
+{
+    for (int e = 0; e < 3 * max_facets; ++e) A[e] = 0.0;
+    for (int e = 0; e < max_facets; ++e) b[e] = 0.0;
+    if (npts < 4) return -1;
+    double scale = 0.0;
+    for (int e = 0; e < 3 * npts; ++e) {
+        const double a = fabs(pts[e]);
+        if (a > scale) scale = a;
+    }
+    const double tol = 1e-12 * (1.0 + scale);
+    const double btol = 1e-9 * (1.0 + scale);
+    int count = 0, overflow = 0;
+    for (int i = 0; i < npts; ++i)
+        for (int j = i + 1; j < npts; ++j)
+            for (int k = j + 1; k < npts; ++k) {
+                const double* pi = pts + 3 * i;
+                const double* pj = pts + 3 * j;
+                const double* pk = pts + 3 * k;
+                const double ux = pj[0] - pi[0], uy = pj[1] - pi[1], uz = pj[2] - pi[2];
+                const double vx = pk[0] - pi[0], vy = pk[1] - pi[1], vz = pk[2] - pi[2];
+                const double cx = uy * vz - uz * vy;
+                const double cy = uz * vx - ux * vz;
+                const double cz = ux * vy - uy * vx;
+                const double len = sqrt(cx * cx + cy * cy + cz * cz);
+                if (!(len > 0.0)) continue;
+                double nx = cx / len, ny = cy / len, nz = cz / len;
+                int pos = 0, neg = 0;
+                for (int l = 0; l < npts; ++l) {
+                    const double* q = pts + 3 * l;
+                    const double d = nx * (q[0] - pi[0]) + ny * (q[1] - pi[1]) + nz * (q[2] - pi[2]);
+                    if (d > tol) pos = 1;
+                    if (d < -tol) neg = 1;
+                }
+                if ((pos && neg) || !(pos || neg)) continue;
+                if (pos) {
+                    nx = -nx;
+                    ny = -ny;
+                    nz = -nz;
+                }
+                double bm = -INFINITY;
+                for (int l = 0; l < npts; ++l) {
+                    const double* q = pts + 3 * l;
+                    const double v = nx * q[0] + ny * q[1] + nz * q[2];
+                    if (v > bm) bm = v;
+                }
+                int dup = 0;
+                for (int e = 0; e < count && e < max_facets; ++e)
+                    if (fabs(A[3 * e] - nx) <= 1e-9 && fabs(A[3 * e + 1] - ny) <= 1e-9 &&
+                        fabs(A[3 * e + 2] - nz) <= 1e-9 && fabs(b[e] - bm) <= btol)
+                        dup = 1;
+                if (dup) continue;
+                if (count < max_facets) {
+                    A[3 * count] = nx;
+                    A[3 * count + 1] = ny;
+                    A[3 * count + 2] = nz;
+                    b[count] = bm;
+                } else {
+                    overflow = 1;
+                }
+                ++count;
+            }
+    if (overflow || count < 4) {
+        for (int e = 0; e < 3 * max_facets; ++e) A[e] = 0.0;
+        for (int e = 0; e < max_facets; ++e) b[e] = 0.0;
+        return -1;
+    }
+    return count;
+}
+
+/* doesPointBelongToConvexHull in any dimension (ConvexHullHelper.cpp:101-117): strict `>` rejects. */
+int orc_halfspace_contains(const double* A, const double* b, int nfacets, int dim, const double* p)
+{
+    if (nfacets < 0) return 0;
+    for (int i = 0; i < nfacets; ++i) {
+        double v = 0.0;
+        for (int c = 0; c < dim; ++c) v = v + A[i * dim + c] * p[c];
+        if (v > b[i]) return 0;
+    }
+    return 1;
+}
+
 int orc_hull2d_contains(const double* A, const double* b, int nfacets, const double* p)
 {
     if (nfacets < 0) return 0;

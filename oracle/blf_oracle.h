@@ -21,6 +21,10 @@
  *                            monotone chain with collinear merge; pinned against scipy's bundled
  *                            Qhull 7.3.2 "Qt" fixtures (tests/golden/hull2d.json)
  *   orc_hull2d_contains      Planners/src/ConvexHullHelper.cpp:101-117
+ *   orc_hull3d_hrep          ConvexHullHelper.cpp:35-99 on 3 x p points (the reference test's case,
+ *                            ConvexHullHelperTest.cpp:15-63); checked as plane sets against scipy's
+ *                            Qhull (tests/golden/hull3d.json)
+ *   orc_halfspace_contains   ConvexHullHelper.cpp:101-117 in any dimension
  *   orc_quintic_*            ABSENT in the reference: parity unpinned against the
  *                            reference; pinned by boundary-condition identities + sympy fixtures
  *   orc_contact_* / orc_fbk_* blf_oracle_contact.c: ContinuousContactModel.cpp:79-254 and
@@ -66,6 +70,8 @@ void orc_dcm_phase_expand(int P, int M, int nphases, const double* begin, const 
 
 int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);
 int orc_hull2d_contains(const double* A, const double* b, int nfacets, const double* p);
+int orc_hull3d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);
+int orc_halfspace_contains(const double* A, const double* b, int nfacets, int dim, const double* p);
 
 void orc_quintic_fit(const double* knots_t, const double* knots_pva, int nknots, int dim,
                      double* coeffs);

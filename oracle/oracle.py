@@ -56,6 +56,8 @@ def lib():
         L.orc_present_index.argtypes = [_dp, ctypes.c_int, ctypes.c_double]
         L.orc_hull2d_hrep.restype = ctypes.c_int
         L.orc_hull2d_hrep.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
+        L.orc_hull3d_hrep.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
+        L.orc_halfspace_contains.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, _dp]
         L.orc_hull2d_contains.restype = ctypes.c_int
         L.orc_hull2d_contains.argtypes = [_dp, _dp, ctypes.c_int, _dp]
         L.orc_quintic_fit.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, _dp]
@@ -170,6 +172,20 @@ def hull2d_hrep(pts, max_facets=8):
 
 def hull2d_contains(A, b, m, p):
     return bool(lib().orc_hull2d_contains(_d(_f64(A)), _d(_f64(b)), m, _d(_f64(p))))
+
+
+def hull3d_hrep(pts, max_facets=64):
+    """orc_hull3d_hrep: pts [p, 3] -> (A [max_facets, 3], b [max_facets], nfacets or -1)."""
+    pts = _f64(pts)
+    A = np.zeros((max_facets, 3))
+    b = np.zeros(max_facets)
+    m = lib().orc_hull3d_hrep(_d(pts), pts.shape[0], max_facets, _d(A), _d(b))
+    return A, b, m
+
+
+def halfspace_contains(A, b, m, p):
+    A = _f64(A)
+    return bool(lib().orc_halfspace_contains(_d(A), _d(_f64(b)), m, A.shape[-1], _d(_f64(p))))
 
 
 def quintic_fit(knots_t, knots_pva):

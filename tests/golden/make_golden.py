@@ -121,6 +121,27 @@ def hull3d():
                 A=eq[:, :3].tolist(), b=(-eq[:, 3]).tolist(), outside=[0.0, 0.0, 0.0])
 
 
+def hull3d_cases():
+    """Qhull planes of a few 3-D point sets: the reference test's 8 points, the unit cube (every
+    face coplanar: Qhull's "Qt" splits each into two triangles with one plane), a tetrahedron,
+    12 points on a sphere, 16 points in a box (some interior)."""
+    from scipy.spatial import ConvexHull
+    rng = np.random.default_rng(31)
+    sph = rng.normal(size=(12, 3))
+    sets = [np.array(hull3d()["points"]),
+            np.array([[x, y, z] for x in (0.0, 1.0) for y in (0.0, 1.0) for z in (0.0, 1.0)]),
+            np.array([[0.0, 0.0, 0.0], [1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]]),
+            sph / np.linalg.norm(sph, axis=1, keepdims=True),
+            rng.uniform(-1.0, 2.0, size=(16, 3))]
+    cases = []
+    for p in sets:
+        eq = ConvexHull(p).equations
+        cases.append(dict(points=p.tolist(), A=eq[:, :3].tolist(), b=(-eq[:, 3]).tolist()))
+    return dict(source="scipy.spatial.ConvexHull (Qhull 7.3.2, Qt always on); reference pins Qhull "
+                       "8.0.0 (src/Planners/CMakeLists.txt:22, ConvexHullHelper.cpp:54-58)",
+                cases=cases)
+
+
 def quintic():
     import sympy as sp
     rng = np.random.default_rng(7)
@@ -144,7 +165,7 @@ def quintic():
 if __name__ == "__main__":
     for name, fn in [("integrator_lti", integrator), ("contact_phases", contact_phases),
                      ("contact_list", contact_list), ("hull2d", hull2d),
-                     ("hull3d_reference", hull3d), ("quintic", quintic)]:
+                     ("hull3d_reference", hull3d), ("hull3d", hull3d_cases), ("quintic", quintic)]:
         with open(os.path.join(HERE, name + ".json"), "w") as f:
             json.dump(fn(), f, indent=1)
         print("wrote", name)

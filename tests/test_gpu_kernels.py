@@ -112,6 +112,72 @@ def test_hull2d_matches_oracle_and_qhull_fixture(handle, oracle):
         np.testing.assert_allclose(np.array(mine), np.array(ref), atol=1e-12)
 
 
+def _sets3d(B, P_, seed):
+    """3-D point sets for hull3d_kernel: points on spheres, boxes with interior points, cubes (flat
+    faces), flat sets, too few points, duplicates."""
+    rng = np.random.default_rng(seed)
+    pts = np.zeros((B, P_, 3))
+    npts = rng.integers(4, P_ + 1, B).astype(np.int32)
+    for i in range(B):
+        n = npts[i]
+        kind = i % 5
+        if kind == 0:
+            p = rng.normal(size=(n, 3))
+            p /= np.linalg.norm(p, axis=1, keepdims=True)
+        elif kind == 1:
+            p = rng.uniform(-1.0, 2.0, (n, 3))
+        elif kind == 2:
+            p = np.array([[x, y, z] for x in (0.0, 1.0) for y in (0.0, 1.0) for z in (0.0, 1.0)])
+            p = np.r_[p, rng.uniform(0.1, 0.9, (max(0, n - 8), 3))][:n] * rng.uniform(0.5, 2.0)
+            n = npts[i] = len(p)
+        elif kind == 3:
+            p = np.c_[rng.uniform(size=(n, 2)), np.full(n, 0.3)]        # flat: no hull
+        else:
+            p = rng.normal(size=(n, 3))
+            p[n // 2:] = p[:n - n // 2]                                   # duplicates
+        pts[i, :n] = p + rng.normal(size=3)
+    npts[5::17] = 3                                                       # too few points
+    return pts, npts
+
+
+@pytest.mark.parametrize("B,P_,M", [(1, 8, 32), (70, 16, 32), (130, 12, 8)])
+def test_hull3d_matches_oracle(handle, oracle, B, P_, M):
+    """hull3d_kernel (ConvexHullHelper on 3 x p points) bit for bit against orc_hull3d_hrep, which
+    tests/test_oracle.py pins to scipy's Qhull; halfspace_contains against the oracle."""
+    pts, npts = _sets3d(B, P_, seed=B + P_)
+    A, b, nf = handle.hull3d_hrep(_d(pts), _d(npts, torch.int32), M)
+    An, bn, nn = A.cpu().numpy(), b.cpu().numpy(), nf.cpu().numpy()
+    for i in range(B):
+        Ao, bo, mo = oracle.hull3d_hrep(pts[i, :npts[i]], M)
+        assert nn[i] == mo, i
+        np.testing.assert_array_equal(An[i], Ao)
+        np.testing.assert_array_equal(bn[i], bo)
+    rng = np.random.default_rng(B)
+    q = pts[:, :4].mean(axis=1) + rng.normal(0, 0.6, (B, 3))
+    inside = handle.halfspace_contains(A, b, nf, _d(q)).cpu().numpy()
+    for i in range(B):
+        assert inside[i] == oracle.halfspace_contains(An[i], bn[i], int(nn[i]), q[i])
+    ok = nn >= 0
+    assert ok.any() and (B == 1 or (~ok).any())
+    # every input point of a valid hull is inside exactly (b = max n . p)
+    for i in np.flatnonzero(ok):
+        p, a = pts[i, :npts[i], None, :], An[None, i, :nn[i], :]
+        nd = (p[..., 0] * a[..., 0] + p[..., 1] * a[..., 1]) + p[..., 2] * a[..., 2]
+        assert (nd <= bn[i, :nn[i]]).all()
+
+
+def test_halfspace_contains_2d_matches_hull2d_contains(handle):
+    """The dimension-generic containment test on the planner's 2-D polygons agrees with the 2-D one."""
+    rng = np.random.default_rng(5)
+    prob = P.make_batch(64, horizon=7, seed=3)
+    pts = prob["corners"][:, :8].reshape(-1, 8, 2)
+    npts = prob["ncorners"][:, :8].reshape(-1).astype(np.int32)
+    A, b, nf = handle.hull2d_hrep(_d(pts), _d(npts, torch.int32), 8)
+    q = _d(pts.mean(axis=1) + rng.normal(0, 0.08, (pts.shape[0], 2)))
+    np.testing.assert_array_equal(handle.halfspace_contains(A, b, nf, q).cpu().numpy(),
+                                  handle.hull2d_contains(A, b, nf, q).cpu().numpy())
+
+
 def test_hull2d_contains(handle, oracle):
     rng = np.random.default_rng(4)
     B = 4096

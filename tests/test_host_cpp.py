@@ -35,7 +35,8 @@ def test_host_bookkeeping_tests():
 @pytest.mark.gpu
 def test_host_device_tests():
     out = _run("gpu")
-    for name in ("Integrator - Linear system", "Convex Hull helper (2-D)", "QuinticSpline",
+    for name in ("Integrator - Linear system", "Convex Hull helper (2-D)",
+                 "Convex Hull helper (3-D, ConvexHullHelperTest.cpp)", "QuinticSpline",
                  "TimeVaryingDCMPlanner advance", "Continuous Contact",
                  "FloatingBaseSystemKinematics", "FloatingBaseDynamicalSystem"):
         assert any(line.startswith(name) and line.rstrip().endswith("ok") for line in out.splitlines()), out

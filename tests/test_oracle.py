@@ -118,6 +118,49 @@ def test_hull_matches_qhull_fixture():
         assert O.hull2d_contains(A, b, m, pts.mean(0))
 
 
+# ---- ConvexHullHelper (3-D) ------------------------------------------------------------------
+def _same_planes(A, b, Ar, br, tol=1e-9):
+    """Every plane of one set within tol of some plane of the other, both ways."""
+    X, Y = np.c_[A, b], np.c_[Ar, br]
+    d = np.abs(X[:, None, :] - Y[None, :, :]).max(axis=2)
+    return (d.min(axis=1) <= tol).all() and (d.min(axis=0) <= tol).all()
+
+
+def test_hull3d_matches_qhull_fixture():
+    """orc_hull3d_hrep against scipy's Qhull ("Qt"): the same planes (Qhull splits a flat face into
+    triangles that share one plane; here it is one row), every input point inside exactly."""
+    for c in _g("hull3d")["cases"]:
+        pts = np.array(c["points"])
+        A, b, m = O.hull3d_hrep(pts, 64)
+        Ar, br = np.array(c["A"]), np.array(c["b"])
+        assert m >= 4 and m <= len(Ar)
+        assert _same_planes(A[:m], b[:m], Ar, br)
+        nd = (pts[:, None, 0] * A[None, :m, 0] + pts[:, None, 1] * A[None, :m, 1]) + \
+            pts[:, None, 2] * A[None, :m, 2]            # the oracle's order (b = max n . p)
+        assert (nd <= b[:m]).all()
+        assert all(O.halfspace_contains(A[:m], b[:m], m, q) for q in pts)
+        assert not O.halfspace_contains(A[:m], b[:m], m, pts.mean(0) + 10.0)
+        np.testing.assert_allclose(np.linalg.norm(A[:m], axis=1), 1.0, atol=1e-14)
+    # the reference test's points and outside point (ConvexHullHelperTest.cpp:15-63)
+    r = _g("hull3d_reference")
+    A, b, m = O.hull3d_hrep(np.array(r["points"]), 64)
+    assert all(O.halfspace_contains(A[:m], b[:m], m, q) for q in r["points"])
+    assert not O.halfspace_contains(A[:m], b[:m], m, r["outside"])
+
+
+def test_hull3d_degenerate():
+    sq = np.array([[0.0, 0, 0.5], [1, 0, 0.5], [0, 1, 0.5], [1, 1, 0.5]])
+    assert O.hull3d_hrep(sq, 64)[2] == -1                       # flat
+    assert O.hull3d_hrep(sq[:3], 64)[2] == -1                   # fewer than 4 points
+    rng = np.random.default_rng(2)
+    sph = rng.normal(size=(16, 3))
+    sph /= np.linalg.norm(sph, axis=1, keepdims=True)
+    assert O.hull3d_hrep(sph, 8)[2] == -1                       # 28 planes > 8 slots
+    A, b, m = O.hull3d_hrep(np.r_[sph[:6], sph[:6]], 64)        # duplicated points
+    A1, b1, m1 = O.hull3d_hrep(sph[:6], 64)
+    assert m == m1 and _same_planes(A[:m], b[:m], A1[:m1], b1[:m1])
+
+
 def test_hull_padding_and_degenerate():
     A, b, m = O.hull2d_hrep(np.array([[0.0, 0], [1, 1], [2, 2]]), 8)   # collinear
     assert m == -1 and not A.any() and not b.any()
