@@ -808,20 +808,24 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
 // Stages the QP's facet slabs A [N][M][2], b [N][M] into LDS ([M][S] normals, [M][S] offsets,
 // facet i of knot k at i S + (k % KPL) NH + k / KPL), in the scalar type V: coalesced loads
 // (consecutive lanes on consecutive 16 B), U per lane in flight before the LDS stores.
-template <int KPL, int U, class V>
-__device__ __forceinline__ void stage_rows(const double* Ain, const double* bin, int64_t p, int N, int M, int S,
-                                           int NH, int lane, int t0, int nA, V* A2v, V* Bv)
+template <int U>
+__device__ __forceinline__ void stage_rows_issue(const double* Ain, const double* bin, int64_t p, int lane,
+                                                 int t0, int nA, double2 (&va)[U], double (&vb)[U])
 {
     const double2* As = reinterpret_cast<const double2*>(Ain) + p * nA;
     const double* bs = bin + p * nA;
-    double2 va[U];
-    double vb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
         const int t = min(t0 + u * kWave + lane, nA - 1);
         va[u] = As[t];
         vb[u] = bs[t];
     }
+}
+
+template <int KPL, int U, class V>
+__device__ __forceinline__ void stage_rows_commit(const double2 (&va)[U], const double (&vb)[U], int M, int S,
+                                                  int NH, int lane, int t0, int nA, V* A2v, V* Bv)
+{
     const bool pow2 = (M & (M - 1)) == 0;
     const int sh = __builtin_ctz(M);
 #pragma unroll
@@ -835,6 +839,16 @@ __device__ __forceinline__ void stage_rows(const double* Ain, const double* bin,
             Bv[o] = V(vb[u]);
         }
     }
+}
+
+template <int KPL, int U, class V>
+__device__ __forceinline__ void stage_rows(const double* Ain, const double* bin, int64_t p, int N, int M, int S,
+                                           int NH, int lane, int t0, int nA, V* A2v, V* Bv)
+{
+    double2 va[U];
+    double vb[U];
+    stage_rows_issue<U>(Ain, bin, p, lane, t0, nA, va, vb);
+    stage_rows_commit<KPL, U, V>(va, vb, M, S, NH, lane, t0, nA, A2v, Bv);
 }
 
 // ---- the phase-indexed input (blf_dcm_mpc_solve_phased) ----
@@ -1041,9 +1055,19 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
     constexpr int U = 2 * kMaxFacets;   // one round of 16 covers N M <= 1024
     double* sBE = smem + 3 * (size_t)M * S;                            // PH: [2][P]
     int32_t* sPh = reinterpret_cast<int32_t*>(sBE + 2 * (size_t)ps.P);  // PH: [N+1]
+    // The facet rows' loads are issued first and land in LDS only after the float LQ step, which
+    // does not read them: the step's arithmetic runs under the loads' latency (at launch every
+    // wave of the first round stages its rows at once).
+    // (KPL = 2 only: the one-knot-per-lane kernels would drop to 2 waves per SIMD.)
+    constexpr bool kOverlap = !PH && KPL == 2;
+    double2 va[U];
+    double vb[U];
     if (PH) {
         ph_stage_phases(ps, p, N, P.dt, lane, sBE, sPh);
         stage_rows_ph<KPL, U>(ps, sPh, p, N, M, S, NH, lane, A2d, Bv);
+    } else if (kOverlap) {
+        // issued below, after the knot loads: a wait for those (vmcnt counts in issue order) then
+        // leaves the younger row loads in flight
     } else {
         stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, 0, nA, A2d, Bv);
     }
@@ -1077,11 +1101,13 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
     }
     const double xi00 = xi_init[2 * p], xi01 = xi_init[2 * p + 1];
     const float xf00 = float(xi00), xf01 = float(xi01);
-    __syncthreads();   // the LDS rows (one wavefront: a wait for the stores)
+    if (kOverlap) stage_rows_issue<U>(Ain, bin, p, lane, 0, nA, va, vb);
     AS_STAMP_ADD(1, t_start);
     {
         AS_STAMP(t_q);
         as_lq_step<KPL, float>(F, Pf, N, lane, xf00, xf01);
+        if (kOverlap) stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, nA, A2d, Bv);
+        __syncthreads();   // the LDS rows (one wavefront: a wait for the stores)
         AS_STAMP_ADD(2, t_q);
         AS_STAMP(t_g);
         const double* const lw0[KPL] = {};
