@@ -1056,14 +1056,13 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
 #endif
 
     const int nA = N * M;
-    constexpr int U = 2 * kMaxFacets;   // one round of 16 covers N M <= 1024
+    constexpr int U = KPL == 2 ? 2 * kMaxFacets : kMaxFacets;   // N M <= 1024 / 512   // one round of 16 covers N M <= 1024
     double* sBE = smem + 3 * (size_t)M * S;                            // PH: [2][P]
     int32_t* sPh = reinterpret_cast<int32_t*>(sBE + 2 * (size_t)ps.P);  // PH: [N+1]
     // The facet rows' loads are issued first and land in LDS only after the float LQ step, which
     // does not read them: the step's arithmetic runs under the loads' latency (at launch every
     // wave of the first round stages its rows at once).
-    // (KPL = 2 only: the one-knot-per-lane kernels would drop to 2 waves per SIMD.)
-    constexpr bool kOverlap = !PH && KPL == 2;
+    constexpr bool kOverlap = !PH;
     double2 va[U];
     double vb[U];
     if (PH) {
