@@ -882,17 +882,15 @@ __device__ __forceinline__ void ph_stage_phases(const PhaseSrc& ps, int64_t p, i
 
 // stage_rows from the phase table: slot (k, i) = row i of knot k's phase (zeros outside every
 // phase).  The table rows are a few KB per problem, read through the caches.
-template <int KPL, int U>
-__device__ __forceinline__ void stage_rows_ph(const PhaseSrc& ps, const int32_t* sPh, int64_t p, int N, int M,
-                                              int S, int NH, int lane, double* A2v, double* Bv)
+template <int U>
+__device__ __forceinline__ void stage_rows_ph_issue(const PhaseSrc& ps, const int32_t* sPh, int64_t p, int N, int M,
+                                                    int lane, double2 (&va)[U], double (&vb)[U])
 {
     const int nA = N * M;
     const double2* As = reinterpret_cast<const double2*>(ps.A) + p * ps.P * M;
     const double* bs = ps.b + p * ps.P * M;
     const bool pow2 = (M & (M - 1)) == 0;
     const int sh = __builtin_ctz(M);
-    double2 va[U];
-    double vb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
         const int t = min(u * kWave + lane, nA - 1);
@@ -904,17 +902,16 @@ __device__ __forceinline__ void stage_rows_ph(const PhaseSrc& ps, const int32_t*
         va[u] = ph < 0 ? make_double2(0.0, 0.0) : a;
         vb[u] = ph < 0 ? 0.0 : b;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int t = u * kWave + lane;
-        if (t < nA) {
-            const int k = pow2 ? t >> sh : t / M, i = t - k * M;
-            const int o = i * S + (k % KPL) * NH + k / KPL;
-            A2v[2 * o] = va[u].x;
-            A2v[2 * o + 1] = va[u].y;
-            Bv[o] = vb[u];
-        }
-    }
+}
+
+template <int KPL, int U>
+__device__ __forceinline__ void stage_rows_ph(const PhaseSrc& ps, const int32_t* sPh, int64_t p, int N, int M,
+                                              int S, int NH, int lane, double* A2v, double* Bv)
+{
+    double2 va[U];
+    double vb[U];
+    stage_rows_ph_issue<U>(ps, sPh, p, N, M, lane, va, vb);
+    stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, N * M, A2v, Bv);
 }
 
 // A knot's own inputs: facet count, omega, references (vrp_ref_k, xi_ref_{k+1}).
@@ -1243,25 +1240,14 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     //      slab loads (one round, U per lane covers N M <= 128 x 8), then the knots' own loads,
     //      then the LDS stores, which wait for the slab loads only ----
     const int nA = N * M;
-    constexpr int U = (2 * kWave * kMaxFacets) / kWave;   // 16: nA <= 1024 in one round
+    constexpr int U = KPL == 2 ? 2 * kMaxFacets : kMaxFacets;   // one round: nA <= 1024 / 512
     double* sBE = smem + 3 * (size_t)M * S;                            // PH: [2][P]
     int32_t* sPh = reinterpret_cast<int32_t*>(sBE + 2 * (size_t)ps.P);  // PH: [N+1]
-    if (PH) {   // the rows from the phase table (the knots' loads then follow the LDS stores)
-        ph_stage_phases(ps, p, N, P.dt, lane, sBE, sPh);
-        stage_rows_ph<KPL, U>(ps, sPh, p, N, M, S, NH, lane, reinterpret_cast<double*>(A2), Bv);
-    }
-    double2 va[PH ? 1 : U];
-    double vb[PH ? 1 : U];
-    if (!PH) {
-        const double2* As = reinterpret_cast<const double2*>(Ain) + p * nA;
-        const double* bs = bin + p * nA;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
-            const int t = min(u * kWave + lane, nA - 1);
-            va[u] = As[t];
-            vb[u] = bs[t];
-        }
-    }
+    if (PH) ph_stage_phases(ps, p, N, P.dt, lane, sBE, sPh);
+    // the rows' loads are issued after the knots' loads (vmcnt counts in issue order) and land in
+    // LDS after the warm start's rollout, which does not read them
+    double2 va[U];
+    double vb[U];
 
     // ---- the knots this lane owns ----
     AKnot K[KPL];
@@ -1291,20 +1277,8 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
             Kj.xr1 = in.xr1;
         }
     }
-    if (!PH) {
-        const bool pow2 = (M & (M - 1)) == 0;
-        const int sh = __builtin_ctz(M);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int t = u * kWave + lane;
-            if (t < nA) {
-                const int k = pow2 ? t >> sh : t / M, i = t - k * M;
-                const int o = i * S + (k % KPL) * NH + k / KPL;
-                A2[o] = va[u];
-                Bv[o] = vb[u];
-            }
-        }
-    }
+    if (PH) stage_rows_ph_issue<U>(ps, sPh, p, N, M, lane, va, vb);
+    else stage_rows_issue<U>(Ain, bin, p, lane, 0, nA, va, vb);
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
         AKnot& Kj = K[j];
@@ -1318,7 +1292,6 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
         Kj.al = 1.0 + Kj.be;
     }
     const bool any_bad = __ballot(bad) != 0;
-    __syncthreads();   // the LDS slabs (one wavefront: a wait for the stores)
     AS_STAMP_ADD(1, t_start);
     const LdsRows<double> R{A2, Bv, S, NH};
 
@@ -1359,6 +1332,8 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
             K[j].x1 = x[j][1];
         }
     }
+    stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, nA, reinterpret_cast<double*>(A2), Bv);
+    __syncthreads();   // the LDS slabs (one wavefront: a wait for the stores)
     AS_STAMP_ADD(2, t_lq);
     if (any_bad) {
         status = BLF_QP_BAD_FACETS;
