@@ -73,11 +73,13 @@ __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
     const int nm = N * M;
     double2* oA = reinterpret_cast<double2*>(A) + q * nm;
     double* oB = b + q * nm;
+    const bool pow2 = (M & (M - 1)) == 0;
+    const int sh = __builtin_ctz(M);
     for (int j = tid; j < nm; j += kExpandBlock) {
-        const int k = j / M, i = j - k * M;
+        const int k = pow2 ? j >> sh : j / M, i = j - k * M;
         const int ph = sPh[k];
         st_stream(oA + j, ph >= 0 ? sA[ph * M + i] : make_double2(0.0, 0.0));
-        oB[j] = ph >= 0 ? sB[ph * M + i] : 0.0;
+        __builtin_nontemporal_store(ph >= 0 ? sB[ph * M + i] : 0.0, oB + j);
     }
     double2* oX = reinterpret_cast<double2*>(xi_ref) + q * (N + 1);
     double2* oR = reinterpret_cast<double2*>(vrp_ref) + q * N;
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
         st_stream(oX + k, ref);
         if (k < N) {
             st_stream(oR + k, ref);
-            oN[k] = ph >= 0 ? sNf[ph] : -1;
+            __builtin_nontemporal_store(ph >= 0 ? sNf[ph] : -1, oN + k);
         }
     }
 }
