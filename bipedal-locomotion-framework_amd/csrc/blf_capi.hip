@@ -510,6 +510,7 @@ blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* 
 {
     BLF_REQUIRE(handle != nullptr, "blf_dcm_posture_reference: null handle");
     BLF_REQUIRE(law != nullptr, "blf_dcm_posture_reference: null law");
+    BLF_REQUIRE(law->reserved == 0, "blf_dcm_posture_reference: reserved must be 0");
     BLF_REQUIRE(law->ndof >= 1 && law->ndof <= BLF_FBD_MAX_DOFS,
                 "blf_dcm_posture_reference: ndof=%d outside [1, %d]", law->ndof, BLF_FBD_MAX_DOFS);
     BLF_REQUIRE(law->q_nominal && law->lean, "blf_dcm_posture_reference: null law array");
@@ -527,6 +528,7 @@ blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_mo
                                              void* stream)
 {
     BLF_REQUIRE(impedance != nullptr, "blf_fbd_euler_integrate_impedance: null impedance");
+    BLF_REQUIRE(impedance->reserved == 0, "blf_fbd_euler_integrate_impedance: reserved must be 0");
     BLF_REQUIRE(impedance->kp && impedance->kd && (batch == 0 || impedance->q_ref),
                 "blf_fbd_euler_integrate_impedance: null impedance array");
     BLF_REQUIRE(model != nullptr && impedance->ndof == model->ndof,

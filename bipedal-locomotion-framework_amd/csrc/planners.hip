@@ -299,8 +299,12 @@ __global__ __launch_bounds__(256) void hull2d_contains_kernel(const double* __re
 {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= batch) return;
-    const int m = nf[q];
-    int in = m >= 0 ? 1 : 0;
+    // a count outside [0, M] is a bad polygon: nothing belongs to it, and no row past the
+    // problem's own M is read
+    const int m0 = nf[q];
+    const bool okm = m0 >= 0 && m0 <= M;
+    const int m = okm ? m0 : 0;
+    int in = okm ? 1 : 0;
     const double px = query[2 * q], py = query[2 * q + 1];
     for (int i = 0; i < m; ++i)
         if (A[(q * M + i) * 2] * px + A[(q * M + i) * 2 + 1] * py > b[q * M + i]) in = 0;
@@ -404,8 +408,10 @@ __global__ __launch_bounds__(256) void halfspace_contains_kernel(const double* _
 {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= batch) return;
-    const int m = nf[s];
-    int in = m >= 0 ? 1 : 0;
+    const int m0 = nf[s];   // outside [0, M]: a bad hull, nothing belongs to it (as above)
+    const bool okm = m0 >= 0 && m0 <= M;
+    const int m = okm ? m0 : 0;
+    int in = okm ? 1 : 0;
     const double* p = query + s * dim;
     for (int i = 0; i < m; ++i) {
         double v = 0.0;

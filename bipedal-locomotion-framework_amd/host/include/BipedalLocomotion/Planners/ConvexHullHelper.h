@@ -9,7 +9,8 @@
  * distinct supporting plane, where Qhull "Qt" may give a split face twice — Qhull's facet order is
  * internal to Qhull, so only the SET of planes is comparable).  doesPointBelongToConvexHull runs
  * blf_hull2d_contains / blf_halfspace_contains (strict `>` rejects, no tolerance).  Other row
- * counts are rejected with false.
+ * counts are rejected with false.  After a failed buildConvexHull (where Qhull would have thrown),
+ * doesPointBelongToConvexHull returns false for every point instead of testing an empty H-rep.
  */
 #ifndef BLF_BIPEDAL_LOCOMOTION_PLANNERS_CONVEX_HULL_HELPER_H
 #define BLF_BIPEDAL_LOCOMOTION_PLANNERS_CONVEX_HULL_HELPER_H
@@ -31,6 +32,7 @@ class ConvexHullHelper
     blf::VectorXd m_b;
     blf::DeviceBuffer<double> m_dPts, m_dA, m_dB, m_dQ;
     blf::DeviceBuffer<int32_t> m_dN, m_dInside;
+    bool m_valid{false};   // the last buildConvexHull succeeded (a failed build rejects every point)
     bool buildConvexHull3(const blf::MatrixXd& points);
 
 public:

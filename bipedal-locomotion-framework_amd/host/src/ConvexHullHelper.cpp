@@ -58,7 +58,8 @@ bool ConvexHullHelper::buildConvexHull3(const blf::MatrixXd& points)
 
 bool ConvexHullHelper::buildConvexHull(const blf::MatrixXd& points)
 {
-    if (points.rows() == 3) return buildConvexHull3(points);
+    m_valid = false;
+    if (points.rows() == 3) return m_valid = buildConvexHull3(points);
     if (points.rows() != 2)
     {
         std::cerr << "[ConvexHullHelper::buildConvexHull] Only 2-D and 3-D point sets are "
@@ -112,6 +113,7 @@ bool ConvexHullHelper::buildConvexHull(const blf::MatrixXd& points)
         m_A(i, 1) = A[2 * i + 1];
         m_b(i) = b[i];
     }
+    m_valid = true;
     return true;
 }
 
@@ -120,6 +122,13 @@ bool ConvexHullHelper::doesPointBelongToConvexHull(const blf::VectorXd& point) c
     if (point.size() != m_A.cols())
     {
         std::cerr << "[ConvexHullHelper::doesPointBelongToConvexHull] Unexpected size of the point."
+                  << std::endl;
+        return false;
+    }
+    if (!m_valid)
+    {
+        std::cerr << "[ConvexHullHelper::doesPointBelongToConvexHull] No convex hull: the last "
+                     "buildConvexHull failed or was never called."
                   << std::endl;
         return false;
     }

@@ -300,6 +300,13 @@ static void testConvexHull3()
     blf::MatrixXd flat(3, 4);
     for (int j = 0; j < 4; ++j) { flat(0, j) = j & 1; flat(1, j) = j >> 1; flat(2, j) = 0.5; }
     REQUIRE_FALSE(helper.buildConvexHull(flat));
+    // ... and after the failed build no point belongs to the (absent) hull, not even one that was
+    // inside the previous hull (no vacuous "inside" from an empty H-representation)
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{p(0, 0), p(1, 0), p(2, 0)}));
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.5, 0.5, 0.5}));
+    // a never-built helper rejects too
+    ConvexHullHelper fresh;
+    REQUIRE_FALSE(fresh.doesPointBelongToConvexHull(blf::VectorXd{0.0, 0.0}));
 }
 
 // ---- QuinticSpline (device) -------------------------------------------------------------------

@@ -126,7 +126,8 @@ blf_status blf_hull2d_hrep(blf_handle* handle, const double* pts, const int32_t*
 
 /* doesPointBelongToConvexHull: inside[q] = 1 iff for all rows i < nfacets: (A p)_i <= b_i
  * (strict `>` rejects, no tolerance, ConvexHullHelper.cpp:110-114).  One query point per polygon:
- * query: [B][2], inside: [B] int32.  A polygon with nfacets < 0 gives 0.                      */
+ * query: [B][2], inside: [B] int32.  A polygon with nfacets < 0 or nfacets > max_facets gives 0
+ * (a bad polygon: no row past its own max_facets is read).                                     */
 blf_status blf_hull2d_contains(blf_handle* handle, const double* A, const double* b,
                                const int32_t* nfacets, int32_t max_facets, const double* query,
                                int64_t batch, int32_t* inside, void* stream);
@@ -145,7 +146,7 @@ blf_status blf_hull3d_hrep(blf_handle* handle, const double* pts, const int32_t*
 
 /* doesPointBelongToConvexHull in `dim` dimensions: A: [B][max_facets][dim], b: [B][max_facets],
  * query: [B][dim]; inside[q] = 1 iff no row i < nfacets has (A p)_i > b_i (sum in column order
- * from 0.0).  nfacets < 0 gives 0.                                                            */
+ * from 0.0).  nfacets < 0 or nfacets > max_facets gives 0.                                      */
 blf_status blf_halfspace_contains(blf_handle* handle, const double* A, const double* b,
                                   const int32_t* nfacets, int32_t dim, int32_t max_facets,
                                   const double* query, int64_t batch, int32_t* inside,
@@ -427,7 +428,7 @@ blf_status blf_fb_dcm(blf_handle* handle, const blf_fb_model* model, const blf_f
  *   impedance of blf_fbd_euler_integrate_impedance tracks them.                               */
 typedef struct blf_posture_law {
     int32_t ndof;                 /* n                                                       */
-    int32_t reserved;
+    int32_t reserved;             /* must be 0                                               */
     const double* q_nominal;      /* [n]                                                     */
     const double* lean;           /* [n][2] joint offset per metre of (r0 - c)              */
 } blf_posture_law;
@@ -442,7 +443,7 @@ blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* 
  * joint-level controller faster than the planner, in one launch.                             */
 typedef struct blf_joint_impedance {
     int32_t ndof;                 /* n, must match the model                                 */
-    int32_t reserved;
+    int32_t reserved;             /* must be 0                                               */
     const double* kp;             /* [n]                                                     */
     const double* kd;             /* [n]                                                     */
     const double* q_ref;          /* [B][n]                                                  */

@@ -40,7 +40,9 @@ def build():
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+        # BLF_ORACLE_LIB: another build of the same sources (the ASan/UBSan build of
+        # `make -C oracle asan`, run by tests/test_sanitizers.py under LD_PRELOAD=libasan)
+        path = os.environ.get("BLF_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)

@@ -78,3 +78,19 @@ def test_lib_loads_after_torch_runtime():
     code = ("import sys; sys.path.insert(0, 'bipedal-locomotion-framework_amd'); "
             "from blf import native; native.lib(); assert 'torch' in sys.modules")
     subprocess.check_call([sys.executable, "-c", code], cwd=ROOT)
+
+
+def test_reserved_fields_must_be_zero():
+    """blf_posture_law.reserved and blf_joint_impedance.reserved are checked like the QP structs'
+    (argument validation before any device work; the handle is only compared with null there)."""
+    L = native.lib()
+    fake_handle = ctypes.c_void_p(1)
+    law = native.PostureLaw()
+    law.ndof, law.reserved = 3, 1
+    rc = L.blf_dcm_posture_reference(fake_handle, ctypes.byref(law), None, None, 2, 0, None, None)
+    assert rc == 1 and "reserved" in native.last_error()
+    imp = native.JointImpedance()
+    imp.ndof, imp.reserved = 3, 7
+    rc = L.blf_fbd_euler_integrate_impedance(None, None, None, ctypes.byref(imp), None, None, 0,
+                                             0.0, 1.0, 0.1, None)
+    assert rc == 1 and "reserved" in native.last_error()
