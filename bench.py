@@ -291,7 +291,10 @@ def main():
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
                        "max_facets": M,
                        "parallelism": f"shard{world} (independent problems)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            # "bound": the roof that binds the kernel as measured (VALU issue and latency,
+            # DESIGN.md 3.1), not HBM; achieved / peak / frac stay the HBM stream the contract
+            # prices (algorithmic bytes over the kernel time against 8 TB/s)
+            "roofline": {"bound": "valu_issue", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": "dcm_mpc_cold_kernel<2> (fp32 active-set search + fp64 "
@@ -458,7 +461,8 @@ def closed_loop(args):
     assert finite, "non-finite robot state in the closed loop"
     stat = torch.bincount(torch.stack(statuses).flatten().to(torch.int64), minlength=4).cpu().numpy()
     z = loop.state["base_pos"][:, 2]
-    nsteps = int(np.ceil(loop.dt / loop.dT))
+    nsteps = len(loop.steps)
+    robot_ms = sum(loop.steps) * 1e3
     if rank == 0:
         line = {"metric": "closed-loop control periods/sec (DCM-MPC + 30-DoF floating-base "
                           "dynamics with 2 ContinuousContactModel feet, configs[4])",
@@ -470,9 +474,12 @@ def closed_loop(args):
                                      "numerical": int(stat[2]), "bad_facets": int(stat[3])},
                 "state_finite": finite,
                 "base_height_range": [float(z.min()), float(z.max())],
-                "config": {"workload": f"configs[4]: {B} robots per GPU x {world} GPU(s), 20 ms control "
+                "robot_time_per_period_ms": robot_ms,
+                "config": {"workload": f"configs[4]: {B} robots per GPU x {world} GPU(s), {loop.dt * 1e3:g} ms control "
                                        f"period = one knot of a horizon-{N} warm-started plan + "
-                                       f"{nsteps} ForwardEuler steps of the 6+24 DoF dynamics",
+                                       f"{nsteps} ForwardEuler steps of the 6+24 DoF dynamics "
+                                       f"(integrate(0, {loop.T * 1e3:g} ms) at dT = {loop.dT * 1e3:g} ms: "
+                                       f"{robot_ms:g} ms of robot time, the reference schedule)",
                            "batch_per_gpu": B, "parallelism": f"shard{world} (independent robots)"}}
         if not args.no_cpu:
             line["cpu_baseline"] = closed_loop_cpu(args, model, N)
@@ -482,9 +489,10 @@ def closed_loop(args):
         dist.destroy_process_group()
 
 
-def pipeline_cpu(N, B=4096):
-    """configs[2] on the CPU, a bounded sample of B problems, the same stages as the device step,
-    each on every CPU this process may use (the oracle's C batch drivers, no Python per item):
+def pipeline_cpu(N, B=65536):
+    """configs[2] on the CPU: the SAME 65 536 problems as the device step (same generator, seed and
+    size), the same stages, each on every CPU this process may use (the oracle's C batch drivers,
+    no Python per item):
     the hull of every phase polygon, the phase expansion of every window, the QPs (sequential
     recursions, one problem per thread) and the swing splines (fit + 32 queries)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -516,11 +524,11 @@ def pipeline_cpu(N, B=4096):
         return t1 - t0, t2 - t1, t3 - t2
 
     run()   # warm-up
-    reps = sorted((run() for _ in range(7)), key=sum)
+    reps = sorted((run() for _ in range(3)), key=sum)
     (ta, tb, tc) = reps[len(reps) // 2]          # the median run
     el = ta + tb + tc
     return {"value": B / el, "unit": "QP/s", "cores": threads, "kind": "port",
-            "sample": f"{B} problems on {threads} threads, median of 7 runs after a warm-up: "
+            "sample": f"the device step's {B} problems on {threads} threads, median of 3 runs after a warm-up: "
                       f"{Bq * Pn} phase hulls + {B} window expansions {ta:.3f} s, QPs {tb:.3f} s "
                       f"(oracle sequential mode), {kt.shape[0]} splines x 32 queries {tc:.3f} s "
                       f"(oracle C batch drivers)"}
@@ -690,7 +698,9 @@ def receding_horizon(args, h, dev):
     params.tol_polish = args.tol_polish if args.tol_polish is not None else 1e-4
     stream = torch.cuda.current_stream()
     state = dict(xi0=t("xi_init").clone(), prev=None, s=0)
-    bufs = [None, None]
+    # one output buffer per window (S x ~39 MB at B = 4096), so that every window's statuses and
+    # iteration counts survive to the checks after the clock stops, with no copy in the timed loop
+    bufs = [None] * S
     iters = []
     evs = []
 
@@ -700,7 +710,7 @@ def receding_horizon(args, h, dev):
         if timed:
             evs.append(ev)
             ev[0].record(stream)
-        cur = s % 2
+        cur = s
         warm = None
         if state["prev"] is not None:
             warm = dict(vrp=state["prev"]["vrp"], lam=state["prev"]["lam"], shift=1, floor=1e-3)
@@ -725,7 +735,7 @@ def receding_horizon(args, h, dev):
         state["prev"] = out
         state["s"] = s + 1
         if timed:
-            iters.append(out["iters"].clone())   # the two output buffers are reused
+            iters.append(out["iters"])
 
     for _ in range(args.warmup):
         step()
@@ -744,13 +754,17 @@ def receding_horizon(args, h, dev):
     torch.cuda.synchronize()
     expand_ms = [e[0].elapsed_time(e[1]) for e in evs]
     solve_ms = [e[2].elapsed_time(e[3]) for e in evs]
-    assert int((state["prev"]["status"] != 0).sum()) == 0, "unsolved QPs in a window"
+    # every window of the run (warmup, timed, bookkeeping): solved
+    statuses = torch.stack([bufs[i]["status"] for i in range(state["s"])])
+    unsolved = int((statuses != 0).sum())
+    assert unsolved == 0, f"{unsolved} unsolved QPs over {state['s']} windows"
     it = torch.stack(iters).float()
     Pn = table["phase_begin"].shape[1]
     line = {"metric": "receding-horizon DCM-MPC advance()/sec (phase expansion + warm-started QP)",
             "value": B / sec, "unit": "QP/s", "n_gpus": 1, "ms_per_step": sec * 1e3,
             "steps": args.steps, "warmup": args.warmup, "dtype": "f64",
             "mean_ipm_iters_warm": float(it.mean()),
+            "windows_checked": {"windows": state["s"], "qps": state["s"] * B, "unsolved": unsolved},
             # events around the solve call in the untimed bookkeeping pass: the GPU waits there
             # for the host's next launch, so this is an upper bound on the solve's kernel time
             "solve_event_ms_median": sorted(solve_ms)[len(solve_ms) // 2],

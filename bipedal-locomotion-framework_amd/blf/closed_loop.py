@@ -14,19 +14,49 @@ One control period of this loop, stream-ordered on the device for a batch of rob
                      previous period's solution (blf_dcm_mpc_solve_warm, shift 1);
   3. plan -> robot:  joint references from the plan's first VRP and the centre of mass, held over
                      the period (blf_dcm_posture_reference);
-  4. robot:          ForwardEuler<FloatingBaseDynamicalSystem>::integrate over the period with a
+  4. robot:          ForwardEuler<FloatingBaseDynamicalSystem>::integrate(0, dt - dT) with a
                      joint impedance tracking them as the control input of every step
-                     (blf_fbd_euler_integrate_impedance, contacts at the feet).
+                     (blf_fbd_euler_integrate_impedance, contacts at the feet): the reference
+                     schedule integrates T + dT (period_final_time), so the robot advances
+                     exactly dt, one knot of the plan, per period.
 
 The control period is the plan's knot spacing dt (the window moves one knot per period); the
 impedance runs at the integration step dT (1 kHz): a 50 Hz zero-order hold of the joint
 torques does not stabilise the robot's fast modes.  Every piece runs on the device; the host only
 enqueues.
 """
+import math
+
 import numpy as np
 
 from . import native
 from . import robot as R
+
+
+def fixed_step_schedule(t0, t1, dT):
+    """The step sizes FixedStepIntegrator::integrate(t0, t1) takes (FixedStepIntegrator.tpp:48-64;
+    blf_capi.hip step_schedule): iterations = ceil((t1 - t0) / dT), steps 0..iterations-2 of dT,
+    the last one t1 - currentTime with the stale currentTime = t0 + dT (iterations - 2)."""
+    iters = int(math.ceil((t1 - t0) / dT))
+    cur = t0 + dT * (iters - 2) if iters >= 2 else t0
+    return [dT] * (iters - 1) + [t1 - cur]
+
+
+def period_final_time(dt, dT):
+    """The final time T of integrate(0, T) that advances the robot by exactly one knot dt.
+
+    With two or more iterations the reference schedule above integrates T + dT, not T: its last
+    step runs from the START of the previous step (the stale currentTime).  integrate(0, dt) would
+    therefore advance the robot dt + dT per period (21 ms at dt = 20 ms, dT = 1 ms) while the plan
+    moves one 20 ms knot.  The loop keeps the reference call and its schedule, and asks for
+    T = dt - dT: (iterations - 1) steps of dT and a last step of 2 dT (or iterations - 1 steps and
+    a last dT when the quotient rounds up), dt in total."""
+    T = dt - dT
+    if not T > dT:
+        raise ValueError(f"the control period {dt} needs at least two integration steps of {dT}")
+    total = math.fsum(fixed_step_schedule(0.0, T, dT))
+    assert abs(total - dt) <= 1e-12 * dt, (total, dt)
+    return T
 
 # ContinuousContactModel of each sole (length, width, spring_coeff, damper_coeff): the reference
 # test's foot size; stiffness and damping for a 50 kg robot on two 0.12 x 0.09 m soles (about
@@ -46,6 +76,8 @@ class ClosedLoop:
         dev = torch.device("cuda", h.device)
         t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
         self.dt = float(plan["dt"])
+        self.T = period_final_time(self.dt, dT)      # integrate(0, T) advances the robot dt
+        self.steps = fixed_step_schedule(0.0, self.T, dT)
         self.B = plan["omega"].shape[0]
         self.dm = h.fb_model(model)
         law = law if law is not None else R.posture_law_arrays(model)
@@ -80,7 +112,9 @@ class ClosedLoop:
                  stream=self.stream)
         warm = None
         if self.prev is not None:
-            warm = dict(vrp=self.prev["vrp"], lam=self.prev["lam"], shift=1, floor=1e-3)
+            # a robot whose previous window was not solved (status != 0) is planned cold
+            warm = dict(vrp=self.prev["vrp"], lam=self.prev["lam"], shift=1, floor=1e-3,
+                        status=self.prev["status"])
         if N <= 128 and not self.expand_path:   # the window read from the phase table
             out = h.dcm_mpc_solve_phased(self.table, s, self.xi, self.omega[:, s:s + N],
                                          self.params, warm=warm, out=self.bufs[s % 2],
@@ -92,9 +126,11 @@ class ClosedLoop:
                                   lambda_out=True, stream=self.stream)
         self.bufs[s % 2] = out
         h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=self.stream)
-        # integrate(0, dt): the dynamics are time-invariant, and a fixed interval keeps the
-        # FixedStepIntegrator step count (ceil((T - t0) / dT)) the same in every period
-        h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.dt,
+        # integrate(0, T) with T = dt - dT: the reference schedule integrates T + dT, so the robot
+        # advances exactly one knot dt per period, in step with the plan (period_final_time); the
+        # dynamics are time-invariant, and a fixed interval keeps the step count the same in every
+        # period
+        h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T,
                                         self.dT, contacts=self.contacts, stream=self.stream)
         self.prev = out
         self.s = s + 1

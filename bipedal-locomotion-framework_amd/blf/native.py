@@ -98,7 +98,18 @@ class DcmMpcWindow(ctypes.Structure):
 
 class DcmMpcWarmStart(ctypes.Structure):
     _fields_ = [("vrp", _vp), ("lambda_", _vp), ("shift", _i32), ("reserved", _i32),
-                ("floor", _f64)]
+                ("floor", _f64), ("prev_status", _vp)]
+
+
+def _warm_start(warm, B, N, M):
+    """blf_dcm_mpc_warm_start from a dict: vrp [B,N,2], lam [B,N,M], shift, floor and optionally
+    status [B] int32 (the previous solve's statuses: problems with status != 0 start cold)."""
+    torch = _torch()
+    st = warm.get("status")
+    return DcmMpcWarmStart(_ptr(warm["vrp"], torch.float64, (B, N, 2), "warm vrp"),
+                           _ptr(warm["lam"], torch.float64, (B, N, M), "warm lam"),
+                           int(warm.get("shift", 1)), 0, float(warm.get("floor", 1e-2)),
+                           _ptr(st, torch.int32, (B,), "warm status") if st is not None else None)
 
 
 _LIB = None
@@ -415,9 +426,7 @@ class Handle:
             _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
         ws = None
         if warm is not None:
-            ws = DcmMpcWarmStart(_ptr(warm["vrp"], torch.float64, (B, N, 2), "warm vrp"),
-                                 _ptr(warm["lam"], torch.float64, (B, N, M), "warm lam"),
-                                 int(warm.get("shift", 1)), 0, float(warm.get("floor", 1e-2)))
+            ws = _warm_start(warm, B, N, M)
         lam_ptr = None
         if lambda_out:
             if "lam" not in out:
@@ -542,9 +551,7 @@ class Handle:
             _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
         ws = None
         if warm is not None:
-            ws = DcmMpcWarmStart(_ptr(warm["vrp"], torch.float64, (B, N, 2), "warm vrp"),
-                                 _ptr(warm["lam"], torch.float64, (B, N, M), "warm lam"),
-                                 int(warm.get("shift", 1)), 0, float(warm.get("floor", 1e-2)))
+            ws = _warm_start(warm, B, N, M)
         lam_ptr = None
         if lambda_out:
             if "lam" not in out:

@@ -291,7 +291,8 @@ blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* 
         BLF_REQUIRE(warm->reserved == 0, "blf_dcm_mpc_solve_warm: reserved must be 0");
         BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
                     "blf_dcm_mpc_solve_warm: floor must be finite and > 0");
-        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out,
+        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out &&
+                        (warm->prev_status == nullptr || warm->prev_status != solution->status),
                     "blf_dcm_mpc_solve_warm: warm-start buffers must not alias the outputs");
     }
     return launch_dcm_mpc(params, problem, warm, batch, solution, lambda_out, (hipStream_t)stream);
@@ -345,7 +346,8 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
         BLF_REQUIRE(warm->reserved == 0, "blf_dcm_mpc_solve_phased: reserved must be 0");
         BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
                     "blf_dcm_mpc_solve_phased: floor must be finite and > 0");
-        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out,
+        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out &&
+                        (warm->prev_status == nullptr || warm->prev_status != solution->status),
                     "blf_dcm_mpc_solve_phased: warm-start buffers must not alias the outputs");
     }
     return launch_dcm_mpc_phased(params, ph, start_knot, xi_init, omega, omega_stride, warm, batch,

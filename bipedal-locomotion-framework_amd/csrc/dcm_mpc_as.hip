@@ -94,6 +94,25 @@ struct LdsRows<double> {
     int S, NH;
     __device__ int col(int j, int lane) const { return j * NH + lane; }
 };
+template <>
+struct LdsRows<float> {
+    const float2* A2;
+    const float* Bv;
+    int S, NH;
+    __device__ int col(int j, int lane) const { return j * NH + lane; }
+};
+
+// Diagnostic builds only (tools/build_variant.sh): BLF_AS_EXPA = the cold kernel's fp32 search
+// alone, with float rows in LDS; BLF_AS_MINWAVES = its __launch_bounds__ waves per SIMD.
+#ifndef BLF_AS_EXPA
+#define BLF_AS_EXPA 0
+#endif
+#ifndef BLF_AS_MINWAVES
+#define BLF_AS_MINWAVES 2
+#endif
+#ifndef BLF_AS_OVERLAP
+#define BLF_AS_OVERLAP 1
+#endif
 
 // One facet row (normal, offset) in the scalar type of the pass.
 template <class T>
@@ -1028,14 +1047,16 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
 // when none certifies, the fp64 LQ optimum from (xi_ref, vrp_ref) becomes the IPM's start point.
 // Measured alternatives: float rows in LDS with phase B reading fp64 rows from
 // global memory, at 2 / 3 / 4 waves per SIMD, and phase A as a kernel of its own — all slower.
+// The cold solve of one QP (the cold kernel's body; the warm kernel runs it for the problems whose
+// previous solve failed, blf_dcm_mpc_warm_start.prev_status).
 template <int KPL, bool LAMOUT, bool PH, bool PAD>
-__global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
-    KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
+__device__ __forceinline__ void cold_solve(
+    const KParams& P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
     const double* __restrict__ Ain, const double* __restrict__ bin,
     const int32_t* __restrict__ nfacets, double* __restrict__ xi_out, double* __restrict__ vrp_out,
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
-    double* __restrict__ lam_out, PhaseSrc ps)
+    double* __restrict__ lam_out, const PhaseSrc& ps)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
@@ -1059,7 +1080,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
     // The facet rows' loads are issued first and land in LDS only after the float LQ step, which
     // does not read them: the step's arithmetic runs under the loads' latency (at launch every
     // wave of the first round stages its rows at once).
-    constexpr bool kOverlap = !PH;
+    constexpr bool kOverlap = !PH && BLF_AS_OVERLAP && !BLF_AS_EXPA;
     double2 va[U];
     double vb[U];
     if (PH) {
@@ -1068,10 +1089,17 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
     } else if (kOverlap) {
         // issued below, after the knot loads: a wait for those (vmcnt counts in issue order) then
         // leaves the younger row loads in flight
+    } else if (BLF_AS_EXPA) {
+        stage_rows<KPL, U, float>(Ain, bin, p, N, M, S, NH, lane, 0, nA, reinterpret_cast<float*>(smem),
+                                  reinterpret_cast<float*>(smem) + 2 * (size_t)M * S);
     } else {
         stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, 0, nA, A2d, Bv);
     }
+#if BLF_AS_EXPA
+    const LdsRows<float> R{reinterpret_cast<const float2*>(smem), reinterpret_cast<const float*>(smem) + 2 * (size_t)M * S, S, NH};
+#else
     const LdsRows<double> R{reinterpret_cast<const double2*>(A2d), Bv, S, NH};
+#endif
 
     // ---- phase A: the float search (facet counts clamped; a bad count is reported below) ----
     AKnotT<float> F[KPL];
@@ -1120,6 +1148,20 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
         AS_STAMP_ADD(13, t_a);
     }
 
+#if BLF_AS_EXPA
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const int k = KPL * lane + j;
+        if (k < N) {
+            vrp_out[2 * (p * N + k)] = F[j].r0;
+            vrp_out[2 * (p * N + k) + 1] = F[j].r1;
+            xi_out[2 * (p * (N + 1) + k + 1)] = F[j].x0;
+            xi_out[2 * (p * (N + 1) + k + 1) + 1] = F[j].x1;
+        }
+    }
+    if (lane == 0) status_out[p] = 0;
+    return;
+#endif
     // ---- phase B: the fp64 passes from the float point ----
     AS_STAMP(t_b);
     const PT<double> Pd = params_d(P);
@@ -1206,6 +1248,19 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_cold_kernel(
 #endif
 }
 
+template <int KPL, bool LAMOUT, bool PH, bool PAD>
+__global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
+    KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
+    const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
+    const double* __restrict__ Ain, const double* __restrict__ bin,
+    const int32_t* __restrict__ nfacets, double* __restrict__ xi_out, double* __restrict__ vrp_out,
+    int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
+    double* __restrict__ lam_out, PhaseSrc ps)
+{
+    cold_solve<KPL, LAMOUT, PH, PAD>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+                                     status_out, iters_out, polished_out, lam_out, ps);
+}
+
 // ---- the warm-start kernel ("Warm start") ----
 // One wavefront per QP, fp64 facet rows in LDS.  From the shifted previous solution (xi rolled
 // out from its VRPs), guess = the facets the rollout violates plus those whose previous multiplier
@@ -1223,6 +1278,13 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
+    // a problem whose previous solve failed (prev_status != 0) is not warm-started from it: it is
+    // solved exactly as a cold launch solves it (the IPM's stage 2 treats it as cold too)
+    if (P.ws_status != nullptr && P.ws_status[blockIdx.x] != 0) {
+        cold_solve<KPL, LAMOUT, PH, PAD>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+                                         status_out, iters_out, polished_out, lam_out, ps);
+        return;
+    }
     assume_pad<KPL, PAD>(N);
     const int NH = (N + KPL - 1) / KPL;   // lanes holding knots
     const int S = KPL * NH;               // LDS row stride: facet i of slot j, lane l at i S + j NH + l
@@ -1380,7 +1442,8 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     const size_t slots = (size_t)kp.M * (KPL * ((kp.N + KPL - 1) / KPL));
     const PhaseSrc none{};
     const PhaseSrc& src = ps ? *ps : none;
-    const size_t lds = 3 * sizeof(double) * slots + (ps ? ph_lds_bytes(ps->P, kp.N) : 0) + AS_EXTRA_LDS;
+    const size_t lds = 3 * (BLF_AS_EXPA && !warm ? sizeof(float) : sizeof(double)) * slots +
+                       (ps ? ph_lds_bytes(ps->P, kp.N) : 0) + AS_EXTRA_LDS;
     if (lds > 64 * 1024)
         return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: %zu B of LDS (%d phases)", lds, ps ? ps->P : 0);
     const bool pad = KPL == 2 && kp.N <= 2 * kWave - 2;

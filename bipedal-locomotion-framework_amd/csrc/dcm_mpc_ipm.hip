@@ -600,7 +600,9 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     const int64_t p = blockIdx.x;
     // after the active-set kernel (dcm_mpc_as.hip): only the QPs it handed over
     if (P.stage2 && status_out[p] != kPending) return;
-    constexpr bool warm = WARM;                           // a separate instantiation each way
+    // a separate instantiation each way; in the warm one, a problem whose previous solve failed
+    // (KParams::ws_status) starts cold, as the cold instantiation would start it
+    const bool warm = WARM && !(P.ws_status != nullptr && P.ws_status[p] != 0);
     const bool ws = warm && k + P.ws_shift < N;           // this knot starts from the warm start
     STAMP(t_start);
 
@@ -1297,6 +1299,7 @@ KParams make_kparams(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_warm_start
     kp.tol_polish = prm->tol_polish;
     kp.ws_shift = warm ? warm->shift : 0;
     kp.ws_floor = warm ? warm->floor : 0.0;
+    kp.ws_status = warm ? warm->prev_status : nullptr;
     kp.stage2 = 0;
     kp.f_dt = (float)kp.dt;
     kp.f_Qw0 = (float)kp.Qw0; kp.f_Qw1 = (float)kp.Qw1;

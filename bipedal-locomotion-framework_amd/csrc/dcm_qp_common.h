@@ -14,6 +14,8 @@ constexpr int kPending = -1;      // status of a QP the active-set kernel hands 
 struct KParams {
     int N, M, max_iter;
     int ws_shift;        // warm start: knot k starts from knot k + ws_shift (ws_vrp != nullptr)
+    const int32_t* ws_status;   // warm start: [B] status of the previous solve, or nullptr; a
+                                // problem with ws_status != 0 starts cold (no warm start)
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_mu, tol_p, tol_d;
     double tol_polish;   // > 0: try the active-set polish once mu <= tol_polish
     double ws_floor;     // warm start: s, lambda >= ws_floor

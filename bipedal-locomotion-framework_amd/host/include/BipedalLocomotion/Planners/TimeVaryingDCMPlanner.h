@@ -87,7 +87,10 @@ class TimeVaryingDCMPlanner : public System::Advanceable<DCMPlanBatch>
     blf::DeviceBuffer<int32_t> m_dNPhases, m_dPhNCorners, m_dPhNf;
     blf::DeviceBuffer<double> m_dXi0, m_dOmega, m_dXiRef, m_dVrpRef, m_dA, m_dB, m_dWinOmega;
     blf::DeviceBuffer<double> m_dXi, m_dVrp[2], m_dLam[2];
-    blf::DeviceBuffer<int32_t> m_dNf, m_dStatus, m_dIters;
+    blf::DeviceBuffer<int32_t> m_dNf, m_dIters;
+    blf::DeviceBuffer<int32_t> m_dStatus[2];   // ping-pong with m_dVrp / m_dLam: the previous
+                                                // window's statuses are the next warm start's
+                                                // prev_status (a failed problem restarts cold)
 
     bool buildPhaseTable(blf_handle* h);
     bool checkWindow() const;

@@ -218,13 +218,19 @@ typedef struct blf_dcm_mpc_solution {
  * (shift = 1 after the window moved one knot):
  *   r_k = vrp[k + shift],  s_i = max(b_i - a_i r_k, floor),  lambda_i = max(lambda[k + shift][i], floor)
  * and the cold start's LQ step is skipped.  Knots with k + shift >= N are new to the window and
- * start cold (r_k = vrp_ref_k, s_i = max(b_i - a_i r_k, 1e-2), lambda_i = 1e-2 / s_i).                 */
+ * start cold (r_k = vrp_ref_k, s_i = max(b_i - a_i r_k, 1e-2), lambda_i = 1e-2 / s_i).
+ * prev_status (optional): the status of the solve that produced vrp / lambda.  A problem whose
+ * previous status is not BLF_QP_OK (e.g. BLF_QP_MAX_ITER) is not warm-started from that iterate:
+ * it is solved exactly as the cold start (warm == NULL) solves it, so one failed window does not
+ * poison the next (Advanceable::advance, System/include/BipedalLocomotion/System/Advanceable.h:24-46,
+ * is called again after a failure with the planner's previous state).                           */
 typedef struct blf_dcm_mpc_warm_start {
     const double* vrp;       /* [B][N][2]  VRPs of the previous solve (must not alias the output) */
     const double* lambda;    /* [B][N][M]  its multipliers (blf_dcm_mpc_solve_warm's lambda_out)  */
     int32_t shift;           /* >= 0                                                          */
     int32_t reserved;        /* must be 0                                                     */
     double floor;            /* > 0, e.g. 1e-2                                                */
+    const int32_t* prev_status; /* [B] or NULL (NULL: every problem warm-started)             */
 } blf_dcm_mpc_warm_start;
 
 /* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-16,

@@ -1697,6 +1697,7 @@ typedef struct {
     const double *xi_init, *omega, *xi_ref, *vrp_ref, *A, *b;
     const int32_t* nfacets;
     const double *vrp_ws, *lam_ws;
+    const int32_t* prev_status;
     int32_t shift;
     double floor;
     double *xi, *vrp, *lam_out;
@@ -1713,7 +1714,8 @@ static void* batch_worker(void* arg)
         if (p >= J->batch) break;
         orc_dcm_warm wm;
         const orc_dcm_warm* wp = NULL;
-        if (J->vrp_ws) {
+        /* a problem whose previous solve failed starts cold (blf_dcm_mpc_warm_start.prev_status) */
+        if (J->vrp_ws && !(J->prev_status && J->prev_status[p] != 0)) {
             wm.vrp = J->vrp_ws + (int64_t)2 * N * p;
             wm.lambda = J->lam_ws + (int64_t)N * M * p;
             wm.shift = J->shift;
@@ -1759,13 +1761,14 @@ void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int 
                                   const double* xi_init, const double* omega, const double* xi_ref,
                                   const double* vrp_ref, const double* A, const double* b,
                                   const int32_t* nfacets, const double* vrp_ws,
-                                  const double* lam_ws, int32_t shift, double floor, double* xi,
-                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters,
-                                  int32_t* polished)
+                                  const double* lam_ws, const int32_t* prev_status, int32_t shift,
+                                  double floor, double* xi, double* vrp, double* lam_out,
+                                  int32_t* status, int32_t* iters, int32_t* polished)
 {
     batch_job J = {.prm = prm, .batch = batch, .xi_init = xi_init, .omega = omega,
                    .xi_ref = xi_ref, .vrp_ref = vrp_ref, .A = A, .b = b, .nfacets = nfacets,
-                   .vrp_ws = vrp_ws, .lam_ws = lam_ws, .shift = shift, .floor = floor,
+                   .vrp_ws = vrp_ws, .lam_ws = lam_ws, .prev_status = prev_status, .shift = shift,
+                   .floor = floor,
                    .xi = xi, .vrp = vrp, .lam_out = lam_out, .status = status, .iters = iters,
                    .polished = polished};
     run_batch(&J, threads);

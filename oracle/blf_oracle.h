@@ -146,14 +146,15 @@ void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threa
                              const int32_t* nfacets, double* xi, double* vrp, int32_t* status,
                              int32_t* iters);
 /* Batch with warm starts: vrp_ws [B][N][2] and lam_ws [B][N][M] (both NULL: cold starts),
- * lam_out [B][N][M] or NULL, polished [B] or NULL. */
+ * prev_status [B] or NULL (a problem with prev_status != 0 is solved cold: the device's
+ * blf_dcm_mpc_warm_start.prev_status), lam_out [B][N][M] or NULL, polished [B] or NULL. */
 void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int threads,
                                   const double* xi_init, const double* omega, const double* xi_ref,
                                   const double* vrp_ref, const double* A, const double* b,
                                   const int32_t* nfacets, const double* vrp_ws,
-                                  const double* lam_ws, int32_t shift, double floor, double* xi,
-                                  double* vrp, double* lam_out, int32_t* status, int32_t* iters,
-                                  int32_t* polished);
+                                  const double* lam_ws, const int32_t* prev_status, int32_t shift,
+                                  double floor, double* xi, double* vrp, double* lam_out,
+                                  int32_t* status, int32_t* iters, int32_t* polished);
 
 /* Tree sum with the device's reduction order: c has n entries, padded with
  * zeros to 64*ceil(n/64); per 64-block xor-butterfly (distances 1, 2, 4, ..., 32), then block

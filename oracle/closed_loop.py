@@ -8,7 +8,8 @@ One control period, as blf.closed_loop.ClosedLoop.period() runs it on the device
   2. the plan window moved one knot: orc_dcm_phase_expand over the oracle hulls of the phases,
      solved warm from the previous period (orc_dcm_mpc_solve_warm, shift 1);
   3. q_ref = q_nom + lean (r0 - c_xy) with r0 the plan's first VRP;
-  4. ForwardEuler<FloatingBaseDynamicalSystem>::integrate(0, dt) of every robot with the control
+  4. ForwardEuler<FloatingBaseDynamicalSystem>::integrate(0, dt - dT) of every robot (dt of robot
+     time: the reference schedule integrates T + dT) with the control
      input tau = kp (q_ref - q) - kd qdot set before every step (FixedStepIntegrator.tpp:21-72,
      ForwardEuler.tpp:18-49 over FloatingBaseSystemDynamics.cpp:102-251, contacts
      ContinuousContactModel.cpp:79-108, through fb_dynamics.dynamics).
@@ -98,6 +99,10 @@ class OracleLoop:
         self.compiled, self.threads = compiled, threads
         self.model, self.N, self.dT = model, horizon, dT
         self.dt = float(plan["dt"])
+        # integrate(0, T) with T = dt - dT: the reference schedule (FixedStepIntegrator.tpp:48-64)
+        # integrates T + dT, so the robot advances exactly one knot per period (the device loop's
+        # blf.closed_loop.period_final_time, restated)
+        self.T = self.dt - dT
         self.law = law
         self.state = {k: np.array(v, dtype=np.float64) for k, v in states.items()
                       if k != "joint_torque"}
@@ -120,25 +125,26 @@ class OracleLoop:
             com, xi = dcm_from_state(self.model, self.state, omega[:, 0])
         w = O.dcm_phase_expand(self.table, s, self.dt, N)
         w.update(xi_init=xi, omega=omega)
-        pv, pl = (None, None) if self.prev is None else (self.prev["vrp"], self.prev["lam"])
+        pv, pl, ps = ((None, None, None) if self.prev is None else
+                      (self.prev["vrp"], self.prev["lam"], self.prev["status"]))
         pol = np.zeros(xi.shape[0], np.int32)
         st, xo, vrp, it, lam = O.dcm_mpc_solve_batch_warm(w, vrp_ws=pv, lam_ws=pl, shift=1, floor=1e-3,
                                                           params=self.params, threads=self.threads,
-                                                          polished=pol)
+                                                          polished=pol, prev_status=ps)
         q_ref = posture_reference(self.law, com, vrp)
         C = len(self.model["frame_link"])
         if self.compiled:
             self.state = O.fbd_euler_impedance_batch(self.model, self.state, q_ref, self.law["kp"],
                                                      self.law["kd"], self.cparams, self.null, 0.0,
-                                                     self.dt, self.dT, threads=self.threads)
+                                                     self.T, self.dT, threads=self.threads)
         for i in range(0 if self.compiled else xi.shape[0]):
             si = euler_integrate_impedance(self.model, self.state, i, q_ref[i], self.law["kp"],
-                                           self.law["kd"], 0.0, self.dt, self.dT,
+                                           self.law["kd"], 0.0, self.T, self.dT,
                                            contacts=list(range(C)), contact_params=self.cparams,
                                            null_poses=self.null[i])
             for k in self.state:
                 self.state[k][i] = si[k]
-        self.prev = dict(vrp=vrp, lam=lam)
+        self.prev = dict(vrp=vrp, lam=lam, status=st)
         self.s = s + 1
         return dict(status=st, xi=xo, vrp=vrp, iters=it, lam=lam, polished=pol, com=com,
                     xi_init=xi, q_ref=q_ref)

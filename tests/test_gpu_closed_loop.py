@@ -100,6 +100,34 @@ def test_fbd_euler_impedance_zero_gains_is_plain_euler(handle):
         np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy())
 
 
+def test_closed_loop_period_advances_one_knot_of_robot_time(handle):
+    """The loop's period integrates exactly one knot dt of robot time (ClosedLoop.T = dt - dT: the
+    reference FixedStepIntegrator schedule integrates T + dT, FixedStepIntegrator.tpp:48-64).
+    Measured on the device: robots in free fall (no contacts, zero gains, at rest), whose base
+    velocity after ForwardEuler is -g times the integrated time, exactly up to rounding."""
+    B = 8
+    plan, st = _setup(B, 2)
+    loop = DL.ClosedLoop(handle, MODEL, plan, st, horizon=100)
+    assert abs(sum(loop.steps) - loop.dt) <= 1e-15 and len(loop.steps) == 19
+    n = MODEL["n"]
+    imp = handle.joint_impedance(np.zeros(n), np.zeros(n))
+    g = 9.81
+
+    def fall(t1):
+        s = {k: _d(v) for k, v in st.items()}
+        s["base_vel"].zero_()
+        s["joint_vel"].zero_()
+        s["base_pos"][:, 2] += 10.0
+        handle.fbd_euler_integrate_impedance(loop.dm, s, imp, s["joint_pos"].clone(), 0.0, t1, loop.dT)
+        torch.cuda.synchronize()
+        return -s["base_vel"][:, 2].cpu().numpy() / g
+
+    t_loop = fall(loop.T)
+    np.testing.assert_allclose(t_loop, loop.dt, rtol=0, atol=1e-12)
+    # the reference call integrate(0, dt) itself advances dt + dT (the stale last step)
+    np.testing.assert_allclose(fall(loop.dt), loop.dt + loop.dT, rtol=0, atol=1e-12)
+
+
 def _setup(B, periods, seed=3):
     N = 100
     plan = P.make_batch(B, horizon=N + periods, n_footsteps=8, seed=P.SEED, first_ds=periods + 10)

@@ -127,3 +127,93 @@ def test_phased_rejects_bad_arguments(handle):
         handle.dcm_mpc_solve_phased(tab, 0, xi0, omega[:, :N],
                                     params=native.default_params(N, tol_polish=0.0))
     assert e.value.code == 1
+
+
+# ---- the phased solve against the ORACLE directly (not only the GPU two-call path) ----
+# Oracle side: the phase polygons' H-rep by the oracle hull (orc_hull2d_hrep, bit-equal to the
+# device hull, test_gpu_kernels.py), the window by orc_dcm_phase_expand, the solve by
+# orc_dcm_mpc_solve_batch_warm (cold: no warm start); device side: blf_dcm_mpc_solve_phased from
+# the device-built table.  Every output bit for bit, window after window.
+
+def _oracle_table(oracle, prob):
+    B, Pn, C, _ = prob["phase_corners"].shape
+    A, b, nf = oracle.hull2d_hrep_batch(prob["phase_corners"].reshape(B * Pn, C, 2),
+                                        prob["phase_ncorners"].reshape(B * Pn), 8, threads=8)
+    return dict(nphases=prob["nphases"], phase_begin=prob["phase_begin"],
+                phase_end=prob["phase_end"], phase_A=A.reshape(B, Pn, 8, 2),
+                phase_b=b.reshape(B, Pn, 8), phase_nf=nf.reshape(B, Pn), phase_ref=prob["phase_ref"])
+
+
+def _oracle_window_solve(oracle, otab, prob, s, xi0, N, warm=None, tol_polish=3e-4):
+    w = oracle.dcm_phase_expand_batch(otab, s, prob["dt"], N, threads=8)
+    w["xi_init"] = np.ascontiguousarray(xi0)
+    w["omega"] = np.ascontiguousarray(prob["omega"][:, s:s + N])
+    pol = np.zeros(xi0.shape[0], dtype=np.int32)
+    prm = oracle.default_params(N, tol_polish=tol_polish)
+    if warm is None:
+        st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(w, params=prm, threads=8, polished=pol)
+    else:
+        st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(w, warm[0], warm[1], 1, 1e-3,
+                                                               params=prm, threads=8, polished=pol)
+    return dict(status=st, xi=xi, vrp=vrp, iters=it, lam=lam, polished=pol)
+
+
+def _assert_vs_oracle(got, ref, what):
+    for k in OUT_KEYS:
+        np.testing.assert_array_equal(got[k].cpu().numpy(), ref[k], err_msg=f"{k} ({what})")
+
+
+@pytest.mark.parametrize("N,B", [(100, 96), (64, 40), (128, 24), (37, 16)])
+def test_phased_cold_vs_oracle(handle, oracle, N, B):
+    S = 9
+    prob = P.make_batch(B, horizon=N + S, n_footsteps=8, seed=77)
+    tab, otab = _table(handle, prob), _oracle_table(oracle, prob)
+    omega = torch.from_numpy(prob["omega"]).cuda()
+    xi0 = torch.from_numpy(prob["xi_init"]).cuda()
+    for s in (0, 4, S):
+        got = handle.dcm_mpc_solve_phased(tab, s, xi0, omega[:, s:s + N], lambda_out=True)
+        ref = _oracle_window_solve(oracle, otab, prob, s, prob["xi_init"], N)
+        torch.cuda.synchronize()
+        _assert_vs_oracle(got, ref, f"N={N} window {s}")
+        assert (ref["status"] == 0).all()
+
+
+def test_phased_warm_vs_oracle(handle, oracle):
+    """The receding horizon as TimeVaryingDCMPlanner::advance runs it (shift 1, floor 1e-3,
+    tol_polish 1e-4), each side warm-started from its own previous window."""
+    N, S, B = 100, 30, 64
+    prob = P.make_batch(B, horizon=N + S, n_footsteps=8, seed=21)
+    tab, otab = _table(handle, prob), _oracle_table(oracle, prob)
+    omega = torch.from_numpy(prob["omega"]).cuda()
+    prm = native.default_params(N)
+    prm.tol_polish = 1e-4
+    xg, xo = torch.from_numpy(prob["xi_init"]).cuda(), prob["xi_init"]
+    pg = po = None
+    for s in range(S):
+        wg = None if pg is None else dict(vrp=pg["vrp"], lam=pg["lam"], shift=1, floor=1e-3)
+        got = handle.dcm_mpc_solve_phased(tab, s, xg, omega[:, s:s + N], warm=wg, params=prm,
+                                          lambda_out=True)
+        ref = _oracle_window_solve(oracle, otab, prob, s, xo, N,
+                                   warm=None if po is None else (po["vrp"], po["lam"]), tol_polish=1e-4)
+        torch.cuda.synchronize()
+        _assert_vs_oracle(got, ref, f"window {s}")
+        assert (ref["status"] == 0).all(), s
+        pg, po = got, ref
+        xg, xo = got["xi"][:, 1].contiguous(), np.ascontiguousarray(ref["xi"][:, 1])
+
+
+def test_phased_pending_vs_oracle(handle, oracle):
+    """QPs the active-set kernel hands to the IPM (initial DCM far outside the polygons): the
+    IPM's result from the window scratch equals the oracle's IPM on the oracle's window."""
+    N, B = 100, 48
+    prob = P.make_batch(B, horizon=N + 3, n_footsteps=8, seed=5)
+    tab, otab = _table(handle, prob), _oracle_table(oracle, prob)
+    omega = torch.from_numpy(prob["omega"]).cuda()
+    xi0 = prob["xi_init"].copy()
+    xi0[::2] += np.array([0.35, -0.25])
+    got = handle.dcm_mpc_solve_phased(tab, 0, torch.from_numpy(xi0).cuda(), omega[:, :N],
+                                      lambda_out=True)
+    ref = _oracle_window_solve(oracle, otab, prob, 0, xi0, N)
+    torch.cuda.synchronize()
+    _assert_vs_oracle(got, ref, "cold, pending")
+    assert (ref["iters"] > 0).any(), "no problem reached the interior point method"
