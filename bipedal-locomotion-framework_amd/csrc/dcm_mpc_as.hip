@@ -93,6 +93,7 @@ struct LdsRows<double> {
     const double* Bv;
     int S, NH;
     __device__ int col(int j, int lane) const { return j * NH + lane; }
+    __device__ int at(int i, int col) const { return i * S + col; }
 };
 template <>
 struct LdsRows<float> {
@@ -100,6 +101,7 @@ struct LdsRows<float> {
     const float* Bv;
     int S, NH;
     __device__ int col(int j, int lane) const { return j * NH + lane; }
+    __device__ int at(int i, int col) const { return i * S + col; }
 };
 
 // Diagnostic builds only (tools/build_variant.sh): BLF_AS_EXPA = the cold kernel's fp32 search
@@ -120,17 +122,18 @@ struct Row {
     T x, y, b;
 };
 
-template <class T, class V>
-__device__ __forceinline__ Row<T> row(const LdsRows<V>& R, int i, int col)
+template <class T, class RS>
+__device__ __forceinline__ Row<T> row(const RS& R, int i, int col)
 {
-    const auto a = R.A2[i * R.S + col];
-    return {T(a.x), T(a.y), T(R.Bv[i * R.S + col])};
+    const int o = R.at(i, col);
+    const auto a = R.A2[o];
+    return {T(a.x), T(a.y), T(R.Bv[o])};
 }
 
-template <class T, class V>
-__device__ __forceinline__ Row<T> normal(const LdsRows<V>& R, int i, int col)
+template <class T, class RS>
+__device__ __forceinline__ Row<T> normal(const RS& R, int i, int col)
 {
-    const auto a = R.A2[i * R.S + col];
+    const auto a = R.A2[R.at(i, col)];
     return {T(a.x), T(a.y), T(0)};
 }
 
@@ -481,13 +484,6 @@ __device__ __forceinline__ void as_solve(const AKnotT<T> (&K)[KPL], const T (&g)
 template <int KPL, class T>
 __device__ __forceinline__ bool as_lq_step(AKnotT<T> (&K)[KPL], const PT<T>& P, int N, int lane, T xi00, T xi01)
 {
-    T xk[KPL][2];
-    as_xi_prev<KPL, T>(K, lane, xi00, xi01, xk);
-#pragma unroll
-    for (int j = 0; j < KPL; ++j) {
-        const int k = KPL * lane + j;
-        if (k < N) as_residuals(K[j], P, k == N - 1, xk[j][0], xk[j][1]);
-    }
     T E[KPL][3];
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
@@ -503,6 +499,16 @@ __device__ __forceinline__ bool as_lq_step(AKnotT<T> (&K)[KPL], const PT<T>& P, 
         }
     }
     bool ok = as_riccati<KPL, T>(K, P, E, N, lane);
+    // the residuals after the sweep, which does not read them (their registers stay free across it)
+    {
+        T xk[KPL][2];
+        as_xi_prev<KPL, T>(K, lane, xi00, xi01, xk);
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const int k = KPL * lane + j;
+            if (k < N) as_residuals(K[j], P, k == N - 1, xk[j][0], xk[j][1]);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
         if (KPL * lane + j < N) {
@@ -763,10 +769,7 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
             sv[j][0] = K[j].r0; sv[j][1] = K[j].r1; sv[j][2] = K[j].x0; sv[j][3] = K[j].x1;
             E[j][0] = E[j][1] = E[j][2] = T(0);
             pk[j] = 0;
-            if (k < N) {
-                as_pass_setup<T>(K[j], P, R, R.col(j, lane), sv[j][0], sv[j][1], pk[j], E[j], okp);
-                as_residuals(K[j], P, k == N - 1, xk[j][0], xk[j][1]);
-            }
+            if (k < N) as_pass_setup<T>(K[j], P, R, R.col(j, lane), sv[j][0], sv[j][1], pk[j], E[j], okp);
         }
         AS_STAMP_ADD(sb + 0, t_s);
         AS_STAMP(t_r);
@@ -774,8 +777,14 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
         AS_STAMP_ADD(sb + 1, t_r);
         AS_STAMP(t_h);
 #pragma unroll
-        for (int j = 0; j < KPL; ++j)
-            if (KPL * lane + j < N) as_pass_h<T>(K[j], P, R, R.col(j, lane), opaque(pk[j]), okp);
+        for (int j = 0; j < KPL; ++j) {
+            const int k = KPL * lane + j;
+            if (k < N) {
+                as_pass_h<T>(K[j], P, R, R.col(j, lane), opaque(pk[j]), okp);
+                // the residuals at the projected point (after the sweep, which does not read them)
+                as_residuals(K[j], P, k == N - 1, xk[j][0], xk[j][1]);
+            }
+        }
         AS_STAMP_ADD(sb + 2, t_h);
         // the Newton step, then the certificate (costates of the new point from the solve)
         bool neg = false, viol = false;
@@ -1090,8 +1099,9 @@ __device__ __forceinline__ void cold_solve(
         // issued below, after the knot loads: a wait for those (vmcnt counts in issue order) then
         // leaves the younger row loads in flight
     } else if (BLF_AS_EXPA) {
-        stage_rows<KPL, U, float>(Ain, bin, p, N, M, S, NH, lane, 0, nA, reinterpret_cast<float*>(smem),
-                                  reinterpret_cast<float*>(smem) + 2 * (size_t)M * S);
+        for (int t0 = 0; t0 < nA; t0 += 4 * kWave)
+            stage_rows<KPL, 4, float>(Ain, bin, p, N, M, S, NH, lane, t0, nA, reinterpret_cast<float*>(smem),
+                                      reinterpret_cast<float*>(smem) + 2 * (size_t)M * S);
     } else {
         stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, 0, nA, A2d, Bv);
     }

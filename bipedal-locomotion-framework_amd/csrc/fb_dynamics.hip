@@ -66,10 +66,22 @@ __device__ __forceinline__ void wave_sync()
 
 // link record: R 9 | p 3 | w 3 | v 3 | al 3 | a 3 | spatial inertia 10 (m, h, Ibar xx xy xz yy yz zz)
 //              | spatial force 6 (tau_O, f)
-constexpr int kLinkRec = 40;
+// Per-lane records are read and written lane-strided (lane l at l * stride), so every stride is
+// an ODD number of doubles: consecutive lanes then fall on distinct LDS bank pairs and an 8-byte
+// access of 32 lanes is conflict-free.  With the even strides of the data sizes (40, 16, 12, 6
+// doubles) SQ_LDS_BANK_CONFLICT was 83k quad-cycles per wave, 16 % of the Euler kernel's cycles
+// (profiles/r03_fbd_euler_sq.json); BLF_FBD_PAD=0 builds the old layout for A/B.
+#ifndef BLF_FBD_PAD
+#define BLF_FBD_PAD 1
+#endif
+constexpr int kPad = BLF_FBD_PAD;
+constexpr int kLinkRec = 40 + kPad;   // record stride (40 doubles of data)
 constexpr int kR = 0, kP = 9, kW = 12, kV = 15, kAl = 18, kA = 21, kSI = 24, kSF = 34;
-constexpr int kComp = 16;   // subtree sum: spatial inertia 10 | spatial force 6
-constexpr int kCs = 16;     // contact scratch: point 3 | wrench 6 | link 1 | spatial wrench 6
+constexpr int kComp = 16;             // subtree sum: spatial inertia 10 | spatial force 6
+constexpr int kCompS = kComp + kPad;  // its stride
+constexpr int kCs = 16 + kPad;        // contact scratch: point 3 | wrench 6 | link 1 | spatial wrench 6
+constexpr int kJrot = 12 + kPad;      // per-joint E_j Rot (9) | E_j a_j (3)
+constexpr int kSax = 6 + kPad;        // column axis (w, u)
 
 struct Smem {
     // one base pointer (per system: the two halves of a wavefront have their own) and wave-uniform
@@ -91,14 +103,14 @@ struct Smem {
         // link records; after the mass matrix is assembled the same space holds L (NV rows)
         const size_t lk = (size_t)kLinkRec * L, lm = (size_t)NV * ms;
         o_link = take(lk > lm ? lk : lm);
-        o_jrot = take(12 * (size_t)n);           // E_j Rot(a_j, s_j) (9) | E_j a_j (3)
+        o_jrot = take(kJrot * (size_t)n);        // E_j Rot(a_j, s_j) (9) | E_j a_j (3)
         o_jz = take(3 * (size_t)n);
         o_jo = take(3 * (size_t)n);
         // subtree sums [j] (joint j's subtree) and [n] (every link); later the pivot-column
         // buffers of the factorization (2 NV)
-        const size_t cp = (size_t)kComp * (n + 1);
+        const size_t cp = (size_t)kCompS * (n + 1);
         o_comp = take(cp > 2 * (size_t)NV ? cp : 2 * (size_t)NV);
-        o_sax = take(6 * (size_t)NV);
+        o_sax = take(kSax * (size_t)NV);
         o_rhs = take((size_t)NV);
         o_cscr = take((size_t)kCs * (C > 0 ? C : 1));
         o_st = take(18 + 2 * (size_t)n + (size_t)NV + 9);   // Euler state (6 + n + 3 + 9 + n) + acc + dR
@@ -283,7 +295,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
                 const double K2 = (K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c]) + K[3 * r + 2] * K[6 + c];
                 Rr[3 * r + c] = ((r == c ? 1.0 : 0.0) + sn * K[3 * r + c]) + c1 * K2;
             }
-        double* out = S.jrot() + 12 * j;
+        double* out = S.jrot() + kJrot * j;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
 #pragma unroll
@@ -313,7 +325,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
 #pragma unroll
             for (int i = 0; i < 24; ++i) pr[i] = prs[i];
 #pragma unroll
-            for (int i = 0; i < 12; ++i) Ej[i] = S.jrot()[12 * j + i];
+            for (int i = 0; i < 12; ++i) Ej[i] = S.jrot()[kJrot * j + i];
             const double o[3] = {T.o0, T.o1, T.o2};
             const double* RP = pr + kR;
             double cR[9], r[3], z[3];
@@ -475,11 +487,11 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                     for (int p = 10; p < kComp; ++p) acc[p] = acc[p] - sc[p];
             }
             for (unsigned long long b = ch; b; b &= b - 1) {
-                const double* cs = S.comp() + kComp * __builtin_ctzll(b);
+                const double* cs = S.comp() + kCompS * __builtin_ctzll(b);
 #pragma unroll
                 for (int p = 0; p < kComp; ++p) acc[p] = acc[p] + cs[p];
             }
-            double* dst = S.comp() + kComp * (lev >= 0 ? lane : n);
+            double* dst = S.comp() + kCompS * (lev >= 0 ? lane : n);
 #pragma unroll
             for (int p = 0; p < kComp; ++p) dst[p] = acc[p];
         }
@@ -504,12 +516,12 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             for (int a = 0; a < 3; ++a) w[a] = S.jz()[3 * j + a];
             cross3(S.jo() + 3 * j, w, u);
         }
-        const double* I = S.comp() + kComp * (c < 6 ? n : c - 6);
+        const double* I = S.comp() + kCompS * (c < 6 ? n : c - 6);
         double Iwv[3], hu[3], wh[3];
         sym_mv(I + 4, w, Iwv);
         cross3(I + 1, u, hu);
         cross3(w, I + 1, wh);
-        double* sa = S.sax() + 6 * c;
+        double* sa = S.sax() + kSax * c;
         for (int a = 0; a < 3; ++a) {
             sa[a] = w[a];
             sa[3 + a] = u[a];
@@ -529,7 +541,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     double r[NVMAX];
 #pragma unroll
     for (int j = 0; j < NVMAX; ++j) {
-        const double* sa = S.sax() + 6 * (j < NV ? j : NV - 1);   // every lane reads the same S_j
+        const double* sa = S.sax() + kSax * (j < NV ? j : NV - 1);   // every lane reads the same S_j
         const double v = dot3(sa, Fc) + dot3(sa + 3, Fc + 3);
         const bool vis = j <= lane && lane < NV && (j < 6 || ((myanc >> (j - 6)) & 1ull));
         r[j] = vis ? v : 0.0;

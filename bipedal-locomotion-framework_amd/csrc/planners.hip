@@ -257,9 +257,10 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
             const double v0x = s_x[a * kHullBlock + r], v0y = s_y[a * kHullBlock + r];
             const double ex = s_x[b * kHullBlock + r] - v0x;
             const double ey = s_y[b * kHullBlock + r] - v0y;
-            const double len = sqrt(ex * ex + ey * ey);
-            nx = ey / len;
-            ny = (-ex) / len;
+            // one reciprocal of the edge length instead of two quotients (oracle orc_hull2d_hrep)
+            const double il = 1.0 / sqrt(ex * ex + ey * ey);
+            nx = ey * il;
+            ny = (-ex) * il;
             bj = nx * v0x + ny * v0y;
         }
     };

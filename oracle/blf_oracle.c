@@ -204,9 +204,11 @@ int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, doub
         const double* v1 = pts + 2 * H[j + 1];
         const double ex = v1[0] - v0[0];
         const double ey = v1[1] - v0[1];
-        const double len = sqrt(ex * ex + ey * ey);
-        const double nx = ey / len;
-        const double ny = (-ex) / len;
+        /* one reciprocal of the edge length per facet (the device's instruction count, DESIGN.md
+         * 3.0); within the Qhull fixture's 1e-12 of the two quotients it replaced */
+        const double il = 1.0 / sqrt(ex * ex + ey * ey);
+        const double nx = ey * il;
+        const double ny = (-ex) * il;
         A[2 * j] = nx;
         A[2 * j + 1] = ny;
         b[j] = nx * v0[0] + ny * v0[1];

@@ -1,5 +1,8 @@
 """Run one streaming kernel a few times (for rocprofv3 counter passes):
-  python tools/stream_one.py rollout|hull|quintic|contact|fbk|fbk_euler"""
+  python tools/stream_one.py rollout|hull|quintic|contact|fbk|fbk_euler|fbd_euler
+fbd_euler: the config-5 dynamics kernel alone, one control period of 16 384 robots
+(blf_fbd_euler_integrate_impedance over ClosedLoop's interval: 19 ForwardEuler steps, two
+contact feet)."""
 import os
 import sys
 
@@ -32,6 +35,26 @@ def main(which):
         co = h.quintic_fit(kt, rnd(S, 3, 3, 3))
         tq = (kt[:, :1] + (kt[:, 2:] - kt[:, :1]) * rnd(S, Q)).contiguous()
         fn = lambda: h.quintic_eval(kt, co, tq)
+    elif which == "fbd_euler":
+        import numpy as np
+        from blf import closed_loop as DL
+        from blf import robot as R
+        B = int(os.environ.get("FBD_BATCH", 16384))
+        model = R.humanoid24()
+        st = R.standing_states(model, B, seed=1000)
+        law = R.posture_law_arrays(model)
+        t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
+        dm = h.fb_model(model)
+        state = {k: t(st[k]) for k in native.FB_STATE_KEYS}
+        C = len(model["frame_link"])
+        contacts = dict(frame=t(np.arange(C), torch.int32),
+                        params=t(np.tile(np.asarray(DL.CONTACT_PARAMS, np.float64), (C, 1))),
+                        null_pose=t(R.sole_null_poses(model, st)))
+        imp = h.joint_impedance(law["kp"], law["kd"])
+        q_ref = state["joint_pos"].clone()
+        T = DL.period_final_time(0.02, 0.001)
+        fn = lambda: h.fbd_euler_integrate_impedance(dm, state, imp, q_ref, 0.0, T, 0.001,
+                                                     contacts=contacts)
     elif which in ("fbk", "fbk_euler"):
         B, n = 2 * 1024 * 1024, 24
         R = torch.linalg.qr(torch.randn(B, 3, 3, dtype=torch.float64, device=dev))[0].contiguous()
