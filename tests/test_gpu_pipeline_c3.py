@@ -77,9 +77,9 @@ def test_c3_splines_interpolate_their_knots(handle, c3):
     assert float((err[:, :, 0] / scale[:, :, 0]).max()) <= 1e-12
     assert float((err[:, :, 1] / scale[:, :, 1]).max()) <= 1e-11
     assert float((err[:, :, 2] / scale[:, :, 2]).max()) <= 1e-9
-    # knot indices: the getPresentContact rule clamped to [0, K - 1]
-    K = kt.shape[1] - 1
-    expect = torch.tensor([0] + list(range(1, K)) + [K - 1], dtype=torch.int32, device=idx.device)
+    # knot indices at the knot times: the getPresentContact rule (the last knot with t_j <= t),
+    # i.e. the knot itself (the evaluated segment is that index clamped to [0, K - 1])
+    expect = torch.arange(kt.shape[1], dtype=torch.int32, device=idx.device)
     assert torch.equal(idx, expect[None, :].expand_as(idx))
 
 

@@ -12,4 +12,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/fetc
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/write -o run -- python3 $BENCH > $OUT/write.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -T --output-format csv -d $OUT/sq -o run -- python3 $BENCH > $OUT/sq.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 -T --output-format csv -d $OUT/sq2 -o run -- python3 $BENCH > $OUT/sq2.log 2>&1 || exit $?
+# the stall breakdown (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY = WAVE_CYCLES) and LDS detail
+timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_ACTIVE_INST_SCA -T --output-format csv -d $OUT/sq3 -o run -- python3 $BENCH > $OUT/sq3.log 2>&1 || exit $?
 find $OUT -name "*.csv" | head -50

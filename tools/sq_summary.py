@@ -1,5 +1,5 @@
 """Median per-dispatch SQ counters from gpurun_out/sq/<target><n>/ (tools/gpu_sq.sh).
-  python tools/sq_summary.py <target> <kernel-name-prefix>"""
+  python tools/sq_summary.py <target> <kernel-name-prefix> [out.json]"""
 import collections
 import csv
 import glob
@@ -15,3 +15,16 @@ med = {c: sorted(v)[len(v) // 2] for c, v in vals.items()}
 w = med.get("SQ_WAVES", 1.0)
 for c in sorted(med):
     print(f"{c:28s} {med[c]:16.0f}   per wave {med[c] / w:12.1f}")
+if len(sys.argv) > 3:
+    import json
+    wc = med.get("SQ_WAVE_CYCLES")
+    out = {"source": f"tools/gpu_sq.sh target {target}, kernel {prefix}: median per dispatch over "
+                     f"the rocprofv3 --pmc passes (gpurun_out/sq/{target}N)",
+           "median_per_dispatch": med,
+           "per_wave": {c: v / w for c, v in med.items()},
+           "note": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* / SQ_LDS_BANK_CONFLICT count quad-cycles"}
+    if wc:
+        out["frac_of_wave_cycles"] = {c: med[c] / wc for c in med
+                                      if c.startswith(("SQ_WAIT", "SQ_ACTIVE_INST", "SQ_LDS_BANK"))}
+    with open(sys.argv[3], "w") as f:
+        json.dump(out, f, indent=1)

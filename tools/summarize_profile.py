@@ -95,6 +95,24 @@ def valu_issue(d, avg_ns):
     return out
 
 
+def stall_breakdown(d):
+    """Where a wave's cycles go (SQ counters in quad-cycles; WAIT_ANY + WAIT_INST_ANY +
+    ACTIVE_INST_ANY = WAVE_CYCLES, MI355X_MICROARCH.md counter table): parked on s_waitcnt /
+    barriers, issue-stalled on dependencies, issuing (of which VALU, LDS, scalar)."""
+    g = lambda c: d.get(c, {}).get("mean_per_dispatch")
+    w, waves = g("SQ_WAVE_CYCLES"), g("SQ_WAVES")
+    parts = {"wait_any": g("SQ_WAIT_ANY"), "wait_inst_any": g("SQ_WAIT_INST_ANY"),
+             "active_inst_any": g("SQ_ACTIVE_INST_ANY"), "active_inst_valu": g("SQ_ACTIVE_INST_VALU"),
+             "active_inst_lds": g("SQ_ACTIVE_INST_LDS"), "active_inst_sca": g("SQ_ACTIVE_INST_SCA"),
+             "wait_inst_lds": g("SQ_WAIT_INST_LDS"), "lds_bank_conflict": g("SQ_LDS_BANK_CONFLICT")}
+    if not w or not waves or parts["wait_any"] is None:
+        return None
+    return {"wave_cycles_per_wave": 4.0 * w / waves,
+            "frac_of_wave_cycles": {k: (v / w if v is not None else None) for k, v in parts.items()},
+            "per_wave_cycles": {k: (4.0 * v / waves if v is not None else None) for k, v in parts.items()},
+            "note": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles; per-wave cycles = 4 x count / SQ_WAVES"}
+
+
 def main():
     tag = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof")
@@ -104,7 +122,7 @@ def main():
                 os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
     pmc = collections.defaultdict(dict)
-    for sub in ("fetch", "write", "sq", "sq2"):
+    for sub in ("fetch", "write", "sq", "sq2", "sq3"):
         for kname, cs in counters(os.path.join(src, sub, "run_counter_collection.csv")).items():
             for c, v in cs.items():
                 pmc[kname][c] = {"dispatches": len(v), "mean_per_dispatch": sum(v) / len(v)}
@@ -127,6 +145,7 @@ def main():
                     "(Infinity-Cache hits included); gfx950 FETCH_SIZE reads 1/2 of wide "
                     "coalesced stream bytes (MI355X_MICROARCH.md HBM section)"},
         "valu_issue": valu_issue(d, float(stats[dom]["AverageNs"])),
+        "stall_breakdown": stall_breakdown(d),
         "occupancy": occupancy(d, float(stats[dom]["AverageNs"])),
         "kernel_resources": resources(),
         "kernel_avg_ns": {k: float(v["AverageNs"]) for k, v in stats.items()},
