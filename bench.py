@@ -698,9 +698,16 @@ def receding_horizon(args, h, dev):
     params.tol_polish = args.tol_polish if args.tol_polish is not None else 1e-4
     stream = torch.cuda.current_stream()
     state = dict(xi0=t("xi_init").clone(), prev=None, s=0)
-    # one output buffer per window (S x ~39 MB at B = 4096), so that every window's statuses and
-    # iteration counts survive to the checks after the clock stops, with no copy in the timed loop
-    bufs = [None] * S
+    # one output buffer per window (S x ~39 MB at B = 4096, allocated here, before any timing), so
+    # that every window's statuses and iteration counts survive to the checks after the clock
+    # stops with no copy in the timed loop; the window scratch (read only by the IPM stage of the
+    # same call) is shared
+    e64 = lambda *shape: torch.empty(shape, dtype=torch.float64, device=dev)
+    e32 = lambda *shape: torch.empty(shape, dtype=torch.int32, device=dev)
+    window = dict(omega=e64(B, N), xi_ref=e64(B, N + 1, 2), vrp_ref=e64(B, N, 2), A=e64(B, N, M, 2),
+                  b=e64(B, N, M), nfacets=e32(B, N))
+    bufs = [dict(xi=e64(B, N + 1, 2), vrp=e64(B, N, 2), status=e32(B), iters=e32(B),
+                 polished=e32(B), lam=e64(B, N, M), window=window) for _ in range(S)]
     iters = []
     evs = []
 

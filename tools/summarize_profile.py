@@ -56,8 +56,10 @@ def resources():
                    "Occupancy [waves/SIMD]": "occupancy_waves_per_simd",
                    "LDS Size [bytes/block]": "static_lds_bytes"}.get(m.group(1), m.group(1).lower())
             res[cur][key] = int(m.group(2))
-    keep = {k: v for k, v in res.items() if "dcm_mpc_cold_kernelILi2ELb0ELb0E" in k
-            or "dcm_mpc_warm_kernelILi2ELb1ELb0E" in k}
+    # the instances the bench runs: cold <KPL 2, no lambda out, per-knot input, PAD> (c2) and warm
+    # <KPL 2, lambda out, phase-indexed input, PAD> (rh)
+    keep = {k: v for k, v in res.items() if "dcm_mpc_cold_kernelILi2ELb0ELb0ELb1E" in k
+            or "dcm_mpc_warm_kernelILi2ELb1ELb1ELb1E" in k}
     return {("dcm_mpc_cold_kernel<2> (c2)" if "cold" in k else "dcm_mpc_warm_kernel<2> (rh)"): v
             for k, v in keep.items()}
 
@@ -148,6 +150,10 @@ def main():
         "stall_breakdown": stall_breakdown(d),
         "occupancy": occupancy(d, float(stats[dom]["AverageNs"])),
         "kernel_resources": resources(),
+        # dynamic LDS of the dominant kernel at the bench's configs[1] (dcm_mpc_as.hip launch_kpl:
+        # fp64 facet rows [M][S] double2 + [M][S] double, S = 2 ceil(N / 2), N = 100, M = 8)
+        "lds_bytes_per_qp": 3 * 8 * 8 * 100,
+        "qps_per_cu_by_lds": (160 * 1024) // (3 * 8 * 8 * 100),
         "kernel_avg_ns": {k: float(v["AverageNs"]) for k, v in stats.items()},
         "pmc_per_kernel": pmc,
     }
