@@ -74,6 +74,7 @@ __device__ __forceinline__ void wave_sync()
 #ifndef BLF_FBD_PAD
 #define BLF_FBD_PAD 1
 #endif
+
 constexpr int kPad = BLF_FBD_PAD;
 constexpr int kLinkRec = 40 + kPad;   // record stride (40 doubles of data)
 constexpr int kR = 0, kP = 9, kW = 12, kV = 15, kAl = 18, kA = 21, kSI = 24, kSF = 34;
@@ -874,9 +875,15 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     Impedance imp{nullptr, nullptr, nullptr};
     if (impedance) imp = Impedance{impedance->kp, impedance->kd, impedance->q_ref};
-    if (md->ndof + 6 <= 32)   // two systems per wavefront
+#ifndef BLF_FBD_SMALL_HW
+#define BLF_FBD_SMALL_HW 32   // diagnostic builds: 64 = one small model per wavefront (A/B)
+#endif
+    if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
         hipLaunchKernelGGL((fbd_euler_kernel<32, 32>), dim3((unsigned)ceil_div(batch, 2)), dim3(kWave),
                            2 * lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp, batch);
+    else if (md->ndof + 6 <= 32)   // one system per wavefront, NV <= 32 rows
+        hipLaunchKernelGGL((fbd_euler_kernel<32, kWave>), dim3((unsigned)batch), dim3(kWave), lds, s,
+                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp, batch);
     else
         hipLaunchKernelGGL((fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave>), dim3((unsigned)batch),
                            dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last,
