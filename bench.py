@@ -408,8 +408,9 @@ def closed_loop(args):
     two ContinuousContactModel feet (blf/closed_loop.py), B = 16384 robots
     per GPU, one process per GPU over disjoint robot shards (no data-path collective).  One step =
     one 20 ms control period of every robot: its DCM -> the plan's xi_init, the warm-started
-    plan window, the plan's first VRP -> joint references, 20 ForwardEuler steps (1 ms) of the
-    dynamics with the joint impedance.  The loop runs from a standing start; warmup periods first,
+    plan window, the plan's first VRP -> joint references, the reference schedule's ForwardEuler
+    steps (1 ms each, 19 steps = 20 ms of robot time, blf/closed_loop.py fixed_step_schedule) of
+    the dynamics with the joint impedance.  The loop runs from a standing start; warmup periods first,
     then the timed ones, stream-ordered and synchronised once."""
     import numpy as np
     import torch
@@ -594,6 +595,7 @@ def closed_loop_cpu(args, model, N, periods=3):
                         robot.posture_law_arrays(model), DL.CONTACT_PARAMS, horizon=N,
                         compiled=True, threads=threads)
     ref.period()   # warm-up (the first period is the cold solve, as on the device)
+    nsteps = len(DL.fixed_step_schedule(0.0, ref.T, ref.dT))
     t0 = time.perf_counter()
     for _ in range(periods - 1):
         ref.period()
@@ -601,7 +603,7 @@ def closed_loop_cpu(args, model, N, periods=3):
     n = robots * (periods - 1)
     return {"value": n / el, "unit": "robot-periods/s", "cores": threads, "kind": "port",
             "sample": f"{robots} robots x {periods - 1} warm periods in {el:.2f} s on {threads} "
-                      f"threads (oracle/closed_loop.py compiled: C centre of mass + 20 impedance "
+                      f"threads (oracle/closed_loop.py compiled: C centre of mass + {nsteps} impedance "
                       f"Euler steps of the C floating-base dynamics per period, the C oracle's "
                       f"warm QP; gcc -O3)"}
 
@@ -629,6 +631,21 @@ def single_solve_latency(args, h, dev):
         t0 = time.perf_counter()
         h.dcm_mpc_solve(d, params, out=out)
         torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    py_us = float(np.median(lat[args.warmup:])) * 1e6
+    # the drop-in boundary: the C-ABI call with its argument structs held (what the C++
+    # TimeVaryingDCMPlanner adapter pays per solve) + hipStreamSynchronize, no Python marshalling
+    import ctypes
+    solve, stream = h.prepare_dcm_mpc_solve(d, params, out)
+    hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch and libblf.so already share
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    sync = hip.hipStreamSynchronize
+    lat = []
+    for _ in range(args.warmup + 200):
+        t0 = time.perf_counter()
+        solve()
+        if sync(stream) != 0:
+            raise RuntimeError("hipStreamSynchronize failed")
         lat.append(time.perf_counter() - t0)
     gpu_us = float(np.median(lat[args.warmup:])) * 1e6
     # the same call timed on the device (HIP events on the stream the solve is enqueued on): the
@@ -662,12 +679,15 @@ def single_solve_latency(args, h, dev):
     line = {"metric": "single DCM-MPC solve latency (configs[0]: 4 footsteps, horizon 50)",
             "value": gpu_us, "unit": "us", "n_gpus": 1, "higher_is_better": False,
             "dtype": "f64", "ipm_iters": int(out["iters"][0]), "polished": int(out["polished"][0]),
-            "device_us": dev_us,
+            "device_us": dev_us, "python_call_us": py_us,
             "cpu_baseline": {"value": cpu_us, "unit": "us", "cores": 1, "kind": "port",
                              "sample": "200 solves of the same problem in one C batch call, "
                                        "oracle/blf_oracle.c sequential mode, gcc -O3, one thread"},
-            "config": {"workload": "configs[0]: batch=1, 4 footsteps, horizon=50, launch to "
-                                   "completion incl. the host synchronisation"}}
+            "config": {"workload": "configs[0]: batch=1, 4 footsteps, horizon=50; value = one "
+                                   "blf_dcm_mpc_solve C-ABI call (argument structs held, inputs "
+                                   "resident) to the end of hipStreamSynchronize, median of 200; "
+                                   "python_call_us = the same through the Python wrapper; "
+                                   "device_us = the kernels alone (HIP events)"}}
     print(json.dumps(line), flush=True)
 
 

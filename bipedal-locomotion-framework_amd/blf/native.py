@@ -443,6 +443,28 @@ class Handle:
                 _stream(stream)))
         return out
 
+    def prepare_dcm_mpc_solve(self, prob, params, out, stream=None):
+        """The cold blf_dcm_mpc_solve with its argument structs built once: returns f(), which
+        makes just the C-ABI call (what a C++ caller holding its device buffers pays, e.g. the
+        TimeVaryingDCMPlanner adapter), and the raw stream handle.  The tensors must outlive f."""
+        torch = _torch()
+        self.dcm_mpc_solve(prob, params, out=out, stream=stream)   # validates every argument
+        B, N = prob["omega"].shape
+        M = prob["b"].shape[2]
+        pb = DcmMpcProblem(*(_vp(prob[k].data_ptr()) for k in
+                             ("xi_init", "omega", "xi_ref", "vrp_ref", "A", "b", "nfacets")))
+        so = DcmMpcSolution(*(_vp(out[k].data_ptr()) for k in ("xi", "vrp", "status", "iters", "polished")))
+        s = _stream(stream)
+        fn, h, pp, ppb, pso = lib().blf_dcm_mpc_solve, self._h, ctypes.byref(params), ctypes.byref(pb), ctypes.byref(so)
+        keep = (pb, so, params, prob, out, torch)
+
+        def f():
+            st = fn(h, pp, ppb, B, pso, s)
+            if st != 0:
+                _check(st)
+            return keep
+        return f, s
+
     def phase_table(self, nphases, begin, end, corners, ncorners, max_facets=8, ref=None,
                     stream=None):
         """Device phase table: the H-rep of every phase's support polygon (blf_hull2d_hrep over

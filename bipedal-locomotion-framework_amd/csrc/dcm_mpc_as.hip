@@ -20,8 +20,12 @@
 // the oracle (oracle/blf_oracle_as32.c for the float search), so the results stay bit-identical.
 // A QP whose fp64 passes do not certify gets the fp64 LQ optimum as its start point, status
 // kPending, and the IPM kernel's stage 2 (dcm_mpc_ipm.hip) continues from there exactly as the
-// oracle does after a failed start.
+// oracle does after a failed start.  Small batches with N <= 64 (configs[0]) run that stage 2 in
+// the same workgroup instead (dcm_mpc_cold_fused_kernel): one launch for the whole solve.
 #include "dcm_qp_common.h"
+#include "dcm_mpc_ipm_body.h"
+
+#include <stdlib.h>
 
 namespace blf {
 namespace {
@@ -1271,6 +1275,31 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
                                      status_out, iters_out, polished_out, lam_out, ps);
 }
 
+// Small batches, N <= 64 (configs[0], one TimeVaryingDCMPlanner solve): the QP the active-set
+// start hands over continues in the same workgroup, the IPM kernel's stage 2 run by the
+// wavefront's 64 lanes (ipm_solve<64>: one thread per knot, exactly the stage-2 workgroup), so the
+// solve is one launch instead of two (the second one's dispatch was 4 us of a 28 us solve, and
+// the host's second enqueue).  Same code, same inputs, so the same bits as the two launches.
+template <bool LAMOUT>
+__global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_fused_kernel(
+    KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
+    const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
+    const double* __restrict__ Ain, const double* __restrict__ bin,
+    const int32_t* __restrict__ nfacets, double* __restrict__ xi_out, double* __restrict__ vrp_out,
+    int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
+    double* __restrict__ lam_out)
+{
+    cold_solve<1, LAMOUT, false, false>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+                                        status_out, iters_out, polished_out, lam_out, PhaseSrc{});
+    // the outputs just written are stage 2's start point and its status gate; the LDS is reused
+    __syncthreads();
+    KParams P2 = P;
+    P2.stage2 = 1;
+    ipm_solve<kWave, false, LAMOUT>(P2, blockIdx.x, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets,
+                                    nullptr, nullptr, xi_out, vrp_out, status_out, iters_out, polished_out,
+                                    lam_out);
+}
+
 // ---- the warm-start kernel ("Warm start") ----
 // One wavefront per QP, fp64 facet rows in LDS.  From the shifted previous solution (xi rolled
 // out from its VRPs), guess = the facets the rollout violates plus those whose previous multiplier
@@ -1441,10 +1470,14 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
 #endif
 }
 
+// Batches up to this size take the fused kernel (N <= 64, cold, per-knot input): they fill at
+// most 4 of a CU's wavefront slots, so its larger LDS / register footprint costs nothing.
+constexpr int64_t kFusedMaxBatch = 1024;
+
 template <int KPL>
 blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const blf_dcm_mpc_warm_start* warm,
                       int64_t batch, const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
-                      const PhaseSrc* ps)
+                      const PhaseSrc* ps, bool* stage2_done)
 {
 #ifndef AS_EXTRA_LDS
 #define AS_EXTRA_LDS 0
@@ -1457,6 +1490,16 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     if (lds > 64 * 1024)
         return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: %zu B of LDS (%d phases)", lds, ps ? ps->P : 0);
     const bool pad = KPL == 2 && kp.N <= 2 * kWave - 2;
+    const char* fz = getenv("BLF_QP_FUSE_STAGE2");
+    if (KPL == 1 && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch && !(fz && fz[0] == '0')) {
+        const size_t lds_f = std::max(lds, sizeof(double) * Lds(nullptr, kp.N, kp.M, 1).total);
+        auto kern = lam_out ? dcm_mpc_cold_fused_kernel<true> : dcm_mpc_cold_fused_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds_f, s, kp,
+                           pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, sol->xi,
+                           sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
+        *stage2_done = true;
+        return check_hip(hipGetLastError(), "dcm_mpc_cold_fused_kernel launch");
+    }
     if (warm == nullptr) {
 #define AS_COLD(L, H, D) dcm_mpc_cold_kernel<KPL, L, H, D>
         auto kern = pad ? (ps ? (lam_out ? AS_COLD(true, true, true) : AS_COLD(false, true, true))
@@ -1512,10 +1555,13 @@ extern "C" int blf_debug_as_stamps(unsigned long long* out, int reset)
 blf_status launch_dcm_mpc_as(const qp::KParams& kp, const blf_dcm_mpc_problem* pb,
                              const blf_dcm_mpc_warm_start* warm, int64_t batch,
                              const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
-                             const qp::PhaseSrc* ps)
+                             const qp::PhaseSrc* ps, bool* stage2_done)
 {
-    if (kp.N <= kWave) return launch_kpl<1>(kp, pb, warm, batch, sol, lam_out, s, ps);
-    if (kp.N <= 2 * kWave) return launch_kpl<2>(kp, pb, warm, batch, sol, lam_out, s, ps);
+    bool none = false;
+    bool* done = stage2_done ? stage2_done : &none;
+    *done = false;
+    if (kp.N <= kWave) return launch_kpl<1>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
+    if (kp.N <= 2 * kWave) return launch_kpl<2>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
     return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: horizon %d > 128", kp.N);
 }
 

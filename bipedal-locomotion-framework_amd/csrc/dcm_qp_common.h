@@ -272,9 +272,10 @@ __device__ __forceinline__ int phase_of(const double* begin, const double* end, 
 
 // dcm_mpc_as.hip: the one-wavefront active-set kernel (N <= 128); QPs it does not certify are left
 // with status qp::kPending for the IPM kernel's stage 2.  ps != nullptr: the phase-indexed input
-// (pb->xi_init and pb->omega are used, the other per-knot arrays are not).
+// (pb->xi_init and pb->omega are used, the other per-knot arrays are not).  *stage2_done: the
+// launch already ran stage 2 (the fused small-batch kernel), so the IPM launch is skipped.
 blf_status launch_dcm_mpc_as(const qp::KParams& kp, const blf_dcm_mpc_problem* pb,
                              const blf_dcm_mpc_warm_start* warm, int64_t batch,
                              const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
-                             const qp::PhaseSrc* ps = nullptr);
+                             const qp::PhaseSrc* ps = nullptr, bool* stage2_done = nullptr);
 }  // namespace blf

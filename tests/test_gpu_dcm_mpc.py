@@ -236,6 +236,40 @@ def test_dcm_mpc_polish_refusal_matches_oracle_bitwise(handle, oracle):
     np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp_o)
 
 
+@pytest.mark.parametrize("horizon", [40, 64])
+def test_dcm_mpc_fused_stage2_equals_two_launches(handle, oracle, horizon, monkeypatch):
+    """Small batches with N <= 64 run the IPM's stage 2 inside the active-set kernel's workgroup
+    (dcm_mpc_cold_fused_kernel, one launch); BLF_QP_FUSE_STAGE2=0 keeps the two launches.  Both
+    give the oracle's bits, with QPs handed over (duplicated facet rows: the polish refuses) and
+    an infeasible one."""
+    B = 8
+    prob = oracle.assemble_constraints(P.make_batch(B, horizon=horizon, n_footsteps=4, seed=82))
+    for q in range(0, B, 2):
+        for k in range(horizon):
+            m = prob["nfacets"][q, k]
+            c = min(2, 8 - m)
+            prob["A"][q, k, m:m + c] = prob["A"][q, k, 0]
+            prob["b"][q, k, m:m + c] = prob["b"][q, k, 0]
+            prob["nfacets"][q, k] = m + c
+    prob["A"][1, 10, :2] = [[1.0, 0.0], [-1.0, 0.0]]   # problem 1: an empty polygon at knot 10
+    prob["b"][1, 10, :2] = [-1.0, -1.0]
+    prob["nfacets"][1, 10] = 2
+    dev = _to_dev(prob)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("BLF_QP_FUSE_STAGE2", mode)
+        out = handle.dcm_mpc_solve(dev, lambda_out=True)
+        torch.cuda.synchronize()
+        res[mode] = {k: v.cpu().numpy().copy() for k, v in out.items()}
+    pol_o = np.zeros(B, np.int32)
+    st_o, xi_o, vrp_o, it_o, lam_o = oracle.dcm_mpc_solve_batch_warm(prob, threads=4, polished=pol_o)
+    assert not pol_o.all() and (st_o[0::2] == 0).all() and st_o[1] != 0
+    for mode, r in res.items():
+        for k, ref in (("status", st_o), ("polished", pol_o), ("iters", it_o), ("xi", xi_o),
+                       ("vrp", vrp_o), ("lam", lam_o)):
+            np.testing.assert_array_equal(r[k], ref, err_msg=f"{k} fuse={mode}")
+
+
 @pytest.mark.parametrize("horizon,footsteps", [(100, 6), (50, 4), (128, 8), (126, 8), (65, 4)])
 def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, footsteps, monkeypatch):
     """The default path for N <= 128 (csrc/dcm_mpc_as.hip: one wavefront per QP, knot pairs per

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--footsteps", type=int, default=6)
     ap.add_argument("--tol-polish", type=float, nargs="*", default=[None])
     args = ap.parse_args()
     for tp in args.tol_polish:
@@ -31,7 +32,7 @@ def main():
 
 def run(args, tol_polish):
     h = native.Handle(0)
-    prob = P.make_batch(args.batch, horizon=args.horizon, n_footsteps=6)
+    prob = P.make_batch(args.batch, horizon=args.horizon, n_footsteps=args.footsteps, seed=P.SEED)
     d = {k: torch.from_numpy(prob[k]).cuda() for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
     A, b, nf = h.assemble_constraints(torch.from_numpy(prob["corners"]).cuda(),
                                       torch.from_numpy(prob["ncorners"]).cuda())
@@ -65,7 +66,7 @@ def run(args, tol_polish):
           f"status!=0: {int((out['status'] != 0).sum())}")
     if as_stamps is not None:
         as_stamps(ctypes.cast(abuf, ctypes.c_void_p), 0)
-        q = 64 * args.reps
+        q = min(args.batch, 64) * args.reps
         npass = max(abuf[10], 1)
         print(f"active-set kernel, lane 0 cycles per QP: total {abuf[0] / q:.0f}, staging + knot loads "
               f"{abuf[1] / q:.0f}, LQ step {abuf[2] / q:.0f}, guess {abuf[3] / q:.0f}, outputs "
@@ -113,7 +114,7 @@ def run(args, tol_polish):
             print(f"polish: {buf[9] / 64 / args.reps:.2f} attempts per QP, {buf[8] / buf[9]:.0f} cycles "
                   f"per attempt; total per QP split: iterations {(tot - buf[8]) / 64 / args.reps:.0f}, "
                   f"polish {buf[8] / 64 / args.reps:.0f}")
-        q = 64 * args.reps
+        q = min(args.batch, 64) * args.reps
         print(f"start-up per QP: loads {buf[10] / q:.0f}, LQ step {buf[11] / q:.0f}, "
               f"slacks/multipliers/dual residual {buf[12] / q:.0f}")
         if buf[9]:
