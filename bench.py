@@ -139,6 +139,14 @@ def host_cpu_info():
     return info
 
 
+def emit(line):
+    """Print one JSON result line with the build provenance of the library it measured: the source
+    hash compiled into lib/libblf.so (blf_version) against the hash of this tree's sources."""
+    from blf import native
+    line["build"] = native.build_provenance()
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -319,7 +327,7 @@ def main():
             threads = cpu_threads()
             host = dict(prob, A=A.cpu().numpy(), b=b.cpu().numpy(), nfacets=nf.cpu().numpy())
             line["cpu_baseline"] = cpu_baseline(host, N, args.cpu_seconds, threads)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -400,7 +408,7 @@ def other_workload(args):
             line["cpu_baseline"] = pipeline_cpu(N)
     else:
         return closed_loop(args, h, dev)
-    print(json.dumps(line), flush=True)
+    emit(line)
 
 
 def closed_loop(args):
@@ -484,7 +492,7 @@ def closed_loop(args):
                            "batch_per_gpu": B, "parallelism": f"shard{world} (independent robots)"}}
         if not args.no_cpu:
             line["cpu_baseline"] = closed_loop_cpu(args, model, N)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -688,7 +696,7 @@ def single_solve_latency(args, h, dev):
                                    "resident) to the end of hipStreamSynchronize, median of 200; "
                                    "python_call_us = the same through the Python wrapper; "
                                    "device_us = the kernels alone (HIP events)"}}
-    print(json.dumps(line), flush=True)
+    emit(line)
 
 
 def phase_expand_bytes(P, N, M):
@@ -808,7 +816,7 @@ def receding_horizon(args, h, dev):
         line["phase_expand"] = {"kernel_ms_median": ex_ms, "bytes_per_problem":
                                 phase_expand_bytes(Pn, N, M), "achieved_gbs": ex_gbs,
                                 "frac_hbm": ex_gbs / HBM_PEAK_GBS}
-    print(json.dumps(line), flush=True)
+    emit(line)
 
 
 if __name__ == "__main__":

@@ -206,6 +206,38 @@ def version():
     return lib().blf_version().decode()
 
 
+def source_hash():
+    """The Makefile's SRC_HASH of the kernel / C-ABI sources in this tree (sha256 of csrc/*.hip and
+    csrc/*.h in sorted path order, then include/blf/blf_c.h; first 16 hex digits), or None when
+    the sources are not present."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = sorted(os.path.relpath(f, pkg) for f in glob.glob(os.path.join(pkg, "csrc", "*.hip")) +
+                   glob.glob(os.path.join(pkg, "csrc", "*.h")))
+    hdr = os.path.join(os.path.dirname(pkg), "include", "blf", "blf_c.h")
+    if not names or not os.path.exists(hdr):
+        return None
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(pkg, n), "rb") as f:
+            h.update(f.read())
+    with open(hdr, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_provenance():
+    """Which library this process loaded and whether it was built from the sources in this tree:
+    {"lib": path, "lib_src_hash": hash in blf_version(), "tree_src_hash": source_hash(),
+    "matches": bool}."""
+    v = version()
+    lib_hash = v.rsplit(" src ", 1)[1] if " src " in v else None
+    tree = source_hash()
+    return {"lib": LIB_PATH, "lib_src_hash": lib_hash, "tree_src_hash": tree,
+            "matches": lib_hash is not None and lib_hash == tree}
+
+
 def default_params(horizon, **kw):
     p = DcmMpcParams()
     lib().blf_dcm_mpc_default_params(ctypes.byref(p), horizon)

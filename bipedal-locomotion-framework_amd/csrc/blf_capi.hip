@@ -96,7 +96,12 @@ blf_status blf_destroy(blf_handle* handle)
 
 const char* blf_last_error(void) { return g_err; }
 
-const char* blf_version(void) { return "blf-mi355x 0.1.0 (gfx950, fp64, -ffp-contract=off)"; }
+#ifndef BLF_SRC_HASH
+#define BLF_SRC_HASH "unknown"
+#endif
+// The sources' hash (Makefile SRC_HASH) makes the loaded library traceable to the tree it was
+// built from (blf/native.py build_provenance).
+const char* blf_version(void) { return "blf-mi355x 0.1.0 (gfx950, fp64, -ffp-contract=off) src " BLF_SRC_HASH; }
 
 blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m, const double* A,
                                    const double* Bm, int32_t shared_matrices, const double* u,

@@ -91,13 +91,15 @@ using AKnot = AKnotT<double>;
 // i S + col), fp64 (rounded to float as the fp32 search reads them).
 template <class V>
 struct LdsRows;
+// at(): a 24-bit multiply (v_mul_u32_u24, full rate; i < 8, S <= 128) for the per-lane facet
+// indices of the passes, which v_mul_lo_u32 (quarter rate) took before.
 template <>
 struct LdsRows<double> {
     const double2* A2;
     const double* Bv;
     int S, NH;
     __device__ int col(int j, int lane) const { return j * NH + lane; }
-    __device__ int at(int i, int col) const { return i * S + col; }
+    __device__ int at(int i, int col) const { return (int)__umul24((unsigned)i, (unsigned)S) + col; }
 };
 template <>
 struct LdsRows<float> {
@@ -105,7 +107,7 @@ struct LdsRows<float> {
     const float* Bv;
     int S, NH;
     __device__ int col(int j, int lane) const { return j * NH + lane; }
-    __device__ int at(int i, int col) const { return i * S + col; }
+    __device__ int at(int i, int col) const { return (int)__umul24((unsigned)i, (unsigned)S) + col; }
 };
 
 // Diagnostic builds only (tools/build_variant.sh): BLF_AS_EXPA = the cold kernel's fp32 search
@@ -141,40 +143,93 @@ __device__ __forceinline__ Row<T> normal(const RS& R, int i, int col)
     return {T(a.x), T(a.y), T(0)};
 }
 
-// The scan tree (oracle scan_backward_pairs / scan_forward_pairs / riccati_sweep_pairs):
-//   KPL = 1 (N <= 64): lane l owns knot l; Kogge-Stone over the 64 lanes (the IPM kernel's tree
-//            for one wavefront);
+// The knots of a lane (oracle scan_backward_as / scan_forward_as / riccati_sweep_as):
+//   KPL = 1 (N <= 64): lane l owns knot l; the tree (TR, below) runs over the 64 lanes (kTreeKS is
+//            the IPM kernel's tree for one wavefront);
 //   KPL = 2 (N <= 128): lane l owns the knot pair (2l, 2l + 1): the pair's element is composed in
-//            the lane, Kogge-Stone runs over the 64 lanes on one element per lane, and the pair's
+//            the lane, the tree runs over the 64 lanes on one element per lane, and the pair's
 //            inner knot is applied in the lane afterwards.
 // Slot j of a lane is knot KPL lane + j.  Knots >= N carry the zero element (affine scans) or the
 // identity (Riccati).
 
-// Backward affine scan v_k = G_k v_{k+1} + c_k, v_N = 0.  Returns v_{k+1} per slot.
-// pad (KPL = 2, N <= 126): lane 63 holds no knot, so it carries the zero element (affine scans) or
+// kTreePad (KPL = 2, N <= 126): lane 63 holds no knot, so it carries the zero element (affine scans) or
 // the identity (Riccati) at every level.  A lane whose partner would lie past the wavefront then
 // combines with lane 63 instead of being masked: the combine leaves its vector part unchanged
 // (signed zeros aside; the oracle's pair tree does the same), and the level needs no exec mask,
 // no branch and no write-back of temporaries (0.141 -> 0.133 ms at B = 4096).
-__device__ __forceinline__ bool as_pad(int KPL, int N) { return KPL == 2 && N <= 2 * kWave - 2; }
 
-// The kernels are instantiated per as_pad value (PAD) and tell the compiler which one holds, so
-// every scan's pad test folds and only one of its two loops is emitted.
-template <int KPL, bool PAD>
+// The scan tree of a launch (template parameter TR of the kernels and the scans):
+//   kTreeKS:  Kogge-Stone over the 64 lanes, distance 1 by DPP, 2..32 by ds_bpermute; a lane whose
+//             partner lies past the wavefront does not combine;
+//   kTreePad: the same for KPL = 2 with N <= 126 (as_pad): lane 63 holds no knot and carries the
+//             zero element / identity, and a lane whose partner lies past the wavefront combines
+//             with lane 63 instead, so no level needs an exec mask (0.141 -> 0.133 ms at B = 4096);
+//   kTreeDpp: every level a VALU move, no LDS round trip (tree_fwd / tree_bwd of dcm_qp_common.h:
+//             Kogge-Stone inside each row of 16 lanes by DPP row shifts, then two row-level steps).
+//             It issues more VALU than the ds_bpermute levels, which move data through the LDS
+//             pipe, but shortens the dependency chain: with one knot per lane (N <= 64) it is
+//             4-8 % faster up to 1024 QPs and even at 2048-4096; with knot pairs it is slower at
+//             every batch size (3-8 %), and so is a fully DPP tree at B = 4096.
+//             So it serves N <= 64 at up to kDppTreeMaxBatch QPs (the oracle's as_tree rule).
+// The pad kernels tell the compiler which as_pad value holds, so every scan's pad test folds.
+enum : int { kTreeKS = 0, kTreePad = 1, kTreeDpp = 2 };
+
+template <int KPL, int TR>
 __device__ __forceinline__ void assume_pad(int N)
 {
-    if (KPL == 2) __builtin_assume(PAD == (N <= 2 * kWave - 2));
+    if (KPL == 2 && TR != kTreeDpp) __builtin_assume((TR == kTreePad) == (N <= 2 * kWave - 2));
 }
 
-template <int KPL, class T>
+// One level L of the DPP tree for the affine scans: (g, e) <- (g, e) o the element of the level's
+// source lane, on the lanes that have one (tree_has); the others keep their element.
+template <int L, bool FWD, class T>
+__device__ __forceinline__ void aff_level(T& g0, T& g1, T& g2, T& g3, T& e0, T& e1, int lane)
+{
+    T p0, p1, p2, p3, q0, q1;
+    if constexpr (FWD) {
+        p0 = tree_fwd<L>(g0); p1 = tree_fwd<L>(g1); p2 = tree_fwd<L>(g2);
+        p3 = tree_fwd<L>(g3); q0 = tree_fwd<L>(e0); q1 = tree_fwd<L>(e1);
+    } else {
+        p0 = tree_bwd<L>(g0); p1 = tree_bwd<L>(g1); p2 = tree_bwd<L>(g2);
+        p3 = tree_bwd<L>(g3); q0 = tree_bwd<L>(e0); q1 = tree_bwd<L>(e1);
+    }
+    if (tree_has<L, FWD>(lane)) COMPOSE(g0, g1, g2, g3, p0, p1, p2, p3, q0, q1, e0, e1);
+}
+
+template <bool FWD, class T>
+__device__ __forceinline__ void aff_tree(T& g0, T& g1, T& g2, T& g3, T& e0, T& e1, int lane)
+{
+    aff_level<0, FWD>(g0, g1, g2, g3, e0, e1, lane);
+    aff_level<1, FWD>(g0, g1, g2, g3, e0, e1, lane);
+    aff_level<2, FWD>(g0, g1, g2, g3, e0, e1, lane);
+    aff_level<3, FWD>(g0, g1, g2, g3, e0, e1, lane);
+    aff_level<4, FWD>(g0, g1, g2, g3, e0, e1, lane);
+    aff_level<5, FWD>(g0, g1, g2, g3, e0, e1, lane);
+}
+
+// One level of the Riccati scan in the DPP tree (backward): e <- e o the source lane's element.
+template <int L, class T>
+__device__ __forceinline__ void rc_tree(RcT<T>& e, bool& ok, int lane)
+{
+    RcT<T> q;
+    q.a0 = tree_bwd<L>(e.a0); q.a1 = tree_bwd<L>(e.a1); q.a2 = tree_bwd<L>(e.a2); q.a3 = tree_bwd<L>(e.a3);
+    q.g0 = tree_bwd<L>(e.g0); q.g1 = tree_bwd<L>(e.g1); q.g2 = tree_bwd<L>(e.g2);
+    q.h0 = tree_bwd<L>(e.h0); q.h1 = tree_bwd<L>(e.h1); q.h2 = tree_bwd<L>(e.h2);
+    if (tree_has<L, false>(lane)) ok = rc_combine(e, q) && ok;
+}
+
+// Backward affine scan v_k = G_k v_{k+1} + c_k, v_N = 0.  Returns v_{k+1} per slot.
+template <int KPL, int TR, class T>
 __device__ __forceinline__ void as_scan_backward(const T (&G)[KPL][4], const T (&c)[KPL][2], int lane,
-                                                 T (&vn)[KPL][2], bool pad)
+                                                 T (&vn)[KPL][2])
 {
     T g0 = G[0][0], g1 = G[0][1], g2 = G[0][2], g3 = G[0][3], e0 = c[0][0], e1 = c[0][1];
     if constexpr (KPL == 2)   // knot 2l after knot 2l + 1
         COMPOSE(g0, g1, g2, g3, G[1][0], G[1][1], G[1][2], G[1][3], c[1][0], c[1][1], e0, e1);
     const int ln = opaque(lane);
-    if (KPL == 2 && pad) {
+    if constexpr (TR == kTreeDpp) {
+        aff_tree<false>(g0, g1, g2, g3, e0, e1, lane);
+    } else if (KPL == 2 && TR == kTreePad) {
         {   // d = 1 (DPP)
             const T p0 = dpp1<kNextKeep>(g0), p1 = dpp1<kNextKeep>(g1), p2 = dpp1<kNextKeep>(g2);
             const T p3 = dpp1<kNextKeep>(g3), q0 = dpp1<kNextKeep>(e0), q1 = dpp1<kNextKeep>(e1);
@@ -219,16 +274,18 @@ __device__ __forceinline__ void as_scan_backward(const T (&G)[KPL][4], const T (
 }
 
 // Forward affine scan x_{k+1} = F_k x_k + f_k, x_0 = 0.  Returns x_{k+1} and x_k per slot.
-template <int KPL, class T>
+template <int KPL, int TR, class T>
 __device__ __forceinline__ void as_scan_forward(const T (&F)[KPL][4], const T (&f)[KPL][2], int lane,
-                                                T (&x)[KPL][2], T (&xk)[KPL][2], bool pad)
+                                                T (&x)[KPL][2], T (&xk)[KPL][2])
 {
     constexpr int L = KPL - 1;   // the lane's last knot
     T g0 = F[L][0], g1 = F[L][1], g2 = F[L][2], g3 = F[L][3], e0 = f[L][0], e1 = f[L][1];
     if constexpr (KPL == 2)   // knot 2l + 1 after knot 2l
         COMPOSE(g0, g1, g2, g3, F[0][0], F[0][1], F[0][2], F[0][3], f[0][0], f[0][1], e0, e1);
     const int ln = opaque(lane);
-    if (KPL == 2 && pad) {   // lanes before the first partner take lane 63's zero element (as_pad)
+    if constexpr (TR == kTreeDpp) {
+        aff_tree<true>(g0, g1, g2, g3, e0, e1, lane);
+    } else if (KPL == 2 && TR == kTreePad) {   // lanes before the first partner take lane 63's zero element (as_pad)
         {   // d = 1 (DPP; lane 0 takes lane 63's)
             const T p0 = dpp1<kPrevWrap>(g0), p1 = dpp1<kPrevWrap>(g1), p2 = dpp1<kPrevWrap>(g2);
             const T p3 = dpp1<kPrevWrap>(g3), q0 = dpp1<kPrevWrap>(e0), q1 = dpp1<kPrevWrap>(e1);
@@ -325,7 +382,7 @@ __device__ __forceinline__ void rc_knot(RcT<T>& e, bool own, T al, const T (&E)[
     }
 }
 
-template <int KPL, class T>
+template <int KPL, int TR, class T>
 __device__ __forceinline__ bool as_riccati(AKnotT<T> (&K)[KPL], const PT<T>& P, const T (&E)[KPL][3], int N,
                                            int lane)
 {
@@ -338,13 +395,14 @@ __device__ __forceinline__ bool as_riccati(AKnotT<T> (&K)[KPL], const PT<T>& P, 
         ok = rc_combine(e, e1) && ok;
     }
     const int ln = opaque(lane);
+    constexpr bool pad = KPL == 2 && TR == kTreePad;
     auto level = [&](int ad, RcT<T>& q) {
         q.a0 = bperm(ad, e.a0); q.a1 = bperm(ad, e.a1); q.a2 = bperm(ad, e.a2); q.a3 = bperm(ad, e.a3);
         q.g0 = bperm(ad, e.g0); q.g1 = bperm(ad, e.g1); q.g2 = bperm(ad, e.g2);
         q.h0 = bperm(ad, e.h0); q.h1 = bperm(ad, e.h1); q.h2 = bperm(ad, e.h2);
     };
     auto level1 = [&](RcT<T>& q) {   // d = 1 (DPP; as_pad: lane 63 keeps its own identity)
-        if (as_pad(KPL, N)) {
+        if (pad) {
             q.a0 = dpp1<kNextKeep>(e.a0); q.a1 = dpp1<kNextKeep>(e.a1);
             q.a2 = dpp1<kNextKeep>(e.a2); q.a3 = dpp1<kNextKeep>(e.a3);
             q.g0 = dpp1<kNextKeep>(e.g0); q.g1 = dpp1<kNextKeep>(e.g1); q.g2 = dpp1<kNextKeep>(e.g2);
@@ -356,7 +414,14 @@ __device__ __forceinline__ bool as_riccati(AKnotT<T> (&K)[KPL], const PT<T>& P, 
             q.h0 = dpp1<kNextWrap>(e.h0); q.h1 = dpp1<kNextWrap>(e.h1); q.h2 = dpp1<kNextWrap>(e.h2);
         }
     };
-    if (as_pad(KPL, N)) {   // past the wavefront: lane 63's identity (as_pad)
+    if constexpr (TR == kTreeDpp) {
+        rc_tree<0>(e, ok, lane);
+        rc_tree<1>(e, ok, lane);
+        rc_tree<2>(e, ok, lane);
+        rc_tree<3>(e, ok, lane);
+        rc_tree<4>(e, ok, lane);
+        rc_tree<5>(e, ok, lane);
+    } else if (pad) {   // past the wavefront: lane 63's identity (as_pad)
         {
             RcT<T> q;
             level1(q);
@@ -415,7 +480,7 @@ __device__ __forceinline__ bool as_riccati(AKnotT<T> (&K)[KPL], const PT<T>& P, 
 }
 
 // Solve the factored Newton system for the right-hand side g (IPM kernel solve) over every slot.
-template <int KPL, class T>
+template <int KPL, int TR, class T>
 __device__ __forceinline__ void as_solve(const AKnotT<T> (&K)[KPL], const T (&g)[KPL][2], int N, int lane,
                                          T (&dr)[KPL][2], T (&dx)[KPL][2], T (&vn)[KPL][2])
 {
@@ -449,7 +514,7 @@ __device__ __forceinline__ void as_solve(const AKnotT<T> (&K)[KPL], const T (&g)
     for (int j = 0; j < KPL; ++j) {
         Gt[j][0] = G[j][0]; Gt[j][1] = G[j][2]; Gt[j][2] = G[j][1]; Gt[j][3] = G[j][3];
     }
-    as_scan_backward<KPL, T>(G, c, lane, vn, as_pad(KPL, N));
+    as_scan_backward<KPL, TR, T>(G, c, lane, vn);
     T k[KPL][2], f[KPL][2];
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
@@ -467,7 +532,7 @@ __device__ __forceinline__ void as_solve(const AKnotT<T> (&K)[KPL], const T (&g)
         }
     }
     T xk[KPL][2];
-    as_scan_forward<KPL, T>(Gt, f, lane, dx, xk, as_pad(KPL, N));
+    as_scan_forward<KPL, TR, T>(Gt, f, lane, dx, xk);
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
         const AKnotT<T>& Kj = K[j];
@@ -485,7 +550,7 @@ __device__ __forceinline__ void as_solve(const AKnotT<T> (&K)[KPL], const T (&g)
 // (W = 0, lambda = 0) from the current (r, xi) (oracle: dcm_residuals(0), dcm_factor, dcm_solve).
 // Returns false when some factorization pivot is not positive definite (status NUMERICAL; the
 // step is still taken, as in the oracle).
-template <int KPL, class T>
+template <int KPL, int TR, class T>
 __device__ __forceinline__ bool as_lq_step(AKnotT<T> (&K)[KPL], const PT<T>& P, int N, int lane, T xi00, T xi01)
 {
     T E[KPL][3];
@@ -502,7 +567,7 @@ __device__ __forceinline__ bool as_lq_step(AKnotT<T> (&K)[KPL], const PT<T>& P, 
             E[j][2] = (P.Rw0 + W00) * ie;
         }
     }
-    bool ok = as_riccati<KPL, T>(K, P, E, N, lane);
+    bool ok = as_riccati<KPL, TR, T>(K, P, E, N, lane);
     // the residuals after the sweep, which does not read them (their registers stay free across it)
     {
         T xk[KPL][2];
@@ -541,7 +606,7 @@ __device__ __forceinline__ bool as_lq_step(AKnotT<T> (&K)[KPL], const PT<T>& P, 
         g[j][0] = K[j].rh0;
         g[j][1] = K[j].rh1;
     }
-    as_solve<KPL, T>(K, g, N, lane, dr, dx, vn);
+    as_solve<KPL, TR, T>(K, g, N, lane, dr, dx, vn);
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
         if (KPL * lane + j < N) {
@@ -753,7 +818,7 @@ __device__ __forceinline__ void as_guess(AKnotT<T> (&K)[KPL], const RS& R, int N
 // certifies it; a failed pass drops the facets with negative multipliers, adds the violated ones
 // and restores the start point.  Returns true when a pass is certified (the point is then the
 // optimum, pk / pl its active facets and multipliers).
-template <int KPL, class T, class RS>
+template <int KPL, int TR, class T, class RS>
 __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, const RS& R, int NH, int N,
                                           int lane, T xi00, T xi01, int (&pk)[KPL],
                                           T (&pl)[KPL][2], int count_slot, int sb)
@@ -777,7 +842,7 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
         }
         AS_STAMP_ADD(sb + 0, t_s);
         AS_STAMP(t_r);
-        okp = as_riccati<KPL, T>(K, P, E, N, lane) && okp;
+        okp = as_riccati<KPL, TR, T>(K, P, E, N, lane) && okp;
         AS_STAMP_ADD(sb + 1, t_r);
         AS_STAMP(t_h);
 #pragma unroll
@@ -800,7 +865,7 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
                 g[j][1] = K[j].rh1;
             }
             AS_STAMP(t_v);
-            as_solve<KPL, T>(K, g, N, lane, dr, dx, vn);
+            as_solve<KPL, TR, T>(K, g, N, lane, dr, dx, vn);
             AS_STAMP_ADD(sb + 3, t_v);
             AS_STAMP(t_c);
 #pragma unroll
@@ -1062,7 +1127,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
 // global memory, at 2 / 3 / 4 waves per SIMD, and phase A as a kernel of its own — all slower.
 // The cold solve of one QP (the cold kernel's body; the warm kernel runs it for the problems whose
 // previous solve failed, blf_dcm_mpc_warm_start.prev_status).
-template <int KPL, bool LAMOUT, bool PH, bool PAD>
+template <int KPL, bool LAMOUT, bool PH, int TR>
 __device__ __forceinline__ void cold_solve(
     const KParams& P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1073,7 +1138,7 @@ __device__ __forceinline__ void cold_solve(
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
-    assume_pad<KPL, PAD>(N);
+    assume_pad<KPL, TR>(N);
     const int NH = (N + KPL - 1) / KPL;
     const int S = KPL * NH;
     double* A2d = smem;                               // [M][S] double2 normals
@@ -1147,7 +1212,7 @@ __device__ __forceinline__ void cold_solve(
     AS_STAMP_ADD(1, t_start);
     {
         AS_STAMP(t_q);
-        as_lq_step<KPL, float>(F, Pf, N, lane, xf00, xf01);
+        as_lq_step<KPL, TR, float>(F, Pf, N, lane, xf00, xf01);
         if (kOverlap) stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, nA, A2d, Bv);
         __syncthreads();   // the LDS rows (one wavefront: a wait for the stores)
         AS_STAMP_ADD(2, t_q);
@@ -1158,7 +1223,7 @@ __device__ __forceinline__ void cold_solve(
         AS_STAMP(t_a);
         int pkf[KPL];
         float plf[KPL][2];
-        as_passes<KPL, float>(F, Pf, R, NH, N, lane, xf00, xf01, pkf, plf, 12, 16);
+        as_passes<KPL, TR, float>(F, Pf, R, NH, N, lane, xf00, xf01, pkf, plf, 12, 16);
         AS_STAMP_ADD(13, t_a);
     }
 
@@ -1232,7 +1297,7 @@ __device__ __forceinline__ void cold_solve(
     } else {
         const double* const lw0[KPL] = {};
         as_guess<KPL, double>(K, R, NH, N, lane, lw0, 0.0, kGuessSlack);
-        certified = as_passes<KPL, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4);
+        certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4);
         if (!certified) {
             // ---- the IPM's start point: the fp64 LQ optimum from (xi_ref, vrp_ref) ----
 #pragma unroll
@@ -1244,7 +1309,7 @@ __device__ __forceinline__ void cold_solve(
                     K[j].x1 = K[j].xr1;
                 }
             }
-            if (!as_lq_step<KPL, double>(K, Pd, N, lane, xi00, xi01)) status = BLF_QP_NUMERICAL;
+            if (!as_lq_step<KPL, TR, double>(K, Pd, N, lane, xi00, xi01)) status = BLF_QP_NUMERICAL;
         }
     }
     AS_STAMP_ADD(14, t_b);
@@ -1262,7 +1327,7 @@ __device__ __forceinline__ void cold_solve(
 #endif
 }
 
-template <int KPL, bool LAMOUT, bool PH, bool PAD>
+template <int KPL, bool LAMOUT, bool PH, int TR>
 __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1271,7 +1336,7 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
     double* __restrict__ lam_out, PhaseSrc ps)
 {
-    cold_solve<KPL, LAMOUT, PH, PAD>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+    cold_solve<KPL, LAMOUT, PH, TR>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
                                      status_out, iters_out, polished_out, lam_out, ps);
 }
 
@@ -1289,7 +1354,7 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_fused_ker
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
     double* __restrict__ lam_out)
 {
-    cold_solve<1, LAMOUT, false, false>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+    cold_solve<1, LAMOUT, false, kTreeDpp>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
                                         status_out, iters_out, polished_out, lam_out, PhaseSrc{});
     // the outputs just written are stage 2's start point and its status gate; the LDS is reused
     __syncthreads();
@@ -1304,7 +1369,7 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_fused_ker
 // One wavefront per QP, fp64 facet rows in LDS.  From the shifted previous solution (xi rolled
 // out from its VRPs), guess = the facets the rollout violates plus those whose previous multiplier
 // exceeds the floor, then the fp64 passes (1.7 per window on average: no float search first).
-template <int KPL, bool LAMOUT, bool PH, bool PAD>
+template <int KPL, bool LAMOUT, bool PH, int TR>
 __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1320,11 +1385,11 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     // a problem whose previous solve failed (prev_status != 0) is not warm-started from it: it is
     // solved exactly as a cold launch solves it (the IPM's stage 2 treats it as cold too)
     if (P.ws_status != nullptr && P.ws_status[blockIdx.x] != 0) {
-        cold_solve<KPL, LAMOUT, PH, PAD>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+        cold_solve<KPL, LAMOUT, PH, TR>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
                                          status_out, iters_out, polished_out, lam_out, ps);
         return;
     }
-    assume_pad<KPL, PAD>(N);
+    assume_pad<KPL, TR>(N);
     const int NH = (N + KPL - 1) / KPL;   // lanes holding knots
     const int S = KPL * NH;               // LDS row stride: facet i of slot j, lane l at i S + j NH + l
     double2* A2 = reinterpret_cast<double2*>(smem);   // [M][S] facet normals
@@ -1426,7 +1491,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
             const double ga = k < N ? K[j].al : 0.0;
             g[j][0] = ga; g[j][1] = 0.0; g[j][2] = 0.0; g[j][3] = ga;
         }
-        as_scan_forward<KPL, double>(g, f, lane, x, xk, as_pad(KPL, N));
+        as_scan_forward<KPL, TR, double>(g, f, lane, x, xk);
 #pragma unroll
         for (int j = 0; j < KPL; ++j) {
             K[j].x0 = x[j][0];
@@ -1449,7 +1514,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
         as_guess<KPL, double>(K, R, NH, N, lane, lw, P.ws_floor, 0.0);
         AS_STAMP_ADD(3, t_g);
         AS_STAMP(t_b);
-        certified = as_passes<KPL, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4);
+        certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4);
         AS_STAMP_ADD(14, t_b);
     }
     AS_STAMP(t_out);
@@ -1471,8 +1536,11 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
 }
 
 // Batches up to this size take the fused kernel (N <= 64, cold, per-knot input): they fill at
-// most 4 of a CU's wavefront slots, so its larger LDS / register footprint costs nothing.
+// most 4 of a CU's wavefront slots, so its larger LDS / register footprint costs nothing.  They
+// also take the DPP scan tree (kTreeDpp): at most one wavefront per SIMD, so the dependency chain
+// of a wavefront, not the SIMD's VALU issue, sets the time.
 constexpr int64_t kFusedMaxBatch = 1024;
+constexpr int64_t kDppTreeMaxBatch = BLF_DPP_TREE_MAX_BATCH;
 
 template <int KPL>
 blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const blf_dcm_mpc_warm_start* warm,
@@ -1489,7 +1557,11 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
                        (ps ? ph_lds_bytes(ps->P, kp.N) : 0) + AS_EXTRA_LDS;
     if (lds > 64 * 1024)
         return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: %zu B of LDS (%d phases)", lds, ps ? ps->P : 0);
-    const bool pad = KPL == 2 && kp.N <= 2 * kWave - 2;
+    // the scan tree: DPP for small batches with one knot per lane (the oracle's as_tree follows the
+    // same rule); knot pairs always take the ds_bpermute tree
+    constexpr int kAltTree = KPL == 2 ? kTreePad : kTreeDpp;   // the instantiated trees: this, kTreeKS
+    const int tr = (KPL == 1 && batch <= kDppTreeMaxBatch) ? kTreeDpp
+                   : (KPL == 2 && kp.N <= 2 * kWave - 2) ? kTreePad : kTreeKS;
     const char* fz = getenv("BLF_QP_FUSE_STAGE2");
     if (KPL == 1 && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch && !(fz && fz[0] == '0')) {
         const size_t lds_f = std::max(lds, sizeof(double) * Lds(nullptr, kp.N, kp.M, 1).total);
@@ -1502,10 +1574,10 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     }
     if (warm == nullptr) {
 #define AS_COLD(L, H, D) dcm_mpc_cold_kernel<KPL, L, H, D>
-        auto kern = pad ? (ps ? (lam_out ? AS_COLD(true, true, true) : AS_COLD(false, true, true))
-                              : (lam_out ? AS_COLD(true, false, true) : AS_COLD(false, false, true)))
-                        : (ps ? (lam_out ? AS_COLD(true, true, false) : AS_COLD(false, true, false))
-                              : (lam_out ? AS_COLD(true, false, false) : AS_COLD(false, false, false)));
+#define AS_COLD_TR(D) (ps ? (lam_out ? AS_COLD(true, true, D) : AS_COLD(false, true, D)) \
+                          : (lam_out ? AS_COLD(true, false, D) : AS_COLD(false, false, D)))
+        auto kern = tr == kAltTree ? AS_COLD_TR(kAltTree) : AS_COLD_TR(kTreeKS);
+#undef AS_COLD_TR
 #undef AS_COLD
         hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds, s, kp,
                            pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, sol->xi,
@@ -1513,10 +1585,10 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
         return check_hip(hipGetLastError(), "dcm_mpc_cold_kernel launch");
     }
 #define AS_WARM(L, H, D) dcm_mpc_warm_kernel<KPL, L, H, D>
-    auto kern = pad ? (ps ? (lam_out ? AS_WARM(true, true, true) : AS_WARM(false, true, true))
-                          : (lam_out ? AS_WARM(true, false, true) : AS_WARM(false, false, true)))
-                    : (ps ? (lam_out ? AS_WARM(true, true, false) : AS_WARM(false, true, false))
-                          : (lam_out ? AS_WARM(true, false, false) : AS_WARM(false, false, false)));
+#define AS_WARM_TR(D) (ps ? (lam_out ? AS_WARM(true, true, D) : AS_WARM(false, true, D)) \
+                          : (lam_out ? AS_WARM(true, false, D) : AS_WARM(false, false, D)))
+    auto kern = tr == kAltTree ? AS_WARM_TR(kAltTree) : AS_WARM_TR(kTreeKS);
+#undef AS_WARM_TR
 #undef AS_WARM
     hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, warm->vrp,

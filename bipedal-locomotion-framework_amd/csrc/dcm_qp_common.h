@@ -100,6 +100,88 @@ __device__ __forceinline__ float dpp1(float x)
     return __int_as_float(dpp1<CTRL>(__float_as_int(x)));
 }
 
+// ---- the DPP scan tree of the active-set kernels (small batches): every level a VALU move ----
+// Kogge-Stone inside each row of 16 lanes by DPP row shifts (4 levels), then two row-level steps
+// (oracle orc_lane_src):
+//   forward (a lane combines with lower lanes): row_shr:1,2,4,8, then rows 1 and 3 take lane 15 of
+//     the row before (row_bcast:15), then rows 2 and 3 take lane 31 (row_bcast:31);
+//   backward (a lane combines with higher lanes): row_shl:1,2,4,8, then rows 0 and 2 take the first
+//     lane of the row after (row_newbcast:0, then v_permlane16_swap moves rows 1 / 3 onto rows
+//     0 / 2), then rows 0 and 1 take lane 32 (v_readlane).
+// tree_fwd / tree_bwd return the level's source value (undefined on a lane without a source);
+// tree_has says whether the lane has one — only those lanes combine (the others keep their
+// element), and the oracle combines at exactly the same lanes.
+enum : int { kRowShr = 0x110, kRowShl = 0x100, kRowBcast15 = 0x142, kRowBcast31 = 0x143, kRowNewBcast0 = 0x150 };
+
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_mov(int x)
+{
+    return __builtin_amdgcn_mov_dpp(x, CTRL, RM, 0xF, true);
+}
+
+// rows 0 and 2 <- the first lane of rows 1 and 3
+__device__ __forceinline__ int next_row_first(int x)
+{
+    const int t = dpp_mov<kRowNewBcast0, 0xF>(x);
+    return (int)__builtin_amdgcn_permlane16_swap((unsigned)t, (unsigned)t, false, false)[1];
+}
+
+template <int L, bool FWD>
+__device__ __forceinline__ int tree_src(int x)
+{
+    if constexpr (FWD) {
+        if constexpr (L < 4) return dpp_mov<kRowShr + (1 << L), 0xF>(x);
+        else if constexpr (L == 4) return dpp_mov<kRowBcast15, 0xA>(x);
+        else return dpp_mov<kRowBcast31, 0xC>(x);
+    } else {
+        if constexpr (L < 4) return dpp_mov<kRowShl + (1 << L), 0xF>(x);
+        else if constexpr (L == 4) return next_row_first(x);
+        else return __builtin_amdgcn_readlane(x, 32);
+    }
+}
+
+template <int L, bool FWD>
+__device__ __forceinline__ float tree_src(float x)
+{
+    return __int_as_float(tree_src<L, FWD>(__float_as_int(x)));
+}
+
+template <int L, bool FWD>
+__device__ __forceinline__ double tree_src(double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = tree_src<L, FWD>((int)b);
+    const int hi = tree_src<L, FWD>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <int L, class T>
+__device__ __forceinline__ T tree_fwd(T x)
+{
+    return tree_src<L, true>(x);
+}
+
+template <int L, class T>
+__device__ __forceinline__ T tree_bwd(T x)
+{
+    return tree_src<L, false>(x);
+}
+
+template <int L, bool FWD>
+__device__ __forceinline__ bool tree_has(int lane)
+{
+    const int r = lane >> 4;
+    if constexpr (FWD) {
+        if constexpr (L < 4) return (lane & 15) >= (1 << L);
+        else if constexpr (L == 4) return (r & 1) != 0;
+        else return r >= 2;
+    } else {
+        if constexpr (L < 4) return (lane & 15) + (1 << L) <= 15;
+        else if constexpr (L == 4) return (r & 1) == 0;
+        else return r < 2;
+    }
+}
+
 // Fused forms used throughout (and in the same places by oracle/blf_oracle.c):
 //   FD2(a, b, c, d)    = a b + c d      as fma(a, b, c d)
 //   FD3(a, b, c, d, e) = a b + c d + e  as fma(a, b, fma(c, d, e))

@@ -22,6 +22,13 @@ namespace blf {
 namespace {
 
 constexpr int kHullBlock = 64;
+// LDS row stride of the X / Y arrays in doubles, and the Y array's extra offset.  A row is 64
+// polygons; 68 = 64 + 4 puts vertex row a of polygon r on bank pair (8 a + 2 r) mod 64, so the
+// eight facets of a polygon that phase 2 reads in one lane group hit distinct banks (a stride of
+// 64 put all eight on one bank: 8-way), and the Y array's 2-double offset interleaves the
+// staging stores of X and Y (16-way on one bank pair before: 13 % of the wave's cycles).
+constexpr int kHullStride = 68;
+constexpr int kHullYOff = 2;
 #ifndef BLF_HULL_U
 #define BLF_HULL_U 8
 #endif
@@ -35,7 +42,7 @@ __device__ __forceinline__ double cross3(double ox, double oy, double ax, double
 
 // Dynamic LDS of hull2d_kernel, per workgroup of 64 polygons (one per lane), lane-minor so that
 // the data-dependent indices of the sort and the chain never conflict:
-//   X, Y   [P][64] doubles: the polygon's points, sorted in place by the lane
+//   X, Y   [P][kHullStride] doubles (Y offset by kHullYOff): the points, sorted in place by the lane
 //   stack  P <= 8: [64] uint64, the monotone chain packed 3 bits per entry (at most 2P + 2 = 18
 //          entries), held in a register while the chain runs;
 //          P > 8: [2P+2][64] int32, the chain as positions in the sorted arrays
@@ -45,10 +52,9 @@ __device__ __forceinline__ double cross3(double ox, double oy, double ax, double
 __host__ __device__ inline bool hull2d_packed(int P) { return P <= 8; }
 __host__ __device__ inline size_t hull2d_lds_bytes(int P, int /*M*/)
 {
-    if (hull2d_packed(P))
-        return sizeof(double) * kHullBlock * 2 * P + sizeof(uint64_t) * kHullBlock +
-               sizeof(int32_t) * kHullBlock;
-    return sizeof(double) * kHullBlock * 2 * P + sizeof(int32_t) * kHullBlock * (2 * P + 3);
+    const size_t xy = sizeof(double) * ((size_t)kHullStride * 2 * P + kHullYOff);
+    if (hull2d_packed(P)) return xy + sizeof(uint64_t) * kHullBlock + sizeof(int32_t) * kHullBlock;
+    return xy + sizeof(int32_t) * kHullBlock * (2 * P + 3);
 }
 
 __device__ __forceinline__ int hull2d_rows(int64_t batch, int64_t p0)
@@ -73,10 +79,10 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     const int t = threadIdx.x;
     const int64_t p0 = (int64_t)blockIdx.x * kHullBlock;
     const int nprob = hull2d_rows(batch, p0);
-    double* s_x = hull_smem;                                               // [P][64]
-    double* s_y = s_x + kHullBlock * P;                                    // [P][64]
-    int32_t* s_stk = reinterpret_cast<int32_t*>(s_y + kHullBlock * P);     // [2P+2][64] (!PK)
-    uint64_t* s_pk = reinterpret_cast<uint64_t*>(s_y + kHullBlock * P);    // [64] (PK)
+    double* s_x = hull_smem;                                               // [P][68]
+    double* s_y = s_x + kHullStride * P + kHullYOff;                       // [P][68]
+    int32_t* s_stk = reinterpret_cast<int32_t*>(s_y + kHullStride * P);    // [2P+2][64] (!PK)
+    uint64_t* s_pk = reinterpret_cast<uint64_t*>(s_y + kHullStride * P);   // [64] (PK)
     int32_t* s_nf = PK ? reinterpret_cast<int32_t*>(s_pk + kHullBlock) : s_stk + kHullBlock * (2 * P + 2);
     {
         // coalesced load of the [64][P][2] slab, transposed into X / Y (8 loads per lane in flight)
@@ -95,14 +101,14 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                 const int e = base + u * kHullBlock + t;
                 if (e < n) {
                     const int r = ix.row(e), c = e - r * 2 * P;
-                    (c & 1 ? s_y : s_x)[(c >> 1) * kHullBlock + r] = v[u];
+                    (c & 1 ? s_y : s_x)[(c >> 1) * kHullStride + r] = v[u];
                 }
             }
         }
     }
     __syncthreads();
-#define HX(i) s_x[(i) * kHullBlock + t]
-#define HY(i) s_y[(i) * kHullBlock + t]
+#define HX(i) s_x[(i) * kHullStride + t]
+#define HY(i) s_y[(i) * kHullStride + t]
     // the chain stack: packed 3-bit entries in a register (PK), else lane-minor int32 in LDS
     uint64_t stk = 0;
 #define STK_GET(i) (PK ? (int)((stk >> (3 * (i))) & 7) : s_stk[(i) * kHullBlock + t])
@@ -254,9 +260,9 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                 a = s_stk[j * kHullBlock + r];
                 b = s_stk[(j + 1) * kHullBlock + r];
             }
-            const double v0x = s_x[a * kHullBlock + r], v0y = s_y[a * kHullBlock + r];
-            const double ex = s_x[b * kHullBlock + r] - v0x;
-            const double ey = s_y[b * kHullBlock + r] - v0y;
+            const double v0x = s_x[a * kHullStride + r], v0y = s_y[a * kHullStride + r];
+            const double ex = s_x[b * kHullStride + r] - v0x;
+            const double ey = s_y[b * kHullStride + r] - v0y;
             // one reciprocal of the edge length instead of two quotients (oracle orc_hull2d_hrep)
             const double il = 1.0 / sqrt(ex * ex + ey * ey);
             nx = ey * il;

@@ -233,6 +233,13 @@ typedef struct blf_dcm_mpc_warm_start {
     const int32_t* prev_status; /* [B] or NULL (NULL: every problem warm-started)             */
 } blf_dcm_mpc_warm_start;
 
+/* Batches of at most this many QPs (horizon <= 64) evaluate the solver's recursions in a
+ * different association order (the DPP scan tree), tuned for latency; larger
+ * batches use the throughput tree.  Both return the certified optimum; the two orders can differ
+ * in the last bits, so a problem is bit-reproducible within either size class (and bit-identical to
+ * the oracle, which follows the same rule). */
+#define BLF_DPP_TREE_MAX_BATCH 1024
+
 /* Fill `p` with the defaults used by the benchmark (dt 0.02, Q 1e2, R 1, P 1e3, tol_mu 1e-16,
  * tol_primal 1e-10, tol_dual 1e-9, tol_polish 3e-4, max_iter 50, max_facets 8). */
 void blf_dcm_mpc_default_params(blf_dcm_mpc_params* p, int32_t horizon);

@@ -450,6 +450,7 @@ typedef struct {
     int N, M, NW, ntot;
     int scans;                             /* 1: device-order Kogge-Stone scans, 0: sequential */
     int pairs;                             /* 1: the active-set kernel's pair tree (64 < N <= 128) */
+    int dpp;                               /* 1: the active-set kernels' DPP tree (N <= 128) */
     double dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1;
     const double *omega, *xi_ref, *vrp_ref, *A, *b;
     const int32_t* nf;
@@ -576,6 +577,114 @@ static void scan_forward_pairs(dcm_ws* w, const double* F, int transpose, const 
     }
 }
 
+/* ---- the active-set kernels' DPP tree (csrc/dcm_qp_common.h tree_fwd / tree_bwd; batches of at
+ * most BLF_DPP_TREE_MAX_BATCH QPs, orc_dcm_params.as_tree = 1): lane l of ONE wavefront owns KPL
+ * knots (knot l for N <= 64, the pair 2l, 2l + 1 for 64 < N <= 128); a pair's element is composed
+ * in the lane, the 64 lane elements are scanned Kogge-Stone inside each row of 16 lanes, then in
+ * two row-level steps (orc_lane_src), and a pair's inner knot is applied in the lane. ---- */
+int orc_lane_src(int L, int fwd, int l)
+{
+    const int r = l >> 4, d = 1 << L;
+    if (fwd) {
+        if (L < 4) return (l & 15) >= d ? l - d : -1;   /* row_shr:d */
+        if (L == 4) return (r & 1) ? 16 * r - 1 : -1;    /* row_bcast:15, rows 1 and 3 */
+        return r >= 2 ? 31 : -1;                         /* row_bcast:31, rows 2 and 3 */
+    }
+    if (L < 4) return (l & 15) + d <= 15 ? l + d : -1;   /* row_shl:d */
+    if (L == 4) return (r & 1) ? -1 : 16 * r + 16;       /* row_newbcast:0 + permlane16_swap */
+    return r < 2 ? 32 : -1;                              /* v_readlane 32, rows 0 and 1 */
+}
+
+#define AS_LEVELS 6
+
+/* the DPP tree over the 64 lane elements (g, e): a lane combines with its level's source lane's
+ * element when it has one (orc_lane_src >= 0), and keeps its element otherwise */
+static void aff_tree(double (*g)[4], double (*e)[2], int fwd)
+{
+    double ng[WV][4], ne[WV][2];
+    for (int L = 0; L < AS_LEVELS; ++L) {
+        for (int l = 0; l < WV; ++l) {
+            const int s = orc_lane_src(L, fwd, l);
+            memcpy(ng[l], g[l], sizeof(ng[l]));
+            memcpy(ne[l], e[l], sizeof(ne[l]));
+            if (s >= 0) aff_compose(ng[l], ne[l], g[s], e[s]);
+        }
+        memcpy(g, ng, sizeof(ng));
+        memcpy(e, ne, sizeof(ne));
+    }
+}
+
+static void scan_backward_dpp(dcm_ws* w, const double* G, const double* c)
+{
+    const int N = w->N, KPL = N > WV ? 2 : 1;
+    double g[WV][4], e[WV][2];
+    for (int l = 0; l < WV; ++l) {
+        const int k0 = KPL * l, k1 = KPL * l + 1;
+        for (int j = 0; j < 4; ++j) g[l][j] = k0 < N ? G[4 * k0 + j] : 0.0;
+        for (int j = 0; j < 2; ++j) e[l][j] = k0 < N ? c[2 * k0 + j] : 0.0;
+        if (KPL == 2) {
+            double b[4], cc[2];
+            for (int j = 0; j < 4; ++j) b[j] = k1 < N ? G[4 * k1 + j] : 0.0;
+            for (int j = 0; j < 2; ++j) cc[j] = k1 < N ? c[2 * k1 + j] : 0.0;
+            aff_compose(g[l], e[l], b, cc);            /* knot 2l after knot 2l + 1 */
+        }
+    }
+    aff_tree(g, e, 0);
+    for (int l = 0; l < WV; ++l) {               /* v_{KPL l} = e_l; v_{2l+1} = G v_{2l+2} + c */
+        const int k0 = KPL * l, k1 = KPL * l + 1;
+        if (k0 < N) { w->v[2 * k0] = e[l][0]; w->v[2 * k0 + 1] = e[l][1]; }
+        if (KPL == 2 && k1 < N) {
+            const double vb0 = l + 1 < WV ? e[l + 1][0] : 0.0, vb1 = l + 1 < WV ? e[l + 1][1] : 0.0;
+            const double* Gk = G + 4 * k1;
+            w->v[2 * k1] = FD3(Gk[0], vb0, Gk[1], vb1, c[2 * k1]);
+            w->v[2 * k1 + 1] = FD3(Gk[2], vb0, Gk[3], vb1, c[2 * k1 + 1]);
+        }
+    }
+}
+
+static void scan_forward_dpp(dcm_ws* w, const double* F, int transpose, const double* f)
+{
+    const int N = w->N, KPL = N > WV ? 2 : 1;
+    double g[WV][4], e[WV][2];
+    double F0[WV][4], f0[WV][2];
+    for (int l = 0; l < WV; ++l) {
+        double Fk[2][4], fk[2][2];
+        for (int q = 0; q < KPL; ++q) {
+            const int k = KPL * l + q;
+            if (k < N) {
+                const double* Fp = F + 4 * k;
+                Fk[q][0] = Fp[0];
+                Fk[q][1] = transpose ? Fp[2] : Fp[1];
+                Fk[q][2] = transpose ? Fp[1] : Fp[2];
+                Fk[q][3] = Fp[3];
+                fk[q][0] = f[2 * k];
+                fk[q][1] = f[2 * k + 1];
+            } else {
+                Fk[q][0] = Fk[q][1] = Fk[q][2] = Fk[q][3] = 0.0;
+                fk[q][0] = fk[q][1] = 0.0;
+            }
+        }
+        memcpy(F0[l], Fk[0], sizeof(F0[l]));
+        memcpy(f0[l], fk[0], sizeof(f0[l]));
+        memcpy(g[l], Fk[KPL - 1], sizeof(g[l]));
+        memcpy(e[l], fk[KPL - 1], sizeof(e[l]));
+        if (KPL == 2) aff_compose(g[l], e[l], Fk[0], fk[0]);   /* knot 2l + 1 after knot 2l */
+    }
+    aff_tree(g, e, 1);
+    for (int l = 0; l < WV; ++l) {               /* x past the lane's last knot = e_l */
+        const int k0 = KPL * l, kl = KPL * l + KPL - 1;
+        if (KPL == 2 && k0 < N) {                /* x_{2l+1} = F x_{2l} + f */
+            const double xb0 = l > 0 ? e[l - 1][0] : 0.0, xb1 = l > 0 ? e[l - 1][1] : 0.0;
+            w->x[2 * (k0 + 1)] = FD3(F0[l][0], xb0, F0[l][1], xb1, f0[l][0]);
+            w->x[2 * (k0 + 1) + 1] = FD3(F0[l][2], xb0, F0[l][3], xb1, f0[l][1]);
+        }
+        if (kl < N) {
+            w->x[2 * (kl + 1)] = e[l][0];
+            w->x[2 * (kl + 1) + 1] = e[l][1];
+        }
+    }
+}
+
 /* Backward affine recursion v_k = G_k v_{k+1} + c_k (v_N = 0) the way the device evaluates it:
  * a Kogge-Stone scan over the 64 lanes of each wavefront (lane l combines with lane l + d from
  * the previous level, d = 1, 2, ..., 32; lanes past the last knot hold the zero element), then
@@ -595,6 +704,7 @@ static void scan_backward(dcm_ws* w, const double* G, const double* c)
         }
         return;
     }
+    if (w->dpp) { scan_backward_dpp(w, G, c); return; }
     if (w->pairs) { scan_backward_pairs(w, G, c); return; }
     for (int wv = w->NW - 1; wv >= 0; --wv) {
         double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
@@ -657,6 +767,7 @@ static void scan_forward(dcm_ws* w, const double* F, int transpose, const double
         }
         return;
     }
+    if (w->dpp) { scan_forward_dpp(w, F, transpose, f); return; }
     if (w->pairs) { scan_forward_pairs(w, F, transpose, f); return; }
     for (int wv = 0; wv < w->NW; ++wv) {
         double g[WV][4], e[WV][2], ng[WV][4], ne[WV][2];
@@ -899,6 +1010,53 @@ static int riccati_sweep_pairs(dcm_ws* w)
     return ok;
 }
 
+/* riccati_sweep in the active-set kernels' DPP tree (see scan_backward_dpp): the lane element
+ * (the pair e_{2l} o e_{2l+1} for KPL = 2), the DPP tree, P at the lane's first knot
+ * = f(P_N); a knot's P_{k+1} from the next lane (P_{2l+1} = f_{2l+1}(P_{2l+2}) in the lane). */
+static int riccati_sweep_dpp(dcm_ws* w)
+{
+    const int N = w->N, KPL = N > WV ? 2 : 1;
+    int ok = 1;
+    rc_el e[WV], ne[WV];
+    for (int l = 0; l < WV; ++l) {
+        rc_knot(w, KPL * l, &e[l]);
+        if (KPL == 2) {
+            rc_el e1;
+            rc_knot(w, 2 * l + 1, &e1);
+            if (!rc_combine(&e[l], &e1)) ok = 0;
+        }
+    }
+    for (int L = 0; L < AS_LEVELS; ++L) {
+        for (int l = 0; l < WV; ++l) {
+            const int src = orc_lane_src(L, 0, l);
+            ne[l] = e[l];
+            if (src >= 0 && !rc_combine(&ne[l], &e[src])) ok = 0;
+        }
+        memcpy(e, ne, sizeof(e));
+    }
+    double P0[WV][3];
+    for (int l = 0; l < WV; ++l)
+        if (!rc_apply(&e[l], w->Pw0, 0.0, w->Pw1, P0[l])) ok = 0;
+    for (int l = 0; l < WV; ++l) {
+        double Pn[3] = {w->Pw0, 0.0, w->Pw1};
+        if (l + 1 < WV) { Pn[0] = P0[l + 1][0]; Pn[1] = P0[l + 1][1]; Pn[2] = P0[l + 1][2]; }
+        const int kl = KPL * l + KPL - 1;   /* the lane's last knot takes P from the next lane */
+        if (kl < N) { w->Pn[3 * kl] = Pn[0]; w->Pn[3 * kl + 1] = Pn[1]; w->Pn[3 * kl + 2] = Pn[2]; }
+        if (KPL == 2) {
+            const int k0 = 2 * l;
+            rc_el e1;
+            rc_knot(w, 2 * l + 1, &e1);
+            double P1[3];
+            if (!rc_apply(&e1, Pn[0], Pn[1], Pn[2], P1)) ok = 0;
+            if (k0 < N) { w->Pn[3 * k0] = P1[0]; w->Pn[3 * k0 + 1] = P1[1]; w->Pn[3 * k0 + 2] = P1[2]; }
+        }
+    }
+    w->Pn[3 * (N - 1)] = w->Pw0;
+    w->Pn[3 * (N - 1) + 1] = 0.0;
+    w->Pn[3 * (N - 1) + 2] = w->Pw1;
+    return ok;
+}
+
 /* Riccati sweep for the per-knot E_k = w->E: P_k for every knot by a Kogge-Stone
  * scan of Riccati map elements over the 64 lanes of each wavefront (lane l composes with lane
  * l + d), then P_k = f_{k..}(P at the next wavefront's first knot, or P_N = diag(Pw)), wavefronts
@@ -921,6 +1079,7 @@ static int riccati_sweep(dcm_ws* w)
             Pb0 = out[0]; Pb1 = out[1]; Pb2 = out[2];
         }
     }
+    if (w->scans && w->dpp) return riccati_sweep_dpp(w);
     if (w->scans && w->pairs) return riccati_sweep_pairs(w);
     for (int wv = w->scans ? w->NW - 1 : -1; wv >= 0; --wv) {
         rc_el e[WV], ne[WV];
@@ -1372,6 +1531,8 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      * with the start enabled (csrc/dcm_mpc_ipm.hip launch_dcm_mpc); the IPM iterations always in
      * the wavefront tree of the IPM kernel */
     w->pairs = (prm->tol_polish > 0.0 && N > WV && N <= 2 * WV && !prm->single_kernel) ? 1 : 0;
+    /* small batches, one knot per lane: the active-set kernels' DPP tree (prm->as_tree) */
+    w->dpp = (prm->tol_polish > 0.0 && N <= WV && !prm->single_kernel && prm->as_tree) ? 1 : 0;
     w->Qw0 = prm->w_xi[0]; w->Qw1 = prm->w_xi[1];
     w->Rw0 = prm->w_vrp[0]; w->Rw1 = prm->w_vrp[1];
     w->Pw0 = prm->w_terminal[0]; w->Pw1 = prm->w_terminal[1];
@@ -1519,6 +1680,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      * the start point was restored exactly */
 
     w->pairs = 0;   /* the IPM kernel's tree from here on */
+    w->dpp = 0;
     /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s; warm: s = max(b - A r, floor),
      *      lam = max(lam_warm[src], floor) with the same source knot as the VRP ---- */
     double dres = 0.0;

@@ -86,7 +86,8 @@ typedef struct orc_dcm_params {
     double dt, w_xi[2], w_vrp[2], w_terminal[2], tol_mu, tol_primal, tol_dual;
     double tol_polish;   /* > 0: try the active-set polish once mu <= tol_polish */
     int32_t single_kernel;   /* 1: the device's BLF_QP_SINGLE_KERNEL=1 path (IPM kernel alone) */
-    int32_t reserved;
+    int32_t as_tree;         /* 1: the active-set kernels' DPP scan tree, as the device evaluates
+                              * horizons <= 64 in batches of at most BLF_DPP_TREE_MAX_BATCH QPs */
 } orc_dcm_params;
 
 /* Solve one problem (arrays for this problem only, same layout as blf_dcm_mpc_problem).
@@ -160,6 +161,10 @@ void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int 
  * zeros to 64*ceil(n/64); per 64-block xor-butterfly (distances 1, 2, 4, ..., 32), then block
  * sums left to right. */
 double orc_wave_tree_sum(const double* c, int n);
+/* The active-set kernels' scan tree (csrc/dcm_qp_common.h tree_fwd / tree_bwd): the lane whose
+ * element lane l combines with at level L = 0..5 (fwd: lower lanes, else higher lanes), or -1 (the
+ * identity element). */
+int orc_lane_src(int level, int fwd, int l);
 
 /* ContinuousContactModel (one contact).  prm = {length, width, spring_coeff, damper_coeff};
  * twist = {v[3], w[3]} (mixed); pose / null_pose = {p[3], R[9] row-major}.  Outputs (NULL to skip):

@@ -7,7 +7,7 @@
  * drop/add passes entirely in float, with the kernel's operations in the kernel's order: every
  * expression below is the float instance of the templated device code, lane by lane (lane l owns
  * knot l for N <= 64, the knot pair 2l, 2l + 1 for 64 < N <= 128), the scans in the same
- * Kogge-Stone tree.  C float arithmetic with fmaf and IEEE division rounds exactly like the
+ * tree (Kogge-Stone, or the DPP tree for small batches).  C float arithmetic with fmaf and IEEE division rounds exactly like the
  * device's v_fma_f32 / correctly rounded division, and the fp64 -> fp32 conversions round to
  * nearest on both sides, so the search's outputs are bit-identical to the kernel's.
  * `sequential` = 1 evaluates the same search with plain recursions (CPU baseline only). */
@@ -29,7 +29,7 @@ typedef struct { float dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_p, tol_d; } pf_t;
 typedef struct { float a0, a1, a2, a3, g0, g1, g2, h0, h1, h2; } rcf;
 
 typedef struct {
-    int N, M, KPL, seq;
+    int N, M, KPL, seq, dpp;   /* dpp: the DPP scan tree (orc_dcm_params.as_tree) */
     pf_t P;
     const double *A, *b;
     int m[2 * WV], gm[2 * WV], drop[2 * WV], add[2 * WV];
@@ -158,7 +158,15 @@ static int riccati32(s32* s, const float (*E)[3])
         }
     }
     const int pad = KPL == 2 && N <= 2 * WV - 2;   /* the kernel's as_pad: lane WV - 1's identity */
-    for (int d = 1; d < WV; d <<= 1) {
+    for (int L = 0; s->dpp && L < 6; ++L) {   /* the DPP tree (orc_lane_src) */
+        for (int l = 0; l < WV; ++l) {
+            const int src = orc_lane_src(L, 0, l);
+            ne[l] = e[l];
+            if (src >= 0 && !rcf_combine(&ne[l], &e[src])) ok = 0;
+        }
+        memcpy(e, ne, sizeof(e));
+    }
+    for (int d = 1; !s->dpp && d < WV; d <<= 1) {
         for (int l = 0; l < WV; ++l) {
             ne[l] = e[l];
             if (l + d < WV) {
@@ -201,6 +209,23 @@ static void compose(float* a, float* e, const float* b, const float* c)
     a[0] = n0; a[1] = n1; a[2] = n2; a[3] = n3; e[0] = m0; e[1] = m1;
 }
 
+/* the DPP tree over the 64 lane elements (g, e): a lane combines with its level's source lane's
+ * element when it has one (orc_lane_src >= 0) */
+static void aff_tree32(float (*g)[4], float (*e)[2], int fwd)
+{
+    float ng[WV][4], ne[WV][2];
+    for (int L = 0; L < 6; ++L) {
+        for (int l = 0; l < WV; ++l) {
+            const int src = orc_lane_src(L, fwd, l);
+            memcpy(ng[l], g[l], sizeof(ng[l]));
+            memcpy(ne[l], e[l], sizeof(ne[l]));
+            if (src >= 0) compose(ng[l], ne[l], g[src], e[src]);
+        }
+        memcpy(g, ng, sizeof(ng));
+        memcpy(e, ne, sizeof(ne));
+    }
+}
+
 /* as_scan_backward: vn[k] = v_{k+1} for v_k = G_k v_{k+1} + c_k, v_N = 0 (every knot < 2 WV) */
 static void scan_backward32(const s32* s, float (*G)[4], float (*c)[2], float (*vn)[2])
 {
@@ -222,7 +247,8 @@ static void scan_backward32(const s32* s, float (*G)[4], float (*c)[2], float (*
         if (KPL == 2) compose(g[l], e[l], G[2 * l + 1], c[2 * l + 1]);
     }
     const int pad = KPL == 2 && N <= 2 * WV - 2;   /* lane WV - 1's zero element (kernel as_pad) */
-    for (int d = 1; d < WV; d <<= 1) {
+    if (s->dpp) aff_tree32(g, e, 0);
+    for (int d = 1; !s->dpp && d < WV; d <<= 1) {
         for (int l = 0; l < WV; ++l) {
             memcpy(ng[l], g[l], sizeof(ng[l]));
             memcpy(ne[l], e[l], sizeof(ne[l]));
@@ -270,7 +296,8 @@ static void scan_forward32(const s32* s, float (*F)[4], float (*f)[2], float (*x
         if (KPL == 2) compose(g[l], e[l], F[2 * l], f[2 * l]);
     }
     const int pad = KPL == 2 && N <= 2 * WV - 2;   /* lane WV - 1's zero element (kernel as_pad) */
-    for (int d = 1; d < WV; d <<= 1) {
+    if (s->dpp) aff_tree32(g, e, 1);
+    for (int d = 1; !s->dpp && d < WV; d <<= 1) {
         for (int l = 0; l < WV; ++l) {
             memcpy(ng[l], g[l], sizeof(ng[l]));
             memcpy(ne[l], e[l], sizeof(ne[l]));
@@ -592,6 +619,7 @@ void orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi
     s->M = prm->max_facets;
     s->KPL = N <= WV ? 1 : 2;
     s->seq = sequential;
+    s->dpp = (prm->as_tree && s->KPL == 1) ? 1 : 0;
     s->A = A;
     s->b = b;
     s->P.dt = (float)prm->dt;

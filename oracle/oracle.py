@@ -30,7 +30,7 @@ class OrcParams(ctypes.Structure):
                 ("w_vrp", ctypes.c_double * 2), ("w_terminal", ctypes.c_double * 2),
                 ("tol_mu", ctypes.c_double), ("tol_primal", ctypes.c_double),
                 ("tol_dual", ctypes.c_double), ("tol_polish", ctypes.c_double),
-                ("single_kernel", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("single_kernel", ctypes.c_int32), ("as_tree", ctypes.c_int32)]
 
 
 def build():
@@ -228,10 +228,25 @@ def default_params(horizon, **kw):
     return p
 
 
-def dcm_mpc_solve(prob, params=None, index=0):
-    """Solve problem `index` of a batch dict (keys as produced by blf.problems)."""
+# The device evaluates batches of at most this many QPs in its DPP scan tree (include/blf/blf_c.h
+# BLF_DPP_TREE_MAX_BATCH); the oracle follows the same rule through orc_dcm_params.as_tree.
+DPP_TREE_MAX_BATCH = 1024
+
+
+def _tree_params(params, N, device_batch):
+    """A copy of `params` (default_params(N) if None) with as_tree set for a device launch of
+    `device_batch` QPs."""
+    p = OrcParams()
+    ctypes.memmove(ctypes.byref(p), ctypes.byref(params or default_params(N)), ctypes.sizeof(OrcParams))
+    p.as_tree = 1 if device_batch <= DPP_TREE_MAX_BATCH else 0
+    return p
+
+
+def dcm_mpc_solve(prob, params=None, index=0, device_batch=None):
+    """Solve problem `index` of a batch dict (keys as produced by blf.problems), as a device launch
+    of `device_batch` QPs evaluates it (default: the dict's batch size)."""
     N = prob["omega"].shape[1]
-    p = params or default_params(N)
+    p = _tree_params(params, N, prob["omega"].shape[0] if device_batch is None else device_batch)
     xi = np.zeros((N + 1, 2))
     vrp = np.zeros((N, 2))
     it = np.zeros(1, dtype=np.int32)
@@ -242,10 +257,12 @@ def dcm_mpc_solve(prob, params=None, index=0):
     return st, xi, vrp, int(it[0])
 
 
-def dcm_mpc_solve_batch(prob, params=None, threads=1, count=None):
+def dcm_mpc_solve_batch(prob, params=None, threads=1, count=None, device_batch=None):
+    """The first `count` problems (default: all), as a device launch of `device_batch` QPs
+    evaluates them (default: the dict's batch size)."""
     B = prob["omega"].shape[0] if count is None else count
     N = prob["omega"].shape[1]
-    p = params or default_params(N)
+    p = _tree_params(params, N, prob["omega"].shape[0] if device_batch is None else device_batch)
     xi = np.zeros((B, N + 1, 2))
     vrp = np.zeros((B, N, 2))
     status = np.zeros(B, dtype=np.int32)
@@ -258,13 +275,13 @@ def dcm_mpc_solve_batch(prob, params=None, threads=1, count=None):
 
 
 def dcm_mpc_solve_batch_warm(prob, vrp_ws=None, lam_ws=None, shift=1, floor=1e-4,
-                             params=None, threads=1, polished=None, prev_status=None):
+                             params=None, threads=1, polished=None, prev_status=None, device_batch=None):
     """Batch solve from warm starts (vrp_ws [B][N][2], lam_ws [B][N][M]; None: cold starts;
     prev_status [B]: problems with a nonzero previous status start cold).
     Returns status, xi, vrp, iters, lam [B][N][M] (final multipliers); `polished` (an int32 [B]
     array, optional) receives whether the active-set polish was accepted."""
     B, N = prob["omega"].shape
-    p = params or default_params(N)
+    p = _tree_params(params, N, B if device_batch is None else device_batch)
     M = p.max_facets
     xi = np.zeros((B, N + 1, 2))
     vrp = np.zeros((B, N, 2))

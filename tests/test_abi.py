@@ -29,6 +29,14 @@ def test_header_declares_and_library_exports_every_symbol():
     assert not missing, missing
 
 
+def test_library_was_built_from_this_tree():
+    """Build provenance: the source hash compiled into blf_version() (Makefile SRC_HASH) equals the
+    hash of the kernel / C-ABI sources in this tree, so the loaded .so is the committed code."""
+    prov = native.build_provenance()
+    assert prov["tree_src_hash"] is not None
+    assert prov["matches"], prov
+
+
 def test_library_is_built_for_gfx950_only():
     # the .hip_fatbin bundle names one code object per offload target
     out = subprocess.run(["strings", native.LIB_PATH], capture_output=True, text=True).stdout

@@ -196,7 +196,7 @@ def test_config3_rank7_shard_bitwise(handle, oracle):
     host = {k: np.ascontiguousarray(prob[k][idx]) for k in ("xi_init", "omega", "xi_ref", "vrp_ref")}
     for k, v in (("A", A), ("b", b), ("nfacets", nf)):
         host[k] = np.ascontiguousarray(v.cpu().numpy()[idx])
-    st, xi, vrp, it = oracle.dcm_mpc_solve_batch(host, threads=8)
+    st, xi, vrp, it = oracle.dcm_mpc_solve_batch(host, threads=8, device_batch=B)   # B-QP launch
     np.testing.assert_array_equal(out["xi"].cpu().numpy()[idx], xi)
     np.testing.assert_array_equal(out["vrp"].cpu().numpy()[idx], vrp)
     np.testing.assert_array_equal(out["iters"].cpu().numpy()[idx], it)

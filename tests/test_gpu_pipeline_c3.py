@@ -102,7 +102,7 @@ def test_c3_subset_bitwise_vs_oracle(c3, oracle):
     w = oracle.dcm_phase_expand_batch(otab, 0, prob["dt"], N, threads=8)
     w.update(xi_init=np.ascontiguousarray(prob["xi_init"][idx]),
              omega=np.ascontiguousarray(prob["omega"][idx]))
-    st, xi, vrp, iters = oracle.dcm_mpc_solve_batch(w, threads=8)
+    st, xi, vrp, iters = oracle.dcm_mpc_solve_batch(w, threads=8, device_batch=B)   # B-QP launch
     np.testing.assert_array_equal(qp["status"][it].cpu().numpy(), st)
     np.testing.assert_array_equal(qp["iters"][it].cpu().numpy(), iters)
     np.testing.assert_array_equal(qp["xi"][it].cpu().numpy(), xi)

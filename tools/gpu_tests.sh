@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest ${PYTEST_ARGS:-tests -m gpu -q -x} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest ${PYTEST_ARGS:-tests -m gpu -q -x} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -40 gpurun_out/pytest_gpu.log
 exit $rc
