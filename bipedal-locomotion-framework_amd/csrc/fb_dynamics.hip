@@ -74,8 +74,8 @@ __device__ __forceinline__ void wave_sync()
 #ifndef BLF_FBD_PAD
 #define BLF_FBD_PAD 1
 #endif
-#ifndef BLF_FBD_CHOL2
-#define BLF_FBD_CHOL2 1
+#ifndef BLF_FBD_CHOLB
+#define BLF_FBD_CHOLB 2
 #endif
 
 constexpr int kPad = BLF_FBD_PAD;
@@ -111,9 +111,9 @@ struct Smem {
         o_jz = take(3 * (size_t)n);
         o_jo = take(3 * (size_t)n);
         // subtree sums [j] (joint j's subtree) and [n] (every link); later the pivot-column
-        // buffers of the factorization (two pairs of columns, 4 NV)
+        // buffers of the factorization (two sets of up to 4 columns, 8 NV)
         const size_t cp = (size_t)kCompS * (n + 1);
-        o_comp = take(cp > 4 * (size_t)NV ? cp : 4 * (size_t)NV);
+        o_comp = take(cp > 8 * (size_t)NV ? cp : 8 * (size_t)NV);
         o_sax = take(kSax * (size_t)NV);
         o_rhs = take((size_t)NV);
         o_cscr = take((size_t)kCs * (C > 0 ? C : 1));
@@ -556,48 +556,66 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             if (j < NV && j <= lane) r[j] = r[j] + reg[NV * lane + j];
     FSTAMP_ADD(6, f_t6);
     FSTAMP(f_t7);
-    // 8. Cholesky M = L L^T, right-looking, lane i keeps row i in registers, two columns per step
-    //    (BLF_FBD_CHOL2; 1: one column per step): every lane factors the step's 2 x 2 diagonal
-    //    block from three broadcasts, scales its own two entries, and the two columns of the rows
-    //    below go through one LDS buffer pair (two pairs, alternating) and are read back as
-    //    broadcasts -- one LDS round trip per two pivots, where the dependent chain of pivot,
-    //    column store and read-back is the Cholesky's time at one wavefront per SIMD
+    // 8. Cholesky M = L L^T, right-looking, lane i keeps row i in registers, CB columns per step
+    //    (BLF_FBD_CHOLB; 1: one column per step): every lane factors the step's CB x CB diagonal
+    //    block from its broadcast entries (rows past the matrix: identity), computes its own CB
+    //    entries by the same forward substitution (so a lane inside the block reproduces the
+    //    block's row bit for bit), and the CB columns of the rows below go through one LDS buffer
+    //    set (two sets, alternating) and are read back as broadcasts: one LDS round trip per CB
+    //    pivots, where the dependent chain of pivot, column store and read-back is the
+    //    Cholesky's time at one wavefront per SIMD
     bool ok = true;
-#if BLF_FBD_CHOL2
+#if BLF_FBD_CHOLB > 1
+    // the block must divide the register row (NVMAX = 54 for the largest model: 2)
+    constexpr int CB = NVMAX % BLF_FBD_CHOLB == 0 ? BLF_FBD_CHOLB : 2;
+    static_assert(NVMAX % CB == 0, "block size divides the register row");
 #pragma unroll
-    for (int k = 0; k < NVMAX; k += 2) {
+    for (int k = 0; k < NVMAX; k += CB) {
         if (k < NV) {
-            const bool two = k + 1 < NV;
-            const int k1 = k + 1 < NVMAX ? k + 1 : k;   // compile-time clamp (r[k1] unused when !two)
-            const double a = H.bcast_k(r[k], k);
-            const double b = two ? H.bcast_k(r[k], k1) : 0.0;
-            const double c = two ? H.bcast_k(r[k1], k1) : 1.0;
-            ok = ok && (a > 0.0);
-            // 1 / sqrt: v_rsq_f64 and one Newton step (parity with the oracle is at 1e-9)
-            double ia = __builtin_amdgcn_rsq(a);
-            ia = ia * (1.5 - (0.5 * a) * (ia * ia));
-            const double l10 = b * ia;                       // L_{k+1,k}
-            const double d = c - l10 * l10;                  // the second pivot
-            ok = ok && (d > 0.0);
-            double id = __builtin_amdgcn_rsq(d);
-            id = id * (1.5 - (0.5 * d) * (id * id));
-            const double lik = r[k] * ia;                    // L_{i,k} of this lane's row
-            const double lik1 = (r[k1] - lik * l10) * id;    // L_{i,k+1}
-            r[k] = lane == k ? a * ia : (lane > k ? lik : r[k]);
-            if (two) r[k1] = lane == k1 ? d * id : (lane > k1 ? lik1 : r[k1]);
-            const double rk1 = two ? r[k1] : 0.0;
-            double* col = S.comp() + ((k >> 1) & 1) * 2 * NV;
-            if (lane < NV) {
-                col[lane] = r[k];
-                col[NV + lane] = rk1;
+            double Lb[CB][CB], il[CB];
+#pragma unroll
+            for (int i = 0; i < CB; ++i) {
+                const bool in = k + i < NV;
+#pragma unroll
+                for (int j = 0; j < i; ++j) {
+                    double t = in ? H.bcast_k(r[k + j], k + i) : 0.0;   // M_{k+i,k+j}
+#pragma unroll
+                    for (int c = 0; c < j; ++c) t = t - Lb[i][c] * Lb[j][c];
+                    Lb[i][j] = t * il[j];
+                }
+                double d = in ? H.bcast_k(r[k + i], k + i) : 1.0;       // M_{k+i,k+i}
+#pragma unroll
+                for (int c = 0; c < i; ++c) d = d - Lb[i][c] * Lb[i][c];
+                ok = ok && (d > 0.0);
+                // 1 / sqrt: v_rsq_f64 and one Newton step (parity with the oracle is at 1e-9)
+                double q = __builtin_amdgcn_rsq(d);
+                il[i] = q * (1.5 - (0.5 * d) * (q * q));
+                Lb[i][i] = d * il[i];
+            }
+            // this lane's entries L_{lane,k..k+CB-1} (upper-triangle junk inside the block, unread)
+            double li[CB];
+#pragma unroll
+            for (int i = 0; i < CB; ++i) {
+                double t = r[k + i];
+#pragma unroll
+                for (int c = 0; c < i; ++c) t = t - li[c] * Lb[i][c];
+                li[i] = t * il[i];
+            }
+            double* col = S.comp() + ((k / CB) & 1) * CB * NV;
+#pragma unroll
+            for (int i = 0; i < CB; ++i) {
+                r[k + i] = lane >= k ? li[i] : r[k + i];
+                if (lane < NV) col[i * NV + lane] = r[k + i];
             }
             wave_sync();
             // no row predicate (as below): lanes above row j update only upper-triangle entries
 #pragma unroll
-            for (int j = k + 2; j < NVMAX; ++j) {
+            for (int j = k + CB; j < NVMAX; ++j) {
                 const int jj = j < NV ? j : NV - 1;
-                const double l0 = col[jj], l1 = col[NV + jj];
-                r[j] = fma(-r[k], l0, fma(-rk1, l1, r[j]));
+                double t = r[j];
+#pragma unroll
+                for (int i = CB - 1; i >= 0; --i) t = fma(-r[k + i], col[i * NV + jj], t);
+                r[j] = t;
             }
         }
     }
@@ -633,7 +651,9 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     FSTAMP_ADD(7, f_t7);
     FSTAMP(f_t8);
     // 9. L z = y with the rows in registers, then L^T x = z with row k of L read from LDS (the
-    //    link records are dead by now); lane k scales its own entry, one broadcast per step
+    //    link records are dead by now); lane k scales its own entry, one broadcast per step.  Two
+    //    unknowns per step (the 2 x 2 block solved by every lane, as in the factorization) measured
+    //    the same: 6.054 / 6.069 against 6.081 / 6.073 ms per c5 period of the Euler kernel
     const double idg = lane < NV ? 1.0 / bcast_own_diag<NVMAX>(r, lane) : 0.0;
 #pragma unroll
     for (int k = 0; k < NVMAX; ++k) {   // k >= NV changes only lanes past the matrix

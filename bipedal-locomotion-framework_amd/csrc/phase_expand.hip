@@ -30,6 +30,14 @@ __host__ __device__ inline size_t expand_lds_bytes(int P, int M, int N)
     return sizeof(double) * ((size_t)P * (3 * M + 4)) + sizeof(int32_t) * ((size_t)P + N + 1);
 }
 
+// The window is read straight back by the QP kernel.  A window set that fits the 256 MB
+// Infinity Cache is stored plainly, so the solve reads it from there; a larger one streams past
+// it non-temporally (measured on one box, two rounds: 4096 windows, 97 MB, plain stores 0.104 /
+// 0.105 ms per expand + solve step against 0.108 / 0.109 ms non-temporal; 65 536 windows, 1.5 GB,
+// non-temporal 2.07 ms per pipeline step against 2.19 ms plain; profiles/r03_expand_nt_ab.log).
+constexpr size_t kExpandNtBytes = (size_t)128 << 20;
+
+template <bool NT>
 __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
     int32_t P, const int32_t* __restrict__ nphases, const double* __restrict__ pbegin,
     const double* __restrict__ pend, const double* __restrict__ pA, const double* __restrict__ pb,
@@ -78,8 +86,8 @@ __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
     for (int j = tid; j < nm; j += kExpandBlock) {
         const int k = pow2 ? j >> sh : j / M, i = j - k * M;
         const int ph = sPh[k];
-        st_stream(oA + j, ph >= 0 ? sA[ph * M + i] : make_double2(0.0, 0.0));
-        __builtin_nontemporal_store(ph >= 0 ? sB[ph * M + i] : 0.0, oB + j);
+        st_out<NT>(oA + j, ph >= 0 ? sA[ph * M + i] : make_double2(0.0, 0.0));
+        st_out<NT>(oB + j, ph >= 0 ? sB[ph * M + i] : 0.0);
     }
     double2* oX = reinterpret_cast<double2*>(xi_ref) + q * (N + 1);
     double2* oR = reinterpret_cast<double2*>(vrp_ref) + q * N;
@@ -87,10 +95,10 @@ __global__ __launch_bounds__(kExpandBlock) void phase_expand_kernel(
     for (int k = tid; k <= N; k += kExpandBlock) {
         const int ph = sPh[k];
         const double2 ref = ph >= 0 ? sRef[ph] : make_double2(0.0, 0.0);
-        st_stream(oX + k, ref);
+        st_out<NT>(oX + k, ref);
         if (k < N) {
-            st_stream(oR + k, ref);
-            __builtin_nontemporal_store(ph >= 0 ? sNf[ph] : -1, oN + k);
+            st_out<NT>(oR + k, ref);
+            st_out<NT>(oN + k, ph >= 0 ? sNf[ph] : -1);
         }
     }
 }
@@ -113,7 +121,9 @@ blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* 
         return set_error(BLF_ERR_UNSUPPORTED,
                          "%d phases and a horizon of %d need %zu B of LDS (64 KiB at most)", P, N,
                          lds);
-    hipLaunchKernelGGL(phase_expand_kernel, dim3((unsigned)batch), dim3(kExpandBlock), lds, s, P,
+    const size_t out_bytes = (size_t)batch * ((size_t)N * M * 24 + (size_t)N * 20 + (size_t)(N + 1) * 16);
+    auto kern = out_bytes > kExpandNtBytes ? phase_expand_kernel<true> : phase_expand_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kExpandBlock), lds, s, P,
                        nphases, begin, end, pA, pb, pnf, pref, M, start_knot, dt, N, A, b,
                        nfacets, xi_ref, vrp_ref);
     return check_hip(hipGetLastError(), "phase_expand_kernel launch");

@@ -27,8 +27,11 @@ constexpr int kHullBlock = 64;
 // eight facets of a polygon that phase 2 reads in one lane group hit distinct banks (a stride of
 // 64 put all eight on one bank: 8-way), and the Y array's 2-double offset interleaves the
 // staging stores of X and Y (16-way on one bank pair before: 13 % of the wave's cycles).
-constexpr int kHullStride = 68;
-constexpr int kHullYOff = 2;
+#ifndef BLF_HULL_PAD
+#define BLF_HULL_PAD 1
+#endif
+constexpr int kHullStride = BLF_HULL_PAD ? 68 : 64;   // BLF_HULL_PAD=0: the unpadded layout (A/B)
+constexpr int kHullYOff = BLF_HULL_PAD ? 2 : 0;
 #ifndef BLF_HULL_U
 #define BLF_HULL_U 8
 #endif

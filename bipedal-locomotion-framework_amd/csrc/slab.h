@@ -39,6 +39,33 @@ __device__ __forceinline__ void st_stream(double2* p, double2 v)
 #endif
 }
 
+// The same for 8-B / 4-B streamed outputs (phase expansion's offsets and facet counts).
+__device__ __forceinline__ void st_stream(double* p, double v)
+{
+#if BLF_NT_STORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
+__device__ __forceinline__ void st_stream(int32_t* p, int32_t v)
+{
+#if BLF_NT_STORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
+// A streamed output stored non-temporally (NT) or plainly, chosen per launch by the output's size.
+template <bool NT, class T>
+__device__ __forceinline__ void st_out(T* p, T v)
+{
+    if constexpr (NT) st_stream(p, v);
+    else *p = v;
+}
+
 // Element e of a slab with W columns is row e / W.  (e + 0.5) / W lies at least 0.5 / W from an
 // integer; in float the product's error is below 2^-22 * rows, so the row is exact for
 // rows * W < 2^20 and W < 2^10 (all slabs here: rows <= 256, W <= 64).

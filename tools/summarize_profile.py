@@ -56,10 +56,10 @@ def resources():
                    "Occupancy [waves/SIMD]": "occupancy_waves_per_simd",
                    "LDS Size [bytes/block]": "static_lds_bytes"}.get(m.group(1), m.group(1).lower())
             res[cur][key] = int(m.group(2))
-    # the instances the bench runs: cold <KPL 2, no lambda out, per-knot input, PAD> (c2) and warm
-    # <KPL 2, lambda out, phase-indexed input, PAD> (rh)
-    keep = {k: v for k, v in res.items() if "dcm_mpc_cold_kernelILi2ELb0ELb0ELb1E" in k
-            or "dcm_mpc_warm_kernelILi2ELb1ELb1ELb1E" in k}
+    # the instances the bench runs: cold <KPL 2, no lambda out, per-knot input, kTreePad> (c2) and
+    # warm <KPL 2, lambda out, phase-indexed input, kTreePad> (rh)
+    keep = {k: v for k, v in res.items() if "dcm_mpc_cold_kernelILi2ELb0ELb0ELi1E" in k
+            or "dcm_mpc_warm_kernelILi2ELb1ELb1ELi1E" in k}
     return {("dcm_mpc_cold_kernel<2> (c2)" if "cold" in k else "dcm_mpc_warm_kernel<2> (rh)"): v
             for k, v in keep.items()}
 
