@@ -1,6 +1,7 @@
 // euler_rollout.hip — ForwardEuler<LinearTimeInvariantSystem> on the device.
 //
 //  * lti_euler_kernel: FixedStepIntegrator::integrate(t0, T) for a batch of small LTI systems
+//    (n, m <= 8; lti_euler_wg_kernel up to BLF_LTI_MAX_DIM)
 //    (reference: src/System/include/BipedalLocomotion/System/FixedStepIntegrator.tpp:21-72,
 //    ForwardEuler.tpp:18-49, src/System/src/LinearTimeInvariantSystem.cpp:71).  The step
 //    schedule (count and the stale-time last step) is computed once on the host (blf_capi.hip)
@@ -69,6 +70,58 @@ __global__ __launch_bounds__(256) void lti_euler_kernel(int n, int m, const doub
 #pragma unroll
     for (int r = 0; r < kNmax; ++r)
         if (r < n) x[q * n + r] = xr[r];
+}
+
+// Systems with n or m above kNmax (up to BLF_LTI_MAX_DIM): one 64-lane workgroup per system, x and
+// B u in LDS, thread t owning rows t, t + 64, ...; each row's sums run left to right exactly as in
+// lti_euler_kernel and the oracle, so the results are the same bits.  A and B are read from
+// global memory (L2; one copy for every system when shared).
+constexpr int kLtiRowsPerLane = (BLF_LTI_MAX_DIM + 63) / 64;
+
+__global__ __launch_bounds__(64) void lti_euler_wg_kernel(int n, int m, const double* __restrict__ A,
+                                                          const double* __restrict__ Bm, int shared,
+                                                          const double* __restrict__ u,
+                                                          double* __restrict__ x, int32_t nsteps,
+                                                          double dT, double dT_last)
+{
+    extern __shared__ double lti_s[];   // x [n], B u [n]
+    const int64_t q = blockIdx.x;
+    const int t = threadIdx.x;
+    const double* Aq = shared ? A : A + q * n * n;
+    const double* Bq = shared ? Bm : Bm + q * n * m;
+    const double* uq = u + q * m;
+    double* xs = lti_s;
+    double* bs = lti_s + n;
+    for (int r = t; r < n; r += 64) {
+        xs[r] = x[q * n + r];
+        double acc = Bq[(int64_t)r * m] * uq[0];
+        for (int c = 1; c < m; ++c) acc = acc + Bq[(int64_t)r * m + c] * uq[c];
+        bs[r] = acc;
+    }
+    __syncthreads();
+    for (int32_t i = 0; i < nsteps; ++i) {
+        const double h = (i == nsteps - 1) ? dT_last : dT;
+        double dx[kLtiRowsPerLane];
+#pragma unroll
+        for (int j = 0; j < kLtiRowsPerLane; ++j) {
+            const int r = t + 64 * j;
+            dx[j] = 0.0;
+            if (r < n) {
+                const double* Ar = Aq + (int64_t)r * n;
+                double acc = Ar[0] * xs[0];
+                for (int c = 1; c < n; ++c) acc = acc + Ar[c] * xs[c];
+                dx[j] = acc + bs[r];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kLtiRowsPerLane; ++j) {
+            const int r = t + 64 * j;
+            if (r < n) xs[r] = xs[r] + dx[j] * h;
+        }
+        __syncthreads();
+    }
+    for (int r = t; r < n; r += 64) x[q * n + r] = xs[r];
 }
 
 __global__ __launch_bounds__(256) void lti_dynamics_kernel(int n, int m,
@@ -335,6 +388,15 @@ blf_status launch_lti_euler(int n, int m, const double* A, const double* Bm, int
                             double dT, double dT_last, hipStream_t s)
 {
     if (batch == 0) return BLF_OK;
+    if (n > kNmax || m > kNmax) {
+        if (batch > 0x7fffffffLL)
+            return set_error(BLF_ERR_UNSUPPORTED, "lti_euler: %lld systems of size %d too many",
+                             (long long)batch, n);
+        hipLaunchKernelGGL(lti_euler_wg_kernel, dim3((unsigned)batch), dim3(64),
+                           2 * sizeof(double) * (size_t)n, s, n, m, A, Bm, shared, u, x, nsteps, dT,
+                           dT_last);
+        return check_hip(hipGetLastError(), "lti_euler_wg_kernel launch");
+    }
     const int64_t blocks = ceil_div(batch, 256);
     hipLaunchKernelGGL(lti_euler_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, m, A, Bm,
                        shared, u, x, batch, nsteps, dT, dT_last);

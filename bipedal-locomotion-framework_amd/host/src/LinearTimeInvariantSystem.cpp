@@ -25,10 +25,10 @@ bool LinearTimeInvariantSystem::setSystemMatrices(const blf::MatrixXd& A, const 
                   << std::endl;
         return false;
     }
-    if (A.rows() < 1 || A.rows() > 8 || B.cols() < 1 || B.cols() > 8)
+    if (A.rows() < 1 || A.rows() > BLF_LTI_MAX_DIM || B.cols() < 1 || B.cols() > BLF_LTI_MAX_DIM)
     {
         std::cerr << "[LinearTimeInvariantSystem::setSystemMatrices] The device integrator "
-                     "supports 1 <= n, m <= 8."
+                     "supports 1 <= n, m <= " << BLF_LTI_MAX_DIM << "."
                   << std::endl;
         return false;
     }

@@ -14,11 +14,13 @@
 /* ------------------------------------------------------------------------------------------ */
 /* ForwardEuler<LinearTimeInvariantSystem>::integrate — FixedStepIntegrator.tpp:21-72          */
 /* ------------------------------------------------------------------------------------------ */
+#define ORC_LTI_MAX_DIM 512   /* BLF_LTI_MAX_DIM */
+
 static void lti_step(int n, int m, const double* A, const double* B, const double* u, double* x,
                      double dT)
 {
     /* LinearTimeInvariantSystem.cpp:71  dx = A x + B u ;  ForwardEuler.tpp:36-38  x += dx*dT */
-    double dx[8];
+    double dx[ORC_LTI_MAX_DIM];
     for (int r = 0; r < n; ++r) {
         double ax = A[r * n + 0] * x[0];
         for (int c = 1; c < n; ++c) ax = ax + A[r * n + c] * x[c];
@@ -32,7 +34,7 @@ static void lti_step(int n, int m, const double* A, const double* B, const doubl
 int orc_lti_euler_integrate(int n, int m, const double* A, const double* B, const double* u,
                             double* x, double t0, double t1, double dT, int64_t* nsteps_out)
 {
-    if (n < 1 || n > 8 || m < 1 || m > 8) return 1;
+    if (n < 1 || n > ORC_LTI_MAX_DIM || m < 1 || m > ORC_LTI_MAX_DIM) return 1;
     if (t0 > t1 || !(dT > 0)) return 4;           /* FixedStepIntegrator.tpp:28-46            */
     if (t0 == t1) return 5;                       /* reference: size_t(i) < -1 -> never ends   */
     double q = ceil((t1 - t0) / dT);

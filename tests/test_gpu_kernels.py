@@ -60,6 +60,40 @@ def test_lti_integrator_step_schedule(handle, oracle, t0, t1, dT):
         np.testing.assert_array_equal(xg[i], xo)
 
 
+@pytest.mark.parametrize("n,m,shared", [(9, 3, False), (12, 8, True), (40, 17, False), (130, 1, True),
+                                        (5, 20, False)])
+def test_lti_integrator_large_systems(handle, oracle, n, m, shared):
+    """n or m above 8: one workgroup per system (lti_euler_wg_kernel), bit-identical to the
+    oracle's step (the same left-to-right sums), per-system and shared matrices."""
+    rng = np.random.default_rng(n * 100 + m)
+    B = 37
+    A = rng.uniform(-1, 1, (n, n) if shared else (B, n, n)) / n
+    Bm = rng.uniform(-1, 1, (n, m) if shared else (B, n, m))
+    u = rng.uniform(-1, 1, (B, m))
+    x0 = rng.uniform(-1, 1, (B, n))
+    x = _d(x0)
+    handle.lti_euler_integrate(_d(A), _d(Bm), _d(u), x, 0.0, 0.093, 0.01, shared=shared)
+    xg = x.cpu().numpy()
+    for i in range(B):
+        st, xo, steps = oracle.lti_euler_integrate(A if shared else A[i], Bm if shared else Bm[i], u[i],
+                                                   x0[i], 0.0, 0.093, 0.01)
+        assert st == 0 and steps == 10
+        np.testing.assert_array_equal(xg[i], xo)
+    dx = handle.lti_dynamics(_d(A), _d(Bm), _d(u), _d(x0), shared=shared).cpu().numpy()
+    for i in range(0, B, 6):
+        Ai, Bi = (A, Bm) if shared else (A[i], Bm[i])
+        np.testing.assert_allclose(dx[i], Ai @ x0[i] + Bi @ u[i], rtol=1e-12, atol=1e-12)
+
+
+def test_lti_integrator_size_limit(handle):
+    n = 513
+    x = _d(np.zeros((1, n)))
+    with pytest.raises(native.BlfError) as e:
+        handle.lti_euler_integrate(_d(np.eye(n)), _d(np.ones((n, 1))), _d(np.ones((1, 1))), x, 0.0, 1.0,
+                                   0.1, shared=True)
+    assert e.value.code == 1
+
+
 def test_lti_integrator_errors(handle):
     A = _d(np.eye(2)); B = _d(np.ones((2, 1))); u = _d(np.ones((1, 1))); x = _d(np.zeros((1, 2)))
     with pytest.raises(native.BlfError) as e:

@@ -48,6 +48,24 @@ def test_integrator_step_schedule_quirks():
     assert O.lti_euler_integrate(ramp["A"], ramp["B"], ramp["u"], [0.0], 1.0, 1.0, 0.1)[0] == 5
 
 
+def test_integrator_lti_large_system_is_euler():
+    """n, m above 8 (up to BLF_LTI_MAX_DIM = 512): the same step, pinned against a plain numpy
+    Euler loop of the reference's schedule (to rounding) and the size limit."""
+    rng = np.random.default_rng(5)
+    n, m = 40, 7
+    A = rng.uniform(-1, 1, (n, n)) / n
+    B = rng.uniform(-1, 1, (n, m))
+    u = rng.uniform(-1, 1, m)
+    x0 = rng.uniform(-1, 1, n)
+    st, x, steps = O.lti_euler_integrate(A, B, u, x0, 0.0, 0.093, 0.01)
+    assert st == 0 and steps == 10
+    xr = x0.copy()
+    for h in [0.01] * 9 + [0.093 - 0.08]:   # the stale last step of FixedStepIntegrator.tpp:63-70
+        xr = xr + (A @ xr + B @ u) * h
+    np.testing.assert_allclose(x, xr, rtol=1e-12, atol=1e-13)
+    assert O.lti_euler_integrate(np.eye(513), np.ones((513, 1)), [1.0], np.zeros(513), 0.0, 1.0, 0.1)[0] == 1
+
+
 def test_dcm_rollout_is_the_lti_step():
     rng = np.random.default_rng(0)
     N = 40
