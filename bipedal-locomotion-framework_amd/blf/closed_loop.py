@@ -135,3 +135,22 @@ class ClosedLoop:
         self.prev = out
         self.s = s + 1
         return out
+
+
+def split_groups(h, model, plan, states, groups, horizon=100, **kw):
+    """The robots of (plan, states) in `groups` contiguous groups, each a ClosedLoop on its own
+    stream (one group: the current stream).  Every robot's periods are the same computation as in
+    one ClosedLoop over all robots; the groups' kernels overlap on the device (the plan kernels'
+    tails, a few QPs on an otherwise idle chip, run beside another group's dynamics)."""
+    import torch
+    B = plan["omega"].shape[0]
+    groups = max(1, min(int(groups), B))
+    cut = [B * g // groups for g in range(groups + 1)]
+    shared = ("knot_phase", "dt", "schedule")   # per-knot / scalar entries of the plan dict
+    sl = lambda d, lo, hi: {k: (v if k in shared else v[lo:hi]) for k, v in d.items()}
+    loops = []
+    for g in range(groups):
+        stream = torch.cuda.Stream(device=h.device) if groups > 1 else None
+        loops.append(ClosedLoop(h, model, sl(plan, cut[g], cut[g + 1]), sl(states, cut[g], cut[g + 1]),
+                                horizon=horizon, stream=stream, **kw))
+    return loops

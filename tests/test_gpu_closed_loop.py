@@ -159,6 +159,27 @@ def test_closed_loop_vs_oracle(handle):
     assert np.abs(loop.q_ref.cpu().numpy()).max() > 0.0
 
 
+def test_closed_loop_stream_groups_bitwise(handle):
+    """The bench's c5 scheduling (bench.py --c5-groups): the robots in three groups, each closed
+    loop on its own stream, run the same computation as one loop over all robots, bit for bit
+    (the QP, the maps and the dynamics are per robot; the groups only overlap on the device)."""
+    B, S = 96, 3
+    plan, st = _setup(B, S)
+    one = DL.ClosedLoop(handle, MODEL, plan, st)
+    groups = DL.split_groups(handle, MODEL, plan, st, 3)
+    assert [lp.B for lp in groups] == [32, 32, 32]
+    for s in range(S):
+        out1 = one.period()
+        outs = [lp.period() for lp in groups]
+    torch.cuda.synchronize()
+    for k in ("xi", "vrp", "status", "iters"):
+        np.testing.assert_array_equal(out1[k].cpu().numpy(),
+                                      torch.cat([o[k] for o in outs]).cpu().numpy(), err_msg=k)
+    for k in native.FB_STATE_KEYS:
+        np.testing.assert_array_equal(one.state[k].cpu().numpy(),
+                                      torch.cat([lp.state[k] for lp in groups]).cpu().numpy(), err_msg=k)
+
+
 def test_closed_loop_config5_full_size(handle):
     """configs[4] at its size on one GPU: 16 384 robots, three coupled periods; finite states,
     every plan solved, xi_init = the robot's DCM."""
