@@ -1158,6 +1158,9 @@ __device__ __forceinline__ void cold_solve(
     // The facet rows' loads are issued first and land in LDS only after the float LQ step, which
     // does not read them: the step's arithmetic runs under the loads' latency (at launch every
     // wave of the first round stages its rows at once).
+    // (The phase-indexed input keeps its gathers before the LQ step: issued after the knot loads
+    // and committed after the step like the slab loads, it measured 1 % slower on the c3 pipeline,
+    // 1.900 / 1.893 against 1.882 / 1.874 ms per step, profiles/r03_ph_overlap_ab.log.)
     constexpr bool kOverlap = !PH && BLF_AS_OVERLAP && !BLF_AS_EXPA;
     double2 va[U];
     double vb[U];
