@@ -19,7 +19,7 @@ STATUS_NAMES = {0: "BLF_OK", 1: "BLF_ERR_INVALID_ARGUMENT", 2: "BLF_ERR_HIP",
 QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 
 # every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
-EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version",
+EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_step_schedule",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_hull3d_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
             "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_solve_warm",

@@ -96,6 +96,20 @@ blf_status blf_destroy(blf_handle* handle)
 
 const char* blf_last_error(void) { return g_err; }
 
+blf_status blf_step_schedule(double initial_time, double final_time, double dT, int32_t* iterations,
+                             double* dT_last, double* t_last)
+{
+    BLF_REQUIRE(iterations && dT_last && t_last, "blf_step_schedule: null output");
+    int it = 0;
+    double last = 0.0;
+    const blf_status st = step_schedule(initial_time, final_time, dT, &it, &last);
+    if (st != BLF_OK) return st;
+    *iterations = it;
+    *dT_last = last;
+    *t_last = it >= 2 ? initial_time + dT * (double)(it - 2) : initial_time;   // :53, as step_schedule
+    return BLF_OK;
+}
+
 #ifndef BLF_SRC_HASH
 #define BLF_SRC_HASH "unknown"
 #endif

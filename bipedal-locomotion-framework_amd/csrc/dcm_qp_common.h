@@ -250,6 +250,15 @@ struct RcT {
 };
 using Rc = RcT<double>;
 
+// BLF_RC_FORM selects where the reciprocal of det(I + G H) enters (the oracle's ORC_RC_FORM must
+// match):  0: T^{-1} = adj(T) / det first (the reciprocal heads the chain of products);
+// 1: rc_apply deferred only; 2: rc_apply deferred, rc_combine scales U = adj(T) A_e and the G
+// block at the end; 3: both scale their outputs at the end, so the products of adj(T) run
+// beside the division (the division no longer heads the dependent chain).
+#ifndef BLF_RC_FORM
+#define BLF_RC_FORM 2
+#endif
+
 template <class T>
 __device__ __forceinline__ bool rc_combine(RcT<T>& e, const RcT<T>& q)
 {
@@ -261,6 +270,52 @@ __device__ __forceinline__ bool rc_combine(RcT<T>& e, const RcT<T>& q)
     const T detT = fma(T00, T11, -(T01 * T10));
     const bool ok = (detT > T(0)) && !__builtin_isinf(detT);
     const T it = one / detT;
+    if constexpr (BLF_RC_FORM >= 2) {
+        // adj(T) = [T11, -T01; -T10, T00]; U' = adj(T) A_e, V' = A_q adj(T), X' = V' G_e
+        const T Up00 = FD2(T11, e.a0, -T01, e.a2);
+        const T Up01 = FD2(T11, e.a1, -T01, e.a3);
+        const T Up10 = FD2(-T10, e.a0, T00, e.a2);
+        const T Up11 = FD2(-T10, e.a1, T00, e.a3);
+        const T Vp00 = FD2(q.a0, T11, q.a1, -T10);
+        const T Vp01 = FD2(q.a0, -T01, q.a1, T00);
+        const T Vp10 = FD2(q.a2, T11, q.a3, -T10);
+        const T Vp11 = FD2(q.a2, -T01, q.a3, T00);
+        const T Xp00 = FD2(Vp00, e.g0, Vp01, e.g1);
+        const T Xp01 = FD2(Vp00, e.g1, Vp01, e.g2);
+        const T Xp10 = FD2(Vp10, e.g0, Vp11, e.g1);
+        const T Xp11 = FD2(Vp10, e.g1, Vp11, e.g2);
+        const T Y00 = FD2(q.h0, e.a0, q.h1, e.a2);
+        const T Y01 = FD2(q.h0, e.a1, q.h1, e.a3);
+        const T Y10 = FD2(q.h1, e.a0, q.h2, e.a2);
+        const T Y11 = FD2(q.h1, e.a1, q.h2, e.a3);
+        const T gp0 = FD2(Xp00, q.a0, Xp01, q.a1);
+        const T gp1 = FD2(Xp00, q.a2, Xp01, q.a3);
+        const T gp2 = FD2(Xp10, q.a2, Xp11, q.a3);
+        RcT<T> r;
+        if constexpr (BLF_RC_FORM == 2) {
+            const T U00 = Up00 * it, U01 = Up01 * it, U10 = Up10 * it, U11 = Up11 * it;
+            r.a0 = FD2(q.a0, U00, q.a1, U10);
+            r.a1 = FD2(q.a0, U01, q.a1, U11);
+            r.a2 = FD2(q.a2, U00, q.a3, U10);
+            r.a3 = FD2(q.a2, U01, q.a3, U11);
+            r.h0 = FD3(U00, Y00, U10, Y10, e.h0);
+            r.h1 = FD3(U00, Y01, U10, Y11, e.h1);
+            r.h2 = FD3(U01, Y01, U11, Y11, e.h2);
+        } else {
+            r.a0 = FD2(q.a0, Up00, q.a1, Up10) * it;
+            r.a1 = FD2(q.a0, Up01, q.a1, Up11) * it;
+            r.a2 = FD2(q.a2, Up00, q.a3, Up10) * it;
+            r.a3 = FD2(q.a2, Up01, q.a3, Up11) * it;
+            r.h0 = fma(FD2(Up00, Y00, Up10, Y10), it, e.h0);
+            r.h1 = fma(FD2(Up00, Y01, Up10, Y11), it, e.h1);
+            r.h2 = fma(FD2(Up01, Y01, Up11, Y11), it, e.h2);
+        }
+        r.g0 = fma(gp0, it, q.g0);
+        r.g1 = fma(gp1, it, q.g1);
+        r.g2 = fma(gp2, it, q.g2);
+        e = r;
+        return ok;
+    }
     const T Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
     const T U00 = FD2(Ti00, e.a0, Ti01, e.a2);
     const T U01 = FD2(Ti00, e.a1, Ti01, e.a3);
@@ -304,6 +359,21 @@ __device__ __forceinline__ bool rc_apply(const RcT<T>& e, T P00, T P01, T P11, T
     const T detS = fma(S00, S11, -(S01 * S10));
     const bool ok = (detS > T(0)) && !__builtin_isinf(detS);
     const T is = one / detS;
+    if constexpr (BLF_RC_FORM >= 1) {
+        // W' = P adj(S), Z' = W' A, out = (A^T Z') / det(S) + H
+        const T Wp00 = FD2(P00, S11, P01, -S10);
+        const T Wp01 = FD2(P00, -S01, P01, S00);
+        const T Wp10 = FD2(P01, S11, P11, -S10);
+        const T Wp11 = FD2(P01, -S01, P11, S00);
+        const T Zp00 = FD2(Wp00, e.a0, Wp01, e.a2);
+        const T Zp01 = FD2(Wp00, e.a1, Wp01, e.a3);
+        const T Zp10 = FD2(Wp10, e.a0, Wp11, e.a2);
+        const T Zp11 = FD2(Wp10, e.a1, Wp11, e.a3);
+        o00 = fma(FD2(e.a0, Zp00, e.a2, Zp10), is, e.h0);
+        o01 = fma(FD2(e.a0, Zp01, e.a2, Zp11), is, e.h1);
+        o11 = fma(FD2(e.a1, Zp01, e.a3, Zp11), is, e.h2);
+        return ok;
+    }
     const T Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
     const T W00 = FD2(P00, Si00, P01, Si10);
     const T W01 = FD2(P00, Si01, P01, Si11);

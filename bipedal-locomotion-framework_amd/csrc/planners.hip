@@ -5,8 +5,10 @@
 //    src/Planners/src/ConvexHullHelper.cpp:35-99).  The workgroup's contiguous slab of input
 //    points is loaded coalesced and transposed into lane-minor LDS arrays; each lane then sorts
 //    its points in place (a sorting network for p <= 8 finite points, else insertion sort) and
-//    runs Andrew's monotone chain with a `cross <= 0` pop (chain stack packed in a register for
-//    P <= 8), which merges collinear boundary points the way Qhull's "Qt" facet merge
+//    chains them: for p <= 8 finite points by the all-triples rule (a point is a lower / upper
+//    chain vertex iff every triple around it turns strictly; branch-free, in registers), else by
+//    Andrew's monotone chain with a `cross <= 0` pop (chain stack packed in a register for
+//    P <= 8).  Both drop collinear boundary points the way Qhull's "Qt" facet merge
 //    does.  The facets are then computed and stored by (polygon, facet) pair, coalesced.  Output rows: unit outward normal,
 //    b = n . v (inside: A x <= b), counter-clockwise from the leftmost-lowest vertex.
 //  * hull2d_contains_kernel: doesPointBelongToConvexHull (ConvexHullHelper.cpp:101-117): strict
@@ -65,10 +67,11 @@ __device__ __forceinline__ int hull2d_rows(int64_t batch, int64_t p0)
     return (int)((batch - p0) < kHullBlock ? (batch - p0) : kHullBlock);
 }
 
-// Phase 1 (lane per polygon): insertion sort of the coordinates by (x, y) with the oracle's
-// comparisons in the oracle's order (a stable sort, identical for any input including NaN), then
-// Andrew's monotone chain with the top two stack points held in registers (LDS is read only on a
-// pop).  Phase 2 (after a barrier): consecutive threads take consecutive (polygon, facet) pairs,
+// Phase 1 (lane per polygon): up to 8 finite points are sorted by a network and chained by the
+// all-triples rule in registers; otherwise an insertion sort of the coordinates by (x, y) with the
+// oracle's comparisons in the oracle's order (a stable sort, identical for any input including
+// NaN), then Andrew's monotone chain with the top two stack points held in registers (LDS is read
+// only on a pop).  Phase 2 (after a barrier): consecutive threads take consecutive (polygon, facet) pairs,
 // compute the facet once and store A as 16-B and b as 8-B coalesced writes.
 template <bool PK>
 __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __restrict__ pts,
@@ -125,10 +128,13 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     if (t < nprob && n >= 3 && n <= P) {
         // Up to 8 points with finite coordinates: a 19-comparator sorting network in registers,
         // branch-free, keyed (x, y, original index) -- for finite keys exactly the permutation of
-        // the stable insertion sort below.  Non-finite coordinates (NaN comparisons) keep the
-        // insertion sort, so every input sorts as the oracle sorts it.
+        // the stable insertion sort below -- and the chain by the all-triples rule (below), also
+        // branch-free and in registers.  Non-finite coordinates (NaN comparisons) or more than 8
+        // points keep the insertion sort and Andrew's chain, so every input sorts and chains as
+        // the oracle does (orc_hull2d_hrep takes the same two paths).
         bool done = false;
-        if (P <= 8) {
+        int nv = 0;
+        if (n <= 8) {
             double x[8], y[8];
             int id[8];
             bool clean = true;
@@ -162,10 +168,71 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                         HX(i) = x[i];
                         HY(i) = y[i];
                     }
+                // The chain without a stack: sorted point j (0 < j < n - 1) is a lower-chain vertex
+                // iff cross3(p_i, p_j, p_k) > 0 for every i < j < k < n, an upper-chain vertex iff
+                // cross3(p_k, p_j, p_i) > 0 for every such pair -- the triples Andrew's pops test,
+                // in the same argument order (in exact arithmetic exactly the chain's vertices:
+                // strictly convex ones, collinear and duplicate points dropped).  56 triples, no
+                // data-dependent loop, no LDS round trip.
+                // Duplicates: Andrew's lower pass keeps the last copy of a repeated point (the first
+                // at the left end), its upper pass the first copy (none at the right end), so a
+                // copy's own duplicates do not reject it there.
+                bool bl[8], bu[8], at0[8], atn[8];
+                double xn = x[0], yn = y[0];
+#pragma unroll
+                for (int s = 1; s < 8; ++s) {
+                    xn = s == n - 1 ? x[s] : xn;
+                    yn = s == n - 1 ? y[s] : yn;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    bl[j] = bu[j] = false;
+                    at0[j] = x[j] == x[0] && y[j] == y[0];
+                    atn[j] = x[j] == xn && y[j] == yn;
+                }
+#pragma unroll
+                for (int k = 2; k < 8; ++k) {
+                    const bool kin = k < n;
+#pragma unroll
+                    for (int j = 1; j < k; ++j) {
+                        const bool ui = !(x[k] == x[j] && y[k] == y[j]) || atn[j];
+#pragma unroll
+                        for (int i = 0; i < j; ++i) {
+                            const bool li = !(x[i] == x[j] && y[i] == y[j]) || at0[j];
+                            const double cl = cross3(x[i], y[i], x[j], y[j], x[k], y[k]);
+                            const double cu = cross3(x[k], y[k], x[j], y[j], x[i], y[i]);
+                            bl[j] = bl[j] || (kin && li && !(cl > 0.0));
+                            bu[j] = bu[j] || (kin && ui && !(cu > 0.0));
+                        }
+                    }
+                }
+                // H: the lower chain left to right (0 and n - 1 always), the upper chain right to
+                // left, then 0 again -- Andrew's stack, 3 bits per entry
+                uint64_t st = 0;
+                int k = 0;
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    if (s < n && (s == 0 || s == n - 1 || !bl[s])) {
+                        st |= (uint64_t)s << (3 * k);
+                        ++k;
+                    }
+#pragma unroll
+                for (int s = 7; s >= 1; --s)
+                    if (s < n - 1 && !bu[s]) {
+                        st |= (uint64_t)s << (3 * k);
+                        ++k;
+                    }
+                ++k;   // the closing 0
+                if (PK) {
+                    stk = st;
+                } else {
+                    for (int i = 0; i < k; ++i) s_stk[i * kHullBlock + t] = (int)((st >> (3 * i)) & 7);
+                }
+                nv = k - 1;
                 done = true;
             }
         }
-        if (!done)
+        if (!done) {
             for (int i = 1; i < n; ++i) {
                 const double vx = HX(i), vy = HY(i);
                 int j = i - 1;
@@ -179,57 +246,58 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
                 HX(j + 1) = vx;
                 HY(j + 1) = vy;
             }
-        // monotone chain; (ax, ay) = STK(k-2), (bx, by) = STK(k-1) when they exist
-        int k = 0;
-        double ax = 0.0, ay = 0.0, bx = 0.0, by = 0.0;
-        for (int i = 0; i < n; ++i) {
-            const double px = HX(i), py = HY(i);
-            while (k >= 2) {
-                if (cross3(ax, ay, bx, by, px, py) <= 0.0) {
-                    --k;
-                    bx = ax;
-                    by = ay;
-                    if (k >= 2) {
-                        const int a = STK_GET(k - 2);
-                        ax = HX(a);
-                        ay = HY(a);
+            // monotone chain; (ax, ay) = STK(k-2), (bx, by) = STK(k-1) when they exist
+            int k = 0;
+            double ax = 0.0, ay = 0.0, bx = 0.0, by = 0.0;
+            for (int i = 0; i < n; ++i) {
+                const double px = HX(i), py = HY(i);
+                while (k >= 2) {
+                    if (cross3(ax, ay, bx, by, px, py) <= 0.0) {
+                        --k;
+                        bx = ax;
+                        by = ay;
+                        if (k >= 2) {
+                            const int a = STK_GET(k - 2);
+                            ax = HX(a);
+                            ay = HY(a);
+                        }
+                    } else {
+                        break;
                     }
-                } else {
-                    break;
                 }
+                STK_SET(k, i);
+                ++k;
+                ax = bx;
+                ay = by;
+                bx = px;
+                by = py;
             }
-            STK_SET(k, i);
-            ++k;
-            ax = bx;
-            ay = by;
-            bx = px;
-            by = py;
-        }
-        const int lower = k + 1;
-        for (int i = n - 2; i >= 0; --i) {
-            const double px = HX(i), py = HY(i);
-            while (k >= lower) {
-                if (cross3(ax, ay, bx, by, px, py) <= 0.0) {
-                    --k;
-                    bx = ax;
-                    by = ay;
-                    if (k >= 2) {
-                        const int a = STK_GET(k - 2);
-                        ax = HX(a);
-                        ay = HY(a);
+            const int lower = k + 1;
+            for (int i = n - 2; i >= 0; --i) {
+                const double px = HX(i), py = HY(i);
+                while (k >= lower) {
+                    if (cross3(ax, ay, bx, by, px, py) <= 0.0) {
+                        --k;
+                        bx = ax;
+                        by = ay;
+                        if (k >= 2) {
+                            const int a = STK_GET(k - 2);
+                            ax = HX(a);
+                            ay = HY(a);
+                        }
+                    } else {
+                        break;
                     }
-                } else {
-                    break;
                 }
+                STK_SET(k, i);
+                ++k;
+                ax = bx;
+                ay = by;
+                bx = px;
+                by = py;
             }
-            STK_SET(k, i);
-            ++k;
-            ax = bx;
-            ay = by;
-            bx = px;
-            by = py;
+            nv = k - 1;
         }
-        const int nv = k - 1;
         if (nv >= 3 && nv <= M) nf = nv;
     }
 #undef HX

@@ -84,6 +84,16 @@ const char* blf_last_error(void);
 /* Version string of the library (build id). */
 const char* blf_version(void);
 
+/* ---- 0. FixedStepIntegrator::integrate's step schedule (FixedStepIntegrator.tpp:21-72) -------
+ * The validation (in the reference's order) and schedule every batched integrator below uses:
+ * iterations = (int)ceil((T - t0) / dT); steps i = 0..iterations-2 run at currentTime = t0 + dT*i
+ * with step dT; the last step runs at the stale currentTime (t0 + dT*(iterations-2), or t0 when
+ * iterations < 2), *t_last, with step *dT_last = T - *t_last.  Errors: BLF_ERR_TIME_INTERVAL
+ * (t0 > T or dT <= 0), BLF_ERR_EMPTY_INTERVAL (t0 == T), BLF_ERR_UNSUPPORTED (>= 2e9 steps).
+ * Host-only; used by include/blf/forward_euler_device.h to integrate user systems. */
+blf_status blf_step_schedule(double initial_time, double final_time, double dT,
+                             int32_t* iterations, double* dT_last, double* t_last);
+
 /* ---- 1. ForwardEuler<LinearTimeInvariantSystem>::integrate(t0, T), batched ------------------
  * x_{i+1} = x_i + (A x_i + B u) * dT_i over the reference's step schedule:
  *   iters = (int)ceil((T - t0) / dT); steps i = 0..iters-2 advance by dT; the final step

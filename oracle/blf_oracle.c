@@ -185,18 +185,50 @@ int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, doub
         }
         idx[j + 1] = v;
     }
-    /* Andrew's monotone chain; cross <= 0 pops collinear and duplicate points */
+    int finite = 1;
+    for (int i = 0; i < 2 * npts; ++i) finite = finite && isfinite(pts[i]);
     int H[34];
     int k = 0;
-    for (int i = 0; i < npts; ++i) {
-        const double* p = pts + 2 * idx[i];
-        while (k >= 2 && cross3(pts + 2 * H[k - 2], pts + 2 * H[k - 1], p) <= 0.0) --k;
-        H[k++] = idx[i];
-    }
-    for (int i = npts - 2, t = k + 1; i >= 0; --i) {
-        const double* p = pts + 2 * idx[i];
-        while (k >= t && cross3(pts + 2 * H[k - 2], pts + 2 * H[k - 1], p) <= 0.0) --k;
-        H[k++] = idx[i];
+    if (npts <= 8 && finite) {
+        /* Up to 8 finite points (the device's register path, hull2d_kernel): sorted point j
+         * (0 < j < n - 1) is a lower-chain vertex iff cross3(p_i, p_j, p_k) > 0 for every
+         * i < j < k < n, an upper-chain vertex iff cross3(p_k, p_j, p_i) > 0 for every such pair:
+         * the triples Andrew's pops test, in the same argument order; in exact arithmetic exactly
+         * the chain's vertices (strictly convex ones; collinear and duplicate points dropped). */
+        int bl[8] = {0}, bu[8] = {0};
+        const double* p0 = pts + 2 * idx[0];
+        const double* pn = pts + 2 * idx[npts - 1];
+        for (int kk = 2; kk < npts; ++kk)
+            for (int j = 1; j < kk; ++j)
+                for (int i = 0; i < j; ++i) {
+                    const double* pi = pts + 2 * idx[i];
+                    const double* pj = pts + 2 * idx[j];
+                    const double* pk = pts + 2 * idx[kk];
+                    /* duplicates: Andrew's lower pass keeps the last copy of a repeated point
+                     * (the first at the left end), its upper pass the first copy (none at the
+                     * right end), so a copy's own duplicates do not reject it there */
+                    const int li = !(pi[0] == pj[0] && pi[1] == pj[1]) || (pj[0] == p0[0] && pj[1] == p0[1]);
+                    const int ui = !(pk[0] == pj[0] && pk[1] == pj[1]) || (pj[0] == pn[0] && pj[1] == pn[1]);
+                    if (li && !(cross3(pi, pj, pk) > 0.0)) bl[j] = 1;
+                    if (ui && !(cross3(pk, pj, pi) > 0.0)) bu[j] = 1;
+                }
+        for (int s = 0; s < npts; ++s)
+            if (s == 0 || s == npts - 1 || !bl[s]) H[k++] = idx[s];
+        for (int s = npts - 2; s >= 1; --s)
+            if (!bu[s]) H[k++] = idx[s];
+        H[k++] = idx[0];
+    } else {
+        /* Andrew's monotone chain; cross <= 0 pops collinear and duplicate points */
+        for (int i = 0; i < npts; ++i) {
+            const double* p = pts + 2 * idx[i];
+            while (k >= 2 && cross3(pts + 2 * H[k - 2], pts + 2 * H[k - 1], p) <= 0.0) --k;
+            H[k++] = idx[i];
+        }
+        for (int i = npts - 2, t = k + 1; i >= 0; --i) {
+            const double* p = pts + 2 * idx[i];
+            while (k >= t && cross3(pts + 2 * H[k - 2], pts + 2 * H[k - 1], p) <= 0.0) --k;
+            H[k++] = idx[i];
+        }
     }
     const int nv = k - 1;  /* last point repeats the first */
     if (nv < 3) return -1;
@@ -882,6 +914,11 @@ static double dcm_residuals(dcm_ws* w, int use_facets)
  * (the structure-preserving doubling composition: only (I + G H)^{-1}, eigenvalues >= 1). */
 typedef struct { double a[4], g[3], h[3]; } rc_el;
 
+/* the kernel's BLF_RC_FORM (dcm_qp_common.h): where 1 / det(I + G H) enters the products */
+#ifndef ORC_RC_FORM
+#define ORC_RC_FORM 2
+#endif
+
 static int rc_combine(rc_el* e1, const rc_el* e2)
 {
     const double* A1 = e1->a; const double* G1 = e1->g; const double* H1 = e1->h;
@@ -893,6 +930,55 @@ static int rc_combine(rc_el* e1, const rc_el* e2)
     const double detT = fma(T00, T11, -(T01 * T10));
     const int ok = (detT > 0.0) && !isinf(detT);
     const double it = 1.0 / detT;
+#if ORC_RC_FORM >= 2
+    {
+        /* adj(T) = [T11, -T01; -T10, T00]: the products run beside the division (rc_combine of
+         * dcm_qp_common.h, BLF_RC_FORM) */
+        const double Up00 = FD2(T11, A1[0], -T01, A1[2]);
+        const double Up01 = FD2(T11, A1[1], -T01, A1[3]);
+        const double Up10 = FD2(-T10, A1[0], T00, A1[2]);
+        const double Up11 = FD2(-T10, A1[1], T00, A1[3]);
+        const double Vp00 = FD2(A2[0], T11, A2[1], -T10);
+        const double Vp01 = FD2(A2[0], -T01, A2[1], T00);
+        const double Vp10 = FD2(A2[2], T11, A2[3], -T10);
+        const double Vp11 = FD2(A2[2], -T01, A2[3], T00);
+        const double Xp00 = FD2(Vp00, G1[0], Vp01, G1[1]);
+        const double Xp01 = FD2(Vp00, G1[1], Vp01, G1[2]);
+        const double Xp10 = FD2(Vp10, G1[0], Vp11, G1[1]);
+        const double Xp11 = FD2(Vp10, G1[1], Vp11, G1[2]);
+        const double Y00 = FD2(H2[0], A1[0], H2[1], A1[2]);
+        const double Y01 = FD2(H2[0], A1[1], H2[1], A1[3]);
+        const double Y10 = FD2(H2[1], A1[0], H2[2], A1[2]);
+        const double Y11 = FD2(H2[1], A1[1], H2[2], A1[3]);
+        const double gp0 = FD2(Xp00, A2[0], Xp01, A2[1]);
+        const double gp1 = FD2(Xp00, A2[2], Xp01, A2[3]);
+        const double gp2 = FD2(Xp10, A2[2], Xp11, A2[3]);
+        rc_el r;
+#if ORC_RC_FORM == 2
+        const double U00 = Up00 * it, U01 = Up01 * it, U10 = Up10 * it, U11 = Up11 * it;
+        r.a[0] = FD2(A2[0], U00, A2[1], U10);
+        r.a[1] = FD2(A2[0], U01, A2[1], U11);
+        r.a[2] = FD2(A2[2], U00, A2[3], U10);
+        r.a[3] = FD2(A2[2], U01, A2[3], U11);
+        r.h[0] = FD3(U00, Y00, U10, Y10, H1[0]);
+        r.h[1] = FD3(U00, Y01, U10, Y11, H1[1]);
+        r.h[2] = FD3(U01, Y01, U11, Y11, H1[2]);
+#else
+        r.a[0] = FD2(A2[0], Up00, A2[1], Up10) * it;
+        r.a[1] = FD2(A2[0], Up01, A2[1], Up11) * it;
+        r.a[2] = FD2(A2[2], Up00, A2[3], Up10) * it;
+        r.a[3] = FD2(A2[2], Up01, A2[3], Up11) * it;
+        r.h[0] = fma(FD2(Up00, Y00, Up10, Y10), it, H1[0]);
+        r.h[1] = fma(FD2(Up00, Y01, Up10, Y11), it, H1[1]);
+        r.h[2] = fma(FD2(Up01, Y01, Up11, Y11), it, H1[2]);
+#endif
+        r.g[0] = fma(gp0, it, G2[0]);
+        r.g[1] = fma(gp1, it, G2[1]);
+        r.g[2] = fma(gp2, it, G2[2]);
+        *e1 = r;
+        return ok;
+    }
+#endif
     const double Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
     const double U00 = FD2(Ti00, A1[0], Ti01, A1[2]);
     const double U01 = FD2(Ti00, A1[1], Ti01, A1[3]);
@@ -936,6 +1022,23 @@ static int rc_apply(const rc_el* e, double P00, double P01, double P11, double* 
     const double detS = fma(S00, S11, -(S01 * S10));
     const int ok = (detS > 0.0) && !isinf(detS);
     const double is = 1.0 / detS;
+#if ORC_RC_FORM >= 1
+    {
+        /* W' = P adj(S), Z' = W' A, out = (A^T Z') / det(S) + H (rc_apply, BLF_RC_FORM) */
+        const double Wp00 = FD2(P00, S11, P01, -S10);
+        const double Wp01 = FD2(P00, -S01, P01, S00);
+        const double Wp10 = FD2(P01, S11, P11, -S10);
+        const double Wp11 = FD2(P01, -S01, P11, S00);
+        const double Zp00 = FD2(Wp00, A[0], Wp01, A[2]);
+        const double Zp01 = FD2(Wp00, A[1], Wp01, A[3]);
+        const double Zp10 = FD2(Wp10, A[0], Wp11, A[2]);
+        const double Zp11 = FD2(Wp10, A[1], Wp11, A[3]);
+        out[0] = fma(FD2(A[0], Zp00, A[2], Zp10), is, H[0]);
+        out[1] = fma(FD2(A[0], Zp01, A[2], Zp11), is, H[1]);
+        out[2] = fma(FD2(A[1], Zp01, A[3], Zp11), is, H[2]);
+        return ok;
+    }
+#endif
     const double Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
     const double W00 = FD2(P00, Si00, P01, Si10);
     const double W01 = FD2(P00, Si01, P01, Si11);

@@ -28,6 +28,10 @@
 typedef struct { float dt, Qw0, Qw1, Rw0, Rw1, Pw0, Pw1, tol_p, tol_d; } pf_t;
 typedef struct { float a0, a1, a2, a3, g0, g1, g2, h0, h1, h2; } rcf;
 
+#ifndef ORC_RC_FORM   /* the kernel's BLF_RC_FORM (dcm_qp_common.h) */
+#define ORC_RC_FORM 2
+#endif
+
 typedef struct {
     int N, M, KPL, seq, dpp;   /* dpp: the DPP scan tree (orc_dcm_params.as_tree) */
     pf_t P;
@@ -60,6 +64,55 @@ static int rcf_combine(rcf* e, const rcf* q)
     const float detT = fmaf(T00, T11, -(T01 * T10));
     const int ok = (detT > 0.0f) && !isinf(detT);
     const float it = one / detT;
+#if ORC_RC_FORM >= 2
+    {
+        /* adj(T) = [T11, -T01; -T10, T00]: the products run beside the division (rc_combine of
+         * dcm_qp_common.h, BLF_RC_FORM) */
+        const float Up00 = F2(T11, e->a0, -T01, e->a2);
+        const float Up01 = F2(T11, e->a1, -T01, e->a3);
+        const float Up10 = F2(-T10, e->a0, T00, e->a2);
+        const float Up11 = F2(-T10, e->a1, T00, e->a3);
+        const float Vp00 = F2(q->a0, T11, q->a1, -T10);
+        const float Vp01 = F2(q->a0, -T01, q->a1, T00);
+        const float Vp10 = F2(q->a2, T11, q->a3, -T10);
+        const float Vp11 = F2(q->a2, -T01, q->a3, T00);
+        const float Xp00 = F2(Vp00, e->g0, Vp01, e->g1);
+        const float Xp01 = F2(Vp00, e->g1, Vp01, e->g2);
+        const float Xp10 = F2(Vp10, e->g0, Vp11, e->g1);
+        const float Xp11 = F2(Vp10, e->g1, Vp11, e->g2);
+        const float Y00 = F2(q->h0, e->a0, q->h1, e->a2);
+        const float Y01 = F2(q->h0, e->a1, q->h1, e->a3);
+        const float Y10 = F2(q->h1, e->a0, q->h2, e->a2);
+        const float Y11 = F2(q->h1, e->a1, q->h2, e->a3);
+        const float gp0 = F2(Xp00, q->a0, Xp01, q->a1);
+        const float gp1 = F2(Xp00, q->a2, Xp01, q->a3);
+        const float gp2 = F2(Xp10, q->a2, Xp11, q->a3);
+        rcf r;
+#if ORC_RC_FORM == 2
+        const float U00 = Up00 * it, U01 = Up01 * it, U10 = Up10 * it, U11 = Up11 * it;
+        r.a0 = F2(q->a0, U00, q->a1, U10);
+        r.a1 = F2(q->a0, U01, q->a1, U11);
+        r.a2 = F2(q->a2, U00, q->a3, U10);
+        r.a3 = F2(q->a2, U01, q->a3, U11);
+        r.h0 = F3(U00, Y00, U10, Y10, e->h0);
+        r.h1 = F3(U00, Y01, U10, Y11, e->h1);
+        r.h2 = F3(U01, Y01, U11, Y11, e->h2);
+#else
+        r.a0 = F2(q->a0, Up00, q->a1, Up10) * it;
+        r.a1 = F2(q->a0, Up01, q->a1, Up11) * it;
+        r.a2 = F2(q->a2, Up00, q->a3, Up10) * it;
+        r.a3 = F2(q->a2, Up01, q->a3, Up11) * it;
+        r.h0 = fmaf(F2(Up00, Y00, Up10, Y10), it, e->h0);
+        r.h1 = fmaf(F2(Up00, Y01, Up10, Y11), it, e->h1);
+        r.h2 = fmaf(F2(Up01, Y01, Up11, Y11), it, e->h2);
+#endif
+        r.g0 = fmaf(gp0, it, q->g0);
+        r.g1 = fmaf(gp1, it, q->g1);
+        r.g2 = fmaf(gp2, it, q->g2);
+        *e = r;
+        return ok;
+    }
+#endif
     const float Ti00 = T11 * it, Ti01 = -(T01 * it), Ti10 = -(T10 * it), Ti11 = T00 * it;
     const float U00 = F2(Ti00, e->a0, Ti01, e->a2);
     const float U01 = F2(Ti00, e->a1, Ti01, e->a3);
@@ -102,6 +155,23 @@ static int rcf_apply(const rcf* e, float P00, float P01, float P11, float* o)
     const float detS = fmaf(S00, S11, -(S01 * S10));
     const int ok = (detS > 0.0f) && !isinf(detS);
     const float is = one / detS;
+#if ORC_RC_FORM >= 1
+    {
+        /* W' = P adj(S), Z' = W' A, out = (A^T Z') / det(S) + H (rc_apply, BLF_RC_FORM) */
+        const float Wp00 = F2(P00, S11, P01, -S10);
+        const float Wp01 = F2(P00, -S01, P01, S00);
+        const float Wp10 = F2(P01, S11, P11, -S10);
+        const float Wp11 = F2(P01, -S01, P11, S00);
+        const float Zp00 = F2(Wp00, e->a0, Wp01, e->a2);
+        const float Zp01 = F2(Wp00, e->a1, Wp01, e->a3);
+        const float Zp10 = F2(Wp10, e->a0, Wp11, e->a2);
+        const float Zp11 = F2(Wp10, e->a1, Wp11, e->a3);
+        o[0] = fmaf(F2(e->a0, Zp00, e->a2, Zp10), is, e->h0);
+        o[1] = fmaf(F2(e->a0, Zp01, e->a2, Zp11), is, e->h1);
+        o[2] = fmaf(F2(e->a1, Zp01, e->a3, Zp11), is, e->h2);
+        return ok;
+    }
+#endif
     const float Si00 = S11 * is, Si01 = -(S01 * is), Si10 = -(S10 * is), Si11 = S00 * is;
     const float W00 = F2(P00, Si00, P01, Si10);
     const float W01 = F2(P00, Si01, P01, Si11);
