@@ -121,9 +121,6 @@ struct LdsRows<float> {
 #ifndef BLF_AS_OVERLAP
 #define BLF_AS_OVERLAP 1
 #endif
-#ifndef BLF_AS_PRIO   // diagnostic: wave issue priority by dispatch order (dcm_mpc_cold_kernel)
-#define BLF_AS_PRIO 0
-#endif
 
 // One facet row (normal, offset) in the scalar type of the pass.
 template <class T>
@@ -1342,18 +1339,6 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
     double* __restrict__ lam_out, PhaseSrc ps)
 {
-#if BLF_AS_PRIO == 1
-    // diagnostic (tools/build_variant.sh): the second half of the grid issues first on a SIMD
-    if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
-#elif BLF_AS_PRIO == 2
-    // diagnostic: priority graded by dispatch quarter (later workgroups issue first)
-    {
-        const unsigned q = (unsigned)(((unsigned long long)blockIdx.x * 4) / gridDim.x);
-        if (q == 1) __builtin_amdgcn_s_setprio(1);
-        else if (q == 2) __builtin_amdgcn_s_setprio(2);
-        else if (q >= 3) __builtin_amdgcn_s_setprio(3);
-    }
-#endif
     cold_solve<KPL, LAMOUT, PH, TR>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
                                      status_out, iters_out, polished_out, lam_out, ps);
 }

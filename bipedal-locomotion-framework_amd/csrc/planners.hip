@@ -90,22 +90,27 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
     int32_t* s_stk = reinterpret_cast<int32_t*>(s_y + kHullStride * P);    // [2P+2][64] (!PK)
     uint64_t* s_pk = reinterpret_cast<uint64_t*>(s_y + kHullStride * P);   // [64] (PK)
     int32_t* s_nf = PK ? reinterpret_cast<int32_t*>(s_pk + kHullBlock) : s_stk + kHullBlock * (2 * P + 2);
+    // the lane's point count, issued before the slab so its latency hides under the slab's
+    const int n = t < nprob ? npts[p0 + t] : 0;
     {
-        // coalesced load of the [64][P][2] slab, transposed into X / Y (8 loads per lane in flight)
+        // coalesced load of the [64][P][2] slab, transposed into X / Y: every load of a lane in
+        // flight before the first LDS store (P <= 8: 16 per lane, one memory round trip; larger
+        // P: 8 at a time)
+        constexpr int UL = PK ? 16 : 8;
         const double* src = pts + p0 * 2 * P;
-        const int n = nprob * 2 * P;
+        const int ne = nprob * 2 * P;
         const SlabIdx ix(2 * P);
-        for (int base = 0; base < n; base += 8 * kHullBlock) {
-            double v[8];
+        for (int base = 0; base < ne; base += UL * kHullBlock) {
+            double v[UL];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < UL; ++u) {
                 const int e = base + u * kHullBlock + t;
-                if (e < n) v[u] = src[e];
+                if (e < ne) v[u] = src[e];
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < UL; ++u) {
                 const int e = base + u * kHullBlock + t;
-                if (e < n) {
+                if (e < ne) {
                     const int r = ix.row(e), c = e - r * 2 * P;
                     (c & 1 ? s_y : s_x)[(c >> 1) * kHullStride + r] = v[u];
                 }
@@ -123,7 +128,6 @@ __global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __rest
         if (PK) stk = (stk & ~(7ull << (3 * (i)))) | ((uint64_t)(v) << (3 * (i)));              \
         else s_stk[(i) * kHullBlock + t] = (v);                                                 \
     } while (0)
-    const int n = t < nprob ? npts[p0 + t] : 0;
     int nf = -1;
     if (t < nprob && n >= 3 && n <= P) {
         // Up to 8 points with finite coordinates: a 19-comparator sorting network in registers,
