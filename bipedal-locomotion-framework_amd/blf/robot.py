@@ -84,6 +84,73 @@ def humanoid24(seed=2020):
                 frame_link=frame_link, frame_pose=frame_pose, names=names)
 
 
+def reduce_fixed_joints(model, fixed):
+    """The model with the joints in `fixed` (names or indices) removed, each fixed joint's child
+    link merged into its parent link: what iDynTree's KinDynComputations does with a URDF's fixed
+    joints, which carry no DoF (the reference's FloatingBaseSystemDynamics.cpp:53-74 sizes the
+    state by the model's DoFs).  At q = 0 a joint's child frame sits at joint_origin with
+    rotation joint_rot in its parent frame, so merging child c of joint j into parent P:
+      mass m_P + m_c; COM (m_P c_P + m_c (o_j + E_j c_c)) / m; inertia about the new COM by the
+      parallel-axis theorem (E_j I_c E_j^T + ...); every joint on c re-parented to P with origin
+      o_j + E_j o_k and rotation E_j E_k (axes unchanged: they live in the joint frame); every
+      frame on c moved to P with position o_j + E_j p and rotation E_j R.
+    Fixed joints are merged deepest first (highest index), so chains of fixed joints collapse.
+    The rigid-body terms of the result equal those of the full model with the fixed joints held at
+    q = 0, q_dot = 0, their rows and columns removed (tests/test_fb_dynamics.py)."""
+    names = list(model["names"]) if "names" in model else None
+    idx = sorted({(names.index(f) - 1) if isinstance(f, str) else int(f) for f in fixed}, reverse=True)
+    n = model["n"]
+    m = {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in model.items()}
+    parent = [int(x) for x in m["parent"]]
+    o = [np.array(x, dtype=np.float64) for x in m["joint_origin"]]
+    E = [np.array(x, dtype=np.float64) for x in m["joint_rot"]]
+    ax = [np.array(x, dtype=np.float64) for x in m["joint_axis"]]
+    mass = [float(x) for x in m["link_mass"]]
+    com = [np.array(x, dtype=np.float64) for x in m["link_com"]]
+    inertia = [np.array(x, dtype=np.float64) for x in m["link_inertia"]]
+    flink = [int(x) for x in m["frame_link"]]
+    fpose = [np.array(x, dtype=np.float64) for x in m["frame_pose"]]
+    lnames = names if names is not None else [str(i) for i in range(n + 1)]
+    S = lambda d: (d @ d) * np.eye(3) - np.outer(d, d)
+    for j in idx:
+        if not 0 <= j < len(parent):
+            raise ValueError(f"reduce_fixed_joints: joint {j} out of range")
+        c, P = j + 1, parent[j]
+        cc = o[j] + E[j] @ com[c]                  # child COM in P's frame
+        mt = mass[P] + mass[c]
+        cn = (mass[P] * com[P] + mass[c] * cc) / mt if mt > 0 else com[P].copy()
+        inertia[P] = (inertia[P] + mass[P] * S(com[P] - cn)
+                      + E[j] @ inertia[c] @ E[j].T + mass[c] * S(cc - cn))
+        mass[P], com[P] = mt, cn
+        for k in range(len(parent)):               # joints on c move to P
+            if parent[k] == c:
+                parent[k] = P
+                o[k] = o[j] + E[j] @ o[k]
+                E[k] = E[j] @ E[k]
+        for f in range(len(flink)):                # frames on c move to P
+            if flink[f] == c:
+                flink[f] = P
+                Rf = fpose[f][3:].reshape(3, 3)
+                fpose[f] = np.concatenate([o[j] + E[j] @ fpose[f][:3], (E[j] @ Rf).reshape(-1)])
+        # drop joint j and link c; links above c shift down by one
+        for lst in (o, E, ax):
+            del lst[j]
+        del parent[j]
+        for lst in (mass, com, inertia, lnames):
+            del lst[c]
+        parent = [x - 1 if x > c else x for x in parent]
+        flink = [x - 1 if x > c else x for x in flink]
+    nr = len(parent)
+    out = dict(m)
+    out.update(n=nr, parent=np.array(parent, dtype=np.int32), joint_origin=np.array(o).reshape(nr, 3),
+               joint_rot=np.array(E).reshape(nr, 3, 3), joint_axis=np.array(ax).reshape(nr, 3),
+               link_mass=np.array(mass), link_com=np.array(com), link_inertia=np.array(inertia),
+               frame_link=np.array(flink, dtype=np.int32), frame_pose=np.array(fpose).reshape(-1, 12))
+    if names is not None:
+        out["names"] = lnames
+    return out
+
+
 def random_states(model, batch, seed=0, spread=0.3):
     """Batch of floating-base states near a standing pose: base at 0.75 m, joints within
     +-spread rad, velocities ~N(0, 0.5)."""

@@ -42,7 +42,18 @@ struct RobotModel
     std::vector<double> linkInertia;   /**< [n+1][9]   */
     std::vector<int32_t> frameLink;    /**< [F]        */
     std::vector<double> framePose;     /**< [F][12]    */
+    /** [n] or empty: 1 marks a fixed joint (a URDF "fixed" joint, no DoF). setRobotModel merges
+     *  each fixed joint's child link into its parent (reduceFixedJoints), as iDynTree's model has
+     *  no DoF for it; the state and torque vectors then cover the remaining joints only. */
+    std::vector<uint8_t> fixedJoint;
 };
+
+/** The model with every joint marked in model.fixedJoint removed and its child link merged into
+ *  the parent link (mass, COM, inertia by the parallel-axis theorem; child joints and frames
+ *  re-expressed in the parent link's frame at q = 0), deepest first.  The result has an empty
+ *  fixedJoint.  Its rigid-body terms equal the full model's with the fixed joints held at
+ *  q = 0, q_dot = 0 (blf/robot.py reduce_fixed_joints, tests/test_fb_dynamics.py). */
+RobotModel reduceFixedJoints(const RobotModel& model);
 } // namespace blf
 
 namespace BipedalLocomotion

@@ -32,8 +32,116 @@ bool FloatingBaseDynamicalSystem::initalize(std::weak_ptr<IParametersHandler> ha
     return true;
 }
 
-bool FloatingBaseDynamicalSystem::setRobotModel(const blf::RobotModel& model)
+blf::RobotModel blf::reduceFixedJoints(const RobotModel& in)
 {
+    RobotModel m = in;
+    m.fixedJoint.clear();
+    const int n0 = in.ndof;
+    if (in.fixedJoint.size() != static_cast<std::size_t>(n0)) return m;
+    auto E = [&](int j, int r, int c) { return m.jointRotation[9 * j + 3 * r + c]; };
+    // y = E_j x (3-vectors)
+    auto rot = [&](int j, const double* x, double* y) {
+        for (int r = 0; r < 3; ++r) y[r] = E(j, r, 0) * x[0] + E(j, r, 1) * x[1] + E(j, r, 2) * x[2];
+    };
+    // C = E_j A (3x3 row-major)
+    auto rotm = [&](int j, const double* A, double* C) {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                C[3 * r + c] = E(j, r, 0) * A[c] + E(j, r, 1) * A[3 + c] + E(j, r, 2) * A[6 + c];
+    };
+    // I += m S(d), S(d) = |d|^2 1 - d d^T
+    auto pax = [](double* I, double mass, const double* d) {
+        const double dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) I[3 * r + c] += mass * ((r == c ? dd : 0.0) - d[r] * d[c]);
+    };
+    for (int j = n0 - 1; j >= 0; --j)
+    {
+        if (!in.fixedJoint[j]) continue;
+        const int c = j + 1, P = m.parent[j];
+        double cc[3], cn[3], Ic[9], T[9];
+        rot(j, &m.linkCom[3 * c], cc);
+        for (int a = 0; a < 3; ++a) cc[a] += m.jointOrigin[3 * j + a];   // child COM in P's frame
+        const double mP = m.linkMass[P], mc = m.linkMass[c], mt = mP + mc;
+        for (int a = 0; a < 3; ++a) cn[a] = mt > 0 ? (mP * m.linkCom[3 * P + a] + mc * cc[a]) / mt : m.linkCom[3 * P + a];
+        // E_j I_c E_j^T
+        rotm(j, &m.linkInertia[9 * c], T);
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) Ic[3 * r + k] = T[3 * r] * E(j, k, 0) + T[3 * r + 1] * E(j, k, 1) + T[3 * r + 2] * E(j, k, 2);
+        double dP[3], dc[3];
+        for (int a = 0; a < 3; ++a) { dP[a] = m.linkCom[3 * P + a] - cn[a]; dc[a] = cc[a] - cn[a]; }
+        double* IP = &m.linkInertia[9 * P];
+        pax(IP, mP, dP);
+        for (int k = 0; k < 9; ++k) IP[k] += Ic[k];
+        pax(IP, mc, dc);
+        m.linkMass[P] = mt;
+        for (int a = 0; a < 3; ++a) m.linkCom[3 * P + a] = cn[a];
+        for (int k = j + 1; k < m.ndof; ++k)   // joints on c move to P
+            if (m.parent[k] == c)
+            {
+                double o[3], R[9];
+                rot(j, &m.jointOrigin[3 * k], o);
+                rotm(j, &m.jointRotation[9 * k], R);
+                for (int a = 0; a < 3; ++a) m.jointOrigin[3 * k + a] = m.jointOrigin[3 * j + a] + o[a];
+                for (int a = 0; a < 9; ++a) m.jointRotation[9 * k + a] = R[a];
+                m.parent[k] = P;
+            }
+        for (std::size_t f = 0; f < m.frameLink.size(); ++f)   // frames on c move to P
+            if (m.frameLink[f] == c)
+            {
+                double p[3], R[9];
+                rot(j, &m.framePose[12 * f], p);
+                rotm(j, &m.framePose[12 * f + 3], R);
+                for (int a = 0; a < 3; ++a) m.framePose[12 * f + a] = m.jointOrigin[3 * j + a] + p[a];
+                for (int a = 0; a < 9; ++a) m.framePose[12 * f + 3 + a] = R[a];
+                m.frameLink[f] = P;
+            }
+        // drop joint j and link c; links above c shift down by one
+        m.parent.erase(m.parent.begin() + j);
+        m.jointOrigin.erase(m.jointOrigin.begin() + 3 * j, m.jointOrigin.begin() + 3 * j + 3);
+        m.jointRotation.erase(m.jointRotation.begin() + 9 * j, m.jointRotation.begin() + 9 * j + 9);
+        m.jointAxis.erase(m.jointAxis.begin() + 3 * j, m.jointAxis.begin() + 3 * j + 3);
+        m.linkMass.erase(m.linkMass.begin() + c);
+        m.linkCom.erase(m.linkCom.begin() + 3 * c, m.linkCom.begin() + 3 * c + 3);
+        m.linkInertia.erase(m.linkInertia.begin() + 9 * c, m.linkInertia.begin() + 9 * c + 9);
+        for (auto& p : m.parent)
+            if (p > c) --p;
+        for (auto& l : m.frameLink)
+            if (l > c) --l;
+        --m.ndof;
+    }
+    return m;
+}
+
+bool FloatingBaseDynamicalSystem::setRobotModel(const blf::RobotModel& fullModel)
+{
+    if (!fullModel.fixedJoint.empty()
+        && fullModel.fixedJoint.size() != static_cast<std::size_t>(fullModel.ndof))
+    {
+        std::cerr << "[FloatingBaseDynamicalSystem::setRobotModel] Corrupted robot model." << std::endl;
+        return false;
+    }
+    // sizes are checked before the merge reads them (the merged model is checked again below)
+    const std::size_t n0 = static_cast<std::size_t>(fullModel.ndof < 0 ? 0 : fullModel.ndof);
+    if (!fullModel.fixedJoint.empty()
+        && (fullModel.parent.size() != n0 || fullModel.jointOrigin.size() != 3 * n0
+            || fullModel.jointRotation.size() != 9 * n0 || fullModel.jointAxis.size() != 3 * n0
+            || fullModel.linkMass.size() != n0 + 1 || fullModel.linkCom.size() != 3 * (n0 + 1)
+            || fullModel.linkInertia.size() != 9 * (n0 + 1)
+            || fullModel.framePose.size() != 12 * fullModel.frameLink.size()))
+    {
+        std::cerr << "[FloatingBaseDynamicalSystem::setRobotModel] Corrupted robot model." << std::endl;
+        return false;
+    }
+    for (std::size_t j = 0; j < fullModel.fixedJoint.size(); ++j)
+        if (fullModel.parent[j] < 0 || fullModel.parent[j] > static_cast<int32_t>(j))
+        {
+            std::cerr << "[FloatingBaseDynamicalSystem::setRobotModel] The joints must be in "
+                         "topological order (parent[j] <= j)."
+                      << std::endl;
+            return false;
+        }
+    const blf::RobotModel model = fullModel.fixedJoint.empty() ? fullModel : blf::reduceFixedJoints(fullModel);
     const std::size_t n = static_cast<std::size_t>(model.ndof);
     const std::size_t F = model.frameLink.size();
     if (model.ndof < 1 || model.ndof > BLF_FBD_MAX_DOFS || model.parent.size() != n

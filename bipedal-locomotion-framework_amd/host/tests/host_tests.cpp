@@ -9,6 +9,7 @@
  *   config.ini (tests/golden/parameters_config.ini) read by StdImplementation::setFromFile.
  * usage: blf_host_tests [cpu|gpu|all]   (exit status = number of failed checks)
  */
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -715,6 +716,89 @@ static void testFloatingBaseDynamics()
     REQUIRE(system->setMassMatrixRegularization(blf::MatrixXd(9, 9)));
 }
 
+// ---- fixed joints (blf::reduceFixedJoints): host-only checks of the merge -------------------------
+// Whole-body mass and centre of mass at q = 0 (base at the origin) of a model, by a forward pass.
+static std::array<double, 4> massAndCom(const blf::RobotModel& m)
+{
+    std::vector<std::array<double, 9>> R(m.ndof + 1);
+    std::vector<std::array<double, 3>> p(m.ndof + 1);
+    R[0] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    p[0] = {0, 0, 0};
+    for (int j = 0; j < m.ndof; ++j)
+    {
+        const int P = m.parent[j], c = j + 1;
+        for (int r = 0; r < 3; ++r)
+        {
+            p[c][r] = p[P][r];
+            for (int k = 0; k < 3; ++k)
+            {
+                p[c][r] += R[P][3 * r + k] * m.jointOrigin[3 * j + k];
+                R[c][3 * r + k] = 0.0;
+                for (int l = 0; l < 3; ++l) R[c][3 * r + k] += R[P][3 * r + l] * m.jointRotation[9 * j + 3 * l + k];
+            }
+        }
+    }
+    std::array<double, 4> out{0, 0, 0, 0};
+    for (int l = 0; l <= m.ndof; ++l)
+    {
+        out[0] += m.linkMass[l];
+        for (int r = 0; r < 3; ++r)
+        {
+            double c = p[l][r];
+            for (int k = 0; k < 3; ++k) c += R[l][3 * r + k] * m.linkCom[3 * l + k];
+            out[1 + r] += m.linkMass[l] * c;
+        }
+    }
+    for (int r = 0; r < 3; ++r) out[1 + r] /= out[0];
+    return out;
+}
+
+static void testFixedJoints()
+{
+    blf::RobotModel full = chainModel();
+    const blf::Matrix3 E1 = rpy(0.1, -0.2, 0.3);
+    for (int k = 0; k < 9; ++k) full.jointRotation[9 + k] = E1[k];   // joint 1 mounted with a rotation
+    full.fixedJoint = {0, 1, 1};                                     // joints 1 and 2 (a chain) fixed
+    const blf::RobotModel red = blf::reduceFixedJoints(full);
+    REQUIRE(red.ndof == 1 && red.parent.size() == 1 && red.linkMass.size() == 2 && red.fixedJoint.empty());
+    REQUIRE(red.frameLink.size() == 1 && red.frameLink[0] == 1);   // the sole frame moved onto link 1
+    const auto a = massAndCom(full), b = massAndCom(red);
+    for (int i = 0; i < 4; ++i) REQUIRE(std::abs(a[i] - b[i]) < 1e-14);
+    // the merged inertia stays symmetric positive definite
+    const double* I = &red.linkInertia[9];
+    REQUIRE(std::abs(I[1] - I[3]) < 1e-15 && std::abs(I[2] - I[6]) < 1e-15 && std::abs(I[5] - I[7]) < 1e-15);
+    REQUIRE(I[0] > 0 && I[0] * I[4] - I[1] * I[3] > 0);
+    // no fixed joint: unchanged; a malformed mask is refused by setRobotModel
+    blf::RobotModel none = chainModel();
+    none.fixedJoint = {0, 0, 0};
+    REQUIRE(blf::reduceFixedJoints(none).ndof == 3);
+    FloatingBaseDynamicalSystem sys;
+    blf::RobotModel bad = chainModel();
+    bad.fixedJoint = {1};
+    REQUIRE_FALSE(sys.setRobotModel(bad));
+}
+
+static void testFixedJointsDevice()
+{
+    // the adapter merges on setRobotModel: one DoF left, free fall as for any model
+    blf::RobotModel full = chainModel();
+    full.fixedJoint = {0, 1, 1};
+    auto system = std::make_shared<FloatingBaseDynamicalSystem>();
+    auto handler = std::make_shared<ParametersHandler::StdImplementation>();
+    handler->setParameter("rho", 0.01);
+    REQUIRE(system->initalize(handler));
+    REQUIRE(system->setRobotModel(full));
+    blf::VectorXd one(1, 0.0), q(1, 0.2);
+    REQUIRE(system->setState({blf::Vector6{}, one, blf::Vector3{{0.0, 0.0, 1.0}}, rpy(0.05, -0.1, 0.2), q}));
+    REQUIRE(system->setControlInput({one, {}}));
+    FloatingBaseDynamicalSystem::StateDerivativeType dx;
+    REQUIRE(system->dynamics(0.0, dx));
+    REQUIRE(std::get<1>(dx).size() == 1);
+    REQUIRE(std::abs(std::get<0>(dx)[2] + 9.81) < 1e-10 && std::abs(std::get<1>(dx)[0]) < 1e-10);
+    REQUIRE(system->setControlInput({blf::VectorXd(3, 0.0), {}}));   // the full model's size: refused
+    REQUIRE_FALSE(system->dynamics(0.0, dx));
+}
+
 // ---- ParametersHandlerYarpTest.cpp:30-140, on the reference's tests/config.ini -----------------
 static std::string g_golden = "tests/golden";
 
@@ -813,6 +897,8 @@ int main(int argc, char** argv)
         {"Continuous Contact", true, testContinuousContact},
         {"FloatingBaseSystemKinematics", true, testFloatingBaseKinematics},
         {"FloatingBaseDynamicalSystem", true, testFloatingBaseDynamics},
+        {"Fixed joints (model merge)", false, testFixedJoints},
+        {"Fixed joints (device)", true, testFixedJointsDevice},
     };
     for (const auto& t : tests)
     {

@@ -110,3 +110,47 @@ def test_frame_jacobian_matches_frame_velocity():
     for f in range(2):
         _, _, vel, J = F.frame_state(MODEL, K, f)
         np.testing.assert_allclose(J @ nu, vel, atol=1e-13)
+
+
+# Fixed joints (blf/robot.py reduce_fixed_joints): a leaf (neck_pitch), an inner joint with
+# children (torso_roll), a chain of two (the left shoulder roll + yaw), and a joint whose child
+# carries a sole frame (l_ankle_roll).
+FIXED = ("neck_pitch", "torso_roll", "l_shoulder_roll", "l_shoulder_yaw", "l_ankle_roll")
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_fixed_joints_reduce_to_the_locked_model(seed):
+    """The reduced model's rigid-body terms equal the full model's with the fixed joints held at
+    q = 0, q_dot = 0 (their rows and columns removed); the sole frames' poses and Jacobians too."""
+    red = robot.reduce_fixed_joints(MODEL, FIXED)
+    keep_j = [j for j in range(MODEL["n"]) if MODEL["names"][j + 1] not in FIXED]
+    assert red["n"] == MODEL["n"] - len(FIXED) and red["names"][1:] == [MODEL["names"][j + 1] for j in keep_j]
+    assert abs(red["link_mass"].sum() - MODEL["link_mass"].sum()) < 1e-12
+    st = state_i(robot.random_states(MODEL, 1, seed=30 + seed), 0)
+    qf, vf = st["joint_pos"].copy(), st["joint_vel"].copy()
+    for name in FIXED:
+        j = MODEL["names"].index(name) - 1
+        qf[j] = 0.0
+        vf[j] = 0.0
+    K = F.kinematics(MODEL, st["base_pos"], st["base_rot"], qf, st["base_vel"], vf)
+    M, h = F.mass_and_bias(MODEL, K)
+    Kr = F.kinematics(red, st["base_pos"], st["base_rot"], qf[keep_j], st["base_vel"], vf[keep_j])
+    Mr, hr = F.mass_and_bias(red, Kr)
+    rows = list(range(6)) + [6 + j for j in keep_j]
+    np.testing.assert_allclose(Mr, M[np.ix_(rows, rows)], rtol=1e-12, atol=1e-12 * np.abs(M).max())
+    np.testing.assert_allclose(hr, h[rows], rtol=1e-12, atol=1e-12 * np.abs(h).max())
+    for f in range(len(MODEL["frame_link"])):
+        pf, Rf, vel, J = F.frame_state(MODEL, K, f)
+        pr, Rr, velr, Jr = F.frame_state(red, Kr, f)
+        np.testing.assert_allclose(pr, pf, atol=1e-14)
+        np.testing.assert_allclose(Rr, Rf, atol=1e-14)
+        np.testing.assert_allclose(velr, vel, atol=1e-13)
+        np.testing.assert_allclose(Jr, J[:, rows], atol=1e-14)
+
+
+def test_fixed_joints_argument_errors():
+    with pytest.raises(ValueError):
+        robot.reduce_fixed_joints(MODEL, [99])
+    same = robot.reduce_fixed_joints(MODEL, [])
+    for k in ("parent", "joint_origin", "joint_rot", "link_inertia", "frame_pose"):
+        np.testing.assert_array_equal(same[k], MODEL[k])

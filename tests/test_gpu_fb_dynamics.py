@@ -137,3 +137,38 @@ def test_fbd_two_systems_per_wavefront_odd_batches(handle, B):
         ref = F.euler_integrate(MODEL, st, i, 0.0, 0.003, 0.001, **kw)
         for k in native.FB_STATE_KEYS:
             assert rel_err(got[k][i], ref[k]) < TOL, (i, k)
+
+
+def test_fbd_fixed_joints_on_device_match_the_locked_full_model(handle):
+    """A model with fixed joints (blf/robot.py reduce_fixed_joints, the DoF-less joints iDynTree
+    loads from a URDF) on the device, against the full model with those joints held at q = 0,
+    q_dot = 0 on the oracle: the full M and h (and contact Jacobians) with the fixed rows and
+    columns removed, then the same LLT solve.  Sole frames sit on a merged link (l_ankle_roll)."""
+    import oracle as O
+    fixed = ("neck_pitch", "torso_roll", "l_shoulder_roll", "l_shoulder_yaw", "l_ankle_roll")
+    red = robot.reduce_fixed_joints(MODEL, fixed)
+    keep = [j for j in range(MODEL["n"]) if MODEL["names"][j + 1] not in fixed]
+    rows = list(range(6)) + [6 + j for j in keep]
+    B = 48
+    full = robot.random_states(MODEL, B, seed=77)
+    st = {k: (v[:, keep] if k in ("joint_pos", "joint_vel", "joint_torque") else v) for k, v in full.items()}
+    host, dev = contacts_for(B, seed=3)
+    dm = handle.fb_model(red)
+    out = handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS}, _d(st["joint_torque"]),
+                              contacts=dev)
+    out = {k: v.cpu().numpy() for k, v in out.items()}
+    for i in range(0, B, 5):
+        q = np.zeros(MODEL["n"]); qd = np.zeros(MODEL["n"]); tau = np.zeros(MODEL["n"])
+        q[keep], qd[keep], tau[keep] = st["joint_pos"][i], st["joint_vel"][i], st["joint_torque"][i]
+        K = F.kinematics(MODEL, full["base_pos"][i], full["base_rot"][i], q, full["base_vel"][i], qd)
+        M, h = F.mass_and_bias(MODEL, K)
+        known = -h
+        for c, f in enumerate(host["frame"]):
+            pf, Rf, vel, J = F.frame_state(MODEL, K, f)
+            wrench = O.contact_eval(host["params"][c], vel, np.concatenate([pf, Rf.reshape(-1)]),
+                                    host["null_pose"][i][c])[0]
+            known = known + J.T @ wrench
+        known[6:] += tau
+        acc = np.linalg.solve(M[np.ix_(rows, rows)], known[rows])
+        assert rel_err(out["base_vel"][i], acc[:6]) < TOL
+        assert rel_err(out["joint_vel"][i], acc[6:]) < TOL
