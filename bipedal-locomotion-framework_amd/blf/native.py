@@ -40,7 +40,7 @@ class FbModel(ctypes.Structure):
     _fields_ = [("ndof", _i32), ("nframes", _i32), ("parent", _vp), ("joint_origin", _vp),
                 ("joint_rot", _vp), ("joint_axis", _vp), ("link_mass", _vp), ("link_com", _vp),
                 ("link_inertia", _vp), ("frame_link", _vp), ("frame_pose", _vp),
-                ("gravity", _f64 * 3), ("rho", _f64)]
+                ("gravity", _f64 * 3), ("rho", _f64), ("joint_type", _vp)]
 
 
 class FbState(ctypes.Structure):
@@ -714,6 +714,8 @@ class Handle:
                     link_mass=f64(model["link_mass"]), link_com=f64(model["link_com"]),
                     link_inertia=f64(model["link_inertia"]), frame_link=i32(model["frame_link"]),
                     frame_pose=f64(model["frame_pose"]))
+        if model.get("joint_type") is not None:   # absent: every joint revolute (NULL)
+            dm.t["joint_type"] = i32(model["joint_type"])
         c = FbModel()
         c.ndof = int(model["n"])
         c.nframes = int(len(model["frame_link"]))

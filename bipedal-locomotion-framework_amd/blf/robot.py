@@ -84,6 +84,21 @@ def humanoid24(seed=2020):
                 frame_link=frame_link, frame_pose=frame_pose, names=names)
 
 
+REVOLUTE, PRISMATIC = 0, 1   # model["joint_type"] (blf_fb_model.joint_type; absent: all revolute)
+
+
+def with_joint_types(model, prismatic=()):
+    """A copy of `model` whose joints named (or indexed) in `prismatic` are prismatic: the child
+    link slides along the joint axis by q instead of rotating about it (URDF "prismatic")."""
+    names = list(model["names"])
+    jt = np.zeros(model["n"], dtype=np.int32)
+    for f in prismatic:
+        jt[(names.index(f) - 1) if isinstance(f, str) else int(f)] = PRISMATIC
+    out = dict(model)
+    out["joint_type"] = jt
+    return out
+
+
 def reduce_fixed_joints(model, fixed):
     """The model with the joints in `fixed` (names or indices) removed, each fixed joint's child
     link merged into its parent link: what iDynTree's KinDynComputations does with a URDF's fixed
@@ -98,6 +113,8 @@ def reduce_fixed_joints(model, fixed):
     The rigid-body terms of the result equal those of the full model with the fixed joints held at
     q = 0, q_dot = 0, their rows and columns removed (tests/test_fb_dynamics.py)."""
     names = list(model["names"]) if "names" in model else None
+    if names is None and any(isinstance(f, str) for f in fixed):
+        raise ValueError("reduce_fixed_joints: joints named, but the model has no names")
     idx = sorted({(names.index(f) - 1) if isinstance(f, str) else int(f) for f in fixed}, reverse=True)
     n = model["n"]
     m = {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in model.items()}
@@ -109,6 +126,7 @@ def reduce_fixed_joints(model, fixed):
     com = [np.array(x, dtype=np.float64) for x in m["link_com"]]
     inertia = [np.array(x, dtype=np.float64) for x in m["link_inertia"]]
     flink = [int(x) for x in m["frame_link"]]
+    jtype = [int(x) for x in m["joint_type"]] if m.get("joint_type") is not None else None
     fpose = [np.array(x, dtype=np.float64) for x in m["frame_pose"]]
     lnames = names if names is not None else [str(i) for i in range(n + 1)]
     S = lambda d: (d @ d) * np.eye(3) - np.outer(d, d)
@@ -133,7 +151,7 @@ def reduce_fixed_joints(model, fixed):
                 Rf = fpose[f][3:].reshape(3, 3)
                 fpose[f] = np.concatenate([o[j] + E[j] @ fpose[f][:3], (E[j] @ Rf).reshape(-1)])
         # drop joint j and link c; links above c shift down by one
-        for lst in (o, E, ax):
+        for lst in (o, E, ax) + ((jtype,) if jtype is not None else ()):
             del lst[j]
         del parent[j]
         for lst in (mass, com, inertia, lnames):
@@ -148,6 +166,8 @@ def reduce_fixed_joints(model, fixed):
                frame_link=np.array(flink, dtype=np.int32), frame_pose=np.array(fpose).reshape(-1, 12))
     if names is not None:
         out["names"] = lnames
+    if jtype is not None:
+        out["joint_type"] = np.array(jtype, dtype=np.int32)
     return out
 
 

@@ -144,6 +144,7 @@ struct Model {
     const double *jorig, *jrot, *jaxis, *mass, *com, *inertia, *fpose;
     const int32_t* flink;
     double g0, g1, g2, rho;
+    const int32_t* jtype;   // [n] or nullptr: BLF_JOINT_PRISMATIC marks a sliding joint
 };
 
 struct Contacts {
@@ -287,8 +288,8 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
         const int j = lane;
         const double* a = m.jaxis + 3 * j;
         const double* E = m.jrot + 9 * j;
-        double sn, cs;
-        sincos(jp[j], &sn, &cs);
+        double sn = 0.0, cs = 1.0;   // a prismatic joint does not rotate: E Rot(a, 0) = E exactly
+        if (!(m.jtype && m.jtype[j] == BLF_JOINT_PRISMATIC)) sincos(jp[j], &sn, &cs);
         const double c1 = 1.0 - cs;
         const double K[9] = {0.0, -a[2], a[1], a[2], 0.0, -a[0], -a[1], a[0], 0.0};
         double Rr[9];
@@ -342,6 +343,14 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
                 z[a] = (RP[3 * a] * Ej[9] + RP[3 * a + 1] * Ej[10]) + RP[3 * a + 2] * Ej[11];
             }
             const double zs[3] = {z[0] * sd, z[1] * sd, z[2] * sd};
+            // prismatic (oracle/fb_dynamics.py): r = R_P o + z q, w_c = w_P, al_c = al_P,
+            // v_c = v_P + w_P x r + z sd, a_c = a_P + al_P x r + w_P x (w_P x r) + 2 w_P x z sd
+            const bool pri = m.jtype && m.jtype[j] == BLF_JOINT_PRISMATIC;
+            if (pri) {
+                const double qj = jp[j];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) r[a] = r[a] + z[a] * qj;
+            }
             double t1[3], t2[3], t3[3], t4[3];
             cross3(pr + kW, r, t1);            // w_P x r
             cross3(pr + kW, zs, t2);           // w_P x z sd
@@ -356,10 +365,11 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
                 cr[kP + a] = pc;
                 S.jz()[3 * j + a] = z[a];
                 S.jo()[3 * j + a] = pc;
-                cr[kW + a] = pr[kW + a] + zs[a];
-                cr[kV + a] = pr[kV + a] + t1[a];
-                cr[kAl + a] = pr[kAl + a] + t2[a];
-                cr[kA + a] = (pr[kA + a] + t3[a]) + t4[a];
+                const double arev = (pr[kA + a] + t3[a]) + t4[a];
+                cr[kW + a] = pri ? pr[kW + a] : pr[kW + a] + zs[a];
+                cr[kV + a] = pri ? (pr[kV + a] + t1[a]) + zs[a] : pr[kV + a] + t1[a];
+                cr[kAl + a] = pri ? pr[kAl + a] : pr[kAl + a] + t2[a];
+                cr[kA + a] = pri ? arev + 2.0 * t2[a] : arev;
             }
         }
         wave_sync();
@@ -517,8 +527,12 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             cross3(pB, w, u);
         } else {
             const int j = c - 6;
-            for (int a = 0; a < 3; ++a) w[a] = S.jz()[3 * j + a];
-            cross3(S.jo() + 3 * j, w, u);
+            if (m.jtype && m.jtype[j] == BLF_JOINT_PRISMATIC) {   // S = (0; z): a pure translation
+                for (int a = 0; a < 3; ++a) u[a] = S.jz()[3 * j + a];
+            } else {
+                for (int a = 0; a < 3; ++a) w[a] = S.jz()[3 * j + a];
+                cross3(S.jo() + 3 * j, w, u);
+            }
         }
         const double* I = S.comp() + kCompS * (c < 6 ? n : c - 6);
         double Iwv[3], hu[3], wh[3];
@@ -901,6 +915,7 @@ Model to_model(const blf_fb_model* md)
     m.g1 = md->gravity[1];
     m.g2 = md->gravity[2];
     m.rho = md->rho;
+    m.jtype = md->joint_type;
     return m;
 }
 

@@ -46,6 +46,9 @@ struct RobotModel
      *  each fixed joint's child link into its parent (reduceFixedJoints), as iDynTree's model has
      *  no DoF for it; the state and torque vectors then cover the remaining joints only. */
     std::vector<uint8_t> fixedJoint;
+    /** [n] or empty (every joint revolute): BLF_JOINT_REVOLUTE / BLF_JOINT_PRISMATIC (the child
+     *  link slides along the joint axis by q, URDF "prismatic"). */
+    std::vector<int32_t> jointType;
 };
 
 /** The model with every joint marked in model.fixedJoint removed and its child link merged into
@@ -74,7 +77,7 @@ class FloatingBaseDynamicalSystem
     bool m_hasModel{false};
     bool m_useMassMatrixRegularizationTerm{false};
     blf::RobotModel m_model;
-    blf::DeviceBuffer<int32_t> m_dParent, m_dFrameLink, m_dContactFrame;
+    blf::DeviceBuffer<int32_t> m_dParent, m_dFrameLink, m_dContactFrame, m_dJointType;
     blf::DeviceBuffer<double> m_dOrigin, m_dRot, m_dAxis, m_dMass, m_dCom, m_dInertia, m_dFramePose;
     blf::DeviceBuffer<double> m_dReg, m_dState, m_dTau, m_dContactParams, m_dNullPose, m_dOut;
 

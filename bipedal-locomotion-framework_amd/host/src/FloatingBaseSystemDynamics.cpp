@@ -101,6 +101,7 @@ blf::RobotModel blf::reduceFixedJoints(const RobotModel& in)
         m.jointOrigin.erase(m.jointOrigin.begin() + 3 * j, m.jointOrigin.begin() + 3 * j + 3);
         m.jointRotation.erase(m.jointRotation.begin() + 9 * j, m.jointRotation.begin() + 9 * j + 9);
         m.jointAxis.erase(m.jointAxis.begin() + 3 * j, m.jointAxis.begin() + 3 * j + 3);
+        if (m.jointType.size() == static_cast<std::size_t>(m.ndof)) m.jointType.erase(m.jointType.begin() + j);
         m.linkMass.erase(m.linkMass.begin() + c);
         m.linkCom.erase(m.linkCom.begin() + 3 * c, m.linkCom.begin() + 3 * c + 3);
         m.linkInertia.erase(m.linkInertia.begin() + 9 * c, m.linkInertia.begin() + 9 * c + 9);
@@ -148,7 +149,8 @@ bool FloatingBaseDynamicalSystem::setRobotModel(const blf::RobotModel& fullModel
         || model.jointOrigin.size() != 3 * n || model.jointRotation.size() != 9 * n
         || model.jointAxis.size() != 3 * n || model.linkMass.size() != n + 1
         || model.linkCom.size() != 3 * (n + 1) || model.linkInertia.size() != 9 * (n + 1)
-        || model.framePose.size() != 12 * F)
+        || model.framePose.size() != 12 * F
+        || (!model.jointType.empty() && model.jointType.size() != n))
     {
         std::cerr << "[FloatingBaseDynamicalSystem::setRobotModel] Corrupted robot model."
                   << std::endl;
@@ -162,13 +164,21 @@ bool FloatingBaseDynamicalSystem::setRobotModel(const blf::RobotModel& fullModel
                       << std::endl;
             return false;
         }
+    for (const int32_t t : model.jointType)
+        if (t != BLF_JOINT_REVOLUTE && t != BLF_JOINT_PRISMATIC)
+        {
+            std::cerr << "[FloatingBaseDynamicalSystem::setRobotModel] Unknown joint type " << t
+                      << " (revolute or prismatic; fixed joints go in fixedJoint)." << std::endl;
+            return false;
+        }
     m_model = model;
     m_actuatedDoFs = n;
     m_hasModel = m_dParent.upload(model.parent) && m_dOrigin.upload(model.jointOrigin)
                  && m_dRot.upload(model.jointRotation) && m_dAxis.upload(model.jointAxis)
                  && m_dMass.upload(model.linkMass) && m_dCom.upload(model.linkCom)
                  && m_dInertia.upload(model.linkInertia) && m_dFrameLink.upload(model.frameLink)
-                 && m_dFramePose.upload(model.framePose);
+                 && m_dFramePose.upload(model.framePose)
+                 && (model.jointType.empty() || m_dJointType.upload(model.jointType));
     return m_hasModel;
 }
 
@@ -259,6 +269,7 @@ bool FloatingBaseDynamicalSystem::prepare(const char* where, blf_fb_model& model
     model.link_inertia = m_dInertia.data();
     model.frame_link = m_dFrameLink.data();
     model.frame_pose = m_dFramePose.data();
+    model.joint_type = m_model.jointType.empty() ? nullptr : m_dJointType.data();
     for (int i = 0; i < 3; ++i) model.gravity[i] = m_gravity[i];
     model.rho = m_rho;
     double* s = m_dState.data();

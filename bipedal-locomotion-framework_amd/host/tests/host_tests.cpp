@@ -797,6 +797,20 @@ static void testFixedJointsDevice()
     REQUIRE(std::abs(std::get<0>(dx)[2] + 9.81) < 1e-10 && std::abs(std::get<1>(dx)[0]) < 1e-10);
     REQUIRE(system->setControlInput({blf::VectorXd(3, 0.0), {}}));   // the full model's size: refused
     REQUIRE_FALSE(system->dynamics(0.0, dx));
+    // a prismatic middle joint (RobotModel::jointType): free fall as well; unknown types refused
+    blf::RobotModel pri = chainModel();
+    pri.jointType = {BLF_JOINT_REVOLUTE, BLF_JOINT_PRISMATIC, BLF_JOINT_REVOLUTE};
+    REQUIRE(system->setRobotModel(pri));
+    blf::VectorXd z3(3, 0.0), q3(3, 0.1);
+    REQUIRE(system->setState({blf::Vector6{}, z3, blf::Vector3{{0.0, 0.0, 1.0}}, rpy(0.05, -0.1, 0.2), q3}));
+    REQUIRE(system->setControlInput({z3, {}}));
+    REQUIRE(system->dynamics(0.0, dx));
+    REQUIRE(std::abs(std::get<0>(dx)[2] + 9.81) < 1e-10);
+    for (int i = 0; i < 3; ++i) REQUIRE(std::abs(std::get<1>(dx)[i]) < 1e-10);
+    pri.jointType = {0, 2, 0};
+    REQUIRE_FALSE(system->setRobotModel(pri));
+    pri.jointType = {0, 1};
+    REQUIRE_FALSE(system->setRobotModel(pri));
 }
 
 // ---- ParametersHandlerYarpTest.cpp:30-140, on the reference's tests/config.ini -----------------
@@ -898,7 +912,7 @@ int main(int argc, char** argv)
         {"FloatingBaseSystemKinematics", true, testFloatingBaseKinematics},
         {"FloatingBaseDynamicalSystem", true, testFloatingBaseDynamics},
         {"Fixed joints (model merge)", false, testFixedJoints},
-        {"Fixed joints (device)", true, testFixedJointsDevice},
+        {"Fixed / prismatic joints (device)", true, testFixedJointsDevice},
     };
     for (const auto& t : tests)
     {

@@ -391,7 +391,14 @@ typedef struct blf_fb_model {
     const double* frame_pose;     /* [F][12] (p, R) of the frame in its link frame           */
     double gravity[3];            /* (0, 0, -9.81) in the reference                          */
     double rho;                   /* Baumgarte parameter of the base rotation rate           */
+    const int32_t* joint_type;    /* [n] or NULL (every joint revolute): BLF_JOINT_REVOLUTE /
+                                     BLF_JOINT_PRISMATIC (the child link slides along the axis
+                                     by q; URDF "prismatic").  Fixed joints carry no DoF: merge
+                                     them into their parent link first (the C++ adapter's
+                                     blf::reduceFixedJoints)                                  */
 } blf_fb_model;
+#define BLF_JOINT_REVOLUTE  0
+#define BLF_JOINT_PRISMATIC 1
 
 /* The state tuple (FloatingBaseSystemDynamics.h: base velocity, joint velocities, base position,
  * base orientation, joint positions); the same struct carries the state derivative (base

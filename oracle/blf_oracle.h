@@ -200,6 +200,7 @@ typedef struct orc_fb_model {
     const double* frame_pose;
     double gravity[3];
     double rho;
+    const int32_t* joint_type;   /* [n] or NULL (all revolute): 1 = prismatic (blf_fb_model) */
 } orc_fb_model;
 int orc_fbd_dynamics(const orc_fb_model* m, const double* bpos, const double* brot, const double* q,
                      const double* bvel, const double* qd, const double* tau, int ncontacts,

@@ -68,6 +68,29 @@ static void kinematics(const orc_fb_model* m, const double* bpos, const double* 
         const int P = m->parent[j], c = j + 1;
         double RE[9], Ra[9], r[3], t[3], zq[3], u[3];
         mm3(K->R[P], m->joint_rot + 9 * j, RE);
+        if (m->joint_type && m->joint_type[j] == 1) {
+            /* prismatic: the child slides along z = R_P E a by q (oracle/fb_dynamics.py) */
+            memcpy(K->R[c], RE, 9 * sizeof(double));
+            mv3(RE, m->joint_axis + 3 * j, K->z[j]);
+            mv3(K->R[P], m->joint_origin + 3 * j, r);
+            for (int i = 0; i < 3; ++i) {
+                r[i] += K->z[j][i] * q[j];
+                K->p[c][i] = K->p[P][i] + r[i];
+                zq[i] = K->z[j][i] * qd[j];
+                K->w[c][i] = K->w[P][i];
+                K->al[c][i] = K->al[P][i];
+            }
+            memcpy(K->o[j], K->p[c], 3 * sizeof(double));
+            cross3(K->w[P], r, t);
+            for (int i = 0; i < 3; ++i) K->v[c][i] = K->v[P][i] + t[i] + zq[i];
+            cross3(K->al[P], r, t);
+            cross3(K->w[P], r, u);
+            cross3(K->w[P], u, u);
+            double wz[3];
+            cross3(K->w[P], zq, wz);
+            for (int i = 0; i < 3; ++i) K->a[c][i] = K->a[P][i] + t[i] + u[i] + 2.0 * wz[i];
+            continue;
+        }
         rot_axis(m->joint_axis + 3 * j, q[j], Ra);
         mm3(RE, Ra, K->R[c]);
         mv3(K->R[P], m->joint_origin + 3 * j, r);
@@ -112,6 +135,10 @@ static void point_jacobian(const orc_fb_model* m, const fb_kin* K, unsigned long
     J[2 * NV + 3] = d[1];  J[2 * NV + 4] = -d[0];
     for (int j = 0; j < m->n; ++j) {
         if (!((anc >> j) & 1)) continue;
+        if (m->joint_type && m->joint_type[j] == 1) {   /* prismatic: (z; 0) */
+            for (int i = 0; i < 3; ++i) J[i * NV + 6 + j] = K->z[j][i];
+            continue;
+        }
         const double e[3] = {x[0] - K->o[j][0], x[1] - K->o[j][1], x[2] - K->o[j][2]};
         double t[3];
         cross3(K->z[j], e, t);

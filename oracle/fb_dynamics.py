@@ -29,11 +29,23 @@ def rot_axis(a, q):
     return np.eye(3) + np.sin(q) * K + (1 - np.cos(q)) * K @ K
 
 
+PRISMATIC = 1   # model["joint_type"][j] (optional; absent: every joint revolute)
+
+
+def prismatic(model):
+    jt = model.get("joint_type")
+    return np.zeros(model["n"], dtype=bool) if jt is None else np.asarray(jt) == PRISMATIC
+
+
 def kinematics(model, base_pos, base_rot, joint_pos, base_vel, joint_vel):
     """World pose, mixed velocity and nu_dot = 0 bias acceleration of every link, plus the joint
-    axes / origins in world coordinates."""
+    axes / origins in world coordinates.  A revolute joint rotates its child about z = R_P E a
+    through the joint origin; a prismatic one (model["joint_type"][j] = 1, URDF "prismatic")
+    translates it along z by q: r = R_P o + z q, w_c = w_P, v_c = v_P + w_P x r + z q_dot,
+    a_c = a_P + al_P x r + w_P x (w_P x r) + 2 w_P x z q_dot (nu_dot = 0)."""
     n = model["n"]
     L = n + 1
+    pri = prismatic(model)
     R = np.zeros((L, 3, 3)); p = np.zeros((L, 3))
     w = np.zeros((L, 3)); v = np.zeros((L, 3)); al = np.zeros((L, 3)); a = np.zeros((L, 3))
     z = np.zeros((n, 3)); o = np.zeros((n, 3))
@@ -41,16 +53,27 @@ def kinematics(model, base_pos, base_rot, joint_pos, base_vel, joint_vel):
     for j in range(n):
         P, c = model["parent"][j], j + 1
         E = model["joint_rot"][j]
+        z[j] = R[P] @ E @ model["joint_axis"][j]
+        zs = z[j] * joint_vel[j]
+        if pri[j]:
+            R[c] = R[P] @ E
+            r = R[P] @ model["joint_origin"][j] + z[j] * joint_pos[j]
+            p[c] = p[P] + r
+            o[j] = p[c]
+            w[c] = w[P]
+            v[c] = v[P] + np.cross(w[P], r) + zs
+            al[c] = al[P]
+            a[c] = a[P] + np.cross(al[P], r) + np.cross(w[P], np.cross(w[P], r)) + 2.0 * np.cross(w[P], zs)
+            continue
         R[c] = R[P] @ E @ rot_axis(model["joint_axis"][j], joint_pos[j])
         r = R[P] @ model["joint_origin"][j]
         p[c] = p[P] + r
-        z[j] = R[P] @ E @ model["joint_axis"][j]
         o[j] = p[c]
-        w[c] = w[P] + z[j] * joint_vel[j]
+        w[c] = w[P] + zs
         v[c] = v[P] + np.cross(w[P], r)
-        al[c] = al[P] + np.cross(w[P], z[j] * joint_vel[j])
+        al[c] = al[P] + np.cross(w[P], zs)
         a[c] = a[P] + np.cross(al[P], r) + np.cross(w[P], np.cross(w[P], r))
-    return dict(R=R, p=p, w=w, v=v, al=al, a=a, z=z, o=o)
+    return dict(R=R, p=p, w=w, v=v, al=al, a=a, z=z, o=o, pri=pri)
 
 
 def ancestors(model):
@@ -70,6 +93,9 @@ def point_jacobian(model, K, anc, l, x):
     J[:3, 3:6] = -skew(x - K["p"][0])
     J[3:, 3:6] = np.eye(3)
     for j in anc[l]:
+        if K["pri"][j]:          # prismatic: the point moves along z, no rotation
+            J[:3, 6 + j] = K["z"][j]
+            continue
         J[:3, 6 + j] = np.cross(K["z"][j], x - K["o"][j])
         J[3:, 6 + j] = K["z"][j]
     return J

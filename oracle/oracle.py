@@ -20,7 +20,7 @@ class OrcFbModel(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("parent", _ip), ("joint_origin", _dp), ("joint_rot", _dp),
                 ("joint_axis", _dp), ("link_mass", _dp), ("link_com", _dp), ("link_inertia", _dp),
                 ("frame_link", _ip), ("frame_pose", _dp), ("gravity", ctypes.c_double * 3),
-                ("rho", ctypes.c_double)]
+                ("rho", ctypes.c_double), ("joint_type", _ip)]
 
 
 class OrcParams(ctypes.Structure):
@@ -468,7 +468,8 @@ def _fb_model(model, keep, rho=0.01, gravity=(0.0, 0.0, -9.81)):
                       _d(arr(model["joint_axis"])), _d(arr(model["link_mass"])),
                       _d(arr(model["link_com"])), _d(arr(model["link_inertia"])),
                       _i(arr(model["frame_link"], np.int32)), _d(arr(model["frame_pose"])),
-                      (ctypes.c_double * 3)(*gravity), rho)
+                      (ctypes.c_double * 3)(*gravity), rho,
+                      None if model.get("joint_type") is None else _i(arr(model["joint_type"], np.int32)))
 
 
 def fbd_com_batch(model, states):

@@ -17,14 +17,22 @@ import oracle as O
 from blf import robot
 
 MODEL = robot.humanoid24()
+# the same tree with four joints prismatic (URDF "prismatic": the child slides along the axis):
+# a leaf (neck), an inner torso joint, a knee and a hip, so every identity below also covers the
+# prismatic kinematics, Jacobian columns and bias terms (oracle/fb_dynamics.py)
+PRISMATIC = ("neck_pitch", "torso_roll", "l_knee", "r_hip_pitch")
+MODEL_P = robot.with_joint_types(MODEL, prismatic=PRISMATIC)
+MODELS = {"revolute": MODEL, "prismatic": MODEL_P}
 
 
 def state_i(st, i):
     return {k: v[i] for k, v in st.items()}
 
 
+@pytest.mark.parametrize("kind", sorted(MODELS))
 @pytest.mark.parametrize("seed", range(3))
-def test_mass_matrix_and_energy(seed):
+def test_mass_matrix_and_energy(seed, kind):
+    MODEL = MODELS[kind]
     st = state_i(robot.random_states(MODEL, 1, seed=seed), 0)
     K = F.kinematics(MODEL, st["base_pos"], st["base_rot"], st["joint_pos"], st["base_vel"],
                      st["joint_vel"])
@@ -43,8 +51,10 @@ def test_mass_matrix_and_energy(seed):
     assert abs(0.5 * nu @ M @ nu - T) < 1e-12 * max(1.0, T)
 
 
+@pytest.mark.parametrize("kind", sorted(MODELS))
 @pytest.mark.parametrize("seed", range(3))
-def test_bias_forces_power_identities(seed):
+def test_bias_forces_power_identities(seed, kind):
+    MODEL = MODELS[kind]
     st = state_i(robot.random_states(MODEL, 1, seed=10 + seed), 0)
     K = F.kinematics(MODEL, st["base_pos"], st["base_rot"], st["joint_pos"], st["base_vel"],
                      st["joint_vel"])
@@ -80,7 +90,9 @@ def contact_setup(B, seed=0):
     return np.array([0, 1], dtype=np.int32), params, null
 
 
-def test_equation_of_motion_with_contacts():
+@pytest.mark.parametrize("kind", sorted(MODELS))
+def test_equation_of_motion_with_contacts(kind):
+    MODEL = MODELS[kind]
     st = robot.random_states(MODEL, 2, seed=4)
     frames, params, null = contact_setup(2)
     for i in range(2):
@@ -102,7 +114,9 @@ def test_equation_of_motion_with_contacts():
         np.testing.assert_array_equal(dq, s["joint_vel"])
 
 
-def test_frame_jacobian_matches_frame_velocity():
+@pytest.mark.parametrize("kind", sorted(MODELS))
+def test_frame_jacobian_matches_frame_velocity(kind):
+    MODEL = MODELS[kind]
     st = state_i(robot.random_states(MODEL, 1, seed=8), 0)
     K = F.kinematics(MODEL, st["base_pos"], st["base_rot"], st["joint_pos"], st["base_vel"],
                      st["joint_vel"])

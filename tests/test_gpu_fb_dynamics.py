@@ -172,3 +172,50 @@ def test_fbd_fixed_joints_on_device_match_the_locked_full_model(handle):
         acc = np.linalg.solve(M[np.ix_(rows, rows)], known[rows])
         assert rel_err(out["base_vel"][i], acc[:6]) < TOL
         assert rel_err(out["joint_vel"][i], acc[6:]) < TOL
+
+
+PRISMATIC = ("neck_pitch", "torso_roll", "l_knee", "r_hip_pitch")
+
+
+@pytest.mark.parametrize("HWkind", ["two_per_wave", "one_per_wave"])
+def test_fbd_prismatic_joints_vs_oracle(handle, HWkind):
+    """Prismatic joints (blf_fb_model.joint_type, URDF "prismatic") on the device against the numpy
+    oracle, whose prismatic kinematics / Jacobian columns the CPU identities of
+    tests/test_fb_dynamics.py pin (energy, power, frame velocity): dynamics with both sole
+    contacts, then a short Euler integration.  "one_per_wave": the same model with enough extra
+    leaf joints to exceed 26 DoF (one system per wavefront)."""
+    model = robot.with_joint_types(MODEL, prismatic=PRISMATIC)
+    if HWkind == "one_per_wave":   # NV = n + 6 > 32: fbd kernels with one system per wavefront
+        model = dict(model)
+        extra = 4
+        n0 = model["n"]
+        model["n"] = n0 + extra
+        model["parent"] = np.concatenate([model["parent"], np.arange(n0 + 1 - 1, n0 + extra) * 0 + 13]).astype(np.int32)
+        model["joint_origin"] = np.concatenate([model["joint_origin"], np.tile([[0.0, 0.01, 0.05]], (extra, 1))])
+        model["joint_rot"] = np.concatenate([model["joint_rot"], np.tile(np.eye(3), (extra, 1, 1))])
+        model["joint_axis"] = np.concatenate([model["joint_axis"], np.tile([[0.0, 0.0, 1.0]], (extra, 1))])
+        model["link_mass"] = np.concatenate([model["link_mass"], np.full(extra, 0.3)])
+        model["link_com"] = np.concatenate([model["link_com"], np.zeros((extra, 3))])
+        model["link_inertia"] = np.concatenate([model["link_inertia"], np.tile(np.eye(3) * 1e-3, (extra, 1, 1))])
+        model["joint_type"] = np.concatenate([model["joint_type"], np.array([1, 0, 1, 0], dtype=np.int32)])
+        model["names"] = list(model["names"]) + [f"extra{i}" for i in range(extra)]
+    B = 40
+    st = robot.random_states(model, B, seed=9)
+    host, dev = contacts_for(B, seed=2)
+    dm = handle.fb_model(model)
+    out = handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS}, _d(st["joint_torque"]),
+                              contacts=dev)
+    out = {k: v.cpu().numpy() for k, v in out.items()}
+    for i in range(0, B, 3):
+        ba, ja, dp, dR, dq = F.dynamics(model, st, i, contacts=host["frame"], contact_params=host["params"],
+                                        null_poses=host["null_pose"][i])
+        assert rel_err(out["base_vel"][i], ba) < TOL
+        assert rel_err(out["joint_vel"][i], ja) < TOL
+    dst = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    handle.fbd_euler_integrate(dm, dst, _d(st["joint_torque"]), 0.0, 0.0035, 0.001, contacts=dev)
+    got = {k: v.cpu().numpy() for k, v in dst.items()}
+    for i in (0, 7, B - 1):
+        ref = F.euler_integrate(model, st, i, 0.0, 0.0035, 0.001, contacts=host["frame"],
+                                contact_params=host["params"], null_poses=host["null_pose"][i])
+        for k in native.FB_STATE_KEYS:
+            assert rel_err(got[k][i], ref[k]) < TOL, k

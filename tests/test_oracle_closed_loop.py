@@ -4,6 +4,7 @@ centre of mass along the motion, the impedance integrator with zero gains is the
 ForwardEuler with zero torques, the posture law's ankle gains put m g / 2 (r0 - c) on each
 ankle, and the standing start puts the soles on the ground."""
 import numpy as np
+import pytest
 
 import closed_loop as CL
 import fb_dynamics as F
@@ -67,11 +68,14 @@ def test_standing_start_puts_the_soles_on_the_ground():
     assert null.shape == (3, 2, 12) and (null[:, :, 2] == 0).all()
 
 
-def test_c_fbd_restatement_matches_numpy():
+@pytest.mark.parametrize("prismatic", [(), ("neck_pitch", "torso_roll", "l_knee", "r_hip_pitch")])
+def test_c_fbd_restatement_matches_numpy(prismatic):
     """oracle/blf_oracle_fbd.c (the configs[4] CPU baseline's dynamics) against the numpy
-    restatement: 20 impedance-driven Euler steps with both soles in contact, to 1e-10."""
+    restatement: 20 impedance-driven Euler steps with both soles in contact, to 1e-10; also with
+    four joints prismatic (blf_fb_model.joint_type)."""
     import oracle as O
     from blf import closed_loop as DL
+    MODEL = R.with_joint_types(globals()["MODEL"], prismatic=prismatic)
     B = 4
     st = R.standing_states(MODEL, B, seed=5)
     st.pop("joint_torque", None)
