@@ -27,6 +27,7 @@
 //   v_readlane, reciprocal pivots precomputed).
 #include "blf_internal.h"
 #include "contact_math.h"
+#include "dcm_qp_common.h"   // the DPP prefix-scan levels (qp::tree_fwd / tree_has)
 #include "fbk_math.h"
 
 namespace blf {
@@ -225,6 +226,8 @@ struct Topo {
     int P, depth, maxdepth;
     double o0, o1, o2;
     unsigned long long cmask, bmask;
+    int last;   // the last joint of joint lane's subtree (DFS preorder: the run [lane, last])
+    bool dfs;   // the joints are in DFS preorder (wave-uniform): every subtree is a contiguous run
 };
 
 template <int HW>
@@ -260,6 +263,22 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
         if (lane == j) t.cmask = b;
     }
     t.bmask = H.ballot(jl && t.P == 0);
+    // DFS preorder: joint k attaches to the base or to a link on the path to link k (joint k - 1's
+    // child), i.e. its parent link's joint is among joint k - 1's ancestors; then the subtree of
+    // joint j is the run [j, j + size_j - 1], size_j = the joints whose ancestor masks hold j
+    {
+        const int src = lane > 0 ? lane - 1 : 0;
+        const int lo = H.shfl((int)an, src), hi = H.shfl((int)(an >> 32), src);
+        const unsigned long long prev = ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+        const bool ok = !jl || lane == 0 || t.P == 0 || ((prev >> (t.P - 1)) & 1ull);
+        t.dfs = H.ballot(!ok) == 0ull;
+        int size = 0;
+        for (int j = 0; j < n; ++j) {
+            const int c = __builtin_popcountll(H.ballot(jl && ((an >> j) & 1ull)));
+            if (lane == j) size = c;
+        }
+        t.last = jl ? lane + size - 1 : 0;
+    }
     int md = depth;
 #pragma unroll
     for (int off = HW / 2; off >= 1; off >>= 1) {
@@ -273,7 +292,9 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
 
 // Steps 1-2 of fbd_eval: per-joint rotations and forward kinematics (poses, mixed velocities,
 // nu_dot = 0 accelerations) of every link into the link records.
-template <int HW>
+// PRI: the model may hold prismatic joints (blf_fb_model.joint_type != NULL); the launchers
+// instantiate the kernels both ways, so all-revolute models (config 5) pay nothing for it.
+template <int HW, bool PRI>
 __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, const double* bv,
                                                const double* jvel, const double* bp, const double* bR,
                                                const double* jp, const Topo& T)
@@ -289,7 +310,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
         const double* a = m.jaxis + 3 * j;
         const double* E = m.jrot + 9 * j;
         double sn = 0.0, cs = 1.0;   // a prismatic joint does not rotate: E Rot(a, 0) = E exactly
-        if (!(m.jtype && m.jtype[j] == BLF_JOINT_PRISMATIC)) sincos(jp[j], &sn, &cs);
+        if (!(PRI && m.jtype[j] == BLF_JOINT_PRISMATIC)) sincos(jp[j], &sn, &cs);
         const double c1 = 1.0 - cs;
         const double K[9] = {0.0, -a[2], a[1], a[2], 0.0, -a[0], -a[1], a[0], 0.0};
         double Rr[9];
@@ -345,7 +366,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
             const double zs[3] = {z[0] * sd, z[1] * sd, z[2] * sd};
             // prismatic (oracle/fb_dynamics.py): r = R_P o + z q, w_c = w_P, al_c = al_P,
             // v_c = v_P + w_P x r + z sd, a_c = a_P + al_P x r + w_P x (w_P x r) + 2 w_P x z sd
-            const bool pri = m.jtype && m.jtype[j] == BLF_JOINT_PRISMATIC;
+            const bool pri = PRI && m.jtype[j] == BLF_JOINT_PRISMATIC;
             if (pri) {
                 const double qj = jp[j];
 #pragma unroll
@@ -381,7 +402,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
 // NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
 // registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
 // steps 6-9.
-template <int NVMAX, int HW>
+template <int NVMAX, int HW, bool PRI>
 __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
                                          const double* jvel, const double* bp, const double* bR,
                                          const double* jp, const double* tau, const Contacts& ct,
@@ -395,7 +416,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     const int depth = T.depth, maxdepth = T.maxdepth;
     FSTAMP(f_t0);
     FSTAMP(f_t1);
-    fbd_kinematics<HW>(m, S, bv, jvel, bp, bR, jp, T);
+    fbd_kinematics<HW, PRI>(m, S, bv, jvel, bp, bR, jp, T);
     FSTAMP_ADD(1, f_t1);
     FSTAMP(f_t2);
     // 3. per link: COM, world inertia, Newton-Euler force / moment, and the spatial inertia and
@@ -484,8 +505,64 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     wave_sync();
     FSTAMP_ADD(3, f_t3);
     FSTAMP(f_t4);
-    // 5. subtree sums of the spatial inertias and (link - contact) forces, from the leaves up:
-    //    joint j's sum = its link's terms + its children's sums (16 accumulators per lane)
+    // 5. subtree sums of the spatial inertias and (link - contact) forces.  DFS-ordered models
+    //    (every subtree a contiguous run of joints, T.dfs): one inclusive prefix sum over the
+    //    joints' link terms per component, subtree_j = prefix[last_j] - prefix[j - 1], the base's
+    //    = prefix[n - 1] + its own link terms: 5-6 shuffle levels instead of one LDS round trip
+    //    and wave sync per tree level.  Other orders: level by level from the leaves up.
+    if (T.dfs) {
+        const int src = lane > 0 ? lane - 1 : 0;
+        constexpr int G = 4;   // components per group (registers)
+#pragma unroll
+        for (int g = 0; g < kComp; g += G) {
+            double v[G], pre[G];
+#pragma unroll
+            for (int q = 0; q < G; ++q) v[q] = jl ? S.link()[kLinkRec * (lane + 1) + kSI + g + q] : 0.0;
+            for (int c = 0; c < ct.C; ++c) {
+                const double* sc = S.cscr() + kCs * c;
+                if (jl && (int)sc[9] == lane + 1)
+#pragma unroll
+                    for (int q = 0; q < G; ++q)
+                        if (g + q >= 10) v[q] = v[q] - sc[g + q];
+            }
+#pragma unroll
+            for (int q = 0; q < G; ++q) pre[q] = v[q];
+            // inclusive prefix over the half's lanes by DPP (VALU moves, no LDS round trip): row
+            // shifts 1, 2, 4, 8 inside each row of 16, then rows 1 / 3 add lane 15 of rows 0 / 2
+            // (for HW = 64 also rows 2, 3 add lane 31) -- the QP kernels' forward tree levels
+            const int wl = (int)threadIdx.x;
+            auto level = [&](auto Lc) {
+                constexpr int L = decltype(Lc)::value;
+#pragma unroll
+                for (int q = 0; q < G; ++q) {
+                    const double t = qp::tree_fwd<L>(pre[q]);
+                    if (qp::tree_has<L, true>(wl)) pre[q] = pre[q] + t;
+                }
+            };
+            level(std::integral_constant<int, 0>{});
+            level(std::integral_constant<int, 1>{});
+            level(std::integral_constant<int, 2>{});
+            level(std::integral_constant<int, 3>{});
+            level(std::integral_constant<int, 4>{});
+            if constexpr (HW == 64) level(std::integral_constant<int, 5>{});
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+                const double atl = __shfl(pre[q], T.last, HW);
+                const double bef = __shfl(pre[q], src, HW);
+                const double tot = __shfl(pre[q], n - 1, HW);
+                if (jl) S.comp()[kCompS * lane + g + q] = lane > 0 ? atl - bef : atl;
+                if (lane == 0) {
+                    double b = S.link()[kSI + g + q] + tot;
+                    for (int c = 0; c < ct.C; ++c) {
+                        const double* sc = S.cscr() + kCs * c;
+                        if (g + q >= 10 && (int)sc[9] == 0) b = b - sc[g + q];
+                    }
+                    S.comp()[kCompS * n + g + q] = b;
+                }
+            }
+        }
+        wave_sync();
+    } else
     for (int lev = maxdepth; lev >= -1; --lev) {
         const bool mine = lev >= 0 ? (jl && depth == lev) : lane == 0;
         if (mine) {
@@ -527,7 +604,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             cross3(pB, w, u);
         } else {
             const int j = c - 6;
-            if (m.jtype && m.jtype[j] == BLF_JOINT_PRISMATIC) {   // S = (0; z): a pure translation
+            if (PRI && m.jtype[j] == BLF_JOINT_PRISMATIC) {   // S = (0; z): a pure translation
                 for (int a = 0; a < 3; ++a) u[a] = S.jz()[3 * j + a];
             } else {
                 for (int a = 0; a < 3; ++a) w[a] = S.jz()[3 * j + a];
@@ -697,7 +774,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     return ok;
 }
 
-template <int NVMAX, int HW>
+template <int NVMAX, int HW, bool PRI>
 __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state st,
                                                           const double* __restrict__ tau,
                                                           Contacts ct, const double* reg,
@@ -725,7 +802,7 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
     }
     wave_sync();
     const Topo T = build_topo<HW>(m, S);
-    const bool ok = fbd_eval<NVMAX, HW>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+    const bool ok = fbd_eval<NVMAX, HW, PRI>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                         tau + (int64_t)n * q, ct, q, reg, T);
     if (!active) return;
     const double nan = __builtin_nan("");
@@ -749,7 +826,7 @@ struct Impedance {
     const double *kp, *kd, *qref;
 };
 
-template <int NVMAX, int HW>
+template <int NVMAX, int HW, bool PRI>
 // Two systems per wavefront (HW = 32) keep more state live per wave: capping it at 256 VGPRs for
 // two waves per SIMD spills (9.40 ms per c5 period), one wave per SIMD does not (8.29 ms, against
 // 9.29 ms with one system per wavefront at two waves per SIMD; tools/ab_c5.sh).
@@ -790,7 +867,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
             wave_sync();
             tq = S.tq();
         }
-        ok = fbd_eval<NVMAX, HW>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+        ok = fbd_eval<NVMAX, HW, PRI>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                  tq, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         wave_sync();
@@ -824,6 +901,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
 //   xi = c_xy + cdot_xy / omega_0
 // (the LIP's divergent component with the plan's first-knot omega).  One wavefront per system:
 // the forward kinematics of fbd_eval, then lane per link and one wave sum per quantity.
+template <bool PRI>
 __global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, const double* __restrict__ omega0,
                                                     int64_t ostride, double* __restrict__ com,
                                                     double* __restrict__ xi)
@@ -845,7 +923,7 @@ __global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, co
     }
     wave_sync();
     const Topo T = build_topo<kWave>(m, S);
-    fbd_kinematics<kWave>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n, T);
+    fbd_kinematics<kWave, PRI>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n, T);
     wave_sync();
     double a[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // m c (3), m cdot (3), m
     if (lane < L) {
@@ -940,12 +1018,15 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
     if (batch == 0) return BLF_OK;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
+    const bool pri = md->joint_type != nullptr;
     if (md->ndof + 6 <= 32)   // two systems per wavefront
-        hipLaunchKernelGGL((fbd_dynamics_kernel<32, 32>), dim3((unsigned)ceil_div(batch, 2)), dim3(kWave),
-                           2 * lds, s, to_model(md), *st, tau, c, reg, *out, batch);
+        hipLaunchKernelGGL((pri ? fbd_dynamics_kernel<32, 32, true> : fbd_dynamics_kernel<32, 32, false>),
+                           dim3((unsigned)ceil_div(batch, 2)), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
+                           reg, *out, batch);
     else
-        hipLaunchKernelGGL((fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6, kWave>), dim3((unsigned)batch),
-                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, *out, batch);
+        hipLaunchKernelGGL((pri ? fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6, kWave, true>
+                                : fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6, kWave, false>),
+                           dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, *out, batch);
     return check_hip(hipGetLastError(), "fbd_dynamics_kernel launch");
 }
 
@@ -962,16 +1043,20 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
 #ifndef BLF_FBD_SMALL_HW
 #define BLF_FBD_SMALL_HW 32   // diagnostic builds: 64 = one small model per wavefront (A/B)
 #endif
+    const bool pri = md->joint_type != nullptr;
     if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
-        hipLaunchKernelGGL((fbd_euler_kernel<32, 32>), dim3((unsigned)ceil_div(batch, 2)), dim3(kWave),
-                           2 * lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp, batch);
+        hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true> : fbd_euler_kernel<32, 32, false>),
+                           dim3((unsigned)ceil_div(batch, 2)), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
+                           reg, nsteps, dT, dT_last, imp, batch);
     else if (md->ndof + 6 <= 32)   // one system per wavefront, NV <= 32 rows
-        hipLaunchKernelGGL((fbd_euler_kernel<32, kWave>), dim3((unsigned)batch), dim3(kWave), lds, s,
-                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp, batch);
+        hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, kWave, true> : fbd_euler_kernel<32, kWave, false>),
+                           dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
+                           dT_last, imp, batch);
     else
-        hipLaunchKernelGGL((fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave>), dim3((unsigned)batch),
-                           dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT, dT_last,
-                           imp, batch);
+        hipLaunchKernelGGL((pri ? fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, true>
+                                : fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, false>),
+                           dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
+                           dT_last, imp, batch);
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
 }
 
@@ -980,7 +1065,8 @@ blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const d
 {
     if (batch == 0) return BLF_OK;
     const size_t lds = fbd_lds_bytes(md->ndof, 0);
-    hipLaunchKernelGGL(fb_dcm_kernel, dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st,
+    hipLaunchKernelGGL((md->joint_type ? fb_dcm_kernel<true> : fb_dcm_kernel<false>), dim3((unsigned)batch),
+                       dim3(kWave), lds, s, to_model(md), *st,
                        omega0, ostride, com, xi);
     return check_hip(hipGetLastError(), "fb_dcm_kernel launch");
 }
