@@ -74,7 +74,10 @@ __device__ __forceinline__ int hull2d_rows(int64_t batch, int64_t p0)
 // only on a pop).  Phase 2 (after a barrier): consecutive threads take consecutive (polygon, facet) pairs,
 // compute the facet once and store A as 16-B and b as 8-B coalesced writes.
 template <bool PK>
-__global__ __launch_bounds__(kHullBlock) void hull2d_kernel(const double* __restrict__ pts,
+#ifndef BLF_HULL_MINWAVES   // waves per SIMD the register allocation must allow (A/B builds)
+#define BLF_HULL_MINWAVES 1
+#endif
+__global__ __launch_bounds__(kHullBlock, BLF_HULL_MINWAVES) void hull2d_kernel(const double* __restrict__ pts,
                                                             const int32_t* __restrict__ npts,
                                                             int32_t P, int32_t M, int64_t batch,
                                                             double* __restrict__ Aout,
