@@ -29,7 +29,8 @@
 
 namespace blf
 {
-/** Kinematic tree of revolute joints on a floating base (see blf_fb_model in blf_c.h). */
+/** Kinematic tree of revolute, prismatic (jointType) and fixed (fixedJoint) joints on a floating
+ *  base (see blf_fb_model in blf_c.h). */
 struct RobotModel
 {
     int ndof{0};

@@ -25,7 +25,9 @@
  * Layout: x [batch][n] (updated in place), u [batch][m], params [batch] (or one shared Params
  * when params_shared != 0).  One lane per system; x_r <- x_r + dx_r * h after every step (no FMA
  * contraction: build the user TU with -ffp-contract=off for results that match a CPU restatement
- * bit for bit).  Returns the C ABI's status codes (blf_c.h). */
+ * bit for bit).  Returns the C ABI's status codes (blf_c.h): the schedule's errors (with
+ * blf_last_error() set), BLF_ERR_INVALID_ARGUMENT for null buffers or a negative batch, and
+ * BLF_ERR_HIP when the launch fails (hipGetLastError() holds the cause). */
 #pragma once
 #include <hip/hip_runtime.h>
 
