@@ -190,7 +190,8 @@ def test_fbd_prismatic_joints_vs_oracle(handle, HWkind):
         extra = 4
         n0 = model["n"]
         model["n"] = n0 + extra
-        model["parent"] = np.concatenate([model["parent"], np.arange(n0 + 1 - 1, n0 + extra) * 0 + 13]).astype(np.int32)
+        torso = model["names"].index("torso_pitch")   # the extra leaves hang off the torso link
+        model["parent"] = np.concatenate([model["parent"], np.full(extra, torso)]).astype(np.int32)
         model["joint_origin"] = np.concatenate([model["joint_origin"], np.tile([[0.0, 0.01, 0.05]], (extra, 1))])
         model["joint_rot"] = np.concatenate([model["joint_rot"], np.tile(np.eye(3), (extra, 1, 1))])
         model["joint_axis"] = np.concatenate([model["joint_axis"], np.tile([[0.0, 0.0, 1.0]], (extra, 1))])
