@@ -35,12 +35,25 @@ def main(which):
         co = h.quintic_fit(kt, rnd(S, 3, 3, 3))
         tq = (kt[:, :1] + (kt[:, 2:] - kt[:, :1]) * rnd(S, Q)).contiguous()
         fn = lambda: h.quintic_eval(kt, co, tq)
-    elif which == "fbd_euler":
+    elif which in ("fbd_euler", "fbd_euler_big"):
         import numpy as np
         from blf import closed_loop as DL
         from blf import robot as R
         B = int(os.environ.get("FBD_BATCH", 16384))
         model = R.humanoid24()
+        if which == "fbd_euler_big":   # 4 extra leaf joints on the torso: NV = 34, one system per wavefront
+            model = dict(model)
+            n0, extra = model["n"], 4
+            torso = model["names"].index("torso_pitch")
+            model["n"] = n0 + extra
+            model["parent"] = np.concatenate([model["parent"], np.full(extra, torso)]).astype(np.int32)
+            model["joint_origin"] = np.concatenate([model["joint_origin"], np.tile([[0.0, 0.01, 0.05]], (extra, 1))])
+            model["joint_rot"] = np.concatenate([model["joint_rot"], np.tile(np.eye(3), (extra, 1, 1))])
+            model["joint_axis"] = np.concatenate([model["joint_axis"], np.tile([[0.0, 0.0, 1.0]], (extra, 1))])
+            model["link_mass"] = np.concatenate([model["link_mass"], np.full(extra, 0.3)])
+            model["link_com"] = np.concatenate([model["link_com"], np.zeros((extra, 3))])
+            model["link_inertia"] = np.concatenate([model["link_inertia"], np.tile(np.eye(3) * 1e-3, (extra, 1, 1))])
+            model["names"] = list(model["names"]) + [f"extra{i}" for i in range(extra)]
         st = R.standing_states(model, B, seed=1000)
         law = R.posture_law_arrays(model)
         t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
