@@ -38,22 +38,28 @@ def algorithmic_bytes_per_qp(N, M):
 
 def profiled_summary():
     """The newest committed rocprofv3 summary of the dominant kernel (profiles/*_summary.json,
-    written by tools/summarize_profile.py from separate FETCH_SIZE / WRITE_SIZE / SQ passes);
-    bench.py cannot read PMC counters itself.  Returns (summary, path) or (None, None)."""
+    written by tools/summarize_profile.py from separate FETCH_SIZE / WRITE_SIZE / SQ passes) whose
+    recorded build is the library this process loaded (lib_src_hash equal to
+    native.build_provenance()'s); bench.py cannot read PMC counters itself.  Counters of another
+    build describe other code, so without a match the counter-derived fields are null.
+    Returns (summary, path) or (None, None)."""
     import glob
     import re
+    from blf import native
+    lib_hash = native.build_provenance().get("lib_src_hash")
     # newest by name (profiles/rNN_vMM_<tag>_summary.json; file times do not survive the copy to a
     # box), numbers compared as numbers so v10 sorts after v9
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")),
                    key=lambda f: [int(t) if t.isdigit() else t
                                   for t in re.split(r"(\d+)", os.path.basename(f))])
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        s = json.load(f)
-    if "dcm_mpc_" not in s.get("dominant_kernel", ""):   # the QP kernels (cold / warm / ipm)
-        return None, None
-    return s, os.path.relpath(files[-1], ROOT)
+    for path in reversed(files):
+        with open(path) as f:
+            s = json.load(f)
+        if "dcm_mpc_" not in s.get("dominant_kernel", ""):   # the QP kernels (cold / warm / ipm)
+            continue
+        if lib_hash and (s.get("build") or {}).get("lib_src_hash") == lib_hash:
+            return s, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def profiled_traffic():

@@ -752,11 +752,15 @@ __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const R
     const T l2 = pc == 2 ? fma(a.x, g1, -(g0 * a.y)) * qd : T(0);
     l1o = l1;
     l2o = l2;
+    // fp64: the dual tolerance relative to |beta nu| beyond 1 / kTolDualRel (oracle dcm_polish);
+    // the fp32 search keeps its absolute kSearchTolD
+    T tol_d = P.tol_d;
+    if constexpr (sizeof(T) == 8) tol_d = P.tol_d * fmax(1.0, kTolDualRel * fmax(fabs(K.be * nu0), fabs(K.be * nu1)));
     bool bad = false;
-    if (pc == 0) bad = !(fabs(g0) <= P.tol_d) || !(fabs(g1) <= P.tol_d);
-    if (pc == 1) bad = !(fabs(fma(-l1, a.x, g0)) <= P.tol_d) || !(fabs(fma(-l1, a.y, g1)) <= P.tol_d);
-    const bool n1 = pc >= 1 && !(l1 >= -P.tol_d);
-    const bool n2 = pc == 2 && !(l2 >= -P.tol_d);
+    if (pc == 0) bad = !(fabs(g0) <= tol_d) || !(fabs(g1) <= tol_d);
+    if (pc == 1) bad = !(fabs(fma(-l1, a.x, g0)) <= tol_d) || !(fabs(fma(-l1, a.y, g1)) <= tol_d);
+    const bool n1 = pc >= 1 && !(l1 >= -tol_d);
+    const bool n2 = pc == 2 && !(l2 >= -tol_d);
     const int dm = (n1 ? 1 << pi1 : 0) | (n2 ? 1 << pi2 : 0);
     if (bad || dm) okp = false;
     if (dm) neg = true;

@@ -556,6 +556,209 @@ __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, doubl
     dr1 = fma(ab, FD2(Mm.m01, xk0, Mm.m11, xk1), k1);
 }
 
+// The saturated LQ start of the interior point method (oracle dcm_saturated_start, DESIGN.md 4
+// item 9), run when the active-set start did not certify (tol_polish > 0): the LQ policy around the
+// current iterate, rolled out from xi_init with every VRP projected onto its support polygon in the
+// one-step Hessian's metric, costates of the rollout by single shooting, multipliers of the
+// projected facets from stationarity, s = max(b - A r, 1e-2), lam = max(estimate, 1e-2 / s).
+// The rollout is sequential over the knots: wavefront w takes its 64 knots in turn (the others
+// wait at a barrier), each knot's policy data broadcast from its lane by v_readlane and its
+// projection candidates (8 single facets, 28 facet pairs) evaluated one per lane, the lowest lane
+// of the least B-distance winning (oracle sat_project's candidate order).  Leaves r, xi, s, lam,
+// the residuals and xb in place; returns mu, pres, dres, and false on a lane whose LQ factorization
+// failed.
+#ifndef BLF_SAT_ON
+#define BLF_SAT_ON 1
+#endif
+constexpr int kBS = 12;   // bnd slot: the rollout's xi at the end of wavefront w
+template <int NW>
+__device__ __forceinline__ bool sat_start(Knot& K, const KParams& P, const Lds& L, Reduce<NW>& R, double* bnd,
+                                          int N, int nwa, int k, int wv, int lane, bool own, bool last,
+                                          int mmax, double xi00, double xi01, const double* rref,
+                                          const double* xref, double& xb0, double& xb1, double& mu,
+                                          double& pres, double& dres)
+{
+    // 1. the LQ step around the current iterate: the LQ optimum (r*, xi*) and its policy
+    double xk0, xk1, pd, cd;
+    xi_prev(K, lane, xb0, xb1, xk0, xk1);
+    if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
+    const bool ok = factor<NW>(K, P, 0.0, 0.0, 0.0, 0.0, bnd, N, nwa, k, wv, lane, own);
+    double dr0, dr1, dx0, dx1, vn0, vn1, dxk0, dxk1;
+    solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1, dxk0, dxk1);
+    const double rs0 = K.r0 + dr0, rs1 = K.r1 + dr1;       // r*_k
+    const double xs0 = xk0 + dxk0, xs1 = xk1 + dxk1;       // xi*_k
+    const Mmat Mm(K);
+    const double ab = K.al * K.be;
+    const double b2 = K.be * K.be;
+    const double B00 = fma(b2, K.P00, P.Rw0);
+    const double B01 = b2 * K.P01;
+    const double B11 = fma(b2, K.P11, P.Rw1);
+    // this lane's projection candidate: lanes 0..7 facet `lane`, lanes 8..35 the facet pair
+    // (cx, cy), cx < cy, in lexicographic order
+    int cx = lane, cy = lane;
+    if (lane >= kMaxFacets) {
+        int q = lane - kMaxFacets;
+        cx = 0;
+        while (cx < kMaxFacets - 1 && q >= kMaxFacets - 1 - cx) { q -= kMaxFacets - 1 - cx; ++cx; }
+        cy = cx + 1 + q;
+    }
+    const bool pair_lane = lane >= kMaxFacets && lane < kMaxFacets + kMaxFacets * (kMaxFacets - 1) / 2;
+    // 2. the rollout
+    int sc = 0, s1 = 0, s2 = 0;   // this knot's projected facets
+    for (int w = 0; w < nwa; ++w) {
+        if (wv == w) {
+            double x0 = xi00, x1 = xi01;
+            if (w > 0) {
+                x0 = bnd[kBnd * (w - 1) + kBS];
+                x1 = bnd[kBnd * (w - 1) + kBS + 1];
+            }
+            xb0 = x0;
+            xb1 = x1;
+            const int jn = N - kWave * w < kWave ? N - kWave * w : kWave;
+            for (int j = 0; j < jn; ++j) {
+                const int kk = kWave * w + j;
+                const int m = __builtin_amdgcn_readlane(K.m, j);
+                const double d0 = x0 - readlane_f64(xs0, j), d1 = x1 - readlane_f64(xs1, j);
+                const double abj = readlane_f64(ab, j);
+                const double t0 = fma(abj, FD2(readlane_f64(Mm.m00, j), d0, readlane_f64(Mm.m10, j), d1),
+                                      readlane_f64(rs0, j));
+                const double t1 = fma(abj, FD2(readlane_f64(Mm.m01, j), d0, readlane_f64(Mm.m11, j), d1),
+                                      readlane_f64(rs1, j));
+                const double c00 = readlane_f64(B00, j), c01 = readlane_f64(B01, j), c11 = readlane_f64(B11, j);
+                bool inside = true;
+                for (int i = 0; i < m; ++i) {
+                    const double2 a = L.A2[i * N + kk];
+                    if (!(FD2(a.x, t0, a.y, t1) - L.BI[i * N + kk].x <= 0.0)) inside = false;
+                }
+                double r0 = t0, r1 = t1;
+                int c = 0, i1 = 0, i2 = 0;
+                if (!inside) {
+                    bool valid = false;
+                    double v0 = 0.0, v1 = 0.0, dist = 0.0;
+                    if (lane < m) {
+                        const double2 a = L.A2[lane * N + kk];
+                        const double u0 = fma(c11, a.x, -(c01 * a.y));
+                        const double u1 = fma(c00, a.y, -(c01 * a.x));
+                        const double aua = FD2(a.x, u0, a.y, u1);
+                        const double viol = FD2(a.x, t0, a.y, t1) - L.BI[lane * N + kk].x;
+                        const double t = viol / aua;
+                        v0 = fma(-t, u0, t0);
+                        v1 = fma(-t, u1, t1);
+                        valid = viol > 0.0;
+                        dist = (t * viol) * fma(c00, c11, -(c01 * c01));
+                    } else if (pair_lane && cy < m) {
+                        const double2 a = L.A2[cx * N + kk];
+                        const double2 e = L.A2[cy * N + kk];
+                        const double ba = L.BI[cx * N + kk].x, be = L.BI[cy * N + kk].x;
+                        const double det = fma(a.x, e.y, -(a.y * e.x));
+                        const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
+                        valid = det * det > 1e-18 * (aa * ee);
+                        const double idet = 1.0 / det;
+                        v0 = fma(ba, e.y, -(a.y * be)) * idet;
+                        v1 = fma(a.x, be, -(ba * e.x)) * idet;
+                        const double e0 = v0 - t0, e1 = v1 - t1;
+                        dist = fma(e0, fma(c00, e0, 2.0 * (c01 * e1)), (c11 * e1) * e1);
+                    }
+                    if (valid) {
+                        for (int l = 0; l < m; ++l) {
+                            const double2 f = L.A2[l * N + kk];
+                            if (!(FD2(f.x, v0, f.y, v1) - L.BI[l * N + kk].x <= P.tol_p)) valid = false;
+                        }
+                    }
+                    if (!(dist == dist)) valid = false;
+                    const double key = valid ? dist : __builtin_inf();
+                    const double kmin = wave_keepmin(key);
+                    const unsigned long long win = __ballot(valid && key == kmin);
+                    if (win != 0ull) {
+                        const int f = __builtin_ctzll(win);
+                        r0 = readlane_f64(v0, f);
+                        r1 = readlane_f64(v1, f);
+                        i1 = __builtin_amdgcn_readlane(cx, f);
+                        i2 = __builtin_amdgcn_readlane(cy, f);
+                        c = f < kMaxFacets ? 1 : 2;
+                    }
+                }
+                const double om = readlane_f64(K.w, j);
+                const double y0 = fma(FD2(om, x0, -om, r0), P.dt, x0);
+                const double y1 = fma(FD2(om, x1, -om, r1), P.dt, x1);
+                if (lane == j) {
+                    K.r0 = r0;
+                    K.r1 = r1;
+                    K.x0 = y0;
+                    K.x1 = y1;
+                    sc = c;
+                    s1 = i1;
+                    s2 = i2;
+                }
+                x0 = y0;
+                x1 = y1;
+            }
+            if (lane == 0) {
+                bnd[kBnd * w + kBS] = x0;
+                bnd[kBnd * w + kBS + 1] = x1;
+            }
+        }
+        if (w < nwa - 1) __syncthreads();
+    }
+    // 3. costates of the rollout (the warm start's backward scan), multiplier estimates, s, lam
+    xi_prev(K, lane, xb0, xb1, xk0, xk1);
+    if (own) residuals(K, false, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
+    {
+        const double ga = own ? K.al : 0.0;
+        const double c0 = own ? K.al * K.qx0 : 0.0, c1 = own ? K.al * K.qx1 : 0.0;
+        scan_backward<NW>(ga, 0.0, 0.0, ga, c0, c1, bnd, nwa, wv, lane, vn0, vn1);
+    }
+    dres = 0.0;
+    if (own) {
+        const int kx = opaque(k);
+        const double nu0 = K.qx0 + vn0;
+        const double nu1 = K.qx1 + vn1;
+        const double g0 = fma(K.be, nu0, -K.rh0);
+        const double g1 = fma(K.be, nu1, -K.rh1);
+        double l1 = 0.0, l2 = 0.0;
+        if (sc == 1) {
+            const double2 a = L.A2[s1 * N + kx];
+            l1 = FD2(a.x, g0, a.y, g1) / FD2(a.x, a.x, a.y, a.y);
+        } else if (sc == 2) {
+            const double2 a = L.A2[s1 * N + kx];
+            const double2 e = L.A2[s2 * N + kx];
+            const double idet = 1.0 / fma(a.x, e.y, -(a.y * e.x));
+            l1 = fma(g0, e.y, -(e.x * g1)) * idet;
+            l2 = fma(a.x, g1, -(g0 * a.y)) * idet;
+        }
+        double al0 = 0.0, al1 = 0.0;
+        const int km = opaque(K.m);
+        // every slot written (the unused ones to their initial 1 / 0), so the old values are dead
+        // during the rollout
+#pragma unroll
+        for (int i = 0; i < kMaxFacets; ++i) {
+            K.s[i] = 1.0;
+            K.lam[i] = 0.0;
+            if (i < km) {
+                const double2 a = L.A2[i * N + kx];
+                const double sl = L.BI[i * N + kx].x - FD2(a.x, K.r0, a.y, K.r1);
+                const double si = sl > 1e-2 ? sl : 1e-2;
+                const double est = (sc >= 1 && i == s1) ? l1 : (sc == 2 && i == s2) ? l2 : 0.0;
+                const double lc = 1e-2 / si;
+                K.s[i] = si;
+                K.lam[i] = est > lc ? est : lc;
+                al0 = fma(a.x, K.lam[i], al0);
+                al1 = fma(a.y, K.lam[i], al1);
+            }
+        }
+        dres = nanmax(nanmax(0.0, fabs(al0 - g0)), fabs(al1 - g1));
+    }
+    // 4. mu and the primal residual at the new point, in one reduction with dres
+    pres = 0.0;
+    double ck = 0.0;
+    if (own) residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pres, ck);
+    double mcount = (double)K.m;
+    R.sums_nanmaxes(mcount, ck, pres, dres);
+    const int ntot = (int)mcount;
+    mu = ntot > 0 ? ck / (double)ntot : 0.0;
+    return ok;
+}
+
 #ifndef BLF_MIN_WAVES
 #define BLF_MIN_WAVES 3   // waves per SIMD the register allocation must allow (<= 168 VGPRs)
 #endif
@@ -777,7 +980,20 @@ __device__ __forceinline__ void ipm_solve(
         // active-set start (oracle: before its IPM loop): the first polish runs before any IPM
         // iteration from the guess gm, with up to kGuessPasses drop/add passes
         bool guess = P.tol_polish > 0.0 && !P.stage2;
+        // the interior point method starts from the saturated LQ start (sat_start) when an
+        // active-set start failed: the kernel's own (guess), or the active-set kernel's (stage 2)
+        bool sat_pending = P.tol_polish > 0.0 && P.stage2;
         for (it = 0; status == 0; ++it) {
+            if (BLF_SAT_ON && sat_pending) {
+                sat_pending = false;
+                const bool oks = sat_start<NW>(K, P, L, R, bnd, N, nwa, k, wv, lane, own, last, mmax, xi00, xi01,
+                                               rref, xref, xb0, xb1, mu, pres, dres);
+                if (__syncthreads_or(!oks)) {
+                    status = BLF_QP_NUMERICAL;
+                    it = 0;
+                    break;
+                }
+            }
             // ---- residuals (knot-parallel) ----
             STAMP(t_r);
             xi_prev(K, lane, xb0, xb1, xk0, xk1);
@@ -806,10 +1022,19 @@ __device__ __forceinline__ void ipm_solve(
                     const int km = opaque(K.m), mm = opaque_s(mmax);
                     const int dm = opaque(drop), am = opaque(add), gk = opaque(gm);
                     int cm = 0;   // the pass's active-set candidates (bit i: facet i)
+                    double lmx = 0.0;   // the knot's largest multiplier (the IPM guess's scale)
+                    if (!guess) {
+#pragma unroll
+                        for (int i = 0; i < kMaxFacets; ++i) {
+                            if (i >= mm) break;
+                            if (i < km) lmx = keepmax(lmx, K.lam[i]);
+                        }
+                    }
 #pragma unroll
                     for (int i = 0; i < kMaxFacets; ++i) {
                         if (i >= mm) break;
-                        const bool base = guess ? ((gk >> i) & 1) != 0 : K.lam[i] > K.s[i];
+                        const bool base = guess ? ((gk >> i) & 1) != 0
+                                                : (K.lam[i] > K.s[i] && K.lam[i] >= kLamRel * lmx);
                         if (i < km && ((base && !((dm >> i) & 1)) || ((am >> i) & 1))) {
                             if (pc == 0) pi1 = i;
                             else if (pc == 1) pi2 = i;
@@ -885,6 +1110,7 @@ __device__ __forceinline__ void ipm_solve(
                     }
                 }
                 double pl1 = 0.0, pl2 = 0.0;
+                double vmx = 0.0;   // this knot's largest violation (the IPM polish's add threshold)
                 {
                     // the Newton step; then the certificate: costates of the new point from the
                     // solve, nu_k = P_{k+1} dxi_{k+1} + (qx_k + v_{k+1}) (oracle dcm_polish step 6)
@@ -907,18 +1133,21 @@ __device__ __forceinline__ void ipm_solve(
                         const double rh1 = P.Rw1 * (K.r1 - rref[1]);
                         const double g0 = fma(K.be, nu0, -rh0);
                         const double g1 = fma(K.be, nu1, -rh1);
+                        // the dual tolerance relative to |beta nu| beyond 1 / kTolDualRel
+                        const double tol_d =
+                            P.tol_d * fmax(1.0, kTolDualRel * fmax(fabs(K.be * nu0), fabs(K.be * nu1)));
                         if (pc == 0) {
-                            if (!(fabs(g0) <= P.tol_d) || !(fabs(g1) <= P.tol_d)) okp = false;
+                            if (!(fabs(g0) <= tol_d) || !(fabs(g1) <= tol_d)) okp = false;
                         } else if (pc == 1) {
                             const double2 a = L.A2[pi1 * N + kx];
                             pl1 = FD2(a.x, g0, a.y, g1) / FD2(a.x, a.x, a.y, a.y);
-                            if (!(pl1 >= -P.tol_d)) {
+                            if (!(pl1 >= -tol_d)) {
                                 okp = false;
                                 neg = true;
                                 drop |= 1 << pi1;
                                 add &= ~(1 << pi1);
                             }
-                            if (!(fabs(fma(-pl1, a.x, g0)) <= P.tol_d) || !(fabs(fma(-pl1, a.y, g1)) <= P.tol_d))
+                            if (!(fabs(fma(-pl1, a.x, g0)) <= tol_d) || !(fabs(fma(-pl1, a.y, g1)) <= tol_d))
                                 okp = false;
                         } else {
                             const double2 a = L.A2[pi1 * N + kx];
@@ -926,13 +1155,13 @@ __device__ __forceinline__ void ipm_solve(
                             const double idet = 1.0 / fma(a.x, e.y, -(a.y * e.x));
                             pl1 = fma(g0, e.y, -(e.x * g1)) * idet;
                             pl2 = fma(a.x, g1, -(g0 * a.y)) * idet;
-                            if (!(pl1 >= -P.tol_d)) {
+                            if (!(pl1 >= -tol_d)) {
                                 okp = false;
                                 neg = true;
                                 drop |= 1 << pi1;
                                 add &= ~(1 << pi1);
                             }
-                            if (!(pl2 >= -P.tol_d)) {
+                            if (!(pl2 >= -tol_d)) {
                                 okp = false;
                                 neg = true;
                                 drop |= 1 << pi2;
@@ -955,14 +1184,19 @@ __device__ __forceinline__ void ipm_solve(
                                 bv[j] = L.BI[i * N + kx].x;
                             }
 #pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                if (!(FD2(av[j].x, K.r0, av[j].y, K.r1) - bv[j] <= P.tol_p)) vm |= 1 << (i0 + j);
+                            for (int j = 0; j < 4; ++j) {
+                                const double vi = FD2(av[j].x, K.r0, av[j].y, K.r1) - bv[j];
+                                if (!(vi <= P.tol_p) && i0 + j < km) {
+                                    vm |= 1 << (i0 + j);
+                                    vmx = nanmax(vmx, vi);
+                                }
+                            }
                         }
                         vm &= (1 << (km < mm ? km : mm)) - 1;
                         if (vm) {
                             okp = false;
                             viol = true;
-                            if (pass >= 1 || guess) {
+                            if (guess) {
                                 add |= vm;
                                 drop &= ~vm;
                             }
@@ -972,6 +1206,27 @@ __device__ __forceinline__ void ipm_solve(
                 const int fl = R.template or_bits<4>((okp ? 0 : 1) | (neg || viol ? 2 : 0) |
                                                      (neg ? 4 : 0) | (viol ? 8 : 0));
                 const bool rejected = (fl & 1) != 0;
+                if (!guess && (fl & 8) != 0) {
+                    // the IPM polish adds only the facets violated by >= kAddRel x the pass's
+                    // largest violation (oracle dcm_polish)
+                    const double thr = kAddRel * R.nanmax_(vmx);
+                    if (own) {
+                        const int kx = opaque(k);
+                        const int km = opaque(K.m), mm = opaque_s(mmax);
+#pragma unroll
+                        for (int i = 0; i < kMaxFacets; ++i) {
+                            if (i >= mm) break;
+                            if (i < km) {
+                                const double2 a = L.A2[i * N + kx];
+                                const double vi = FD2(a.x, K.r0, a.y, K.r1) - L.BI[i * N + kx].x;
+                                if (vi > P.tol_p && vi >= thr) {
+                                    add |= 1 << i;
+                                    drop &= ~(1 << i);
+                                }
+                            }
+                        }
+                    }
+                }
                 STAMP_ADD(8, t_p);
 #ifdef BLF_STAMPS
                 if (blockIdx.x < 64 && threadIdx.x == 0) atomicAdd(&g_blf_stamps[9], 1ull);
@@ -991,14 +1246,13 @@ __device__ __forceinline__ void ipm_solve(
                 K.r1 = sr1;
                 K.x0 = sx0;
                 K.x1 = sx1;
-                const bool more = guess ? (pass + 1 < kGuessPasses && (fl & 2) != 0)
-                                        : ((pass == 0 && (fl & 4) != 0) || (pass == 1 && (fl & 8) != 0));
+                const bool more = pass + 1 < kGuessPasses && (fl & 2) != 0;
                 if (more) {
-                    // IPM polish, pass 1: the same iterate without the facets whose multiplier came
-                    // out negative; pass 2: pass 1's set plus the facets it left violated.  Active-
-                    // set start: every pass drops the negative and adds the violated facets.  Each
-                    // runs this block again from the top of the loop (one copy of the polish code)
-                    // and does not count as an IPM iteration.
+                    // every further pass starts from the same iterate without the facets whose
+                    // multiplier came out negative and with the violated ones (the IPM polish: those
+                    // violated by >= kAddRel x the largest), up to kGuessPasses.  Each runs this
+                    // block again from the top of the loop (one copy of the polish code) and does
+                    // not count as an IPM iteration.
                     ++pass;
                     --it;
                     continue;
@@ -1013,8 +1267,9 @@ __device__ __forceinline__ void ipm_solve(
                     double pd, cd;
                     residuals(K, true, P, last, L.A2, L.BI, N, k, mmax, xk0, xk1, rref, xref, pd, cd);
                 }
-                if (guess) {   // the active-set start failed: the IPM takes over from the top
-                    guess = false;
+                if (guess) {   // the active-set start failed: the IPM takes over from the top,
+                    guess = false;   // from the saturated LQ start
+                    sat_pending = true;
                     --it;
                     continue;
                 }

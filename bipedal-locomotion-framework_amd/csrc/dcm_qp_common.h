@@ -33,6 +33,25 @@ constexpr float kSearchTolD = 1e-4f;
 // The fp64 passes' guess after the search: the facets whose slack at the float point is below
 // this (oracle ORC_GUESS_SLACK).
 constexpr double kGuessSlack = 1e-5;
+// The fp64 certificate's dual tolerance grows with the knot's costate force once
+// |beta nu| > 1 / kTolDualRel: tol_d max(1, kTolDualRel max |beta nu|) (oracle ORC_TOL_DUAL_REL).
+// A planned walk keeps |beta nu| below ~2, so only the QPs of uncapturable DCM states (|beta nu|
+// and the multipliers up to ~1e8, tests/golden/c5_hard_windows.npz) see a larger tolerance.
+constexpr double kTolDualRel = 1e-3;
+// The IPM polish's guess from an iterate: lam_i > s_i and lam_i >= kLamRel x the knot's largest
+// multiplier (oracle ORC_LAM_REL); it adds only the facets violated by >= kAddRel x the pass's
+// largest violation (oracle ORC_ADD_REL).
+constexpr double kLamRel = 1e-8;
+constexpr double kAddRel = 1e-2;
+
+// v_readlane of a double (lane l uniform)
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
 // The facet rows never change during a solve, so the compiler would hoist every phase's row loads
 // out of the IPM loop and keep 8 facets x 4 doubles live in VGPRs across it (spilling).  Each phase

@@ -636,6 +636,70 @@ static void testFloatingBaseKinematics()
     REQUIRE_FALSE(system->dynamics(0.0, dx));
 }
 
+// ---- IntegratorTest.cpp:77-126, "Floating base System Kinematics", restated literally ----------
+// Random twist and 20 joint velocities (Eigen setRandom: uniform in [-1, 1]; here a seeded
+// std::mt19937), identity rotation, zero position and joints, ForwardEuler at dT = 1e-4 called as
+// integrate(0, dT) once per step for simulationTime = 2 s, every step's solution isApprox
+// (Frobenius norms, Eigen's definition) the closed form at tolerance 1e-3: position p0 + t v,
+// rotation AngleAxis(|w| t, w / |w|) R0, joints s0 + t sdot.
+template <class A, class B>
+static bool isApprox(const A& a, const B& b, double prec)
+{
+    double d = 0.0, na = 0.0, nb = 0.0;
+    for (size_t i = 0; i < a.size(); ++i) {
+        d += (a[i] - b[i]) * (a[i] - b[i]);
+        na += a[i] * a[i];
+        nb += b[i] * b[i];
+    }
+    return d <= prec * prec * std::min(na, nb);
+}
+
+static void testIntegratorKinematicsLiteral()
+{
+    constexpr double dT = 0.0001;
+    constexpr double tolerance = 1e-3;
+    constexpr double simulationTime = 2;
+    auto system = std::make_shared<FloatingBaseSystemKinematics>();
+    std::mt19937 gen(20201015);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    blf::Vector6 twist;
+    for (auto& v : twist) v = U(gen);
+    blf::VectorXd jointVelocity(20);
+    for (std::size_t i = 0; i < jointVelocity.size(); ++i) jointVelocity[i] = U(gen);
+    const blf::Matrix3 rotation0{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    const blf::Vector3 position0{{0.0, 0.0, 0.0}};
+    const blf::VectorXd jointPosition0(20, 0.0);
+    const double wn = std::sqrt(twist[3] * twist[3] + twist[4] * twist[4] + twist[5] * twist[5]);
+    auto closeFormSolution = [&](double t, blf::Vector3& pos, blf::Matrix3& rot, blf::VectorXd& q) {
+        for (int i = 0; i < 3; ++i) pos[i] = position0[i] + t * twist[i];
+        // AngleAxis(|w| t, w / |w|) = exp(skew(w t))
+        rot = matmul(expSkew({{twist[3] / wn * (wn * t), twist[4] / wn * (wn * t), twist[5] / wn * (wn * t)}}),
+                     rotation0);
+        q.resize(20);
+        for (int i = 0; i < 20; ++i) q[i] = jointPosition0[i] + t * jointVelocity[i];
+    };
+    REQUIRE(system->setControlInput({twist, jointVelocity}));
+    REQUIRE(system->setState({position0, rotation0, jointPosition0}));
+    ForwardEuler<FloatingBaseSystemKinematics> integrator(dT);
+    REQUIRE(integrator.setDynamicalSystem(system));
+    int bad = 0, steps = 0;
+    for (int i = 0; i < simulationTime / dT; i++) {
+        const auto& [basePosition, baseRotation, jointPosition] = integrator.getSolution();
+        blf::Vector3 pe;
+        blf::Matrix3 Re;
+        blf::VectorXd qe;
+        closeFormSolution(dT * i, pe, Re, qe);
+        // one aggregate check per step, so a failure does not print 20 000 lines
+        if (!isApprox(baseRotation, Re, tolerance) || !isApprox(basePosition, pe, tolerance)
+            || !isApprox(jointPosition, qe, tolerance))
+            ++bad;
+        if (!integrator.integrate(0, dT)) ++bad;
+        ++steps;
+    }
+    REQUIRE(steps == 20000);
+    REQUIRE(bad == 0);
+}
+
 // ---- FloatingBaseDynamicalSystem (FloatingBaseSystemDynamics.cpp:102-251) on a 3-joint chain ---
 static blf::RobotModel chainModel()
 {
@@ -910,6 +974,7 @@ int main(int argc, char** argv)
         {"TimeVaryingDCMPlanner advance", true, testPlanner},
         {"Continuous Contact", true, testContinuousContact},
         {"FloatingBaseSystemKinematics", true, testFloatingBaseKinematics},
+        {"IntegratorTest: floating base kinematics (literal)", true, testIntegratorKinematicsLiteral},
         {"FloatingBaseDynamicalSystem", true, testFloatingBaseDynamics},
         {"Fixed joints (model merge)", false, testFixedJoints},
         {"Fixed / prismatic joints (device)", true, testFixedJointsDevice},

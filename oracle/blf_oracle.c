@@ -6,6 +6,7 @@
 #include "blf_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
@@ -468,7 +469,12 @@ double orc_wave_tree_sum(const double* c, int n)
 }
 
 #define MF 8
-#define ORC_GUESS_PASSES 8   /* active-set start: drop/add passes (kernel: kGuessPasses) */
+#ifndef ORC_GUESS_PASSES
+#define ORC_GUESS_PASSES 8    /* active-set start: drop/add passes (kernel: kGuessPasses) */
+#endif
+#define ORC_TOL_DUAL_REL 1e-3   /* the certificate's relative dual tolerance (kernel kTolDualRel) */
+#define ORC_LAM_REL 1e-8        /* the IPM polish's guess: lam_i >= this x the knot's largest (kernel kLamRel) */
+#define ORC_ADD_REL 1e-2        /* the IPM polish adds facets violated by >= this x the largest (kernel kAddRel) */
 #define ORC_GUESS_SLACK 1e-5  /* the fp64 passes' guess after the fp32 search (kernel: kGuessSlack) */
 #define WV 64
 
@@ -1411,13 +1417,22 @@ static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
  * and 1 is returned.  Rejected: xi, vrp are restored, 0 is returned. */
 /* Facet i of knot k is in a polish pass's active set: guessed (the active-set start's guess bits,
  * or an IPM iterate's lam_i > s_i) and not dropped, or added. */
+/* An IPM iterate's guess: lam_i > s_i, and lam_i at least ORC_LAM_REL (1e-8) of the knot's
+ * largest multiplier.  The second condition only matters where multipliers reach ~1e7 (the
+ * uncapturable-state windows, tests/golden/c5_hard_windows.npz): on an edge that meets a nearly
+ * parallel neighbour (support polygons of slightly rotated feet, facets 0.1 degree apart) the
+ * neighbour's slack is ~1e-5 while its multiplier is ~0.1, rounding-level against the edge's
+ * 1e6, and lam > s alone would put the knot on their ill-conditioned vertex. */
 static int cand_bit(const dcm_ws* w, const int* guess, const int* drop, const int* add, int k, int i)
 {
-    const int base = guess ? ((guess[k] >> i) & 1) : (w->lam[k * MF + i] > w->s[k * MF + i]);
+    double lmx = 0.0;
+    for (int j = 0; j < w->nf[k]; ++j) lmx = keepmax(lmx, w->lam[k * MF + j]);
+    const int base = guess ? ((guess[k] >> i) & 1)
+                           : (w->lam[k * MF + i] > w->s[k * MF + i] && w->lam[k * MF + i] >= ORC_LAM_REL * lmx);
     return (base && !((drop[k] >> i) & 1)) || ((add[k] >> i) & 1);
 }
 
-static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, int max_pass)
+static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, int max_pass)
 {
     const int N = w->N, M = w->M;
     int ok = 1;
@@ -1431,12 +1446,16 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, i
     memcpy(bak, w->vrp, sizeof(double) * 2 * N);
     memcpy(bak + 2 * N, w->xi, sizeof(double) * (2 * (size_t)N + 2));
     for (int k = 0; k < N; ++k) drop[k] = 0;
-    /* pass 0: the guessed active set; pass 1 (only if pass 0 found negative multipliers): the same
-     * set without those facets; pass 2 (only if pass 1 left facets violated): pass 1's set plus
-     * those facets.  Every pass starts from the same iterate. */
+    /* pass 0: the guessed active set; every further pass drops the facets whose multiplier came
+     * out negative and adds the facets left violated (a facet's drop and add bits are exclusive,
+     * the later event wins), up to max_pass passes.  Every pass starts from the same iterate.
+     * (Until round 3 the IPM's polish ran at most three passes: pass 1 only dropping, pass 2 only
+     * adding; the uncapturable-state windows of tests/golden/c5_hard_windows.npz need the
+     * alternating moves of the active-set start there too.) */
     for (int pass = 0; pass < max_pass; ++pass) {
     ok = 1;
     int neg = 0, viol = 0;
+    double vmax = 0.0;   /* the pass's largest violation (the IPM polish's add threshold) */
     /* 1. active sets, projection onto the active lines, E_k (knot-parallel) */
     for (int k = 0; k < N; ++k) {
         const int m = w->nf[k];
@@ -1560,6 +1579,11 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, i
         const double rh1 = w->Rw1 * (w->vrp[2 * k + 1] - w->vrp_ref[2 * k + 1]);
         const double g0 = fma(w->be[k], nu0, -rh0);
         const double g1 = fma(w->be[k], nu1, -rh1);
+        /* the dual tolerance grows with the knot's costate force beta nu once it exceeds
+         * 1 / ORC_TOL_DUAL_REL (1e3; a planned walk's |beta nu| stays below ~2): the rounding of
+         * nu grows with it, and the QPs of uncapturable DCM states carry |beta nu| and multipliers
+         * up to ~1e8 (tests/golden/c5_hard_windows.npz) */
+        const double tol_d = tol_dd * fmax(1.0, ORC_TOL_DUAL_REL * fmax(fabs(w->be[k] * nu0), fabs(w->be[k] * nu1)));
         const int c = pc[k];
         double l1 = 0.0, l2 = 0.0;
         if (c == 0) {
@@ -1577,21 +1601,53 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, i
             l2 = fma(a[0], g1, -(g0 * a[1])) * idet;
             if (!(l1 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi1[k]; add[k] &= ~(1 << pi1[k]); }
             if (!(l2 >= -tol_d)) { ok = 0; neg = 1; drop[k] |= 1 << pi2[k]; add[k] &= ~(1 << pi2[k]); }
+#ifdef ORC_TRACE
+            if (!(l1 >= -tol_d) || !(l2 >= -tol_d)) fprintf(stderr, "  k %d pair %d %d l1 %.3g l2 %.3g tol %.3g\n", k, pi1[k], pi2[k], l1, l2, tol_d);
+#endif
         }
         lm[2 * k] = l1 > 0.0 ? l1 : 0.0;
         lm[2 * k + 1] = l2 > 0.0 ? l2 : 0.0;
         const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
         for (int i = 0; i < w->nf[k]; ++i) {
             const double* a = w->A + (k * M + i) * 2;
-            if (!(FD2(a[0], r0, a[1], r1) - w->b[k * M + i] <= tol_p)) {
+            const double vi = FD2(a[0], r0, a[1], r1) - w->b[k * M + i];
+            if (!(vi <= tol_p)) {
+#ifdef ORC_TRACE
+                fprintf(stderr, "  k %d facet %d viol %.3g c %d\n", k, i, vi, c);
+#endif
                 ok = 0;
                 viol = 1;
-                if (pass >= 1 || guess) { add[k] |= 1 << i; drop[k] &= ~(1 << i); }
+                vmax = nanmax(vmax, vi);
+                if (guess) { add[k] |= 1 << i; drop[k] &= ~(1 << i); }
+            }
+        }
+    }
+#ifdef ORC_TRACE
+    {
+        int n0 = 0, n1 = 0, n2 = 0, nd = 0, na = 0;
+        for (int k = 0; k < N; ++k) { n0 += pc[k] == 0; n1 += pc[k] == 1; n2 += pc[k] == 2;
+                                      nd += __builtin_popcount(drop[k]); na += __builtin_popcount(add[k]); }
+        fprintf(stderr, "pass %d guess %d ok %d neg %d viol %d c0 %d c1 %d c2 %d drop %d add %d\n", pass,
+                guess != 0, ok, neg, viol, n0, n1, n2, nd, na);
+    }
+#endif
+    /* the IPM polish adds only the facets violated by at least ORC_ADD_REL of the pass's largest
+     * violation: the knots next to a misidentified one are pushed over their own facets by
+     * rounding-level amounts that the next pass removes (adding them as well made the passes
+     * alternate on the uncapturable-state windows); the active-set start adds every one */
+    if (!guess && viol) {
+        const double thr = ORC_ADD_REL * vmax;
+        for (int k = 0; k < N; ++k) {
+            const double r0 = w->vrp[2 * k], r1 = w->vrp[2 * k + 1];
+            for (int i = 0; i < w->nf[k]; ++i) {
+                const double* a = w->A + (k * M + i) * 2;
+                const double vi = FD2(a[0], r0, a[1], r1) - w->b[k * M + i];
+                if (vi > tol_p && vi >= thr) { add[k] |= 1 << i; drop[k] &= ~(1 << i); }
             }
         }
     }
     if (ok) break;
-    if (guess ? !(neg || viol) : ((pass == 0 && !neg) || (pass == 1 && !viol))) break;
+    if (!(neg || viol)) break;
     memcpy(w->vrp, bak, sizeof(double) * 2 * N);   /* pass 1 starts from the same iterate */
     memcpy(w->xi, bak + 2 * N, sizeof(double) * (2 * (size_t)N + 2));
     }
@@ -1607,6 +1663,176 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_d, const int* guess, i
     free(pc);
     free(bak);
     free(add);
+    return ok;
+}
+
+/* B-metric projection of rs onto the polygon {r : a_i . r <= b_i, i < m} of knot k (the saturated
+ * start's one-step problem, see dcm_saturated_start): rs itself if no facet is violated; else the
+ * candidate of least (r - rs)^T B (r - rs) among the projections onto single facet lines (valid
+ * when the facet is violated and the point is feasible) and the vertices of facet pairs (valid
+ * when feasible), candidates in the order: facets 0..m-1, then pairs (i, j), i < j, lexicographic;
+ * the first of equal distances wins (the kernel: one candidate per lane, the lowest lane of the
+ * minimum).  None valid (rounding): rs.  Returns the active count (0, 1, 2), facets in *i1, *i2. */
+static int sat_project(const dcm_ws* w, int k, double rs0, double rs1, double B00, double B01,
+                       double B11, double tol_p, double* r0, double* r1, int* i1, int* i2)
+{
+    const int M = w->M, m = w->nf[k];
+    const double* A = w->A + (size_t)k * M * 2;
+    const double* b = w->b + (size_t)k * M;
+    *r0 = rs0; *r1 = rs1; *i1 = 0; *i2 = 0;
+    int inside = 1;
+    for (int i = 0; i < m; ++i)
+        if (!(FD2(A[2 * i], rs0, A[2 * i + 1], rs1) - b[i] <= 0.0)) inside = 0;
+    if (inside) return 0;
+    const double detB = fma(B00, B11, -(B01 * B01));
+    double best = 0.0;
+    int bc = -1;
+    for (int c = 0; c < MF + MF * (MF - 1) / 2; ++c) {
+        double v0, v1, dist;
+        int x, y;
+        if (c < MF) {
+            x = c; y = c;
+            if (x >= m) continue;
+            const double a0 = A[2 * x], a1 = A[2 * x + 1];
+            const double u0 = fma(B11, a0, -(B01 * a1));       /* adj(B) a = det(B) B^{-1} a */
+            const double u1 = fma(B00, a1, -(B01 * a0));
+            const double aua = FD2(a0, u0, a1, u1);
+            const double viol = FD2(a0, rs0, a1, rs1) - b[x];
+            const double t = viol / aua;
+            v0 = fma(-t, u0, rs0);
+            v1 = fma(-t, u1, rs1);
+            if (!(viol > 0.0)) continue;
+            dist = (t * viol) * detB;
+        } else {
+            /* pair q = c - MF of (0,1), (0,2), .., (0,7), (1,2), .. (6,7) */
+            int q = c - MF;
+            x = 0;
+            while (q >= MF - 1 - x) { q -= MF - 1 - x; ++x; }
+            y = x + 1 + q;
+            if (y >= m) continue;
+            const double a0 = A[2 * x], a1 = A[2 * x + 1], e0 = A[2 * y], e1 = A[2 * y + 1];
+            const double det = fma(a0, e1, -(a1 * e0));
+            const double aa = FD2(a0, a0, a1, a1), ee = FD2(e0, e0, e1, e1);
+            if (!(det * det > 1e-18 * (aa * ee))) continue;
+            const double idet = 1.0 / det;
+            v0 = fma(b[x], e1, -(a1 * b[y])) * idet;
+            v1 = fma(a0, b[y], -(b[x] * e0)) * idet;
+            const double d0 = v0 - rs0, d1 = v1 - rs1;
+            dist = fma(d0, fma(B00, d0, 2.0 * (B01 * d1)), (B11 * d1) * d1);
+        }
+        int feas = 1;
+        for (int l = 0; l < m; ++l)
+            if (!(FD2(A[2 * l], v0, A[2 * l + 1], v1) - b[l] <= tol_p)) feas = 0;
+        if (!feas || !(dist == dist)) continue;
+        if (bc < 0 || dist < best) { best = dist; bc = c; *r0 = v0; *r1 = v1; *i1 = x; *i2 = y; }
+    }
+    if (bc < 0) { *r0 = rs0; *r1 = rs1; return 0; }
+    return bc < MF ? 1 : 2;
+}
+
+/* The saturated LQ start of the interior point method: when the active-set
+ * start does not certify, the IPM starts from the closed-loop rollout of the unconstrained LQ
+ * policy with every VRP projected onto its support polygon, instead of from the LQ optimum with
+ * centred multipliers.  The QPs that get here are those of uncapturable DCM states
+ * (tests/golden/c5_hard_windows.npz): the optimal VRPs sit on polygon vertices at nearly every
+ * knot and the multipliers reach ~1e7, which an IPM started at lam ~ 1 takes 30-60 iterations to
+ * reach.  The rollout puts the trajectory on the escaping side, and its costates give the
+ * multipliers their scale:
+ *   1. the LQ policy around the current iterate (one Newton step of the QP without facets):
+ *      r_k(xi) = r*_k + alpha_k beta_k M_k^T (xi - xi*_k), with the one-step Hessian
+ *      B_k = R + beta_k^2 P_{k+1};
+ *   2. the rollout xi_0 = xi_init, r_k = the B_k-metric projection of r_k(xi_k) onto polygon k
+ *      (sat_project), xi_{k+1} = xi_k + (omega xi_k - omega r_k) dt (the dynamics' own form: no
+ *      defects);
+ *   3. costates by single shooting over the rollout, nu_k = qx_k + alpha_k nu_{k+1}, and at each
+ *      knot the multipliers of its projected facets from stationarity beta nu - R (r - r_ref) =
+ *      A_act^T lam (clamped at 0);
+ *   4. s = max(b - A r, 1e-2), lam = max(estimate, 1e-2 / s).
+ * Returns 0 if the factorization fails; *dres receives max |R (r - r_ref) + A^T lam - beta nu|. */
+static int dcm_saturated_start(dcm_ws* w, const double* xi_init, double tol_p, double* dres_out)
+{
+    const int N = w->N, M = w->M;
+    int* act = (int*)malloc(sizeof(int) * 3 * (size_t)N);
+    for (int k = 0; k < N; ++k) { w->W[4 * k] = w->W[4 * k + 1] = w->W[4 * k + 2] = w->W[4 * k + 3] = 0.0; }
+    dcm_residuals(w, 0);
+    for (int k = 0; k < N; ++k) { w->g[2 * k] = w->rh[2 * k]; w->g[2 * k + 1] = w->rh[2 * k + 1]; }
+    const int ok = dcm_factor(w);
+    dcm_solve(w);
+    /* the LQ optimum: r*_k, xi*_k (knot k's own state; xi*_0 = xi_init) */
+    for (int k = 0; k < N; ++k) {
+        double* S = w->sg + 4 * k;
+        S[0] = w->vrp[2 * k] + w->dr[2 * k];
+        S[1] = w->vrp[2 * k + 1] + w->dr[2 * k + 1];
+        S[2] = (k ? w->xi[2 * k] : xi_init[0]) + (k ? w->x[2 * k] : 0.0);
+        S[3] = (k ? w->xi[2 * k + 1] : xi_init[1]) + (k ? w->x[2 * k + 1] : 0.0);
+    }
+    double x0 = xi_init[0], x1 = xi_init[1];
+    for (int k = 0; k < N; ++k) {
+        const double* S = w->sg + 4 * k;
+        const double* Mk = w->Mm + 4 * k;
+        const double d0 = x0 - S[2], d1 = x1 - S[3];
+        const double rs0 = fma(w->ab[k], FD2(Mk[0], d0, Mk[2], d1), S[0]);
+        const double rs1 = fma(w->ab[k], FD2(Mk[1], d0, Mk[3], d1), S[1]);
+        const double b2 = w->b2[k];
+        const double B00 = fma(b2, w->Pn[3 * k], w->Rw0);
+        const double B01 = b2 * w->Pn[3 * k + 1];
+        const double B11 = fma(b2, w->Pn[3 * k + 2], w->Rw1);
+        double r0, r1;
+        act[3 * k] = sat_project(w, k, rs0, rs1, B00, B01, B11, tol_p, &r0, &r1, &act[3 * k + 1], &act[3 * k + 2]);
+        const double om = w->omega[k];
+        const double dx0 = FD2(om, x0, -om, r0);
+        const double dx1 = FD2(om, x1, -om, r1);
+        x0 = fma(dx0, w->dt, x0);
+        x1 = fma(dx1, w->dt, x1);
+        w->vrp[2 * k] = r0;
+        w->vrp[2 * k + 1] = r1;
+        w->xi[2 * (k + 1)] = x0;
+        w->xi[2 * (k + 1) + 1] = x1;
+    }
+    /* costates of the rollout (the warm start's backward scan) */
+    dcm_residuals(w, 0);
+    for (int k = 0; k < N; ++k) {
+        double* G = w->sg + 4 * k;
+        G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
+        w->sc[2 * k] = w->al[k] * w->qx[2 * k];
+        w->sc[2 * k + 1] = w->al[k] * w->qx[2 * k + 1];
+    }
+    scan_backward(w, w->sg, w->sc);
+    double dres = 0.0;
+    for (int k = 0; k < N; ++k) {
+        const double nu0 = w->qx[2 * k] + w->v[2 * (k + 1)];
+        const double nu1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
+        const double g0 = fma(w->be[k], nu0, -w->rh[2 * k]);
+        const double g1 = fma(w->be[k], nu1, -w->rh[2 * k + 1]);
+        const int c = act[3 * k], x = act[3 * k + 1], y = act[3 * k + 2];
+        double l1 = 0.0, l2 = 0.0;
+        if (c == 1) {
+            const double* a = w->A + (k * M + x) * 2;
+            l1 = FD2(a[0], g0, a[1], g1) / FD2(a[0], a[0], a[1], a[1]);
+        } else if (c == 2) {
+            const double* a = w->A + (k * M + x) * 2;
+            const double* e = w->A + (k * M + y) * 2;
+            const double idet = 1.0 / fma(a[0], e[1], -(a[1] * e[0]));
+            l1 = fma(g0, e[1], -(e[0] * g1)) * idet;
+            l2 = fma(a[0], g1, -(g0 * a[1])) * idet;
+        }
+        double al0 = 0.0, al1 = 0.0;   /* A^T lam */
+        for (int i = 0; i < w->nf[k]; ++i) {
+            const double* a = w->A + (k * M + i) * 2;
+            const double sl = w->b[k * M + i] - FD2(a[0], w->vrp[2 * k], a[1], w->vrp[2 * k + 1]);
+            const double si = sl > 1e-2 ? sl : 1e-2;
+            const double est = (c >= 1 && i == x) ? l1 : (c == 2 && i == y) ? l2 : 0.0;
+            const double lc = 1e-2 / si;
+            w->s[k * MF + i] = si;
+            w->lam[k * MF + i] = est > lc ? est : lc;
+            al0 = fma(a[0], w->lam[k * MF + i], al0);
+            al1 = fma(a[1], w->lam[k * MF + i], al1);
+        }
+        dres = nanmax(dres, fabs(al0 - g0));
+        dres = nanmax(dres, fabs(al1 - g1));
+    }
+    free(act);
+    *dres_out = dres;
     return ok;
 }
 
@@ -1786,10 +2012,14 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
 
     w->pairs = 0;   /* the IPM kernel's tree from here on */
     w->dpp = 0;
-    /* ---- initial point 3: s = max(b - A r, 1e-2), lam = 1e-2 / s; warm: s = max(b - A r, floor),
-     *      lam = max(lam_warm[src], floor) with the same source knot as the VRP ---- */
     double dres = 0.0;
-    for (int k = 0; k < N; ++k) {
+    /* ---- after a failed active-set start: the saturated LQ start (dcm_saturated_start) ---- */
+    const int sat = prm->tol_polish > 0.0;
+    if (sat && !dcm_saturated_start(w, xi_init, prm->tol_primal, &dres)) { status = 2; goto done; }
+    /* ---- initial point 3 (the interior point method alone, tol_polish = 0): s = max(b - A r,
+     *      1e-2), lam = 1e-2 / s; warm: s = max(b - A r, floor), lam = max(lam_warm[src], floor)
+     *      with the same source knot as the VRP ---- */
+    for (int k = 0; k < N && !sat; ++k) {
         const int m = nfacets[k];
         const int ws = warm && k + warm->shift < N;
         const double sfloor = ws ? warm->floor : 1e-2;
@@ -1817,7 +2047,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      *      carries them (the QP's linear residuals contract by (1 - a)) ---- */
     double pres = dcm_residuals(w, 1);
     double mu = ntot > 0 ? orc_wave_tree_sum(w->c, N) / (double)ntot : 0.0;
-    if (warm) {
+    if (warm && !sat) {
         for (int k = 0; k < N; ++k) {
             double* G = w->sg + 4 * k;
             G[0] = w->al[k]; G[1] = 0.0; G[2] = 0.0; G[3] = w->al[k];
@@ -1840,7 +2070,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         if (it > 0) dcm_residuals(w, 1);   /* the iterate's gradient, defects, Q (xi - xi_ref) */
         if (!(mu == mu) || !(pres == pres) || !(dres == dres) || isinf(mu)) { status = 2; break; }
         if (prm->tol_polish > 0.0 && mu <= prm->tol_polish) {
-            if (dcm_polish(w, prm->tol_primal, prm->tol_dual, NULL, 3)) { polished = 1; status = 0; break; }
+            if (dcm_polish(w, prm->tol_primal, prm->tol_dual, NULL, ORC_GUESS_PASSES)) { polished = 1; status = 0; break; }
             dcm_residuals(w, 1);   /* the iterate's gradient and defects again (the polish reused them) */
         }
         if (mu <= prm->tol_mu && pres <= prm->tol_primal && dres <= prm->tol_dual) { status = 0; break; }
@@ -1938,6 +2168,16 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
                 w->lam[k * MF + i] = fma(a, w->cdl[k * MF + i], w->lam[k * MF + i]);
             }
         }
+#ifdef ORC_TRACE
+        {
+            int nact = 0; double lmax = 0.0;
+            for (int k = 0; k < N; ++k) for (int i = 0; i < nfacets[k]; ++i) {
+                nact += w->lam[k * MF + i] > w->s[k * MF + i];
+                lmax = fmax(lmax, w->lam[k * MF + i]); }
+            fprintf(stderr, "it %d mu %.3g a_aff %.3g a %.3g sigma %.3g pres %.3g dres %.3g nact %d lmax %.3g\n",
+                    it, mu, a_aff, a, sigma, pres, dres, nact, lmax);
+        }
+#endif
         dres = dres * (1.0 - a);
         pres = pres * (1.0 - a);
         /* sum (s + a ds)(lam + a dl) = U0 + a T1 + a^2 T2 with T1 = sum (s dl + lam ds) = -sum rc

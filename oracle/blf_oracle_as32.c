@@ -19,7 +19,10 @@
 
 #define WV 64
 #define MF 8
-#define PASSES 8                 /* ORC_GUESS_PASSES, kernel kGuessPasses */
+#ifndef ORC_GUESS_PASSES
+#define ORC_GUESS_PASSES 8
+#endif
+#define PASSES ORC_GUESS_PASSES   /* kernel kGuessPasses */
 #define SEARCH_TOL_P 1e-5f       /* kernel kSearchTolP */
 #define SEARCH_TOL_D 1e-4f       /* kernel kSearchTolD */
 #define F2(a, b, c, d) fmaf((a), (b), (c) * (d))

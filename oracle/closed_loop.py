@@ -128,6 +128,8 @@ class OracleLoop:
         pv, pl, ps = ((None, None, None) if self.prev is None else
                       (self.prev["vrp"], self.prev["lam"], self.prev["status"]))
         pol = np.zeros(xi.shape[0], np.int32)
+        # the window's QP and its warm start, kept for tests/golden/make_c5_windows.py
+        self.last_window = dict(w, vrp_ws=pv, lam_ws=pl, prev_status=ps)
         st, xo, vrp, it, lam = O.dcm_mpc_solve_batch_warm(w, vrp_ws=pv, lam_ws=pl, shift=1, floor=1e-3,
                                                           params=self.params, threads=self.threads,
                                                           polished=pol, prev_status=ps)

@@ -1,0 +1,58 @@
+"""The config-5 windows of uncapturable DCM states on the device (tests/test_c5_windows.py has the
+oracle's certificates): the warm solve the closed loop runs and a cold solve of every window of
+tests/golden/c5_failed_windows_r03.npz (the 68 windows that ended at the iteration cap in round 3)
+and c5_hard_windows.npz (the 128 that need the most interior point iterations now), through the C
+ABI, against the oracle bit for bit (status, iterations, xi, VRPs, multipliers), every one
+certified (status 0, polished)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from blf import native
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KEYS = ("xi_init", "omega", "xi_ref", "vrp_ref", "A", "b", "nfacets")
+
+
+def _load(name):
+    d = dict(np.load(os.path.join(GOLDEN, name)))
+    return {k: d[k] for k in KEYS}, d
+
+
+@pytest.mark.parametrize("name", ["c5_failed_windows_r03.npz", "c5_hard_windows.npz"])
+def test_c5_windows_warm_bitwise(handle, oracle, name):
+    prob, d = _load(name)
+    B, N = prob["omega"].shape
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in prob.items()}
+    prm = native.default_params(N, tol_polish=1e-4)
+    warm = dict(vrp=torch.from_numpy(d["vrp_ws"]).cuda(), lam=torch.from_numpy(d["lam_ws"]).cuda(),
+                shift=1, floor=1e-3, status=torch.from_numpy(d["prev_status"]).cuda())
+    out = handle.dcm_mpc_solve(dev, prm, warm=warm, lambda_out=True)
+    torch.cuda.synchronize()
+    st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(
+        prob, vrp_ws=d["vrp_ws"], lam_ws=d["lam_ws"], shift=1, floor=1e-3,
+        params=oracle.default_params(N, tol_polish=1e-4), prev_status=d["prev_status"], threads=8)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), st)
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), it)
+    np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi)
+    np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp)
+    np.testing.assert_array_equal(out["lam"].cpu().numpy(), lam)
+    assert out["polished"].cpu().numpy().all()
+
+
+@pytest.mark.parametrize("name", ["c5_failed_windows_r03.npz", "c5_hard_windows.npz"])
+def test_c5_windows_cold_bitwise(handle, oracle, name):
+    prob, _ = _load(name)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in prob.items()}
+    out = handle.dcm_mpc_solve(dev)
+    torch.cuda.synchronize()
+    st, xi, vrp, it = oracle.dcm_mpc_solve_batch(prob, threads=8)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), st)
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), it)
+    np.testing.assert_array_equal(out["xi"].cpu().numpy(), xi)
+    np.testing.assert_array_equal(out["vrp"].cpu().numpy(), vrp)

@@ -5,6 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/stream_prof
 mkdir -p $OUT
+timeout -k 10 120 python3 -c "import json, sys; sys.path.insert(0, 'bipedal-locomotion-framework_amd'); from blf import native; print(json.dumps(native.build_provenance()))" > $OUT/build.json || exit $?
 export TMPDIR=/tmp
 timeout -k 10 300 python tools/stream_bench.py --out gpurun_out/stream.json > gpurun_out/stream.log 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/stream.log | tail -8

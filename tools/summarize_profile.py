@@ -132,7 +132,14 @@ def main():
     d = pmc.get(dom, {})
     fetch_kib = d.get("FETCH_SIZE", {}).get("mean_per_dispatch")
     write_kib = d.get("WRITE_SIZE", {}).get("mean_per_dispatch")
+    try:
+        build = json.load(open(os.path.join(src, "build.json")))
+    except (OSError, ValueError):
+        build = None
     summary = {
+        # the library these counters come from (blf/native.py build_provenance on the box):
+        # bench.py uses a summary only when its lib_src_hash is the measured library's
+        "build": build,
         "source": "tools/profile_round.sh (rocprofv3 --kernel-trace --stats; separate --pmc passes "
                   "FETCH_SIZE | WRITE_SIZE | SQ_*) on `python3 bench.py --steps 10 --warmup 2 --no-cpu`",
         "dominant_kernel": dom,

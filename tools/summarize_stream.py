@@ -46,7 +46,12 @@ def main():
         if c and c["fetch_x2_corrected_MB"] is not None and c["write_MB"] is not None and bases[base] == 1:
             l["traffic_MB"] = c["fetch_x2_corrected_MB"] + c["write_MB"]
             l["traffic_over_algorithmic"] = l["traffic_MB"] * 1e6 / l["algorithmic_bytes"]
-    out = {"source": "tools/gpu_stream.sh: tools/stream_bench.py timed with HIP events (median); "
+    try:
+        build = json.load(open(os.path.join(src, "stream_prof", "build.json")))
+    except (OSError, ValueError):
+        build = None
+    out = {"build": build,
+           "source": "tools/gpu_stream.sh: tools/stream_bench.py timed with HIP events (median); "
                      "rocprofv3 --kernel-trace --stats and separate --pmc FETCH_SIZE / WRITE_SIZE "
                      "passes of the same program (per-dispatch means over every dispatch of the "
                      "kernel in the program)",
