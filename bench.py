@@ -165,6 +165,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dump-state", default=None,
+                    help="c5: write each rank's final robot state to DIR/c5_state_rank<r>.npz")
     ap.add_argument("--c5-groups", type=int, default=1,
                     help="c5: robots in this many groups, each closed loop on its own stream "
                          "(measured: 1 group 6.96 ms, 2 groups 6.98 ms, 4 groups 7.4 ms per period)")
@@ -420,6 +422,16 @@ def other_workload(args):
     emit(line)
 
 
+def c5_shard(model, rank, B, N, periods):
+    """Rank `rank`'s robots of configs[4]: the plans of problems [rank B, (rank + 1) B) (8
+    footsteps, a standing start longer than the run) and standing states of seed 1000 + rank."""
+    from blf import problems as P
+    from blf import robot
+    plan = P.make_batch(B, horizon=N + periods, n_footsteps=8, seed=P.SEED, start=rank * B,
+                        first_ds=periods + 10)
+    return plan, robot.standing_states(model, B, seed=1000 + rank)
+
+
 def closed_loop(args):
     """configs[4]: the closed loop of the DCM-MPC planner and the 30-DoF floating-base robot with
     two ContinuousContactModel feet (blf/closed_loop.py), B = 16384 robots
@@ -428,68 +440,106 @@ def closed_loop(args):
     plan window, the plan's first VRP -> joint references, the reference schedule's ForwardEuler
     steps (1 ms each, 19 steps = 20 ms of robot time, blf/closed_loop.py fixed_step_schedule) of
     the dynamics with the joint impedance.  The loop runs from a standing start; warmup periods first,
-    then the timed ones, stream-ordered and synchronised once."""
+    then the timed ones, stream-ordered and synchronised once.
+
+    BLF_C5_ORACLE=1 (with BLF_BENCH_BACKEND=gloo) rehearses this multi-rank path on the CPU: every
+    rank runs the CPU restatement of the loop (oracle/closed_loop.py, compiled) over its shard
+    through the same sharding, barriers and max-over-ranks timing (tests/test_distributed.py);
+    --dump-state writes each rank's final robot state."""
     import numpy as np
     import torch
     import torch.distributed as dist
     from blf import closed_loop as DL
-    from blf import native
-    from blf import problems as P
     from blf import robot
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     backend = os.environ.get("BLF_BENCH_BACKEND", "nccl")
-    if world > 1:
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    torch.cuda.set_device(local)
-    h = native.Handle(local)
+    on_cpu = os.environ.get("BLF_C5_ORACLE") == "1"
+    if on_cpu and backend != "gloo":
+        sys.exit("bench.py: BLF_C5_ORACLE=1 runs on the CPU and needs BLF_BENCH_BACKEND=gloo")
     B = args.batch if args.batch != 4096 else 16384   # configs[4]: 16 384 robots per GPU
     N, S = args.horizon, args.warmup + args.steps
     model = robot.humanoid24()
-    plan = P.make_batch(B, horizon=N + S, n_footsteps=8, seed=P.SEED, start=rank * B, first_ds=S + 10)
-    st = robot.standing_states(model, B, seed=1000 + rank)
-    # the robots in G groups, each closed loop on its own stream (--c5-groups, default 1): every
-    # robot's period is the same computation as in one group (DL.split_groups); more groups did
-    # not pay (DESIGN.md section 11: the dynamics kernel holds every SIMD, so the plan kernels'
-    # tails find no room beside it)
-    loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N)
+    plan, st = c5_shard(model, rank, B, N, S)
+    if on_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import closed_loop as CL
+        if world > 1:
+            dist.init_process_group("gloo")
+        sync = lambda: None
+        loops = [CL.OracleLoop(model, plan, st, robot.sole_null_poses(model, st),
+                               robot.posture_law_arrays(model), DL.CONTACT_PARAMS, horizon=N,
+                               compiled=True, threads=max(1, cpu_threads() // max(1, world)))]
+        state_of = lambda lp: lp.state
+        dt_ms, T, dT = float(plan["dt"]), loops[0].T, loops[0].dT
+    else:
+        from blf import native
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        if world > 1:
+            torch.cuda.set_device(local)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend)
+        torch.cuda.set_device(local)
+        sync = torch.cuda.synchronize
+        h = native.Handle(local)
+        # the robots in G groups, each closed loop on its own stream (--c5-groups, default 1): every
+        # robot's period is the same computation as in one group (DL.split_groups); more groups did
+        # not pay (DESIGN.md section 11: the dynamics kernel holds every SIMD, so the plan kernels'
+        # tails find no room beside it)
+        loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N)
+        for lp in loops:
+            lp.expand_path = args.expand_path
+        state_of = lambda lp: {k: v.cpu().numpy() for k, v in lp.state.items()}
+        dt_ms, T, dT = loops[0].dt, loops[0].T, loops[0].dT
     loop = loops[0]
-    for lp in loops:
-        lp.expand_path = args.expand_path
     for _ in range(args.warmup):
         for lp in loops:
             lp.period()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     statuses = []
     for _ in range(args.steps):
         for lp in loops:
             out = lp.period()
-            with torch.cuda.stream(lp.stream or torch.cuda.current_stream()):   # after the group's solve
-                statuses.append(out["status"].clone())
-    torch.cuda.synchronize()
+            if on_cpu:
+                statuses.append(torch.from_numpy(np.asarray(out["status"], dtype=np.int64)))
+            else:
+                with torch.cuda.stream(lp.stream or torch.cuda.current_stream()):   # after the group's solve
+                    statuses.append(out["status"].clone())
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=("cuda" if backend == "nccl" else "cpu"))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    finite = all(bool(torch.isfinite(v).all()) for lp in loops for v in lp.state.values())
+    states = [state_of(lp) for lp in loops]
+    finite = all(bool(np.isfinite(v).all()) for s_ in states for v in s_.values())
     assert finite, "non-finite robot state in the closed loop"
-    stat = torch.bincount(torch.cat(statuses).to(torch.int64), minlength=4).cpu().numpy()
-    z = torch.cat([lp.state["base_pos"][:, 2] for lp in loops])
-    nsteps = len(loop.steps)
-    robot_ms = sum(loop.steps) * 1e3
+    if args.dump_state:
+        os.makedirs(args.dump_state, exist_ok=True)
+        np.savez(os.path.join(args.dump_state, f"c5_state_rank{rank}.npz"),
+                 **{k: np.concatenate([s_[k] for s_ in states]) for k in states[0]})
+    stat = torch.bincount(torch.cat(statuses).to(torch.int64).cpu(), minlength=4)[:4].to(torch.float64)
+    z = np.concatenate([s_["base_pos"][:, 2] for s_ in states])
+    zr = torch.tensor([-z.min(), z.max(), 0.0 if finite else 1.0], dtype=torch.float64)
+    if world > 1:   # the whole job's statuses and heights (outside the timed region)
+        dev = "cuda" if backend == "nccl" else "cpu"
+        stat, zr = stat.to(dev), zr.to(dev)
+        dist.all_reduce(stat, op=dist.ReduceOp.SUM)
+        dist.all_reduce(zr, op=dist.ReduceOp.MAX)
+    stat, zr = stat.cpu().numpy().astype(np.int64), zr.cpu().numpy()
+    finite = bool(finite and zr[2] == 0.0)
+    steps = DL.fixed_step_schedule(0.0, T, dT)
+    nsteps = len(steps)
+    robot_ms = sum(steps) * 1e3
     if rank == 0:
         line = {"metric": "closed-loop control periods/sec (DCM-MPC + 30-DoF floating-base "
                           "dynamics with 2 ContinuousContactModel feet, configs[4])",
@@ -500,15 +550,17 @@ def closed_loop(args):
                 "qp_status_counts": {"solved": int(stat[0]), "max_iter": int(stat[1]),
                                      "numerical": int(stat[2]), "bad_facets": int(stat[3])},
                 "state_finite": finite,
-                "base_height_range": [float(z.min()), float(z.max())],
+                "base_height_range": [float(-zr[0]), float(zr[1])],
                 "robot_time_per_period_ms": robot_ms,
-                "config": {"workload": f"configs[4]: {B} robots per GPU x {world} GPU(s), {loop.dt * 1e3:g} ms control "
+                "config": {"workload": f"configs[4]: {B} robots per GPU x {world} GPU(s), {dt_ms * 1e3:g} ms control "
                                        f"period = one knot of a horizon-{N} warm-started plan + "
                                        f"{nsteps} ForwardEuler steps of the 6+24 DoF dynamics "
-                                       f"(integrate(0, {loop.T * 1e3:g} ms) at dT = {loop.dT * 1e3:g} ms: "
+                                       f"(integrate(0, {T * 1e3:g} ms) at dT = {dT * 1e3:g} ms: "
                                        f"{robot_ms:g} ms of robot time, the reference schedule)",
                            "batch_per_gpu": B, "parallelism": f"shard{world} (independent robots)",
                            "stream_groups": len(loops)}}
+        if on_cpu:
+            line["device"] = "CPU rehearsal (BLF_C5_ORACLE=1: oracle/closed_loop.py on every rank)"
         if not args.no_cpu:
             line["cpu_baseline"] = closed_loop_cpu(args, model, N)
         emit(line)

@@ -63,3 +63,45 @@ def test_two_rank_shard_and_gather():
     np.testing.assert_array_equal(got["vrp"], vrp)
     np.testing.assert_array_equal(got["status"], st)
     np.testing.assert_array_equal(got["iters"], it)
+
+
+def test_c5_two_rank_bench_path_cpu(tmp_path):
+    """The config-5 multi-rank path of bench.py, rehearsed on the CPU: two gloo ranks
+    launched by torch.distributed.run exactly as the driver launches the scaling bench, each
+    running its disjoint robot shard (bench.c5_shard) through the same barriers and
+    max-over-ranks timing, with the CPU restatement of the loop (BLF_C5_ORACLE=1) in place of the
+    device kernels.  Each rank's robot state after warmup + timed periods equals, bit for bit, the
+    same robots' rows of one single-process loop over both shards."""
+    import json
+    import subprocess
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "bipedal-locomotion-framework_amd"), os.path.join(ROOT, "oracle")]
+    B, N, warmup, steps = 3, 100, 1, 1
+    env = dict(os.environ, BLF_C5_ORACLE="1", BLF_BENCH_BACKEND="gloo", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "c5", "--batch", str(B),
+           "--horizon", str(N), "--warmup", str(warmup), "--steps", str(steps), "--no-cpu",
+           "--dump-state", str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["batch_per_gpu"] == B and line["state_finite"]
+    assert line["qp_status_counts"]["solved"] == 2 * B * steps
+    import bench
+    import closed_loop as CL
+    from blf import closed_loop as DL
+    from blf import robot
+    model = robot.humanoid24()
+    shards = [bench.c5_shard(model, rk, B, N, warmup + steps) for rk in range(2)]
+    shared = ("knot_phase", "dt", "schedule")
+    plan = {k: (v if k in shared else np.concatenate([s[0][k] for s in shards])) for k, v in shards[0][0].items()}
+    st = {k: np.concatenate([s[1][k] for s in shards]) for k in shards[0][1]}
+    ref = CL.OracleLoop(model, plan, st, robot.sole_null_poses(model, st), robot.posture_law_arrays(model),
+                        DL.CONTACT_PARAMS, horizon=N, compiled=True, threads=2)
+    for _ in range(warmup + steps):
+        ref.period()
+    for rk in range(2):
+        got = np.load(os.path.join(tmp_path, f"c5_state_rank{rk}.npz"))
+        for k in ref.state:
+            np.testing.assert_array_equal(got[k], ref.state[k][rk * B:(rk + 1) * B], err_msg=k)
