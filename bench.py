@@ -484,10 +484,10 @@ def closed_loop(args):
         torch.cuda.set_device(local)
         sync = torch.cuda.synchronize
         h = native.Handle(local)
-        # the robots in G groups, each closed loop on its own stream (--c5-groups, default 1): every
-        # robot's period is the same computation as in one group (DL.split_groups); more groups did
-        # not pay (the dynamics kernel holds every SIMD, so the plan kernels'
-        # tails find no room beside it)
+        # the robots in G groups, each closed loop on its own stream (--c5-groups, default 1): at
+        # horizon 100 every robot's period is the same computation as in one group
+        # (DL.split_groups states when); more groups did not pay (the
+        # dynamics kernel holds every SIMD, so the plan kernels' tails find no room beside it)
         loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N)
         for lp in loops:
             lp.expand_path = args.expand_path

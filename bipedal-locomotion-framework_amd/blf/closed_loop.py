@@ -139,9 +139,15 @@ class ClosedLoop:
 
 def split_groups(h, model, plan, states, groups, horizon=100, **kw):
     """The robots of (plan, states) in `groups` contiguous groups, each a ClosedLoop on its own
-    stream (one group: the current stream).  Every robot's periods are the same computation as in
-    one ClosedLoop over all robots; the groups' kernels overlap on the device (the plan kernels'
-    tails, a few QPs on an otherwise idle chip, run beside another group's dynamics)."""
+    stream (one group: the current stream); the groups' kernels overlap on the device (the plan
+    kernels' tails, a few QPs on an otherwise idle chip, run beside another group's dynamics).
+
+    Every robot's periods are the same computation as in one ClosedLoop over all robots, bit for
+    bit, when the QP launches of a group and of the whole batch pick the same kernels: the QP
+    kernels choose their scan tree and the fused small-batch kernel by batch size
+    (BLF_DPP_TREE_MAX_BATCH = 1024 and the fused kernel's limit, both for horizons <= 64 only).
+    Horizons > 64 (the configs[4] loop's 100) are unaffected; with horizon <= 64, groups on the
+    other side of those limits than the whole batch agree to rounding, not bit for bit."""
     import torch
     B = plan["omega"].shape[0]
     groups = max(1, min(int(groups), B))

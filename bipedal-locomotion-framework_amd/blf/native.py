@@ -19,7 +19,8 @@ STATUS_NAMES = {0: "BLF_OK", 1: "BLF_ERR_INVALID_ARGUMENT", 2: "BLF_ERR_HIP",
 QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 
 # every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
-EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_step_schedule",
+EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_set_qp_launch_mode",
+            "blf_step_schedule",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_hull3d_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
             "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_solve_warm",
@@ -183,6 +184,7 @@ def lib():
             _vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), ctypes.POINTER(JointImpedance),
             ctypes.POINTER(FbContacts), _vp, _i64, _f64, _f64, _f64, _vp]
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
+        L.blf_set_qp_launch_mode.argtypes = [_i32, _i32]
         for name in EXPORTED:
             if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
                             "blf_dcm_mpc_default_params", "blf_dcm_mpc_flops_per_iter"):
@@ -191,6 +193,12 @@ def lib():
         L.blf_destroy.restype = _i32
         _LIB = L
     return _LIB
+
+
+def set_qp_launch_mode(fuse_stage2=-1, single_kernel=-1):
+    """blf_set_qp_launch_mode: the QP kernel routing for A/B and parity tests (-1: unchanged).
+    Returns nothing; the defaults are the product's (fuse_stage2 = 1, single_kernel = 0)."""
+    _check(lib().blf_set_qp_launch_mode(int(fuse_stage2), int(single_kernel)))
 
 
 def _check(code):

@@ -112,6 +112,22 @@ def reduce_fixed_joints(model, fixed):
     Fixed joints are merged deepest first (highest index), so chains of fixed joints collapse.
     The rigid-body terms of the result equal those of the full model with the fixed joints held at
     q = 0, q_dot = 0, their rows and columns removed (tests/test_fb_dynamics.py)."""
+    n = int(model["n"])
+    sizes = {"parent": n, "joint_origin": n, "joint_rot": n, "joint_axis": n, "link_mass": n + 1,
+             "link_com": n + 1, "link_inertia": n + 1}
+    for k, want in sizes.items():
+        if len(model[k]) != want:
+            raise ValueError(f"reduce_fixed_joints: {k} has {len(model[k])} entries, the model "
+                             f"has {n} joints")
+    if model.get("joint_type") is not None and len(model["joint_type"]) != n:
+        raise ValueError("reduce_fixed_joints: joint_type must have one entry per joint")
+    if len(model["frame_link"]) != len(model["frame_pose"]):
+        raise ValueError("reduce_fixed_joints: frame_link and frame_pose differ in length")
+    # the merge re-indexes joints and links in place, which assumes topological order
+    for j, pj in enumerate(model["parent"]):
+        if not 0 <= int(pj) <= j:
+            raise ValueError(f"reduce_fixed_joints: joint {j} has parent link {int(pj)}; the joints "
+                             f"must be in topological order (0 <= parent[j] <= j)")
     names = list(model["names"]) if "names" in model else None
     if names is None and any(isinstance(f, str) for f in fixed):
         raise ValueError("reduce_fixed_joints: joints named, but the model has no names")

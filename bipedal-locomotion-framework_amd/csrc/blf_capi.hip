@@ -12,6 +12,16 @@ namespace blf {
 
 static thread_local char g_err[512] = "no error";
 
+QpLaunchMode& qp_launch_mode()
+{
+    static QpLaunchMode mode = [] {
+        const char* fz = getenv("BLF_QP_FUSE_STAGE2");
+        const char* sk = getenv("BLF_QP_SINGLE_KERNEL");
+        return QpLaunchMode{!(fz && fz[0] == '0'), sk && sk[0] == '1'};
+    }();
+    return mode;
+}
+
 blf_status set_error(blf_status code, const char* fmt, ...)
 {
     va_list ap;
@@ -116,6 +126,17 @@ blf_status blf_step_schedule(double initial_time, double final_time, double dT, 
 // The sources' hash (Makefile SRC_HASH) makes the loaded library traceable to the tree it was
 // built from (blf/native.py build_provenance).
 const char* blf_version(void) { return "blf-mi355x 0.1.0 (gfx950, fp64, -ffp-contract=off) src " BLF_SRC_HASH; }
+
+
+blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel)
+{
+    BLF_REQUIRE(fuse_stage2 >= -1 && fuse_stage2 <= 1 && single_kernel >= -1 && single_kernel <= 1,
+                "blf_set_qp_launch_mode: settings are -1, 0 or 1");
+    QpLaunchMode& m = qp_launch_mode();
+    if (fuse_stage2 >= 0) m.fuse_stage2 = fuse_stage2;
+    if (single_kernel >= 0) m.single_kernel = single_kernel;
+    return BLF_OK;
+}
 
 blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m, const double* A,
                                    const double* Bm, int32_t shared_matrices, const double* u,

@@ -54,6 +54,12 @@ blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* 
                                int64_t start_knot, double dt, int32_t N, int64_t batch, double* A,
                                double* b, int32_t* nfacets, double* xi_ref, double* vrp_ref,
                                hipStream_t s);
+// The QP kernel routing (blf_set_qp_launch_mode); initialised once from the environment.
+struct QpLaunchMode {
+    int fuse_stage2;     // 1 (default): stage 2 inside the small-batch active-set kernel
+    int single_kernel;   // 0 (default): active-set kernel first
+};
+QpLaunchMode& qp_launch_mode();
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
                           const blf_dcm_mpc_warm_start* warm, int64_t batch,
                           const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);

@@ -1569,8 +1569,7 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     constexpr int kAltTree = KPL == 2 ? kTreePad : kTreeDpp;   // the instantiated trees: this, kTreeKS
     const int tr = (KPL == 1 && batch <= kDppTreeMaxBatch) ? kTreeDpp
                    : (KPL == 2 && kp.N <= 2 * kWave - 2) ? kTreePad : kTreeKS;
-    const char* fz = getenv("BLF_QP_FUSE_STAGE2");
-    if (KPL == 1 && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch && !(fz && fz[0] == '0')) {
+    if (KPL == 1 && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch && qp_launch_mode().fuse_stage2) {
         const size_t lds_f = std::max(lds, sizeof(double) * Lds(nullptr, kp.N, kp.M, 1).total);
         auto kern = lam_out ? dcm_mpc_cold_fused_kernel<true> : dcm_mpc_cold_fused_kernel<false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds_f, s, kp,

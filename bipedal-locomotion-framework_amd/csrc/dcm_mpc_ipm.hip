@@ -127,8 +127,7 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     // solves the QPs its start certifies; this kernel then takes only the rest (stage 2), from
     // scratch and without the start.  BLF_QP_SINGLE_KERNEL=1 keeps everything in this kernel
     // (A/B and parity tests: both ways give the same bits).
-    const char* single = getenv("BLF_QP_SINGLE_KERNEL");
-    if (kp.tol_polish > 0.0 && N <= 2 * kWave && !(single && single[0] == '1')) {
+    if (kp.tol_polish > 0.0 && N <= 2 * kWave && !qp_launch_mode().single_kernel) {
         bool stage2_done = false;
         const blf_status st = launch_dcm_mpc_as(kp, pb, warm, batch, sol, lam_out, s, nullptr, &stage2_done);
         if (st != BLF_OK || stage2_done) return st;

@@ -58,6 +58,10 @@ struct RobotModel
  *  fixedJoint.  Its rigid-body terms equal the full model's with the fixed joints held at
  *  q = 0, q_dot = 0 (blf/robot.py reduce_fixed_joints, tests/test_fb_dynamics.py). */
 RobotModel reduceFixedJoints(const RobotModel& model);
+/** Whether reduceFixedJoints can merge `model`: consistent array sizes (fixedJoint of ndof
+ *  entries), joints in topological order (parent[j] <= j), frames on existing links.  A model that
+ *  fails this comes back from reduceFixedJoints unchanged. */
+bool fixedJointMergeable(const RobotModel& model);
 } // namespace blf
 
 namespace BipedalLocomotion

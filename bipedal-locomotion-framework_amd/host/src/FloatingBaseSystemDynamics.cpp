@@ -32,12 +32,33 @@ bool FloatingBaseDynamicalSystem::initalize(std::weak_ptr<IParametersHandler> ha
     return true;
 }
 
+bool blf::fixedJointMergeable(const RobotModel& in)
+{
+    if (in.ndof < 0) return false;
+    const std::size_t n0 = static_cast<std::size_t>(in.ndof);
+    if (in.fixedJoint.size() != n0 || in.parent.size() != n0 || in.jointOrigin.size() != 3 * n0
+        || in.jointRotation.size() != 9 * n0 || in.jointAxis.size() != 3 * n0
+        || in.linkMass.size() != n0 + 1 || in.linkCom.size() != 3 * (n0 + 1)
+        || in.linkInertia.size() != 9 * (n0 + 1) || in.framePose.size() != 12 * in.frameLink.size()
+        || (!in.jointType.empty() && in.jointType.size() != n0))
+        return false;
+    // the merge re-indexes joints and links assuming topological order (a joint's parent link
+    // precedes its child: parent[j] <= j), and moves frames by link index
+    for (std::size_t j = 0; j < n0; ++j)
+        if (in.parent[j] < 0 || in.parent[j] > static_cast<int32_t>(j)) return false;
+    for (const int32_t l : in.frameLink)
+        if (l < 0 || l > static_cast<int32_t>(n0)) return false;
+    return true;
+}
+
 blf::RobotModel blf::reduceFixedJoints(const RobotModel& in)
 {
+    // an inconsistent model (sizes, order) comes back unchanged, its fixedJoint still set, so the
+    // caller's own validation (setRobotModel) reports it instead of a merge reading out of bounds
+    if (!fixedJointMergeable(in)) return in;
     RobotModel m = in;
     m.fixedJoint.clear();
     const int n0 = in.ndof;
-    if (in.fixedJoint.size() != static_cast<std::size_t>(n0)) return m;
     auto E = [&](int j, int r, int c) { return m.jointRotation[9 * j + 3 * r + c]; };
     // y = E_j x (3-vectors)
     auto rot = [&](int j, const double* x, double* y) {

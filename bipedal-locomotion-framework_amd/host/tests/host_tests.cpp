@@ -819,6 +819,18 @@ static std::array<double, 4> massAndCom(const blf::RobotModel& m)
 
 static void testFixedJoints()
 {
+    {   // inconsistent models come back unchanged: non-topological, wrong sizes
+        blf::RobotModel bad = chainModel();
+        bad.fixedJoint = {0, 1, 0};
+        bad.parent = {0, 2, 1};
+        REQUIRE_FALSE(blf::fixedJointMergeable(bad));
+        REQUIRE(blf::reduceFixedJoints(bad).fixedJoint.size() == 3);
+        bad = chainModel();
+        bad.fixedJoint = {0, 1, 0};
+        bad.linkMass.pop_back();
+        REQUIRE_FALSE(blf::fixedJointMergeable(bad));
+        REQUIRE(blf::reduceFixedJoints(bad).ndof == 3);
+    }
     blf::RobotModel full = chainModel();
     const blf::Matrix3 E1 = rpy(0.1, -0.2, 0.3);
     for (int k = 0; k < 9; ++k) full.jointRotation[9 + k] = E1[k];   // joint 1 mounted with a rotation

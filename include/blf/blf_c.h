@@ -83,6 +83,12 @@ blf_status blf_destroy(blf_handle* handle);
 const char* blf_last_error(void);
 /* Version string of the library (build id). */
 const char* blf_version(void);
+/* QP kernel routing for A/B and parity tests (no reference counterpart; the defaults are the
+ * product's).  fuse_stage2 = 0: small cold batches with N <= 64 run the IPM's stage 2 as its own
+ * launch instead of inside the active-set kernel; single_kernel = 1: every QP runs in the
+ * interior point kernel alone (no active-set kernel).  -1 leaves a setting unchanged.  The initial
+ * values come from BLF_QP_FUSE_STAGE2 / BLF_QP_SINGLE_KERNEL, read once at the first solve. */
+blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel);
 
 /* ---- 0. FixedStepIntegrator::integrate's step schedule (FixedStepIntegrator.tpp:21-72) -------
  * The validation (in the reference's order) and schedule every batched integrator below uses:

@@ -170,6 +170,11 @@ static double cross3(const double* o, const double* a, const double* b)
     return (a[0] - o[0]) * (b[1] - o[1]) - (a[1] - o[1]) * (b[0] - o[0]);
 }
 
+/* Test switch (tests/test_oracle.py): 1 forces Andrew's monotone chain for every point count, so
+ * the all-triples rule the device uses for up to 8 finite points can be compared with it. */
+static int g_hull_force_andrew = 0;
+void orc_hull2d_force_andrew(int on) { g_hull_force_andrew = on; }
+
 int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, double* b)
 {
     for (int i = 0; i < max_facets; ++i) { A[2 * i] = 0.0; A[2 * i + 1] = 0.0; b[i] = 0.0; }
@@ -190,7 +195,7 @@ int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, doub
     for (int i = 0; i < 2 * npts; ++i) finite = finite && isfinite(pts[i]);
     int H[34];
     int k = 0;
-    if (npts <= 8 && finite) {
+    if (npts <= 8 && finite && !g_hull_force_andrew) {
         /* Up to 8 finite points (the device's register path, hull2d_kernel): sorted point j
          * (0 < j < n - 1) is a lower-chain vertex iff cross3(p_i, p_j, p_k) > 0 for every
          * i < j < k < n, an upper-chain vertex iff cross3(p_k, p_j, p_i) > 0 for every such pair:

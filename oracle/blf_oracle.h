@@ -68,6 +68,7 @@ void orc_dcm_phase_expand(int P, int M, int nphases, const double* begin, const 
                           const double* pref, int64_t start, double dt, int N, double* A,
                           double* b, int32_t* nfacets, double* xi_ref, double* vrp_ref);
 
+void orc_hull2d_force_andrew(int on);
 int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);
 int orc_hull2d_contains(const double* A, const double* b, int nfacets, const double* p);
 int orc_hull3d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);

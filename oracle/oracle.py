@@ -172,6 +172,11 @@ def hull2d_hrep(pts, max_facets=8):
     return A, b, m
 
 
+def hull2d_force_andrew(on):
+    """Test switch: Andrew's monotone chain for every point count (orc_hull2d_force_andrew)."""
+    lib().orc_hull2d_force_andrew(int(bool(on)))
+
+
 def hull2d_contains(A, b, m, p):
     return bool(lib().orc_hull2d_contains(_d(_f64(A)), _d(_f64(b)), m, _d(_f64(p))))
 

@@ -168,3 +168,15 @@ def test_fixed_joints_argument_errors():
     same = robot.reduce_fixed_joints(MODEL, [])
     for k in ("parent", "joint_origin", "joint_rot", "link_inertia", "frame_pose"):
         np.testing.assert_array_equal(same[k], MODEL[k])
+
+
+def test_fixed_joints_reject_inconsistent_models():
+    """reduce_fixed_joints re-indexes in place, so a non-topological model or one with
+    inconsistent array sizes is refused instead of being merged wrong."""
+    bad = dict(MODEL, parent=np.array(MODEL["parent"]).copy())
+    bad["parent"][3] = 7                          # joint 3 hangs from a later link
+    with pytest.raises(ValueError, match="topological"):
+        robot.reduce_fixed_joints(bad, FIXED)
+    short = dict(MODEL, link_mass=np.asarray(MODEL["link_mass"])[:-1])
+    with pytest.raises(ValueError, match="link_mass"):
+        robot.reduce_fixed_joints(short, FIXED)

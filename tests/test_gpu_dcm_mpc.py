@@ -252,9 +252,10 @@ def test_dcm_mpc_polish_refusal_matches_oracle_bitwise(handle, oracle):
 
 
 @pytest.mark.parametrize("horizon", [40, 64])
-def test_dcm_mpc_fused_stage2_equals_two_launches(handle, oracle, horizon, monkeypatch):
+def test_dcm_mpc_fused_stage2_equals_two_launches(handle, oracle, horizon):
     """Small batches with N <= 64 run the IPM's stage 2 inside the active-set kernel's workgroup
-    (dcm_mpc_cold_fused_kernel, one launch); BLF_QP_FUSE_STAGE2=0 keeps the two launches.  Both
+    (dcm_mpc_cold_fused_kernel, one launch); blf_set_qp_launch_mode(fuse_stage2 = 0) keeps the two
+    launches.  Both
     give the oracle's bits, with QPs handed over (duplicated facet rows: the polish refuses) and
     an infeasible one."""
     B = 8
@@ -271,11 +272,14 @@ def test_dcm_mpc_fused_stage2_equals_two_launches(handle, oracle, horizon, monke
     prob["nfacets"][1, 10] = 2
     dev = _to_dev(prob)
     res = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("BLF_QP_FUSE_STAGE2", mode)
-        out = handle.dcm_mpc_solve(dev, lambda_out=True)
-        torch.cuda.synchronize()
-        res[mode] = {k: v.cpu().numpy().copy() for k, v in out.items()}
+    try:
+        for mode in ("1", "0"):
+            native.set_qp_launch_mode(fuse_stage2=int(mode))
+            out = handle.dcm_mpc_solve(dev, lambda_out=True)
+            torch.cuda.synchronize()
+            res[mode] = {k: v.cpu().numpy().copy() for k, v in out.items()}
+    finally:
+        native.set_qp_launch_mode(fuse_stage2=1)
     pol_o = np.zeros(B, np.int32)
     st_o, xi_o, vrp_o, it_o, lam_o = oracle.dcm_mpc_solve_batch_warm(prob, threads=4, polished=pol_o)
     assert not pol_o.all() and (st_o[0::2] == 0).all() and st_o[1] != 0
@@ -286,10 +290,10 @@ def test_dcm_mpc_fused_stage2_equals_two_launches(handle, oracle, horizon, monke
 
 
 @pytest.mark.parametrize("horizon,footsteps", [(100, 6), (50, 4), (128, 8), (126, 8), (65, 4)])
-def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, footsteps, monkeypatch):
+def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, footsteps):
     """The default path for N <= 128 (csrc/dcm_mpc_as.hip: one wavefront per QP, knot pairs per
     lane, then the IPM kernel's stage 2 on the QPs it hands over) and the IPM kernel alone
-    (BLF_QP_SINGLE_KERNEL=1, the wavefront scan tree) each equal the oracle evaluated the same way
+    (blf_set_qp_launch_mode(single_kernel = 1), the wavefront scan tree) each equal the oracle evaluated the same way
     bit for bit, cold and warm; the two trees agree to rounding (both are certified optima)."""
     B = 1024
     prob = P.make_batch(B, horizon=horizon, n_footsteps=footsteps, seed=5)
@@ -298,28 +302,31 @@ def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, fo
     for k in ("A", "b", "nfacets"):
         host[k] = dev[k].cpu().numpy()
     res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("BLF_QP_SINGLE_KERNEL", mode)
-        prm_o = oracle.default_params(horizon, single_kernel=int(mode))
-        out = handle.dcm_mpc_solve(dev, lambda_out=True)
-        torch.cuda.synchronize()
-        cold = {k: v.cpu().numpy().copy() for k, v in out.items()}
-        pol = np.zeros(B, np.int32)
-        st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(host, params=prm_o, threads=8, polished=pol)
-        for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
-                       ("polished", pol)):
-            np.testing.assert_array_equal(cold[k], ref, err_msg=f"cold {k} mode {mode}")
-        warm = dict(vrp=out["vrp"], lam=out["lam"], shift=1, floor=1e-3)
-        outw = handle.dcm_mpc_solve(dev, warm=warm, lambda_out=True)
-        torch.cuda.synchronize()
-        pol = np.zeros(B, np.int32)
-        st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(
-            host, vrp_ws=cold["vrp"], lam_ws=cold["lam"], shift=1, floor=1e-3, params=prm_o,
-            threads=8, polished=pol)
-        for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
-                       ("polished", pol)):
-            np.testing.assert_array_equal(outw[k].cpu().numpy(), ref, err_msg=f"warm {k} mode {mode}")
-        res[mode] = cold
+    try:
+        for mode in ("0", "1"):
+            native.set_qp_launch_mode(single_kernel=int(mode))
+            prm_o = oracle.default_params(horizon, single_kernel=int(mode))
+            out = handle.dcm_mpc_solve(dev, lambda_out=True)
+            torch.cuda.synchronize()
+            cold = {k: v.cpu().numpy().copy() for k, v in out.items()}
+            pol = np.zeros(B, np.int32)
+            st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(host, params=prm_o, threads=8, polished=pol)
+            for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
+                           ("polished", pol)):
+                np.testing.assert_array_equal(cold[k], ref, err_msg=f"cold {k} mode {mode}")
+            warm = dict(vrp=out["vrp"], lam=out["lam"], shift=1, floor=1e-3)
+            outw = handle.dcm_mpc_solve(dev, warm=warm, lambda_out=True)
+            torch.cuda.synchronize()
+            pol = np.zeros(B, np.int32)
+            st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(
+                host, vrp_ws=cold["vrp"], lam_ws=cold["lam"], shift=1, floor=1e-3, params=prm_o,
+                threads=8, polished=pol)
+            for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
+                           ("polished", pol)):
+                np.testing.assert_array_equal(outw[k].cpu().numpy(), ref, err_msg=f"warm {k} mode {mode}")
+            res[mode] = cold
+    finally:
+        native.set_qp_launch_mode(single_kernel=0)
     assert (res["0"]["status"] == 0).all()
     assert np.abs(res["0"]["xi"] - res["1"]["xi"]).max() <= 1e-12
     assert np.abs(res["0"]["vrp"] - res["1"]["vrp"]).max() <= 1e-12

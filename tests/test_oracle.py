@@ -363,3 +363,61 @@ def test_oracle_batch_drivers_match_single_item_calls():
         np.testing.assert_array_equal(co[s], c1)
         np.testing.assert_array_equal(pva[s], p1)
         np.testing.assert_array_equal(idx[s], i1)
+
+
+def _hull_is_tight(pts, A, b, m, tol):
+    """(A, b) of m facets is the convex hull of pts up to tol: every point satisfies every facet
+    (a . p - b <= tol) and every facet touches some point (min_p b - a . p <= tol)."""
+    if m < 0:
+        return False
+    g = pts @ A[:m].T - b[:m]            # [P, m]
+    return bool(g.max() <= tol and (-g).min(axis=0).max() <= tol)
+
+
+def test_hull2d_all_triples_vs_andrew_degenerate():
+    """up to 8 finite points the device chains the hull by the all-triples rule, which
+    is Andrew's monotone chain only in exact arithmetic.  On near-collinear, duplicate-heavy and
+    tiny-scale point sets both oracle paths (the all-triples rule, and Andrew's chain forced) must
+    give the convex hull up to rounding: every point inside both H-reps and every facet tight, at
+    1e-12 of the set's scale.  Where the two differ in facet count (a vertex within rounding of
+    collinear) the count is reported, bounded, and both are still the hull."""
+    rng = np.random.default_rng(7)
+    differ = 0
+    cases = 0
+    for kind in ("near_collinear", "duplicates", "tiny", "grid", "foot_union"):
+        for _ in range(3000):
+            n = int(rng.integers(3, 9))
+            if kind == "near_collinear":
+                t = rng.uniform(-1, 1, n)
+                pts = np.stack([t, 0.3 * t + rng.normal(0, 1e-13, n)], -1)
+                pts[0] += [0.0, 1e-3 * rng.choice([-1, 1])]      # one point off the line
+            elif kind == "duplicates":
+                base = rng.uniform(-1, 1, (max(2, n // 2), 2))
+                pts = base[rng.integers(0, base.shape[0], n)]
+                pts[: min(3, n)] = rng.uniform(-1, 1, (min(3, n), 2))
+            elif kind == "tiny":
+                pts = 1e-9 * rng.uniform(-1, 1, (n, 2)) + rng.uniform(-1, 1, 2)
+            elif kind == "grid":
+                pts = np.round(rng.uniform(-1, 1, (n, 2)) * 4) / 4
+            else:   # two slightly rotated feet (the workloads' double support), 8 corners
+                P = __import__("blf.problems", fromlist=["x"])
+                pose = np.array([[0.0, 0.1, rng.normal(0, 1e-3)], [rng.normal(0, 1e-6), -0.1, rng.normal(0, 1e-3)]])
+                pts = P.rectangle_corners(pose).reshape(8, 2)
+            scale = max(1.0, np.abs(pts).max())
+            tol = 1e-12 * scale
+            O.hull2d_force_andrew(False)
+            A1, b1, m1 = O.hull2d_hrep(pts)
+            O.hull2d_force_andrew(True)
+            A2, b2, m2 = O.hull2d_hrep(pts)
+            O.hull2d_force_andrew(False)
+            cases += 1
+            if m1 == -1 and m2 == -1:
+                continue   # degenerate (all points collinear): both refuse alike
+            assert (m1 == -1) == (m2 == -1), (kind, pts, m1, m2)
+            span = np.ptp(pts, axis=0).max()
+            if m1 > 0 and span > 1e3 * tol:
+                assert _hull_is_tight(pts, A1, b1, m1, tol), (kind, pts)
+                assert _hull_is_tight(pts, A2, b2, m2, tol), (kind, pts)
+            if m1 != m2 or not np.array_equal(b1, b2):
+                differ += 1
+    assert differ <= 0.02 * cases, (differ, cases)
