@@ -822,10 +822,21 @@ __device__ __forceinline__ void as_guess(AKnotT<T> (&K)[KPL], const RS& R, int N
 // certifies it; a failed pass drops the facets with negative multipliers, adds the violated ones
 // and restores the start point.  Returns true when a pass is certified (the point is then the
 // optimum, pk / pl its active facets and multipliers).
+// The candidate set of a knot's next pass: guessed and not dropped, or added (bit i, i < m).
+template <class T>
+__device__ __forceinline__ int as_cand(const AKnotT<T>& K)
+{
+    return ((K.gm & ~K.drop) | K.add) & ((1 << K.m) - 1);
+}
+
+// handover >= 0 (the fp32 search): a failed pass that changed the candidate sets of at most
+// `handover` knots ends the search, its next candidate sets going to the fp64 passes instead of
+// another float pass (oracle passes32): the last float pass before the
+// certifying one changes a few knots, and the fp64 passes certify that set.  -1: never.
 template <int KPL, int TR, class T, class RS>
 __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, const RS& R, int NH, int N,
                                           int lane, T xi00, T xi01, int (&pk)[KPL],
-                                          T (&pl)[KPL][2], int count_slot, int sb)
+                                          T (&pl)[KPL][2], int count_slot, int sb, int handover = -1)
 {
     T xk[KPL][2];
     as_xi_prev<KPL, T>(K, lane, xi00, xi01, xk);
@@ -835,10 +846,12 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
         AS_STAMP(t_s);
         T sv[KPL][4];
         T E[KPL][3];
+        int c0[KPL];
         bool okp = true;
 #pragma unroll
         for (int j = 0; j < KPL; ++j) {
             const int k = KPL * lane + j;
+            c0[j] = as_cand(K[j]);
             sv[j][0] = K[j].r0; sv[j][1] = K[j].r1; sv[j][2] = K[j].x0; sv[j][3] = K[j].x1;
             E[j][0] = E[j][1] = E[j][2] = T(0);
             pk[j] = 0;
@@ -902,6 +915,12 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
         }
         AS_STAMP_ADD(sb + 5, t_o);
         if (!more) break;
+        if (handover >= 0) {
+            int ch = 0;
+#pragma unroll
+            for (int j = 0; j < KPL; ++j) ch += __builtin_popcountll(__ballot(as_cand(K[j]) != c0[j]));
+            if (ch <= handover) break;
+        }
     }
     return certified;
 }
@@ -1217,6 +1236,7 @@ __device__ __forceinline__ void cold_solve(
     const float xf00 = float(xi00), xf01 = float(xi01);
     if (kOverlap) stage_rows_issue<U>(Ain, bin, p, lane, 0, nA, va, vb);
     AS_STAMP_ADD(1, t_start);
+    bool cert32 = false;   // the float search certified its point
     {
         AS_STAMP(t_q);
         as_lq_step<KPL, TR, float>(F, Pf, N, lane, xf00, xf01);
@@ -1230,7 +1250,7 @@ __device__ __forceinline__ void cold_solve(
         AS_STAMP(t_a);
         int pkf[KPL];
         float plf[KPL][2];
-        as_passes<KPL, TR, float>(F, Pf, R, NH, N, lane, xf00, xf01, pkf, plf, 12, 16);
+        cert32 = as_passes<KPL, TR, float>(F, Pf, R, NH, N, lane, xf00, xf01, pkf, plf, 12, 16, N / kHandoverDiv);
         AS_STAMP_ADD(13, t_a);
     }
 
@@ -1302,8 +1322,14 @@ __device__ __forceinline__ void cold_solve(
             K[j].x1 = K[j].xr1;
         }
     } else {
+        // the fp64 passes' guess: the facets active at a certified float point (slack below
+        // kGuessSlack); when the search stopped uncertified, its next candidate sets
         const double* const lw0[KPL] = {};
         as_guess<KPL, double>(K, R, NH, N, lane, lw0, 0.0, kGuessSlack);
+        if (!cert32) {
+#pragma unroll
+            for (int j = 0; j < KPL; ++j) K[j].gm = KPL * lane + j < N ? as_cand(F[j]) : 0;
+        }
         certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4);
         if (!certified) {
             // ---- the IPM's start point: the fp64 LQ optimum from (xi_ref, vrp_ref) ----

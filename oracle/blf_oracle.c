@@ -1941,17 +1941,18 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         double* r32 = (double*)malloc(sizeof(double) * 4 * (size_t)N);
         double* x32 = r32 + 2 * N;
         int* g32 = (int*)malloc(sizeof(int) * (size_t)N);
-        orc_as32_search(prm, prm->sequential, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets,
-                        r32, x32, g32);
+        const int cert32 = orc_as32_search(prm, prm->sequential, xi_init, omega, xi_ref, vrp_ref, Ain,
+                                           bin, nfacets, r32, x32, g32);
         for (int k = 0; k < N; ++k) {
             vrp[2 * k] = r32[2 * k];
             vrp[2 * k + 1] = r32[2 * k + 1];
             xi[2 * (k + 1)] = x32[2 * k];
             xi[2 * (k + 1) + 1] = x32[2 * k + 1];
         }
-        /* the fp64 passes' guess: the facets whose slack at the float point is below
-         * ORC_GUESS_SLACK (kernel kGuessSlack) */
-        for (int k = 0; k < N; ++k) {
+        /* the fp64 passes' guess: the facets whose slack at a certified float point is below
+         * ORC_GUESS_SLACK (kernel kGuessSlack); when the search stopped uncertified (its hand-over,
+         * or the pass cap), its next candidate sets as returned in g32 */
+        for (int k = 0; k < N && cert32; ++k) {
             int gk = 0;
             for (int i = 0; i < nfacets[k]; ++i) {
                 const double* a = Ain + (k * M + i) * 2;

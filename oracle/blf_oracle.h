@@ -112,10 +112,11 @@ void orc_quintic_batch(int64_t S, int K1, int dim, int Q, const double* knots_t,
                        int32_t* idx, int threads);
 
 /* The fp32 active-set search of a cold start as the device's active-set kernel runs it
- * (blf_oracle_as32.c): returns the float point (r [N][2], xi_{k+1} [N][2], as
- * doubles) and the search's active set (guess bits per knot) the fp64 passes start from.
+ * (blf_oracle_as32.c): returns 1 when a float pass certified, the float point
+ * (r [N][2], xi_{k+1} [N][2], as doubles) and the search's next candidate sets (guess bits per
+ * knot), which the fp64 passes start from when it did not certify.
  * sequential = 1: plain recursions instead of the kernel's scan tree (CPU baseline). */
-void orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_init,
+int orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_init,
                      const double* omega, const double* xi_ref, const double* vrp_ref,
                      const double* A, const double* b, const int32_t* nfacets, double* r_out,
                      double* x_out, int32_t* guess);

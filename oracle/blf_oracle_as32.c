@@ -552,7 +552,10 @@ static int vertex_pair32(const s32* s, int k, int km, int cm, int* pi1, int* pi2
 static int popc(int x) { int n = 0; while (x) { n += x & 1; x >>= 1; } return n; }
 static int ctz(int x) { int n = 0; while (!(x & 1)) { ++n; x >>= 1; } return n; }
 
-/* as_passes (float): returns 1 when a pass certifies */
+/* as_passes (float): returns 1 when a pass certifies.  A failed pass that changed the candidate
+ * sets of at most N / ORC_HANDOVER_DIV knots ends the search (the kernel's handover): its next
+ * candidate sets go to the fp64 passes (orc_dcm_mpc_solve_warm) instead of another float pass. */
+#define ORC_HANDOVER_DIV 16   /* kernel kHandoverDiv */
 static int passes32(s32* s)
 {
     const int N = s->N;
@@ -561,6 +564,7 @@ static int passes32(s32* s)
         vn[2 * WV][2];
     static __thread int pk[2 * WV];
     xi_prev32(s, xk);
+    static __thread int cand0[2 * WV];
     for (int pass = 0; pass < PASSES; ++pass) {
         int okp = 1, neg = 0, viol = 0;
         for (int k = 0; k < 2 * WV; ++k) { E[k][0] = E[k][1] = E[k][2] = 0.0f; pk[k] = 0; }
@@ -569,6 +573,7 @@ static int passes32(s32* s)
             sv[k][0] = s->r0[k]; sv[k][1] = s->r1[k]; sv[k][2] = s->x0[k]; sv[k][3] = s->x1[k];
             const int km = s->m[k];
             const int cm = ((s->gm[k] & ~s->drop[k]) | s->add[k]) & ((1 << km) - 1);
+            cand0[k] = cm;
             int pc = popc(cm);
             const int cm2 = cm & (cm - 1);
             int pi1 = cm ? ctz(cm) : 0;
@@ -675,11 +680,15 @@ static int passes32(s32* s)
             s->r0[k] = sv[k][0]; s->r1[k] = sv[k][1]; s->x0[k] = sv[k][2]; s->x1[k] = sv[k][3];
         }
         if (!(neg || viol)) break;
+        int ch = 0;
+        for (int k = 0; k < N; ++k)
+            ch += (((s->gm[k] & ~s->drop[k]) | s->add[k]) & ((1 << s->m[k]) - 1)) != cand0[k];
+        if (ch <= N / ORC_HANDOVER_DIV) break;
     }
     return 0;
 }
 
-void orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_init,
+int orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_init,
                      const double* omega, const double* xi_ref, const double* vrp_ref,
                      const double* A, const double* b, const int32_t* nfacets, double* r_out,
                      double* x_out, int32_t* guess)
@@ -727,7 +736,7 @@ void orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi
         }
         s->gm[k] = gm;
     }
-    passes32(s);
+    const int cert = passes32(s);
     for (int k = 0; k < N; ++k) {
         r_out[2 * k] = (double)s->r0[k];
         r_out[2 * k + 1] = (double)s->r1[k];
@@ -735,4 +744,5 @@ void orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi
         x_out[2 * k + 1] = (double)s->x1[k];
         guess[k] = ((s->gm[k] & ~s->drop[k]) | s->add[k]) & ((1 << s->m[k]) - 1);
     }
+    return cert;
 }
