@@ -288,8 +288,8 @@ blf_status blf_dcm_phase_expand(blf_handle* handle, const blf_phase_table* ph,
     BLF_REQUIRE(handle != nullptr, "blf_dcm_phase_expand: null handle");
     BLF_REQUIRE(ph != nullptr, "blf_dcm_phase_expand: null phase table");
     BLF_REQUIRE(ph->max_phases >= 1, "blf_dcm_phase_expand: max_phases %d < 1", ph->max_phases);
-    BLF_REQUIRE(ph->max_facets >= 1 && ph->max_facets <= kMaxFacets,
-                "blf_dcm_phase_expand: max_facets %d outside [1, %d]", ph->max_facets, kMaxFacets);
+    BLF_REQUIRE(ph->max_facets >= 1 && ph->max_facets <= kMaxFacetsWide,
+                "blf_dcm_phase_expand: max_facets %d outside [1, %d]", ph->max_facets, kMaxFacetsWide);
     BLF_REQUIRE(horizon >= 1, "blf_dcm_phase_expand: horizon %d < 1", horizon);
     BLF_REQUIRE(dt > 0 && std::isfinite(dt), "blf_dcm_phase_expand: dt must be finite and > 0");
     BLF_REQUIRE(start_knot >= 0, "blf_dcm_phase_expand: start_knot < 0");
@@ -311,8 +311,8 @@ blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* 
     BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve: null handle");
     BLF_REQUIRE(params && problem && solution, "blf_dcm_mpc_solve: null argument");
     BLF_REQUIRE(params->horizon >= 1, "blf_dcm_mpc_solve: horizon %d < 1", params->horizon);
-    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacets,
-                "blf_dcm_mpc_solve: max_facets %d outside [1, %d]", params->max_facets, kMaxFacets);
+    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacetsWide,
+                "blf_dcm_mpc_solve: max_facets %d outside [1, %d]", params->max_facets, kMaxFacetsWide);
     BLF_REQUIRE(params->max_iter >= 0, "blf_dcm_mpc_solve: max_iter < 0");
     BLF_REQUIRE(params->reserved == 0, "blf_dcm_mpc_solve: reserved must be 0");
     BLF_REQUIRE(params->dt > 0, "blf_dcm_mpc_solve: dt must be > 0");
@@ -367,8 +367,8 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
                     "blf_dcm_mpc_solve_phased: horizon %d outside [1, 128]", params->horizon);
         BLF_REQUIRE(params->tol_polish > 0, "blf_dcm_mpc_solve_phased: tol_polish must be > 0");
     }
-    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacets,
-                "blf_dcm_mpc_solve_phased: max_facets %d outside [1, %d]", params->max_facets, kMaxFacets);
+    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacetsWide,
+                "blf_dcm_mpc_solve_phased: max_facets %d outside [1, %d]", params->max_facets, kMaxFacetsWide);
     BLF_REQUIRE(params->max_iter >= 0, "blf_dcm_mpc_solve_phased: max_iter < 0");
     BLF_REQUIRE(params->reserved == 0, "blf_dcm_mpc_solve_phased: reserved must be 0");
     BLF_REQUIRE(params->dt > 0 && std::isfinite(params->dt), "blf_dcm_mpc_solve_phased: dt must be finite and > 0");

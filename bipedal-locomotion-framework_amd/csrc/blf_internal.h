@@ -12,7 +12,8 @@
 namespace blf {
 
 constexpr int kWave = 64;   // CDNA wavefront width
-constexpr int kMaxFacets = 8;
+constexpr int kMaxFacets = 8;       // facet slots per knot of the active-set kernels (and the default)
+constexpr int kMaxFacetsWide = 16;  // max_facets up to this: the interior point kernel alone
 
 // ---- error plumbing (blf_capi.hip) ----
 blf_status set_error(blf_status code, const char* fmt, ...);

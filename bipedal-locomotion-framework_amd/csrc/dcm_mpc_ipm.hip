@@ -21,11 +21,15 @@
 // DESIGN.md section 4 is the algorithm statement.
 #include "dcm_mpc_ipm_body.h"
 
+// The 16-slot instantiations (max_facets > 8) keep their facet loops rolled where the unroller
+// gives up; that is expected, not a defect.
+#pragma clang diagnostic ignored "-Wpass-failed"
+
 namespace blf {
 namespace {
 using namespace qp;
 
-template <int NT, bool WARM, bool LAMOUT>
+template <int NT, bool WARM, bool LAMOUT, int MF>
 __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_ipm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -35,11 +39,13 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     double* __restrict__ vrp_out, int32_t* __restrict__ status_out,
     int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out)
 {
-    ipm_solve<NT, WARM, LAMOUT>(P, blockIdx.x, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, ws_vrp,
+    ipm_solve<NT, WARM, LAMOUT, MF>(P, blockIdx.x, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, ws_vrp,
                                 ws_lam, xi_out, vrp_out, status_out, iters_out, polished_out, lam_out);
 }
 
-template <int NT>
+// MF facet slots per knot in the registers: 8, or 16 when max_facets > 8 (support polygons of up
+// to four contacts; those QPs run in this kernel alone, without the active-set kernel)
+template <int NT, int MF = kMaxFacets>
 blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
                      const blf_dcm_mpc_warm_start* warm, int64_t batch,
                      const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
@@ -49,8 +55,8 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
         return set_error(BLF_ERR_UNSUPPORTED, "horizon %d with %d facet slots needs %zu B of LDS",
                          kp.N, kp.M, lds);
     auto kern = (warm != nullptr)
-                    ? (lam_out ? dcm_mpc_ipm_kernel<NT, true, true> : dcm_mpc_ipm_kernel<NT, true, false>)
-                    : (lam_out ? dcm_mpc_ipm_kernel<NT, false, true> : dcm_mpc_ipm_kernel<NT, false, false>);
+                    ? (lam_out ? dcm_mpc_ipm_kernel<NT, true, true, MF> : dcm_mpc_ipm_kernel<NT, true, false, MF>)
+                    : (lam_out ? dcm_mpc_ipm_kernel<NT, false, true, MF> : dcm_mpc_ipm_kernel<NT, false, false, MF>);
     hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(NT), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                        pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr,
@@ -106,6 +112,13 @@ blf_status launch_ipm(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
                       int64_t batch, const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
 {
     const int N = kp.N;
+    if (kp.M > kMaxFacets) {
+        if (N <= 64) return launch_nt<64, kMaxFacetsWide>(kp, pb, warm, batch, sol, lam_out, s);
+        if (N <= 128) return launch_nt<128, kMaxFacetsWide>(kp, pb, warm, batch, sol, lam_out, s);
+        if (N <= 256) return launch_nt<256, kMaxFacetsWide>(kp, pb, warm, batch, sol, lam_out, s);
+        return set_error(BLF_ERR_UNSUPPORTED, "horizon %d > 256 with %d facet slots (> %d)", N, kp.M,
+                         kMaxFacets);
+    }
     if (N <= 64) return launch_nt<64>(kp, pb, warm, batch, sol, lam_out, s);
     if (N <= 128) return launch_nt<128>(kp, pb, warm, batch, sol, lam_out, s);
     if (N <= 256) return launch_nt<256>(kp, pb, warm, batch, sol, lam_out, s);
@@ -127,7 +140,7 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     // solves the QPs its start certifies; this kernel then takes only the rest (stage 2), from
     // scratch and without the start.  BLF_QP_SINGLE_KERNEL=1 keeps everything in this kernel
     // (A/B and parity tests: both ways give the same bits).
-    if (kp.tol_polish > 0.0 && N <= 2 * kWave && !qp_launch_mode().single_kernel) {
+    if (kp.tol_polish > 0.0 && N <= 2 * kWave && kp.M <= kMaxFacets && !qp_launch_mode().single_kernel) {
         bool stage2_done = false;
         const blf_status st = launch_dcm_mpc_as(kp, pb, warm, batch, sol, lam_out, s, nullptr, &stage2_done);
         if (st != BLF_OK || stage2_done) return st;
@@ -152,6 +165,21 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
         return set_error(BLF_ERR_UNSUPPORTED,
                          "phase-indexed solve: horizon %d > 128 or tol_polish = 0 (use blf_dcm_phase_expand "
                          "+ blf_dcm_mpc_solve_warm)", kp.N);
+    if (kp.M > kMaxFacets) {
+        // more facet slots than the active-set kernels hold (phases of up to four contacts): the
+        // window expanded into the caller's scratch, then the interior point kernel's solve of it
+        // (the same bits as blf_dcm_phase_expand + blf_dcm_mpc_solve_warm)
+        blf_status st = launch_phase_expand(ph->max_phases, ph->nphases, ph->begin, ph->end, ph->A, ph->b,
+                                            ph->nfacets, ph->ref, kp.M, start_knot, kp.dt, kp.N, batch, win->A,
+                                            win->b, win->nfacets, win->xi_ref, win->vrp_ref, s);
+        if (st != BLF_OK) return st;
+        st = check_hip(hipMemcpy2DAsync(win->omega, sizeof(double) * kp.N, omega, sizeof(double) * omega_stride,
+                                        sizeof(double) * kp.N, (size_t)batch, hipMemcpyDeviceToDevice, s),
+                       "phase-indexed solve: omega copy");
+        if (st != BLF_OK) return st;
+        const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
+        return launch_dcm_mpc(prm, &pw, warm, batch, sol, lam_out, s);
+    }
     PhaseSrc ps{};
     ps.P = ph->max_phases;
     ps.nphases = ph->nphases;

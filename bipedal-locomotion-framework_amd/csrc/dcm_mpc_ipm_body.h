@@ -306,10 +306,13 @@ __device__ __forceinline__ void scan_forward(double g0, double g1, double g2, do
     }
 }
 
-// Per-knot state (registers of the knot's thread).
-struct Knot {
+// Per-knot state (registers of the knot's thread); MF facet slots (8, or 16 for phases of up to
+// four contacts, max_facets > 8).
+template <int MF>
+struct KnotT {
+    static constexpr int kMF = MF;
     int m;                                      // facet count
-    double s[kMaxFacets], lam[kMaxFacets];
+    double s[MF], lam[MF];
     double r0, r1;                              // VRP
     double x0, x1;                              // xi_{k+1}
     double w, al, be;                           // omega_k, 1 + dt omega_k, dt omega_k
@@ -321,7 +324,8 @@ struct Knot {
 // M = P_{k+1} H_k^{-1} (recomputed where needed: cheaper than 8 live VGPRs).
 struct Mmat {
     double m00, m01, m10, m11;
-    __device__ __forceinline__ explicit Mmat(const Knot& K)
+    template <class KN>
+    __device__ __forceinline__ explicit Mmat(const KN& K)
     {
         m00 = FD2(K.P00, K.h00, K.P01, K.h01);
         m01 = FD2(K.P00, K.h01, K.P01, K.h11);
@@ -331,13 +335,15 @@ struct Mmat {
 };
 
 // Facet residual rp_i = (a . r + s_i) - b_i.
-__device__ __forceinline__ double facet_rp(const Knot& K, double2 a, double bi, int i)
+template <class KN>
+__device__ __forceinline__ double facet_rp(const KN& K, double2 a, double bi, int i)
 {
     return (FD2(a.x, K.r0, a.y, K.r1) + K.s[i]) - bi;
 }
 
 // The affine slack / multiplier step of facet i for the VRP step (dra0, dra1) (oracle affine_step).
-__device__ __forceinline__ void affine_step(const Knot& K, double2 a, double bi, double is, int i,
+template <class KN>
+__device__ __forceinline__ void affine_step(const KN& K, double2 a, double bi, double is, int i,
                                             double dra0, double dra1, double& ds, double& dl)
 {
     const double rpi = facet_rp(K, a, bi, i);
@@ -346,7 +352,8 @@ __device__ __forceinline__ void affine_step(const Knot& K, double2 a, double bi,
 }
 
 // Residual pass (oracle dcm_residuals) for this lane's knot; xk = xi_k.  Returns pres, ck.
-__device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P, bool last,
+template <class KN>
+__device__ __forceinline__ void residuals(KN& K, bool facets, const KParams& P, bool last,
                                           const double2* A2, const double2* BI, int N, int k,
                                           int mmax, double xk0, double xk1, const double* rref,
                                           const double* xref, double& pres, double& ck)
@@ -359,7 +366,7 @@ __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P
         const int kx = opaque(k);
         const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
-        for (int i = 0; i < kMaxFacets; ++i) {
+        for (int i = 0; i < KN::kMF; ++i) {
             if (i >= mm) break;
             if (i < km) {
                 const double2 a = A2[i * N + kx];
@@ -391,7 +398,8 @@ __device__ __forceinline__ void residuals(Knot& K, bool facets, const KParams& P
 // xi_k of this lane's knot: xi_{k+1} of the previous lane; lane 0 takes the wavefront's left boundary
 // xb = xi_{64 w}, which every wavefront tracks itself (from the forward scans' boundary values, with
 // the same arithmetic as the previous wavefront's last lane), so no barrier publishes it.
-__device__ __forceinline__ void xi_prev(const Knot& K, int lane, double xb0, double xb1, double& xk0,
+template <class KN>
+__device__ __forceinline__ void xi_prev(const KN& K, int lane, double xb0, double xb1, double& xk0,
                                         double& xk1)
 {
     xk0 = dpp1<kPrevWrap>(K.x0);
@@ -404,8 +412,8 @@ __device__ __forceinline__ void xi_prev(const Knot& K, int lane, double xb0, dou
 
 // Riccati sweep (oracle riccati_sweep) for this lane's E_k.  Leaves P_{k+1} in K.  Returns false
 // on this lane if some (I + G H) or (I + G P) is not positive definite.
-template <int NW>
-__device__ __forceinline__ bool riccati(Knot& K, const KParams& P, double E00, double E01,
+template <int NW, class KN>
+__device__ __forceinline__ bool riccati(KN& K, const KParams& P, double E00, double E01,
                                         double E11, double* bnd, int N, int nwa, int k, int wv,
                                         int lane, bool own)
 {
@@ -480,8 +488,8 @@ __device__ __forceinline__ bool riccati(Knot& K, const KParams& P, double E00, d
 
 // Factorization (oracle dcm_factor) from W = (W00, W01, W11, detW).  Leaves P_{k+1}, h, M in K.
 // Returns false on this lane if its K or H block is not positive definite.
-template <int NW>
-__device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, double W01,
+template <int NW, class KN>
+__device__ __forceinline__ bool factor(KN& K, const KParams& P, double W00, double W01,
                                        double W11, double dW, double* bnd, int N, int nwa, int k,
                                        int wv, int lane, bool own)
 {
@@ -517,8 +525,8 @@ __device__ __forceinline__ bool factor(Knot& K, const KParams& P, double W00, do
 // Solve the factored Newton system for the right-hand side g (oracle dcm_solve).  Returns
 // dr (the VRP step of this knot), dx (the DCM step of xi_{k+1}), v_{k+1} of the backward scan and
 // the DCM step of xi_k (lane 0 of a wavefront: its left boundary, from the previous wavefront).
-template <int NW>
-__device__ __forceinline__ void solve(const Knot& K, double g0, double g1, double* bnd, int nwa,
+template <int NW, class KN>
+__device__ __forceinline__ void solve(const KN& K, double g0, double g1, double* bnd, int nwa,
                                       int wv, int lane, bool own, double& dr0, double& dr1, double& dx0,
                                       double& dx1, double& vn0, double& vn1, double& xk0, double& xk1)
 {
@@ -571,8 +579,8 @@ __device__ __forceinline__ void solve(const Knot& K, double g0, double g1, doubl
 #define BLF_SAT_ON 1
 #endif
 constexpr int kBS = 12;   // bnd slot: the rollout's xi at the end of wavefront w
-template <int NW>
-__device__ __forceinline__ bool sat_start(Knot& K, const KParams& P, const Lds& L, Reduce<NW>& R, double* bnd,
+template <int NW, class KN>
+__device__ __forceinline__ bool sat_start(KN& K, const KParams& P, const Lds& L, Reduce<NW>& R, double* bnd,
                                           int N, int nwa, int k, int wv, int lane, bool own, bool last,
                                           int mmax, double xi00, double xi01, const double* rref,
                                           const double* xref, double& xb0, double& xb1, double& mu,
@@ -593,16 +601,6 @@ __device__ __forceinline__ bool sat_start(Knot& K, const KParams& P, const Lds& 
     const double B00 = fma(b2, K.P00, P.Rw0);
     const double B01 = b2 * K.P01;
     const double B11 = fma(b2, K.P11, P.Rw1);
-    // this lane's projection candidate: lanes 0..7 facet `lane`, lanes 8..35 the facet pair
-    // (cx, cy), cx < cy, in lexicographic order
-    int cx = lane, cy = lane;
-    if (lane >= kMaxFacets) {
-        int q = lane - kMaxFacets;
-        cx = 0;
-        while (cx < kMaxFacets - 1 && q >= kMaxFacets - 1 - cx) { q -= kMaxFacets - 1 - cx; ++cx; }
-        cy = cx + 1 + q;
-    }
-    const bool pair_lane = lane >= kMaxFacets && lane < kMaxFacets + kMaxFacets * (kMaxFacets - 1) / 2;
     // 2. the rollout
     int sc = 0, s1 = 0, s2 = 0;   // this knot's projected facets
     for (int w = 0; w < nwa; ++w) {
@@ -633,49 +631,67 @@ __device__ __forceinline__ bool sat_start(Knot& K, const KParams& P, const Lds& 
                 double r0 = t0, r1 = t1;
                 int c = 0, i1 = 0, i2 = 0;
                 if (!inside) {
-                    bool valid = false;
-                    double v0 = 0.0, v1 = 0.0, dist = 0.0;
-                    if (lane < m) {
-                        const double2 a = L.A2[lane * N + kk];
-                        const double u0 = fma(c11, a.x, -(c01 * a.y));
-                        const double u1 = fma(c00, a.y, -(c01 * a.x));
-                        const double aua = FD2(a.x, u0, a.y, u1);
-                        const double viol = FD2(a.x, t0, a.y, t1) - L.BI[lane * N + kk].x;
-                        const double t = viol / aua;
-                        v0 = fma(-t, u0, t0);
-                        v1 = fma(-t, u1, t1);
-                        valid = viol > 0.0;
-                        dist = (t * viol) * fma(c00, c11, -(c01 * c01));
-                    } else if (pair_lane && cy < m) {
-                        const double2 a = L.A2[cx * N + kk];
-                        const double2 e = L.A2[cy * N + kk];
-                        const double ba = L.BI[cx * N + kk].x, be = L.BI[cy * N + kk].x;
-                        const double det = fma(a.x, e.y, -(a.y * e.x));
-                        const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
-                        valid = det * det > 1e-18 * (aa * ee);
-                        const double idet = 1.0 / det;
-                        v0 = fma(ba, e.y, -(a.y * be)) * idet;
-                        v1 = fma(a.x, be, -(ba * e.x)) * idet;
-                        const double e0 = v0 - t0, e1 = v1 - t1;
-                        dist = fma(e0, fma(c00, e0, 2.0 * (c01 * e1)), (c11 * e1) * e1);
-                    }
-                    if (valid) {
-                        for (int l = 0; l < m; ++l) {
-                            const double2 f = L.A2[l * N + kk];
-                            if (!(FD2(f.x, v0, f.y, v1) - L.BI[l * N + kk].x <= P.tol_p)) valid = false;
+                    // the candidates, one per lane in rounds of 64: c < m facet c; c >= m the
+                    // facet pair q = c - m of (x, y), x < y < m, in lexicographic order
+                    const int nc = m + (m * (m - 1)) / 2;
+                    bool have = false;
+                    double best = 0.0;
+                    for (int c0 = 0; c0 < nc; c0 += kWave) {
+                        const int cc = c0 + lane;
+                        int cx = cc, cy = cc;
+                        if (cc >= m) {
+                            int q = cc - m;
+                            cx = 0;
+                            while (cx < m - 1 && q >= m - 1 - cx) { q -= m - 1 - cx; ++cx; }
+                            cy = cx + 1 + q;
                         }
-                    }
-                    if (!(dist == dist)) valid = false;
-                    const double key = valid ? dist : __builtin_inf();
-                    const double kmin = wave_keepmin(key);
-                    const unsigned long long win = __ballot(valid && key == kmin);
-                    if (win != 0ull) {
-                        const int f = __builtin_ctzll(win);
-                        r0 = readlane_f64(v0, f);
-                        r1 = readlane_f64(v1, f);
-                        i1 = __builtin_amdgcn_readlane(cx, f);
-                        i2 = __builtin_amdgcn_readlane(cy, f);
-                        c = f < kMaxFacets ? 1 : 2;
+                        bool valid = false;
+                        double v0 = 0.0, v1 = 0.0, dist = 0.0;
+                        if (cc < m) {
+                            const double2 a = L.A2[cx * N + kk];
+                            const double u0 = fma(c11, a.x, -(c01 * a.y));
+                            const double u1 = fma(c00, a.y, -(c01 * a.x));
+                            const double aua = FD2(a.x, u0, a.y, u1);
+                            const double viol = FD2(a.x, t0, a.y, t1) - L.BI[cx * N + kk].x;
+                            const double t = viol / aua;
+                            v0 = fma(-t, u0, t0);
+                            v1 = fma(-t, u1, t1);
+                            valid = viol > 0.0;
+                            dist = (t * viol) * fma(c00, c11, -(c01 * c01));
+                        } else if (cc < nc) {
+                            const double2 a = L.A2[cx * N + kk];
+                            const double2 e = L.A2[cy * N + kk];
+                            const double ba = L.BI[cx * N + kk].x, be = L.BI[cy * N + kk].x;
+                            const double det = fma(a.x, e.y, -(a.y * e.x));
+                            const double aa = FD2(a.x, a.x, a.y, a.y), ee = FD2(e.x, e.x, e.y, e.y);
+                            valid = det * det > 1e-18 * (aa * ee);
+                            const double idet = 1.0 / det;
+                            v0 = fma(ba, e.y, -(a.y * be)) * idet;
+                            v1 = fma(a.x, be, -(ba * e.x)) * idet;
+                            const double e0 = v0 - t0, e1 = v1 - t1;
+                            dist = fma(e0, fma(c00, e0, 2.0 * (c01 * e1)), (c11 * e1) * e1);
+                        }
+                        if (valid) {
+                            for (int l = 0; l < m; ++l) {
+                                const double2 f = L.A2[l * N + kk];
+                                if (!(FD2(f.x, v0, f.y, v1) - L.BI[l * N + kk].x <= P.tol_p)) valid = false;
+                            }
+                        }
+                        if (!(dist == dist)) valid = false;
+                        const double key = valid ? dist : __builtin_inf();
+                        const double kmin = wave_keepmin(key);
+                        const unsigned long long win = __ballot(valid && key == kmin);
+                        // the first of equal distances wins: a later round only with a smaller one
+                        if (win != 0ull && (!have || kmin < best)) {
+                            const int f = __builtin_ctzll(win);
+                            have = true;
+                            best = kmin;
+                            r0 = readlane_f64(v0, f);
+                            r1 = readlane_f64(v1, f);
+                            i1 = __builtin_amdgcn_readlane(cx, f);
+                            i2 = __builtin_amdgcn_readlane(cy, f);
+                            c = c0 + f < m ? 1 : 2;
+                        }
                     }
                 }
                 const double om = readlane_f64(K.w, j);
@@ -731,7 +747,7 @@ __device__ __forceinline__ bool sat_start(Knot& K, const KParams& P, const Lds& 
         // every slot written (the unused ones to their initial 1 / 0), so the old values are dead
         // during the rollout
 #pragma unroll
-        for (int i = 0; i < kMaxFacets; ++i) {
+        for (int i = 0; i < KN::kMF; ++i) {
             K.s[i] = 1.0;
             K.lam[i] = 0.0;
             if (i < km) {
@@ -764,7 +780,7 @@ __device__ __forceinline__ bool sat_start(Knot& K, const KParams& P, const Lds& 
 #endif
 // The solve of QP p by one workgroup of NT threads (the kernel below; the active-set kernel's
 // fused stage 2 for N <= 64, dcm_mpc_as.hip, calls it from its own 64-thread workgroup).
-template <int NT, bool WARM, bool LAMOUT>
+template <int NT, bool WARM, bool LAMOUT, int MF = kMaxFacets>
 __device__ __forceinline__ void ipm_solve(
     const KParams P, const int64_t p, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -796,13 +812,13 @@ __device__ __forceinline__ void ipm_solve(
     STAMP(t_start);
 
     // ---- load the knot this thread owns ----
-    Knot K;
+    KnotT<MF> K;
     K.m = 0;
     K.r0 = K.r1 = K.x0 = K.x1 = K.w = K.be = 0.0;
     K.rh0 = K.rh1 = K.d0 = K.d1 = K.qx0 = K.qx1 = 0.0;
     K.P00 = K.P01 = K.P11 = K.h00 = K.h01 = K.h11 = 0.0;
 #pragma unroll
-    for (int i = 0; i < kMaxFacets; ++i) { K.s[i] = 1.0; K.lam[i] = 0.0; }
+    for (int i = 0; i < MF; ++i) { K.s[i] = 1.0; K.lam[i] = 0.0; }
     bool bad = false;
     const double xi00 = xi_init[2 * p], xi01 = xi_init[2 * p + 1];
     if (own) {
@@ -923,7 +939,7 @@ __device__ __forceinline__ void ipm_solve(
             const double* lw = ws_lam + (ws ? (p * N + k + P.ws_shift) * M : 0);
             double al0 = 0.0, al1 = 0.0;   // A^T lam
 #pragma unroll
-            for (int i = 0; i < kMaxFacets; ++i) {
+            for (int i = 0; i < MF; ++i) {
                 if (i >= mmax) break;
                 if (i < K.m) {
                     const double2 a = L.A2[i * N + k];
@@ -1025,13 +1041,13 @@ __device__ __forceinline__ void ipm_solve(
                     double lmx = 0.0;   // the knot's largest multiplier (the IPM guess's scale)
                     if (!guess) {
 #pragma unroll
-                        for (int i = 0; i < kMaxFacets; ++i) {
+                        for (int i = 0; i < MF; ++i) {
                             if (i >= mm) break;
                             if (i < km) lmx = keepmax(lmx, K.lam[i]);
                         }
                     }
 #pragma unroll
-                    for (int i = 0; i < kMaxFacets; ++i) {
+                    for (int i = 0; i < MF; ++i) {
                         if (i >= mm) break;
                         const bool base = guess ? ((gk >> i) & 1) != 0
                                                 : (K.lam[i] > K.s[i] && K.lam[i] >= kLamRel * lmx);
@@ -1044,7 +1060,7 @@ __device__ __forceinline__ void ipm_solve(
                     }
                     if (pc > 2) pc = vertex_pair(L.A2, reinterpret_cast<const double*>(L.BI), 2, N, kx, km, cm, P.tol_p, pi1, pi2);
                     okp = pc <= 2;
-                    pk = (pc < 3 ? pc : 2) | (pi1 << 2) | (pi2 << 5);
+                    pk = (pc < 3 ? pc : 2) | (pi1 << 2) | (pi2 << 6);
                     const double b2 = K.be * K.be;
                     if (pc == 0) {
                         E00 = b2 / P.Rw0;
@@ -1080,8 +1096,8 @@ __device__ __forceinline__ void ipm_solve(
                 STAMP_ADD(14, t_pr);
                 pk = opaque(pk);
                 pc = pk & 3;
-                pi1 = (pk >> 2) & 7;
-                pi2 = (pk >> 5) & 7;
+                pi1 = (pk >> 2) & 15;
+                pi2 = (pk >> 6) & 15;
                 if (own) {
                     const double b2 = K.be * K.be;
                     const double B00 = fma(b2, K.P00, P.Rw0);
@@ -1173,7 +1189,7 @@ __device__ __forceinline__ void ipm_solve(
                         const int km = opaque(K.m), mm = opaque_s(mmax);
                         int vm = 0;
 #pragma unroll
-                        for (int i0 = 0; i0 < kMaxFacets; i0 += 4) {
+                        for (int i0 = 0; i0 < MF; i0 += 4) {
                             if (i0 >= mm) break;
                             double2 av[4];
                             double bv[4];
@@ -1214,7 +1230,7 @@ __device__ __forceinline__ void ipm_solve(
                         const int kx = opaque(k);
                         const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
-                        for (int i = 0; i < kMaxFacets; ++i) {
+                        for (int i = 0; i < MF; ++i) {
                             if (i >= mm) break;
                             if (i < km) {
                                 const double2 a = L.A2[i * N + kx];
@@ -1236,7 +1252,7 @@ __device__ __forceinline__ void ipm_solve(
                         pl1 = pl1 > 0.0 ? pl1 : 0.0;
                         pl2 = pl2 > 0.0 ? pl2 : 0.0;
 #pragma unroll
-                        for (int i = 0; i < kMaxFacets; ++i)
+                        for (int i = 0; i < MF; ++i)
                             K.lam[i] = (pc >= 1 && i == pi1) ? pl1 : (pc == 2 && i == pi2) ? pl2 : 0.0;
                     }
                     polished = 1;
@@ -1288,7 +1304,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int kx = opaque(k);
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
-                for (int i = 0; i < kMaxFacets; ++i) {
+                for (int i = 0; i < MF; ++i) {
                     if (i >= mm) break;
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
@@ -1309,7 +1325,7 @@ __device__ __forceinline__ void ipm_solve(
                 // sg_i = lam_i / s_i is recomputed from the stored 1/s (bit-identical) rather than
                 // kept in an 8-entry register array across the pair loop (which spilled)
 #pragma unroll
-                for (int i = 1; i < kMaxFacets; ++i) {
+                for (int i = 1; i < MF; ++i) {
                     if (i >= mm) break;
                     if (i < km) {
                         const int ki = opaque(k);
@@ -1342,7 +1358,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int kx = opaque(k);
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
-                for (int i = 0; i < kMaxFacets; ++i) {
+                for (int i = 0; i < MF; ++i) {
                     if (i >= mm) break;
                     if (i < km) {
                         double ds, dl;
@@ -1377,7 +1393,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int kx = opaque(k);
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
-                for (int i = 0; i < kMaxFacets; ++i) {
+                for (int i = 0; i < MF; ++i) {
                     if (i >= mm) break;
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
@@ -1403,7 +1419,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int kx = opaque(k);
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
-                for (int i = 0; i < kMaxFacets; ++i) {
+                for (int i = 0; i < MF; ++i) {
                     if (i >= mm) break;
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
@@ -1429,7 +1445,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int kx = opaque(k);
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
-                for (int i = 0; i < kMaxFacets; ++i) {
+                for (int i = 0; i < MF; ++i) {
                     if (i >= mm) break;
                     if (i < km) {
                         const double2 fa = L.A2[i * N + kx];
@@ -1469,7 +1485,7 @@ __device__ __forceinline__ void ipm_solve(
         if (LAMOUT) {
             double* lo = lam_out + st * M;
 #pragma unroll
-            for (int i = 0; i < kMaxFacets; ++i) {
+            for (int i = 0; i < MF; ++i) {
                 if (i >= M) break;
                 lo[i] = i < K.m ? K.lam[i] : 0.0;
             }

@@ -16,7 +16,7 @@ using namespace BipedalLocomotion::Planners;
 
 namespace
 {
-constexpr int kCorners = 8;   // two rectangular feet at most per knot
+constexpr int kCorners = 16;  // four rectangular contacts at most per phase (the hull kernel's limit)
 }
 
 TimeVaryingDCMPlanner::TimeVaryingDCMPlanner()
@@ -61,6 +61,19 @@ bool TimeVaryingDCMPlanner::initialize(std::weak_ptr<ParametersHandler::IParamet
     }
     int maxIter = m_params.max_iter;
     if (ptr->getParameter("max_iterations", maxIter)) m_params.max_iter = maxIter;
+    // facet slots per knot: 8 (default) covers one or two feet; phases with three or four
+    // contacts can need more (up to 16, then the interior point kernel alone)
+    int maxFacets = m_params.max_facets;
+    if (ptr->getParameter("max_facets", maxFacets))
+    {
+        if (maxFacets < 3 || maxFacets > 16)
+        {
+            std::cerr << "[TimeVaryingDCMPlanner::initialize] max_facets must be in [3, 16]."
+                      << std::endl;
+            return false;
+        }
+        m_params.max_facets = maxFacets;
+    }
     auto weight = [&](const char* key, double* w) {
         std::vector<double> v;
         if (!ptr->getParameter(key, v)) return true;
@@ -164,7 +177,7 @@ bool TimeVaryingDCMPlanner::buildPhaseTable(blf_handle* h)
             std::map<std::string, ContactList::const_iterator> active(
                 plan[p].activeContacts.begin(), plan[p].activeContacts.end());
             if (active.size() > static_cast<std::size_t>(kCorners / 4))
-            {   // the support polygon holds two rectangular feet (8 corners) at most
+            {   // the support polygon holds four rectangular contacts (16 corners) at most
                 std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b << ": phase " << p
                           << " has " << active.size() << " active contacts; at most "
                           << kCorners / 4 << " are supported." << std::endl;
@@ -204,10 +217,30 @@ bool TimeVaryingDCMPlanner::buildPhaseTable(blf_handle* h)
         !m_dPhRef.upload(ref) || !m_dPhA.resize(BP * M * 2) || !m_dPhB.resize(BP * M) ||
         !m_dPhNf.resize(BP))
         return false;
-    return blf::report(blf_hull2d_hrep(h, m_dPhCorners.data(), m_dPhNCorners.data(), kCorners, M,
-                                       static_cast<int64_t>(BP), m_dPhA.data(), m_dPhB.data(),
-                                       m_dPhNf.data(), nullptr),
-                       "TimeVaryingDCMPlanner::advance");
+    if (!blf::report(blf_hull2d_hrep(h, m_dPhCorners.data(), m_dPhNCorners.data(), kCorners, M,
+                                     static_cast<int64_t>(BP), m_dPhA.data(), m_dPhB.data(),
+                                     m_dPhNf.data(), nullptr),
+                     "TimeVaryingDCMPlanner::advance"))
+        return false;
+    // once per plan: every phase with contacts must have a support polygon that fits the QP's
+    // facet slots (a hull of three or four contacts can need more than the default 8: set
+    // max_facets up to 16)
+    std::vector<int32_t> nf(BP);
+    if (!m_dPhNf.download(nf)) return false;
+    for (int b = 0; b < B; ++b)
+        for (std::size_t p = 0; p < m_plans[b].size(); ++p)
+        {
+            const std::size_t row = static_cast<std::size_t>(b) * P + p;
+            if (ncorners[row] > 0 && nf[row] < 0)
+            {
+                std::cerr << "[TimeVaryingDCMPlanner::advance] Problem " << b << ": the support "
+                          << "polygon of phase " << p << " (" << ncorners[row] / 4
+                          << " contacts) is degenerate or needs more than max_facets = " << M
+                          << " facets (at most " << kCorners << ")." << std::endl;
+                return false;
+            }
+        }
+    return true;
 }
 
 bool TimeVaryingDCMPlanner::checkWindow() const

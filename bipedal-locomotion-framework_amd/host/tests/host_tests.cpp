@@ -460,6 +460,83 @@ static void testPlanner()
     REQUIRE_FALSE(shortPlanner.isValid());
 }
 
+// Three active contacts: the lists of ContactPhaseListTest.cpp:32-47 (left, right, additional;
+// phases [4, 5) and [6, 7) with all three), feet turned out and a hand support ahead, so the
+// three-contact polygons need 9 facets: refused at max_facets 8, planned at max_facets 16.
+static ContactPhaseList threeContactPlan(double dx)
+{
+    ContactList left, right, additional;
+    left.setDefaultName("left");
+    right.setDefaultName("right");
+    additional.setDefaultName("additional");
+    const Transform pl = Transform::fromPlanar(dx, 0.14, 1.50);
+    const Transform pr = Transform::fromPlanar(dx, -0.14, -0.03);
+    const Transform pa = Transform::fromPlanar(dx + 0.19, 0.0, 0.85);
+    left.addContact(pl, 0.0, 1.0);
+    left.addContact(pl, 2.0, 5.0);
+    left.addContact(pl, 6.0, 7.0);
+    right.addContact(pr, 0.0, 3.0);
+    right.addContact(pr, 4.0, 7.0);
+    additional.addContact(pa, 4.0, 5.0);
+    additional.addContact(pa, 6.0, 7.5);
+    ContactPhaseList plan;
+    plan.setLists({left, right, additional});
+    return plan;
+}
+
+static void testPlannerThreeContacts()
+{
+    std::vector<ContactPhaseList> plans;
+    std::vector<std::array<double, 2>> xi0;
+    for (int b = 0; b < 8; ++b)
+    {
+        plans.push_back(threeContactPlan(0.002 * b));
+        xi0.push_back({{0.002 * b + 0.01, 0.12}});   // near the first phase's centre (left+right)
+    }
+    auto narrow = std::make_shared<ParametersHandler::StdImplementation>();
+    narrow->setParameter("horizon", 60);
+    narrow->setParameter("sampling_time", 0.1);
+    TimeVaryingDCMPlanner p8;
+    REQUIRE(p8.initialize(narrow));
+    REQUIRE(p8.setContactPhaseLists(plans) && p8.setInitialDCM(xi0));
+    REQUIRE_FALSE(p8.advance());   // a 9-facet polygon does not fit 8 facet slots
+    REQUIRE_FALSE(p8.isValid());
+
+    auto wide = std::make_shared<ParametersHandler::StdImplementation>();
+    wide->setParameter("horizon", 60);
+    wide->setParameter("sampling_time", 0.1);
+    wide->setParameter("max_facets", 16);
+    TimeVaryingDCMPlanner p16;
+    REQUIRE(p16.initialize(wide));
+    REQUIRE(p16.setContactPhaseLists(plans) && p16.setInitialDCM(xi0));
+    for (int step = 0; step < 10; ++step)
+    {
+        REQUIRE(p16.advance());
+        REQUIRE(p16.isValid());
+        const DCMPlanBatch& plan = p16.get();
+        REQUIRE(plan.batch == 8 && plan.horizon == 60);
+        bool ok = true;
+        for (int b = 0; b < 8; ++b)
+        {
+            ok = ok && plan.status[b] == 0;
+            const double* xi = &plan.dcm[static_cast<std::size_t>(b) * 61 * 2];
+            const double* r = &plan.vrp[static_cast<std::size_t>(b) * 60 * 2];
+            for (int k = 0; k < 60; ++k)
+                for (int j = 0; j < 2; ++j)
+                {
+                    const double w = std::sqrt(9.81 / 0.53);
+                    const double nxt = xi[2 * k + j] + (w * xi[2 * k + j] + (-w) * r[2 * k + j]) * 0.1;
+                    ok = ok && std::fabs(nxt - xi[2 * (k + 1) + j]) < 1e-12;
+                }
+        }
+        REQUIRE(ok);
+    }
+    auto bad = std::make_shared<ParametersHandler::StdImplementation>();
+    bad->setParameter("max_facets", 17);
+    TimeVaryingDCMPlanner pBad;
+    REQUIRE_FALSE(pBad.initialize(bad));
+}
+
 
 // ---- ContinousContactModelTest.cpp:30-214 ------------------------------------------------------
 static blf::Matrix3 rpy(double r, double p, double y)   // iDynTree Rotation::RPY = Rz(y) Ry(p) Rx(r)
@@ -984,6 +1061,7 @@ int main(int argc, char** argv)
         {"Convex Hull helper (3-D, ConvexHullHelperTest.cpp)", true, testConvexHull3},
         {"QuinticSpline", true, testQuinticSpline},
         {"TimeVaryingDCMPlanner advance", true, testPlanner},
+        {"TimeVaryingDCMPlanner three contacts", true, testPlannerThreeContacts},
         {"Continuous Contact", true, testContinuousContact},
         {"FloatingBaseSystemKinematics", true, testFloatingBaseKinematics},
         {"IntegratorTest: floating base kinematics (literal)", true, testIntegratorKinematicsLiteral},

@@ -195,7 +195,8 @@ blf_status blf_quintic_eval(blf_handle* handle, const double* knots_t, const dou
  * Riccati recursion over the knots (DESIGN.md section 4 gives the exact iteration).           */
 typedef struct blf_dcm_mpc_params {
     int32_t horizon;       /* N >= 1                                                        */
-    int32_t max_facets;    /* M, 1..8 (padded facet slots per knot)                         */
+    int32_t max_facets;    /* M, 1..16 (padded facet slots per knot; above 8 the interior     *
+                            * point kernel alone: support polygons of three or four contacts) */
     int32_t max_iter;      /* IPM iteration cap (e.g. 50)                                   */
     int32_t reserved;      /* must be 0                                                     */
     double dt;             /* knot spacing [s]                                              */
@@ -289,7 +290,7 @@ blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* 
  *   phase gets nfacets = -1 (the QP reports BLF_QP_BAD_FACETS) and zero rows / references.   */
 typedef struct blf_phase_table {
     int32_t max_phases;        /* P >= 1                                                     */
-    int32_t max_facets;        /* M, 1..8                                                    */
+    int32_t max_facets;        /* M, 1..16                                                   */
     const int32_t* nphases;    /* [B]                                                        */
     const double* begin;       /* [B][P]                                                     */
     const double* end;         /* [B][P]                                                     */

@@ -473,7 +473,7 @@ double orc_wave_tree_sum(const double* c, int n)
     return total;
 }
 
-#define MF 8
+#define MF 16   /* facet slots (max_facets <= 16; above 8 the device runs the IPM kernel alone) */
 #ifndef ORC_GUESS_PASSES
 #define ORC_GUESS_PASSES 8    /* active-set start: drop/add passes (kernel: kGuessPasses) */
 #endif
@@ -1675,7 +1675,8 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
  * start's one-step problem, see dcm_saturated_start): rs itself if no facet is violated; else the
  * candidate of least (r - rs)^T B (r - rs) among the projections onto single facet lines (valid
  * when the facet is violated and the point is feasible) and the vertices of facet pairs (valid
- * when feasible), candidates in the order: facets 0..m-1, then pairs (i, j), i < j, lexicographic;
+ * when feasible), candidates in the order: facets 0..m-1, then pairs (i, j), i < j < m,
+ * lexicographic (the kernel: rounds of 64 candidates, one per lane);
  * the first of equal distances wins (the kernel: one candidate per lane, the lowest lane of the
  * minimum).  None valid (rounding): rs.  Returns the active count (0, 1, 2), facets in *i1, *i2. */
 static int sat_project(const dcm_ws* w, int k, double rs0, double rs1, double B00, double B01,
@@ -1692,12 +1693,12 @@ static int sat_project(const dcm_ws* w, int k, double rs0, double rs1, double B0
     const double detB = fma(B00, B11, -(B01 * B01));
     double best = 0.0;
     int bc = -1;
-    for (int c = 0; c < MF + MF * (MF - 1) / 2; ++c) {
+    const int nc = m + m * (m - 1) / 2;
+    for (int c = 0; c < nc; ++c) {
         double v0, v1, dist;
         int x, y;
-        if (c < MF) {
+        if (c < m) {
             x = c; y = c;
-            if (x >= m) continue;
             const double a0 = A[2 * x], a1 = A[2 * x + 1];
             const double u0 = fma(B11, a0, -(B01 * a1));       /* adj(B) a = det(B) B^{-1} a */
             const double u1 = fma(B00, a1, -(B01 * a0));
@@ -1709,12 +1710,11 @@ static int sat_project(const dcm_ws* w, int k, double rs0, double rs1, double B0
             if (!(viol > 0.0)) continue;
             dist = (t * viol) * detB;
         } else {
-            /* pair q = c - MF of (0,1), (0,2), .., (0,7), (1,2), .. (6,7) */
-            int q = c - MF;
+            /* pair q = c - m of (0,1), (0,2), .., (0,m-1), (1,2), .. (m-2,m-1) */
+            int q = c - m;
             x = 0;
-            while (q >= MF - 1 - x) { q -= MF - 1 - x; ++x; }
+            while (q >= m - 1 - x) { q -= m - 1 - x; ++x; }
             y = x + 1 + q;
-            if (y >= m) continue;
             const double a0 = A[2 * x], a1 = A[2 * x + 1], e0 = A[2 * y], e1 = A[2 * y + 1];
             const double det = fma(a0, e1, -(a1 * e0));
             const double aa = FD2(a0, a0, a1, a1), ee = FD2(e0, e0, e1, e1);
@@ -1732,7 +1732,7 @@ static int sat_project(const dcm_ws* w, int k, double rs0, double rs1, double B0
         if (bc < 0 || dist < best) { best = dist; bc = c; *r0 = v0; *r1 = v1; *i1 = x; *i2 = y; }
     }
     if (bc < 0) { *r0 = rs0; *r1 = rs1; return 0; }
-    return bc < MF ? 1 : 2;
+    return bc < m ? 1 : 2;
 }
 
 /* The saturated LQ start of the interior point method: when the active-set
@@ -1866,9 +1866,11 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      * evaluates them (one wavefront, knot pairs per lane) when that kernel runs: 64 < N <= 128
      * with the start enabled (csrc/dcm_mpc_ipm.hip launch_dcm_mpc); the IPM iterations always in
      * the wavefront tree of the IPM kernel */
-    w->pairs = (prm->tol_polish > 0.0 && N > WV && N <= 2 * WV && !prm->single_kernel) ? 1 : 0;
+    /* the active-set kernels run for N <= 128 with the polish on and at most 8 facet slots */
+    const int as_kernel = prm->tol_polish > 0.0 && N <= 2 * WV && !prm->single_kernel && M <= 8;
+    w->pairs = (as_kernel && N > WV) ? 1 : 0;
     /* small batches, one knot per lane: the active-set kernels' DPP tree (prm->as_tree) */
-    w->dpp = (prm->tol_polish > 0.0 && N <= WV && !prm->single_kernel && prm->as_tree) ? 1 : 0;
+    w->dpp = (as_kernel && N <= WV && prm->as_tree) ? 1 : 0;
     w->Qw0 = prm->w_xi[0]; w->Qw1 = prm->w_xi[1];
     w->Rw0 = prm->w_vrp[0]; w->Rw1 = prm->w_vrp[1];
     w->Pw0 = prm->w_terminal[0]; w->Pw1 = prm->w_terminal[1];
@@ -1937,7 +1939,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      *      passes), then the fp64 passes (kernel B) from the float point with the facets active
      *      there as the guess;
      *      when they do not certify, the IPM's start from the fp64 LQ optimum below ---- */
-    if (!warm && prm->tol_polish > 0.0 && N <= 2 * WV && !prm->single_kernel) {
+    if (!warm && as_kernel) {
         double* r32 = (double*)malloc(sizeof(double) * 4 * (size_t)N);
         double* x32 = r32 + 2 * N;
         int* g32 = (int*)malloc(sizeof(int) * (size_t)N);
@@ -1998,7 +2000,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      *      guess "facets the start point violates" (a warm start: also the facets whose previous
      *      multiplier exceeds the floor), with up to ORC_GUESS_PASSES drop/add passes (the cold
      *      starts of the active-set kernel already ran theirs above) ---- */
-    if (prm->tol_polish > 0.0 && (warm || N > 2 * WV || prm->single_kernel)) {
+    if (prm->tol_polish > 0.0 && (warm || !as_kernel)) {
         int* gm = (int*)calloc((size_t)N, sizeof(int));
         for (int k = 0; k < N; ++k) {
             const int ws = warm && k + warm->shift < N;
