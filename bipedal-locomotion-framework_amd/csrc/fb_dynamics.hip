@@ -78,6 +78,11 @@ __device__ __forceinline__ void wave_sync()
 #ifndef BLF_FBD_CHOLB
 #define BLF_FBD_CHOLB 2
 #endif
+// the Euler kernel's substitutions (fbd_eval FOLD): 0 two loops after the factorization, 1 the
+// forward one inside it, 2 that and L stored column-major by the factorization itself
+#ifndef BLF_FBD_FOLD
+#define BLF_FBD_FOLD 1
+#endif
 
 constexpr int kPad = BLF_FBD_PAD;
 constexpr int kLinkRec = 40 + kPad;   // record stride (40 doubles of data)
@@ -402,7 +407,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
 // NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
 // registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
 // steps 6-9.
-template <int NVMAX, int HW, bool PRI>
+template <int NVMAX, int HW, bool PRI, int FOLD = 0>
 __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
                                          const double* jvel, const double* bp, const double* bR,
                                          const double* jp, const double* tau, const Contacts& ct,
@@ -660,6 +665,13 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     // the block must divide the register row (NVMAX = 54 for the largest model: 2)
     constexpr int CB = NVMAX % BLF_FBD_CHOLB == 0 ? BLF_FBD_CHOLB : 2;
     static_assert(NVMAX % CB == 0, "block size divides the register row");
+    // FOLD >= 1: the forward substitution L z = y rides along: every lane also solves the block's
+    // CB unknowns z_{k..k+CB-1} from the broadcast y entries of the block's lanes, the block's
+    // lanes keep theirs, the rows below subtract L_{lane,k+i} z_{k+i}: no separate loop of NV
+    // dependent broadcasts.  FOLD == 2: the columns also go to their final place, L column-major
+    // over the dead link records (Lm[MS c + row], odd MS), which the back substitution then reads
+    // lane-strided, instead of a separate row-major store of L.
+    double* Lm = S.link();
 #pragma unroll
     for (int k = 0; k < NVMAX; k += CB) {
         if (k < NV) {
@@ -692,11 +704,29 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                 for (int c = 0; c < i; ++c) t = t - li[c] * Lb[i][c];
                 li[i] = t * il[i];
             }
-            double* col = S.comp() + ((k / CB) & 1) * CB * NV;
+            if constexpr (FOLD >= 1) {
+            double z[CB];
+#pragma unroll
+            for (int i = 0; i < CB; ++i) {
+                double t = k + i < NV ? H.bcast_k(y, k + i) : 0.0;
+#pragma unroll
+                for (int c = 0; c < i; ++c) t = t - Lb[i][c] * z[c];
+                z[i] = t * il[i];
+            }
+            double yl = y;
+#pragma unroll
+            for (int i = 0; i < CB; ++i) yl = yl - li[i] * z[i];
+#pragma unroll
+            for (int i = 0; i < CB; ++i) y = lane == k + i ? z[i] : y;
+            y = lane >= k + CB ? yl : y;
+            }
+            double* col = FOLD >= 2 ? Lm + MS * k : S.comp() + ((k / CB) & 1) * CB * NV;
+            const int cst = FOLD >= 2 ? MS : NV;
+#define FBD_COL(i, row) col[(i) * cst + (row)]
 #pragma unroll
             for (int i = 0; i < CB; ++i) {
                 r[k + i] = lane >= k ? li[i] : r[k + i];
-                if (lane < NV) col[i * NV + lane] = r[k + i];
+                if (lane < NV && k + i < NV) FBD_COL(i, lane) = r[k + i];
             }
             wave_sync();
             // no row predicate (as below): lanes above row j update only upper-triangle entries
@@ -705,9 +735,10 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                 const int jj = j < NV ? j : NV - 1;
                 double t = r[j];
 #pragma unroll
-                for (int i = CB - 1; i >= 0; --i) t = fma(-r[k + i], col[i * NV + jj], t);
+                for (int i = CB - 1; i >= 0; --i) t = fma(-r[k + i], FBD_COL(i, jj), t);
                 r[j] = t;
             }
+#undef FBD_COL
         }
     }
 #else
@@ -741,19 +772,11 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
 #endif
     FSTAMP_ADD(7, f_t7);
     FSTAMP(f_t8);
-    // 9. L z = y with the rows in registers, then L^T x = z with row k of L read from LDS (the
-    //    link records are dead by now); lane k scales its own entry, one broadcast per step.  Two
-    //    unknowns per step (the 2 x 2 block solved by every lane, as in the factorization) measured
-    //    the same: 6.054 / 6.069 against 6.081 / 6.073 ms per c5 period of the Euler kernel
+#if BLF_FBD_CHOLB > 1
+    if constexpr (FOLD == 1) {
+    // 9. L z = y is done (folded into the factorization); L^T x = z with row k of L read from
+    //    LDS (the link records are dead by now), one step ahead
     const double idg = lane < NV ? 1.0 / bcast_own_diag<NVMAX>(r, lane) : 0.0;
-#pragma unroll
-    for (int k = 0; k < NVMAX; ++k) {   // k >= NV changes only lanes past the matrix
-        y = lane == k ? y * idg : y;
-        const double xk = H.bcast_k(y, k);
-        const double f = lane > k ? r[k] : 0.0;
-        y = y - f * xk;
-    }
-    double* Lm = S.link();
     if (lane < NV)
 #pragma unroll
         for (int j = 0; j < NVMAX; ++j)
@@ -767,6 +790,50 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         if (lane < k) y = y - lki * xk;
         lki = lnext;
     }
+    } else if constexpr (FOLD >= 2) {
+    // 9. L z = y is done (folded into the factorization); L^T x = z with L's row k read from the
+    //    column-major L (Lm[MS lane + k] = L_{k,lane}, lane-strided, one step ahead); lane k
+    //    scales its own entry, one broadcast per step
+    const double idg = lane < NV ? 1.0 / bcast_own_diag<NVMAX>(r, lane) : 0.0;
+    double lki = (lane < NV - 1) ? Lm[MS * lane + (NV - 1)] : 0.0;
+    for (int k = NV - 1; k >= 0; --k) {
+        const double lnext = (k > 0 && lane < k - 1) ? Lm[MS * lane + (k - 1)] : 0.0;   // read ahead
+        if (lane == k) y = y * idg;
+        const double xk = H.bcast_k(y, k);
+        if (lane < k) y = y - lki * xk;
+        lki = lnext;
+    }
+    } else {
+#endif
+    // 9. L z = y with the rows in registers, then L^T x = z with row k of L read from LDS (the
+    //    link records are dead by now); lane k scales its own entry, one broadcast per step.  Two
+    //    unknowns per step (the 2 x 2 block solved by every lane, as in the factorization) measured
+    //    the same: 6.054 / 6.069 against 6.081 / 6.073 ms per c5 period of the Euler kernel
+    const double idg = lane < NV ? 1.0 / bcast_own_diag<NVMAX>(r, lane) : 0.0;
+#pragma unroll
+    for (int k = 0; k < NVMAX; ++k) {   // k >= NV changes only lanes past the matrix
+        y = lane == k ? y * idg : y;
+        const double xk = H.bcast_k(y, k);
+        const double f = lane > k ? r[k] : 0.0;
+        y = y - f * xk;
+    }
+    double* Lr = S.link();
+    if (lane < NV)
+#pragma unroll
+        for (int j = 0; j < NVMAX; ++j)
+            if (j < NV && j <= lane) Lr[MS * lane + j] = r[j];
+    wave_sync();
+    double lki = (lane < NV - 1) ? Lr[MS * (NV - 1) + lane] : 0.0;
+    for (int k = NV - 1; k >= 0; --k) {
+        const double lnext = (k > 0 && lane < k - 1) ? Lr[MS * (k - 1) + lane] : 0.0;   // read ahead
+        if (lane == k) y = y * idg;
+        const double xk = H.bcast_k(y, k);
+        if (lane < k) y = y - lki * xk;
+        lki = lnext;
+    }
+#if BLF_FBD_CHOLB > 1
+    }
+#endif
     if (lane < NV) S.rhs()[lane] = y;
     wave_sync();
     FSTAMP_ADD(8, f_t8);
@@ -867,7 +934,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
             wave_sync();
             tq = S.tq();
         }
-        ok = fbd_eval<NVMAX, HW, PRI>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+        ok = fbd_eval<NVMAX, HW, PRI, BLF_FBD_FOLD>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                  tq, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         wave_sync();
