@@ -20,6 +20,7 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 
 # every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_set_qp_launch_mode",
+            "blf_set_qp_split_batch",
             "blf_step_schedule",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_hull3d_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
@@ -185,6 +186,7 @@ def lib():
             ctypes.POINTER(FbContacts), _vp, _i64, _f64, _f64, _f64, _vp]
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         L.blf_set_qp_launch_mode.argtypes = [_i32, _i32]
+        L.blf_set_qp_split_batch.argtypes = [_i64, _vp]
         for name in EXPORTED:
             if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
                             "blf_dcm_mpc_default_params", "blf_dcm_mpc_flops_per_iter"):
@@ -199,6 +201,14 @@ def set_qp_launch_mode(fuse_stage2=-1, single_kernel=-1):
     """blf_set_qp_launch_mode: the QP kernel routing for A/B and parity tests (-1: unchanged).
     Returns nothing; the defaults are the product's (fuse_stage2 = 1, single_kernel = 0)."""
     _check(lib().blf_set_qp_launch_mode(int(fuse_stage2), int(single_kernel)))
+
+
+def set_qp_split_batch(min_batch):
+    """blf_set_qp_split_batch: cold per-knot batches of at least min_batch QPs run the search and
+    certify kernels (0: never, < 0: unchanged).  Returns the previous setting (0: never)."""
+    prev = ctypes.c_int64(0)
+    _check(lib().blf_set_qp_split_batch(int(min_batch), ctypes.byref(prev)))
+    return prev.value
 
 
 def _check(code):

@@ -17,7 +17,13 @@ QpLaunchMode& qp_launch_mode()
     static QpLaunchMode mode = [] {
         const char* fz = getenv("BLF_QP_FUSE_STAGE2");
         const char* sk = getenv("BLF_QP_SINGLE_KERNEL");
-        return QpLaunchMode{!(fz && fz[0] == '0'), sk && sk[0] == '1'};
+        const char* sp = getenv("BLF_QP_SPLIT_MIN_BATCH");
+        int64_t split = kSplitMinBatchDefault;
+        if (sp && sp[0]) {
+            const long long v = atoll(sp);
+            split = v <= 0 ? INT64_MAX : (int64_t)v;
+        }
+        return QpLaunchMode{!(fz && fz[0] == '0'), sk && sk[0] == '1', split};
     }();
     return mode;
 }
@@ -135,6 +141,14 @@ blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel)
     QpLaunchMode& m = qp_launch_mode();
     if (fuse_stage2 >= 0) m.fuse_stage2 = fuse_stage2;
     if (single_kernel >= 0) m.single_kernel = single_kernel;
+    return BLF_OK;
+}
+
+blf_status blf_set_qp_split_batch(int64_t min_batch, int64_t* previous)
+{
+    QpLaunchMode& m = qp_launch_mode();
+    if (previous) *previous = m.split_min_batch == INT64_MAX ? 0 : m.split_min_batch;
+    if (min_batch >= 0) m.split_min_batch = min_batch == 0 ? INT64_MAX : min_batch;
     return BLF_OK;
 }
 

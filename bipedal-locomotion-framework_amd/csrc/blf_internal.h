@@ -59,8 +59,10 @@ blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* 
 struct QpLaunchMode {
     int fuse_stage2;     // 1 (default): stage 2 inside the small-batch active-set kernel
     int single_kernel;   // 0 (default): active-set kernel first
+    int64_t split_min_batch;   // cold per-knot batches from this size: search + certify kernels
 };
 QpLaunchMode& qp_launch_mode();
+constexpr int64_t kSplitMinBatchDefault = 16384;
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
                           const blf_dcm_mpc_warm_start* warm, int64_t batch,
                           const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);

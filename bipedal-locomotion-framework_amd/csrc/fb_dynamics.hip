@@ -79,9 +79,12 @@ __device__ __forceinline__ void wave_sync()
 #define BLF_FBD_CHOLB 2
 #endif
 // the Euler kernel's substitutions (fbd_eval FOLD): 0 two loops after the factorization, 1 the
-// forward one inside it, 2 that and L stored column-major by the factorization itself
+// forward one inside it, 2 that and L stored column-major by the factorization itself.  Measured
+// (profiles/r04_fbd_fold_ab.log, one c5 period of fbd_euler_kernel, two rounds on one box): 1 took
+// 4.747 / 4.740 ms against 4.701 / 4.705 ms for 0 (the block's y broadcasts lengthen every
+// factorization step's chain more than the separate loop costs); 2 spills 318 VGPRs.  So 0.
 #ifndef BLF_FBD_FOLD
-#define BLF_FBD_FOLD 1
+#define BLF_FBD_FOLD 0
 #endif
 
 constexpr int kPad = BLF_FBD_PAD;

@@ -89,6 +89,12 @@ const char* blf_version(void);
  * interior point kernel alone (no active-set kernel).  -1 leaves a setting unchanged.  The initial
  * values come from BLF_QP_FUSE_STAGE2 / BLF_QP_SINGLE_KERNEL, read once at the first solve. */
 blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel);
+/* Cold solves of the per-knot input (blf_dcm_mpc_solve without warm start) with N <= 128 and at
+ * least min_batch QPs run the active-set search and its fp64 certification as two kernels (more
+ * resident search wavefronts; the same bits as the one-kernel path).  min_batch 0: never; < 0:
+ * unchanged.  *previous (optional) receives the setting before the call (0: never).  Initial value
+ * from BLF_QP_SPLIT_MIN_BATCH, else the library's default. */
+blf_status blf_set_qp_split_batch(int64_t min_batch, int64_t* previous);
 
 /* ---- 0. FixedStepIntegrator::integrate's step schedule (FixedStepIntegrator.tpp:21-72) -------
  * The validation (in the reference's order) and schedule every batched integrator below uses:
