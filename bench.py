@@ -170,6 +170,10 @@ def main():
     ap.add_argument("--c5-groups", type=int, default=1,
                     help="c5: robots in this many groups, each closed loop on its own stream "
                          "(measured: 1 group 6.96 ms, 2 groups 6.98 ms, 4 groups 7.4 ms per period)")
+    ap.add_argument("--c5-overlap", type=int, default=0,
+                    help="c5: 1 = the robots whose plan the active-set kernel solved integrate while "
+                         "the interior point kernel finishes the rest on a side stream (ClosedLoop "
+                         "overlap; the same bits)")
     ap.add_argument("--tol-polish", type=float, default=None,
                     help="override blf_dcm_mpc_default_params' tol_polish (also the CPU baseline's)")
     ap.add_argument("--expand-path", action="store_true",
@@ -488,7 +492,7 @@ def closed_loop(args):
         # horizon 100 every robot's period is the same computation as in one group
         # (DL.split_groups states when); more groups did not pay (the
         # dynamics kernel holds every SIMD, so the plan kernels' tails find no room beside it)
-        loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N)
+        loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N, overlap=bool(args.c5_overlap))
         for lp in loops:
             lp.expand_path = args.expand_path
         state_of = lambda lp: {k: v.cpu().numpy() for k, v in lp.state.items()}
@@ -558,7 +562,7 @@ def closed_loop(args):
                                        f"(integrate(0, {T * 1e3:g} ms) at dT = {dT * 1e3:g} ms: "
                                        f"{robot_ms:g} ms of robot time, the reference schedule)",
                            "batch_per_gpu": B, "parallelism": f"shard{world} (independent robots)",
-                           "stream_groups": len(loops)}}
+                           "stream_groups": len(loops), "overlap": bool(args.c5_overlap)}}
         if on_cpu:
             line["device"] = "CPU rehearsal (BLF_C5_ORACLE=1: oracle/closed_loop.py on every rank)"
         if not args.no_cpu:

@@ -70,9 +70,16 @@ class ClosedLoop:
     problem dict with a horizon of at least horizon + the number of periods to run."""
 
     def __init__(self, h, model, plan, states, horizon=100, dT=0.001, law=None,
-                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None):
+                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None, overlap=False):
         import torch
         self.h, self.N, self.dT, self.stream = h, horizon, dT, stream
+        # overlap: the robots whose window the active-set kernel solved go on to the posture and
+        # the dynamics at once; the few it hands to the interior point kernel (uncapturable DCM
+        # states, tens of iterations on an otherwise idle chip) finish on a side stream, where
+        # their own posture and dynamics follow (blf_dcm_mpc_solve_phased_begin / _finish and the
+        # masked kernels).  Every robot's computation is the same, so the states are the same bits.
+        self.overlap = bool(overlap)
+        self.side = torch.cuda.Stream(device=h.device) if self.overlap else None
         dev = torch.device("cuda", h.device)
         t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
         self.dt = float(plan["dt"])
@@ -115,6 +122,8 @@ class ClosedLoop:
             # a robot whose previous window was not solved (status != 0) is planned cold
             warm = dict(vrp=self.prev["vrp"], lam=self.prev["lam"], shift=1, floor=1e-3,
                         status=self.prev["status"])
+        if N <= 128 and not self.expand_path and self.overlap:
+            return self._period_overlap(warm)
         if N <= 128 and not self.expand_path:   # the window read from the phase table
             out = h.dcm_mpc_solve_phased(self.table, s, self.xi, self.omega[:, s:s + N],
                                          self.params, warm=warm, out=self.bufs[s % 2],
@@ -132,6 +141,33 @@ class ClosedLoop:
         # period
         h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T,
                                         self.dT, contacts=self.contacts, stream=self.stream)
+        self.prev = out
+        self.s = s + 1
+        return out
+
+    def _period_overlap(self, warm):
+        """period() with the interior point kernel's problems on the side stream (overlap)."""
+        import torch
+        h, s, N = self.h, self.s, self.N
+        main = self.stream if self.stream is not None else torch.cuda.current_stream(h.device)
+        out = h.dcm_mpc_solve_phased(self.table, s, self.xi, self.omega[:, s:s + N], self.params,
+                                     warm=warm, out=self.bufs[s % 2], lambda_out=True, stream=main,
+                                     begin=True)
+        self.bufs[s % 2] = out
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self.side.wait_event(ready)
+        pending = out["pending"]
+        h.dcm_mpc_solve_phased_finish(self.xi, self.params, out, warm=warm, lambda_out=True, stream=self.side)
+        for stream, want in ((self.side, 1), (main, 0)):
+            h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=stream,
+                                mask=pending, want=want)
+            h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T,
+                                            self.dT, contacts=self.contacts, stream=stream,
+                                            mask=pending, want=want)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        main.wait_event(done)
         self.prev = out
         self.s = s + 1
         return out

@@ -29,7 +29,9 @@ EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_s
             "blf_dcm_mpc_flops_per_iter",
             "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
             "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate",
-            "blf_fb_dcm", "blf_dcm_posture_reference", "blf_fbd_euler_integrate_impedance"]
+            "blf_fb_dcm", "blf_dcm_posture_reference", "blf_fbd_euler_integrate_impedance",
+            "blf_dcm_mpc_solve_phased_begin", "blf_dcm_mpc_solve_phased_finish",
+            "blf_dcm_posture_reference_masked", "blf_fbd_euler_integrate_impedance_masked"]
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -163,6 +165,11 @@ def lib():
                                                ctypes.POINTER(DcmMpcWarmStart), _i64,
                                                ctypes.POINTER(DcmMpcWindow),
                                                ctypes.POINTER(DcmMpcSolution), _vp, _vp]
+        L.blf_dcm_mpc_solve_phased_begin.argtypes = L.blf_dcm_mpc_solve_phased.argtypes[:-1] + [_vp, _vp]
+        L.blf_dcm_mpc_solve_phased_finish.argtypes = [_vp, ctypes.POINTER(DcmMpcParams), _vp,
+                                                      ctypes.POINTER(DcmMpcWarmStart), _i64,
+                                                      ctypes.POINTER(DcmMpcWindow),
+                                                      ctypes.POINTER(DcmMpcSolution), _vp, _vp]
         L.blf_dcm_mpc_flops_per_iter.argtypes = [_i32, _i64]
         L.blf_contact_model_eval.argtypes = [_vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                              _vp, _vp]
@@ -184,6 +191,10 @@ def lib():
         L.blf_fbd_euler_integrate_impedance.argtypes = [
             _vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), ctypes.POINTER(JointImpedance),
             ctypes.POINTER(FbContacts), _vp, _i64, _f64, _f64, _f64, _vp]
+        L.blf_dcm_posture_reference_masked.argtypes = [_vp, ctypes.POINTER(PostureLaw), _vp, _vp, _i64,
+                                                       _i64, _vp, _vp, _i32, _vp]
+        L.blf_fbd_euler_integrate_impedance_masked.argtypes = (
+            L.blf_fbd_euler_integrate_impedance.argtypes[:-1] + [_vp, _i32, _vp])
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         L.blf_set_qp_launch_mode.argtypes = [_i32, _i32]
         L.blf_set_qp_split_batch.argtypes = [_i64, _vp]
@@ -576,12 +587,14 @@ class Handle:
                           _ptr(table["phase_ref"], torch.float64, (B, P, 2), "phase_ref"))
 
     def dcm_mpc_solve_phased(self, table, start, xi_init, omega, params=None, warm=None,
-                             out=None, window=None, lambda_out=False, stream=None):
+                             out=None, window=None, lambda_out=False, stream=None, begin=False):
         """blf_dcm_mpc_solve_phased: dcm_phase_expand(table, start, params.dt, N) followed by
         dcm_mpc_solve on that window, fused (same results bit for bit, N <= 128).
         omega [B, N] or a row-strided view [B, N] of a longer [B, L] array (stride(1) == 1).
         window: scratch dict (omega, xi_ref, vrp_ref, A, b, nfacets) of the window's shapes, kept
-        in out["window"] (allocated once when absent)."""
+        in out["window"] (allocated once when absent).
+        begin=True: blf_dcm_mpc_solve_phased_begin, the active-set part alone; out["pending"] [B]
+        int32 marks the problems dcm_mpc_solve_phased_finish(...) then solves."""
         torch = _torch()
         B, N = omega.shape
         M = table["phase_b"].shape[2]
@@ -630,11 +643,46 @@ class Handle:
                 out["lam"] = torch.empty((B, N, M), dtype=torch.float64, device=dev)
             lam_ptr = _ptr(out["lam"], torch.float64, (B, N, M), "lam")
         self._keep = (tb, so, ws, win)
-        _check(lib().blf_dcm_mpc_solve_phased(
-            self._h, ctypes.byref(p), ctypes.byref(tb), int(start),
-            _ptr(xi_init, torch.float64, (B, 2), "xi_init"), _vp(omega.data_ptr()), ostride,
-            ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(win), ctypes.byref(so),
-            lam_ptr, _stream(stream)))
+        args = (self._h, ctypes.byref(p), ctypes.byref(tb), int(start),
+                _ptr(xi_init, torch.float64, (B, 2), "xi_init"), _vp(omega.data_ptr()), ostride,
+                ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(win), ctypes.byref(so),
+                lam_ptr)
+        if begin:
+            if "pending" not in out:
+                out["pending"] = torch.empty((B,), dtype=torch.int32, device=dev)
+            _check(lib().blf_dcm_mpc_solve_phased_begin(
+                *args, _ptr(out["pending"], torch.int32, (B,), "pending"), _stream(stream)))
+        else:
+            _check(lib().blf_dcm_mpc_solve_phased(*args, _stream(stream)))
+        return out
+
+    def dcm_mpc_solve_phased_finish(self, xi_init, params, out, warm=None, lambda_out=False, stream=None):
+        """blf_dcm_mpc_solve_phased_finish: the interior point kernel on the problems a
+        dcm_mpc_solve_phased(..., begin=True) call left pending, with that call's xi_init, params,
+        warm and out (its window scratch and outputs)."""
+        torch = _torch()
+        B, N1 = out["xi"].shape[0], out["xi"].shape[1]
+        N, M = N1 - 1, params.max_facets
+        window = out["window"]
+        win = DcmMpcWindow(_ptr(window["omega"], torch.float64, (B, N), "window omega"),
+                           _ptr(window["xi_ref"], torch.float64, (B, N + 1, 2), "window xi_ref"),
+                           _ptr(window["vrp_ref"], torch.float64, (B, N, 2), "window vrp_ref"),
+                           _ptr(window["A"], torch.float64, (B, N, M, 2), "window A"),
+                           _ptr(window["b"], torch.float64, (B, N, M), "window b"),
+                           _ptr(window["nfacets"], torch.int32, (B, N), "window nfacets"))
+        so = DcmMpcSolution(
+            _ptr(out["xi"], torch.float64, (B, N + 1, 2), "xi"),
+            _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
+            _ptr(out["status"], torch.int32, (B,), "status"),
+            _ptr(out["iters"], torch.int32, (B,), "iters"),
+            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
+        ws = _warm_start(warm, B, N, M) if warm is not None else None
+        lam_ptr = _ptr(out["lam"], torch.float64, (B, N, M), "lam") if lambda_out else None
+        self._keep_finish = (so, ws, win)
+        _check(lib().blf_dcm_mpc_solve_phased_finish(
+            self._h, ctypes.byref(params), _ptr(xi_init, torch.float64, (B, 2), "xi_init"),
+            ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(win), ctypes.byref(so), lam_ptr,
+            _stream(stream)))
         return out
 
     # --- C3 pipeline: corner sets -> polygons (device hull) -> QP arrays ---
@@ -844,19 +892,23 @@ class Handle:
         law.c = c
         return law
 
-    def posture_reference(self, law, com, vrp, q_ref=None, stream=None):
+    def posture_reference(self, law, com, vrp, q_ref=None, stream=None, mask=None, want=1):
         """blf_dcm_posture_reference: joint references [B,n] from the plan's first VRP (vrp
-        [B,N,2], a blf_dcm_mpc_solve output) and the centre of mass com [B,6] (fb_dcm)."""
+        [B,N,2], a blf_dcm_mpc_solve output) and the centre of mass com [B,6] (fb_dcm).
+        mask [B] int32 (device): only the rows with (mask != 0) == want (blf_..._masked)."""
         torch = _torch()
         B, N = vrp.shape[0], vrp.shape[1]
         n = law.c.ndof
         q_ref = q_ref if q_ref is not None else torch.empty((B, n), dtype=torch.float64,
                                                             device=vrp.device)
-        _check(lib().blf_dcm_posture_reference(self._h, ctypes.byref(law.c),
-                                               _ptr(com, torch.float64, (B, 6), "com"),
-                                               _ptr(vrp, torch.float64, (B, N, 2), "vrp"), 2 * N, B,
-                                               _ptr(q_ref, torch.float64, (B, n), "q_ref"),
-                                               _stream(stream)))
+        args = (self._h, ctypes.byref(law.c), _ptr(com, torch.float64, (B, 6), "com"),
+                _ptr(vrp, torch.float64, (B, N, 2), "vrp"), 2 * N, B,
+                _ptr(q_ref, torch.float64, (B, n), "q_ref"))
+        if mask is None:
+            _check(lib().blf_dcm_posture_reference(*args, _stream(stream)))
+        else:
+            _check(lib().blf_dcm_posture_reference_masked(*args, _ptr(mask, torch.int32, (B,), "mask"),
+                                                          int(want), _stream(stream)))
         return q_ref
 
     def joint_impedance(self, kp, kd):
@@ -867,9 +919,10 @@ class Handle:
         return dict(kp=f64(kp), kd=f64(kd))
 
     def fbd_euler_integrate_impedance(self, dm, state, impedance, q_ref, t0, t1, dT, contacts=None,
-                                      mass_reg=None, stream=None):
+                                      mass_reg=None, stream=None, mask=None, want=1):
         """blf_fbd_euler_integrate_impedance in place on `state`: the control input of every
-        Euler step is tau = kp (q_ref - q) - kd qdot (impedance: joint_impedance())."""
+        Euler step is tau = kp (q_ref - q) - kd qdot (impedance: joint_impedance()).
+        mask [B] int32 (device): only the systems with (mask != 0) == want (blf_..._masked)."""
         torch = _torch()
         B, n = state["joint_pos"].shape
         NV = n + 6
@@ -879,8 +932,11 @@ class Handle:
         imp.kp = _ptr(impedance["kp"], torch.float64, (n,), "kp")
         imp.kd = _ptr(impedance["kd"], torch.float64, (n,), "kd")
         imp.q_ref = _ptr(q_ref, torch.float64, (B, n), "q_ref")
-        _check(lib().blf_fbd_euler_integrate_impedance(
-            self._h, ctypes.byref(dm.c), ctypes.byref(self._fb_state(state, B, n)), ctypes.byref(imp),
-            ctypes.byref(self._fb_contacts(contacts, B)), reg, B, float(t0), float(t1), float(dT),
-            _stream(stream)))
+        args = (self._h, ctypes.byref(dm.c), ctypes.byref(self._fb_state(state, B, n)), ctypes.byref(imp),
+                ctypes.byref(self._fb_contacts(contacts, B)), reg, B, float(t0), float(t1), float(dT))
+        if mask is None:
+            _check(lib().blf_fbd_euler_integrate_impedance(*args, _stream(stream)))
+        else:
+            _check(lib().blf_fbd_euler_integrate_impedance_masked(
+                *args, _ptr(mask, torch.int32, (B,), "mask"), int(want), _stream(stream)))
         return state

@@ -352,6 +352,61 @@ blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* 
     return launch_dcm_mpc(params, problem, warm, batch, solution, lambda_out, (hipStream_t)stream);
 }
 
+static blf_status phased_solve(const char* fn, int part, int32_t* pending, blf_handle* handle,
+                               const blf_dcm_mpc_params* params, const blf_phase_table* ph, int64_t start_knot,
+                               const double* xi_init, const double* omega, int64_t omega_stride,
+                               const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                               const blf_dcm_mpc_window* win, const blf_dcm_mpc_solution* solution,
+                               double* lambda_out, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "%s: null handle", fn);
+    BLF_REQUIRE(params && ph && win && solution, "%s: null argument", fn);
+    BLF_REQUIRE(ph->max_phases >= 1, "%s: max_phases %d < 1", fn, ph->max_phases);
+    BLF_REQUIRE(ph->max_facets == params->max_facets,
+                "%s: phase table max_facets %d != params max_facets %d", fn,
+                ph->max_facets, params->max_facets);
+    BLF_REQUIRE(start_knot >= 0, "%s: start_knot < 0", fn);
+    BLF_REQUIRE(omega_stride >= params->horizon, "%s: omega_stride %lld < horizon %d", fn,
+                (long long)omega_stride, params->horizon);
+    BLF_REQUIRE(batch == 0 || (ph->nphases && ph->begin && ph->end && ph->A && ph->b && ph->nfacets &&
+                               ph->ref && win->omega && win->xi_ref && win->vrp_ref && win->A &&
+                               win->b && win->nfacets),
+                "%s: null buffer", fn);
+    // the QP arguments as blf_dcm_mpc_solve_warm checks them (the window scratch stands in for the
+    // per-knot arrays, which this call does not read)
+    const blf_dcm_mpc_problem pb{xi_init, omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
+    if (batch > 0) {
+        BLF_REQUIRE(params->horizon >= 1 && params->horizon <= 128,
+                    "%s: horizon %d outside [1, 128]", fn, params->horizon);
+        BLF_REQUIRE(params->tol_polish > 0, "%s: tol_polish must be > 0", fn);
+    }
+    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacetsWide,
+                "%s: max_facets %d outside [1, %d]", fn, params->max_facets, kMaxFacetsWide);
+    BLF_REQUIRE(params->max_iter >= 0, "%s: max_iter < 0", fn);
+    BLF_REQUIRE(params->reserved == 0, "%s: reserved must be 0", fn);
+    BLF_REQUIRE(params->dt > 0 && std::isfinite(params->dt), "%s: dt must be finite and > 0", fn);
+    BLF_REQUIRE(params->w_vrp[0] > 0 && params->w_vrp[1] > 0 && params->w_xi[0] >= 0 &&
+                    params->w_xi[1] >= 0 && params->w_terminal[0] >= 0 && params->w_terminal[1] >= 0,
+                "%s: weights must be R > 0, Q >= 0, P >= 0", fn);
+    BLF_REQUIRE(batch >= 0, "%s: negative batch", fn);
+    BLF_REQUIRE(batch == 0 || (pb.xi_init && pb.omega && solution->xi && solution->vrp &&
+                               solution->status && solution->iters),
+                "%s: null buffer", fn);
+    if (warm) {
+        BLF_REQUIRE(batch == 0 || (warm->vrp && warm->lambda),
+                    "%s: null warm-start buffer", fn);
+        BLF_REQUIRE(warm->shift >= 0, "%s: shift %d < 0", fn, warm->shift);
+        BLF_REQUIRE(warm->reserved == 0, "%s: reserved must be 0", fn);
+        BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
+                    "%s: floor must be finite and > 0", fn);
+        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out &&
+                        (warm->prev_status == nullptr || warm->prev_status != solution->status),
+                    "%s: warm-start buffers must not alias the outputs", fn);
+    }
+    return launch_dcm_mpc_phased(params, ph, start_knot, xi_init, omega, omega_stride, warm, batch,
+                                 win, solution, lambda_out, (hipStream_t)stream, part, pending);
+}
+
 blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params* params,
                                     const blf_phase_table* ph, int64_t start_knot,
                                     const double* xi_init, const double* omega,
@@ -360,52 +415,41 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
                                     const blf_dcm_mpc_solution* solution, double* lambda_out,
                                     void* stream)
 {
-    BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve_phased: null handle");
-    BLF_REQUIRE(params && ph && win && solution, "blf_dcm_mpc_solve_phased: null argument");
-    BLF_REQUIRE(ph->max_phases >= 1, "blf_dcm_mpc_solve_phased: max_phases %d < 1", ph->max_phases);
-    BLF_REQUIRE(ph->max_facets == params->max_facets,
-                "blf_dcm_mpc_solve_phased: phase table max_facets %d != params max_facets %d",
-                ph->max_facets, params->max_facets);
-    BLF_REQUIRE(start_knot >= 0, "blf_dcm_mpc_solve_phased: start_knot < 0");
-    BLF_REQUIRE(omega_stride >= params->horizon, "blf_dcm_mpc_solve_phased: omega_stride %lld < horizon %d",
-                (long long)omega_stride, params->horizon);
-    BLF_REQUIRE(batch == 0 || (ph->nphases && ph->begin && ph->end && ph->A && ph->b && ph->nfacets &&
-                               ph->ref && win->omega && win->xi_ref && win->vrp_ref && win->A &&
-                               win->b && win->nfacets),
-                "blf_dcm_mpc_solve_phased: null buffer");
-    // the QP arguments as blf_dcm_mpc_solve_warm checks them (the window scratch stands in for the
-    // per-knot arrays, which this call does not read)
-    const blf_dcm_mpc_problem pb{xi_init, omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
-    if (batch > 0) {
-        BLF_REQUIRE(params->horizon >= 1 && params->horizon <= 128,
-                    "blf_dcm_mpc_solve_phased: horizon %d outside [1, 128]", params->horizon);
-        BLF_REQUIRE(params->tol_polish > 0, "blf_dcm_mpc_solve_phased: tol_polish must be > 0");
-    }
-    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacetsWide,
-                "blf_dcm_mpc_solve_phased: max_facets %d outside [1, %d]", params->max_facets, kMaxFacetsWide);
-    BLF_REQUIRE(params->max_iter >= 0, "blf_dcm_mpc_solve_phased: max_iter < 0");
-    BLF_REQUIRE(params->reserved == 0, "blf_dcm_mpc_solve_phased: reserved must be 0");
-    BLF_REQUIRE(params->dt > 0 && std::isfinite(params->dt), "blf_dcm_mpc_solve_phased: dt must be finite and > 0");
-    BLF_REQUIRE(params->w_vrp[0] > 0 && params->w_vrp[1] > 0 && params->w_xi[0] >= 0 &&
-                    params->w_xi[1] >= 0 && params->w_terminal[0] >= 0 && params->w_terminal[1] >= 0,
-                "blf_dcm_mpc_solve_phased: weights must be R > 0, Q >= 0, P >= 0");
-    BLF_REQUIRE(batch >= 0, "blf_dcm_mpc_solve_phased: negative batch");
-    BLF_REQUIRE(batch == 0 || (pb.xi_init && pb.omega && solution->xi && solution->vrp &&
-                               solution->status && solution->iters),
-                "blf_dcm_mpc_solve_phased: null buffer");
-    if (warm) {
-        BLF_REQUIRE(batch == 0 || (warm->vrp && warm->lambda),
-                    "blf_dcm_mpc_solve_phased: null warm-start buffer");
-        BLF_REQUIRE(warm->shift >= 0, "blf_dcm_mpc_solve_phased: shift %d < 0", warm->shift);
-        BLF_REQUIRE(warm->reserved == 0, "blf_dcm_mpc_solve_phased: reserved must be 0");
-        BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
-                    "blf_dcm_mpc_solve_phased: floor must be finite and > 0");
-        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out &&
-                        (warm->prev_status == nullptr || warm->prev_status != solution->status),
-                    "blf_dcm_mpc_solve_phased: warm-start buffers must not alias the outputs");
-    }
-    return launch_dcm_mpc_phased(params, ph, start_knot, xi_init, omega, omega_stride, warm, batch,
-                                 win, solution, lambda_out, (hipStream_t)stream);
+    return phased_solve("blf_dcm_mpc_solve_phased", 0, nullptr, handle, params, ph, start_knot, xi_init, omega,
+                        omega_stride, warm, batch, win, solution, lambda_out, stream);
+}
+
+blf_status blf_dcm_mpc_solve_phased_begin(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                          const blf_phase_table* ph, int64_t start_knot,
+                                          const double* xi_init, const double* omega,
+                                          int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
+                                          int64_t batch, const blf_dcm_mpc_window* win,
+                                          const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                          int32_t* pending, void* stream)
+{
+    BLF_REQUIRE(batch == 0 || pending != nullptr, "blf_dcm_mpc_solve_phased_begin: null pending buffer");
+    return phased_solve("blf_dcm_mpc_solve_phased_begin", 1, pending, handle, params, ph, start_knot, xi_init,
+                        omega, omega_stride, warm, batch, win, solution, lambda_out, stream);
+}
+
+blf_status blf_dcm_mpc_solve_phased_finish(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                           const double* xi_init, const blf_dcm_mpc_warm_start* warm,
+                                           int64_t batch, const blf_dcm_mpc_window* win,
+                                           const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                           void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve_phased_finish: null handle");
+    BLF_REQUIRE(params && win && solution, "blf_dcm_mpc_solve_phased_finish: null argument");
+    BLF_REQUIRE(batch >= 0, "blf_dcm_mpc_solve_phased_finish: negative batch");
+    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacetsWide && params->horizon >= 1 &&
+                    params->horizon <= 128 && params->tol_polish > 0,
+                "blf_dcm_mpc_solve_phased_finish: params unlike a phase-indexed solve's");
+    BLF_REQUIRE(batch == 0 || (xi_init && win->omega && win->xi_ref && win->vrp_ref && win->A && win->b &&
+                               win->nfacets && solution->xi && solution->vrp && solution->status &&
+                               solution->iters),
+                "blf_dcm_mpc_solve_phased_finish: null buffer");
+    return launch_dcm_mpc_phased(params, nullptr, 0, xi_init, nullptr, params->horizon, warm, batch, win,
+                                 solution, lambda_out, (hipStream_t)stream, 2, nullptr);
 }
 
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
@@ -575,6 +619,20 @@ blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* 
     return launch_posture_reference(law, com, vrp, vrp_stride, batch, q_ref, (hipStream_t)stream);
 }
 
+blf_status blf_dcm_posture_reference_masked(blf_handle* handle, const blf_posture_law* law,
+                                            const double* com, const double* vrp, int64_t vrp_stride,
+                                            int64_t batch, double* q_ref, const int32_t* mask, int32_t want,
+                                            void* stream)
+{
+    BLF_REQUIRE(batch == 0 || mask != nullptr, "blf_dcm_posture_reference_masked: null mask");
+    BLF_REQUIRE(want == 0 || want == 1, "blf_dcm_posture_reference_masked: want must be 0 or 1");
+    const blf_status st = blf_dcm_posture_reference(handle, law, com, vrp, vrp_stride, 0, q_ref, stream);
+    if (st != BLF_OK) return st;   // the argument checks (batch 0: nothing launched)
+    BLF_REQUIRE(batch >= 0 && vrp_stride >= 2, "blf_dcm_posture_reference_masked: bad batch / vrp stride");
+    BLF_REQUIRE(batch == 0 || (com && vrp && q_ref), "blf_dcm_posture_reference_masked: null buffer");
+    return launch_posture_reference(law, com, vrp, vrp_stride, batch, q_ref, (hipStream_t)stream, mask, want);
+}
+
 blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_model* model,
                                              const blf_fb_state* state,
                                              const blf_joint_impedance* impedance,
@@ -600,6 +658,34 @@ blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_mo
     if (st != BLF_OK) return st;
     return launch_fbd_euler(model, state, nullptr, contacts, mass_reg, batch, iterations, dT,
                             dT_last, (hipStream_t)stream, impedance);
+}
+
+blf_status blf_fbd_euler_integrate_impedance_masked(blf_handle* handle, const blf_fb_model* model,
+                                                    const blf_fb_state* state,
+                                                    const blf_joint_impedance* impedance,
+                                                    const blf_fb_contacts* contacts,
+                                                    const double* mass_reg, int64_t batch,
+                                                    double initial_time, double final_time, double dT,
+                                                    const int32_t* mask, int32_t want, void* stream)
+{
+    BLF_REQUIRE(batch == 0 || mask != nullptr, "blf_fbd_euler_integrate_impedance_masked: null mask");
+    BLF_REQUIRE(want == 0 || want == 1, "blf_fbd_euler_integrate_impedance_masked: want must be 0 or 1");
+    BLF_REQUIRE(impedance != nullptr, "blf_fbd_euler_integrate_impedance_masked: null impedance");
+    BLF_REQUIRE(impedance->reserved == 0, "blf_fbd_euler_integrate_impedance_masked: reserved must be 0");
+    BLF_REQUIRE(impedance->kp && impedance->kd && (batch == 0 || impedance->q_ref),
+                "blf_fbd_euler_integrate_impedance_masked: null impedance array");
+    BLF_REQUIRE(model != nullptr && impedance->ndof == model->ndof,
+                "blf_fbd_euler_integrate_impedance_masked: impedance ndof %d != model ndof %d",
+                impedance->ndof, model ? model->ndof : -1);
+    blf_status st = check_fbd("blf_fbd_euler_integrate_impedance_masked", handle, model, state,
+                              impedance->kp, contacts, batch);
+    if (st != BLF_OK) return st;
+    int iterations = 0;
+    double dT_last = 0.0;
+    st = step_schedule(initial_time, final_time, dT, &iterations, &dT_last);
+    if (st != BLF_OK) return st;
+    return launch_fbd_euler(model, state, nullptr, contacts, mass_reg, batch, iterations, dT,
+                            dT_last, (hipStream_t)stream, impedance, mask, want);
 }
 
 blf_status blf_fbd_euler_integrate(blf_handle* handle, const blf_fb_model* model,

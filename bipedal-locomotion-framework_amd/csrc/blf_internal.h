@@ -62,7 +62,9 @@ struct QpLaunchMode {
     int64_t split_min_batch;   // cold per-knot batches from this size: search + certify kernels
 };
 QpLaunchMode& qp_launch_mode();
-constexpr int64_t kSplitMinBatchDefault = 16384;
+// the split is bit-identical but measured slower at 4096 / 16 384 / 65 536 QPs:
+// off unless blf_set_qp_split_batch / BLF_QP_SPLIT_MIN_BATCH asks for it
+constexpr int64_t kSplitMinBatchDefault = INT64_MAX;
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
                           const blf_dcm_mpc_warm_start* warm, int64_t batch,
                           const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);
@@ -70,7 +72,8 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
                                  int64_t start_knot, const double* xi_init, const double* omega,
                                  int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                  int64_t batch, const blf_dcm_mpc_window* win,
-                                 const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);
+                                 const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s,
+                                 int part = 0, int32_t* pending = nullptr);
 blf_status launch_contact_eval(const double* prm, int shared, const double* twist,
                                const double* pose, const double* null_pose, int64_t batch,
                                double* wrench, double* autonomous, double* control,
@@ -88,12 +91,14 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s,
-                            const blf_joint_impedance* impedance = nullptr);
+                            const blf_joint_impedance* impedance = nullptr, const int32_t* mask = nullptr,
+                            int want = 1);
 size_t fbd_lds_bytes(int n, int C);
 blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const double* omega0,
                          int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s);
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
-                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s);
+                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s,
+                                    const int32_t* mask = nullptr, int want = 1);
 blf_status launch_fbk_euler(int n, double rho, double* pos, double* rot, double* joints,
                             const double* twist, const double* joint_vel, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s);

@@ -126,6 +126,14 @@ blf_status launch_ipm(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     if (N <= 1024) return launch_nt<1024>(kp, pb, warm, batch, sol, lam_out, s);
     return set_error(BLF_ERR_UNSUPPORTED, "horizon %d > 1024", N);
 }
+
+// pending[p] = 1 for the QPs the active-set kernel handed to stage 2 (status kPending), else 0
+__global__ __launch_bounds__(256) void pending_mask_kernel(const int32_t* __restrict__ status, int64_t batch,
+                                                           int32_t* __restrict__ pending)
+{
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p < batch) pending[p] = status[p] == kPending ? 1 : 0;
+}
 }  // namespace
 
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
@@ -152,14 +160,29 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
 // blf_dcm_mpc_solve_phased: the active-set kernels read the window from the phase table (PhaseSrc);
 // the QPs they hand over (kPending) leave their expanded window in the caller's scratch, from
 // which the IPM kernel's stage 2 continues exactly as after blf_dcm_phase_expand + solve.
+// part: 0 the whole solve; 1 the active-set part alone (stage 2's QPs left at kPending, their
+// windows in the scratch, `pending` marking them); 2 stage 2 alone (blf_dcm_mpc_solve_phased_begin /
+// _finish: parts 1 then 2 on one stream are part 0).  With more than 8 facet slots there is no
+// active-set part: part 1 solves everything and marks nothing, part 2 does nothing.
 blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_table* ph,
                                  int64_t start_knot, const double* xi_init, const double* omega,
                                  int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                  int64_t batch, const blf_dcm_mpc_window* win,
-                                 const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+                                 const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
+                                 int part, int32_t* pending)
 {
     KParams kp = make_kparams(prm, warm);
     if (batch == 0) return BLF_OK;
+    if (part == 2) {
+        if (kp.M > kMaxFacets) return BLF_OK;
+        kp.stage2 = 1;
+        const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
+        return launch_ipm(kp, &pw, warm, batch, sol, lam_out, s);
+    }
+    if (pending && (kp.M > kMaxFacets || part == 0)) {
+        blf_status st = check_hip(hipMemsetAsync(pending, 0, sizeof(int32_t) * (size_t)batch, s), "pending mask");
+        if (st != BLF_OK) return st;
+    }
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     if (kp.N > 2 * kWave || !(kp.tol_polish > 0.0))
         return set_error(BLF_ERR_UNSUPPORTED,
@@ -200,6 +223,12 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
     const blf_dcm_mpc_problem pin{xi_init, omega, nullptr, nullptr, nullptr, nullptr, nullptr};
     const blf_status st = launch_dcm_mpc_as(kp, &pin, warm, batch, sol, lam_out, s, &ps);
     if (st != BLF_OK) return st;
+    if (part == 1) {
+        if (!pending) return BLF_OK;
+        hipLaunchKernelGGL(pending_mask_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256), 0, s,
+                           sol->status, batch, pending);
+        return check_hip(hipGetLastError(), "pending_mask_kernel launch");
+    }
     kp.stage2 = 1;
     const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
     return launch_ipm(kp, &pw, warm, batch, sol, lam_out, s);

@@ -1002,8 +1002,10 @@ __device__ __forceinline__ void ipm_solve(
         for (it = 0; status == 0; ++it) {
             if (BLF_SAT_ON && sat_pending) {
                 sat_pending = false;
+                STAMP(t_sat);   // (stamp builds: the saturated start counts as start-up, slot 12)
                 const bool oks = sat_start<NW>(K, P, L, R, bnd, N, nwa, k, wv, lane, own, last, mmax, xi00, xi01,
                                                rref, xref, xb0, xb1, mu, pres, dres);
+                STAMP_ADD(12, t_sat);
                 if (__syncthreads_or(!oks)) {
                     status = BLF_QP_NUMERICAL;
                     it = 0;

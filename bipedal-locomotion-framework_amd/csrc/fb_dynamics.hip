@@ -895,6 +895,13 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
 struct Impedance {
     const double *kp, *kd, *qref;
 };
+// A subset of the batch (blf_fbd_euler_integrate_impedance_masked): system q runs iff
+// (mask[q] != 0) == want; mask == nullptr: every system.
+struct Select {
+    const int32_t* mask;
+    int want;
+    __device__ __forceinline__ bool has(int64_t q) const { return !mask || ((mask[q] != 0) == (want != 0)); }
+};
 
 template <int NVMAX, int HW, bool PRI>
 // Two systems per wavefront (HW = 32) keep more state live per wave: capping it at 256 VGPRs for
@@ -904,15 +911,18 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
                                                           const double* __restrict__ tau,
                                                           Contacts ct, const double* reg,
                                                           int32_t nsteps, double dT, double dT_last,
-                                                          Impedance imp, int64_t batch)
+                                                          Impedance imp, int64_t batch, Select sel)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const Half<HW> H;
     const int n = m.n, NV = n + 6;
     const Smem S(smem + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
     const int64_t q0 = (int64_t)blockIdx.x * (kWave / HW) + H.half;
-    const bool active = q0 < batch;   // see fbd_dynamics_kernel
-    const int64_t q = active ? q0 : batch - 1;
+    // a system outside the batch or outside the selection is computed (as the other half's
+    // partner) and written nowhere; a wavefront with no selected system leaves at once
+    const bool active = q0 < batch && sel.has(q0);   // see fbd_dynamics_kernel
+    if (__ballot(active) == 0ull) return;
+    const int64_t q = q0 < batch ? q0 : batch - 1;
     const int lane = H.hl;
     double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n | dR 9
     double* dR = loc + 18 + 2 * n;
@@ -1034,11 +1044,12 @@ __global__ __launch_bounds__(256) void posture_reference_kernel(int n, const dou
                                                                 const double* __restrict__ com,
                                                                 const double* __restrict__ vrp,
                                                                 int64_t vstride, int64_t total,
-                                                                double* __restrict__ qref)
+                                                                double* __restrict__ qref, Select sel)
 {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     const int64_t q = e / n;
+    if (!sel.has(q)) return;
     const int j = (int)(e - q * n);
     const double ex = vrp[q * vstride] - com[6 * q];
     const double ey = vrp[q * vstride + 1] - com[6 * q + 1];
@@ -1103,9 +1114,10 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s,
-                            const blf_joint_impedance* impedance)
+                            const blf_joint_impedance* impedance, const int32_t* mask, int want)
 {
     if (batch == 0) return BLF_OK;
+    const Select sel{mask, want};
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     Impedance imp{nullptr, nullptr, nullptr};
@@ -1117,16 +1129,16 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
     if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true> : fbd_euler_kernel<32, 32, false>),
                            dim3((unsigned)ceil_div(batch, 2)), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
-                           reg, nsteps, dT, dT_last, imp, batch);
+                           reg, nsteps, dT, dT_last, imp, batch, sel);
     else if (md->ndof + 6 <= 32)   // one system per wavefront, NV <= 32 rows
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, kWave, true> : fbd_euler_kernel<32, kWave, false>),
                            dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
-                           dT_last, imp, batch);
+                           dT_last, imp, batch, sel);
     else
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, true>
                                 : fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, false>),
                            dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
-                           dT_last, imp, batch);
+                           dT_last, imp, batch, sel);
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
 }
 
@@ -1142,12 +1154,13 @@ blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const d
 }
 
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
-                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s)
+                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s,
+                                    const int32_t* mask, int want)
 {
     const int64_t total = batch * law->ndof;
     if (total == 0) return BLF_OK;
     hipLaunchKernelGGL(posture_reference_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       law->ndof, law->q_nominal, law->lean, com, vrp, vstride, total, qref);
+                       law->ndof, law->q_nominal, law->lean, com, vrp, vstride, total, qref, Select{mask, want});
     return check_hip(hipGetLastError(), "posture_reference_kernel launch");
 }
 

@@ -93,7 +93,7 @@ blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel);
  * least min_batch QPs run the active-set search and its fp64 certification as two kernels (more
  * resident search wavefronts; the same bits as the one-kernel path).  min_batch 0: never; < 0:
  * unchanged.  *previous (optional) receives the setting before the call (0: never).  Initial value
- * from BLF_QP_SPLIT_MIN_BATCH, else the library's default. */
+ * from BLF_QP_SPLIT_MIN_BATCH, else never (the split measured slower). */
 blf_status blf_set_qp_split_batch(int64_t min_batch, int64_t* previous);
 
 /* ---- 0. FixedStepIntegrator::integrate's step schedule (FixedStepIntegrator.tpp:21-72) -------
@@ -340,6 +340,26 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
                                     int64_t batch, const blf_dcm_mpc_window* window,
                                     const blf_dcm_mpc_solution* solution, double* lambda_out,
                                     void* stream);
+/* blf_dcm_mpc_solve_phased in two calls, so that a caller can go on with the problems solved by
+ * the active-set kernel while the interior point kernel finishes the rest on another stream.
+ * _begin: the active-set kernel (every argument as for blf_dcm_mpc_solve_phased); the problems it
+ * hands over get status -1 and pending[q] = 1 (others 0), their windows expanded into `window`.
+ * _finish: the interior point kernel on those, with the same params, xi_init, warm, window,
+ * solution and lambda_out as the _begin call.  _begin then _finish on one stream give the same bits
+ * as blf_dcm_mpc_solve_phased.  With max_facets > 8 (no active-set kernel) _begin solves every
+ * problem and marks none, and _finish does nothing. */
+blf_status blf_dcm_mpc_solve_phased_begin(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                          const blf_phase_table* phases, int64_t start_knot,
+                                          const double* xi_init, const double* omega,
+                                          int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
+                                          int64_t batch, const blf_dcm_mpc_window* window,
+                                          const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                          int32_t* pending, void* stream);
+blf_status blf_dcm_mpc_solve_phased_finish(blf_handle* handle, const blf_dcm_mpc_params* params,
+                                           const double* xi_init, const blf_dcm_mpc_warm_start* warm,
+                                           int64_t batch, const blf_dcm_mpc_window* window,
+                                           const blf_dcm_mpc_solution* solution, double* lambda_out,
+                                           void* stream);
 
 /* ---- 6. Contact model (ContinuousContactModel), batched ------------------------------------
  * Rectangular L x W patch, spring k, damper b (ContinuousContactModel.h:22-57).
@@ -481,6 +501,12 @@ typedef struct blf_posture_law {
 blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* law,
                                      const double* com, const double* vrp, int64_t vrp_stride,
                                      int64_t batch, double* q_ref, void* stream);
+/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1); the other rows of q_ref
+ * are not written. */
+blf_status blf_dcm_posture_reference_masked(blf_handle* handle, const blf_posture_law* law,
+                                            const double* com, const double* vrp, int64_t vrp_stride,
+                                            int64_t batch, double* q_ref, const int32_t* mask,
+                                            int32_t want, void* stream);
 
 /* blf_fbd_euler_integrate_impedance: ForwardEuler<FloatingBaseDynamicalSystem>::integrate(t0, T)
  * (the schedule of blf_fbd_euler_integrate) with the control input set before EVERY step from a
@@ -501,6 +527,16 @@ blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_mo
                                              const double* mass_reg, int64_t batch,
                                              double initial_time, double final_time, double dT,
                                              void* stream);
+/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1); the others' state is
+ * neither read for their results nor written.  A closed loop integrates the systems whose plan is
+ * ready while the rest wait for theirs (blf_dcm_mpc_solve_phased_begin / _finish). */
+blf_status blf_fbd_euler_integrate_impedance_masked(blf_handle* handle, const blf_fb_model* model,
+                                                    const blf_fb_state* state,
+                                                    const blf_joint_impedance* impedance,
+                                                    const blf_fb_contacts* contacts,
+                                                    const double* mass_reg, int64_t batch,
+                                                    double initial_time, double final_time, double dT,
+                                                    const int32_t* mask, int32_t want, void* stream);
 
 /* Algorithmic flop count of one IPM iteration of one problem (what the fp64 roofline field
  * of bench.py is computed from); `active_facets` = sum_k nfacets[k]. */

@@ -180,6 +180,30 @@ def test_closed_loop_stream_groups_bitwise(handle):
                                       torch.cat([lp.state[k] for lp in groups]).cpu().numpy(), err_msg=k)
 
 
+def test_closed_loop_overlap_bitwise(handle):
+    """ClosedLoop(overlap=True) (bench.py --c5-overlap): the robots the active-set kernel solved go
+    on to the posture and the dynamics while the interior point kernel finishes the others on a
+    side stream (blf_dcm_mpc_solve_phased_begin / _finish, the masked kernels).  Pushed robots (a
+    lateral base velocity: uncapturable DCM states) make sure some windows take that path; every
+    robot's state and plan equal the one-stream loop's bit for bit."""
+    B, S = 160, 4
+    plan, st = _setup(B, S)
+    st["base_vel"][::5, 1] += 1.2
+    one = DL.ClosedLoop(handle, MODEL, plan, st)
+    ovl = DL.ClosedLoop(handle, MODEL, plan, st, overlap=True)
+    npend = 0
+    for s in range(S):
+        out1 = one.period()
+        out2 = ovl.period()
+        torch.cuda.synchronize()
+        npend += int(out2["pending"].sum())
+        for k in ("xi", "vrp", "status", "iters", "polished", "lam"):
+            np.testing.assert_array_equal(out1[k].cpu().numpy(), out2[k].cpu().numpy(), err_msg=f"{k} period {s}")
+    assert npend > 0, "no window went to the interior point kernel"
+    for k in native.FB_STATE_KEYS:
+        np.testing.assert_array_equal(one.state[k].cpu().numpy(), ovl.state[k].cpu().numpy(), err_msg=k)
+
+
 def test_closed_loop_config5_full_size(handle):
     """configs[4] at its size on one GPU: 16 384 robots, three coupled periods; finite states,
     every plan solved, xi_init = the robot's DCM."""
