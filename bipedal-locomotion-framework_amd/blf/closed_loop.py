@@ -79,7 +79,9 @@ class ClosedLoop:
         # their own posture and dynamics follow (blf_dcm_mpc_solve_phased_begin / _finish and the
         # masked kernels).  Every robot's computation is the same, so the states are the same bits.
         self.overlap = bool(overlap)
-        self.side = torch.cuda.Stream(device=h.device) if self.overlap else None
+        # the side stream at high priority: its few waves take the SIMDs the dynamics kernel frees
+        # before that kernel's queued waves (otherwise they would wait for the whole launch)
+        self.side = torch.cuda.Stream(device=h.device, priority=-1) if self.overlap else None
         dev = torch.device("cuda", h.device)
         t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
         self.dt = float(plan["dt"])
@@ -157,14 +159,17 @@ class ClosedLoop:
         ready = torch.cuda.Event()
         ready.record(main)
         self.side.wait_event(ready)
-        pending = out["pending"]
+        pending, plist = out["pending"], out["pending_list"]
+        # the side stream works through the pending list with a few workgroups per kernel: a
+        # batch-sized grid there would be dispatched only as the main stream's dynamics frees the
+        # chip, and end with it
         h.dcm_mpc_solve_phased_finish(self.xi, self.params, out, warm=warm, lambda_out=True, stream=self.side)
-        for stream, want in ((self.side, 1), (main, 0)):
-            h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=stream,
-                                mask=pending, want=want)
-            h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T,
-                                            self.dT, contacts=self.contacts, stream=stream,
-                                            mask=pending, want=want)
+        h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=self.side, rows=plist)
+        h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T, self.dT,
+                                        contacts=self.contacts, stream=self.side, rows=plist)
+        h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=main, mask=pending, want=0)
+        h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T, self.dT,
+                                        contacts=self.contacts, stream=main, mask=pending, want=0)
         done = torch.cuda.Event()
         done.record(self.side)
         main.wait_event(done)

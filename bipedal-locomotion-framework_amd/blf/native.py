@@ -165,11 +165,11 @@ def lib():
                                                ctypes.POINTER(DcmMpcWarmStart), _i64,
                                                ctypes.POINTER(DcmMpcWindow),
                                                ctypes.POINTER(DcmMpcSolution), _vp, _vp]
-        L.blf_dcm_mpc_solve_phased_begin.argtypes = L.blf_dcm_mpc_solve_phased.argtypes[:-1] + [_vp, _vp]
+        L.blf_dcm_mpc_solve_phased_begin.argtypes = L.blf_dcm_mpc_solve_phased.argtypes[:-1] + [_vp, _vp, _vp]
         L.blf_dcm_mpc_solve_phased_finish.argtypes = [_vp, ctypes.POINTER(DcmMpcParams), _vp,
                                                       ctypes.POINTER(DcmMpcWarmStart), _i64,
                                                       ctypes.POINTER(DcmMpcWindow),
-                                                      ctypes.POINTER(DcmMpcSolution), _vp, _vp]
+                                                      ctypes.POINTER(DcmMpcSolution), _vp, _vp, _vp]
         L.blf_dcm_mpc_flops_per_iter.argtypes = [_i32, _i64]
         L.blf_contact_model_eval.argtypes = [_vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                              _vp, _vp]
@@ -192,9 +192,9 @@ def lib():
             _vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), ctypes.POINTER(JointImpedance),
             ctypes.POINTER(FbContacts), _vp, _i64, _f64, _f64, _f64, _vp]
         L.blf_dcm_posture_reference_masked.argtypes = [_vp, ctypes.POINTER(PostureLaw), _vp, _vp, _i64,
-                                                       _i64, _vp, _vp, _i32, _vp]
+                                                       _i64, _vp, _vp, _i32, _vp, _vp]
         L.blf_fbd_euler_integrate_impedance_masked.argtypes = (
-            L.blf_fbd_euler_integrate_impedance.argtypes[:-1] + [_vp, _i32, _vp])
+            L.blf_fbd_euler_integrate_impedance.argtypes[:-1] + [_vp, _i32, _vp, _vp])
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         L.blf_set_qp_launch_mode.argtypes = [_i32, _i32]
         L.blf_set_qp_split_batch.argtypes = [_i64, _vp]
@@ -650,8 +650,10 @@ class Handle:
         if begin:
             if "pending" not in out:
                 out["pending"] = torch.empty((B,), dtype=torch.int32, device=dev)
+                out["pending_list"] = torch.empty((B + 1,), dtype=torch.int32, device=dev)
             _check(lib().blf_dcm_mpc_solve_phased_begin(
-                *args, _ptr(out["pending"], torch.int32, (B,), "pending"), _stream(stream)))
+                *args, _ptr(out["pending"], torch.int32, (B,), "pending"),
+                _ptr(out["pending_list"], torch.int32, (B + 1,), "pending_list"), _stream(stream)))
         else:
             _check(lib().blf_dcm_mpc_solve_phased(*args, _stream(stream)))
         return out
@@ -679,10 +681,11 @@ class Handle:
         ws = _warm_start(warm, B, N, M) if warm is not None else None
         lam_ptr = _ptr(out["lam"], torch.float64, (B, N, M), "lam") if lambda_out else None
         self._keep_finish = (so, ws, win)
+        lst = out.get("pending_list")
         _check(lib().blf_dcm_mpc_solve_phased_finish(
             self._h, ctypes.byref(params), _ptr(xi_init, torch.float64, (B, 2), "xi_init"),
             ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(win), ctypes.byref(so), lam_ptr,
-            _stream(stream)))
+            _ptr(lst, torch.int32, (B + 1,), "pending_list") if lst is not None else None, _stream(stream)))
         return out
 
     # --- C3 pipeline: corner sets -> polygons (device hull) -> QP arrays ---
@@ -892,10 +895,11 @@ class Handle:
         law.c = c
         return law
 
-    def posture_reference(self, law, com, vrp, q_ref=None, stream=None, mask=None, want=1):
+    def posture_reference(self, law, com, vrp, q_ref=None, stream=None, mask=None, want=1, rows=None):
         """blf_dcm_posture_reference: joint references [B,n] from the plan's first VRP (vrp
         [B,N,2], a blf_dcm_mpc_solve output) and the centre of mass com [B,6] (fb_dcm).
-        mask [B] int32 (device): only the rows with (mask != 0) == want (blf_..._masked)."""
+        mask [B] int32 (device): only the rows with (mask != 0) == want; rows [B+1] int32
+        (device, count then indices): only those (blf_..._masked)."""
         torch = _torch()
         B, N = vrp.shape[0], vrp.shape[1]
         n = law.c.ndof
@@ -904,11 +908,12 @@ class Handle:
         args = (self._h, ctypes.byref(law.c), _ptr(com, torch.float64, (B, 6), "com"),
                 _ptr(vrp, torch.float64, (B, N, 2), "vrp"), 2 * N, B,
                 _ptr(q_ref, torch.float64, (B, n), "q_ref"))
-        if mask is None:
+        if mask is None and rows is None:
             _check(lib().blf_dcm_posture_reference(*args, _stream(stream)))
         else:
-            _check(lib().blf_dcm_posture_reference_masked(*args, _ptr(mask, torch.int32, (B,), "mask"),
-                                                          int(want), _stream(stream)))
+            _check(lib().blf_dcm_posture_reference_masked(
+                *args, _ptr(mask, torch.int32, (B,), "mask") if mask is not None else None, int(want),
+                _ptr(rows, torch.int32, (B + 1,), "rows") if rows is not None else None, _stream(stream)))
         return q_ref
 
     def joint_impedance(self, kp, kd):
@@ -919,10 +924,11 @@ class Handle:
         return dict(kp=f64(kp), kd=f64(kd))
 
     def fbd_euler_integrate_impedance(self, dm, state, impedance, q_ref, t0, t1, dT, contacts=None,
-                                      mass_reg=None, stream=None, mask=None, want=1):
+                                      mass_reg=None, stream=None, mask=None, want=1, rows=None):
         """blf_fbd_euler_integrate_impedance in place on `state`: the control input of every
         Euler step is tau = kp (q_ref - q) - kd qdot (impedance: joint_impedance()).
-        mask [B] int32 (device): only the systems with (mask != 0) == want (blf_..._masked)."""
+        mask [B] int32 (device): only the systems with (mask != 0) == want; rows [B+1] int32
+        (device, count then indices): only those (blf_..._masked)."""
         torch = _torch()
         B, n = state["joint_pos"].shape
         NV = n + 6
@@ -934,9 +940,10 @@ class Handle:
         imp.q_ref = _ptr(q_ref, torch.float64, (B, n), "q_ref")
         args = (self._h, ctypes.byref(dm.c), ctypes.byref(self._fb_state(state, B, n)), ctypes.byref(imp),
                 ctypes.byref(self._fb_contacts(contacts, B)), reg, B, float(t0), float(t1), float(dT))
-        if mask is None:
+        if mask is None and rows is None:
             _check(lib().blf_fbd_euler_integrate_impedance(*args, _stream(stream)))
         else:
             _check(lib().blf_fbd_euler_integrate_impedance_masked(
-                *args, _ptr(mask, torch.int32, (B,), "mask"), int(want), _stream(stream)))
+                *args, _ptr(mask, torch.int32, (B,), "mask") if mask is not None else None, int(want),
+                _ptr(rows, torch.int32, (B + 1,), "rows") if rows is not None else None, _stream(stream)))
         return state

@@ -352,7 +352,7 @@ blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* 
     return launch_dcm_mpc(params, problem, warm, batch, solution, lambda_out, (hipStream_t)stream);
 }
 
-static blf_status phased_solve(const char* fn, int part, int32_t* pending, blf_handle* handle,
+static blf_status phased_solve(const char* fn, int part, int32_t* pending, int32_t* list, blf_handle* handle,
                                const blf_dcm_mpc_params* params, const blf_phase_table* ph, int64_t start_knot,
                                const double* xi_init, const double* omega, int64_t omega_stride,
                                const blf_dcm_mpc_warm_start* warm, int64_t batch,
@@ -404,7 +404,7 @@ static blf_status phased_solve(const char* fn, int part, int32_t* pending, blf_h
                     "%s: warm-start buffers must not alias the outputs", fn);
     }
     return launch_dcm_mpc_phased(params, ph, start_knot, xi_init, omega, omega_stride, warm, batch,
-                                 win, solution, lambda_out, (hipStream_t)stream, part, pending);
+                                 win, solution, lambda_out, (hipStream_t)stream, part, pending, list);
 }
 
 blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params* params,
@@ -415,7 +415,7 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
                                     const blf_dcm_mpc_solution* solution, double* lambda_out,
                                     void* stream)
 {
-    return phased_solve("blf_dcm_mpc_solve_phased", 0, nullptr, handle, params, ph, start_knot, xi_init, omega,
+    return phased_solve("blf_dcm_mpc_solve_phased", 0, nullptr, nullptr, handle, params, ph, start_knot, xi_init, omega,
                         omega_stride, warm, batch, win, solution, lambda_out, stream);
 }
 
@@ -425,10 +425,10 @@ blf_status blf_dcm_mpc_solve_phased_begin(blf_handle* handle, const blf_dcm_mpc_
                                           int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                           int64_t batch, const blf_dcm_mpc_window* win,
                                           const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                          int32_t* pending, void* stream)
+                                          int32_t* pending, int32_t* pending_list, void* stream)
 {
     BLF_REQUIRE(batch == 0 || pending != nullptr, "blf_dcm_mpc_solve_phased_begin: null pending buffer");
-    return phased_solve("blf_dcm_mpc_solve_phased_begin", 1, pending, handle, params, ph, start_knot, xi_init,
+    return phased_solve("blf_dcm_mpc_solve_phased_begin", 1, pending, pending_list, handle, params, ph, start_knot, xi_init,
                         omega, omega_stride, warm, batch, win, solution, lambda_out, stream);
 }
 
@@ -436,7 +436,7 @@ blf_status blf_dcm_mpc_solve_phased_finish(blf_handle* handle, const blf_dcm_mpc
                                            const double* xi_init, const blf_dcm_mpc_warm_start* warm,
                                            int64_t batch, const blf_dcm_mpc_window* win,
                                            const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                           void* stream)
+                                           const int32_t* pending_list, void* stream)
 {
     BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve_phased_finish: null handle");
     BLF_REQUIRE(params && win && solution, "blf_dcm_mpc_solve_phased_finish: null argument");
@@ -449,7 +449,8 @@ blf_status blf_dcm_mpc_solve_phased_finish(blf_handle* handle, const blf_dcm_mpc
                                solution->iters),
                 "blf_dcm_mpc_solve_phased_finish: null buffer");
     return launch_dcm_mpc_phased(params, nullptr, 0, xi_init, nullptr, params->horizon, warm, batch, win,
-                                 solution, lambda_out, (hipStream_t)stream, 2, nullptr);
+                                 solution, lambda_out, (hipStream_t)stream, 2, nullptr,
+                                 const_cast<int32_t*>(pending_list));
 }
 
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
@@ -622,15 +623,15 @@ blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* 
 blf_status blf_dcm_posture_reference_masked(blf_handle* handle, const blf_posture_law* law,
                                             const double* com, const double* vrp, int64_t vrp_stride,
                                             int64_t batch, double* q_ref, const int32_t* mask, int32_t want,
-                                            void* stream)
+                                            const int32_t* list, void* stream)
 {
-    BLF_REQUIRE(batch == 0 || mask != nullptr, "blf_dcm_posture_reference_masked: null mask");
+    BLF_REQUIRE(batch == 0 || mask != nullptr || list != nullptr, "blf_dcm_posture_reference_masked: null mask");
     BLF_REQUIRE(want == 0 || want == 1, "blf_dcm_posture_reference_masked: want must be 0 or 1");
     const blf_status st = blf_dcm_posture_reference(handle, law, com, vrp, vrp_stride, 0, q_ref, stream);
     if (st != BLF_OK) return st;   // the argument checks (batch 0: nothing launched)
     BLF_REQUIRE(batch >= 0 && vrp_stride >= 2, "blf_dcm_posture_reference_masked: bad batch / vrp stride");
     BLF_REQUIRE(batch == 0 || (com && vrp && q_ref), "blf_dcm_posture_reference_masked: null buffer");
-    return launch_posture_reference(law, com, vrp, vrp_stride, batch, q_ref, (hipStream_t)stream, mask, want);
+    return launch_posture_reference(law, com, vrp, vrp_stride, batch, q_ref, (hipStream_t)stream, mask, want, list);
 }
 
 blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_model* model,
@@ -666,9 +667,11 @@ blf_status blf_fbd_euler_integrate_impedance_masked(blf_handle* handle, const bl
                                                     const blf_fb_contacts* contacts,
                                                     const double* mass_reg, int64_t batch,
                                                     double initial_time, double final_time, double dT,
-                                                    const int32_t* mask, int32_t want, void* stream)
+                                                    const int32_t* mask, int32_t want, const int32_t* list,
+                                                    void* stream)
 {
-    BLF_REQUIRE(batch == 0 || mask != nullptr, "blf_fbd_euler_integrate_impedance_masked: null mask");
+    BLF_REQUIRE(batch == 0 || mask != nullptr || list != nullptr,
+                "blf_fbd_euler_integrate_impedance_masked: null mask");
     BLF_REQUIRE(want == 0 || want == 1, "blf_fbd_euler_integrate_impedance_masked: want must be 0 or 1");
     BLF_REQUIRE(impedance != nullptr, "blf_fbd_euler_integrate_impedance_masked: null impedance");
     BLF_REQUIRE(impedance->reserved == 0, "blf_fbd_euler_integrate_impedance_masked: reserved must be 0");
@@ -685,7 +688,7 @@ blf_status blf_fbd_euler_integrate_impedance_masked(blf_handle* handle, const bl
     st = step_schedule(initial_time, final_time, dT, &iterations, &dT_last);
     if (st != BLF_OK) return st;
     return launch_fbd_euler(model, state, nullptr, contacts, mass_reg, batch, iterations, dT,
-                            dT_last, (hipStream_t)stream, impedance, mask, want);
+                            dT_last, (hipStream_t)stream, impedance, mask, want, list);
 }
 
 blf_status blf_fbd_euler_integrate(blf_handle* handle, const blf_fb_model* model,

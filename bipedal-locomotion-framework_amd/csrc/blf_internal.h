@@ -14,6 +14,8 @@ namespace blf {
 constexpr int kWave = 64;   // CDNA wavefront width
 constexpr int kMaxFacets = 8;       // facet slots per knot of the active-set kernels (and the default)
 constexpr int kMaxFacetsWide = 16;  // max_facets up to this: the interior point kernel alone
+// grid of a kernel that loops over a pending list (stage 2, the closed loop's side stream)
+constexpr int kListGrid = 64;
 
 // ---- error plumbing (blf_capi.hip) ----
 blf_status set_error(blf_status code, const char* fmt, ...);
@@ -73,7 +75,8 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
                                  int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                  int64_t batch, const blf_dcm_mpc_window* win,
                                  const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s,
-                                 int part = 0, int32_t* pending = nullptr);
+                                 int part = 0, int32_t* pending = nullptr, int32_t* list = nullptr);
+
 blf_status launch_contact_eval(const double* prm, int shared, const double* twist,
                                const double* pose, const double* null_pose, int64_t batch,
                                double* wrench, double* autonomous, double* control,
@@ -92,13 +95,13 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s,
                             const blf_joint_impedance* impedance = nullptr, const int32_t* mask = nullptr,
-                            int want = 1);
+                            int want = 1, const int32_t* list = nullptr);
 size_t fbd_lds_bytes(int n, int C);
 blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const double* omega0,
                          int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s);
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
                                     int64_t vstride, int64_t batch, double* qref, hipStream_t s,
-                                    const int32_t* mask = nullptr, int want = 1);
+                                    const int32_t* mask = nullptr, int want = 1, const int32_t* list = nullptr);
 blf_status launch_fbk_euler(int n, double rho, double* pos, double* rot, double* joints,
                             const double* twist, const double* joint_vel, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s);

@@ -39,8 +39,18 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     double* __restrict__ vrp_out, int32_t* __restrict__ status_out,
     int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out)
 {
-    ipm_solve<NT, WARM, LAMOUT, MF>(P, blockIdx.x, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, ws_vrp,
-                                ws_lam, xi_out, vrp_out, status_out, iters_out, polished_out, lam_out);
+    // one problem per workgroup, or stage 2 over the pending list: a grid of a few workgroups,
+    // each taking every gridDim-th listed problem (the whole batch's grid would have to be
+    // dispatched beside whatever else holds the chip -- the closed loop's dynamics -- before the
+    // launch could end).  One call site of the solve either way.
+    const bool lst = P.list != nullptr;
+    const int count = lst ? P.list[0] : (int)blockIdx.x + 1;
+    for (int i = lst ? (int)blockIdx.x : (int)blockIdx.x; i < count; i += lst ? (int)gridDim.x : count) {
+        const int64_t p = lst ? P.list[1 + i] : (int64_t)blockIdx.x;
+        ipm_solve<NT, WARM, LAMOUT, MF>(P, p, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, ws_vrp,
+                                    ws_lam, xi_out, vrp_out, status_out, iters_out, polished_out, lam_out);
+        if (lst) __syncthreads();   // the LDS is the next problem's
+    }
 }
 
 // MF facet slots per knot in the registers: 8, or 16 when max_facets > 8 (support polygons of up
@@ -57,7 +67,9 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
     auto kern = (warm != nullptr)
                     ? (lam_out ? dcm_mpc_ipm_kernel<NT, true, true, MF> : dcm_mpc_ipm_kernel<NT, true, false, MF>)
                     : (lam_out ? dcm_mpc_ipm_kernel<NT, false, true, MF> : dcm_mpc_ipm_kernel<NT, false, false, MF>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(NT), lds, s, kp,
+    // a pending list: at most kListGrid workgroups loop over it
+    const unsigned grid = kp.list ? (unsigned)std::min<int64_t>(batch, kListGrid) : (unsigned)batch;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                        pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr,
                        sol->xi, sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
@@ -99,6 +111,7 @@ KParams make_kparams(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_warm_start
     kp.ws_floor = warm ? warm->floor : 0.0;
     kp.ws_status = warm ? warm->prev_status : nullptr;
     kp.stage2 = 0;
+    kp.list = nullptr;
     kp.f_dt = (float)kp.dt;
     kp.f_Qw0 = (float)kp.Qw0; kp.f_Qw1 = (float)kp.Qw1;
     kp.f_Rw0 = (float)kp.Rw0; kp.f_Rw1 = (float)kp.Rw1;
@@ -127,12 +140,17 @@ blf_status launch_ipm(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     return set_error(BLF_ERR_UNSUPPORTED, "horizon %d > 1024", N);
 }
 
-// pending[p] = 1 for the QPs the active-set kernel handed to stage 2 (status kPending), else 0
+// pending[p] = 1 for the QPs the active-set kernel handed to stage 2 (status kPending), else 0;
+// list (optional, list[0] zeroed before): their indices appended after the count, in no
+// particular order (each problem is solved on its own, so the order changes no result)
 __global__ __launch_bounds__(256) void pending_mask_kernel(const int32_t* __restrict__ status, int64_t batch,
-                                                           int32_t* __restrict__ pending)
+                                                           int32_t* __restrict__ pending, int32_t* __restrict__ list)
 {
     const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p < batch) pending[p] = status[p] == kPending ? 1 : 0;
+    if (p >= batch) return;
+    const bool pend = status[p] == kPending;
+    pending[p] = pend ? 1 : 0;
+    if (list && pend) list[1 + atomicAdd(&list[0], 1)] = (int32_t)p;
 }
 }  // namespace
 
@@ -169,18 +187,23 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
                                  int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                  int64_t batch, const blf_dcm_mpc_window* win,
                                  const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
-                                 int part, int32_t* pending)
+                                 int part, int32_t* pending, int32_t* list)
 {
     KParams kp = make_kparams(prm, warm);
     if (batch == 0) return BLF_OK;
     if (part == 2) {
         if (kp.M > kMaxFacets) return BLF_OK;
         kp.stage2 = 1;
+        kp.list = list;
         const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
         return launch_ipm(kp, &pw, warm, batch, sol, lam_out, s);
     }
     if (pending && (kp.M > kMaxFacets || part == 0)) {
         blf_status st = check_hip(hipMemsetAsync(pending, 0, sizeof(int32_t) * (size_t)batch, s), "pending mask");
+        if (st != BLF_OK) return st;
+    }
+    if (list) {   // the count; the kernel below (or nothing, M > 8) appends
+        blf_status st = check_hip(hipMemsetAsync(list, 0, sizeof(int32_t), s), "pending list");
         if (st != BLF_OK) return st;
     }
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
@@ -226,7 +249,7 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
     if (part == 1) {
         if (!pending) return BLF_OK;
         hipLaunchKernelGGL(pending_mask_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256), 0, s,
-                           sol->status, batch, pending);
+                           sol->status, batch, pending, list);
         return check_hip(hipGetLastError(), "pending_mask_kernel launch");
     }
     kp.stage2 = 1;

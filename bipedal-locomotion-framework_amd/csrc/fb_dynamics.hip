@@ -83,6 +83,9 @@ __device__ __forceinline__ void wave_sync()
 // (profiles/r04_fbd_fold_ab.log, one c5 period of fbd_euler_kernel, two rounds on one box): 1 took
 // 4.747 / 4.740 ms against 4.701 / 4.705 ms for 0 (the block's y broadcasts lengthen every
 // factorization step's chain more than the separate loop costs); 2 spills 318 VGPRs.  So 0.
+#ifndef BLF_FBD_SCANX   // the subtree sums' gathers: 1 = one ds_bpermute per component (0: three, A/B)
+#define BLF_FBD_SCANX 1   // 4.657 / 4.640 against 4.671 / 4.656 ms per c5 period (profiles/r04_fbd_scanx_ab.log)
+#endif
 #ifndef BLF_FBD_FOLD
 #define BLF_FBD_FOLD 0
 #endif
@@ -555,9 +558,18 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             if constexpr (HW == 64) level(std::integral_constant<int, 5>{});
 #pragma unroll
             for (int q = 0; q < G; ++q) {
+#if BLF_FBD_SCANX
+                // the previous lane's prefix by a DPP wavefront rotation (a half's lane 0 does not
+                // use it) and the total by v_readlane: one ds_bpermute per component, not three
+                const double atl = __shfl(pre[q], T.last, HW);
+                const double bef = qp::dpp1<qp::kPrevWrap>(pre[q]);
+                const double tot = H.bcast_k(pre[q], n - 1);
+                (void)src;
+#else
                 const double atl = __shfl(pre[q], T.last, HW);
                 const double bef = __shfl(pre[q], src, HW);
                 const double tot = __shfl(pre[q], n - 1, HW);
+#endif
                 if (jl) S.comp()[kCompS * lane + g + q] = lane > 0 ? atl - bef : atl;
                 if (lane == 0) {
                     double b = S.link()[kSI + g + q] + tot;
@@ -900,10 +912,14 @@ struct Impedance {
 struct Select {
     const int32_t* mask;
     int want;
+    const int32_t* list;   // or: [0] = count, [1..count] = the systems (mask and want unused)
     __device__ __forceinline__ bool has(int64_t q) const { return !mask || ((mask[q] != 0) == (want != 0)); }
 };
 
-template <int NVMAX, int HW, bool PRI>
+// NFIX > 0: a model of exactly NFIX joints (the launcher checks): the joint count is a compile-time
+// constant, so every `< n` / `< NV` bound of the unrolled loops folds away instead of living in
+// scalar registers across the Euler loop (BLF_FBD_NFIX).
+template <int NVMAX, int HW, bool PRI, int NFIX = 0>
 // Two systems per wavefront (HW = 32) keep more state live per wave: capping it at 256 VGPRs for
 // two waves per SIMD spills (9.40 ms per c5 period), one wave per SIMD does not (8.29 ms, against
 // 9.29 ms with one system per wavefront at two waves per SIMD; tools/ab_c5.sh).
@@ -913,19 +929,28 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
                                                           int32_t nsteps, double dT, double dT_last,
                                                           Impedance imp, int64_t batch, Select sel)
 {
+    if constexpr (NFIX > 0) m.n = NFIX;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const Half<HW> H;
     const int n = m.n, NV = n + 6;
     const Smem S(smem + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
-    const int64_t q0 = (int64_t)blockIdx.x * (kWave / HW) + H.half;
-    // a system outside the batch or outside the selection is computed (as the other half's
-    // partner) and written nowhere; a wavefront with no selected system leaves at once
-    const bool active = q0 < batch && sel.has(q0);   // see fbd_dynamics_kernel
-    if (__ballot(active) == 0ull) return;
-    const int64_t q = q0 < batch ? q0 : batch - 1;
     const int lane = H.hl;
+    constexpr int per = kWave / HW;   // systems per wavefront
+    // the systems: the batch (q = blockIdx.x * per + half), or a list (sel.list: a grid of a few
+    // wavefronts loops over the listed systems, per at a time)
+    const bool lst = sel.list != nullptr;
+    const int64_t nitems = lst ? (int64_t)sel.list[0] : batch;
+    const int64_t g_end = lst ? (nitems + per - 1) / per : (int64_t)blockIdx.x + 1;
+    const Topo T = build_topo<HW>(m, S);
     double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n | dR 9
     double* dR = loc + 18 + 2 * n;
+    for (int64_t g = blockIdx.x; g < g_end; g += lst ? (int64_t)gridDim.x : g_end) {
+    const int64_t i0 = g * per + H.half;
+    // a system outside the batch, the list or the selection is computed (as the other half's
+    // partner) and written nowhere; a wavefront with no selected system skips the group
+    const bool active = lst ? i0 < nitems : (i0 < batch && sel.has(i0));   // see fbd_dynamics_kernel
+    if (__ballot(active) == 0ull) continue;
+    const int64_t q = lst ? (int64_t)sel.list[1 + (i0 < nitems ? i0 : nitems - 1)] : (i0 < batch ? i0 : batch - 1);
     for (int i = lane; i < 18 + 2 * n; i += HW) {
         double v;
         if (i < 6) v = st.base_vel[6 * q + i];
@@ -936,7 +961,6 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
         loc[i] = v;
     }
     wave_sync();
-    const Topo T = build_topo<HW>(m, S);
     bool ok = true;
     const double* tq = tau + (int64_t)n * q;
     for (int32_t step = 0; step < nsteps; ++step) {
@@ -963,15 +987,18 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
         for (int i = lane; i < NV; i += HW) loc[i] = loc[i] + S.rhs()[i] * h;
         wave_sync();
     }
-    if (!active) return;
-    const double nan = __builtin_nan("");
-    for (int i = lane; i < 18 + 2 * n; i += HW) {
-        const double v = ok ? loc[i] : nan;
-        if (i < 6) st.base_vel[6 * q + i] = v;
-        else if (i < 6 + n) st.joint_vel[(int64_t)n * q + (i - 6)] = v;
-        else if (i < 9 + n) st.base_pos[3 * q + (i - 6 - n)] = v;
-        else if (i < 18 + n) st.base_rot[9 * q + (i - 9 - n)] = v;
-        else st.joint_pos[(int64_t)n * q + (i - 18 - n)] = v;
+    if (active) {
+        const double nan = __builtin_nan("");
+        for (int i = lane; i < 18 + 2 * n; i += HW) {
+            const double v = ok ? loc[i] : nan;
+            if (i < 6) st.base_vel[6 * q + i] = v;
+            else if (i < 6 + n) st.joint_vel[(int64_t)n * q + (i - 6)] = v;
+            else if (i < 9 + n) st.base_pos[3 * q + (i - 6 - n)] = v;
+            else if (i < 18 + n) st.base_rot[9 * q + (i - 9 - n)] = v;
+            else st.joint_pos[(int64_t)n * q + (i - 18 - n)] = v;
+        }
+    }
+    wave_sync();   // the next group's loads overwrite the state
     }
 }
 
@@ -1046,6 +1073,17 @@ __global__ __launch_bounds__(256) void posture_reference_kernel(int n, const dou
                                                                 int64_t vstride, int64_t total,
                                                                 double* __restrict__ qref, Select sel)
 {
+    if (sel.list) {   // the listed systems' rows, a few workgroups looping over them
+        const int64_t tl = (int64_t)sel.list[0] * n;
+        for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tl; t += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t q = sel.list[1 + t / n];
+            const int j = (int)(t % n);
+            const double ex = vrp[q * vstride] - com[6 * q];
+            const double ey = vrp[q * vstride + 1] - com[6 * q + 1];
+            qref[q * n + j] = (qnom[j] + lean[2 * j] * ex) + lean[2 * j + 1] * ey;
+        }
+        return;
+    }
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     const int64_t q = e / n;
@@ -1114,10 +1152,15 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s,
-                            const blf_joint_impedance* impedance, const int32_t* mask, int want)
+                            const blf_joint_impedance* impedance, const int32_t* mask, int want,
+                            const int32_t* list)
 {
     if (batch == 0) return BLF_OK;
-    const Select sel{mask, want};
+    const Select sel{mask, want, list};
+    // a list: at most kListGrid wavefronts loop over it (the grid the batch would need is dispatched
+    // only as the other stream's dynamics frees the chip, wavefront by wavefront)
+    const int64_t wv2 = list ? std::min<int64_t>(ceil_div(batch, 2), kListGrid) : ceil_div(batch, 2);
+    const int64_t wv1 = list ? std::min<int64_t>(batch, kListGrid) : batch;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     Impedance imp{nullptr, nullptr, nullptr};
@@ -1126,18 +1169,26 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
 #define BLF_FBD_SMALL_HW 32   // diagnostic builds: 64 = one small model per wavefront (A/B)
 #endif
     const bool pri = md->joint_type != nullptr;
-    if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
+#ifndef BLF_FBD_NFIX
+#define BLF_FBD_NFIX 0   // A/B builds: a joint count with its own instantiation (0: none)
+#endif
+    if (BLF_FBD_NFIX > 0 && md->ndof == BLF_FBD_NFIX && BLF_FBD_NFIX + 6 <= 32 && BLF_FBD_SMALL_HW == 32)
+        hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>
+                                : fbd_euler_kernel<32, 32, false, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>),
+                           dim3((unsigned)wv2), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
+                           reg, nsteps, dT, dT_last, imp, batch, sel);
+    else if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true> : fbd_euler_kernel<32, 32, false>),
-                           dim3((unsigned)ceil_div(batch, 2)), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
+                           dim3((unsigned)wv2), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
                            reg, nsteps, dT, dT_last, imp, batch, sel);
     else if (md->ndof + 6 <= 32)   // one system per wavefront, NV <= 32 rows
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, kWave, true> : fbd_euler_kernel<32, kWave, false>),
-                           dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
+                           dim3((unsigned)wv1), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
                            dT_last, imp, batch, sel);
     else
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, true>
                                 : fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, false>),
-                           dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
+                           dim3((unsigned)wv1), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
                            dT_last, imp, batch, sel);
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
 }
@@ -1155,12 +1206,13 @@ blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const d
 
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
                                     int64_t vstride, int64_t batch, double* qref, hipStream_t s,
-                                    const int32_t* mask, int want)
+                                    const int32_t* mask, int want, const int32_t* list)
 {
     const int64_t total = batch * law->ndof;
     if (total == 0) return BLF_OK;
-    hipLaunchKernelGGL(posture_reference_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       law->ndof, law->q_nominal, law->lean, com, vrp, vstride, total, qref, Select{mask, want});
+    const int64_t grid = list ? std::min<int64_t>((total + 255) / 256, 4) : (total + 255) / 256;
+    hipLaunchKernelGGL(posture_reference_kernel, dim3((unsigned)grid), dim3(256), 0, s,
+                       law->ndof, law->q_nominal, law->lean, com, vrp, vstride, total, qref, Select{mask, want, list});
     return check_hip(hipGetLastError(), "posture_reference_kernel launch");
 }
 

@@ -343,9 +343,11 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
 /* blf_dcm_mpc_solve_phased in two calls, so that a caller can go on with the problems solved by
  * the active-set kernel while the interior point kernel finishes the rest on another stream.
  * _begin: the active-set kernel (every argument as for blf_dcm_mpc_solve_phased); the problems it
- * hands over get status -1 and pending[q] = 1 (others 0), their windows expanded into `window`.
- * _finish: the interior point kernel on those, with the same params, xi_init, warm, window,
- * solution and lambda_out as the _begin call.  _begin then _finish on one stream give the same bits
+ * hands over get status -1 and pending[q] = 1 (others 0), their windows expanded into `window`;
+ * pending_list (optional, [B + 1]): [0] = their count, [1..count] = their indices (in no
+ * particular order).  _finish: the interior point kernel on those, with the same params, xi_init,
+ * warm, window, solution and lambda_out as the _begin call; given the pending_list, a small grid
+ * loops over the listed problems instead of one workgroup per problem of the batch.  _begin then _finish on one stream give the same bits
  * as blf_dcm_mpc_solve_phased.  With max_facets > 8 (no active-set kernel) _begin solves every
  * problem and marks none, and _finish does nothing. */
 blf_status blf_dcm_mpc_solve_phased_begin(blf_handle* handle, const blf_dcm_mpc_params* params,
@@ -354,12 +356,12 @@ blf_status blf_dcm_mpc_solve_phased_begin(blf_handle* handle, const blf_dcm_mpc_
                                           int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                           int64_t batch, const blf_dcm_mpc_window* window,
                                           const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                          int32_t* pending, void* stream);
+                                          int32_t* pending, int32_t* pending_list, void* stream);
 blf_status blf_dcm_mpc_solve_phased_finish(blf_handle* handle, const blf_dcm_mpc_params* params,
                                            const double* xi_init, const blf_dcm_mpc_warm_start* warm,
                                            int64_t batch, const blf_dcm_mpc_window* window,
                                            const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                           void* stream);
+                                           const int32_t* pending_list, void* stream);
 
 /* ---- 6. Contact model (ContinuousContactModel), batched ------------------------------------
  * Rectangular L x W patch, spring k, damper b (ContinuousContactModel.h:22-57).
@@ -501,12 +503,13 @@ typedef struct blf_posture_law {
 blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* law,
                                      const double* com, const double* vrp, int64_t vrp_stride,
                                      int64_t batch, double* q_ref, void* stream);
-/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1); the other rows of q_ref
- * are not written. */
+/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1), or, when list is not NULL,
+ * for the systems list[1..list[0]] (a device array, e.g. blf_dcm_mpc_solve_phased_begin's
+ * pending_list; mask and want unused); the other rows of q_ref are not written. */
 blf_status blf_dcm_posture_reference_masked(blf_handle* handle, const blf_posture_law* law,
                                             const double* com, const double* vrp, int64_t vrp_stride,
                                             int64_t batch, double* q_ref, const int32_t* mask,
-                                            int32_t want, void* stream);
+                                            int32_t want, const int32_t* list, void* stream);
 
 /* blf_fbd_euler_integrate_impedance: ForwardEuler<FloatingBaseDynamicalSystem>::integrate(t0, T)
  * (the schedule of blf_fbd_euler_integrate) with the control input set before EVERY step from a
@@ -527,16 +530,18 @@ blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_mo
                                              const double* mass_reg, int64_t batch,
                                              double initial_time, double final_time, double dT,
                                              void* stream);
-/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1); the others' state is
- * neither read for their results nor written.  A closed loop integrates the systems whose plan is
- * ready while the rest wait for theirs (blf_dcm_mpc_solve_phased_begin / _finish). */
+/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1), or, when list is not NULL,
+ * for the systems list[1..list[0]] (a few wavefronts loop over them; mask and want unused); the
+ * others' state is not written.  A closed loop integrates the systems whose plan is ready while
+ * the rest wait for theirs (blf_dcm_mpc_solve_phased_begin / _finish). */
 blf_status blf_fbd_euler_integrate_impedance_masked(blf_handle* handle, const blf_fb_model* model,
                                                     const blf_fb_state* state,
                                                     const blf_joint_impedance* impedance,
                                                     const blf_fb_contacts* contacts,
                                                     const double* mass_reg, int64_t batch,
                                                     double initial_time, double final_time, double dT,
-                                                    const int32_t* mask, int32_t want, void* stream);
+                                                    const int32_t* mask, int32_t want, const int32_t* list,
+                                                    void* stream);
 
 /* Algorithmic flop count of one IPM iteration of one problem (what the fp64 roofline field
  * of bench.py is computed from); `active_facets` = sum_k nfacets[k]. */
