@@ -62,6 +62,8 @@ def period_final_time(dt, dT):
 # test's foot size; stiffness and damping for a 50 kg robot on two 0.12 x 0.09 m soles (about
 # 1 cm of sink) that explicit Euler at dT = 1 ms integrates stably
 CONTACT_PARAMS = (0.12, 0.09, 2.0e6, 2.0e4)
+# CUs the overlap's side stream keeps for itself (of 256 on an MI355X)
+OVERLAP_SIDE_CUS = 8
 
 
 class ClosedLoop:
@@ -70,18 +72,29 @@ class ClosedLoop:
     problem dict with a horizon of at least horizon + the number of periods to run."""
 
     def __init__(self, h, model, plan, states, horizon=100, dT=0.001, law=None,
-                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None, overlap=False):
+                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None, overlap=False,
+                 side_cus=OVERLAP_SIDE_CUS):
         import torch
         self.h, self.N, self.dT, self.stream = h, horizon, dT, stream
         # overlap: the robots whose window the active-set kernel solved go on to the posture and
         # the dynamics at once; the few it hands to the interior point kernel (uncapturable DCM
         # states, tens of iterations on an otherwise idle chip) finish on a side stream, where
         # their own posture and dynamics follow (blf_dcm_mpc_solve_phased_begin / _finish and the
-        # masked kernels).  Every robot's computation is the same, so the states are the same bits.
+        # list-driven kernels).  Every robot's computation is the same, so the states are the same
+        # bits.  The side stream runs on `side_cus` CUs of its own and the main stream on the
+        # rest (blf_stream_create_cu_range): sharing every CU, the side's few waves waited behind
+        # the dynamics kernel that fills the chip (profiles/r04_c5_overlap_trace.log).
         self.overlap = bool(overlap)
-        # the side stream at high priority: its few waves take the SIMDs the dynamics kernel frees
-        # before that kernel's queued waves (otherwise they would wait for the whole launch)
-        self.side = torch.cuda.Stream(device=h.device, priority=-1) if self.overlap else None
+        self.side = None
+        if self.overlap:
+            import os
+            mode = os.environ.get("BLF_OVERLAP_CU_MODE", "side")   # A/B: side | split | none
+            if side_cus > 0 and mode in ("side", "split"):
+                if mode == "split" and stream is None:
+                    self.stream = h.cu_stream(0, side_cus, exclude=True)
+                self.side = h.cu_stream(0, side_cus)
+            else:
+                self.side = torch.cuda.Stream(device=h.device)
         dev = torch.device("cuda", h.device)
         t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
         self.dt = float(plan["dt"])

@@ -20,7 +20,7 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 
 # every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_set_qp_launch_mode",
-            "blf_set_qp_split_batch",
+            "blf_set_qp_split_batch", "blf_stream_create_cu_range", "blf_stream_destroy",
             "blf_step_schedule",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_hull3d_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
@@ -198,6 +198,8 @@ def lib():
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         L.blf_set_qp_launch_mode.argtypes = [_i32, _i32]
         L.blf_set_qp_split_batch.argtypes = [_i64, _vp]
+        L.blf_stream_create_cu_range.argtypes = [_vp, _i32, _i32, _i32, _i32, ctypes.POINTER(_vp)]
+        L.blf_stream_destroy.argtypes = [_vp]
         for name in EXPORTED:
             if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
                             "blf_dcm_mpc_default_params", "blf_dcm_mpc_flops_per_iter"):
@@ -321,6 +323,8 @@ class Handle:
         self.device = device
 
     def close(self):
+        for raw in self.__dict__.pop("_cu_streams", []):
+            lib().blf_stream_destroy(raw)
         if self._h:
             lib().blf_destroy(self._h)
             self._h = _vp()
@@ -334,6 +338,17 @@ class Handle:
     @property
     def ptr(self):
         return self._h
+
+    def cu_stream(self, first_cu, num_cus, exclude=False):
+        """blf_stream_create_cu_range as a torch stream (torch.cuda.ExternalStream): kernels on CUs
+        [first_cu, first_cu + num_cus) only, or (exclude) on the others only.  The HIP stream
+        lives as long as the handle."""
+        torch = _torch()
+        raw = _vp()
+        _check(lib().blf_stream_create_cu_range(self._h, int(first_cu), int(num_cus), 1 if exclude else 0, 0,
+                                                ctypes.byref(raw)))
+        self.__dict__.setdefault("_cu_streams", []).append(raw)
+        return torch.cuda.ExternalStream(raw.value, device=torch.device("cuda", self.device))
 
     # --- ForwardEuler<LinearTimeInvariantSystem>::integrate, batched, in place on x ---
     def lti_euler_integrate(self, A, Bm, u, x, t0, t1, dT, shared=False, stream=None):

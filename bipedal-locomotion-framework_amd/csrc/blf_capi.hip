@@ -110,6 +110,39 @@ blf_status blf_destroy(blf_handle* handle)
     return BLF_OK;
 }
 
+blf_status blf_stream_create_cu_range(blf_handle* handle, int32_t first_cu, int32_t num_cus, int32_t exclude,
+                                      int32_t priority, void** stream)
+{
+    BLF_REQUIRE(handle != nullptr && stream != nullptr, "blf_stream_create_cu_range: null argument");
+    const int ncu = handle->h.num_cus;
+    BLF_REQUIRE(ncu > 0, "blf_stream_create_cu_range: the device's CU count is unknown");
+    BLF_REQUIRE(first_cu >= 0 && num_cus >= 1 && first_cu + num_cus <= ncu && (exclude == 0 || exclude == 1) &&
+                    !(exclude && num_cus == ncu),
+                "blf_stream_create_cu_range: CUs [%d, %d) of %d (exclude %d)", first_cu, first_cu + num_cus, ncu,
+                exclude);
+    BLF_REQUIRE(priority == 0 || priority == -1, "blf_stream_create_cu_range: priority 0 or -1");
+    const int words = (ncu + 31) / 32;
+    uint32_t mask[64] = {};
+    BLF_REQUIRE(words <= 64, "blf_stream_create_cu_range: %d CUs", ncu);
+    for (int c = 0; c < ncu; ++c) {
+        const bool in = c >= first_cu && c < first_cu + num_cus;
+        if (in != (exclude != 0)) mask[c / 32] |= 1u << (c % 32);
+    }
+    blf_status st = check_hip(hipSetDevice(handle->h.device), "hipSetDevice");
+    if (st != BLF_OK) return st;
+    hipStream_t s = nullptr;
+    st = check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask), "hipExtStreamCreateWithCUMask");
+    if (st != BLF_OK) return st;
+    (void)priority;   // (a CU-masked stream takes the default priority; the masks keep the streams apart)
+    *stream = s;
+    return BLF_OK;
+}
+
+blf_status blf_stream_destroy(void* stream)
+{
+    return check_hip(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
+}
+
 const char* blf_last_error(void) { return g_err; }
 
 blf_status blf_step_schedule(double initial_time, double final_time, double dT, int32_t* iterations,

@@ -79,6 +79,14 @@ typedef struct blf_handle blf_handle;
 /* Create a handle bound to HIP device `device`.  Fails with BLF_ERR_HIP if no device. */
 blf_status blf_create(blf_handle** handle, int32_t device);
 blf_status blf_destroy(blf_handle* handle);
+/* A HIP stream whose kernels run only on CUs [first_cu, first_cu + num_cus) of the handle's
+ * device (exclude = 0), or only on the others (exclude = 1) (hipExtStreamCreateWithCUMask).  Two
+ * such streams with complementary ranges keep a small side computation (the closed loop's
+ * interior point problems) from waiting behind a kernel that fills the chip.  priority: 0 (reserved:
+ * -1 is accepted and treated as 0).  Release with blf_stream_destroy. */
+blf_status blf_stream_create_cu_range(blf_handle* handle, int32_t first_cu, int32_t num_cus,
+                                      int32_t exclude, int32_t priority, void** stream);
+blf_status blf_stream_destroy(void* stream);
 /* Human-readable description of the last error on this thread (never NULL). */
 const char* blf_last_error(void);
 /* Version string of the library (build id). */
