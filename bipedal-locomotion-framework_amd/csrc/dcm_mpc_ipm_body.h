@@ -623,10 +623,15 @@ __device__ __forceinline__ bool sat_start(KN& K, const KParams& P, const Lds& L,
                 const double t1 = fma(abj, FD2(readlane_f64(Mm.m01, j), d0, readlane_f64(Mm.m11, j), d1),
                                       readlane_f64(rs1, j));
                 const double c00 = readlane_f64(B00, j), c01 = readlane_f64(B01, j), c11 = readlane_f64(B11, j);
+                // (the facet loops below are unrolled over the slots and predicated on i < m, so
+                // every row's LDS read issues at once; the same comparisons as a loop to m)
                 bool inside = true;
-                for (int i = 0; i < m; ++i) {
-                    const double2 a = L.A2[i * N + kk];
-                    if (!(FD2(a.x, t0, a.y, t1) - L.BI[i * N + kk].x <= 0.0)) inside = false;
+#pragma unroll
+                for (int i = 0; i < KN::kMF; ++i) {
+                    const int ii = i < m ? i : 0;
+                    const double2 a = L.A2[ii * N + kk];
+                    const double bi = L.BI[ii * N + kk].x;
+                    if (i < m && !(FD2(a.x, t0, a.y, t1) - bi <= 0.0)) inside = false;
                 }
                 double r0 = t0, r1 = t1;
                 int c = 0, i1 = 0, i2 = 0;
@@ -671,11 +676,12 @@ __device__ __forceinline__ bool sat_start(KN& K, const KParams& P, const Lds& L,
                             const double e0 = v0 - t0, e1 = v1 - t1;
                             dist = fma(e0, fma(c00, e0, 2.0 * (c01 * e1)), (c11 * e1) * e1);
                         }
-                        if (valid) {
-                            for (int l = 0; l < m; ++l) {
-                                const double2 f = L.A2[l * N + kk];
-                                if (!(FD2(f.x, v0, f.y, v1) - L.BI[l * N + kk].x <= P.tol_p)) valid = false;
-                            }
+#pragma unroll
+                        for (int l = 0; l < KN::kMF; ++l) {
+                            const int ll = l < m ? l : 0;
+                            const double2 f = L.A2[ll * N + kk];
+                            const double bl = L.BI[ll * N + kk].x;
+                            if (l < m && !(FD2(f.x, v0, f.y, v1) - bl <= P.tol_p)) valid = false;
                         }
                         if (!(dist == dist)) valid = false;
                         const double key = valid ? dist : __builtin_inf();

@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/sq
 mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 120 python3 -c "import json, sys; sys.path.insert(0, 'bipedal-locomotion-framework_amd'); from blf import native; print(json.dumps(native.build_provenance()))" > $OUT/build.json || exit $?
 GROUPS_=(
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
   "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"

@@ -26,5 +26,9 @@ if len(sys.argv) > 3:
     if wc:
         out["frac_of_wave_cycles"] = {c: med[c] / wc for c in med
                                       if c.startswith(("SQ_WAIT", "SQ_ACTIVE_INST", "SQ_LDS_BANK"))}
+    import os
+    bj = "gpurun_out/sq/build.json"   # the library the passes ran (tools/gpu_sq.sh writes it)
+    if os.path.exists(bj):
+        out["build"] = json.load(open(bj))
     with open(sys.argv[3], "w") as f:
         json.dump(out, f, indent=1)
