@@ -550,7 +550,10 @@ constexpr int kEvalBlock = 256;
 #ifndef BLF_Q_STAGE
 #define BLF_Q_STAGE 512
 #endif
-constexpr int kEvalStage = BLF_Q_STAGE;   // doubles of staged spline data per workgroup (4 KB)
+constexpr int kEvalStage = BLF_Q_STAGE;
+#ifndef BLF_Q_DIRECT
+#define BLF_Q_DIRECT 0
+#endif   // doubles of staged spline data per workgroup (4 KB)
 
 template <bool VEC>
 __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* __restrict__ kt,
@@ -626,11 +629,19 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
             const double p = c0 + tau * (c1 + tau * (c2 + tau * (c3 + tau * (c4 + tau * c5))));
             const double v = c1 + tau * (2.0 * c2 + tau * (3.0 * c3 + tau * (4.0 * c4 + tau * (5.0 * c5))));
             const double a = 2.0 * c2 + tau * (6.0 * c3 + tau * (12.0 * c4 + tau * (20.0 * c5)));
-            o[d] = p;
-            o[D + d] = v;
-            o[2 * D + d] = a;
+            if (BLF_Q_DIRECT) {   // A/B: the lane's own row straight to HBM (plain stores)
+                double* og = pva + gid * W;
+                og[d] = p;
+                og[D + d] = v;
+                og[2 * D + d] = a;
+            } else {
+                o[d] = p;
+                o[D + d] = v;
+                o[2 * D + d] = a;
+            }
         }
     }
+    if (BLF_Q_DIRECT) return;
     __syncthreads();
     slab_store<kEvalBlock, 6>(pva + g0 * W, W, s_out, SW, rows, W);   // 9 doubles x 256: one batch
 }
