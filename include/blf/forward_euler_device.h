@@ -23,7 +23,8 @@
  *          time of the step before it, :63-64), x: [n], u: [m], dx: [n] output.
  *
  * Layout: x [batch][n] (updated in place), u [batch][m], params [batch] (or one shared Params
- * when params_shared != 0).  One lane per system; x_r <- x_r + dx_r * h after every step (no FMA
+ * when params_shared != 0).  One lane per system (states of up to 16 doubles staged through LDS,
+ * so the batch's state is read and written coalesced); x_r <- x_r + dx_r * h after every step (no FMA
  * contraction: build the user TU with -ffp-contract=off for results that match a CPU restatement
  * bit for bit).  Returns the C ABI's status codes (blf_c.h): the schedule's errors (with
  * blf_last_error() set), BLF_ERR_INVALID_ARGUMENT for null buffers or a negative batch, and
@@ -43,25 +44,51 @@ __global__ __launch_bounds__(256) void forward_euler_user_kernel(
 {
     constexpr int n = System::kStateSize;
     constexpr int m = System::kInputSize > 0 ? System::kInputSize : 1;
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= batch) return;
-    const typename System::Params p = params[params_shared ? 0 : q];
+    // States of up to 16 doubles move through LDS: the workgroup's contiguous [256][n] slab is read
+    // and written with consecutive lanes on consecutive doubles (coalesced), and each lane takes its
+    // own row from LDS (odd row stride: no bank conflicts).  Larger states are read lane by lane.
+    constexpr bool kStage = n <= 16;
+    constexpr int SW = n | 1;
+    __shared__ double sx[kStage ? 256 * SW : 1];
+    const int64_t q0 = (int64_t)blockIdx.x * blockDim.x;
+    const int64_t q = q0 + threadIdx.x;
+    const int rows = (int)(batch - q0 < (int64_t)blockDim.x ? batch - q0 : (int64_t)blockDim.x);
     double xr[n], ur[m], dx[n];
-#pragma unroll
-    for (int r = 0; r < n; ++r) xr[r] = x[q * n + r];
-#pragma unroll
-    for (int c = 0; c < m; ++c) ur[c] = System::kInputSize > 0 ? u[q * System::kInputSize + c] : 0.0;
-    // steps 0 .. iterations-2 at currentTime = t0 + dT i, then the last one at the stale time
-    for (int32_t i = 0; i < iterations; ++i) {
-        const bool last = i == iterations - 1;
-        const double t = last ? t_last : t0 + dT * (double)i;
-        const double h = last ? dT_last : dT;
-        System::dynamics(t, xr, ur, p, dx);
-#pragma unroll
-        for (int r = 0; r < n; ++r) xr[r] = xr[r] + dx[r] * h;
+    if (kStage) {
+        for (int e = threadIdx.x; e < rows * n; e += blockDim.x) {
+            const int r = e / n;
+            sx[r * SW + (e - r * n)] = x[q0 * n + e];
+        }
+        __syncthreads();
     }
+    if (q < batch) {
+        const typename System::Params p = params[params_shared ? 0 : q];
 #pragma unroll
-    for (int r = 0; r < n; ++r) x[q * n + r] = xr[r];
+        for (int r = 0; r < n; ++r) xr[r] = kStage ? sx[threadIdx.x * SW + r] : x[q * n + r];
+#pragma unroll
+        for (int c = 0; c < m; ++c) ur[c] = System::kInputSize > 0 ? u[q * System::kInputSize + c] : 0.0;
+        // steps 0 .. iterations-2 at currentTime = t0 + dT i, then the last one at the stale time
+        for (int32_t i = 0; i < iterations; ++i) {
+            const bool last = i == iterations - 1;
+            const double t = last ? t_last : t0 + dT * (double)i;
+            const double h = last ? dT_last : dT;
+            System::dynamics(t, xr, ur, p, dx);
+#pragma unroll
+            for (int r = 0; r < n; ++r) xr[r] = xr[r] + dx[r] * h;
+        }
+#pragma unroll
+        for (int r = 0; r < n; ++r) {
+            if (kStage) sx[threadIdx.x * SW + r] = xr[r];
+            else x[q * n + r] = xr[r];
+        }
+    }
+    if (kStage) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < rows * n; e += blockDim.x) {
+            const int r = e / n;
+            x[q0 * n + e] = sx[r * SW + (e - r * n)];
+        }
+    }
 }
 
 /* ForwardEuler<System>::integrate(initial_time, final_time) with sampling time dT, for `batch`
