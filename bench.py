@@ -167,9 +167,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dump-state", default=None,
                     help="c5: write each rank's final robot state to DIR/c5_state_rank<r>.npz")
-    ap.add_argument("--c5-groups", type=int, default=1,
+    ap.add_argument("--c5-groups", type=int, default=2,
                     help="c5: robots in this many groups, each closed loop on its own stream "
-                         "(measured: 1 group 6.96 ms, 2 groups 6.98 ms, 4 groups 7.4 ms per period)")
+                         "(round 4, profiles/r04_v2_c5_g*.log: 1 group 5.88 / 5.88 ms, 2 groups "
+                         "5.74 / 5.67 ms per period; 3 groups 6.05 / 6.13 ms, profiles/r04f_*)")
     ap.add_argument("--c5-overlap", type=int, default=0,
                     help="c5: 1 = the robots whose plan the active-set kernel solved integrate while "
                          "the interior point kernel finishes the rest on a side stream (ClosedLoop "
@@ -488,10 +489,11 @@ def closed_loop(args):
         torch.cuda.set_device(local)
         sync = torch.cuda.synchronize
         h = native.Handle(local)
-        # the robots in G groups, each closed loop on its own stream (--c5-groups, default 1): at
+        # the robots in G groups, each closed loop on its own stream (--c5-groups, default 2): at
         # horizon 100 every robot's period is the same computation as in one group
-        # (DL.split_groups states when); more groups did not pay (the
-        # dynamics kernel holds every SIMD, so the plan kernels' tails find no room beside it)
+        # (DL.split_groups states when); two groups let one group's plan tail (the interior
+        # point kernel's few uncapturable windows) run beside the other group's kernels
+        # 
         loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N, overlap=bool(args.c5_overlap))
         for lp in loops:
             lp.expand_path = args.expand_path

@@ -17,8 +17,8 @@
 // which is exactly sum_l m Jv^T Jv + Jw^T I Jw, h and J_c^T w_c of the Jacobian form
 // (oracle/fb_dynamics.py evaluates that form; the two agree to rounding).
 // One 64-lane workgroup (one wavefront) per system, everything in LDS:
-//   1. per-joint rotations, lane per joint;  2. forward kinematics level by level over the tree
-//   depth (lane per joint of the level);  3. per-link spatial inertia / force, lane per link;
+//   1. per-joint rotations, lane per joint;  2. forward kinematics by pointer jumping along the
+//   ancestor chains (every joint lane at once, log2 of the depth rounds);  3. per-link spatial inertia / force, lane per link;
 //   4. contact wrenches, lane per contact;  5. subtree sums, lane per (subtree, parameter), the
 //   ancestor bitmask of each link selecting the members;  6. column axes, their composite products
 //   and the right-hand side, lane per column;  7. M, lane per lower-triangle entry;  8. Cholesky,
@@ -86,6 +86,9 @@ __device__ __forceinline__ void wave_sync()
 #ifndef BLF_FBD_SCANX   // the subtree sums' gathers: 1 = one ds_bpermute per component (0: three, A/B)
 #define BLF_FBD_SCANX 1   // 4.657 / 4.640 against 4.671 / 4.656 ms per c5 period (profiles/r04_fbd_scanx_ab.log)
 #endif
+#ifndef BLF_FBD_LDSMODEL   // fbd_euler_kernel reads the model's constants from an LDS copy (A/B)
+#define BLF_FBD_LDSMODEL 0   // 1: 5.92 / 5.93 against 4.24 / 4.24 ms per c5 period (profiles/r04_fbd_kinjump_ab.log)
+#endif
 #ifndef BLF_FBD_FOLD
 #define BLF_FBD_FOLD 0
 #endif
@@ -150,6 +153,15 @@ struct Smem {
     }
 };
 
+// doubles of fbd_euler_kernel's LDS model block (BLF_FBD_LDSMODEL)
+template <int NVMAX>
+__host__ __device__ constexpr int fbd_model_block()
+{
+    // rounded up to an even count: the halves' state blocks after it stay 16-B aligned
+    return (3 * (NVMAX - 6) + 9 * (NVMAX - 6) + 3 * (NVMAX - 5) + 9 * (NVMAX - 5) + (NVMAX - 5) + 2 * (NVMAX - 6) +
+            13 * BLF_FBD_MAX_CONTACTS + 1) & ~1;
+}
+
 struct Model {
     int n, F;
     const int32_t* parent;
@@ -157,6 +169,10 @@ struct Model {
     const int32_t* flink;
     double g0, g1, g2, rho;
     const int32_t* jtype;   // [n] or nullptr: BLF_JOINT_PRISMATIC marks a sliding joint
+    // fbd_euler_kernel's LDS copy (BLF_FBD_LDSMODEL): each contact's frame pose [C][12] and link
+    // [C] (read through these when fbd_eval's LM is set)
+    const double* cpose;
+    const double* clink;
 };
 
 struct Contacts {
@@ -306,9 +322,9 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
 // PRI: the model may hold prismatic joints (blf_fb_model.joint_type != NULL); the launchers
 // instantiate the kernels both ways, so all-revolute models (config 5) pay nothing for it.
 template <int HW, bool PRI>
-__device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, const double* bv,
-                                               const double* jvel, const double* bp, const double* bR,
-                                               const double* jp, const Topo& T)
+__device__ __forceinline__ void fbd_kinematics_levels(const Model& m, const Smem& S, const double* bv,
+                                                      const double* jvel, const double* bp, const double* bR,
+                                                      const double* jp, const Topo& T)
 {
     const int n = m.n;
     const int lane = Half<HW>().hl;
@@ -408,12 +424,257 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
     }
 }
 
+// motion cross product (w, v) x (w2, v2) = (w x w2, w x v2 + v x w2), accumulated into o
+__device__ __forceinline__ void crm_add(const double* s, const double* t, double* o)
+{
+    double a[3], b[3], c[3];
+    cross3(s, t, a);
+    cross3(s, t + 3, b);
+    cross3(s + 3, t, c);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        o[i] = o[i] + a[i];
+        o[3 + i] = o[3 + i] + (b[i] + c[i]);
+    }
+}
+
+// Steps 1-2 by pointer jumping along the ancestor chains (BLF_FBD_KINJUMP): every joint lane runs
+// at once, and a chain of depth D takes ceil(log2(D + 1)) rounds instead of D + 1 tree levels.
+//  * Poses: lane j holds the transform (R, p) from link ptr (initially its parent; the base's
+//    world pose is folded in at once where the parent is the base, ptr = 0 then means "anchored in
+//    the world") to its link j + 1.  A round composes the record of link ptr -- the segment from
+//    that link's own ptr -- in front: (R, p) <- (R_X R, p_X + R_X p), ptr <- ptr_X.
+//  * Velocities and nu_dot = 0 accelerations as spatial vectors about the world origin: with the
+//    joint motion U_k = qdot_k S_k (S_k = (z_k, o_k x z_k), prismatic (0, z_k)),
+//      V_c = V_B + sum_{k in chain(c)} U_k,   A_c = A_B + V_B x s + sum_{i before k} U_i x U_k,
+//    so the chain element (s, x) = (sum U, sum of the ordered cross products) composes as
+//    (s_X + s_Y, x_X + x_Y + s_X x s_Y) -- the same jumping rounds.  The link records' mixed
+//    quantities follow: w = V_w, v = V_v + w x p, al = A_w, a = A_v + al x p + w x v (V_B =
+//    (w_B, v_B + p_B x w_B), A_B = (0, -(w_B x v_B)): the base's nu_dot = 0).
+// A lane reads its partner's record before it writes its own in the same round: the wavefront's
+// LDS operations complete in program order, so every read sees the previous round's values.
+// Rounding differs from the level recursion (parity is the 1e-9 bar of the fb tests).
+template <int HW, bool PRI>
+__device__ __forceinline__ void fbd_kinematics_jump(const Model& m, const Smem& S, const double* bv,
+                                                    const double* jvel, const double* bp, const double* bR,
+                                                    const double* jp, const Topo& T)
+{
+    const Half<HW> H;
+    const int n = m.n;
+    const int lane = H.hl;
+    const bool jl = lane < n;
+    const int maxdepth = T.maxdepth;
+    const double sd = jl ? jvel[lane] : 0.0;
+    double Rb[9], pb[3], wb[3], vb[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rb[i] = bR[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        pb[i] = bp[i];
+        vb[i] = bv[i];
+        wb[i] = bv[3 + i];
+    }
+    if (lane == 0) {
+        double* b = S.link();
+        for (int i = 0; i < 9; ++i) b[kR + i] = Rb[i];
+        for (int i = 0; i < 3; ++i) {
+            b[kP + i] = pb[i]; b[kV + i] = vb[i]; b[kW + i] = wb[i];
+            b[kAl + i] = 0.0; b[kA + i] = 0.0;
+        }
+    }
+    // 1. the joint's own transform: E_j Rot(a_j, s_j) (Rodrigues) and the origin o_j (+ E_j a_j q)
+    double R[9], p[3], ax[3];
+    const bool pri = PRI && jl && m.jtype[lane] == BLF_JOINT_PRISMATIC;
+    {
+        const int j = jl ? lane : 0;
+        const double* a = m.jaxis + 3 * j;
+        const double* E = m.jrot + 9 * j;
+        ax[0] = a[0]; ax[1] = a[1]; ax[2] = a[2];
+        double sn = 0.0, cs = 1.0;
+        if (jl && !pri) sincos(jp[j], &sn, &cs);
+        const double c1 = 1.0 - cs;
+        const double K[9] = {0.0, -a[2], a[1], a[2], 0.0, -a[0], -a[1], a[0], 0.0};
+        double Rr[9];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const double K2 = (K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c]) + K[3 * r + 2] * K[6 + c];
+                Rr[3 * r + c] = ((r == c ? 1.0 : 0.0) + sn * K[3 * r + c]) + c1 * K2;
+            }
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                R[3 * r + c] = (E[3 * r] * Rr[c] + E[3 * r + 1] * Rr[3 + c]) + E[3 * r + 2] * Rr[6 + c];
+        p[0] = T.o0; p[1] = T.o1; p[2] = T.o2;
+        if (pri) {
+            const double qj = jp[j];
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+                p[r] = p[r] + ((E[3 * r] * a[0] + E[3 * r + 1] * a[1]) + E[3 * r + 2] * a[2]) * qj;
+        }
+    }
+    // the transform (RX, pX) in front of (R, p)
+    auto compose = [&](const double* RX, const double* pX) {
+        double Rn[9], pn[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                Rn[3 * r + c] = (RX[3 * r] * R[c] + RX[3 * r + 1] * R[3 + c]) + RX[3 * r + 2] * R[6 + c];
+            pn[r] = pX[r] + ((RX[3 * r] * p[0] + RX[3 * r + 1] * p[1]) + RX[3 * r + 2] * p[2]);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) p[i] = pn[i];
+    };
+    int ptr = jl ? T.P : 0;
+    if (jl && ptr == 0) compose(Rb, pb);
+    double* own = S.link() + kLinkRec * (lane + 1);
+    if (jl) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) own[kR + i] = R[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) own[kP + i] = p[i];
+    }
+    wave_sync();
+    // 2a. poses: ceil(log2(maxdepth + 1)) rounds
+    for (int span = 1; span <= maxdepth; span <<= 1) {
+        const bool act = jl && ptr > 0;
+        const int pn = H.shfl(ptr, act ? ptr - 1 : 0);
+        if (act) {
+            const double* x = S.link() + kLinkRec * ptr;
+            double RX[9], pX[3];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) RX[i] = x[kR + i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) pX[i] = x[kP + i];
+            compose(RX, pX);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) own[kR + i] = R[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) own[kP + i] = p[i];
+            ptr = pn;
+        }
+        wave_sync();
+    }
+    // 2b. the joint's world axis z = R_child a (Rot(a, s) a = a) and origin o = p_child; its motion
+    double z[3], s[6], x[6];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) z[r] = (R[3 * r] * ax[0] + R[3 * r + 1] * ax[1]) + R[3 * r + 2] * ax[2];
+    {
+        double oz[3];
+        cross3(p, z, oz);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s[i] = pri ? 0.0 : z[i] * sd;
+            s[3 + i] = pri ? z[i] * sd : oz[i] * sd;
+            x[i] = 0.0;
+            x[3 + i] = 0.0;
+        }
+    }
+    if (jl) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            S.jz()[3 * lane + a] = z[a];
+            S.jo()[3 * lane + a] = p[a];
+        }
+        // the chain element in the record's w, v, al, a slots until the end
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            own[kW + i] = s[i];
+            own[kAl + i] = x[i];
+        }
+    }
+    wave_sync();
+    // 2c. the chain sums: the same rounds
+    ptr = jl ? T.P : 0;
+    for (int span = 1; span <= maxdepth; span <<= 1) {
+        const bool act = jl && ptr > 0;
+        const int pn = H.shfl(ptr, act ? ptr - 1 : 0);
+        if (act) {
+            const double* e = S.link() + kLinkRec * ptr;
+            double sX[6], xX[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                sX[i] = e[kW + i];
+                xX[i] = e[kAl + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) x[i] = xX[i] + x[i];
+            crm_add(sX, s, x);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) s[i] = sX[i] + s[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                own[kW + i] = s[i];
+                own[kAl + i] = x[i];
+            }
+            ptr = pn;
+        }
+        wave_sync();
+    }
+    // 2d. the records' mixed velocities and accelerations
+    if (jl) {
+        double VB[6], A[6], t[3];
+        cross3(pb, wb, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            VB[i] = wb[i];
+            VB[3 + i] = vb[i] + t[i];
+        }
+        cross3(wb, vb, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            A[i] = x[i];
+            A[3 + i] = x[3 + i] - t[i];
+        }
+        crm_add(VB, s, A);
+        double w[3], v[3], al[3], acc[3], u[3], q[3], r[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            w[i] = VB[i] + s[i];
+            al[i] = A[i];
+        }
+        cross3(w, p, u);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = (VB[3 + i] + s[3 + i]) + u[i];
+        cross3(al, p, q);
+        cross3(w, v, r);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) acc[i] = (A[3 + i] + q[i]) + r[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            own[kW + i] = w[i];
+            own[kV + i] = v[i];
+            own[kAl + i] = al[i];
+            own[kA + i] = acc[i];
+        }
+    }
+    wave_sync();
+}
+
+#ifndef BLF_FBD_KINJUMP   // steps 1-2 by pointer jumping (1) or tree level by level (0, A/B)
+#define BLF_FBD_KINJUMP 1     // 4.238 / 4.239 against 4.688 / 4.704 ms per c5 period of fbd_euler_kernel
+#endif                        // (profiles/r04_fbd_kinjump_ab.log); 15.3k -> 9.3k cycles per evaluation
+
+template <int HW, bool PRI>
+__device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, const double* bv,
+                                               const double* jvel, const double* bp, const double* bR,
+                                               const double* jp, const Topo& T)
+{
+    if constexpr (BLF_FBD_KINJUMP) fbd_kinematics_jump<HW, PRI>(m, S, bv, jvel, bp, bR, jp, T);
+    else fbd_kinematics_levels<HW, PRI>(m, S, bv, jvel, bp, bR, jp, T);
+}
+
 // One evaluation of the dynamics for the system whose state sits in LDS (bv, jv, bp, bR, jp).
 // Leaves the generalized acceleration in S.rhs() and returns false if the factorization failed.
 // NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
 // registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
 // steps 6-9.
-template <int NVMAX, int HW, bool PRI, int FOLD = 0>
+template <int NVMAX, int HW, bool PRI, int FOLD = 0, bool LM = false>
 __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
                                          const double* jvel, const double* bp, const double* bR,
                                          const double* jp, const double* tau, const Contacts& ct,
@@ -485,10 +746,17 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     FSTAMP(f_t3);
     // 4. contacts: frame state + ContinuousContactModel wrench, and the wrench about the origin
     for (int c = lane; c < ct.C; c += HW) {
-        const int f = ct.frame[c];
-        const int l = m.flink[f];
+        int l;
+        const double* fp;
+        if constexpr (LM) {
+            l = (int)m.clink[c];
+            fp = m.cpose + 12 * c;
+        } else {
+            const int f = ct.frame[c];
+            l = m.flink[f];
+            fp = m.fpose + 12 * f;
+        }
         const double* k = S.link() + kLinkRec * l;
-        const double* fp = m.fpose + 12 * f;
         const double* R = k + kR;
         double pose[12], tw[6], d[3], t1[3];
         for (int a = 0; a < 3; ++a) {
@@ -933,8 +1201,43 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const Half<HW> H;
     const int n = m.n, NV = n + 6;
-    const Smem S(smem + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
+    // BLF_FBD_LDSMODEL (two systems per wavefront): the model's per-joint / per-link constants,
+    // the gains and the contacts' frames copied once into a block at the start of LDS, at
+    // compile-time offsets, so the Euler loop reads them from LDS and holds no pointers to them
+    constexpr bool kLM = BLF_FBD_LDSMODEL && HW == 32;
+    constexpr int kMB = kLM ? fbd_model_block<NVMAX>() : 0;
+    const Smem S(smem + kMB + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
     const int lane = H.hl;
+    if constexpr (kLM) {
+        constexpr int J = NVMAX - 6, Lk = NVMAX - 5;
+        constexpr int oA = 0, oR = oA + 3 * J, oC = oR + 9 * J, oI = oC + 3 * Lk, oM = oI + 9 * Lk;
+        constexpr int oKp = oM + Lk, oKd = oKp + J, oP = oKd + J, oL = oP + 12 * BLF_FBD_MAX_CONTACTS;
+        const int t = threadIdx.x, L = n + 1;
+        for (int i = t; i < 3 * n; i += kWave) smem[oA + i] = m.jaxis[i];
+        for (int i = t; i < 9 * n; i += kWave) smem[oR + i] = m.jrot[i];
+        for (int i = t; i < 3 * L; i += kWave) smem[oC + i] = m.com[i];
+        for (int i = t; i < 9 * L; i += kWave) smem[oI + i] = m.inertia[i];
+        for (int i = t; i < L; i += kWave) smem[oM + i] = m.mass[i];
+        if (imp.kp)
+            for (int i = t; i < n; i += kWave) {
+                smem[oKp + i] = imp.kp[i];
+                smem[oKd + i] = imp.kd[i];
+            }
+        for (int i = t; i < 12 * ct.C; i += kWave) smem[oP + i] = m.fpose[12 * ct.frame[i / 12] + i % 12];
+        for (int i = t; i < ct.C; i += kWave) smem[oL + i] = (double)m.flink[ct.frame[i]];
+        wave_sync();
+        m.jaxis = smem + oA;
+        m.jrot = smem + oR;
+        m.com = smem + oC;
+        m.inertia = smem + oI;
+        m.mass = smem + oM;
+        m.cpose = smem + oP;
+        m.clink = smem + oL;
+        if (imp.kp) {
+            imp.kp = smem + oKp;
+            imp.kd = smem + oKd;
+        }
+    }
     constexpr int per = kWave / HW;   // systems per wavefront
     // the systems: the batch (q = blockIdx.x * per + half), or a list (sel.list: a grid of a few
     // wavefronts loops over the listed systems, per at a time)
@@ -971,7 +1274,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
             wave_sync();
             tq = S.tq();
         }
-        ok = fbd_eval<NVMAX, HW, PRI, BLF_FBD_FOLD>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+        ok = fbd_eval<NVMAX, HW, PRI, BLF_FBD_FOLD, kLM>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                  tq, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         wave_sync();
@@ -1108,6 +1411,8 @@ Model to_model(const blf_fb_model* md)
     m.inertia = md->link_inertia;
     m.flink = md->frame_link;
     m.fpose = md->frame_pose;
+    m.cpose = nullptr;
+    m.clink = nullptr;
     m.g0 = md->gravity[0];
     m.g1 = md->gravity[1];
     m.g2 = md->gravity[2];
@@ -1161,6 +1466,7 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
     // only as the other stream's dynamics frees the chip, wavefront by wavefront)
     const int64_t wv2 = list ? std::min<int64_t>(ceil_div(batch, 2), kListGrid) : ceil_div(batch, 2);
     const int64_t wv1 = list ? std::min<int64_t>(batch, kListGrid) : batch;
+    const size_t mb32 = BLF_FBD_LDSMODEL ? sizeof(double) * fbd_model_block<32>() : 0;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     Impedance imp{nullptr, nullptr, nullptr};
@@ -1175,11 +1481,11 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
     if (BLF_FBD_NFIX > 0 && md->ndof == BLF_FBD_NFIX && BLF_FBD_NFIX + 6 <= 32 && BLF_FBD_SMALL_HW == 32)
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>
                                 : fbd_euler_kernel<32, 32, false, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>),
-                           dim3((unsigned)wv2), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
+                           dim3((unsigned)wv2), dim3(kWave), 2 * lds + mb32, s, to_model(md), *st, tau, c,
                            reg, nsteps, dT, dT_last, imp, batch, sel);
     else if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true> : fbd_euler_kernel<32, 32, false>),
-                           dim3((unsigned)wv2), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
+                           dim3((unsigned)wv2), dim3(kWave), 2 * lds + mb32, s, to_model(md), *st, tau, c,
                            reg, nsteps, dT, dT_last, imp, batch, sel);
     else if (md->ndof + 6 <= 32)   // one system per wavefront, NV <= 32 rows
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, kWave, true> : fbd_euler_kernel<32, kWave, false>),
