@@ -92,8 +92,19 @@ __device__ __forceinline__ void wave_sync()
 #ifndef BLF_FBD_FOLD
 #define BLF_FBD_FOLD 0
 #endif
+#ifndef BLF_FBD_PREFIX_LDS   // DFS subtree sums: step 5 leaves the prefix sums, step 6 takes the differences (1)
+#define BLF_FBD_PREFIX_LDS 1   // or step 5 gathers them by lane shuffles (0, A/B): 3.812 / 3.811 against
+                               // 4.077 / 4.074 ms per c5 period (profiles/r04_fbd_prefix_opq_ab.log)
+#endif
+#ifndef BLF_FBD_OPQLANE   // fbd_eval's lane index opaque per evaluation (1) or not (0, A/B)
+#define BLF_FBD_OPQLANE 1   // 3.812 / 3.811 against 3.856 / 3.860 ms per c5 period; SGPR spills 595 -> 366,
+#endif                      // VGPR spills 17 -> 0 (profiles/r04_fbd_prefix_opq_ab.log)
+#ifndef BLF_FBD_CSUB   // contact wrenches subtracted from the link forces in step 3 (1) or in step 5 (0, A/B)
+#define BLF_FBD_CSUB 1  // 4.070 / 4.078 against 4.198 / 4.200 ms per c5 period (profiles/r04_fbd_csub_ab.log)
+#endif
 
 constexpr int kPad = BLF_FBD_PAD;
+constexpr bool kPrefixLds = BLF_FBD_PREFIX_LDS && BLF_FBD_CSUB;   // (the base's contacts: step 3)
 constexpr int kLinkRec = 40 + kPad;   // record stride (40 doubles of data)
 constexpr int kR = 0, kP = 9, kW = 12, kV = 15, kAl = 18, kA = 21, kSI = 24, kSF = 34;
 constexpr int kComp = 16;             // subtree sum: spatial inertia 10 | spatial force 6
@@ -254,6 +265,7 @@ struct Topo {
     double o0, o1, o2;
     unsigned long long cmask, bmask;
     int last;   // the last joint of joint lane's subtree (DFS preorder: the run [lane, last])
+    int lastc;  // the same for column lane's joint (lane - 6; lanes < 6: 0)
     bool dfs;   // the joints are in DFS preorder (wave-uniform): every subtree is a contiguous run
 };
 
@@ -305,6 +317,7 @@ __device__ __forceinline__ Topo build_topo(const Model& m, const Smem& S)
             if (lane == j) size = c;
         }
         t.last = jl ? lane + size - 1 : 0;
+        t.lastc = H.shfl(t.last, lane >= 6 && lane < n + 6 ? lane - 6 : 0);
     }
     int md = depth;
 #pragma unroll
@@ -683,7 +696,11 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     static_assert(NVMAX <= HW, "a system's rows must fit its lanes");
     const Half<HW> H;
     const int n = m.n, L = n + 1, NV = n + 6, MS = S.ms;
-    const int lane = H.hl;
+    // BLF_FBD_OPQLANE: the lane index made opaque once per evaluation, so the lane masks of the
+    // unrolled loops (lane == k, lane > k, ...) are recomputed by one compare each instead of being
+    // hoisted out of the Euler loop into SGPRs, which spill to VGPR lanes and reload by v_readlane
+    int lane = H.hl;
+    if constexpr (BLF_FBD_OPQLANE) asm volatile("" : "+v"(lane));
     const bool jl = lane < n;   // n <= 48 < 64: one joint per lane
     const int depth = T.depth, maxdepth = T.maxdepth;
     FSTAMP(f_t0);
@@ -692,7 +709,10 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     FSTAMP_ADD(1, f_t1);
     FSTAMP(f_t2);
     // 3. per link: COM, world inertia, Newton-Euler force / moment, and the spatial inertia and
-    //    force about the world origin (lane per link)
+    //    force about the world origin (lane per link); BLF_FBD_CSUB: after step 4, with the
+    //    contact wrenches on the link (about the origin) subtracted from its force here, once,
+    //    instead of in every component group of the subtree sums
+    auto link_step = [&]() {
     for (int l = lane; l < L; l += HW) {
         double* k = S.link() + kLinkRec * l;
         const double* R = k + kR;
@@ -736,15 +756,28 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         si[7] = Iw[3] + ms * (cc - c[1] * c[1]);
         si[8] = Iw[4] - ms * (c[1] * c[2]);
         si[9] = Iw[5] + ms * (cc - c[2] * c[2]);
-        double* sf = k + kSF;
+        double sfv[6];
         for (int a = 0; a < 3; ++a) {
-            sf[a] = tq[a] + cf[a];
-            sf[3 + a] = f[a];
+            sfv[a] = tq[a] + cf[a];
+            sfv[3 + a] = f[a];
         }
+        if constexpr (BLF_FBD_CSUB) {
+            for (int cc2 = 0; cc2 < ct.C; ++cc2) {   // branch-free: the loads do not wait for the test
+                const double* sc = S.cscr() + kCs * cc2;
+                const bool hit = (int)sc[9] == l;
+                double w[6];
+#pragma unroll
+                for (int a = 0; a < 6; ++a) w[a] = sc[10 + a];
+#pragma unroll
+                for (int a = 0; a < 6; ++a) sfv[a] = hit ? sfv[a] - w[a] : sfv[a];
+            }
+        }
+        double* sf = k + kSF;
+        for (int a = 0; a < 6; ++a) sf[a] = sfv[a];
     }
-    FSTAMP_ADD(2, f_t2);
-    FSTAMP(f_t3);
+    };
     // 4. contacts: frame state + ContinuousContactModel wrench, and the wrench about the origin
+    auto contacts_step = [&]() {
     for (int c = lane; c < ct.C; c += HW) {
         int l;
         const double* fp;
@@ -782,7 +815,22 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         }
     }
     wave_sync();
-    FSTAMP_ADD(3, f_t3);
+    };
+    if constexpr (!BLF_FBD_CSUB) {
+        link_step();
+        FSTAMP_ADD(2, f_t2);
+        FSTAMP(f_t3);
+        contacts_step();
+        FSTAMP_ADD(3, f_t3);
+    } else {
+        FSTAMP(f_t3);
+        contacts_step();
+        FSTAMP_ADD(3, f_t3);
+        FSTAMP(f_t2b);
+        link_step();
+        wave_sync();
+        FSTAMP_ADD(2, f_t2b);
+    }
     FSTAMP(f_t4);
     // 5. subtree sums of the spatial inertias and (link - contact) forces.  DFS-ordered models
     //    (every subtree a contiguous run of joints, T.dfs): one inclusive prefix sum over the
@@ -795,8 +843,13 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
 #pragma unroll
         for (int g = 0; g < kComp; g += G) {
             double v[G], pre[G];
+            double bo[G];   // the base link's own terms (every lane reads them: no branch)
 #pragma unroll
-            for (int q = 0; q < G; ++q) v[q] = jl ? S.link()[kLinkRec * (lane + 1) + kSI + g + q] : 0.0;
+            for (int q = 0; q < G; ++q) {
+                v[q] = jl ? S.link()[kLinkRec * (lane + 1) + kSI + g + q] : 0.0;
+                bo[q] = kPrefixLds ? 0.0 : S.link()[kSI + g + q];
+            }
+            if constexpr (!BLF_FBD_CSUB)
             for (int c = 0; c < ct.C; ++c) {
                 const double* sc = S.cscr() + kCs * c;
                 if (jl && (int)sc[9] == lane + 1)
@@ -824,6 +877,14 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             level(std::integral_constant<int, 3>{});
             level(std::integral_constant<int, 4>{});
             if constexpr (HW == 64) level(std::integral_constant<int, 5>{});
+            if constexpr (kPrefixLds) {   // step 6 takes prefix[last_j] - prefix[j - 1] itself
+#pragma unroll
+                for (int q = 0; q < G; ++q)
+                    if (jl) S.comp()[kCompS * lane + g + q] = pre[q];
+                (void)bo;
+                (void)src;
+                continue;
+            }
 #pragma unroll
             for (int q = 0; q < G; ++q) {
 #if BLF_FBD_SCANX
@@ -839,8 +900,11 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                 const double tot = __shfl(pre[q], n - 1, HW);
 #endif
                 if (jl) S.comp()[kCompS * lane + g + q] = lane > 0 ? atl - bef : atl;
-                if (lane == 0) {
-                    double b = S.link()[kSI + g + q] + tot;
+                if constexpr (BLF_FBD_CSUB) {
+                    const double b = bo[q] + tot;
+                    if (lane == 0) S.comp()[kCompS * n + g + q] = b;
+                } else if (lane == 0) {
+                    double b = bo[q] + tot;
                     for (int c = 0; c < ct.C; ++c) {
                         const double* sc = S.cscr() + kCs * c;
                         if (g + q >= 10 && (int)sc[9] == 0) b = b - sc[g + q];
@@ -859,6 +923,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             double acc[kComp];
 #pragma unroll
             for (int p = 0; p < kComp; ++p) acc[p] = S.link()[kLinkRec * l + kSI + p];
+            if constexpr (!BLF_FBD_CSUB)
             for (int c = 0; c < ct.C; ++c) {
                 const double* sc = S.cscr() + kCs * c;
                 if ((int)sc[9] == l)
@@ -899,7 +964,21 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                 cross3(S.jo() + 3 * j, w, u);
             }
         }
-        const double* I = S.comp() + kCompS * (c < 6 ? n : c - 6);
+        double Iv[kComp];
+        if (kPrefixLds && T.dfs) {   // the subtree sums from the prefix sums step 5 left
+            const int j = c - 6;
+            const double* hp = S.comp() + kCompS * (c < 6 ? n - 1 : T.lastc);
+            const double* lp = c < 6 ? S.link() + kSI : S.comp() + kCompS * (j > 0 ? j - 1 : 0);
+#pragma unroll
+            for (int p = 0; p < kComp; ++p) {
+                const double h = hp[p], l = lp[p];
+                Iv[p] = c < 6 ? l + h : (j > 0 ? h - l : h);
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < kComp; ++p) Iv[p] = S.comp()[kCompS * (c < 6 ? n : c - 6) + p];
+        }
+        const double* I = Iv;
         double Iwv[3], hu[3], wh[3];
         sym_mv(I + 4, w, Iwv);
         cross3(I + 1, u, hu);
