@@ -96,6 +96,9 @@ __device__ __forceinline__ void wave_sync()
 #define BLF_FBD_PREFIX_LDS 1   // or step 5 gathers them by lane shuffles (0, A/B): 3.812 / 3.811 against
                                // 4.077 / 4.074 ms per c5 period (profiles/r04_fbd_prefix_opq_ab.log)
 #endif
+#ifndef BLF_FBD_SUBST   // substitutions with the pivot scaling on the multipliers (1, A/B) or on the unknowns (0)
+#define BLF_FBD_SUBST 0   // 1: 3.914 / 3.904 against 3.792 / 3.792 ms per c5 period (profiles/r04_fbd_subst_ab.log)
+#endif
 #ifndef BLF_FBD_OPQLANE   // fbd_eval's lane index opaque per evaluation (1) or not (0, A/B)
 #define BLF_FBD_OPQLANE 1   // 3.812 / 3.811 against 3.856 / 3.860 ms per c5 period; SGPR spills 595 -> 366,
 #endif                      // VGPR spills 17 -> 0 (profiles/r04_fbd_prefix_opq_ab.log)
@@ -105,6 +108,7 @@ __device__ __forceinline__ void wave_sync()
 
 constexpr int kPad = BLF_FBD_PAD;
 constexpr bool kPrefixLds = BLF_FBD_PREFIX_LDS && BLF_FBD_CSUB;   // (the base's contacts: step 3)
+constexpr bool kSubst = BLF_FBD_SUBST && BLF_FBD_CHOLB > 1;        // (the pivots: the block factorization)
 constexpr int kLinkRec = 40 + kPad;   // record stride (40 doubles of data)
 constexpr int kR = 0, kP = 9, kW = 12, kV = 15, kAl = 18, kA = 21, kSI = 24, kSF = 34;
 constexpr int kComp = 16;             // subtree sum: spatial inertia 10 | spatial force 6
@@ -1056,6 +1060,8 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                 double q = __builtin_amdgcn_rsq(d);
                 il[i] = q * (1.5 - (0.5 * d) * (q * q));
                 Lb[i][i] = d * il[i];
+                // 1 / L_kk for the substitutions (BLF_FBD_SUBST); S.rhs() is free until the end
+                if (kSubst && HW == 32 && lane == 0 && k + i < NV) S.rhs()[k + i] = il[i];
             }
             // this lane's entries L_{lane,k..k+CB-1} (upper-triangle junk inside the block, unread)
             double li[CB];
@@ -1171,6 +1177,44 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     //    link records are dead by now); lane k scales its own entry, one broadcast per step.  Two
     //    unknowns per step (the 2 x 2 block solved by every lane, as in the factorization) measured
     //    the same: 6.054 / 6.069 against 6.081 / 6.073 ms per c5 period of the Euler kernel
+    if constexpr (kSubst && HW == 32) {
+    // BLF_FBD_SUBST (two systems per wavefront; LLVM's register allocator crashes on it in the
+    // one-system instantiations): the unknown's scaling rides on the multiplier, not on the broadcast value:
+    // step k broadcasts lane k's unscaled entry t_k and the rows update y_i -= (L_ik / L_kk) t_k,
+    // whose factor is known ahead; the pivots 1 / L_kk come from the factorization (S.rhs()), and
+    // every entry is scaled once at the end.  Per step the dependent chain is the broadcast and
+    // one fma (was: scale, select, broadcast, multiply, subtract).
+    const double* ilv = S.rhs();
+    const double idg = lane < NV ? ilv[lane] : 0.0;
+    double ilk = ilv[0];
+#pragma unroll
+    for (int k = 0; k < NVMAX; ++k) {   // k >= NV changes only lanes past the matrix
+        const double ilnext = ilv[k + 1 < NV ? k + 1 : NV - 1];   // read ahead
+        const double t = H.bcast_k(y, k);
+        const double f = lane > k ? r[k] * ilk : 0.0;
+        y = fma(-f, t, y);
+        ilk = ilnext;
+    }
+    y = y * idg;
+    double* Lr = S.link();
+    if (lane < NV)
+#pragma unroll
+        for (int j = 0; j < NVMAX; ++j)
+            if (j < NV && j <= lane) Lr[MS * lane + j] = r[j];
+    wave_sync();
+    double lki = (lane < NV - 1) ? Lr[MS * (NV - 1) + lane] : 0.0;
+    ilk = ilv[NV - 1];
+    for (int k = NV - 1; k >= 0; --k) {
+        const double lnext = (k > 0 && lane < k - 1) ? Lr[MS * (k - 1) + lane] : 0.0;   // read ahead
+        const double ilnext = ilv[k > 0 ? k - 1 : 0];
+        const double t = H.bcast_k(y, k);
+        const double f = lane < k ? lki * ilk : 0.0;
+        y = fma(-f, t, y);
+        lki = lnext;
+        ilk = ilnext;
+    }
+    y = y * idg;
+    } else {
     const double idg = lane < NV ? 1.0 / bcast_own_diag<NVMAX>(r, lane) : 0.0;
 #pragma unroll
     for (int k = 0; k < NVMAX; ++k) {   // k >= NV changes only lanes past the matrix
@@ -1192,6 +1236,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         const double xk = H.bcast_k(y, k);
         if (lane < k) y = y - lki * xk;
         lki = lnext;
+    }
     }
 #if BLF_FBD_CHOLB > 1
     }
