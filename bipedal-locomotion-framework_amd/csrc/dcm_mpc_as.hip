@@ -835,6 +835,10 @@ __device__ __forceinline__ int as_cand(const AKnotT<T>& K)
 // `handover` knots ends the search, its next candidate sets going to the fp64 passes instead of
 // another float pass (oracle passes32): the last float pass before the
 // certifying one changes a few knots, and the fp64 passes certify that set.  -1: never.
+#ifndef BLF_AS_OPQLANE   // A/B: 1 (VGPRs 228 -> 221, SGPR spills 36 -> 44) took 0.127 / 0.128 against 0.125 /
+#define BLF_AS_OPQLANE 0   // 0.126 ms at B = 4096 (profiles/r04_cstage_asopq_ab.log), so 0
+#endif
+
 template <int KPL, int TR, class T, class RS>
 __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, const RS& R, int NH, int N,
                                           int lane, T xi00, T xi01, int (&pk)[KPL],
@@ -843,7 +847,12 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
     T xk[KPL][2];
     as_xi_prev<KPL, T>(K, lane, xi00, xi01, xk);
     bool certified = false;
+    const int lane0 = lane;
     for (int pass = 0; pass < kGuessPasses; ++pass) {
+        // BLF_AS_OPQLANE: the lane index opaque per pass, so its masks are recomputed inside the
+        // pass instead of hoisted out of the loop into SGPRs (which spill)
+        int lane = lane0;
+        if constexpr (BLF_AS_OPQLANE) asm volatile("" : "+v"(lane));
         AS_COUNT(count_slot);
         AS_STAMP(t_s);
         T sv[KPL][4];

@@ -99,6 +99,16 @@ __device__ __forceinline__ void wave_sync()
 #ifndef BLF_FBD_SUBST   // substitutions with the pivot scaling on the multipliers (1, A/B) or on the unknowns (0)
 #define BLF_FBD_SUBST 0   // 1: 3.914 / 3.904 against 3.792 / 3.792 ms per c5 period (profiles/r04_fbd_subst_ab.log)
 #endif
+#ifndef BLF_FBD_KINJUMP   // steps 1-2 by pointer jumping (1) or tree level by level (0, A/B)
+#define BLF_FBD_KINJUMP 1     // 4.238 / 4.239 against 4.688 / 4.704 ms per c5 period of fbd_euler_kernel
+#endif                        // (profiles/r04_fbd_kinjump_ab.log); 15.3k -> 9.3k cycles per evaluation
+#ifndef BLF_FBD_CSTAGE   // fbd_euler_kernel stages each system's contact / impedance constants in LDS (1) or
+#define BLF_FBD_CSTAGE 1   // reads them from global memory every Euler step (0, A/B): 3.793 / 3.773 against
+                           // 3.805 / 3.785 ms per c5 period (profiles/r04_cstage_asopq_ab.log)
+#endif
+#ifndef BLF_FBD_COLFIX   // the factorization's column sets at a compile-time stride (1, A/B) or at NV (0)
+#define BLF_FBD_COLFIX 0   // 1: Cholesky 19.9k -> 14.8k cycles in fbd_dynamics_kernel, but one c5 period of the
+#endif                     // Euler kernel 4.04 / 4.02 against 3.77 / 3.76 ms (profiles/r04_fbd_colfix_cstage_ab.log)
 #ifndef BLF_FBD_OPQLANE   // fbd_eval's lane index opaque per evaluation (1) or not (0, A/B)
 #define BLF_FBD_OPQLANE 1   // 3.812 / 3.811 against 3.856 / 3.860 ms per c5 period; SGPR spills 595 -> 366,
 #endif                      // VGPR spills 17 -> 0 (profiles/r04_fbd_prefix_opq_ab.log)
@@ -121,7 +131,7 @@ struct Smem {
     // one base pointer (per system: the two halves of a wavefront have their own) and wave-uniform
     // offsets, so the per-half base costs one address, not one per array
     double* base;
-    int o_link, o_jrot, o_jz, o_jo, o_comp, o_sax, o_rhs, o_cscr, o_st, o_tq, o_anc;
+    int o_link, o_jrot, o_jz, o_jo, o_comp, o_sax, o_rhs, o_cscr, o_st, o_tq, o_anc, o_cst, o_imp;
     int ms;   // row stride of L (odd: the per-lane row accesses do not conflict)
     size_t total;
     __host__ __device__ Smem(double* b, int n, int C) : base(b)
@@ -137,19 +147,24 @@ struct Smem {
         // link records; after the mass matrix is assembled the same space holds L (NV rows)
         const size_t lk = (size_t)kLinkRec * L, lm = (size_t)NV * ms;
         o_link = take(lk > lm ? lk : lm);
-        o_jrot = take(kJrot * (size_t)n);        // E_j Rot(a_j, s_j) (9) | E_j a_j (3)
+        o_jrot = take(BLF_FBD_KINJUMP ? 0 : kJrot * (size_t)n);   // E_j Rot(a_j, s_j) (9) | E_j a_j (3): levels only
         o_jz = take(3 * (size_t)n);
         o_jo = take(3 * (size_t)n);
         // subtree sums [j] (joint j's subtree) and [n] (every link); later the pivot-column
         // buffers of the factorization (two sets of up to 4 columns, 8 NV)
         const size_t cp = (size_t)kCompS * (n + 1);
-        o_comp = take(cp > 8 * (size_t)NV ? cp : 8 * (size_t)NV);
+        const size_t cb = 8 * (size_t)(NV > 32 ? NV : 32);   // (BLF_FBD_COLFIX: 2 CB NVMAX)
+        o_comp = take(cp > cb ? cp : cb);
         o_sax = take(kSax * (size_t)NV);
         o_rhs = take((size_t)NV);
         o_cscr = take((size_t)kCs * (C > 0 ? C : 1));
         o_st = take(18 + 2 * (size_t)n + (size_t)NV + 9);   // Euler state (6 + n + 3 + 9 + n) + acc + dR
         o_tq = take((size_t)n);                              // the joint impedance's torques
         o_anc = take((size_t)L);
+        // fbd_euler_kernel's per-system constants (BLF_FBD_CSTAGE): each contact's link, frame
+        // pose, null pose and parameters [C | 12 C | 12 C | 4 C]; the impedance's kp, kd, q_ref
+        o_cst = take(BLF_FBD_CSTAGE ? 29 * (size_t)C : 0);
+        o_imp = take(BLF_FBD_CSTAGE ? 3 * (size_t)n : 0);
         total = o;
     }
     __device__ __forceinline__ double* link() const { return base + o_link; }
@@ -162,6 +177,8 @@ struct Smem {
     __device__ __forceinline__ double* cscr() const { return base + o_cscr; }
     __device__ __forceinline__ double* st() const { return base + o_st; }
     __device__ __forceinline__ double* tq() const { return base + o_tq; }
+    __device__ __forceinline__ double* cst() const { return base + o_cst; }
+    __device__ __forceinline__ double* imp() const { return base + o_imp; }
     __device__ __forceinline__ unsigned long long* anc() const
     {
         return reinterpret_cast<unsigned long long*>(base + o_anc);
@@ -673,9 +690,6 @@ __device__ __forceinline__ void fbd_kinematics_jump(const Model& m, const Smem& 
     wave_sync();
 }
 
-#ifndef BLF_FBD_KINJUMP   // steps 1-2 by pointer jumping (1) or tree level by level (0, A/B)
-#define BLF_FBD_KINJUMP 1     // 4.238 / 4.239 against 4.688 / 4.704 ms per c5 period of fbd_euler_kernel
-#endif                        // (profiles/r04_fbd_kinjump_ab.log); 15.3k -> 9.3k cycles per evaluation
 
 template <int HW, bool PRI>
 __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, const double* bv,
@@ -691,7 +705,7 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
 // NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
 // registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
 // steps 6-9.
-template <int NVMAX, int HW, bool PRI, int FOLD = 0, bool LM = false>
+template <int NVMAX, int HW, bool PRI, int FOLD = 0, bool LM = false, bool CS = false>
 __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
                                          const double* jvel, const double* bp, const double* bR,
                                          const double* jp, const double* tau, const Contacts& ct,
@@ -785,7 +799,10 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     for (int c = lane; c < ct.C; c += HW) {
         int l;
         const double* fp;
-        if constexpr (LM) {
+        if constexpr (CS) {
+            l = (int)S.cst()[c];
+            fp = S.cst() + ct.C + 12 * c;
+        } else if constexpr (LM) {
             l = (int)m.clink[c];
             fp = m.cpose + 12 * c;
         } else {
@@ -808,7 +825,10 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             tw[3 + a] = k[kW + a];
         }
         double* sc = S.cscr() + kCs * c;
-        contact_wrench(ct.params + 4 * c, tw, pose, ct.null_pose + (sys * ct.C + c) * 12, sc + 3);
+        if constexpr (CS)
+            contact_wrench(S.cst() + 25 * ct.C + 4 * c, tw, pose, S.cst() + 13 * ct.C + 12 * c, sc + 3);
+        else
+            contact_wrench(ct.params + 4 * c, tw, pose, ct.null_pose + (sys * ct.C + c) * 12, sc + 3);
         sc[0] = pose[0]; sc[1] = pose[1]; sc[2] = pose[2];
         sc[9] = (double)l;
         double xf[3];
@@ -1088,19 +1108,24 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             for (int i = 0; i < CB; ++i) y = lane == k + i ? z[i] : y;
             y = lane >= k + CB ? yl : y;
             }
-            double* col = FOLD >= 2 ? Lm + MS * k : S.comp() + ((k / CB) & 1) * CB * NV;
-            const int cst = FOLD >= 2 ? MS : NV;
+            // BLF_FBD_COLFIX: the column sets at the compile-time stride NVMAX, every lane of the
+            // rows (padding lanes: zeros) writing its entry, so the update reads every row at a
+            // constant offset (no clamped per-row address registers; paired LDS reads)
+            constexpr int kColS = BLF_FBD_COLFIX ? NVMAX : 0;
+            double* col = FOLD >= 2 ? Lm + MS * k
+                                    : S.comp() + ((k / CB) & 1) * CB * (BLF_FBD_COLFIX ? NVMAX : NV);
+            const int cst = FOLD >= 2 ? MS : (BLF_FBD_COLFIX ? kColS : NV);
 #define FBD_COL(i, row) col[(i) * cst + (row)]
 #pragma unroll
             for (int i = 0; i < CB; ++i) {
                 r[k + i] = lane >= k ? li[i] : r[k + i];
-                if (lane < NV && k + i < NV) FBD_COL(i, lane) = r[k + i];
+                if ((BLF_FBD_COLFIX && FOLD < 2 ? lane < NVMAX : lane < NV) && k + i < NV) FBD_COL(i, lane) = r[k + i];
             }
             wave_sync();
             // no row predicate (as below): lanes above row j update only upper-triangle entries
 #pragma unroll
             for (int j = k + CB; j < NVMAX; ++j) {
-                const int jj = j < NV ? j : NV - 1;
+                const int jj = (BLF_FBD_COLFIX && FOLD < 2) ? j : (j < NV ? j : NV - 1);
                 double t = r[j];
 #pragma unroll
                 for (int i = CB - 1; i >= 0; --i) t = fma(-r[k + i], FBD_COL(i, jj), t);
@@ -1329,6 +1354,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
     // the gains and the contacts' frames copied once into a block at the start of LDS, at
     // compile-time offsets, so the Euler loop reads them from LDS and holds no pointers to them
     constexpr bool kLM = BLF_FBD_LDSMODEL && HW == 32;
+    constexpr bool kCS = BLF_FBD_CSTAGE && !kLM && HW == 32;   // (LLVM's allocator crashes on the HW = 64 form)
     constexpr int kMB = kLM ? fbd_model_block<NVMAX>() : 0;
     const Smem S(smem + kMB + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
     const int lane = H.hl;
@@ -1387,18 +1413,39 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
         else v = st.joint_pos[(int64_t)n * q + (i - 18 - n)];
         loc[i] = v;
     }
+    if constexpr (kCS) {   // this system's constants of the Euler loop, once (BLF_FBD_CSTAGE)
+        const int C = ct.C;
+        for (int i = lane; i < 29 * C; i += HW) {
+            double v;
+            if (i < C) v = (double)m.flink[ct.frame[i]];
+            else if (i < 13 * C) v = m.fpose[12 * ct.frame[(i - C) / 12] + (i - C) % 12];
+            else if (i < 25 * C) v = ct.null_pose[(q * C) * 12 + (i - 13 * C)];
+            else v = ct.params[i - 25 * C];
+            S.cst()[i] = v;
+        }
+        if (imp.kp)
+            for (int j = lane; j < n; j += HW) {
+                S.imp()[j] = imp.kp[j];
+                S.imp()[n + j] = imp.kd[j];
+                S.imp()[2 * n + j] = imp.qref[(int64_t)n * q + j];
+            }
+    }
     wave_sync();
     bool ok = true;
     const double* tq = tau + (int64_t)n * q;
     for (int32_t step = 0; step < nsteps; ++step) {
         const double h = step + 1 < nsteps ? dT : dT_last;
         if (imp.kp) {   // the control input of this step from its start state
-            for (int j = lane; j < n; j += HW)
-                S.tq()[j] = imp.kp[j] * (imp.qref[(int64_t)n * q + j] - loc[18 + n + j]) - imp.kd[j] * loc[6 + j];
+            for (int j = lane; j < n; j += HW) {
+                if constexpr (kCS)
+                    S.tq()[j] = S.imp()[j] * (S.imp()[2 * n + j] - loc[18 + n + j]) - S.imp()[n + j] * loc[6 + j];
+                else
+                    S.tq()[j] = imp.kp[j] * (imp.qref[(int64_t)n * q + j] - loc[18 + n + j]) - imp.kd[j] * loc[6 + j];
+            }
             wave_sync();
             tq = S.tq();
         }
-        ok = fbd_eval<NVMAX, HW, PRI, BLF_FBD_FOLD, kLM>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+        ok = fbd_eval<NVMAX, HW, PRI, BLF_FBD_FOLD, kLM, kCS>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                  tq, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         wave_sync();
