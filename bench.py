@@ -171,10 +171,6 @@ def main():
                     help="c5: robots in this many groups, each closed loop on its own stream "
                          "(round 4, profiles/r04_v2_c5_g*.log: 1 group 5.88 / 5.88 ms, 2 groups "
                          "5.74 / 5.67 ms per period; 3 groups 6.05 / 6.13 ms, profiles/r04f_*)")
-    ap.add_argument("--c5-overlap", type=int, default=0,
-                    help="c5: 1 = the robots whose plan the active-set kernel solved integrate while "
-                         "the interior point kernel finishes the rest on a side stream (ClosedLoop "
-                         "overlap; the same bits)")
     ap.add_argument("--tol-polish", type=float, default=None,
                     help="override blf_dcm_mpc_default_params' tol_polish (also the CPU baseline's)")
     ap.add_argument("--expand-path", action="store_true",
@@ -494,7 +490,7 @@ def closed_loop(args):
         # (DL.split_groups states when); two groups let one group's plan tail (the interior
         # point kernel's few uncapturable windows) run beside the other group's kernels
         # 
-        loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N, overlap=bool(args.c5_overlap))
+        loops = DL.split_groups(h, model, plan, st, args.c5_groups, horizon=N)
         for lp in loops:
             lp.expand_path = args.expand_path
         state_of = lambda lp: {k: v.cpu().numpy() for k, v in lp.state.items()}
@@ -564,7 +560,7 @@ def closed_loop(args):
                                        f"(integrate(0, {T * 1e3:g} ms) at dT = {dT * 1e3:g} ms: "
                                        f"{robot_ms:g} ms of robot time, the reference schedule)",
                            "batch_per_gpu": B, "parallelism": f"shard{world} (independent robots)",
-                           "stream_groups": len(loops), "overlap": bool(args.c5_overlap)}}
+                           "stream_groups": len(loops)}}
         if on_cpu:
             line["device"] = "CPU rehearsal (BLF_C5_ORACLE=1: oracle/closed_loop.py on every rank)"
         if not args.no_cpu:

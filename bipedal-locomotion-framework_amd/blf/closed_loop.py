@@ -62,8 +62,6 @@ def period_final_time(dt, dT):
 # test's foot size; stiffness and damping for a 50 kg robot on two 0.12 x 0.09 m soles (about
 # 1 cm of sink) that explicit Euler at dT = 1 ms integrates stably
 CONTACT_PARAMS = (0.12, 0.09, 2.0e6, 2.0e4)
-# CUs the overlap's side stream keeps for itself (of 256 on an MI355X)
-OVERLAP_SIDE_CUS = 8
 
 
 class ClosedLoop:
@@ -72,29 +70,9 @@ class ClosedLoop:
     problem dict with a horizon of at least horizon + the number of periods to run."""
 
     def __init__(self, h, model, plan, states, horizon=100, dT=0.001, law=None,
-                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None, overlap=False,
-                 side_cus=OVERLAP_SIDE_CUS):
+                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None):
         import torch
         self.h, self.N, self.dT, self.stream = h, horizon, dT, stream
-        # overlap: the robots whose window the active-set kernel solved go on to the posture and
-        # the dynamics at once; the few it hands to the interior point kernel (uncapturable DCM
-        # states, tens of iterations on an otherwise idle chip) finish on a side stream, where
-        # their own posture and dynamics follow (blf_dcm_mpc_solve_phased_begin / _finish and the
-        # list-driven kernels).  Every robot's computation is the same, so the states are the same
-        # bits.  The side stream runs on `side_cus` CUs of its own and the main stream on the
-        # rest (blf_stream_create_cu_range): sharing every CU, the side's few waves waited behind
-        # the dynamics kernel that fills the chip (profiles/r04_c5_overlap_trace.log).
-        self.overlap = bool(overlap)
-        self.side = None
-        if self.overlap:
-            import os
-            mode = os.environ.get("BLF_OVERLAP_CU_MODE", "side")   # A/B: side | split | none
-            if side_cus > 0 and mode in ("side", "split"):
-                if mode == "split" and stream is None:
-                    self.stream = h.cu_stream(0, side_cus, exclude=True)
-                self.side = h.cu_stream(0, side_cus)
-            else:
-                self.side = torch.cuda.Stream(device=h.device)
         dev = torch.device("cuda", h.device)
         t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)
         self.dt = float(plan["dt"])
@@ -137,8 +115,6 @@ class ClosedLoop:
             # a robot whose previous window was not solved (status != 0) is planned cold
             warm = dict(vrp=self.prev["vrp"], lam=self.prev["lam"], shift=1, floor=1e-3,
                         status=self.prev["status"])
-        if N <= 128 and not self.expand_path and self.overlap:
-            return self._period_overlap(warm)
         if N <= 128 and not self.expand_path:   # the window read from the phase table
             out = h.dcm_mpc_solve_phased(self.table, s, self.xi, self.omega[:, s:s + N],
                                          self.params, warm=warm, out=self.bufs[s % 2],
@@ -159,37 +135,6 @@ class ClosedLoop:
         self.prev = out
         self.s = s + 1
         return out
-
-    def _period_overlap(self, warm):
-        """period() with the interior point kernel's problems on the side stream (overlap)."""
-        import torch
-        h, s, N = self.h, self.s, self.N
-        main = self.stream if self.stream is not None else torch.cuda.current_stream(h.device)
-        out = h.dcm_mpc_solve_phased(self.table, s, self.xi, self.omega[:, s:s + N], self.params,
-                                     warm=warm, out=self.bufs[s % 2], lambda_out=True, stream=main,
-                                     begin=True)
-        self.bufs[s % 2] = out
-        ready = torch.cuda.Event()
-        ready.record(main)
-        self.side.wait_event(ready)
-        pending, plist = out["pending"], out["pending_list"]
-        # the side stream works through the pending list with a few workgroups per kernel: a
-        # batch-sized grid there would be dispatched only as the main stream's dynamics frees the
-        # chip, and end with it
-        h.dcm_mpc_solve_phased_finish(self.xi, self.params, out, warm=warm, lambda_out=True, stream=self.side)
-        h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=self.side, rows=plist)
-        h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T, self.dT,
-                                        contacts=self.contacts, stream=self.side, rows=plist)
-        h.posture_reference(self.law, self.com, out["vrp"], q_ref=self.q_ref, stream=main, mask=pending, want=0)
-        h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T, self.dT,
-                                        contacts=self.contacts, stream=main, mask=pending, want=0)
-        done = torch.cuda.Event()
-        done.record(self.side)
-        main.wait_event(done)
-        self.prev = out
-        self.s = s + 1
-        return out
-
 
 def split_groups(h, model, plan, states, groups, horizon=100, **kw):
     """The robots of (plan, states) in `groups` contiguous groups, each a ClosedLoop on its own

@@ -20,7 +20,6 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 
 # every symbol include/blf/blf_c.h declares (tests/test_abi.py checks the .so exports them)
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_set_qp_launch_mode",
-            "blf_set_qp_split_batch", "blf_stream_create_cu_range", "blf_stream_destroy",
             "blf_step_schedule",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
             "blf_hull2d_contains", "blf_hull3d_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
@@ -29,9 +28,12 @@ EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_s
             "blf_dcm_mpc_flops_per_iter",
             "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
             "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate",
-            "blf_fb_dcm", "blf_dcm_posture_reference", "blf_fbd_euler_integrate_impedance",
-            "blf_dcm_mpc_solve_phased_begin", "blf_dcm_mpc_solve_phased_finish",
-            "blf_dcm_posture_reference_masked", "blf_fbd_euler_integrate_impedance_masked"]
+            "blf_fb_dcm", "blf_dcm_posture_reference", "blf_fbd_euler_integrate_impedance"]
+# entry points removed in round 5 (measured slower, never the default; tests/test_abi.py checks
+# that the library no longer exports them)
+REMOVED = ["blf_set_qp_split_batch", "blf_stream_create_cu_range", "blf_stream_destroy",
+           "blf_dcm_mpc_solve_phased_begin", "blf_dcm_mpc_solve_phased_finish",
+           "blf_dcm_posture_reference_masked", "blf_fbd_euler_integrate_impedance_masked"]
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -165,11 +167,6 @@ def lib():
                                                ctypes.POINTER(DcmMpcWarmStart), _i64,
                                                ctypes.POINTER(DcmMpcWindow),
                                                ctypes.POINTER(DcmMpcSolution), _vp, _vp]
-        L.blf_dcm_mpc_solve_phased_begin.argtypes = L.blf_dcm_mpc_solve_phased.argtypes[:-1] + [_vp, _vp, _vp]
-        L.blf_dcm_mpc_solve_phased_finish.argtypes = [_vp, ctypes.POINTER(DcmMpcParams), _vp,
-                                                      ctypes.POINTER(DcmMpcWarmStart), _i64,
-                                                      ctypes.POINTER(DcmMpcWindow),
-                                                      ctypes.POINTER(DcmMpcSolution), _vp, _vp, _vp]
         L.blf_dcm_mpc_flops_per_iter.argtypes = [_i32, _i64]
         L.blf_contact_model_eval.argtypes = [_vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                              _vp, _vp]
@@ -191,15 +188,8 @@ def lib():
         L.blf_fbd_euler_integrate_impedance.argtypes = [
             _vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), ctypes.POINTER(JointImpedance),
             ctypes.POINTER(FbContacts), _vp, _i64, _f64, _f64, _f64, _vp]
-        L.blf_dcm_posture_reference_masked.argtypes = [_vp, ctypes.POINTER(PostureLaw), _vp, _vp, _i64,
-                                                       _i64, _vp, _vp, _i32, _vp, _vp]
-        L.blf_fbd_euler_integrate_impedance_masked.argtypes = (
-            L.blf_fbd_euler_integrate_impedance.argtypes[:-1] + [_vp, _i32, _vp, _vp])
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         L.blf_set_qp_launch_mode.argtypes = [_i32, _i32]
-        L.blf_set_qp_split_batch.argtypes = [_i64, _vp]
-        L.blf_stream_create_cu_range.argtypes = [_vp, _i32, _i32, _i32, _i32, ctypes.POINTER(_vp)]
-        L.blf_stream_destroy.argtypes = [_vp]
         for name in EXPORTED:
             if name not in ("blf_create", "blf_destroy", "blf_last_error", "blf_version",
                             "blf_dcm_mpc_default_params", "blf_dcm_mpc_flops_per_iter"):
@@ -214,14 +204,6 @@ def set_qp_launch_mode(fuse_stage2=-1, single_kernel=-1):
     """blf_set_qp_launch_mode: the QP kernel routing for A/B and parity tests (-1: unchanged).
     Returns nothing; the defaults are the product's (fuse_stage2 = 1, single_kernel = 0)."""
     _check(lib().blf_set_qp_launch_mode(int(fuse_stage2), int(single_kernel)))
-
-
-def set_qp_split_batch(min_batch):
-    """blf_set_qp_split_batch: cold per-knot batches of at least min_batch QPs run the search and
-    certify kernels (0: never, < 0: unchanged).  Returns the previous setting (0: never)."""
-    prev = ctypes.c_int64(0)
-    _check(lib().blf_set_qp_split_batch(int(min_batch), ctypes.byref(prev)))
-    return prev.value
 
 
 def _check(code):
@@ -323,8 +305,6 @@ class Handle:
         self.device = device
 
     def close(self):
-        for raw in self.__dict__.pop("_cu_streams", []):
-            lib().blf_stream_destroy(raw)
         if self._h:
             lib().blf_destroy(self._h)
             self._h = _vp()
@@ -338,17 +318,6 @@ class Handle:
     @property
     def ptr(self):
         return self._h
-
-    def cu_stream(self, first_cu, num_cus, exclude=False):
-        """blf_stream_create_cu_range as a torch stream (torch.cuda.ExternalStream): kernels on CUs
-        [first_cu, first_cu + num_cus) only, or (exclude) on the others only.  The HIP stream
-        lives as long as the handle."""
-        torch = _torch()
-        raw = _vp()
-        _check(lib().blf_stream_create_cu_range(self._h, int(first_cu), int(num_cus), 1 if exclude else 0, 0,
-                                                ctypes.byref(raw)))
-        self.__dict__.setdefault("_cu_streams", []).append(raw)
-        return torch.cuda.ExternalStream(raw.value, device=torch.device("cuda", self.device))
 
     # --- ForwardEuler<LinearTimeInvariantSystem>::integrate, batched, in place on x ---
     def lti_euler_integrate(self, A, Bm, u, x, t0, t1, dT, shared=False, stream=None):
@@ -602,14 +571,12 @@ class Handle:
                           _ptr(table["phase_ref"], torch.float64, (B, P, 2), "phase_ref"))
 
     def dcm_mpc_solve_phased(self, table, start, xi_init, omega, params=None, warm=None,
-                             out=None, window=None, lambda_out=False, stream=None, begin=False):
+                             out=None, window=None, lambda_out=False, stream=None):
         """blf_dcm_mpc_solve_phased: dcm_phase_expand(table, start, params.dt, N) followed by
         dcm_mpc_solve on that window, fused (same results bit for bit, N <= 128).
         omega [B, N] or a row-strided view [B, N] of a longer [B, L] array (stride(1) == 1).
         window: scratch dict (omega, xi_ref, vrp_ref, A, b, nfacets) of the window's shapes, kept
-        in out["window"] (allocated once when absent).
-        begin=True: blf_dcm_mpc_solve_phased_begin, the active-set part alone; out["pending"] [B]
-        int32 marks the problems dcm_mpc_solve_phased_finish(...) then solves."""
+        in out["window"] (allocated once when absent)."""
         torch = _torch()
         B, N = omega.shape
         M = table["phase_b"].shape[2]
@@ -662,45 +629,7 @@ class Handle:
                 _ptr(xi_init, torch.float64, (B, 2), "xi_init"), _vp(omega.data_ptr()), ostride,
                 ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(win), ctypes.byref(so),
                 lam_ptr)
-        if begin:
-            if "pending" not in out:
-                out["pending"] = torch.empty((B,), dtype=torch.int32, device=dev)
-                out["pending_list"] = torch.empty((B + 1,), dtype=torch.int32, device=dev)
-            _check(lib().blf_dcm_mpc_solve_phased_begin(
-                *args, _ptr(out["pending"], torch.int32, (B,), "pending"),
-                _ptr(out["pending_list"], torch.int32, (B + 1,), "pending_list"), _stream(stream)))
-        else:
-            _check(lib().blf_dcm_mpc_solve_phased(*args, _stream(stream)))
-        return out
-
-    def dcm_mpc_solve_phased_finish(self, xi_init, params, out, warm=None, lambda_out=False, stream=None):
-        """blf_dcm_mpc_solve_phased_finish: the interior point kernel on the problems a
-        dcm_mpc_solve_phased(..., begin=True) call left pending, with that call's xi_init, params,
-        warm and out (its window scratch and outputs)."""
-        torch = _torch()
-        B, N1 = out["xi"].shape[0], out["xi"].shape[1]
-        N, M = N1 - 1, params.max_facets
-        window = out["window"]
-        win = DcmMpcWindow(_ptr(window["omega"], torch.float64, (B, N), "window omega"),
-                           _ptr(window["xi_ref"], torch.float64, (B, N + 1, 2), "window xi_ref"),
-                           _ptr(window["vrp_ref"], torch.float64, (B, N, 2), "window vrp_ref"),
-                           _ptr(window["A"], torch.float64, (B, N, M, 2), "window A"),
-                           _ptr(window["b"], torch.float64, (B, N, M), "window b"),
-                           _ptr(window["nfacets"], torch.int32, (B, N), "window nfacets"))
-        so = DcmMpcSolution(
-            _ptr(out["xi"], torch.float64, (B, N + 1, 2), "xi"),
-            _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
-            _ptr(out["status"], torch.int32, (B,), "status"),
-            _ptr(out["iters"], torch.int32, (B,), "iters"),
-            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
-        ws = _warm_start(warm, B, N, M) if warm is not None else None
-        lam_ptr = _ptr(out["lam"], torch.float64, (B, N, M), "lam") if lambda_out else None
-        self._keep_finish = (so, ws, win)
-        lst = out.get("pending_list")
-        _check(lib().blf_dcm_mpc_solve_phased_finish(
-            self._h, ctypes.byref(params), _ptr(xi_init, torch.float64, (B, 2), "xi_init"),
-            ctypes.byref(ws) if ws is not None else None, B, ctypes.byref(win), ctypes.byref(so), lam_ptr,
-            _ptr(lst, torch.int32, (B + 1,), "pending_list") if lst is not None else None, _stream(stream)))
+        _check(lib().blf_dcm_mpc_solve_phased(*args, _stream(stream)))
         return out
 
     # --- C3 pipeline: corner sets -> polygons (device hull) -> QP arrays ---
@@ -910,11 +839,9 @@ class Handle:
         law.c = c
         return law
 
-    def posture_reference(self, law, com, vrp, q_ref=None, stream=None, mask=None, want=1, rows=None):
+    def posture_reference(self, law, com, vrp, q_ref=None, stream=None):
         """blf_dcm_posture_reference: joint references [B,n] from the plan's first VRP (vrp
-        [B,N,2], a blf_dcm_mpc_solve output) and the centre of mass com [B,6] (fb_dcm).
-        mask [B] int32 (device): only the rows with (mask != 0) == want; rows [B+1] int32
-        (device, count then indices): only those (blf_..._masked)."""
+        [B,N,2], a blf_dcm_mpc_solve output) and the centre of mass com [B,6] (fb_dcm)."""
         torch = _torch()
         B, N = vrp.shape[0], vrp.shape[1]
         n = law.c.ndof
@@ -923,12 +850,7 @@ class Handle:
         args = (self._h, ctypes.byref(law.c), _ptr(com, torch.float64, (B, 6), "com"),
                 _ptr(vrp, torch.float64, (B, N, 2), "vrp"), 2 * N, B,
                 _ptr(q_ref, torch.float64, (B, n), "q_ref"))
-        if mask is None and rows is None:
-            _check(lib().blf_dcm_posture_reference(*args, _stream(stream)))
-        else:
-            _check(lib().blf_dcm_posture_reference_masked(
-                *args, _ptr(mask, torch.int32, (B,), "mask") if mask is not None else None, int(want),
-                _ptr(rows, torch.int32, (B + 1,), "rows") if rows is not None else None, _stream(stream)))
+        _check(lib().blf_dcm_posture_reference(*args, _stream(stream)))
         return q_ref
 
     def joint_impedance(self, kp, kd):
@@ -939,11 +861,9 @@ class Handle:
         return dict(kp=f64(kp), kd=f64(kd))
 
     def fbd_euler_integrate_impedance(self, dm, state, impedance, q_ref, t0, t1, dT, contacts=None,
-                                      mass_reg=None, stream=None, mask=None, want=1, rows=None):
+                                      mass_reg=None, stream=None):
         """blf_fbd_euler_integrate_impedance in place on `state`: the control input of every
-        Euler step is tau = kp (q_ref - q) - kd qdot (impedance: joint_impedance()).
-        mask [B] int32 (device): only the systems with (mask != 0) == want; rows [B+1] int32
-        (device, count then indices): only those (blf_..._masked)."""
+        Euler step is tau = kp (q_ref - q) - kd qdot (impedance: joint_impedance())."""
         torch = _torch()
         B, n = state["joint_pos"].shape
         NV = n + 6
@@ -955,10 +875,5 @@ class Handle:
         imp.q_ref = _ptr(q_ref, torch.float64, (B, n), "q_ref")
         args = (self._h, ctypes.byref(dm.c), ctypes.byref(self._fb_state(state, B, n)), ctypes.byref(imp),
                 ctypes.byref(self._fb_contacts(contacts, B)), reg, B, float(t0), float(t1), float(dT))
-        if mask is None and rows is None:
-            _check(lib().blf_fbd_euler_integrate_impedance(*args, _stream(stream)))
-        else:
-            _check(lib().blf_fbd_euler_integrate_impedance_masked(
-                *args, _ptr(mask, torch.int32, (B,), "mask") if mask is not None else None, int(want),
-                _ptr(rows, torch.int32, (B + 1,), "rows") if rows is not None else None, _stream(stream)))
+        _check(lib().blf_fbd_euler_integrate_impedance(*args, _stream(stream)))
         return state

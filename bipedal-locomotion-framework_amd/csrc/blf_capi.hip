@@ -1,5 +1,6 @@
 // blf_capi.hip — the extern "C" boundary declared in include/blf/blf_c.h: argument validation,
 // the reference's error semantics, and dispatch to the kernels' launchers.
+#include <algorithm>
 #include <cmath>
 #include <math.h>
 #include <stdarg.h>
@@ -14,17 +15,14 @@ static thread_local char g_err[512] = "no error";
 
 QpLaunchMode& qp_launch_mode()
 {
-    static QpLaunchMode mode = [] {
-        const char* fz = getenv("BLF_QP_FUSE_STAGE2");
-        const char* sk = getenv("BLF_QP_SINGLE_KERNEL");
-        const char* sp = getenv("BLF_QP_SPLIT_MIN_BATCH");
-        int64_t split = kSplitMinBatchDefault;
-        if (sp && sp[0]) {
-            const long long v = atoll(sp);
-            split = v <= 0 ? INT64_MAX : (int64_t)v;
-        }
-        return QpLaunchMode{!(fz && fz[0] == '0'), sk && sk[0] == '1', split};
-    }();
+    static QpLaunchMode mode{{[] {
+                                 const char* fz = getenv("BLF_QP_FUSE_STAGE2");
+                                 return !(fz && fz[0] == '0') ? 1 : 0;
+                             }()},
+                             {[] {
+                                 const char* sk = getenv("BLF_QP_SINGLE_KERNEL");
+                                 return (sk && sk[0] == '1') ? 1 : 0;
+                             }()}};
     return mode;
 }
 
@@ -41,6 +39,38 @@ blf_status check_hip(hipError_t e, const char* what)
 {
     if (e == hipSuccess) return BLF_OK;
     return set_error(BLF_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+Handle::~Handle()
+{
+    for (auto& kv : lists) (void)hipFree(kv.second.buf);   // (hipFree waits for the device)
+}
+
+blf_status Handle::stage2_list(hipStream_t s, int64_t batch, Stage2List* out)
+{
+    std::lock_guard<std::mutex> lock(mu);
+    List& l = lists[s];
+    if (l.cap < batch) {
+        // the old list may still be read by the stream's last solve: let it finish first
+        blf_status st = check_hip(hipStreamSynchronize(s), "stage-2 list: hipStreamSynchronize");
+        if (st != BLF_OK) return st;
+        if (l.buf) (void)hipFree(l.buf);
+        l.buf = nullptr;
+        l.cap = 0;
+        const int64_t cap = std::max<int64_t>(batch, 4096);
+        st = check_hip(hipMalloc(&l.buf, sizeof(int32_t) * (size_t)(cap + 2)), "stage-2 list: hipMalloc");
+        if (st != BLF_OK) return st;
+        st = check_hip(hipMemset(l.buf, 0, sizeof(int32_t) * 2), "stage-2 list: hipMemset");
+        if (st != BLF_OK) {
+            (void)hipFree(l.buf);
+            l.buf = nullptr;
+            return st;
+        }
+        l.cap = cap;
+        l.slot = 0;
+    }
+    *out = Stage2List{l.buf, &l.slot};
+    return BLF_OK;
 }
 
 }  // namespace blf
@@ -110,39 +140,6 @@ blf_status blf_destroy(blf_handle* handle)
     return BLF_OK;
 }
 
-blf_status blf_stream_create_cu_range(blf_handle* handle, int32_t first_cu, int32_t num_cus, int32_t exclude,
-                                      int32_t priority, void** stream)
-{
-    BLF_REQUIRE(handle != nullptr && stream != nullptr, "blf_stream_create_cu_range: null argument");
-    const int ncu = handle->h.num_cus;
-    BLF_REQUIRE(ncu > 0, "blf_stream_create_cu_range: the device's CU count is unknown");
-    BLF_REQUIRE(first_cu >= 0 && num_cus >= 1 && first_cu + num_cus <= ncu && (exclude == 0 || exclude == 1) &&
-                    !(exclude && num_cus == ncu),
-                "blf_stream_create_cu_range: CUs [%d, %d) of %d (exclude %d)", first_cu, first_cu + num_cus, ncu,
-                exclude);
-    BLF_REQUIRE(priority == 0 || priority == -1, "blf_stream_create_cu_range: priority 0 or -1");
-    const int words = (ncu + 31) / 32;
-    uint32_t mask[64] = {};
-    BLF_REQUIRE(words <= 64, "blf_stream_create_cu_range: %d CUs", ncu);
-    for (int c = 0; c < ncu; ++c) {
-        const bool in = c >= first_cu && c < first_cu + num_cus;
-        if (in != (exclude != 0)) mask[c / 32] |= 1u << (c % 32);
-    }
-    blf_status st = check_hip(hipSetDevice(handle->h.device), "hipSetDevice");
-    if (st != BLF_OK) return st;
-    hipStream_t s = nullptr;
-    st = check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask), "hipExtStreamCreateWithCUMask");
-    if (st != BLF_OK) return st;
-    (void)priority;   // (a CU-masked stream takes the default priority; the masks keep the streams apart)
-    *stream = s;
-    return BLF_OK;
-}
-
-blf_status blf_stream_destroy(void* stream)
-{
-    return check_hip(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
-}
-
 const char* blf_last_error(void) { return g_err; }
 
 blf_status blf_step_schedule(double initial_time, double final_time, double dT, int32_t* iterations,
@@ -172,16 +169,8 @@ blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel)
     BLF_REQUIRE(fuse_stage2 >= -1 && fuse_stage2 <= 1 && single_kernel >= -1 && single_kernel <= 1,
                 "blf_set_qp_launch_mode: settings are -1, 0 or 1");
     QpLaunchMode& m = qp_launch_mode();
-    if (fuse_stage2 >= 0) m.fuse_stage2 = fuse_stage2;
-    if (single_kernel >= 0) m.single_kernel = single_kernel;
-    return BLF_OK;
-}
-
-blf_status blf_set_qp_split_batch(int64_t min_batch, int64_t* previous)
-{
-    QpLaunchMode& m = qp_launch_mode();
-    if (previous) *previous = m.split_min_batch == INT64_MAX ? 0 : m.split_min_batch;
-    if (min_batch >= 0) m.split_min_batch = min_batch == 0 ? INT64_MAX : min_batch;
+    if (fuse_stage2 >= 0) m.fuse_stage2.store(fuse_stage2, std::memory_order_relaxed);
+    if (single_kernel >= 0) m.single_kernel.store(single_kernel, std::memory_order_relaxed);
     return BLF_OK;
 }
 
@@ -349,6 +338,21 @@ blf_status blf_dcm_phase_expand(blf_handle* handle, const blf_phase_table* ph,
                                batch, A, b, nfacets, xi_ref, vrp_ref, (hipStream_t)stream);
 }
 
+// The warm-start argument checks of every QP entry point.
+static blf_status check_warm(const char* fn, const blf_dcm_mpc_warm_start* warm, int64_t batch,
+                             const blf_dcm_mpc_solution* solution, const double* lambda_out)
+{
+    if (!warm) return BLF_OK;
+    BLF_REQUIRE(batch == 0 || (warm->vrp && warm->lambda), "%s: null warm-start buffer", fn);
+    BLF_REQUIRE(warm->shift >= 0, "%s: shift %d < 0", fn, warm->shift);
+    BLF_REQUIRE(warm->reserved == 0, "%s: reserved must be 0", fn);
+    BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor), "%s: floor must be finite and > 0", fn);
+    BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out &&
+                    (warm->prev_status == nullptr || warm->prev_status != solution->status),
+                "%s: warm-start buffers must not alias the outputs", fn);
+    return BLF_OK;
+}
+
 blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* params,
                                   const blf_dcm_mpc_problem* problem,
                                   const blf_dcm_mpc_warm_start* warm, int64_t batch,
@@ -371,21 +375,18 @@ blf_status blf_dcm_mpc_solve_warm(blf_handle* handle, const blf_dcm_mpc_params* 
                                problem->vrp_ref && problem->A && problem->b && problem->nfacets &&
                                solution->xi && solution->vrp && solution->status && solution->iters),
                 "blf_dcm_mpc_solve: null buffer");
-    if (warm) {
-        BLF_REQUIRE(batch == 0 || (warm->vrp && warm->lambda),
-                    "blf_dcm_mpc_solve_warm: null warm-start buffer");
-        BLF_REQUIRE(warm->shift >= 0, "blf_dcm_mpc_solve_warm: shift %d < 0", warm->shift);
-        BLF_REQUIRE(warm->reserved == 0, "blf_dcm_mpc_solve_warm: reserved must be 0");
-        BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
-                    "blf_dcm_mpc_solve_warm: floor must be finite and > 0");
-        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out &&
-                        (warm->prev_status == nullptr || warm->prev_status != solution->status),
-                    "blf_dcm_mpc_solve_warm: warm-start buffers must not alias the outputs");
+    {
+        const blf_status st = check_warm("blf_dcm_mpc_solve_warm", warm, batch, solution, lambda_out);
+        if (st != BLF_OK) return st;
     }
-    return launch_dcm_mpc(params, problem, warm, batch, solution, lambda_out, (hipStream_t)stream);
+    if (batch == 0) return BLF_OK;
+    Stage2List list{};
+    const blf_status st = handle->h.stage2_list((hipStream_t)stream, batch, &list);
+    if (st != BLF_OK) return st;
+    return launch_dcm_mpc(params, problem, warm, batch, solution, lambda_out, (hipStream_t)stream, list);
 }
 
-static blf_status phased_solve(const char* fn, int part, int32_t* pending, int32_t* list, blf_handle* handle,
+static blf_status phased_solve(const char* fn, blf_handle* handle,
                                const blf_dcm_mpc_params* params, const blf_phase_table* ph, int64_t start_knot,
                                const double* xi_init, const double* omega, int64_t omega_stride,
                                const blf_dcm_mpc_warm_start* warm, int64_t batch,
@@ -425,19 +426,13 @@ static blf_status phased_solve(const char* fn, int part, int32_t* pending, int32
     BLF_REQUIRE(batch == 0 || (pb.xi_init && pb.omega && solution->xi && solution->vrp &&
                                solution->status && solution->iters),
                 "%s: null buffer", fn);
-    if (warm) {
-        BLF_REQUIRE(batch == 0 || (warm->vrp && warm->lambda),
-                    "%s: null warm-start buffer", fn);
-        BLF_REQUIRE(warm->shift >= 0, "%s: shift %d < 0", fn, warm->shift);
-        BLF_REQUIRE(warm->reserved == 0, "%s: reserved must be 0", fn);
-        BLF_REQUIRE(warm->floor > 0 && std::isfinite(warm->floor),
-                    "%s: floor must be finite and > 0", fn);
-        BLF_REQUIRE(warm->vrp != solution->vrp && warm->lambda != lambda_out &&
-                        (warm->prev_status == nullptr || warm->prev_status != solution->status),
-                    "%s: warm-start buffers must not alias the outputs", fn);
-    }
+    blf_status st = check_warm(fn, warm, batch, solution, lambda_out);
+    if (st != BLF_OK || batch == 0) return st;
+    Stage2List list{};
+    st = handle->h.stage2_list((hipStream_t)stream, batch, &list);
+    if (st != BLF_OK) return st;
     return launch_dcm_mpc_phased(params, ph, start_knot, xi_init, omega, omega_stride, warm, batch,
-                                 win, solution, lambda_out, (hipStream_t)stream, part, pending, list);
+                                 win, solution, lambda_out, (hipStream_t)stream, list);
 }
 
 blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params* params,
@@ -448,42 +443,8 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
                                     const blf_dcm_mpc_solution* solution, double* lambda_out,
                                     void* stream)
 {
-    return phased_solve("blf_dcm_mpc_solve_phased", 0, nullptr, nullptr, handle, params, ph, start_knot, xi_init, omega,
+    return phased_solve("blf_dcm_mpc_solve_phased", handle, params, ph, start_knot, xi_init, omega,
                         omega_stride, warm, batch, win, solution, lambda_out, stream);
-}
-
-blf_status blf_dcm_mpc_solve_phased_begin(blf_handle* handle, const blf_dcm_mpc_params* params,
-                                          const blf_phase_table* ph, int64_t start_knot,
-                                          const double* xi_init, const double* omega,
-                                          int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
-                                          int64_t batch, const blf_dcm_mpc_window* win,
-                                          const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                          int32_t* pending, int32_t* pending_list, void* stream)
-{
-    BLF_REQUIRE(batch == 0 || pending != nullptr, "blf_dcm_mpc_solve_phased_begin: null pending buffer");
-    return phased_solve("blf_dcm_mpc_solve_phased_begin", 1, pending, pending_list, handle, params, ph, start_knot, xi_init,
-                        omega, omega_stride, warm, batch, win, solution, lambda_out, stream);
-}
-
-blf_status blf_dcm_mpc_solve_phased_finish(blf_handle* handle, const blf_dcm_mpc_params* params,
-                                           const double* xi_init, const blf_dcm_mpc_warm_start* warm,
-                                           int64_t batch, const blf_dcm_mpc_window* win,
-                                           const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                           const int32_t* pending_list, void* stream)
-{
-    BLF_REQUIRE(handle != nullptr, "blf_dcm_mpc_solve_phased_finish: null handle");
-    BLF_REQUIRE(params && win && solution, "blf_dcm_mpc_solve_phased_finish: null argument");
-    BLF_REQUIRE(batch >= 0, "blf_dcm_mpc_solve_phased_finish: negative batch");
-    BLF_REQUIRE(params->max_facets >= 1 && params->max_facets <= kMaxFacetsWide && params->horizon >= 1 &&
-                    params->horizon <= 128 && params->tol_polish > 0,
-                "blf_dcm_mpc_solve_phased_finish: params unlike a phase-indexed solve's");
-    BLF_REQUIRE(batch == 0 || (xi_init && win->omega && win->xi_ref && win->vrp_ref && win->A && win->b &&
-                               win->nfacets && solution->xi && solution->vrp && solution->status &&
-                               solution->iters),
-                "blf_dcm_mpc_solve_phased_finish: null buffer");
-    return launch_dcm_mpc_phased(params, nullptr, 0, xi_init, nullptr, params->horizon, warm, batch, win,
-                                 solution, lambda_out, (hipStream_t)stream, 2, nullptr,
-                                 const_cast<int32_t*>(pending_list));
 }
 
 blf_status blf_dcm_mpc_solve(blf_handle* handle, const blf_dcm_mpc_params* params,
@@ -653,20 +614,6 @@ blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* 
     return launch_posture_reference(law, com, vrp, vrp_stride, batch, q_ref, (hipStream_t)stream);
 }
 
-blf_status blf_dcm_posture_reference_masked(blf_handle* handle, const blf_posture_law* law,
-                                            const double* com, const double* vrp, int64_t vrp_stride,
-                                            int64_t batch, double* q_ref, const int32_t* mask, int32_t want,
-                                            const int32_t* list, void* stream)
-{
-    BLF_REQUIRE(batch == 0 || mask != nullptr || list != nullptr, "blf_dcm_posture_reference_masked: null mask");
-    BLF_REQUIRE(want == 0 || want == 1, "blf_dcm_posture_reference_masked: want must be 0 or 1");
-    const blf_status st = blf_dcm_posture_reference(handle, law, com, vrp, vrp_stride, 0, q_ref, stream);
-    if (st != BLF_OK) return st;   // the argument checks (batch 0: nothing launched)
-    BLF_REQUIRE(batch >= 0 && vrp_stride >= 2, "blf_dcm_posture_reference_masked: bad batch / vrp stride");
-    BLF_REQUIRE(batch == 0 || (com && vrp && q_ref), "blf_dcm_posture_reference_masked: null buffer");
-    return launch_posture_reference(law, com, vrp, vrp_stride, batch, q_ref, (hipStream_t)stream, mask, want, list);
-}
-
 blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_model* model,
                                              const blf_fb_state* state,
                                              const blf_joint_impedance* impedance,
@@ -692,36 +639,6 @@ blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_mo
     if (st != BLF_OK) return st;
     return launch_fbd_euler(model, state, nullptr, contacts, mass_reg, batch, iterations, dT,
                             dT_last, (hipStream_t)stream, impedance);
-}
-
-blf_status blf_fbd_euler_integrate_impedance_masked(blf_handle* handle, const blf_fb_model* model,
-                                                    const blf_fb_state* state,
-                                                    const blf_joint_impedance* impedance,
-                                                    const blf_fb_contacts* contacts,
-                                                    const double* mass_reg, int64_t batch,
-                                                    double initial_time, double final_time, double dT,
-                                                    const int32_t* mask, int32_t want, const int32_t* list,
-                                                    void* stream)
-{
-    BLF_REQUIRE(batch == 0 || mask != nullptr || list != nullptr,
-                "blf_fbd_euler_integrate_impedance_masked: null mask");
-    BLF_REQUIRE(want == 0 || want == 1, "blf_fbd_euler_integrate_impedance_masked: want must be 0 or 1");
-    BLF_REQUIRE(impedance != nullptr, "blf_fbd_euler_integrate_impedance_masked: null impedance");
-    BLF_REQUIRE(impedance->reserved == 0, "blf_fbd_euler_integrate_impedance_masked: reserved must be 0");
-    BLF_REQUIRE(impedance->kp && impedance->kd && (batch == 0 || impedance->q_ref),
-                "blf_fbd_euler_integrate_impedance_masked: null impedance array");
-    BLF_REQUIRE(model != nullptr && impedance->ndof == model->ndof,
-                "blf_fbd_euler_integrate_impedance_masked: impedance ndof %d != model ndof %d",
-                impedance->ndof, model ? model->ndof : -1);
-    blf_status st = check_fbd("blf_fbd_euler_integrate_impedance_masked", handle, model, state,
-                              impedance->kp, contacts, batch);
-    if (st != BLF_OK) return st;
-    int iterations = 0;
-    double dT_last = 0.0;
-    st = step_schedule(initial_time, final_time, dT, &iterations, &dT_last);
-    if (st != BLF_OK) return st;
-    return launch_fbd_euler(model, state, nullptr, contacts, mass_reg, batch, iterations, dT,
-                            dT_last, (hipStream_t)stream, impedance, mask, want, list);
 }
 
 blf_status blf_fbd_euler_integrate(blf_handle* handle, const blf_fb_model* model,

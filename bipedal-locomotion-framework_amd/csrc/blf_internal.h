@@ -7,6 +7,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <mutex>
+#include <unordered_map>
+
 #include "blf/blf_c.h"
 
 namespace blf {
@@ -14,16 +18,34 @@ namespace blf {
 constexpr int kWave = 64;   // CDNA wavefront width
 constexpr int kMaxFacets = 8;       // facet slots per knot of the active-set kernels (and the default)
 constexpr int kMaxFacetsWide = 16;  // max_facets up to this: the interior point kernel alone
-// grid of a kernel that loops over a pending list (stage 2, the closed loop's side stream)
-constexpr int kListGrid = 64;
+// grid of the QP's stage 2, which loops over the pending list (one workgroup per CU)
+constexpr int kListGrid = 256;
 
 // ---- error plumbing (blf_capi.hip) ----
 blf_status set_error(blf_status code, const char* fmt, ...);
 blf_status check_hip(hipError_t e, const char* what);
 
+// A stream's stage-2 work list (Handle::stage2_list; dcm_mpc_ipm.hip)
+struct Stage2List {
+    int32_t* buf;
+    int* slot;
+};
+
 struct Handle {
     int device = 0;
     int num_cus = 0;
+    // The QP's stage-2 work list of each stream the handle solves on (dcm_mpc_ipm.hip): device
+    // int32 [0], [1] two count slots, [2..] the QPs; grown (after a sync of the stream) when a
+    // batch outgrows it.  `slot`: the count slot the stream's next solve appends to (0 there).
+    struct List {
+        int32_t* buf = nullptr;
+        int64_t cap = 0;   // QPs it holds
+        int slot = 0;
+    };
+    std::mutex mu;
+    std::unordered_map<hipStream_t, List> lists;
+    ~Handle();
+    blf_status stage2_list(hipStream_t s, int64_t batch, Stage2List* out);
 };
 
 // ---- launchers (one per kernel file) ----
@@ -57,25 +79,25 @@ blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* 
                                int64_t start_knot, double dt, int32_t N, int64_t batch, double* A,
                                double* b, int32_t* nfacets, double* xi_ref, double* vrp_ref,
                                hipStream_t s);
-// The QP kernel routing (blf_set_qp_launch_mode); initialised once from the environment.
+// The QP kernel routing (blf_set_qp_launch_mode): process-wide, not per handle; initialised once
+// from the environment, read on every solve (relaxed atomics: a setting applies to the solves
+// enqueued after it).
 struct QpLaunchMode {
-    int fuse_stage2;     // 1 (default): stage 2 inside the small-batch active-set kernel
-    int single_kernel;   // 0 (default): active-set kernel first
-    int64_t split_min_batch;   // cold per-knot batches from this size: search + certify kernels
+    std::atomic<int> fuse_stage2;     // 1 (default): stage 2 inside the small-batch active-set kernel
+    std::atomic<int> single_kernel;   // 0 (default): active-set kernel first
 };
 QpLaunchMode& qp_launch_mode();
-// the split is bit-identical but measured slower at 4096 / 16 384 / 65 536 QPs:
-// off unless blf_set_qp_split_batch / BLF_QP_SPLIT_MIN_BATCH asks for it
-constexpr int64_t kSplitMinBatchDefault = INT64_MAX;
+// l: the stream's stage-2 work list (Handle::stage2_list)
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
                           const blf_dcm_mpc_warm_start* warm, int64_t batch,
-                          const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s);
+                          const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s,
+                          const Stage2List& l);
 blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_table* ph,
                                  int64_t start_knot, const double* xi_init, const double* omega,
                                  int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                  int64_t batch, const blf_dcm_mpc_window* win,
                                  const blf_dcm_mpc_solution* sol, double* lambda_out, hipStream_t s,
-                                 int part = 0, int32_t* pending = nullptr, int32_t* list = nullptr);
+                                 const Stage2List& l);
 
 blf_status launch_contact_eval(const double* prm, int shared, const double* twist,
                                const double* pose, const double* null_pose, int64_t batch,
@@ -94,14 +116,12 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s,
-                            const blf_joint_impedance* impedance = nullptr, const int32_t* mask = nullptr,
-                            int want = 1, const int32_t* list = nullptr);
+                            const blf_joint_impedance* impedance = nullptr);
 size_t fbd_lds_bytes(int n, int C);
 blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const double* omega0,
                          int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s);
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
-                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s,
-                                    const int32_t* mask = nullptr, int want = 1, const int32_t* list = nullptr);
+                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s);
 blf_status launch_fbk_euler(int n, double rho, double* pos, double* rot, double* joints,
                             const double* twist, const double* joint_vel, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s);

@@ -113,10 +113,6 @@ struct LdsRows<float> {
 };
 
 // BLF_AS_MINWAVES: the fused cold kernel's __launch_bounds__ waves per SIMD (A/B builds);
-// BLF_AS_SEARCH_WAVES: the split search kernel's (dcm_mpc_search_kernel).
-#ifndef BLF_AS_SEARCH_WAVES
-#define BLF_AS_SEARCH_WAVES 4
-#endif
 #ifndef BLF_AS_MINWAVES
 #define BLF_AS_MINWAVES 2
 #endif
@@ -1117,7 +1113,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
                                                  bool certified, int status, int64_t p, int N, int M, int lane,
                                                  double xi00, double xi01, double* xi_out, double* vrp_out,
                                                  int32_t* status_out, int32_t* iters_out, int32_t* polished_out,
-                                                 double* lam_out)
+                                                 double* lam_out, int32_t* list, int list_slot)
 {
     const bool done = certified || status != 0;
 #pragma unroll
@@ -1147,6 +1143,10 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
         if (done) {
             iters_out[p] = 0;
             if (polished_out) polished_out[p] = certified ? 1 : 0;
+        } else if (list != nullptr) {
+            // stage 2's work list: its kernel loops over the listed QPs only, so a batch with none
+            // pending costs one tiny launch (order is irrelevant: each QP is solved on its own)
+            list[2 + atomicAdd(&list[list_slot], 1)] = (int32_t)p;
         }
     }
 }
@@ -1159,13 +1159,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
 // when none certifies, the fp64 LQ optimum from (xi_ref, vrp_ref) becomes the IPM's start point.
 // The cold solve of one QP (the cold kernel's body; the warm kernel runs it for the problems whose
 // previous solve failed, blf_dcm_mpc_warm_start.prev_status).
-// SPLIT (large batches): 0 both phases in one kernel; 1 phase A alone (float rows
-// in LDS, rounded as they are staged: the same floats phase A reads in the fused kernel), its
-// hand-over state parked in the caller's output arrays (per knot the float VRP and DCM as four
-// floats in the VRP slot, the candidate set in the DCM slot; per QP whether it certified, in the
-// status slot); 2 phase B alone from that state.  Split or fused, the same operations on the same
-// values: the same bits.
-template <int KPL, bool LAMOUT, bool PH, int TR, int SPLIT = 0>
+template <int KPL, bool LAMOUT, bool PH, int TR>
 __device__ __forceinline__ void cold_solve(
     const KParams& P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1174,7 +1168,6 @@ __device__ __forceinline__ void cold_solve(
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
     double* __restrict__ lam_out, const PhaseSrc& ps)
 {
-    static_assert(!(PH && SPLIT), "the split path serves the per-knot input");
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
     assume_pad<KPL, TR>(N);
@@ -1200,7 +1193,7 @@ __device__ __forceinline__ void cold_solve(
     // (The phase-indexed input keeps its gathers before the LQ step: issued after the knot loads
     // and committed after the step like the slab loads, it measured 1 % slower on the c3 pipeline,
     // 1.900 / 1.893 against 1.882 / 1.874 ms per step, profiles/r03_ph_overlap_ab.log.)
-    constexpr bool kOverlap = !PH && BLF_AS_OVERLAP && SPLIT == 0;
+    constexpr bool kOverlap = !PH && BLF_AS_OVERLAP;
     double2 va[U];
     double vb[U];
     if (PH) {
@@ -1209,42 +1202,16 @@ __device__ __forceinline__ void cold_solve(
     } else if (kOverlap) {
         // issued below, after the knot loads: a wait for those (vmcnt counts in issue order) then
         // leaves the younger row loads in flight
-    } else if (SPLIT == 1) {
-        for (int t0 = 0; t0 < nA; t0 += 4 * kWave)
-            stage_rows<KPL, 4, float>(Ain, bin, p, N, M, S, NH, lane, t0, nA, reinterpret_cast<float*>(smem),
-                                      reinterpret_cast<float*>(smem) + 2 * (size_t)M * S);
     } else {
         stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, 0, nA, A2d, Bv);
     }
-    using RowT = typename std::conditional<SPLIT == 1, float, double>::type;
-    const LdsRows<RowT> R{reinterpret_cast<const typename LdsRows<RowT>::V2*>(smem),
-                          reinterpret_cast<const RowT*>(smem) + 2 * (size_t)M * S, S, NH};
+    const LdsRows<double> R{reinterpret_cast<const typename LdsRows<double>::V2*>(smem),
+                            smem + 2 * (size_t)M * S, S, NH};
 
     AKnotT<float> F[KPL];
     int cand[KPL];         // the float search's next candidate sets (phase B's guess when uncertified)
     bool cert32 = false;   // the float search certified its point
     const double xi00 = xi_init[2 * p], xi01 = xi_init[2 * p + 1];
-    float* const fst = reinterpret_cast<float*>(vrp_out);   // SPLIT: [B][N] x 4 floats (r0 r1 x0 x1)
-    int32_t* const cst = reinterpret_cast<int32_t*>(xi_out);   // SPLIT: [B][N + 1] x 4 ints, slot 0
-    if constexpr (SPLIT == 2) {
-        // ---- phase A's hand-over state, parked by dcm_mpc_search_kernel ----
-#pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-            const int k = KPL * lane + j;
-            F[j].r0 = F[j].r1 = F[j].x0 = F[j].x1 = 0.0f;
-            cand[j] = 0;
-            if (k < N) {
-                const int64_t st = p * N + k, sx = p * (N + 1) + (k + 1);
-                F[j].r0 = fst[4 * st];
-                F[j].r1 = fst[4 * st + 1];
-                F[j].x0 = fst[4 * st + 2];
-                F[j].x1 = fst[4 * st + 3];
-                cand[j] = cst[4 * sx];
-            }
-        }
-        cert32 = status_out[p] != 0;
-        __syncthreads();   // the LDS rows (one wavefront: a wait for the stores)
-    } else {
     // ---- phase A: the float search (facet counts clamped; a bad count is reported below) ----
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
@@ -1291,24 +1258,7 @@ __device__ __forceinline__ void cold_solve(
     }
 #pragma unroll
     for (int j = 0; j < KPL; ++j) cand[j] = as_cand(F[j]);
-    }
 
-    if constexpr (SPLIT == 1) {
-#pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-            const int k = KPL * lane + j;
-            if (k < N) {
-                const int64_t st = p * N + k, sx = p * (N + 1) + (k + 1);
-                fst[4 * st] = F[j].r0;
-                fst[4 * st + 1] = F[j].r1;
-                fst[4 * st + 2] = F[j].x0;
-                fst[4 * st + 3] = F[j].x1;
-                cst[4 * sx] = cand[j];
-            }
-        }
-        if (lane == 0) status_out[p] = cert32 ? 1 : 0;
-        return;
-    }
     // ---- phase B: the fp64 passes from the float point ----
     AS_STAMP(t_b);
     const PT<double> Pd = params_d(P);
@@ -1388,7 +1338,7 @@ __device__ __forceinline__ void cold_solve(
     }
     AS_STAMP_ADD(14, t_b);
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
-                                  status_out, iters_out, polished_out, lam_out);
+                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot);
     if (PH && !certified && status == 0) ph_write_window<KPL>(ps, sPh, omega, A2d, Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(0, t_start);
 #ifdef BLF_STAMPS
@@ -1412,35 +1362,6 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
 {
     cold_solve<KPL, LAMOUT, PH, TR>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
                                      status_out, iters_out, polished_out, lam_out, ps);
-}
-
-// The large-batch split of the cold kernel: phase A alone at BLF_AS_SEARCH_WAVES
-// waves per SIMD (float rows: 9.6 KB of LDS per QP at N = 100), then phase B alone at 2 (fp64
-// rows).  The search is most of a cold solve's instructions and is issue- and latency-bound at two
-// waves per SIMD; phase B re-reads the rows from HBM.  Bit-identical to the fused kernel.
-template <int KPL, int TR>
-__global__ __launch_bounds__(kWave, BLF_AS_SEARCH_WAVES) void dcm_mpc_search_kernel(
-    KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
-    const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
-    const double* __restrict__ Ain, const double* __restrict__ bin,
-    const int32_t* __restrict__ nfacets, double* __restrict__ xi_out, double* __restrict__ vrp_out,
-    int32_t* __restrict__ status_out)
-{
-    cold_solve<KPL, false, false, TR, 1>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
-                                         status_out, nullptr, nullptr, nullptr, PhaseSrc{});
-}
-
-template <int KPL, bool LAMOUT, int TR>
-__global__ __launch_bounds__(kWave, 2) void dcm_mpc_certify_kernel(
-    KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
-    const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
-    const double* __restrict__ Ain, const double* __restrict__ bin,
-    const int32_t* __restrict__ nfacets, double* __restrict__ xi_out, double* __restrict__ vrp_out,
-    int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
-    double* __restrict__ lam_out)
-{
-    cold_solve<KPL, LAMOUT, false, TR, 2>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
-                                          status_out, iters_out, polished_out, lam_out, PhaseSrc{});
 }
 
 // Small batches, N <= 64 (configs[0], one TimeVaryingDCMPlanner solve): the QP the active-set
@@ -1623,7 +1544,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     AS_STAMP(t_out);
 
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
-                                  status_out, iters_out, polished_out, lam_out);
+                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot);
     if (PH && !certified && status == 0)
         ph_write_window<KPL>(ps, sPh, omega, reinterpret_cast<const double*>(A2), Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(11, t_out);
@@ -1665,31 +1586,17 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     constexpr int kAltTree = KPL == 2 ? kTreePad : kTreeDpp;   // the instantiated trees: this, kTreeKS
     const int tr = (KPL == 1 && batch <= kDppTreeMaxBatch) ? kTreeDpp
                    : (KPL == 2 && kp.N <= 2 * kWave - 2) ? kTreePad : kTreeKS;
-    if (KPL == 1 && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch && qp_launch_mode().fuse_stage2) {
+    if (KPL == 1 && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch &&
+        qp_launch_mode().fuse_stage2.load(std::memory_order_relaxed)) {
         const size_t lds_f = std::max(lds, sizeof(double) * Lds(nullptr, kp.N, kp.M, 1).total);
         auto kern = lam_out ? dcm_mpc_cold_fused_kernel<true> : dcm_mpc_cold_fused_kernel<false>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds_f, s, kp,
+        KParams kf = kp;
+        kf.list = nullptr;   // its own stage 2 follows in the workgroup: nothing to list
+        hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(kWave), lds_f, s, kf,
                            pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, sol->xi,
                            sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
         *stage2_done = true;
         return check_hip(hipGetLastError(), "dcm_mpc_cold_fused_kernel launch");
-    }
-    if (warm == nullptr && ps == nullptr && batch >= qp_launch_mode().split_min_batch) {
-        // the large-batch split: phase A, then phase B, on the same stream
-        auto ks = tr == kAltTree ? dcm_mpc_search_kernel<KPL, kAltTree> : dcm_mpc_search_kernel<KPL, kTreeKS>;
-        hipLaunchKernelGGL(ks, dim3((unsigned)batch), dim3(kWave), 3 * sizeof(float) * slots, s, kp,
-                           pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, sol->xi,
-                           sol->vrp, sol->status);
-        blf_status st = check_hip(hipGetLastError(), "dcm_mpc_search_kernel launch");
-        if (st != BLF_OK) return st;
-#define AS_CERT(L, D) dcm_mpc_certify_kernel<KPL, L, D>
-        auto kc = tr == kAltTree ? (lam_out ? AS_CERT(true, kAltTree) : AS_CERT(false, kAltTree))
-                                 : (lam_out ? AS_CERT(true, kTreeKS) : AS_CERT(false, kTreeKS));
-#undef AS_CERT
-        hipLaunchKernelGGL(kc, dim3((unsigned)batch), dim3(kWave), lds, s, kp,
-                           pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets, sol->xi,
-                           sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
-        return check_hip(hipGetLastError(), "dcm_mpc_certify_kernel launch");
     }
     if (warm == nullptr) {
 #define AS_COLD(L, H, D) dcm_mpc_cold_kernel<KPL, L, H, D>

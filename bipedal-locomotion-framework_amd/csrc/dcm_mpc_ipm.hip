@@ -39,17 +39,47 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     double* __restrict__ vrp_out, int32_t* __restrict__ status_out,
     int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out)
 {
-    // one problem per workgroup, or stage 2 over the pending list: a grid of a few workgroups,
-    // each taking every gridDim-th listed problem (the whole batch's grid would have to be
-    // dispatched beside whatever else holds the chip -- the closed loop's dynamics -- before the
-    // launch could end).  One call site of the solve either way.
-    const bool lst = P.list != nullptr;
-    const int count = lst ? P.list[0] : (int)blockIdx.x + 1;
-    for (int i = lst ? (int)blockIdx.x : (int)blockIdx.x; i < count; i += lst ? (int)gridDim.x : count) {
-        const int64_t p = lst ? P.list[1 + i] : (int64_t)blockIdx.x;
-        ipm_solve<NT, WARM, LAMOUT, MF>(P, p, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, ws_vrp,
+    ipm_solve<NT, WARM, LAMOUT, MF>(P, blockIdx.x, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, ws_vrp,
                                     ws_lam, xi_out, vrp_out, status_out, iters_out, polished_out, lam_out);
-        if (lst) __syncthreads();   // the LDS is the next problem's
+}
+
+// Stage 2 over the pending list the active-set kernel appended to (KParams::list): a grid of a
+// few workgroups, each taking every gridDim-th listed problem.  The solve is an out-of-line call
+// that reads the kernel's arguments itself, so a workgroup that finds nothing listed -- every
+// workgroup of a batch the active-set kernel certified whole -- loads the count and leaves without
+// touching scratch (the batch-sized grid of the inlined kernel stored 12.5 KB of register spills
+// per QP on its way to the status check, round 4).  Workgroup 0 zeroes the other count slot, the
+// one the stream's next solve appends to.
+struct IpmArgs {
+    KParams P;
+    const double *xi_init, *omega, *xi_ref, *vrp_ref, *Ain, *bin;
+    const int32_t* nfacets;
+    const double *ws_vrp, *ws_lam;
+    double *xi_out, *vrp_out;
+    int32_t *status_out, *iters_out, *polished_out;
+    double* lam_out;
+};
+
+template <int NT, bool WARM, bool LAMOUT, int MF>
+__device__ __noinline__ void ipm_solve_listed(int64_t p)
+{
+#ifdef __HIP_DEVICE_COMPILE__   // (the kernarg segment exists in the device pass only)
+    const IpmArgs& A = *reinterpret_cast<const IpmArgs*>(__builtin_amdgcn_kernarg_segment_ptr());
+    ipm_solve<NT, WARM, LAMOUT, MF>(A.P, p, A.xi_init, A.omega, A.xi_ref, A.vrp_ref, A.Ain, A.bin, A.nfacets,
+                                    A.ws_vrp, A.ws_lam, A.xi_out, A.vrp_out, A.status_out, A.iters_out,
+                                    A.polished_out, A.lam_out);
+#endif
+}
+
+template <int NT, bool WARM, bool LAMOUT, int MF>
+__global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_ipm_list_kernel(IpmArgs A)
+{
+    const int32_t* idx = A.P.list + 2;
+    const int count = __builtin_amdgcn_readfirstlane(A.P.list[A.P.list_slot]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.P.list[A.P.list_slot ^ 1] = 0;
+    for (int i = (int)blockIdx.x; i < count; i += (int)gridDim.x) {
+        ipm_solve_listed<NT, WARM, LAMOUT, MF>(__builtin_amdgcn_readfirstlane(idx[i]));
+        __syncthreads();   // the LDS is the next problem's
     }
 }
 
@@ -64,15 +94,27 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
     if (lds > 160 * 1024)
         return set_error(BLF_ERR_UNSUPPORTED, "horizon %d with %d facet slots needs %zu B of LDS",
                          kp.N, kp.M, lds);
-    auto kern = (warm != nullptr)
-                    ? (lam_out ? dcm_mpc_ipm_kernel<NT, true, true, MF> : dcm_mpc_ipm_kernel<NT, true, false, MF>)
-                    : (lam_out ? dcm_mpc_ipm_kernel<NT, false, true, MF> : dcm_mpc_ipm_kernel<NT, false, false, MF>);
-    // a pending list: at most kListGrid workgroups loop over it
-    const unsigned grid = kp.list ? (unsigned)std::min<int64_t>(batch, kListGrid) : (unsigned)batch;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, s, kp,
+#define IPM_KERN(K) ((warm != nullptr) ? (lam_out ? K<NT, true, true, MF> : K<NT, true, false, MF>) \
+                                       : (lam_out ? K<NT, false, true, MF> : K<NT, false, false, MF>))
+    if (kp.list) {
+        // stage 2 runs only after the active-set kernels (N <= 128, at most kMaxFacets facet
+        // slots); at most kListGrid workgroups loop over the pending list
+        if constexpr (NT <= 2 * kWave && MF == kMaxFacets) {
+            const IpmArgs a{kp, pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets,
+                            warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr, sol->xi, sol->vrp,
+                            sol->status, sol->iters, sol->polished, lam_out};
+            hipLaunchKernelGGL(IPM_KERN(dcm_mpc_ipm_list_kernel), dim3((unsigned)std::min<int64_t>(batch, kListGrid)),
+                               dim3(NT), lds, s, a);
+            return check_hip(hipGetLastError(), "dcm_mpc_ipm_list_kernel launch");
+        } else {
+            return set_error(BLF_ERR_UNSUPPORTED, "stage 2 with %d threads, %d facet slots", NT, MF);
+        }
+    }
+    hipLaunchKernelGGL(IPM_KERN(dcm_mpc_ipm_kernel), dim3((unsigned)batch), dim3(NT), lds, s, kp,
                        pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                        pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr,
                        sol->xi, sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
+#undef IPM_KERN
     return check_hip(hipGetLastError(), "dcm_mpc_ipm_kernel launch");
 }
 
@@ -112,6 +154,7 @@ KParams make_kparams(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_warm_start
     kp.ws_status = warm ? warm->prev_status : nullptr;
     kp.stage2 = 0;
     kp.list = nullptr;
+    kp.list_slot = 0;
     kp.f_dt = (float)kp.dt;
     kp.f_Qw0 = (float)kp.Qw0; kp.f_Qw1 = (float)kp.Qw1;
     kp.f_Rw0 = (float)kp.Rw0; kp.f_Rw1 = (float)kp.Rw1;
@@ -140,37 +183,46 @@ blf_status launch_ipm(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     return set_error(BLF_ERR_UNSUPPORTED, "horizon %d > 1024", N);
 }
 
-// pending[p] = 1 for the QPs the active-set kernel handed to stage 2 (status kPending), else 0;
-// list (optional, list[0] zeroed before): their indices appended after the count, in no
-// particular order (each problem is solved on its own, so the order changes no result)
-__global__ __launch_bounds__(256) void pending_mask_kernel(const int32_t* __restrict__ status, int64_t batch,
-                                                           int32_t* __restrict__ pending, int32_t* __restrict__ list)
-{
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= batch) return;
-    const bool pend = status[p] == kPending;
-    pending[p] = pend ? 1 : 0;
-    if (list && pend) list[1 + atomicAdd(&list[0], 1)] = (int32_t)p;
-}
 }  // namespace
+
+// The QPs the active-set kernel hands over go to stage 2 through the stream's pending list
+// (Handle::stage2_list: [0], [1] two count slots, [2..] the QPs).  The active-set kernel appends
+// to slot *slot, which is 0 when it starts; the IPM kernel's list instantiation loops over what it
+// finds there with kListGrid workgroups and zeroes the other slot, and *slot flips to that one
+// for the stream's next solve.
+static void set_pend(KParams& kp, const Stage2List& l)
+{
+    kp.list = l.buf;
+    kp.list_slot = *l.slot;
+}
+static void set_stage2(KParams& kp, const Stage2List& l)
+{
+    kp.stage2 = 1;
+    kp.list = l.buf;
+    kp.list_slot = *l.slot;
+    *l.slot ^= 1;
+}
 
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
                           const blf_dcm_mpc_warm_start* warm, int64_t batch,
-                          const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s)
+                          const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
+                          const Stage2List& l)
 {
     KParams kp = make_kparams(prm, warm);
     if (batch == 0) return BLF_OK;
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     const int N = kp.N;
     // With the active-set start (tol_polish > 0) and N <= 128, the one-wavefront active-set kernel
-    // solves the QPs its start certifies; this kernel then takes only the rest (stage 2), from
-    // scratch and without the start.  BLF_QP_SINGLE_KERNEL=1 keeps everything in this kernel
+    // solves the QPs its start certifies; the IPM kernel then takes only the rest (stage 2), from
+    // scratch and without the start.  BLF_QP_SINGLE_KERNEL=1 keeps everything in the IPM kernel
     // (A/B and parity tests: both ways give the same bits).
-    if (kp.tol_polish > 0.0 && N <= 2 * kWave && kp.M <= kMaxFacets && !qp_launch_mode().single_kernel) {
+    if (kp.tol_polish > 0.0 && N <= 2 * kWave && kp.M <= kMaxFacets && !qp_launch_mode().single_kernel.load(std::memory_order_relaxed)) {
         bool stage2_done = false;
+        set_pend(kp, l);
         const blf_status st = launch_dcm_mpc_as(kp, pb, warm, batch, sol, lam_out, s, nullptr, &stage2_done);
+        kp.list = nullptr;
         if (st != BLF_OK || stage2_done) return st;
-        kp.stage2 = 1;
+        set_stage2(kp, l);
     }
     return launch_ipm(kp, pb, warm, batch, sol, lam_out, s);
 }
@@ -178,34 +230,15 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
 // blf_dcm_mpc_solve_phased: the active-set kernels read the window from the phase table (PhaseSrc);
 // the QPs they hand over (kPending) leave their expanded window in the caller's scratch, from
 // which the IPM kernel's stage 2 continues exactly as after blf_dcm_phase_expand + solve.
-// part: 0 the whole solve; 1 the active-set part alone (stage 2's QPs left at kPending, their
-// windows in the scratch, `pending` marking them); 2 stage 2 alone (blf_dcm_mpc_solve_phased_begin /
-// _finish: parts 1 then 2 on one stream are part 0).  With more than 8 facet slots there is no
-// active-set part: part 1 solves everything and marks nothing, part 2 does nothing.
 blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_table* ph,
                                  int64_t start_knot, const double* xi_init, const double* omega,
                                  int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
                                  int64_t batch, const blf_dcm_mpc_window* win,
                                  const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
-                                 int part, int32_t* pending, int32_t* list)
+                                 const Stage2List& l)
 {
     KParams kp = make_kparams(prm, warm);
     if (batch == 0) return BLF_OK;
-    if (part == 2) {
-        if (kp.M > kMaxFacets) return BLF_OK;
-        kp.stage2 = 1;
-        kp.list = list;
-        const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
-        return launch_ipm(kp, &pw, warm, batch, sol, lam_out, s);
-    }
-    if (pending && (kp.M > kMaxFacets || part == 0)) {
-        blf_status st = check_hip(hipMemsetAsync(pending, 0, sizeof(int32_t) * (size_t)batch, s), "pending mask");
-        if (st != BLF_OK) return st;
-    }
-    if (list) {   // the count; the kernel below (or nothing, M > 8) appends
-        blf_status st = check_hip(hipMemsetAsync(list, 0, sizeof(int32_t), s), "pending list");
-        if (st != BLF_OK) return st;
-    }
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     if (kp.N > 2 * kWave || !(kp.tol_polish > 0.0))
         return set_error(BLF_ERR_UNSUPPORTED,
@@ -224,7 +257,7 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
                        "phase-indexed solve: omega copy");
         if (st != BLF_OK) return st;
         const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
-        return launch_dcm_mpc(prm, &pw, warm, batch, sol, lam_out, s);
+        return launch_dcm_mpc(prm, &pw, warm, batch, sol, lam_out, s, l);
     }
     PhaseSrc ps{};
     ps.P = ph->max_phases;
@@ -244,15 +277,11 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
     ps.wb = win->b;
     ps.wnf = win->nfacets;
     const blf_dcm_mpc_problem pin{xi_init, omega, nullptr, nullptr, nullptr, nullptr, nullptr};
+    set_pend(kp, l);
     const blf_status st = launch_dcm_mpc_as(kp, &pin, warm, batch, sol, lam_out, s, &ps);
+    kp.list = nullptr;
     if (st != BLF_OK) return st;
-    if (part == 1) {
-        if (!pending) return BLF_OK;
-        hipLaunchKernelGGL(pending_mask_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256), 0, s,
-                           sol->status, batch, pending, list);
-        return check_hip(hipGetLastError(), "pending_mask_kernel launch");
-    }
-    kp.stage2 = 1;
+    set_stage2(kp, l);
     const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
     return launch_ipm(kp, &pw, warm, batch, sol, lam_out, s);
 }

@@ -782,7 +782,9 @@ __device__ __forceinline__ bool sat_start(KN& K, const KParams& P, const Lds& L,
 }
 
 #ifndef BLF_MIN_WAVES
-#define BLF_MIN_WAVES 3   // waves per SIMD the register allocation must allow (<= 168 VGPRs)
+// waves per SIMD the register allocation must allow: 2 (<= 256 VGPRs).  At 3 (<= 168) the polish
+// and the saturated start spill 89-118 VGPRs and ~210 B of scratch per lane (round 4).
+#define BLF_MIN_WAVES 2
 #endif
 // The solve of QP p by one workgroup of NT threads (the kernel below; the active-set kernel's
 // fused stage 2 for N <= 64, dcm_mpc_as.hip, calls it from its own 64-thread workgroup).

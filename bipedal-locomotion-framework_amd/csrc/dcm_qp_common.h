@@ -21,8 +21,10 @@ struct KParams {
     double ws_floor;     // warm start: s, lambda >= ws_floor
     int stage2;          // IPM kernel after the active-set kernel: only QPs with status kPending,
                          // and no active-set start (it already failed for them)
-    const int32_t* list; // stage 2 over a list (blf_dcm_mpc_solve_phased_finish): [0] = count,
-                         // [1..count] = the pending problems; a small grid loops over it
+    int32_t* list;       // the pending list of stage 2 (or nullptr): [list_slot] = count, [2..] =
+                         // the problems the active-set kernel handed over.  The active-set
+                         // kernels append to it; stage 2's small grid loops over it.
+    int list_slot;       // 0 or 1
     // The active-set kernel's fp32 search (cold starts): the parameters rounded to float, and the
     // search's own certificate tolerances (kSearchTolP / kSearchTolD)
     float f_dt, f_Qw0, f_Qw1, f_Rw0, f_Rw1, f_Pw0, f_Pw1, f_tol_p, f_tol_d;

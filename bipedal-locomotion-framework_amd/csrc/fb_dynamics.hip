@@ -1324,14 +1324,6 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
 struct Impedance {
     const double *kp, *kd, *qref;
 };
-// A subset of the batch (blf_fbd_euler_integrate_impedance_masked): system q runs iff
-// (mask[q] != 0) == want; mask == nullptr: every system.
-struct Select {
-    const int32_t* mask;
-    int want;
-    const int32_t* list;   // or: [0] = count, [1..count] = the systems (mask and want unused)
-    __device__ __forceinline__ bool has(int64_t q) const { return !mask || ((mask[q] != 0) == (want != 0)); }
-};
 
 // NFIX > 0: a model of exactly NFIX joints (the launcher checks): the joint count is a compile-time
 // constant, so every `< n` / `< NV` bound of the unrolled loops folds away instead of living in
@@ -1344,7 +1336,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
                                                           const double* __restrict__ tau,
                                                           Contacts ct, const double* reg,
                                                           int32_t nsteps, double dT, double dT_last,
-                                                          Impedance imp, int64_t batch, Select sel)
+                                                          Impedance imp, int64_t batch)
 {
     if constexpr (NFIX > 0) m.n = NFIX;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1389,21 +1381,14 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
         }
     }
     constexpr int per = kWave / HW;   // systems per wavefront
-    // the systems: the batch (q = blockIdx.x * per + half), or a list (sel.list: a grid of a few
-    // wavefronts loops over the listed systems, per at a time)
-    const bool lst = sel.list != nullptr;
-    const int64_t nitems = lst ? (int64_t)sel.list[0] : batch;
-    const int64_t g_end = lst ? (nitems + per - 1) / per : (int64_t)blockIdx.x + 1;
     const Topo T = build_topo<HW>(m, S);
     double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n | dR 9
     double* dR = loc + 18 + 2 * n;
-    for (int64_t g = blockIdx.x; g < g_end; g += lst ? (int64_t)gridDim.x : g_end) {
-    const int64_t i0 = g * per + H.half;
-    // a system outside the batch, the list or the selection is computed (as the other half's
-    // partner) and written nowhere; a wavefront with no selected system skips the group
-    const bool active = lst ? i0 < nitems : (i0 < batch && sel.has(i0));   // see fbd_dynamics_kernel
-    if (__ballot(active) == 0ull) continue;
-    const int64_t q = lst ? (int64_t)sel.list[1 + (i0 < nitems ? i0 : nitems - 1)] : (i0 < batch ? i0 : batch - 1);
+    const int64_t i0 = (int64_t)blockIdx.x * per + H.half;
+    // a system past the end of an odd batch is computed (as the last system's copy, beside its
+    // partner) and written nowhere
+    const bool active = i0 < batch;   // see fbd_dynamics_kernel
+    const int64_t q = active ? i0 : batch - 1;
     for (int i = lane; i < 18 + 2 * n; i += HW) {
         double v;
         if (i < 6) v = st.base_vel[6 * q + i];
@@ -1471,8 +1456,6 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
             else if (i < 18 + n) st.base_rot[9 * q + (i - 9 - n)] = v;
             else st.joint_pos[(int64_t)n * q + (i - 18 - n)] = v;
         }
-    }
-    wave_sync();   // the next group's loads overwrite the state
     }
 }
 
@@ -1545,23 +1528,11 @@ __global__ __launch_bounds__(256) void posture_reference_kernel(int n, const dou
                                                                 const double* __restrict__ com,
                                                                 const double* __restrict__ vrp,
                                                                 int64_t vstride, int64_t total,
-                                                                double* __restrict__ qref, Select sel)
+                                                                double* __restrict__ qref)
 {
-    if (sel.list) {   // the listed systems' rows, a few workgroups looping over them
-        const int64_t tl = (int64_t)sel.list[0] * n;
-        for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tl; t += (int64_t)gridDim.x * blockDim.x) {
-            const int64_t q = sel.list[1 + t / n];
-            const int j = (int)(t % n);
-            const double ex = vrp[q * vstride] - com[6 * q];
-            const double ey = vrp[q * vstride + 1] - com[6 * q + 1];
-            qref[q * n + j] = (qnom[j] + lean[2 * j] * ex) + lean[2 * j + 1] * ey;
-        }
-        return;
-    }
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     const int64_t q = e / n;
-    if (!sel.has(q)) return;
     const int j = (int)(e - q * n);
     const double ex = vrp[q * vstride] - com[6 * q];
     const double ey = vrp[q * vstride + 1] - com[6 * q + 1];
@@ -1628,15 +1599,10 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s,
-                            const blf_joint_impedance* impedance, const int32_t* mask, int want,
-                            const int32_t* list)
+                            const blf_joint_impedance* impedance)
 {
     if (batch == 0) return BLF_OK;
-    const Select sel{mask, want, list};
-    // a list: at most kListGrid wavefronts loop over it (the grid the batch would need is dispatched
-    // only as the other stream's dynamics frees the chip, wavefront by wavefront)
-    const int64_t wv2 = list ? std::min<int64_t>(ceil_div(batch, 2), kListGrid) : ceil_div(batch, 2);
-    const int64_t wv1 = list ? std::min<int64_t>(batch, kListGrid) : batch;
+    const int64_t wv2 = ceil_div(batch, 2), wv1 = batch;
     const size_t mb32 = BLF_FBD_LDSMODEL ? sizeof(double) * fbd_model_block<32>() : 0;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
@@ -1653,20 +1619,20 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>
                                 : fbd_euler_kernel<32, 32, false, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>),
                            dim3((unsigned)wv2), dim3(kWave), 2 * lds + mb32, s, to_model(md), *st, tau, c,
-                           reg, nsteps, dT, dT_last, imp, batch, sel);
+                           reg, nsteps, dT, dT_last, imp, batch);
     else if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true> : fbd_euler_kernel<32, 32, false>),
                            dim3((unsigned)wv2), dim3(kWave), 2 * lds + mb32, s, to_model(md), *st, tau, c,
-                           reg, nsteps, dT, dT_last, imp, batch, sel);
+                           reg, nsteps, dT, dT_last, imp, batch);
     else if (md->ndof + 6 <= 32)   // one system per wavefront, NV <= 32 rows
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, kWave, true> : fbd_euler_kernel<32, kWave, false>),
                            dim3((unsigned)wv1), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
-                           dT_last, imp, batch, sel);
+                           dT_last, imp, batch);
     else
         hipLaunchKernelGGL((pri ? fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, true>
                                 : fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, false>),
                            dim3((unsigned)wv1), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
-                           dT_last, imp, batch, sel);
+                           dT_last, imp, batch);
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
 }
 
@@ -1682,14 +1648,12 @@ blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const d
 }
 
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
-                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s,
-                                    const int32_t* mask, int want, const int32_t* list)
+                                    int64_t vstride, int64_t batch, double* qref, hipStream_t s)
 {
     const int64_t total = batch * law->ndof;
     if (total == 0) return BLF_OK;
-    const int64_t grid = list ? std::min<int64_t>((total + 255) / 256, 4) : (total + 255) / 256;
-    hipLaunchKernelGGL(posture_reference_kernel, dim3((unsigned)grid), dim3(256), 0, s,
-                       law->ndof, law->q_nominal, law->lean, com, vrp, vstride, total, qref, Select{mask, want, list});
+    hipLaunchKernelGGL(posture_reference_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s,
+                       law->ndof, law->q_nominal, law->lean, com, vrp, vstride, total, qref);
     return check_hip(hipGetLastError(), "posture_reference_kernel launch");
 }
 

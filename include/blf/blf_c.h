@@ -76,17 +76,13 @@ typedef int32_t blf_status;
 
 typedef struct blf_handle blf_handle;
 
-/* Create a handle bound to HIP device `device`.  Fails with BLF_ERR_HIP if no device. */
+/* Create a handle bound to HIP device `device`.  Fails with BLF_ERR_HIP if no device.  A handle
+ * keeps, per stream it solves QPs on, a small device work list (the problems the active-set
+ * kernel hands to the interior point kernel; allocated at the first solve on the stream and grown,
+ * after a synchronisation of that stream, when a batch outgrows it).  Solves on one handle and one
+ * stream must be enqueued from one host thread at a time. */
 blf_status blf_create(blf_handle** handle, int32_t device);
 blf_status blf_destroy(blf_handle* handle);
-/* A HIP stream whose kernels run only on CUs [first_cu, first_cu + num_cus) of the handle's
- * device (exclude = 0), or only on the others (exclude = 1) (hipExtStreamCreateWithCUMask).  Two
- * such streams with complementary ranges keep a small side computation (the closed loop's
- * interior point problems) from waiting behind a kernel that fills the chip.  priority: 0 (reserved:
- * -1 is accepted and treated as 0).  Release with blf_stream_destroy. */
-blf_status blf_stream_create_cu_range(blf_handle* handle, int32_t first_cu, int32_t num_cus,
-                                      int32_t exclude, int32_t priority, void** stream);
-blf_status blf_stream_destroy(void* stream);
 /* Human-readable description of the last error on this thread (never NULL). */
 const char* blf_last_error(void);
 /* Version string of the library (build id). */
@@ -95,15 +91,9 @@ const char* blf_version(void);
  * product's).  fuse_stage2 = 0: small cold batches with N <= 64 run the IPM's stage 2 as its own
  * launch instead of inside the active-set kernel; single_kernel = 1: every QP runs in the
  * interior point kernel alone (no active-set kernel).  -1 leaves a setting unchanged.  The initial
- * values come from BLF_QP_FUSE_STAGE2 / BLF_QP_SINGLE_KERNEL, read once at the first solve. */
+ * values come from BLF_QP_FUSE_STAGE2 / BLF_QP_SINGLE_KERNEL, read once at the first solve.  The
+ * setting is process-wide (every handle and thread), not per handle. */
 blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel);
-/* Cold solves of the per-knot input (blf_dcm_mpc_solve without warm start) with N <= 128 and at
- * least min_batch QPs run the active-set search and its fp64 certification as two kernels (more
- * resident search wavefronts; the same bits as the one-kernel path).  min_batch 0: never; < 0:
- * unchanged.  *previous (optional) receives the setting before the call (0: never).  Initial value
- * from BLF_QP_SPLIT_MIN_BATCH, else never (the split measured slower). */
-blf_status blf_set_qp_split_batch(int64_t min_batch, int64_t* previous);
-
 /* ---- 0. FixedStepIntegrator::integrate's step schedule (FixedStepIntegrator.tpp:21-72) -------
  * The validation (in the reference's order) and schedule every batched integrator below uses:
  * iterations = (int)ceil((T - t0) / dT); steps i = 0..iterations-2 run at currentTime = t0 + dT*i
@@ -348,29 +338,6 @@ blf_status blf_dcm_mpc_solve_phased(blf_handle* handle, const blf_dcm_mpc_params
                                     int64_t batch, const blf_dcm_mpc_window* window,
                                     const blf_dcm_mpc_solution* solution, double* lambda_out,
                                     void* stream);
-/* blf_dcm_mpc_solve_phased in two calls, so that a caller can go on with the problems solved by
- * the active-set kernel while the interior point kernel finishes the rest on another stream.
- * _begin: the active-set kernel (every argument as for blf_dcm_mpc_solve_phased); the problems it
- * hands over get status -1 and pending[q] = 1 (others 0), their windows expanded into `window`;
- * pending_list (optional, [B + 1]): [0] = their count, [1..count] = their indices (in no
- * particular order).  _finish: the interior point kernel on those, with the same params, xi_init,
- * warm, window, solution and lambda_out as the _begin call; given the pending_list, a small grid
- * loops over the listed problems instead of one workgroup per problem of the batch.  _begin then _finish on one stream give the same bits
- * as blf_dcm_mpc_solve_phased.  With max_facets > 8 (no active-set kernel) _begin solves every
- * problem and marks none, and _finish does nothing. */
-blf_status blf_dcm_mpc_solve_phased_begin(blf_handle* handle, const blf_dcm_mpc_params* params,
-                                          const blf_phase_table* phases, int64_t start_knot,
-                                          const double* xi_init, const double* omega,
-                                          int64_t omega_stride, const blf_dcm_mpc_warm_start* warm,
-                                          int64_t batch, const blf_dcm_mpc_window* window,
-                                          const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                          int32_t* pending, int32_t* pending_list, void* stream);
-blf_status blf_dcm_mpc_solve_phased_finish(blf_handle* handle, const blf_dcm_mpc_params* params,
-                                           const double* xi_init, const blf_dcm_mpc_warm_start* warm,
-                                           int64_t batch, const blf_dcm_mpc_window* window,
-                                           const blf_dcm_mpc_solution* solution, double* lambda_out,
-                                           const int32_t* pending_list, void* stream);
-
 /* ---- 6. Contact model (ContinuousContactModel), batched ------------------------------------
  * Rectangular L x W patch, spring k, damper b (ContinuousContactModel.h:22-57).
  * params: [B][4] = {length, width, spring_coeff, damper_coeff} (or one shared [4] when
@@ -511,14 +478,6 @@ typedef struct blf_posture_law {
 blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* law,
                                      const double* com, const double* vrp, int64_t vrp_stride,
                                      int64_t batch, double* q_ref, void* stream);
-/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1), or, when list is not NULL,
- * for the systems list[1..list[0]] (a device array, e.g. blf_dcm_mpc_solve_phased_begin's
- * pending_list; mask and want unused); the other rows of q_ref are not written. */
-blf_status blf_dcm_posture_reference_masked(blf_handle* handle, const blf_posture_law* law,
-                                            const double* com, const double* vrp, int64_t vrp_stride,
-                                            int64_t batch, double* q_ref, const int32_t* mask,
-                                            int32_t want, const int32_t* list, void* stream);
-
 /* blf_fbd_euler_integrate_impedance: ForwardEuler<FloatingBaseDynamicalSystem>::integrate(t0, T)
  * (the schedule of blf_fbd_euler_integrate) with the control input set before EVERY step from a
  * joint impedance, tau = kp (q_ref - q) - kd qdot at the step's start state: the reference loop
@@ -538,19 +497,6 @@ blf_status blf_fbd_euler_integrate_impedance(blf_handle* handle, const blf_fb_mo
                                              const double* mass_reg, int64_t batch,
                                              double initial_time, double final_time, double dT,
                                              void* stream);
-/* The same for the systems q with (mask[q] != 0) == want (want 0 or 1), or, when list is not NULL,
- * for the systems list[1..list[0]] (a few wavefronts loop over them; mask and want unused); the
- * others' state is not written.  A closed loop integrates the systems whose plan is ready while
- * the rest wait for theirs (blf_dcm_mpc_solve_phased_begin / _finish). */
-blf_status blf_fbd_euler_integrate_impedance_masked(blf_handle* handle, const blf_fb_model* model,
-                                                    const blf_fb_state* state,
-                                                    const blf_joint_impedance* impedance,
-                                                    const blf_fb_contacts* contacts,
-                                                    const double* mass_reg, int64_t batch,
-                                                    double initial_time, double final_time, double dT,
-                                                    const int32_t* mask, int32_t want, const int32_t* list,
-                                                    void* stream);
-
 /* Algorithmic flop count of one IPM iteration of one problem (what the fp64 roofline field
  * of bench.py is computed from); `active_facets` = sum_k nfacets[k]. */
 double blf_dcm_mpc_flops_per_iter(int32_t horizon, int64_t active_facets);

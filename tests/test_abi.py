@@ -27,6 +27,11 @@ def test_header_declares_and_library_exports_every_symbol():
     exported = set(re.findall(r"\bT (blf_[a-z0-9_]+)$", out, flags=re.M))
     missing = set(declared) - exported
     assert not missing, missing
+    # the round-4 paths measured slower and never the default (split search / certify kernels,
+    # the closed loop's begin / finish overlap with its masked kernels and CU-ranged streams)
+    # are gone from the product
+    assert not set(native.REMOVED) & exported, set(native.REMOVED) & exported
+    assert not set(native.REMOVED) & set(declared)
 
 
 def test_library_was_built_from_this_tree():
