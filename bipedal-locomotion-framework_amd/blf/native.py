@@ -89,7 +89,8 @@ class DcmMpcProblem(ctypes.Structure):
 
 
 class DcmMpcSolution(ctypes.Structure):
-    _fields_ = [("xi", _vp), ("vrp", _vp), ("status", _vp), ("iters", _vp), ("polished", _vp)]
+    _fields_ = [("xi", _vp), ("vrp", _vp), ("status", _vp), ("iters", _vp), ("polished", _vp),
+                ("passes", _vp)]
 
 
 class PhaseTable(ctypes.Structure):
@@ -441,7 +442,8 @@ class Handle:
         vrp_ref [B,N,2], A [B,N,M,2], b [B,N,M], nfacets [B,N] (int32).
         warm: None (cold start) or dict(vrp [B,N,2], lam [B,N,M], shift, floor)
         (blf_dcm_mpc_solve_warm); lambda_out: also return the final multipliers out["lam"].
-        out["polished"] [B] says which solutions are the certified active-set polish."""
+        out["polished"] [B] says which solutions are the certified active-set polish; out["passes"]
+        [B] how many drop/add passes the active-set kernels ran for each."""
         torch = _torch()
         B, N = prob["omega"].shape
         M = prob["b"].shape[2]
@@ -454,7 +456,8 @@ class Handle:
                        vrp=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
                        status=torch.empty((B,), dtype=torch.int32, device=dev),
                        iters=torch.empty((B,), dtype=torch.int32, device=dev),
-                       polished=torch.empty((B,), dtype=torch.int32, device=dev))
+                       polished=torch.empty((B,), dtype=torch.int32, device=dev),
+                       passes=torch.empty((B,), dtype=torch.int32, device=dev))
         pb = DcmMpcProblem(
             _ptr(prob["xi_init"], torch.float64, (B, 2), "xi_init"),
             _ptr(prob["omega"], torch.float64, (B, N), "omega"),
@@ -468,7 +471,8 @@ class Handle:
             _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
             _ptr(out["status"], torch.int32, (B,), "status"),
             _ptr(out["iters"], torch.int32, (B,), "iters"),
-            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
+            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None,
+            _ptr(out["passes"], torch.int32, (B,), "passes") if "passes" in out else None)
         ws = None
         if warm is not None:
             ws = _warm_start(warm, B, N, M)
@@ -498,7 +502,8 @@ class Handle:
         M = prob["b"].shape[2]
         pb = DcmMpcProblem(*(_vp(prob[k].data_ptr()) for k in
                              ("xi_init", "omega", "xi_ref", "vrp_ref", "A", "b", "nfacets")))
-        so = DcmMpcSolution(*(_vp(out[k].data_ptr()) for k in ("xi", "vrp", "status", "iters", "polished")))
+        so = DcmMpcSolution(*(_vp(out[k].data_ptr()) if k in out else None
+                              for k in ("xi", "vrp", "status", "iters", "polished", "passes")))
         s = _stream(stream)
         fn, h, pp, ppb, pso = lib().blf_dcm_mpc_solve, self._h, ctypes.byref(params), ctypes.byref(pb), ctypes.byref(so)
         keep = (pb, so, params, prob, out, torch)
@@ -592,7 +597,8 @@ class Handle:
                        vrp=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
                        status=torch.empty((B,), dtype=torch.int32, device=dev),
                        iters=torch.empty((B,), dtype=torch.int32, device=dev),
-                       polished=torch.empty((B,), dtype=torch.int32, device=dev))
+                       polished=torch.empty((B,), dtype=torch.int32, device=dev),
+                       passes=torch.empty((B,), dtype=torch.int32, device=dev))
         if window is None:
             window = out.get("window")
         if window is None:
@@ -615,7 +621,8 @@ class Handle:
             _ptr(out["vrp"], torch.float64, (B, N, 2), "vrp"),
             _ptr(out["status"], torch.int32, (B,), "status"),
             _ptr(out["iters"], torch.int32, (B,), "iters"),
-            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None)
+            _ptr(out["polished"], torch.int32, (B,), "polished") if "polished" in out else None,
+            _ptr(out["passes"], torch.int32, (B,), "passes") if "passes" in out else None)
         ws = None
         if warm is not None:
             ws = _warm_start(warm, B, N, M)

@@ -838,13 +838,14 @@ __device__ __forceinline__ int as_cand(const AKnotT<T>& K)
 template <int KPL, int TR, class T, class RS>
 __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, const RS& R, int NH, int N,
                                           int lane, T xi00, T xi01, int (&pk)[KPL],
-                                          T (&pl)[KPL][2], int count_slot, int sb, int handover = -1)
+                                          T (&pl)[KPL][2], int count_slot, int sb, int handover, int& npass)
 {
     T xk[KPL][2];
     as_xi_prev<KPL, T>(K, lane, xi00, xi01, xk);
     bool certified = false;
     const int lane0 = lane;
-    for (int pass = 0; pass < kGuessPasses; ++pass) {
+    int pass = 0;
+    for (; pass < kGuessPasses; ++pass) {
         // BLF_AS_OPQLANE: the lane index opaque per pass, so its masks are recomputed inside the
         // pass instead of hoisted out of the loop into SGPRs (which spill)
         int lane = lane0;
@@ -929,6 +930,7 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
             if (ch <= handover) break;
         }
     }
+    npass = pass < kGuessPasses ? pass + 1 : kGuessPasses;   // the passes run (wave-uniform)
     return certified;
 }
 
@@ -1113,7 +1115,8 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
                                                  bool certified, int status, int64_t p, int N, int M, int lane,
                                                  double xi00, double xi01, double* xi_out, double* vrp_out,
                                                  int32_t* status_out, int32_t* iters_out, int32_t* polished_out,
-                                                 double* lam_out, int32_t* list, int list_slot)
+                                                 double* lam_out, int32_t* list, int list_slot,
+                                                 int32_t* passes_out, int npass)
 {
     const bool done = certified || status != 0;
 #pragma unroll
@@ -1140,6 +1143,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
         xi_out[2 * p * (N + 1)] = xi00;
         xi_out[2 * p * (N + 1) + 1] = xi01;
         status_out[p] = done ? status : kPending;
+        if (passes_out) passes_out[p] = npass;
         if (done) {
             iters_out[p] = 0;
             if (polished_out) polished_out[p] = certified ? 1 : 0;
@@ -1211,6 +1215,7 @@ __device__ __forceinline__ void cold_solve(
     AKnotT<float> F[KPL];
     int cand[KPL];         // the float search's next candidate sets (phase B's guess when uncertified)
     bool cert32 = false;   // the float search certified its point
+    int npass32 = 0;       // its passes
     const double xi00 = xi_init[2 * p], xi01 = xi_init[2 * p + 1];
     // ---- phase A: the float search (facet counts clamped; a bad count is reported below) ----
 #pragma unroll
@@ -1253,7 +1258,8 @@ __device__ __forceinline__ void cold_solve(
         AS_STAMP(t_a);
         int pkf[KPL];
         float plf[KPL][2];
-        cert32 = as_passes<KPL, TR, float>(F, Pf, R, NH, N, lane, xf00, xf01, pkf, plf, 12, 16, N / kHandoverDiv);
+        cert32 = as_passes<KPL, TR, float>(F, Pf, R, NH, N, lane, xf00, xf01, pkf, plf, 12, 16, N / kHandoverDiv,
+                                           npass32);
         AS_STAMP_ADD(13, t_a);
     }
 #pragma unroll
@@ -1295,6 +1301,7 @@ __device__ __forceinline__ void cold_solve(
         Kj.al = 1.0 + Kj.be;
     }
     int status = 0;
+    int npass = npass32;   // active-set passes run (float + fp64), blf_dcm_mpc_solution.passes
     bool certified = false;
     double pl[KPL][2];
     int pk[KPL];
@@ -1305,6 +1312,7 @@ __device__ __forceinline__ void cold_solve(
     }
     if (__ballot(bad) != 0) {
         status = BLF_QP_BAD_FACETS;   // outputs (xi_ref, vrp_ref), as the oracle
+        npass = 0;                    // (and no passes reported)
 #pragma unroll
         for (int j = 0; j < KPL; ++j) {
             K[j].r0 = K[j].rr0;
@@ -1321,7 +1329,9 @@ __device__ __forceinline__ void cold_solve(
 #pragma unroll
             for (int j = 0; j < KPL; ++j) K[j].gm = KPL * lane + j < N ? cand[j] : 0;
         }
-        certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4);
+        int npass64 = 0;
+        certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4, -1, npass64);
+        npass += npass64;
         if (!certified) {
             // ---- the IPM's start point: the fp64 LQ optimum from (xi_ref, vrp_ref) ----
 #pragma unroll
@@ -1338,7 +1348,8 @@ __device__ __forceinline__ void cold_solve(
     }
     AS_STAMP_ADD(14, t_b);
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
-                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot);
+                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot,
+                                  P.passes_out, npass);
     if (PH && !certified && status == 0) ph_write_window<KPL>(ps, sPh, omega, A2d, Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(0, t_start);
 #ifdef BLF_STAMPS
@@ -1486,6 +1497,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     const LdsRows<double> R{A2, Bv, S, NH};
 
     int status = 0;
+    int npass = 0;   // active-set passes run (float + fp64), blf_dcm_mpc_solution.passes
     bool certified = false;
     double pl[KPL][2];
     int pk[KPL];
@@ -1538,13 +1550,14 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
         as_guess<KPL, double>(K, R, NH, N, lane, lw, P.ws_floor, 0.0);
         AS_STAMP_ADD(3, t_g);
         AS_STAMP(t_b);
-        certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4);
+        certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4, -1, npass);
         AS_STAMP_ADD(14, t_b);
     }
     AS_STAMP(t_out);
 
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
-                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot);
+                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot,
+                                  P.passes_out, npass);
     if (PH && !certified && status == 0)
         ph_write_window<KPL>(ps, sPh, omega, reinterpret_cast<const double*>(A2), Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(11, t_out);

@@ -155,6 +155,7 @@ KParams make_kparams(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_warm_start
     kp.stage2 = 0;
     kp.list = nullptr;
     kp.list_slot = 0;
+    kp.passes_out = nullptr;
     kp.f_dt = (float)kp.dt;
     kp.f_Qw0 = (float)kp.Qw0; kp.f_Qw1 = (float)kp.Qw1;
     kp.f_Rw0 = (float)kp.Rw0; kp.f_Rw1 = (float)kp.Rw1;
@@ -209,6 +210,7 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
                           const Stage2List& l)
 {
     KParams kp = make_kparams(prm, warm);
+    kp.passes_out = sol->passes;
     if (batch == 0) return BLF_OK;
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     const int N = kp.N;
@@ -238,6 +240,7 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
                                  const Stage2List& l)
 {
     KParams kp = make_kparams(prm, warm);
+    kp.passes_out = sol->passes;
     if (batch == 0) return BLF_OK;
     if (batch > 0x7fffffffLL) return set_error(BLF_ERR_UNSUPPORTED, "batch %lld too large", (long long)batch);
     if (kp.N > 2 * kWave || !(kp.tol_polish > 0.0))

@@ -813,6 +813,8 @@ __device__ __forceinline__ void ipm_solve(
     const bool last = k == N - 1;
     // after the active-set kernel (dcm_mpc_as.hip): only the QPs it handed over
     if (P.stage2 && status_out[p] != kPending) return;
+    // solved here alone (no active-set kernel before): no active-set kernel passes
+    if (!P.stage2 && P.passes_out != nullptr && threadIdx.x == 0) P.passes_out[p] = 0;
     // a separate instantiation each way; in the warm one, a problem whose previous solve failed
     // (KParams::ws_status) starts cold, as the cold instantiation would start it
     const bool warm = WARM && !(P.ws_status != nullptr && P.ws_status[p] != 0);

@@ -25,6 +25,8 @@ struct KParams {
                          // the problems the active-set kernel handed over.  The active-set
                          // kernels append to it; stage 2's small grid loops over it.
     int list_slot;       // 0 or 1
+    int32_t* passes_out; // [B] or nullptr: the active-set kernels' passes per QP (float + fp64);
+                         // the IPM kernel writes 0 for the problems it solves alone
     // The active-set kernel's fp32 search (cold starts): the parameters rounded to float, and the
     // search's own certificate tolerances (kSearchTolP / kSearchTolD)
     float f_dt, f_Qw0, f_Qw1, f_Rw0, f_Rw1, f_Pw0, f_Pw1, f_tol_p, f_tol_d;

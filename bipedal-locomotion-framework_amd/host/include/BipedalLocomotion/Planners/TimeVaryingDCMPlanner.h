@@ -46,7 +46,10 @@ struct DCMPlanBatch
     std::vector<double> dcm;          /**< [batch][horizon+1][2] */
     std::vector<double> vrp;          /**< [batch][horizon][2]   */
     std::vector<int32_t> status;      /**< [batch] BLF_QP_*      */
-    std::vector<int32_t> iterations;  /**< [batch]               */
+    std::vector<int32_t> iterations;  /**< [batch] interior point iterations */
+    /** [batch] active-set passes the solve ran (blf_dcm_mpc_solution.passes): what a warm start
+     * saves over a cold one */
+    std::vector<int32_t> passes;
     /** [batch][n] each problem's QP variables in the planner's VariablesHandler layout
      * (TimeVaryingDCMPlanner::variablesHandler(): "dcm" then "vrp", n = 4 horizon + 2). */
     std::vector<double> variables;
@@ -87,7 +90,7 @@ class TimeVaryingDCMPlanner : public System::Advanceable<DCMPlanBatch>
     blf::DeviceBuffer<int32_t> m_dNPhases, m_dPhNCorners, m_dPhNf;
     blf::DeviceBuffer<double> m_dXi0, m_dOmega, m_dXiRef, m_dVrpRef, m_dA, m_dB, m_dWinOmega;
     blf::DeviceBuffer<double> m_dXi, m_dVrp[2], m_dLam[2];
-    blf::DeviceBuffer<int32_t> m_dNf, m_dIters;
+    blf::DeviceBuffer<int32_t> m_dNf, m_dIters, m_dPasses;
     blf::DeviceBuffer<int32_t> m_dStatus[2];   // ping-pong with m_dVrp / m_dLam: the previous
                                                 // window's statuses are the next warm start's
                                                 // prev_status (a failed problem restarts cold)

@@ -325,9 +325,10 @@ bool TimeVaryingDCMPlanner::advance()
     const int nxt = m_solved ? 1 - m_cur : m_cur;
     if (!m_dXi.resize(static_cast<std::size_t>(B) * (N + 1) * 2) ||
         !m_dVrp[nxt].resize(BN * 2) || !m_dLam[nxt].resize(BN * M) || !m_dStatus[nxt].resize(B) ||
-        !m_dIters.resize(B))
+        !m_dIters.resize(B) || !m_dPasses.resize(B))
         return false;
-    blf_dcm_mpc_solution sol{m_dXi.data(), m_dVrp[nxt].data(), m_dStatus[nxt].data(), m_dIters.data()};
+    blf_dcm_mpc_solution sol{m_dXi.data(), m_dVrp[nxt].data(), m_dStatus[nxt].data(), m_dIters.data(),
+                             nullptr,      m_dPasses.data()};
     // the previous window's statuses ride along: a plan whose last window was not solved is
     // planned cold this time instead of from that failed iterate
     blf_dcm_mpc_warm_start warm{m_dVrp[m_cur].data(), m_dLam[m_cur].data(), 1, 0, m_warmFloor,
@@ -381,7 +382,8 @@ void TimeVaryingDCMPlanner::download() const
     m_output.batch = B;
     m_output.horizon = m_params.horizon;
     bool ok = m_dXi.download(m_output.dcm) && m_dVrp[m_cur].download(m_output.vrp) &&
-              m_dStatus[m_cur].download(m_output.status) && m_dIters.download(m_output.iterations);
+              m_dStatus[m_cur].download(m_output.status) && m_dIters.download(m_output.iterations) &&
+              m_dPasses.download(m_output.passes);
     if (ok)
     {
         for (int b = 0; b < B; ++b) ok = ok && m_output.status[b] == BLF_QP_SOLVED;
@@ -422,5 +424,5 @@ bool TimeVaryingDCMPlanner::isValid() const
 blf_dcm_mpc_solution TimeVaryingDCMPlanner::deviceSolution()
 {
     return blf_dcm_mpc_solution{m_dXi.data(), m_dVrp[m_cur].data(), m_dStatus[m_cur].data(),
-                                m_dIters.data()};
+                                m_dIters.data(), nullptr, m_dPasses.data()};
 }

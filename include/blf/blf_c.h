@@ -234,6 +234,11 @@ typedef struct blf_dcm_mpc_solution {
     int32_t* iters;          /* [B]  IPM iterations taken                                   */
     int32_t* polished;       /* [B]  optional (NULL: not written): 1 if the solution is the
                               *      certified active-set polish, 0 if the IPM's own iterate    */
+    int32_t* passes;         /* [B]  optional (NULL: not written): the drop/add passes the
+                              *      active-set kernels ran (a cold start's fp32 search plus its
+                              *      fp64 passes; a warm start's fp64 passes), what a warm start
+                              *      saves; 0 for a problem the interior point kernel solves alone
+                              *      (horizon > 128, max_facets > 8, tol_polish = 0)             */
 } blf_dcm_mpc_solution;
 
 /* Warm start of a receding-horizon re-solve (TimeVaryingDCMPlanner::advance()):

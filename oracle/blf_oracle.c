@@ -509,6 +509,7 @@ typedef struct {
     double *sc, *sg;                       /* [N][2], [N][4] scan elements */
     double *v, *x;                         /* [N+1][2] scan results */
     double *xi, *vrp;                      /* outputs, updated in place */
+    int npass;   /* dcm_polish passes run since the solve began */
 } dcm_ws;
 
 static double keepmax(double q, double x) { return x > q ? x : q; }
@@ -1458,6 +1459,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
      * adding; the uncapturable-state windows of tests/golden/c5_hard_windows.npz need the
      * alternating moves of the active-set start there too.) */
     for (int pass = 0; pass < max_pass; ++pass) {
+    ++w->npass;
     ok = 1;
     int neg = 0, viol = 0;
     double vmax = 0.0;   /* the pass's largest violation (the IPM polish's add threshold) */
@@ -1847,14 +1849,14 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                       int32_t* iters_out)
 {
     return orc_dcm_mpc_solve_warm(prm, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, NULL,
-                                  xi, vrp, NULL, iters_out, NULL);
+                                  xi, vrp, NULL, iters_out, NULL, NULL);
 }
 
 int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, const double* omega,
                            const double* xi_ref, const double* vrp_ref, const double* Ain,
                            const double* bin, const int32_t* nfacets, const orc_dcm_warm* warm,
                            double* xi, double* vrp, double* lam_out, int32_t* iters_out,
-                           int32_t* polished_out)
+                           int32_t* polished_out, int32_t* passes_out)
 {
     const int N = prm->horizon;
     const int M = prm->max_facets;
@@ -1892,6 +1894,8 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
     w->v = p; p += 2 * (N + 1); w->x = p; p += 2 * (N + 1);
 
     int status = 0, it = 0, ntot = 0, polished = 0;
+    int as_passes = 0;   /* the active-set kernels' drop/add passes (blf_dcm_mpc_solution.passes) */
+    w->npass = 0;
     for (int k = 0; k < N; ++k) {
         if (nfacets[k] < 0 || nfacets[k] > M) status = 3;
         else ntot += nfacets[k];
@@ -1943,8 +1947,9 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         double* r32 = (double*)malloc(sizeof(double) * 4 * (size_t)N);
         double* x32 = r32 + 2 * N;
         int* g32 = (int*)malloc(sizeof(int) * (size_t)N);
+        int32_t np32 = 0;
         const int cert32 = orc_as32_search(prm, prm->sequential, xi_init, omega, xi_ref, vrp_ref, Ain,
-                                           bin, nfacets, r32, x32, g32);
+                                           bin, nfacets, r32, x32, g32, &np32);
         for (int k = 0; k < N; ++k) {
             vrp[2 * k] = r32[2 * k];
             vrp[2 * k + 1] = r32[2 * k + 1];
@@ -1964,6 +1969,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             g32[k] = gk;
         }
         const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, g32, ORC_GUESS_PASSES);
+        as_passes = np32 + w->npass;
         free(r32);
         free(g32);
         if (okg) { polished = 1; status = 0; it = 0; goto done; }
@@ -2012,6 +2018,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             }
         }
         const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, ORC_GUESS_PASSES);
+        if (as_kernel) as_passes = w->npass;   /* the warm kernel's passes */
         free(gm);
         if (okg) { polished = 1; status = 0; it = 0; goto done; }
     }
@@ -2198,6 +2205,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
 done:
     if (iters_out) *iters_out = it;
     if (polished_out) *polished_out = polished;
+    if (passes_out) *passes_out = as_passes;
     if (lam_out) {   /* final multipliers, [N][M], zero in unused facet slots */
         for (int k = 0; k < N; ++k)
             for (int i = 0; i < M; ++i)
@@ -2218,7 +2226,7 @@ typedef struct {
     int32_t shift;
     double floor;
     double *xi, *vrp, *lam_out;
-    int32_t *status, *iters, *polished;
+    int32_t *status, *iters, *polished, *passes;
     atomic_llong next;
 } batch_job;
 
@@ -2246,7 +2254,7 @@ static void* batch_worker(void* arg)
             J->A + (int64_t)2 * N * M * p, J->b + (int64_t)N * M * p, J->nfacets + (int64_t)N * p,
             wp, J->xi + (int64_t)2 * (N + 1) * p, J->vrp + (int64_t)2 * N * p,
             J->lam_out ? J->lam_out + (int64_t)N * M * p : NULL, J->iters + p,
-            J->polished ? J->polished + p : NULL);
+            J->polished ? J->polished + p : NULL, J->passes ? J->passes + p : NULL);
     }
     return NULL;
 }
@@ -2280,13 +2288,13 @@ void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int 
                                   const int32_t* nfacets, const double* vrp_ws,
                                   const double* lam_ws, const int32_t* prev_status, int32_t shift,
                                   double floor, double* xi, double* vrp, double* lam_out,
-                                  int32_t* status, int32_t* iters, int32_t* polished)
+                                  int32_t* status, int32_t* iters, int32_t* polished, int32_t* passes)
 {
     batch_job J = {.prm = prm, .batch = batch, .xi_init = xi_init, .omega = omega,
                    .xi_ref = xi_ref, .vrp_ref = vrp_ref, .A = A, .b = b, .nfacets = nfacets,
                    .vrp_ws = vrp_ws, .lam_ws = lam_ws, .prev_status = prev_status, .shift = shift,
                    .floor = floor,
                    .xi = xi, .vrp = vrp, .lam_out = lam_out, .status = status, .iters = iters,
-                   .polished = polished};
+                   .polished = polished, .passes = passes};
     run_batch(&J, threads);
 }

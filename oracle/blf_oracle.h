@@ -114,12 +114,13 @@ void orc_quintic_batch(int64_t S, int K1, int dim, int Q, const double* knots_t,
 /* The fp32 active-set search of a cold start as the device's active-set kernel runs it
  * (blf_oracle_as32.c): returns 1 when a float pass certified, the float point
  * (r [N][2], xi_{k+1} [N][2], as doubles) and the search's next candidate sets (guess bits per
- * knot), which the fp64 passes start from when it did not certify.
+ * knot), which the fp64 passes start from when it did not certify; *npass (NULL: not written) the
+ * float passes it ran.
  * sequential = 1: plain recursions instead of the kernel's scan tree (CPU baseline). */
 int orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_init,
                      const double* omega, const double* xi_ref, const double* vrp_ref,
                      const double* A, const double* b, const int32_t* nfacets, double* r_out,
-                     double* x_out, int32_t* guess);
+                     double* x_out, int32_t* guess, int32_t* npass);
 
 /* Warm start of a receding-horizon re-solve ("Warm start"): knot k
  * starts from knot src = min(k + shift, N - 1) of a previous solution: r_k = vrp[src],
@@ -133,13 +134,15 @@ typedef struct orc_dcm_warm {
 } orc_dcm_warm;
 
 /* As orc_dcm_mpc_solve, from the warm start `warm` (NULL: the cold start), also writing the final
- * multipliers to lam_out [N][M] (NULL: not written; zero in unused facet slots) and whether the
- * active-set polish was accepted to *polished (NULL: not written). */
+ * multipliers to lam_out [N][M] (NULL: not written; zero in unused facet slots), whether the
+ * active-set polish was accepted to *polished and the active-set kernels' drop/add passes (a cold
+ * start's fp32 search plus its fp64 passes, a warm start's fp64 passes; 0 without the active-set
+ * kernels) to *passes (NULL: not written; blf_dcm_mpc_solution.passes). */
 int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, const double* omega,
                            const double* xi_ref, const double* vrp_ref, const double* A,
                            const double* b, const int32_t* nfacets, const orc_dcm_warm* warm,
                            double* xi, double* vrp, double* lam_out, int32_t* iters,
-                           int32_t* polished);
+                           int32_t* polished, int32_t* passes);
 
 /* Whole batch (problem-major arrays), split over `threads` POSIX threads (one problem per
  * thread at a time).  Used as bench.py's CPU baseline. */
@@ -150,14 +153,15 @@ void orc_dcm_mpc_solve_batch(const orc_dcm_params* prm, int64_t batch, int threa
                              int32_t* iters);
 /* Batch with warm starts: vrp_ws [B][N][2] and lam_ws [B][N][M] (both NULL: cold starts),
  * prev_status [B] or NULL (a problem with prev_status != 0 is solved cold: the device's
- * blf_dcm_mpc_warm_start.prev_status), lam_out [B][N][M] or NULL, polished [B] or NULL. */
+ * blf_dcm_mpc_warm_start.prev_status), lam_out [B][N][M] or NULL, polished [B] or NULL, passes
+ * [B] or NULL. */
 void orc_dcm_mpc_solve_batch_warm(const orc_dcm_params* prm, int64_t batch, int threads,
                                   const double* xi_init, const double* omega, const double* xi_ref,
                                   const double* vrp_ref, const double* A, const double* b,
                                   const int32_t* nfacets, const double* vrp_ws,
                                   const double* lam_ws, const int32_t* prev_status, int32_t shift,
                                   double floor, double* xi, double* vrp, double* lam_out,
-                                  int32_t* status, int32_t* iters, int32_t* polished);
+                                  int32_t* status, int32_t* iters, int32_t* polished, int32_t* passes);
 
 /* Tree sum with the device's reduction order: c has n entries, padded with
  * zeros to 64*ceil(n/64); per 64-block xor-butterfly (distances 1, 2, 4, ..., 32), then block

@@ -45,6 +45,7 @@ typedef struct {
     float P00[2 * WV], P01[2 * WV], P11[2 * WV], h00[2 * WV], h01[2 * WV], h11[2 * WV];
     float rr0[2 * WV], rr1[2 * WV], xr0[2 * WV], xr1[2 * WV];
     float xi00, xi01;
+    int npass;   /* the passes run (the kernel's as_passes npass) */
 } s32;
 
 /* facet row i of knot k, rounded to float */
@@ -566,6 +567,7 @@ static int passes32(s32* s)
     xi_prev32(s, xk);
     static __thread int cand0[2 * WV];
     for (int pass = 0; pass < PASSES; ++pass) {
+        s->npass = pass + 1;
         int okp = 1, neg = 0, viol = 0;
         for (int k = 0; k < 2 * WV; ++k) { E[k][0] = E[k][1] = E[k][2] = 0.0f; pk[k] = 0; }
         /* setup + residuals */
@@ -691,7 +693,7 @@ static int passes32(s32* s)
 int orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_init,
                      const double* omega, const double* xi_ref, const double* vrp_ref,
                      const double* A, const double* b, const int32_t* nfacets, double* r_out,
-                     double* x_out, int32_t* guess)
+                     double* x_out, int32_t* guess, int32_t* npass)
 {
     static __thread s32 st;
     s32* s = &st;
@@ -737,6 +739,7 @@ int orc_as32_search(const orc_dcm_params* prm, int sequential, const double* xi_
         s->gm[k] = gm;
     }
     const int cert = passes32(s);
+    if (npass) *npass = s->npass;
     for (int k = 0; k < N; ++k) {
         r_out[2 * k] = (double)s->r0[k];
         r_out[2 * k + 1] = (double)s->r1[k];

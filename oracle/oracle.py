@@ -73,7 +73,7 @@ def lib():
                                               _dp, _dp, _ip, _ip]
         L.orc_dcm_mpc_solve_batch_warm.argtypes = [
             ctypes.POINTER(OrcParams), ctypes.c_int64, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp,
-            _ip, _dp, _dp, _ip, ctypes.c_int32, ctypes.c_double, _dp, _dp, _dp, _ip, _ip, _ip]
+            _ip, _dp, _dp, _ip, ctypes.c_int32, ctypes.c_double, _dp, _dp, _dp, _ip, _ip, _ip, _ip]
         L.orc_dcm_phase_expand.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp,
                                            _dp, _dp, _ip, _dp, ctypes.c_int64, ctypes.c_double,
                                            ctypes.c_int, _dp, _dp, _ip, _dp, _dp]
@@ -280,11 +280,13 @@ def dcm_mpc_solve_batch(prob, params=None, threads=1, count=None, device_batch=N
 
 
 def dcm_mpc_solve_batch_warm(prob, vrp_ws=None, lam_ws=None, shift=1, floor=1e-4,
-                             params=None, threads=1, polished=None, prev_status=None, device_batch=None):
+                             params=None, threads=1, polished=None, prev_status=None, device_batch=None,
+                             passes=None):
     """Batch solve from warm starts (vrp_ws [B][N][2], lam_ws [B][N][M]; None: cold starts;
     prev_status [B]: problems with a nonzero previous status start cold).
     Returns status, xi, vrp, iters, lam [B][N][M] (final multipliers); `polished` (an int32 [B]
-    array, optional) receives whether the active-set polish was accepted."""
+    array, optional) receives whether the active-set polish was accepted, `passes` (int32 [B],
+    optional) the active-set kernels' drop/add passes (blf_dcm_mpc_solution.passes)."""
     B, N = prob["omega"].shape
     p = _tree_params(params, N, B if device_batch is None else device_batch)
     M = p.max_facets
@@ -302,7 +304,7 @@ def dcm_mpc_solve_batch_warm(prob, vrp_ws=None, lam_ws=None, shift=1, floor=1e-4
         None if ws_v is None else _d(ws_v), None if ws_l is None else _d(ws_l),
         None if prev_status is None else _i(np.ascontiguousarray(prev_status, dtype=np.int32)), int(shift),
         float(floor), _d(xi), _d(vrp), _d(lam), _i(status), _i(iters),
-        None if polished is None else _i(polished))
+        None if polished is None else _i(polished), None if passes is None else _i(passes))
     return status, xi, vrp, iters, lam
 
 

@@ -310,20 +310,27 @@ def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, fo
             torch.cuda.synchronize()
             cold = {k: v.cpu().numpy().copy() for k, v in out.items()}
             pol = np.zeros(B, np.int32)
-            st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(host, params=prm_o, threads=8, polished=pol)
+            pas = np.zeros(B, np.int32)
+            st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(host, params=prm_o, threads=8, polished=pol,
+                                                                   passes=pas)
             for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
-                           ("polished", pol)):
+                           ("polished", pol), ("passes", pas)):
                 np.testing.assert_array_equal(cold[k], ref, err_msg=f"cold {k} mode {mode}")
             warm = dict(vrp=out["vrp"], lam=out["lam"], shift=1, floor=1e-3)
             outw = handle.dcm_mpc_solve(dev, warm=warm, lambda_out=True)
             torch.cuda.synchronize()
             pol = np.zeros(B, np.int32)
+            pas = np.zeros(B, np.int32)
             st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(
                 host, vrp_ws=cold["vrp"], lam_ws=cold["lam"], shift=1, floor=1e-3, params=prm_o,
-                threads=8, polished=pol)
+                threads=8, polished=pol, passes=pas)
             for k, ref in (("status", st), ("xi", xi), ("vrp", vrp), ("iters", it), ("lam", lam),
-                           ("polished", pol)):
+                           ("polished", pol), ("passes", pas)):
                 np.testing.assert_array_equal(outw[k].cpu().numpy(), ref, err_msg=f"warm {k} mode {mode}")
+            if mode == "0":   # the active-set kernels: a cold start runs the fp32 search first
+                assert (cold["passes"] >= 1).all() and (outw["passes"].cpu().numpy() >= 1).all()
+            else:             # the interior point kernel alone
+                assert (cold["passes"] == 0).all()
             res[mode] = cold
     finally:
         native.set_qp_launch_mode(single_kernel=0)
