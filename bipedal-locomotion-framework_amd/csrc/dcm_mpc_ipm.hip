@@ -60,14 +60,18 @@ struct IpmArgs {
     double* lam_out;
 };
 
+// the kernel's arguments in the kernarg segment (address space 4), passed to the callee
+// explicitly: a callee has no kernarg segment pointer of its own (it reads as null)
+typedef __attribute__((address_space(4))) const IpmArgs* KernArgs;
+
 template <int NT, bool WARM, bool LAMOUT, int MF>
-__device__ __noinline__ void ipm_solve_listed(int64_t p)
+__device__ __noinline__ void ipm_solve_listed(KernArgs A, int64_t p)
 {
-#ifdef __HIP_DEVICE_COMPILE__   // (the kernarg segment exists in the device pass only)
-    const IpmArgs& A = *reinterpret_cast<const IpmArgs*>(__builtin_amdgcn_kernarg_segment_ptr());
-    ipm_solve<NT, WARM, LAMOUT, MF>(A.P, p, A.xi_init, A.omega, A.xi_ref, A.vrp_ref, A.Ain, A.bin, A.nfacets,
-                                    A.ws_vrp, A.ws_lam, A.xi_out, A.vrp_out, A.status_out, A.iters_out,
-                                    A.polished_out, A.lam_out);
+#ifdef __HIP_DEVICE_COMPILE__   // (address space 4 exists in the device pass only)
+    const KParams P = A->P;
+    ipm_solve<NT, WARM, LAMOUT, MF>(P, p, A->xi_init, A->omega, A->xi_ref, A->vrp_ref, A->Ain, A->bin, A->nfacets,
+                                    A->ws_vrp, A->ws_lam, A->xi_out, A->vrp_out, A->status_out, A->iters_out,
+                                    A->polished_out, A->lam_out);
 #endif
 }
 
@@ -78,7 +82,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     const int count = __builtin_amdgcn_readfirstlane(A.P.list[A.P.list_slot]);
     if (blockIdx.x == 0 && threadIdx.x == 0) A.P.list[A.P.list_slot ^ 1] = 0;
     for (int i = (int)blockIdx.x; i < count; i += (int)gridDim.x) {
-        ipm_solve_listed<NT, WARM, LAMOUT, MF>(__builtin_amdgcn_readfirstlane(idx[i]));
+        ipm_solve_listed<NT, WARM, LAMOUT, MF>((KernArgs)__builtin_amdgcn_kernarg_segment_ptr(),
+                                               __builtin_amdgcn_readfirstlane(idx[i]));
         __syncthreads();   // the LDS is the next problem's
     }
 }
