@@ -44,46 +44,28 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
 }
 
 // Stage 2 over the pending list the active-set kernel appended to (KParams::list): a grid of a
-// few workgroups, each taking every gridDim-th listed problem.  The solve is an out-of-line call
-// that reads the kernel's arguments itself, so a workgroup that finds nothing listed -- every
-// workgroup of a batch the active-set kernel certified whole -- loads the count and leaves without
-// touching scratch (the batch-sized grid of the inlined kernel stored 12.5 KB of register spills
-// per QP on its way to the status check, round 4).  Workgroup 0 zeroes the other count slot, the
-// one the stream's next solve appends to.
-struct IpmArgs {
-    KParams P;
-    const double *xi_init, *omega, *xi_ref, *vrp_ref, *Ain, *bin;
-    const int32_t* nfacets;
-    const double *ws_vrp, *ws_lam;
-    double *xi_out, *vrp_out;
-    int32_t *status_out, *iters_out, *polished_out;
-    double* lam_out;
-};
-
-// the kernel's arguments in the kernarg segment (address space 4), passed to the callee
-// explicitly: a callee has no kernarg segment pointer of its own (it reads as null)
-typedef __attribute__((address_space(4))) const IpmArgs* KernArgs;
-
+// few workgroups, each taking every gridDim-th listed problem.  With a budget of 256 VGPRs the
+// solve needs no scratch, so a workgroup that finds nothing listed -- every workgroup of a batch
+// the active-set kernel certified whole -- loads the count and leaves (round 4's batch-sized grid
+// at 168 VGPRs stored 12.5 KB of register spills per QP on its way to the status check).
+// Workgroup 0 zeroes the other count slot, the one the stream's next solve appends to.
 template <int NT, bool WARM, bool LAMOUT, int MF>
-__device__ __noinline__ void ipm_solve_listed(KernArgs A, int64_t p)
+__global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_ipm_list_kernel(
+    KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
+    const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
+    const double* __restrict__ Ain, const double* __restrict__ bin,
+    const int32_t* __restrict__ nfacets, const double* __restrict__ ws_vrp,
+    const double* __restrict__ ws_lam, double* __restrict__ xi_out,
+    double* __restrict__ vrp_out, int32_t* __restrict__ status_out,
+    int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out)
 {
-#ifdef __HIP_DEVICE_COMPILE__   // (address space 4 exists in the device pass only)
-    const KParams P = A->P;
-    ipm_solve<NT, WARM, LAMOUT, MF>(P, p, A->xi_init, A->omega, A->xi_ref, A->vrp_ref, A->Ain, A->bin, A->nfacets,
-                                    A->ws_vrp, A->ws_lam, A->xi_out, A->vrp_out, A->status_out, A->iters_out,
-                                    A->polished_out, A->lam_out);
-#endif
-}
-
-template <int NT, bool WARM, bool LAMOUT, int MF>
-__global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_ipm_list_kernel(IpmArgs A)
-{
-    const int32_t* idx = A.P.list + 2;
-    const int count = __builtin_amdgcn_readfirstlane(A.P.list[A.P.list_slot]);
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.P.list[A.P.list_slot ^ 1] = 0;
+    const int32_t* idx = P.list + 2;
+    const int count = __builtin_amdgcn_readfirstlane(P.list[P.list_slot]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) P.list[P.list_slot ^ 1] = 0;
     for (int i = (int)blockIdx.x; i < count; i += (int)gridDim.x) {
-        ipm_solve_listed<NT, WARM, LAMOUT, MF>((KernArgs)__builtin_amdgcn_kernarg_segment_ptr(),
-                                               __builtin_amdgcn_readfirstlane(idx[i]));
+        ipm_solve<NT, WARM, LAMOUT, MF>(P, __builtin_amdgcn_readfirstlane(idx[i]), xi_init, omega, xi_ref, vrp_ref,
+                                        Ain, bin, nfacets, ws_vrp, ws_lam, xi_out, vrp_out, status_out, iters_out,
+                                        polished_out, lam_out);
         __syncthreads();   // the LDS is the next problem's
     }
 }
@@ -105,11 +87,10 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
         // stage 2 runs only after the active-set kernels (N <= 128, at most kMaxFacets facet
         // slots); at most kListGrid workgroups loop over the pending list
         if constexpr (NT <= 2 * kWave && MF == kMaxFacets) {
-            const IpmArgs a{kp, pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b, pb->nfacets,
-                            warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr, sol->xi, sol->vrp,
-                            sol->status, sol->iters, sol->polished, lam_out};
             hipLaunchKernelGGL(IPM_KERN(dcm_mpc_ipm_list_kernel), dim3((unsigned)std::min<int64_t>(batch, kListGrid)),
-                               dim3(NT), lds, s, a);
+                               dim3(NT), lds, s, kp, pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
+                               pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr, sol->xi,
+                               sol->vrp, sol->status, sol->iters, sol->polished, lam_out);
             return check_hip(hipGetLastError(), "dcm_mpc_ipm_list_kernel launch");
         } else {
             return set_error(BLF_ERR_UNSUPPORTED, "stage 2 with %d threads, %d facet slots", NT, MF);
