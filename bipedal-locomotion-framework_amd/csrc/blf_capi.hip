@@ -22,7 +22,12 @@ QpLaunchMode& qp_launch_mode()
                              {[] {
                                  const char* sk = getenv("BLF_QP_SINGLE_KERNEL");
                                  return (sk && sk[0] == '1') ? 1 : 0;
-                             }()}};
+                             }()},
+                             [] {
+                                 const char* lg = getenv("BLF_QP_LIST_GRID");
+                                 const int v = lg ? atoi(lg) : 0;
+                                 return v > 0 ? v : kListGrid;
+                             }()};
     return mode;
 }
 

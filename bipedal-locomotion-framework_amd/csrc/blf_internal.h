@@ -85,6 +85,7 @@ blf_status launch_phase_expand(int32_t P, const int32_t* nphases, const double* 
 struct QpLaunchMode {
     std::atomic<int> fuse_stage2;     // 1 (default): stage 2 inside the small-batch active-set kernel
     std::atomic<int> single_kernel;   // 0 (default): active-set kernel first
+    int list_grid;                    // stage 2's grid (kListGrid; BLF_QP_LIST_GRID, A/B only)
 };
 QpLaunchMode& qp_launch_mode();
 // l: the stream's stage-2 work list (Handle::stage2_list)

@@ -87,7 +87,7 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
         // stage 2 runs only after the active-set kernels (N <= 128, at most kMaxFacets facet
         // slots); at most kListGrid workgroups loop over the pending list
         if constexpr (NT <= 2 * kWave && MF == kMaxFacets) {
-            hipLaunchKernelGGL(IPM_KERN(dcm_mpc_ipm_list_kernel), dim3((unsigned)std::min<int64_t>(batch, kListGrid)),
+            hipLaunchKernelGGL(IPM_KERN(dcm_mpc_ipm_list_kernel), dim3((unsigned)std::min<int64_t>(batch, qp_launch_mode().list_grid)),
                                dim3(NT), lds, s, kp, pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                                pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr, sol->xi,
                                sol->vrp, sol->status, sol->iters, sol->polished, lam_out);

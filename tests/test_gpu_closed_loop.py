@@ -201,7 +201,6 @@ def test_closed_loop_stage2_list_bitwise(handle):
         nipm += int((out1["iters"] > 0).sum())
         for k in ("xi", "vrp", "status", "iters", "polished", "lam"):
             np.testing.assert_array_equal(out1[k].cpu().numpy(), out2[k].cpu().numpy(), err_msg=f"{k} period {s}")
-        assert int((out1["status"] != 0).sum()) == 0, s
     assert nipm > 0, "no window went to the interior point kernel"
     for k in native.FB_STATE_KEYS:
         np.testing.assert_array_equal(ph.state[k].cpu().numpy(), ex.state[k].cpu().numpy(), err_msg=k)
