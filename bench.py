@@ -176,13 +176,15 @@ def main():
     ap.add_argument("--expand-path", action="store_true",
                     help="rh / c3 / c5: expand the window through HBM (blf_dcm_phase_expand) and "
                          "solve it (the two calls blf_dcm_mpc_solve_phased fuses; A/B only)")
-    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c5", "rh"), default="c2",
+    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c5", "rh", "mc"), default="c2",
                     help="c2 (default, the driver's metric): configs[1]; c1: configs[0] single-solve "
                          "latency (4 footsteps, N=50) on the GPU and the CPU; c3: configs[2] pipeline "
                          "(hull H-rep + QP + swing splines, B=65536); c5: configs[4] closed loop "
                          "(robot DCM -> warm-started QP -> joint references -> 30-DoF floating-"
                          "base dynamics with contact feet, B=16384 per GPU, multi-rank); rh: "
-                         "receding-horizon advance() (phase expansion + warm-started QP, B=4096)")
+                         "receding-horizon advance() (phase expansion + warm-started QP, B=4096); "
+                         "mc: plans with three-contact phases (the reference ContactPhaseList "
+                         "test's lists, 16 facet slots, N=50): cold solves and warm windows")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus != world:
@@ -372,6 +374,8 @@ def other_workload(args):
     N = args.horizon
     if args.workload == "rh":
         return receding_horizon(args, h, dev)
+    if args.workload == "mc":
+        return three_contact(args, h, dev)
     if args.workload == "c1":
         return single_solve_latency(args, h, dev)
     if args.workload == "c3":
@@ -776,6 +780,101 @@ def phase_expand_bytes(P, N, M):
     """Algorithmic bytes of blf_dcm_phase_expand per problem: the phase table read once
     (nphases, begin/end, A rows, b, counts, reference points) and the window written."""
     return 4 + P * (16 + 24 * M + 4 + 16) + N * (24 * M + 4 + 16) + 16 * (N + 1)
+
+
+def three_contact(args, h, dev):
+    """Plans with three-contact phases: the reference ContactPhaseList test's
+    three lists (src/Planners/tests/ContactPhaseListTest.cpp:32-47) with the feet turned out and
+    a hand support ahead, B = 4096 plans, N = 50 knots of 0.1 s, max_facets 16 (hulls of up to 9
+    facets).  Two lines' worth in one: the cold phase-indexed solve of window 0, repeated on the
+    same inputs (cold QP/s), and the receding horizon, every window warm-started from the last
+    (blf_dcm_mpc_solve_phased; --expand-path: blf_dcm_phase_expand + blf_dcm_mpc_solve_warm, with
+    BLF_QP_SINGLE_KERNEL=1 the interior point kernel alone)."""
+    import torch
+    from blf import native
+    from blf import problems as P
+    B, N, M = args.batch, 50, 16
+    S = args.warmup + 2 * args.steps + 1
+    knots = max(75, N + S)
+    prob = P.three_contact_plan(B, knots=knots, seed=P.SEED)
+    t = lambda k: torch.from_numpy(prob[k]).to(dev)
+    table = h.phase_table(t("nphases"), t("phase_begin"), t("phase_end"), t("phase_corners"),
+                          t("phase_ncorners"), max_facets=M, ref=t("phase_ref"))
+    omega_full = t("omega")
+    params = native.default_params(N, max_facets=M, dt=prob["dt"])
+    params.tol_polish = args.tol_polish if args.tol_polish is not None else 1e-4
+    xi0 = t("xi_init")
+    e64 = lambda *shape: torch.empty(shape, dtype=torch.float64, device=dev)
+    e32 = lambda *shape: torch.empty(shape, dtype=torch.int32, device=dev)
+    window = dict(omega=e64(B, N), xi_ref=e64(B, N + 1, 2), vrp_ref=e64(B, N, 2), A=e64(B, N, M, 2),
+                  b=e64(B, N, M), nfacets=e32(B, N))
+    newbuf = lambda: dict(xi=e64(B, N + 1, 2), vrp=e64(B, N, 2), status=e32(B), iters=e32(B),
+                          polished=e32(B), passes=e32(B), lam=e64(B, N, M), window=window)
+
+    def solve(s, xi, warm, out):
+        if args.expand_path:
+            w = h.dcm_phase_expand(table, s, prob["dt"], N)
+            w.update(xi_init=xi, omega=omega_full[:, s:s + N].contiguous())
+            return h.dcm_mpc_solve(w, params, out=out, warm=warm, lambda_out=True)
+        return h.dcm_mpc_solve_phased(table, s, xi, omega_full[:, s:s + N], params, warm=warm, out=out,
+                                      lambda_out=True)
+
+    # cold: window 0 from the plans' initial DCMs, the same inputs every step
+    cold = newbuf()
+    for _ in range(args.warmup):
+        solve(0, xi0, None, cold)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        solve(0, xi0, None, cold)
+    torch.cuda.synchronize()
+    sec_cold = (time.perf_counter() - t0) / args.steps
+    cold_unsolved = int((cold["status"] != 0).sum())
+    cold_passes = float(cold["passes"].float().mean())
+    cold_ipm = int((cold["iters"] > 0).sum())
+    # warm: the receding horizon, window s + 1 warm-started from window s
+    bufs = [newbuf() for _ in range(S)]
+    state = dict(xi=xi0.clone(), prev=None, s=0)
+
+    def step():
+        s = state["s"]
+        warm = None
+        if state["prev"] is not None:
+            warm = dict(vrp=state["prev"]["vrp"], lam=state["prev"]["lam"], shift=1, floor=1e-3)
+        out = solve(s, state["xi"], warm, bufs[s])
+        state["xi"] = out["xi"][:, 1].contiguous()
+        state["prev"] = out
+        state["s"] = s + 1
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    sec_warm = (time.perf_counter() - t0) / args.steps
+    statuses = torch.stack([bufs[i]["status"] for i in range(state["s"])])
+    warm_unsolved = int((statuses != 0).sum())
+    warm_passes = float(torch.stack([bufs[i]["passes"] for i in range(1, state["s"])]).float().mean())
+    nf = table["phase_nf"]
+    line = {"metric": "three-contact DCM-MPC QP solves/sec (cold window; warm receding horizon)",
+            "value": B / sec_cold, "unit": "QP/s", "n_gpus": 1, "ms_per_step": sec_cold * 1e3,
+            "warm_value": B / sec_warm, "warm_ms_per_step": sec_warm * 1e3,
+            "steps": args.steps, "warmup": args.warmup, "dtype": "f64",
+            "cold": {"unsolved": cold_unsolved, "mean_active_set_passes": cold_passes,
+                     "qps_to_interior_point": cold_ipm},
+            "warm": {"windows": state["s"], "unsolved": warm_unsolved,
+                     "mean_active_set_passes": warm_passes},
+            "max_hull_facets": int(nf.max()),
+            "path": ("blf_dcm_phase_expand + blf_dcm_mpc_solve_warm" if args.expand_path else
+                     "blf_dcm_mpc_solve_phased") +
+                    (" (interior point kernel alone, BLF_QP_SINGLE_KERNEL=1)"
+                     if os.environ.get("BLF_QP_SINGLE_KERNEL") == "1" else ""),
+            "data": "synthetic (the reference ContactPhaseList test's three lists, randomised poses)",
+            "config": {"workload": "three-contact plans, B=4096, horizon=50, dt=0.1, max_facets=16",
+                       "batch": B, "horizon": N, "max_facets": M}}
+    emit(line)
 
 
 def receding_horizon(args, h, dev):

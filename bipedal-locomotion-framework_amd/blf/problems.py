@@ -215,3 +215,50 @@ def window(full, start, horizon, xi_init=None):
         v = out[k]
         out[k] = v.contiguous() if hasattr(v, "contiguous") else np.ascontiguousarray(v)
     return out
+
+
+# The phases of the reference's ContactPhaseList test (src/Planners/tests/ContactPhaseListTest.cpp
+# :15-153; tests/golden/contact_phases.json): (begin, end, contact index per list or -1), lists in
+# std::map order (additional, left, right).  Phases [4, 5) and [6, 7) have three contacts.
+REFERENCE_THREE_CONTACT_PHASES = (
+    (0.0, 1.0, (-1, 0, 0)), (1.0, 2.0, (-1, -1, 0)), (2.0, 3.0, (-1, 1, 0)), (3.0, 4.0, (-1, 1, -1)),
+    (4.0, 5.0, (0, 1, 1)), (5.0, 6.0, (-1, -1, 1)), (6.0, 7.0, (1, 2, 1)), (7.0, 7.5, (1, -1, -1)))
+
+
+def three_contact_plan(batch, dt=0.1, knots=75, seed=SEED, xi_offset=0.05,
+                       phases=REFERENCE_THREE_CONTACT_PHASES):
+    """Plans over three contact lists (bench.py --workload mc; tests/multi_contact.py builds the same
+    plans from the oracle's createPhases): standing with the feet turned out and a hand support
+    ahead, so a phase with all three contacts has a hull of up to 9 facets (max_facets 16).  Each
+    contact is a 0.12 x 0.09 m rectangle; returns make_batch's phase-table keys plus omega,
+    xi_init (the first phase's centroid plus a uniform offset) and dt."""
+    begin = np.array([p[0] for p in phases])
+    end = np.array([p[1] for p in phases])
+    active = np.array([p[2] for p in phases], dtype=np.int64)
+    NP = len(phases)
+    rng = np.random.default_rng(seed)
+    corners = np.zeros((batch, NP, 16, 2))
+    ncorners = np.zeros((batch, NP), dtype=np.int32)
+    for q in range(batch):
+        u = rng.uniform(-1.0, 1.0, (3, 4, 3))
+        pose = np.zeros((3, 4, 3))      # [list][contact][x, y, yaw]
+        for c in range(4):
+            pose[1, c] = (0.005 * u[1, c, 0], 0.14 + 0.005 * u[1, c, 1], 1.50 + 0.03 * u[1, c, 2])
+            pose[2, c] = (0.005 * u[2, c, 0], -0.14 + 0.005 * u[2, c, 1], -0.03 + 0.03 * u[2, c, 2])
+            pose[0, c] = (0.19 + 0.005 * u[0, c, 0], 0.005 * u[0, c, 1], 0.85 + 0.03 * u[0, c, 2])
+        for p in range(NP):
+            pts = [rectangle_corners(pose[l, active[p, l]]) for l in range(3) if active[p, l] >= 0]
+            if pts:
+                pts = np.concatenate(pts)
+                corners[q, p, :len(pts)] = pts
+                ncorners[q, p] = len(pts)
+    ref = corners.sum(axis=2) / np.maximum(ncorners, 1)[..., None]
+    k = np.arange(knots)
+    z = 0.53 + 0.01 * np.sin(2.0 * np.pi * k / knots)[None, :] * np.ones((batch, 1))
+    omega = np.sqrt(GRAVITY / z)
+    xi_init = ref[:, 0] + rng.uniform(-xi_offset, xi_offset, (batch, 2))
+    return dict(nphases=np.full(batch, NP, dtype=np.int32),
+                phase_begin=np.ascontiguousarray(np.broadcast_to(begin, (batch, NP))),
+                phase_end=np.ascontiguousarray(np.broadcast_to(end, (batch, NP))),
+                phase_corners=corners, phase_ncorners=ncorners, phase_ref=ref,
+                omega=np.ascontiguousarray(omega), xi_init=xi_init, dt=dt)

@@ -89,12 +89,13 @@ using AKnot = AKnotT<double>;
 
 // The QP's facet rows in LDS, [M][S] normals and [M][S] offsets (facet i of column col at
 // i S + col), fp64 (rounded to float as the fp32 search reads them).
-template <class V>
+template <class V, int MF = kMaxFacets>
 struct LdsRows;
 // at(): a 24-bit multiply (v_mul_u32_u24, full rate; i < 8, S <= 128) for the per-lane facet
 // indices of the passes, which v_mul_lo_u32 (quarter rate) took before.
-template <>
-struct LdsRows<double> {
+template <int MF>
+struct LdsRows<double, MF> {
+    static constexpr int kMF = MF;   // facet slots (8, or 16 for phases of three or four contacts)
     using V2 = double2;
     const double2* A2;
     const double* Bv;
@@ -102,8 +103,9 @@ struct LdsRows<double> {
     __device__ int col(int j, int lane) const { return j * NH + lane; }
     __device__ int at(int i, int col) const { return (int)__umul24((unsigned)i, (unsigned)S) + col; }
 };
-template <>
-struct LdsRows<float> {
+template <int MF>
+struct LdsRows<float, MF> {
+    static constexpr int kMF = MF;
     using V2 = float2;
     const float2* A2;
     const float* Bv;
@@ -652,7 +654,7 @@ __device__ __forceinline__ int as_vertex_pair(const RS& R, int kx, int km, int c
     return 3;
 }
 
-// Candidate facets of a pass -> (pc, pi1, pi2) packed as pc | pi1 << 2 | pi2 << 5, the VRP moved
+// Candidate facets of a pass -> (pc, pi1, pi2) packed as pc | pi1 << 2 | pi2 << 6, the VRP moved
 // onto the active lines and E_k (IPM kernel polish block, "active sets, projection").
 // Branch-free: the two knots of a lane, and the lanes of a wavefront, have every mix of 0, 1 and 2
 // active lines, so per-case branches serialised all three bodies and their divisions.  Each knot
@@ -674,7 +676,7 @@ __device__ __forceinline__ void as_pass_setup(AKnotT<T>& K, const PT<T>& P, cons
     if (pc > 2) pc = as_vertex_pair<T>(R, cx, km, cm, P.tol_p, pi1, pi2);
     if (pc > 2) okp = false;
     const int c = pc < 3 ? pc : 2;
-    pk = c | (pi1 << 2) | (pi2 << 5);
+    pk = c | (pi1 << 2) | (pi2 << 6);
     const T b2 = K.be * K.be;
     const Row<T> a = row<T>(R, pi1, cx);
     const Row<T> e = row<T>(R, pi2, cx);
@@ -706,7 +708,7 @@ template <class T, class RS>
 __device__ __forceinline__ void as_pass_h(AKnotT<T>& K, const PT<T>& P, const RS& R, int col, int pk,
                                           bool& okp)
 {
-    const int pc = pk & 3, pi1 = (pk >> 2) & 7;
+    const int pc = pk & 3, pi1 = (pk >> 2) & 15;
     const T b2 = K.be * K.be;
     const T B00 = fma(b2, K.P00, P.Rw0);
     const T B01 = b2 * K.P01;
@@ -732,7 +734,7 @@ __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const R
                                            bool& viol)
 {
     const int cx = opaque(col);
-    const int pc = pk & 3, pi1 = (pk >> 2) & 7, pi2 = (pk >> 5) & 7;
+    const int pc = pk & 3, pi1 = (pk >> 2) & 15, pi2 = (pk >> 6) & 15;
     const T s0 = K.qx0 + vn0;
     const T s1 = K.qx1 + vn1;
     const T nu0 = FD3(K.P00, dx0, K.P01, dx1, s0);
@@ -768,7 +770,7 @@ __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const R
     const int km = opaque(K.m);
     int vm = 0;
 #pragma unroll
-    for (int i0 = 0; i0 < kMaxFacets; i0 += 4) {
+    for (int i0 = 0; i0 < RS::kMF; i0 += 4) {
         if (i0 >= km) break;
         Row<T> rv[4];
 #pragma unroll
@@ -1013,7 +1015,7 @@ __device__ __forceinline__ void ph_stage_phases(const PhaseSrc& ps, int64_t p, i
 // phase).  The table rows are a few KB per problem, read through the caches.
 template <int U>
 __device__ __forceinline__ void stage_rows_ph_issue(const PhaseSrc& ps, const int32_t* sPh, int64_t p, int N, int M,
-                                                    int lane, double2 (&va)[U], double (&vb)[U])
+                                                    int lane, double2 (&va)[U], double (&vb)[U], int t0 = 0)
 {
     const int nA = N * M;
     const double2* As = reinterpret_cast<const double2*>(ps.A) + p * ps.P * M;
@@ -1022,7 +1024,7 @@ __device__ __forceinline__ void stage_rows_ph_issue(const PhaseSrc& ps, const in
     const int sh = __builtin_ctz(M);
 #pragma unroll
     for (int u = 0; u < U; ++u) {   // clamped, so every load is unconditional
-        const int t = min(u * kWave + lane, nA - 1);
+        const int t = min(t0 + u * kWave + lane, nA - 1);
         const int k = pow2 ? t >> sh : t / M, i = t - k * M;
         const int ph = sPh[k];
         const int src = (ph < 0 ? 0 : ph) * M + i;
@@ -1033,14 +1035,32 @@ __device__ __forceinline__ void stage_rows_ph_issue(const PhaseSrc& ps, const in
     }
 }
 
-template <int KPL, int U>
+// ROUNDS = false: one round of U loads per lane covers the rows (M <= kMaxFacets); true: as many
+// rounds as N M needs (the 16-slot instantiations)
+template <int KPL, int U, bool ROUNDS = false>
 __device__ __forceinline__ void stage_rows_ph(const PhaseSrc& ps, const int32_t* sPh, int64_t p, int N, int M,
                                               int S, int NH, int lane, double* A2v, double* Bv)
 {
     double2 va[U];
     double vb[U];
-    stage_rows_ph_issue<U>(ps, sPh, p, N, M, lane, va, vb);
-    stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, N * M, A2v, Bv);
+    if constexpr (ROUNDS) {
+        for (int t0 = 0; t0 < N * M; t0 += U * kWave) {
+            stage_rows_ph_issue<U>(ps, sPh, p, N, M, lane, va, vb, t0);
+            stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, t0, N * M, A2v, Bv);
+        }
+    } else {
+        stage_rows_ph_issue<U>(ps, sPh, p, N, M, lane, va, vb);
+        stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, N * M, A2v, Bv);
+    }
+}
+
+// The QP's rows into LDS in rounds of U loads per lane (the 16-slot instantiations).
+template <int KPL, int U>
+__device__ __forceinline__ void stage_rows_rounds(const double* Ain, const double* bin, int64_t p, int N, int M,
+                                                  int S, int NH, int lane, double* A2v, double* Bv)
+{
+    for (int t0 = 0; t0 < N * M; t0 += U * kWave)
+        stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, t0, N * M, A2v, Bv);
 }
 
 // A knot's own inputs: facet count, omega, references (vrp_ref_k, xi_ref_{k+1}).
@@ -1130,7 +1150,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
             xi_out[2 * sx] = K[j].x0;
             xi_out[2 * sx + 1] = K[j].x1;
             if (LAMOUT && done) {   // the optimum's multipliers: active facets, 0 elsewhere
-                const int pc = certified ? (pk[j] & 3) : 0, pi1 = (pk[j] >> 2) & 7, pi2 = (pk[j] >> 5) & 7;
+                const int pc = certified ? (pk[j] & 3) : 0, pi1 = (pk[j] >> 2) & 15, pi2 = (pk[j] >> 6) & 15;
                 const double l1 = pl[j][0] > 0.0 ? pl[j][0] : 0.0;
                 const double l2 = pl[j][1] > 0.0 ? pl[j][1] : 0.0;
                 double* lo = lam_out + st * M;
@@ -1163,7 +1183,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
 // when none certifies, the fp64 LQ optimum from (xi_ref, vrp_ref) becomes the IPM's start point.
 // The cold solve of one QP (the cold kernel's body; the warm kernel runs it for the problems whose
 // previous solve failed, blf_dcm_mpc_warm_start.prev_status).
-template <int KPL, bool LAMOUT, bool PH, int TR>
+template <int KPL, bool LAMOUT, bool PH, int TR, int MF = kMaxFacets>
 __device__ __forceinline__ void cold_solve(
     const KParams& P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1188,7 +1208,8 @@ __device__ __forceinline__ void cold_solve(
 #endif
 
     const int nA = N * M;
-    constexpr int U = KPL == 2 ? 2 * kMaxFacets : kMaxFacets;   // N M <= 1024 / 512   // one round of 16 covers N M <= 1024
+    constexpr bool kWide = MF > kMaxFacets;   // 16 slots: the rows staged in rounds
+    constexpr int U = KPL == 2 ? 2 * kMaxFacets : kMaxFacets;   // one round covers N M <= 1024 / 512
     double* sBE = smem + 3 * (size_t)M * S;                            // PH: [2][P]
     int32_t* sPh = reinterpret_cast<int32_t*>(sBE + 2 * (size_t)ps.P);  // PH: [N+1]
     // The facet rows' loads are issued first and land in LDS only after the float LQ step, which
@@ -1197,20 +1218,22 @@ __device__ __forceinline__ void cold_solve(
     // (The phase-indexed input keeps its gathers before the LQ step: issued after the knot loads
     // and committed after the step like the slab loads, it measured 1 % slower on the c3 pipeline,
     // 1.900 / 1.893 against 1.882 / 1.874 ms per step, profiles/r03_ph_overlap_ab.log.)
-    constexpr bool kOverlap = !PH && BLF_AS_OVERLAP;
+    constexpr bool kOverlap = !PH && BLF_AS_OVERLAP && !kWide;
     double2 va[U];
     double vb[U];
     if (PH) {
         ph_stage_phases(ps, p, N, P.dt, lane, sBE, sPh);
-        stage_rows_ph<KPL, U>(ps, sPh, p, N, M, S, NH, lane, A2d, Bv);
+        stage_rows_ph<KPL, U, kWide>(ps, sPh, p, N, M, S, NH, lane, A2d, Bv);
     } else if (kOverlap) {
         // issued below, after the knot loads: a wait for those (vmcnt counts in issue order) then
         // leaves the younger row loads in flight
+    } else if (kWide) {
+        stage_rows_rounds<KPL, U>(Ain, bin, p, N, M, S, NH, lane, A2d, Bv);
     } else {
         stage_rows<KPL, U, double>(Ain, bin, p, N, M, S, NH, lane, 0, nA, A2d, Bv);
     }
-    const LdsRows<double> R{reinterpret_cast<const typename LdsRows<double>::V2*>(smem),
-                            smem + 2 * (size_t)M * S, S, NH};
+    const LdsRows<double, MF> R{reinterpret_cast<const typename LdsRows<double, MF>::V2*>(smem),
+                                smem + 2 * (size_t)M * S, S, NH};
 
     AKnotT<float> F[KPL];
     int cand[KPL];         // the float search's next candidate sets (phase B's guess when uncertified)
@@ -1362,7 +1385,7 @@ __device__ __forceinline__ void cold_solve(
 #endif
 }
 
-template <int KPL, bool LAMOUT, bool PH, int TR>
+template <int KPL, bool LAMOUT, bool PH, int TR, int MF>
 __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1371,8 +1394,8 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_kernel(
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
     double* __restrict__ lam_out, PhaseSrc ps)
 {
-    cold_solve<KPL, LAMOUT, PH, TR>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
-                                     status_out, iters_out, polished_out, lam_out, ps);
+    cold_solve<KPL, LAMOUT, PH, TR, MF>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+                                         status_out, iters_out, polished_out, lam_out, ps);
 }
 
 // Small batches, N <= 64 (configs[0], one TimeVaryingDCMPlanner solve): the QP the active-set
@@ -1404,7 +1427,7 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_fused_ker
 // One wavefront per QP, fp64 facet rows in LDS.  From the shifted previous solution (xi rolled
 // out from its VRPs), guess = the facets the rollout violates plus those whose previous multiplier
 // exceeds the floor, then the fp64 passes (1.7 per window on average: no float search first).
-template <int KPL, bool LAMOUT, bool PH, int TR>
+template <int KPL, bool LAMOUT, bool PH, int TR, int MF>
 __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     KParams P, const double* __restrict__ xi_init, const double* __restrict__ omega,
     const double* __restrict__ xi_ref, const double* __restrict__ vrp_ref,
@@ -1420,8 +1443,8 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     // a problem whose previous solve failed (prev_status != 0) is not warm-started from it: it is
     // solved exactly as a cold launch solves it (the IPM's stage 2 treats it as cold too)
     if (P.ws_status != nullptr && P.ws_status[blockIdx.x] != 0) {
-        cold_solve<KPL, LAMOUT, PH, TR>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
-                                         status_out, iters_out, polished_out, lam_out, ps);
+        cold_solve<KPL, LAMOUT, PH, TR, MF>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+                                             status_out, iters_out, polished_out, lam_out, ps);
         return;
     }
     assume_pad<KPL, TR>(N);
@@ -1441,10 +1464,15 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     //      slab loads (one round, U per lane covers N M <= 128 x 8), then the knots' own loads,
     //      then the LDS stores, which wait for the slab loads only ----
     const int nA = N * M;
+    constexpr bool kWide = MF > kMaxFacets;   // 16 slots: the rows staged in rounds, up front
     constexpr int U = KPL == 2 ? 2 * kMaxFacets : kMaxFacets;   // one round: nA <= 1024 / 512
     double* sBE = smem + 3 * (size_t)M * S;                            // PH: [2][P]
     int32_t* sPh = reinterpret_cast<int32_t*>(sBE + 2 * (size_t)ps.P);  // PH: [N+1]
     if (PH) ph_stage_phases(ps, p, N, P.dt, lane, sBE, sPh);
+    if constexpr (kWide) {
+        if (PH) stage_rows_ph<KPL, U, true>(ps, sPh, p, N, M, S, NH, lane, reinterpret_cast<double*>(A2), Bv);
+        else stage_rows_rounds<KPL, U>(Ain, bin, p, N, M, S, NH, lane, reinterpret_cast<double*>(A2), Bv);
+    }
     // the rows' loads are issued after the knots' loads (vmcnt counts in issue order) and land in
     // LDS after the warm start's rollout, which does not read them
     double2 va[U];
@@ -1478,8 +1506,10 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
             Kj.xr1 = in.xr1;
         }
     }
-    if (PH) stage_rows_ph_issue<U>(ps, sPh, p, N, M, lane, va, vb);
-    else stage_rows_issue<U>(Ain, bin, p, lane, 0, nA, va, vb);
+    if constexpr (!kWide) {
+        if (PH) stage_rows_ph_issue<U>(ps, sPh, p, N, M, lane, va, vb);
+        else stage_rows_issue<U>(Ain, bin, p, lane, 0, nA, va, vb);
+    }
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
         AKnot& Kj = K[j];
@@ -1494,7 +1524,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     }
     const bool any_bad = __ballot(bad) != 0;
     AS_STAMP_ADD(1, t_start);
-    const LdsRows<double> R{A2, Bv, S, NH};
+    const LdsRows<double, MF> R{A2, Bv, S, NH};
 
     int status = 0;
     int npass = 0;   // active-set passes run (float + fp64), blf_dcm_mpc_solution.passes
@@ -1534,7 +1564,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
             K[j].x1 = x[j][1];
         }
     }
-    stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, nA, reinterpret_cast<double*>(A2), Bv);
+    if constexpr (!kWide) stage_rows_commit<KPL, U, double>(va, vb, M, S, NH, lane, 0, nA, reinterpret_cast<double*>(A2), Bv);
     __syncthreads();   // the LDS slabs (one wavefront: a wait for the stores)
     AS_STAMP_ADD(2, t_lq);
     if (any_bad) {
@@ -1579,7 +1609,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
 constexpr int64_t kFusedMaxBatch = 1024;
 constexpr int64_t kDppTreeMaxBatch = BLF_DPP_TREE_MAX_BATCH;
 
-template <int KPL>
+template <int KPL, int MF>
 blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const blf_dcm_mpc_warm_start* warm,
                       int64_t batch, const blf_dcm_mpc_solution* sol, double* lam_out, hipStream_t s,
                       const PhaseSrc* ps, bool* stage2_done)
@@ -1599,7 +1629,7 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
     constexpr int kAltTree = KPL == 2 ? kTreePad : kTreeDpp;   // the instantiated trees: this, kTreeKS
     const int tr = (KPL == 1 && batch <= kDppTreeMaxBatch) ? kTreeDpp
                    : (KPL == 2 && kp.N <= 2 * kWave - 2) ? kTreePad : kTreeKS;
-    if (KPL == 1 && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch &&
+    if (KPL == 1 && MF == kMaxFacets && warm == nullptr && ps == nullptr && batch <= kFusedMaxBatch &&
         qp_launch_mode().fuse_stage2.load(std::memory_order_relaxed)) {
         const size_t lds_f = std::max(lds, sizeof(double) * Lds(nullptr, kp.N, kp.M, 1).total);
         auto kern = lam_out ? dcm_mpc_cold_fused_kernel<true> : dcm_mpc_cold_fused_kernel<false>;
@@ -1612,7 +1642,7 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
         return check_hip(hipGetLastError(), "dcm_mpc_cold_fused_kernel launch");
     }
     if (warm == nullptr) {
-#define AS_COLD(L, H, D) dcm_mpc_cold_kernel<KPL, L, H, D>
+#define AS_COLD(L, H, D) dcm_mpc_cold_kernel<KPL, L, H, D, MF>
 #define AS_COLD_TR(D) (ps ? (lam_out ? AS_COLD(true, true, D) : AS_COLD(false, true, D)) \
                           : (lam_out ? AS_COLD(true, false, D) : AS_COLD(false, false, D)))
         auto kern = tr == kAltTree ? AS_COLD_TR(kAltTree) : AS_COLD_TR(kTreeKS);
@@ -1623,7 +1653,7 @@ blf_status launch_kpl(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
                            sol->vrp, sol->status, sol->iters, sol->polished, lam_out, src);
         return check_hip(hipGetLastError(), "dcm_mpc_cold_kernel launch");
     }
-#define AS_WARM(L, H, D) dcm_mpc_warm_kernel<KPL, L, H, D>
+#define AS_WARM(L, H, D) dcm_mpc_warm_kernel<KPL, L, H, D, MF>
 #define AS_WARM_TR(D) (ps ? (lam_out ? AS_WARM(true, true, D) : AS_WARM(false, true, D)) \
                           : (lam_out ? AS_WARM(true, false, D) : AS_WARM(false, false, D)))
     auto kern = tr == kAltTree ? AS_WARM_TR(kAltTree) : AS_WARM_TR(kTreeKS);
@@ -1671,8 +1701,16 @@ blf_status launch_dcm_mpc_as(const qp::KParams& kp, const blf_dcm_mpc_problem* p
     bool none = false;
     bool* done = stage2_done ? stage2_done : &none;
     *done = false;
-    if (kp.N <= kWave) return launch_kpl<1>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
-    if (kp.N <= 2 * kWave) return launch_kpl<2>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
+    // facet slots: 8, or 16 for phases of three or four contacts (twice the LDS per QP)
+    if (kp.M <= kMaxFacets) {
+        if (kp.N <= kWave) return launch_kpl<1, kMaxFacets>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
+        if (kp.N <= 2 * kWave) return launch_kpl<2, kMaxFacets>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
+    } else if (kp.M <= kMaxFacetsWide) {
+        if (kp.N <= kWave) return launch_kpl<1, kMaxFacetsWide>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
+        if (kp.N <= 2 * kWave) return launch_kpl<2, kMaxFacetsWide>(kp, pb, warm, batch, sol, lam_out, s, ps, done);
+    } else {
+        return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: %d facet slots > %d", kp.M, kMaxFacetsWide);
+    }
     return set_error(BLF_ERR_UNSUPPORTED, "active-set kernel: horizon %d > 128", kp.N);
 }
 

@@ -84,9 +84,9 @@ blf_status launch_nt(const KParams& kp, const blf_dcm_mpc_problem* pb,
 #define IPM_KERN(K) ((warm != nullptr) ? (lam_out ? K<NT, true, true, MF> : K<NT, true, false, MF>) \
                                        : (lam_out ? K<NT, false, true, MF> : K<NT, false, false, MF>))
     if (kp.list) {
-        // stage 2 runs only after the active-set kernels (N <= 128, at most kMaxFacets facet
-        // slots); at most kListGrid workgroups loop over the pending list
-        if constexpr (NT <= 2 * kWave && MF == kMaxFacets) {
+        // stage 2 runs only after the active-set kernels (N <= 128); at most kListGrid
+        // workgroups loop over the pending list
+        if constexpr (NT <= 2 * kWave) {
             hipLaunchKernelGGL(IPM_KERN(dcm_mpc_ipm_list_kernel), dim3((unsigned)std::min<int64_t>(batch, qp_launch_mode().list_grid)),
                                dim3(NT), lds, s, kp, pb->xi_init, pb->omega, pb->xi_ref, pb->vrp_ref, pb->A, pb->b,
                                pb->nfacets, warm ? warm->vrp : nullptr, warm ? warm->lambda : nullptr, sol->xi,
@@ -204,7 +204,8 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
     // solves the QPs its start certifies; the IPM kernel then takes only the rest (stage 2), from
     // scratch and without the start.  BLF_QP_SINGLE_KERNEL=1 keeps everything in the IPM kernel
     // (A/B and parity tests: both ways give the same bits).
-    if (kp.tol_polish > 0.0 && N <= 2 * kWave && kp.M <= kMaxFacets && !qp_launch_mode().single_kernel.load(std::memory_order_relaxed)) {
+    if (kp.tol_polish > 0.0 && N <= 2 * kWave && kp.M <= kMaxFacetsWide &&
+        !qp_launch_mode().single_kernel.load(std::memory_order_relaxed)) {
         bool stage2_done = false;
         set_pend(kp, l);
         const blf_status st = launch_dcm_mpc_as(kp, pb, warm, batch, sol, lam_out, s, nullptr, &stage2_done);
@@ -233,21 +234,6 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
         return set_error(BLF_ERR_UNSUPPORTED,
                          "phase-indexed solve: horizon %d > 128 or tol_polish = 0 (use blf_dcm_phase_expand "
                          "+ blf_dcm_mpc_solve_warm)", kp.N);
-    if (kp.M > kMaxFacets) {
-        // more facet slots than the active-set kernels hold (phases of up to four contacts): the
-        // window expanded into the caller's scratch, then the interior point kernel's solve of it
-        // (the same bits as blf_dcm_phase_expand + blf_dcm_mpc_solve_warm)
-        blf_status st = launch_phase_expand(ph->max_phases, ph->nphases, ph->begin, ph->end, ph->A, ph->b,
-                                            ph->nfacets, ph->ref, kp.M, start_knot, kp.dt, kp.N, batch, win->A,
-                                            win->b, win->nfacets, win->xi_ref, win->vrp_ref, s);
-        if (st != BLF_OK) return st;
-        st = check_hip(hipMemcpy2DAsync(win->omega, sizeof(double) * kp.N, omega, sizeof(double) * omega_stride,
-                                        sizeof(double) * kp.N, (size_t)batch, hipMemcpyDeviceToDevice, s),
-                       "phase-indexed solve: omega copy");
-        if (st != BLF_OK) return st;
-        const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
-        return launch_dcm_mpc(prm, &pw, warm, batch, sol, lam_out, s, l);
-    }
     PhaseSrc ps{};
     ps.P = ph->max_phases;
     ps.nphases = ph->nphases;

@@ -473,7 +473,7 @@ double orc_wave_tree_sum(const double* c, int n)
     return total;
 }
 
-#define MF 16   /* facet slots (max_facets <= 16; above 8 the device runs the IPM kernel alone) */
+#define MF 16   /* facet slots (max_facets <= 16) */
 #ifndef ORC_GUESS_PASSES
 #define ORC_GUESS_PASSES 8    /* active-set start: drop/add passes (kernel: kGuessPasses) */
 #endif
@@ -1868,8 +1868,8 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      * evaluates them (one wavefront, knot pairs per lane) when that kernel runs: 64 < N <= 128
      * with the start enabled (csrc/dcm_mpc_ipm.hip launch_dcm_mpc); the IPM iterations always in
      * the wavefront tree of the IPM kernel */
-    /* the active-set kernels run for N <= 128 with the polish on and at most 8 facet slots */
-    const int as_kernel = prm->tol_polish > 0.0 && N <= 2 * WV && !prm->single_kernel && M <= 8;
+    /* the active-set kernels run for N <= 128 with the polish on (8 or 16 facet slots) */
+    const int as_kernel = prm->tol_polish > 0.0 && N <= 2 * WV && !prm->single_kernel && M <= MF;
     w->pairs = (as_kernel && N > WV) ? 1 : 0;
     /* small batches, one knot per lane: the active-set kernels' DPP tree (prm->as_tree) */
     w->dpp = (as_kernel && N <= WV && prm->as_tree) ? 1 : 0;

@@ -18,7 +18,6 @@
 #include "blf_oracle.h"
 
 #define WV 64
-#define MF 8
 #ifndef ORC_GUESS_PASSES
 #define ORC_GUESS_PASSES 8
 #endif
@@ -583,7 +582,7 @@ static int passes32(s32* s)
             if (pc > 2) pc = vertex_pair32(s, k, km, cm, &pi1, &pi2);
             if (pc > 2) okp = 0;
             const int c = pc < 3 ? pc : 2;
-            pk[k] = c | (pi1 << 2) | (pi2 << 5);
+            pk[k] = c | (pi1 << 2) | (pi2 << 6);
             const float b2 = s->be[k] * s->be[k];
             float ax, ay, ab, ex, ey, eb;
             rowf(s, k, pi1, &ax, &ay, &ab);
@@ -613,7 +612,7 @@ static int passes32(s32* s)
         if (!riccati32(s, (const float (*)[3])E)) okp = 0;
         /* h */
         for (int k = 0; k < N; ++k) {
-            const int pc = pk[k] & 3, pi1 = (pk[k] >> 2) & 7;
+            const int pc = pk[k] & 3, pi1 = (pk[k] >> 2) & 15;
             const float b2 = s->be[k] * s->be[k];
             const float B00 = fmaf(b2, s->P00[k], P->Rw0);
             const float B01 = b2 * s->P01[k];
@@ -637,7 +636,7 @@ static int passes32(s32* s)
             s->r1[k] = s->r1[k] + dr[k][1];
             s->x0[k] = s->x0[k] + dx[k][0];
             s->x1[k] = s->x1[k] + dx[k][1];
-            const int pc = pk[k] & 3, pi1 = (pk[k] >> 2) & 7, pi2 = (pk[k] >> 5) & 7;
+            const int pc = pk[k] & 3, pi1 = (pk[k] >> 2) & 15, pi2 = (pk[k] >> 6) & 15;
             const float s0 = s->qx0[k] + vn[k][0];
             const float s1 = s->qx1[k] + vn[k][1];
             const float nu0 = F3(s->P00[k], dx[k][0], s->P01[k], dx[k][1], s0);

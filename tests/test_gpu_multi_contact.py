@@ -58,3 +58,32 @@ def test_three_contact_receding_horizon_vs_oracle(handle, oracle, poses, M, off)
         assert (st == 0).all(), s
         pg, po = got, ref
         xg, xo = got["xi"][:, 1].contiguous(), np.ascontiguousarray(xi[:, 1])
+
+
+@pytest.mark.parametrize("N,B", [(50, 64), (60, 2048), (40, 96)])
+def test_three_contact_cold_per_knot_vs_oracle(handle, oracle, N, B):
+    """The 16-slot active-set kernels on the per-knot input (blf_dcm_mpc_solve, cold; the expanded
+    window of a three-contact plan): status, solution, multipliers, polish flag and active-set
+    passes bit for bit against the oracle, which runs the same active-set start for 16 slots.
+    Knot pairs (N = 50, 60) and one knot per lane (N = 40), a batch past the DPP-tree limit."""
+    M = 16
+    plan = MC.plan(B, poses="spread", seed=5, xi_offset=0.05)
+    otab = CL.phase_table(plan, max_facets=M)
+    w = oracle.dcm_phase_expand(otab, 3, plan["dt"], N)
+    w.update(xi_init=np.ascontiguousarray(plan["xi_init"]), omega=np.ascontiguousarray(plan["omega"][:, 3:3 + N]))
+    assert w["nfacets"].max() > 8
+    dev = {k: torch.from_numpy(np.ascontiguousarray(w[k])).cuda() for k in
+           ("xi_init", "omega", "xi_ref", "vrp_ref", "A", "b", "nfacets")}
+    prm = native.default_params(N, max_facets=M, dt=plan["dt"])
+    got = handle.dcm_mpc_solve(dev, prm, lambda_out=True)
+    torch.cuda.synchronize()
+    oprm = oracle.default_params(N, max_facets=M, dt=plan["dt"])
+    pol = np.zeros(B, np.int32)
+    pas = np.zeros(B, np.int32)
+    st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(w, params=oprm, threads=8, polished=pol, passes=pas,
+                                                           device_batch=B)
+    ref = dict(status=st, xi=xi, vrp=vrp, iters=it, lam=lam, polished=pol, passes=pas)
+    for k in OUT_KEYS + ("passes",):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), ref[k], err_msg=k)
+    assert (st == 0).all()
+    assert (pas > 0).all()   # the active-set kernels ran (not the interior point kernel alone)
