@@ -2206,6 +2206,9 @@ done:
     if (iters_out) *iters_out = it;
     if (polished_out) *polished_out = polished;
     if (passes_out) *passes_out = as_passes;
+#ifdef ORC_STATS   /* diagnostic builds only: the solve's IPM iterations and all polish passes */
+    fprintf(stderr, "ORC_STATS it %d as_passes %d all_polish_passes %d status %d\n", it, as_passes, w->npass, status);
+#endif
     if (lam_out) {   /* final multipliers, [N][M], zero in unused facet slots */
         for (int k = 0; k < N; ++k)
             for (int i = 0; i < M; ++i)
