@@ -152,7 +152,8 @@ struct Smem {
         o_jo = take(3 * (size_t)n);
         // subtree sums [j] (joint j's subtree) and [n] (every link); later the pivot-column
         // buffers of the factorization (two sets of up to 4 columns, 8 NV)
-        const size_t cp = (size_t)kCompS * (n + 1);
+        // (the articulated-body solve's per-joint slots, 27 n, use the same space)
+        const size_t cp = (size_t)kCompS * (n + 1) > (size_t)27 * n ? (size_t)kCompS * (n + 1) : (size_t)28 * n;
         const size_t cb = 8 * (size_t)(NV > 32 ? NV : 32);   // (BLF_FBD_COLFIX: 2 CB NVMAX)
         o_comp = take(cp > cb ? cp : cb);
         o_sax = take(kSax * (size_t)NV);
@@ -700,12 +701,195 @@ __device__ __forceinline__ void fbd_kinematics(const Model& m, const Smem& S, co
     else fbd_kinematics_levels<HW, PRI>(m, S, bv, jvel, bp, bR, jp, T);
 }
 
+// ---- The articulated-body solve (round 5): nu_dot without M, its factorization or the
+//      substitutions.  With every spatial quantity about the world origin no transform is needed
+//      between a link and its parent, and the accelerations relative to nu_dot = 0 satisfy
+//        da_c = da_p + s_j qdd_j   (joint j moves link c = j + 1 from its parent link p),
+//        f_c  = F_c + I_c da_c     (F_c: step 3's force at nu_dot = 0, contacts subtracted),
+//        s_j^T (sum of f over the subtree of c) = tau_j,
+//      which the articulated inertias IA and biases pA solve in one inward and one outward sweep
+//      over the tree levels (lane per joint):
+//        IA_c = I_c + sum_children (IA_k - U_k U_k^T / D_k),  pA_c = F_c + sum_children (pA_k + U_k u_k / D_k),
+//        U_j = IA_c s_j,  D_j = s_j^T U_j,  u_j = tau_j - s_j^T pA_c;
+//        base: IA_0 da_0 = -pA_0 (6 x 6, every lane), qdd_B from da_0 = S_B qdd_B;
+//        outward: qdd_j = (u_j - U_j^T da_p) / D_j,  da_c = da_p + s_j qdd_j.
+//      The same solution as M nu_dot = rhs (Featherstone's ABA; the oracle's Jacobian form agrees
+//      to rounding, tests/test_gpu_fb_dynamics.py at 1e-9 relative).  A model with a mass-matrix
+//      regularisation (reg != NULL) keeps the factorization, which that term needs.
+// 6 x 6 symmetric matrices as their upper triangle, row-major (21 entries).
+__host__ __device__ constexpr int s6(int i, int j)
+{
+    return i <= j ? i * 6 - i * (i - 1) / 2 + (j - i) : j * 6 - j * (j - 1) / 2 + (i - j);
+}
+constexpr int kAbaSlot = 27 + (1 - kPad);   // Ia (21) | pa (6), odd stride (27); later da (6)
+
+// the spatial inertia about the origin (m, h, Ibar xx xy xz yy yz zz) as a 6 x 6 on (w; u)
+__device__ __forceinline__ void spatial6(const double* si, double (&I)[21])
+{
+    const double m = si[0], h0 = si[1], h1 = si[2], h2 = si[3];
+    I[s6(0, 0)] = si[4]; I[s6(0, 1)] = si[5]; I[s6(0, 2)] = si[6];
+    I[s6(1, 1)] = si[7]; I[s6(1, 2)] = si[8]; I[s6(2, 2)] = si[9];
+    I[s6(0, 3)] = 0.0; I[s6(0, 4)] = -h2; I[s6(0, 5)] = h1;
+    I[s6(1, 3)] = h2; I[s6(1, 4)] = 0.0; I[s6(1, 5)] = -h0;
+    I[s6(2, 3)] = -h1; I[s6(2, 4)] = h0; I[s6(2, 5)] = 0.0;
+    I[s6(3, 3)] = m; I[s6(3, 4)] = 0.0; I[s6(3, 5)] = 0.0;
+    I[s6(4, 4)] = m; I[s6(4, 5)] = 0.0; I[s6(5, 5)] = m;
+}
+
+template <int HW, bool PRI>
+__device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const double* tau, const Topo& T, int lane)
+{
+    const int n = m.n;
+    const bool jl = lane < n;
+    double* slot = S.comp();   // [n][kAbaSlot]; the subtree sums / pivot columns are not used here
+    bool ok = true;
+    // this lane's joint axis s = (w; u) and torque
+    double sv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double tq = 0.0;
+    if (jl) {
+        const double* z = S.jz() + 3 * lane;
+        if (PRI && m.jtype[lane] == BLF_JOINT_PRISMATIC) {
+            sv[3] = z[0]; sv[4] = z[1]; sv[5] = z[2];
+        } else {
+            sv[0] = z[0]; sv[1] = z[1]; sv[2] = z[2];
+            cross3(S.jo() + 3 * lane, z, sv + 3);
+        }
+        tq = tau[lane];
+    }
+    double U[6], uD = 0.0, iD = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) U[a] = 0.0;
+    // inward sweep, deepest joints first
+    for (int lev = T.maxdepth; lev >= 0; --lev) {
+        if (jl && T.depth == lev) {
+            const double* k = S.link() + kLinkRec * (lane + 1);
+            double IA[21], pA[6];
+            spatial6(k + kSI, IA);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) pA[a] = k[kSF + a];
+            for (unsigned long long b = T.cmask; b; b &= b - 1) {
+                const double* c = slot + kAbaSlot * __builtin_ctzll(b);
+#pragma unroll
+                for (int e = 0; e < 21; ++e) IA[e] = IA[e] + c[e];
+#pragma unroll
+                for (int a = 0; a < 6; ++a) pA[a] = pA[a] + c[21 + a];
+            }
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                double t = 0.0;
+#pragma unroll
+                for (int b = 0; b < 6; ++b) t = fma(IA[s6(a, b)], sv[b], t);
+                U[a] = t;
+            }
+            double D = 0.0, sp = 0.0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                D = fma(sv[a], U[a], D);
+                sp = fma(sv[a], pA[a], sp);
+            }
+            ok = ok && D > 0.0;
+            iD = 1.0 / D;
+            uD = (tq - sp) * iD;
+            double* o = slot + kAbaSlot * lane;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const double Ua = U[a] * iD;
+#pragma unroll
+                for (int b = a; b < 6; ++b) o[s6(a, b)] = fma(-Ua, U[b], IA[s6(a, b)]);
+                o[21 + a] = fma(U[a], uD, pA[a]);
+            }
+        }
+        wave_sync();
+    }
+    // the base: IA_0 da_0 = -pA_0 (every lane, from the base's children's slots)
+    double da[6];
+    {
+        double IA[21], pA[6];
+        const double* k = S.link();
+        spatial6(k + kSI, IA);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) pA[a] = k[kSF + a];
+        for (unsigned long long b = T.bmask; b; b &= b - 1) {
+            const double* c = slot + kAbaSlot * __builtin_ctzll(b);
+#pragma unroll
+            for (int e = 0; e < 21; ++e) IA[e] = IA[e] + c[e];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) pA[a] = pA[a] + c[21 + a];
+        }
+        // LDL^T of IA_0 in registers, then the two substitutions
+        double L[21], d[6], x[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double dj = IA[s6(j, j)];
+#pragma unroll
+            for (int c = 0; c < j; ++c) dj = dj - (L[s6(j, c)] * L[s6(j, c)]) * d[c];
+            ok = ok && dj > 0.0;
+            d[j] = dj;
+            const double idj = 1.0 / dj;
+#pragma unroll
+            for (int i = j + 1; i < 6; ++i) {
+                double t = IA[s6(i, j)];
+#pragma unroll
+                for (int c = 0; c < j; ++c) t = t - (L[s6(i, c)] * L[s6(j, c)]) * d[c];
+                L[s6(i, j)] = t * idj;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double t = -pA[i];
+#pragma unroll
+            for (int c = 0; c < i; ++c) t = t - L[s6(i, c)] * x[c];
+            x[i] = t;
+        }
+#pragma unroll
+        for (int i = 5; i >= 0; --i) {
+            double t = x[i] / d[i];
+#pragma unroll
+            for (int c = i + 1; c < 6; ++c) t = t - L[s6(c, i)] * da[c];
+            da[i] = t;
+        }
+    }
+    // outward sweep: qdd_j and the joint's child link's da, shallowest first
+    double qdd = 0.0;
+    for (int lev = 0; lev <= T.maxdepth; ++lev) {
+        if (jl && T.depth == lev) {
+            double dp[6];
+            const double* src = slot + kAbaSlot * (T.P > 0 ? T.P - 1 : 0);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) dp[a] = T.P > 0 ? src[a] : da[a];
+            double Ud = 0.0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) Ud = fma(U[a], dp[a], Ud);
+            qdd = fma(-Ud, iD, uD);
+            double* o = slot + kAbaSlot * lane;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) o[a] = fma(sv[a], qdd, dp[a]);
+        }
+        wave_sync();
+    }
+    // nu_dot: base (linear: da_0's u - p_B x w; angular: w), then the joints
+    const double* pB = S.link() + kP;
+    if (lane < 6) {
+        const double w[3] = {da[0], da[1], da[2]};
+        double pw[3];
+        cross3(pB, w, pw);
+        // (selects, not a lane-indexed array: that would live in scratch)
+        const double lin = lane == 0 ? da[3] - pw[0] : lane == 1 ? da[4] - pw[1] : da[5] - pw[2];
+        const double ang = lane == 3 ? da[0] : lane == 4 ? da[1] : da[2];
+        S.rhs()[lane] = lane < 3 ? lin : ang;
+    }
+    if (jl) S.rhs()[6 + lane] = qdd;
+    wave_sync();
+    const Half<HW> H;
+    return H.ballot(!ok) == 0ull;
+}
+
 // One evaluation of the dynamics for the system whose state sits in LDS (bv, jv, bp, bR, jp).
 // Leaves the generalized acceleration in S.rhs() and returns false if the factorization failed.
 // NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
 // registers).  Lane j < n owns joint j in steps 1, 2 and 5; lane i < NV owns row / column i in
 // steps 6-9.
-template <int NVMAX, int HW, bool PRI, int FOLD = 0, bool LM = false, bool CS = false>
+template <int NVMAX, int HW, bool PRI, int FOLD = 0, bool LM = false, bool CS = false, bool ABA = false>
 __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const double* bv,
                                          const double* jvel, const double* bp, const double* bR,
                                          const double* jp, const double* tau, const Contacts& ct,
@@ -854,6 +1038,13 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         link_step();
         wave_sync();
         FSTAMP_ADD(2, f_t2b);
+    }
+    if constexpr (ABA) {   // steps 5-9 replaced by the articulated-body solve (no regularisation)
+        FSTAMP(f_t4a);
+        const bool ok = fbd_aba<HW, PRI>(m, S, tau, T, lane);
+        FSTAMP_ADD(7, f_t4a);
+        FSTAMP_ADD(9, f_t0);
+        return ok;
     }
     FSTAMP(f_t4);
     // 5. subtree sums of the spatial inertias and (link - contact) forces.  DFS-ordered models
@@ -1273,7 +1464,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     return ok;
 }
 
-template <int NVMAX, int HW, bool PRI>
+template <int NVMAX, int HW, bool PRI, bool ABA>
 __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state st,
                                                           const double* __restrict__ tau,
                                                           Contacts ct, const double* reg,
@@ -1301,7 +1492,7 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
     }
     wave_sync();
     const Topo T = build_topo<HW>(m, S);
-    const bool ok = fbd_eval<NVMAX, HW, PRI>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+    const bool ok = fbd_eval<NVMAX, HW, PRI, 0, false, false, ABA>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                         tau + (int64_t)n * q, ct, q, reg, T);
     if (!active) return;
     const double nan = __builtin_nan("");
@@ -1325,10 +1516,7 @@ struct Impedance {
     const double *kp, *kd, *qref;
 };
 
-// NFIX > 0: a model of exactly NFIX joints (the launcher checks): the joint count is a compile-time
-// constant, so every `< n` / `< NV` bound of the unrolled loops folds away instead of living in
-// scalar registers across the Euler loop (BLF_FBD_NFIX).
-template <int NVMAX, int HW, bool PRI, int NFIX = 0>
+template <int NVMAX, int HW, bool PRI, bool ABA>
 // Two systems per wavefront (HW = 32) keep more state live per wave: capping it at 256 VGPRs for
 // two waves per SIMD spills (9.40 ms per c5 period), one wave per SIMD does not (8.29 ms, against
 // 9.29 ms with one system per wavefront at two waves per SIMD; tools/ab_c5.sh).
@@ -1338,7 +1526,6 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
                                                           int32_t nsteps, double dT, double dT_last,
                                                           Impedance imp, int64_t batch)
 {
-    if constexpr (NFIX > 0) m.n = NFIX;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const Half<HW> H;
     const int n = m.n, NV = n + 6;
@@ -1430,7 +1617,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
             wave_sync();
             tq = S.tq();
         }
-        ok = fbd_eval<NVMAX, HW, PRI, BLF_FBD_FOLD, kLM, kCS>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
+        ok = fbd_eval<NVMAX, HW, PRI, BLF_FBD_FOLD, kLM, kCS, ABA>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n,
                                  tq, ct, q, reg, T) && ok;
         if (lane == 0) fbk_rot_rate(m.rho, loc + 9 + n, loc + 3, dR);
         wave_sync();
@@ -1577,6 +1764,17 @@ Contacts to_contacts(const blf_fb_contacts* c)
 
 size_t fbd_lds_bytes(int n, int C) { return sizeof(double) * Smem(nullptr, n, C).total; }
 
+// The articulated-body solve (fbd_aba) unless the model carries a mass-matrix regularisation,
+// which needs M itself; BLF_FBD_ABA=0 keeps the factorization for every model (A/B only).
+static bool use_aba(const double* reg)
+{
+    static const bool on = [] {
+        const char* e = getenv("BLF_FBD_ABA");
+        return !(e && e[0] == '0');
+    }();
+    return on && reg == nullptr;
+}
+
 blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, const double* tau,
                                const blf_fb_contacts* ct, const double* reg, int64_t batch,
                                const blf_fb_state* out, hipStream_t s)
@@ -1584,15 +1782,16 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
     if (batch == 0) return BLF_OK;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
-    const bool pri = md->joint_type != nullptr;
+    const bool pri = md->joint_type != nullptr, aba = use_aba(reg);
+#define FBD_DYN(NV, HW) (pri ? (aba ? fbd_dynamics_kernel<NV, HW, true, true> : fbd_dynamics_kernel<NV, HW, true, false>) \
+                             : (aba ? fbd_dynamics_kernel<NV, HW, false, true> : fbd_dynamics_kernel<NV, HW, false, false>))
     if (md->ndof + 6 <= 32)   // two systems per wavefront
-        hipLaunchKernelGGL((pri ? fbd_dynamics_kernel<32, 32, true> : fbd_dynamics_kernel<32, 32, false>),
-                           dim3((unsigned)ceil_div(batch, 2)), dim3(kWave), 2 * lds, s, to_model(md), *st, tau, c,
-                           reg, *out, batch);
+        hipLaunchKernelGGL(FBD_DYN(32, 32), dim3((unsigned)ceil_div(batch, 2)), dim3(kWave), 2 * lds, s,
+                           to_model(md), *st, tau, c, reg, *out, batch);
     else
-        hipLaunchKernelGGL((pri ? fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6, kWave, true>
-                                : fbd_dynamics_kernel<BLF_FBD_MAX_DOFS + 6, kWave, false>),
-                           dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, *out, batch);
+        hipLaunchKernelGGL(FBD_DYN(BLF_FBD_MAX_DOFS + 6, kWave), dim3((unsigned)batch), dim3(kWave), lds, s,
+                           to_model(md), *st, tau, c, reg, *out, batch);
+#undef FBD_DYN
     return check_hip(hipGetLastError(), "fbd_dynamics_kernel launch");
 }
 
@@ -1602,37 +1801,21 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
                             const blf_joint_impedance* impedance)
 {
     if (batch == 0) return BLF_OK;
-    const int64_t wv2 = ceil_div(batch, 2), wv1 = batch;
     const size_t mb32 = BLF_FBD_LDSMODEL ? sizeof(double) * fbd_model_block<32>() : 0;
     const Contacts c = to_contacts(ct);
     const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     Impedance imp{nullptr, nullptr, nullptr};
     if (impedance) imp = Impedance{impedance->kp, impedance->kd, impedance->q_ref};
-#ifndef BLF_FBD_SMALL_HW
-#define BLF_FBD_SMALL_HW 32   // diagnostic builds: 64 = one small model per wavefront (A/B)
-#endif
-    const bool pri = md->joint_type != nullptr;
-#ifndef BLF_FBD_NFIX
-#define BLF_FBD_NFIX 0   // A/B builds: a joint count with its own instantiation (0: none)
-#endif
-    if (BLF_FBD_NFIX > 0 && md->ndof == BLF_FBD_NFIX && BLF_FBD_NFIX + 6 <= 32 && BLF_FBD_SMALL_HW == 32)
-        hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>
-                                : fbd_euler_kernel<32, 32, false, (BLF_FBD_NFIX + 6 <= 32 ? BLF_FBD_NFIX : 0)>),
-                           dim3((unsigned)wv2), dim3(kWave), 2 * lds + mb32, s, to_model(md), *st, tau, c,
-                           reg, nsteps, dT, dT_last, imp, batch);
-    else if (md->ndof + 6 <= 32 && BLF_FBD_SMALL_HW == 32)   // two systems per wavefront
-        hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, 32, true> : fbd_euler_kernel<32, 32, false>),
-                           dim3((unsigned)wv2), dim3(kWave), 2 * lds + mb32, s, to_model(md), *st, tau, c,
-                           reg, nsteps, dT, dT_last, imp, batch);
-    else if (md->ndof + 6 <= 32)   // one system per wavefront, NV <= 32 rows
-        hipLaunchKernelGGL((pri ? fbd_euler_kernel<32, kWave, true> : fbd_euler_kernel<32, kWave, false>),
-                           dim3((unsigned)wv1), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
-                           dT_last, imp, batch);
+    const bool pri = md->joint_type != nullptr, aba = use_aba(reg);
+#define FBD_EUL(NV, HW) (pri ? (aba ? fbd_euler_kernel<NV, HW, true, true> : fbd_euler_kernel<NV, HW, true, false>) \
+                             : (aba ? fbd_euler_kernel<NV, HW, false, true> : fbd_euler_kernel<NV, HW, false, false>))
+    if (md->ndof + 6 <= 32)   // two systems per wavefront
+        hipLaunchKernelGGL(FBD_EUL(32, 32), dim3((unsigned)ceil_div(batch, 2)), dim3(kWave), 2 * lds + mb32, s,
+                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp, batch);
     else
-        hipLaunchKernelGGL((pri ? fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, true>
-                                : fbd_euler_kernel<BLF_FBD_MAX_DOFS + 6, kWave, false>),
-                           dim3((unsigned)wv1), dim3(kWave), lds, s, to_model(md), *st, tau, c, reg, nsteps, dT,
-                           dT_last, imp, batch);
+        hipLaunchKernelGGL(FBD_EUL(BLF_FBD_MAX_DOFS + 6, kWave), dim3((unsigned)batch), dim3(kWave), lds, s,
+                           to_model(md), *st, tau, c, reg, nsteps, dT, dT_last, imp, batch);
+#undef FBD_EUL
     return check_hip(hipGetLastError(), "fbd_euler_kernel launch");
 }
 
