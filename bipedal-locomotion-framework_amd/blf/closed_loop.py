@@ -62,6 +62,12 @@ def period_final_time(dt, dT):
 # test's foot size; stiffness and damping for a 50 kg robot on two 0.12 x 0.09 m soles (about
 # 1 cm of sink) that explicit Euler at dT = 1 ms integrates stably
 CONTACT_PARAMS = (0.12, 0.09, 2.0e6, 2.0e4)
+# The interior point iteration cap of the loop's plans (TimeVaryingDCMPlanner's "max_iterations";
+# the solver default is 50).  A window the active-set start cannot certify -- an uncapturable DCM
+# state, multipliers ~1e7 -- can need more from its warm start: tests/golden/c5_device_windows_r05.npz
+# holds one that takes 92 (31 cold), on the device's trajectory of bench.py's loop.  Only such
+# windows run that long; every other window stops at its certificate.
+MAX_ITER = 100
 
 
 class ClosedLoop:
@@ -70,7 +76,7 @@ class ClosedLoop:
     problem dict with a horizon of at least horizon + the number of periods to run."""
 
     def __init__(self, h, model, plan, states, horizon=100, dT=0.001, law=None,
-                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None):
+                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None, max_iter=MAX_ITER):
         import torch
         self.h, self.N, self.dT, self.stream = h, horizon, dT, stream
         dev = torch.device("cuda", h.device)
@@ -94,6 +100,7 @@ class ClosedLoop:
         self.omega = t(plan["omega"])
         self.params = native.default_params(horizon, max_facets=self.table["phase_b"].shape[2])
         self.params.tol_polish = tol_polish     # TimeVaryingDCMPlanner's warm-start trigger
+        self.params.max_iter = max_iter         # (MAX_ITER: the uncapturable windows' iteration cap)
         self.params.dt = self.dt                # the knots of the plan are the QP's knots
         self.com = torch.empty((self.B, 6), dtype=torch.float64, device=dev)
         self.xi = torch.empty((self.B, 2), dtype=torch.float64, device=dev)

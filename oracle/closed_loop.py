@@ -111,7 +111,7 @@ class OracleLoop:
         self.cparams = np.tile(np.asarray(contact_params, np.float64), (C, 1))
         self.table = phase_table(plan)
         self.omega = plan["omega"]
-        self.params = O.default_params(horizon, tol_polish=tol_polish)
+        self.params = O.default_params(horizon, tol_polish=tol_polish, max_iter=100)   # blf/closed_loop.py MAX_ITER
         self.prev = None
         self.s = 0
 
