@@ -16,6 +16,9 @@ from blf import problems as P        # noqa: E402
 from blf import robot                # noqa: E402
 
 
+INTS = ("nfacets", "prev_status", "robot", "period", "status", "iters")
+
+
 def main():
     B, N, periods = 16384, 100, 23
     model = robot.humanoid24()
@@ -48,7 +51,7 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     if keep["robot"]:
         np.savez(os.path.join(ROOT, "gpurun_out", "c5_device_failures.npz"),
-                 **{k: np.asarray(v) for k, v in keep.items()})
+                 **{k: np.asarray(v, dtype=np.int32 if k in INTS else None) for k, v in keep.items()})
     print("captured", len(keep["robot"]))
 
 
