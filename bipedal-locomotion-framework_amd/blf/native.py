@@ -28,7 +28,8 @@ EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_s
             "blf_dcm_mpc_flops_per_iter",
             "blf_contact_model_eval", "blf_contact_point_wrench", "blf_fbk_dynamics",
             "blf_fbk_euler_integrate", "blf_fbd_dynamics", "blf_fbd_euler_integrate",
-            "blf_fb_dcm", "blf_dcm_posture_reference", "blf_fbd_euler_integrate_impedance"]
+            "blf_fb_dcm", "blf_dcm_posture_reference", "blf_fbd_euler_integrate_impedance",
+            "blf_fb_frame_state"]
 # entry points removed in round 5 (measured slower, never the default; tests/test_abi.py checks
 # that the library no longer exports them)
 REMOVED = ["blf_set_qp_split_batch", "blf_stream_create_cu_range", "blf_stream_destroy",
@@ -54,8 +55,12 @@ class FbState(ctypes.Structure):
                 ("joint_pos", _vp)]
 
 
+CONTACT_CONTINUOUS, CONTACT_WRENCH = 0, 1   # blf_fb_contacts.law (BLF_CONTACT_*)
+
+
 class FbContacts(ctypes.Structure):
-    _fields_ = [("ncontacts", _i32), ("frame", _vp), ("params", _vp), ("null_pose", _vp)]
+    _fields_ = [("ncontacts", _i32), ("frame", _vp), ("params", _vp), ("null_pose", _vp),
+                ("law", _vp), ("wrench", _vp)]
 
 
 class PostureLaw(ctypes.Structure):
@@ -189,6 +194,8 @@ def lib():
         L.blf_fbd_euler_integrate_impedance.argtypes = [
             _vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), ctypes.POINTER(JointImpedance),
             ctypes.POINTER(FbContacts), _vp, _i64, _f64, _f64, _f64, _vp]
+        L.blf_fb_frame_state.argtypes = [_vp, ctypes.POINTER(FbModel), ctypes.POINTER(FbState), _i32,
+                                         _vp, _i64, _vp, _vp, _vp]
         L.blf_dcm_mpc_flops_per_iter.restype = _f64
         L.blf_set_qp_launch_mode.argtypes = [_i32, _i32]
         for name in EXPORTED:
@@ -768,12 +775,18 @@ class Handle:
         c.frame = _ptr(contacts["frame"], torch.int32, (C,), "frame")
         c.params = _ptr(contacts["params"], torch.float64, (C, 4), "params")
         c.null_pose = _ptr(contacts["null_pose"], torch.float64, (B, C, 12), "null_pose")
+        if contacts.get("law") is not None:
+            c.law = _ptr(contacts["law"], torch.int32, (C,), "law")
+            w = contacts.get("wrench")   # required by the library (checked there)
+            c.wrench = _ptr(w, torch.float64, (B, C, 6), "wrench") if w is not None else None
         return c
 
     def fbd_dynamics(self, dm, state, torque, contacts=None, mass_reg=None, stream=None):
         """FloatingBaseDynamicalSystem::dynamics for a batch.  state: dict of device tensors
         (base_vel [B,6], joint_vel [B,n], base_pos [B,3], base_rot [B,3,3], joint_pos [B,n]);
-        torque [B,n]; contacts: dict(frame [C] int32, params [C,4], null_pose [B,C,12]).
+        torque [B,n]; contacts: dict(frame [C] int32, params [C,4], null_pose [B,C,12]) and
+        optionally law [C] int32 (CONTACT_CONTINUOUS / CONTACT_WRENCH) with wrench [B,C,6] (the
+        CONTACT_WRENCH contacts' (force, torque), mixed representation at the frame).
         Returns the derivative with the same keys (base_vel -> base acceleration, ...)."""
         torch = _torch()
         B, n = state["joint_pos"].shape
@@ -802,6 +815,24 @@ class Handle:
                                              ctypes.byref(ct), reg, B, float(t0), float(t1),
                                              float(dT), _stream(stream)))
         return state
+
+    def fb_frame_state(self, dm, state, frames, pose=None, twist=None, stream=None):
+        """blf_fb_frame_state: world transform pose [B,K,12] = (p, R row-major) and mixed twist
+        [B,K,6] = (v, w) of the frames [K] (int32 device tensor) of every system -- the state a
+        CONTACT_WRENCH contact model is evaluated at."""
+        torch = _torch()
+        B, n = state["joint_pos"].shape
+        K = frames.shape[0]
+        dev = state["joint_pos"].device
+        pose = pose if pose is not None else torch.empty((B, K, 12), dtype=torch.float64, device=dev)
+        twist = twist if twist is not None else torch.empty((B, K, 6), dtype=torch.float64, device=dev)
+        _check(lib().blf_fb_frame_state(self._h, ctypes.byref(dm.c),
+                                        ctypes.byref(self._fb_state(state, B, n)), K,
+                                        _ptr(frames, torch.int32, (K,), "frames"), B,
+                                        _ptr(pose, torch.float64, (B, K, 12), "pose"),
+                                        _ptr(twist, torch.float64, (B, K, 6), "twist"),
+                                        _stream(stream)))
+        return pose, twist
 
     # ---- config 5: the closed loop's maps (DESIGN.md section 11) ----------------------------------
     def fb_dcm(self, dm, state, omega=None, column=0, com=None, xi=None, stream=None):

@@ -563,6 +563,8 @@ static blf_status check_fbd(const char* fn, blf_handle* handle, const blf_fb_mod
     BLF_REQUIRE(C == 0 || (contacts->frame && contacts->params && contacts->null_pose &&
                            model->frame_link && model->frame_pose && model->nframes > 0),
                 "%s: null contact buffer", fn);
+    BLF_REQUIRE(C == 0 || contacts->law == nullptr || batch == 0 || contacts->wrench != nullptr,
+                "%s: contact laws given without the wrench buffer", fn);
     if (fbd_lds_bytes(model->ndof, C) > 160 * 1024)
         return set_error(BLF_ERR_UNSUPPORTED, "%s: model too large for one workgroup's LDS", fn);
     return BLF_OK;
@@ -602,6 +604,28 @@ blf_status blf_fb_dcm(blf_handle* handle, const blf_fb_model* model, const blf_f
     BLF_REQUIRE(xi == nullptr || omega0 != nullptr, "blf_fb_dcm: xi requested without omega0");
     BLF_REQUIRE(omega0_stride >= 0, "blf_fb_dcm: negative omega0 stride");
     return launch_fb_dcm(model, state, omega0, omega0_stride, batch, com, xi, (hipStream_t)stream);
+}
+
+blf_status blf_fb_frame_state(blf_handle* handle, const blf_fb_model* model,
+                              const blf_fb_state* state, int32_t nframes, const int32_t* frames,
+                              int64_t batch, double* pose, double* twist, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_fb_frame_state: null handle");
+    BLF_REQUIRE(model != nullptr && state != nullptr, "blf_fb_frame_state: null model / state");
+    BLF_REQUIRE(model->ndof >= 1 && model->ndof <= BLF_FBD_MAX_DOFS,
+                "blf_fb_frame_state: ndof=%d outside [1, %d]", model->ndof, BLF_FBD_MAX_DOFS);
+    BLF_REQUIRE(batch >= 0 && nframes >= 0, "blf_fb_frame_state: negative size");
+    BLF_REQUIRE(model->parent && model->joint_origin && model->joint_rot && model->joint_axis &&
+                    model->link_mass && model->link_com && model->link_inertia,
+                "blf_fb_frame_state: null model array");
+    BLF_REQUIRE(nframes == 0 || (frames && model->frame_link && model->frame_pose && model->nframes > 0),
+                "blf_fb_frame_state: null frame buffer");
+    BLF_REQUIRE(batch == 0 || nframes == 0 ||
+                    ((pose || twist) && state->base_vel && state->joint_vel && state->base_pos &&
+                     state->base_rot && state->joint_pos),
+                "blf_fb_frame_state: null state / output buffer");
+    return launch_fb_frame_state(model, state, nframes, frames, batch, pose, twist,
+                                 (hipStream_t)stream);
 }
 
 blf_status blf_dcm_posture_reference(blf_handle* handle, const blf_posture_law* law,

@@ -121,6 +121,9 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
 size_t fbd_lds_bytes(int n, int C);
 blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const double* omega0,
                          int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s);
+blf_status launch_fb_frame_state(const blf_fb_model* md, const blf_fb_state* st, int32_t K,
+                                 const int32_t* frames, int64_t batch, double* pose, double* twist,
+                                 hipStream_t s);
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,
                                     int64_t vstride, int64_t batch, double* qref, hipStream_t s);
 blf_status launch_fbk_euler(int n, double rho, double* pos, double* rot, double* joints,

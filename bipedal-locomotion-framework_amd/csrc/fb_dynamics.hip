@@ -213,7 +213,19 @@ struct Contacts {
     const int32_t* frame;
     const double* params;
     const double* null_pose;   // [B][C][12]
+    const int32_t* law;        // [C] or null (every contact BLF_CONTACT_CONTINUOUS)
+    const double* wrench;      // [B][C][6] the BLF_CONTACT_WRENCH contacts' wrenches
 };
+
+// Whether contact c applies the caller's wrench (BLF_CONTACT_WRENCH) instead of the
+// ContinuousContactModel law
+#ifndef BLF_FBD_LAWS   // 0: the continuous law only (A/B of the law branch, tools/gpu_r05i.sh)
+#define BLF_FBD_LAWS 1
+#endif
+__device__ __forceinline__ bool given_wrench(const Contacts& ct, int c)
+{
+    return BLF_FBD_LAWS && ct.law != nullptr && ct.law[c] == BLF_CONTACT_WRENCH;
+}
 
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* o)
 {
@@ -884,6 +896,26 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
     return H.ballot(!ok) == 0ull;
 }
 
+// World transform pose = (p, R row-major) and mixed twist tw = (v, w) of the frame whose pose in
+// its link is fp, from the link's kinematics record k (the getWorldTransform / getFrameVel the
+// reference hands each contact model, FloatingBaseSystemDynamics.cpp:225-226)
+__device__ __forceinline__ void frame_state(const double* k, const double* fp, double* pose, double* tw)
+{
+    const double* R = k + kR;
+    double d[3], t1[3];
+    for (int a = 0; a < 3; ++a) {
+        pose[a] = k[kP + a] + ((R[3 * a] * fp[0] + R[3 * a + 1] * fp[1]) + R[3 * a + 2] * fp[2]);
+        for (int b = 0; b < 3; ++b)
+            pose[3 + 3 * a + b] = (R[3 * a] * fp[3 + b] + R[3 * a + 1] * fp[6 + b]) + R[3 * a + 2] * fp[9 + b];
+        d[a] = pose[a] - k[kP + a];
+    }
+    cross3(k + kW, d, t1);
+    for (int a = 0; a < 3; ++a) {
+        tw[a] = k[kV + a] + t1[a];
+        tw[3 + a] = k[kW + a];
+    }
+}
+
 // One evaluation of the dynamics for the system whose state sits in LDS (bv, jv, bp, bR, jp).
 // Leaves the generalized acceleration in S.rhs() and returns false if the factorization failed.
 // NVMAX >= n + 6 bounds the unrolled factorization loops (each lane keeps its row of M in
@@ -994,22 +1026,13 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             l = m.flink[f];
             fp = m.fpose + 12 * f;
         }
-        const double* k = S.link() + kLinkRec * l;
-        const double* R = k + kR;
-        double pose[12], tw[6], d[3], t1[3];
-        for (int a = 0; a < 3; ++a) {
-            pose[a] = k[kP + a] + ((R[3 * a] * fp[0] + R[3 * a + 1] * fp[1]) + R[3 * a + 2] * fp[2]);
-            for (int b = 0; b < 3; ++b)
-                pose[3 + 3 * a + b] = (R[3 * a] * fp[3 + b] + R[3 * a + 1] * fp[6 + b]) + R[3 * a + 2] * fp[9 + b];
-            d[a] = pose[a] - k[kP + a];
-        }
-        cross3(k + kW, d, t1);
-        for (int a = 0; a < 3; ++a) {
-            tw[a] = k[kV + a] + t1[a];
-            tw[3 + a] = k[kW + a];
-        }
+        double pose[12], tw[6];
+        frame_state(S.link() + kLinkRec * l, fp, pose, tw);
         double* sc = S.cscr() + kCs * c;
-        if constexpr (CS)
+        if (given_wrench(ct, c)) {   // any ContactModel, evaluated by the caller
+            const double* gw = ct.wrench + (sys * ct.C + c) * 6;
+            for (int a = 0; a < 6; ++a) sc[3 + a] = gw[a];
+        } else if constexpr (CS)
             contact_wrench(S.cst() + 25 * ct.C + 4 * c, tw, pose, S.cst() + 13 * ct.C + 12 * c, sc + 3);
         else
             contact_wrench(ct.params + 4 * c, tw, pose, ct.null_pose + (sys * ct.C + c) * 12, sc + 3);
@@ -1705,6 +1728,45 @@ __global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, co
     }
 }
 
+// The world transform and mixed twist of K frames of every system (blf_fb_frame_state): the state
+// a caller hands a ContactModel it evaluates itself (BLF_CONTACT_WRENCH).  One wavefront per
+// system: the forward kinematics of fbd_eval, then lane per frame with fbd_eval's own frame_state.
+template <bool PRI>
+__global__ __launch_bounds__(64) void fb_frame_state_kernel(Model m, blf_fb_state st, int K,
+                                                            const int32_t* __restrict__ frames,
+                                                            double* __restrict__ pose,
+                                                            double* __restrict__ twist)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int n = m.n;
+    const Smem S(smem, n, 0);
+    const int64_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n
+    for (int i = lane; i < 18 + 2 * n; i += kWave) {
+        double v;
+        if (i < 6) v = st.base_vel[6 * q + i];
+        else if (i < 6 + n) v = st.joint_vel[(int64_t)n * q + (i - 6)];
+        else if (i < 9 + n) v = st.base_pos[3 * q + (i - 6 - n)];
+        else if (i < 18 + n) v = st.base_rot[9 * q + (i - 9 - n)];
+        else v = st.joint_pos[(int64_t)n * q + (i - 18 - n)];
+        loc[i] = v;
+    }
+    wave_sync();
+    const Topo T = build_topo<kWave>(m, S);
+    fbd_kinematics<kWave, PRI>(m, S, loc, loc + 6, loc + 6 + n, loc + 9 + n, loc + 18 + n, T);
+    wave_sync();
+    for (int c = lane; c < K; c += kWave) {
+        const int f = frames[c];
+        double p[12], tw[6];
+        frame_state(S.link() + kLinkRec * m.flink[f], m.fpose + 12 * f, p, tw);
+        if (pose)
+            for (int a = 0; a < 12; ++a) pose[(q * K + c) * 12 + a] = p[a];
+        if (twist)
+            for (int a = 0; a < 6; ++a) twist[(q * K + c) * 6 + a] = tw[a];
+    }
+}
+
 // The closed loop's plan -> robot map: the joint references held over one
 // control period,
 //   q_ref_j = q_nom_j + lean_j0 (r0_x - c_x) + lean_j1 (r0_y - c_y)
@@ -1757,6 +1819,8 @@ Contacts to_contacts(const blf_fb_contacts* c)
     o.frame = c ? c->frame : nullptr;
     o.params = c ? c->params : nullptr;
     o.null_pose = c ? c->null_pose : nullptr;
+    o.law = c ? c->law : nullptr;
+    o.wrench = c ? c->wrench : nullptr;
     return o;
 }
 
@@ -1828,6 +1892,18 @@ blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const d
                        dim3(kWave), lds, s, to_model(md), *st,
                        omega0, ostride, com, xi);
     return check_hip(hipGetLastError(), "fb_dcm_kernel launch");
+}
+
+blf_status launch_fb_frame_state(const blf_fb_model* md, const blf_fb_state* st, int32_t K,
+                                 const int32_t* frames, int64_t batch, double* pose, double* twist,
+                                 hipStream_t s)
+{
+    if (batch == 0 || K == 0) return BLF_OK;
+    const size_t lds = fbd_lds_bytes(md->ndof, 0);
+    hipLaunchKernelGGL((md->joint_type ? fb_frame_state_kernel<true> : fb_frame_state_kernel<false>),
+                       dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, (int)K, frames,
+                       pose, twist);
+    return check_hip(hipGetLastError(), "fb_frame_state_kernel launch");
 }
 
 blf_status launch_posture_reference(const blf_posture_law* law, const double* com, const double* vrp,

@@ -11,9 +11,13 @@
  * setKinDyn(); this build has no iDynTree, so the robot is given as a kinematic tree with
  * setRobotModel() (blf::RobotModel, the layout of blf/robot.py) and the rigid-body terms are
  * computed on the device (blf_fbd_dynamics / blf_fbd_euler_integrate, include/blf/blf_c.h).
- * Contacts must be ContinuousContactModel instances (their formula is evaluated in the kernel).
- * Divergence: the contact models are not left in the frame state after dynamics() (the reference
- * calls contactModel->setState as a side effect, FloatingBaseSystemDynamics.cpp:225-226).
+ * Contacts may hold any ContactModel.  A ContinuousContactModel is evaluated in the kernel
+ * (BLF_CONTACT_CONTINUOUS); any other model is set to the frame state the device computes
+ * (blf_fb_frame_state) and its getContactWrench() is passed to the kernel (BLF_CONTACT_WRENCH):
+ * forwardEulerIntegrate() then launches one Euler step at a time, so that the wrench is taken at
+ * every step's start state as in the reference.  dynamics() leaves every contact model in its
+ * frame's state (the reference's setState side effect, FloatingBaseSystemDynamics.cpp:225-226);
+ * the one-launch forwardEulerIntegrate() of ContinuousContactModel-only contacts does not.
  */
 #ifndef BLF_BIPEDAL_LOCOMOTION_SYSTEM_FLOATING_BASE_SYSTEM_DYNAMICS_H
 #define BLF_BIPEDAL_LOCOMOTION_SYSTEM_FLOATING_BASE_SYSTEM_DYNAMICS_H
@@ -82,12 +86,17 @@ class FloatingBaseDynamicalSystem
     bool m_hasModel{false};
     bool m_useMassMatrixRegularizationTerm{false};
     blf::RobotModel m_model;
-    blf::DeviceBuffer<int32_t> m_dParent, m_dFrameLink, m_dContactFrame, m_dJointType;
+    blf::DeviceBuffer<int32_t> m_dParent, m_dFrameLink, m_dContactFrame, m_dJointType, m_dContactLaw;
     blf::DeviceBuffer<double> m_dOrigin, m_dRot, m_dAxis, m_dMass, m_dCom, m_dInertia, m_dFramePose;
     blf::DeviceBuffer<double> m_dReg, m_dState, m_dTau, m_dContactParams, m_dNullPose, m_dOut;
+    blf::DeviceBuffer<double> m_dContactWrench, m_dFrameOut;
+    std::vector<std::shared_ptr<ContactModels::ContactModel>> m_contactModels;
+    bool m_hostContacts{false};   /**< a contact model the kernel cannot evaluate */
 
     bool prepare(const char* where, blf_fb_model& model, blf_fb_state& state,
                  blf_fb_contacts& contacts);
+    bool updateContactModels(const char* where, const blf_fb_model& model,
+                             const blf_fb_state& state, bool wrenches);
 
 public:
     bool initalize(std::weak_ptr<ParametersHandler::IParametersHandler> handler) final;

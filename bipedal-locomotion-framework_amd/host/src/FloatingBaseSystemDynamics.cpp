@@ -253,16 +253,17 @@ bool FloatingBaseDynamicalSystem::prepare(const char* where, blf_fb_model& model
     for (int i = 0; i < 3; ++i) st[6 + n + i] = basePosition[i];
     for (int i = 0; i < 9; ++i) st[9 + n + i] = baseOrientation[i];
     for (std::size_t i = 0; i < n; ++i) st[18 + n + i] = jointPositions[i];
-    std::vector<int32_t> frames;
+    std::vector<int32_t> frames, laws;
     std::vector<double> params, nulls;
+    m_contactModels.clear();
+    m_hostContacts = false;
     for (const auto& c : contactWrenches)
     {
         auto ptr = c.contactModel().lock();
-        auto cm = std::dynamic_pointer_cast<ContactModels::ContinuousContactModel>(ptr);
-        if (cm == nullptr)
+        if (ptr == nullptr)
         {
             std::cerr << "[" << where << "] The contact model associated to the frame " << c.index()
-                      << " has expired or is not a ContinuousContactModel." << std::endl;
+                      << " has been expired." << std::endl;
             return false;
         }
         if (c.index() < 0 || c.index() >= static_cast<int>(m_model.frameLink.size()))
@@ -271,10 +272,28 @@ bool FloatingBaseDynamicalSystem::prepare(const char* where, blf_fb_model& model
             return false;
         }
         frames.push_back(c.index());
-        params.insert(params.end(), {cm->length(), cm->width(), cm->springCoeff(), cm->damperCoeff()});
-        const auto np = cm->nullForceTransform().packed();
-        nulls.insert(nulls.end(), np.begin(), np.end());
+        // a ContinuousContactModel is evaluated in the kernel; any other model by its own
+        // getContactWrench() at the frame state the device computes (BLF_CONTACT_WRENCH)
+        auto cm = std::dynamic_pointer_cast<ContactModels::ContinuousContactModel>(ptr);
+        if (cm != nullptr)
+        {
+            laws.push_back(BLF_CONTACT_CONTINUOUS);
+            params.insert(params.end(), {cm->length(), cm->width(), cm->springCoeff(), cm->damperCoeff()});
+            const auto np = cm->nullForceTransform().packed();
+            nulls.insert(nulls.end(), np.begin(), np.end());
+        } else
+        {
+            laws.push_back(BLF_CONTACT_WRENCH);
+            m_hostContacts = true;
+            params.insert(params.end(), 4, 0.0);
+            const auto np = blf::Transform::Identity().packed();
+            nulls.insert(nulls.end(), np.begin(), np.end());
+        }
+        m_contactModels.push_back(ptr);
     }
+    if (m_hostContacts
+        && (!m_dContactLaw.upload(laws) || !m_dContactWrench.resize(6 * laws.size())))
+        return false;
     if (!m_dState.upload(st) || !m_dTau.upload(jointTorques.data(), n)
         || !m_dContactFrame.upload(frames) || !m_dContactParams.upload(params)
         || !m_dNullPose.upload(nulls))
@@ -303,7 +322,45 @@ bool FloatingBaseDynamicalSystem::prepare(const char* where, blf_fb_model& model
     contacts.frame = m_dContactFrame.data();
     contacts.params = m_dContactParams.data();
     contacts.null_pose = m_dNullPose.data();
+    contacts.law = m_hostContacts ? m_dContactLaw.data() : nullptr;
+    contacts.wrench = m_hostContacts ? m_dContactWrench.data() : nullptr;
     return true;
+}
+
+// The reference's per-contact `contactPtr->setState(getFrameVel, getWorldTransform)` (FloatingBase
+// SystemDynamics.cpp:225-226) at the device's frame state; then, when `wrenches` is set, the
+// BLF_CONTACT_WRENCH contacts' getContactWrench() uploaded for the next launch.
+bool FloatingBaseDynamicalSystem::updateContactModels(const char* where, const blf_fb_model& model,
+                                                      const blf_fb_state& state, bool wrenches)
+{
+    const std::size_t C = m_contactModels.size();
+    if (C == 0) return true;
+    blf_handle* h = blf::threadHandle();
+    if (!m_dFrameOut.resize(18 * C)) return false;
+    double* pose = m_dFrameOut.data();
+    if (!blf::report(blf_fb_frame_state(h, &model, &state, static_cast<int32_t>(C),
+                                        m_dContactFrame.data(), 1, pose, pose + 12 * C, nullptr),
+                     where))
+        return false;
+    std::vector<double> host(18 * C), wrench(6 * C, 0.0);
+    if (!m_dFrameOut.download(host.data(), host.size())) return false;
+    for (std::size_t c = 0; c < C; ++c)
+    {
+        blf::Transform T;
+        blf::Twist tw;
+        for (int i = 0; i < 3; ++i) T.position[i] = host[12 * c + i];
+        for (int i = 0; i < 9; ++i) T.rotation[i] = host[12 * c + 3 + i];
+        for (int i = 0; i < 6; ++i) tw[i] = host[12 * C + 6 * c + i];
+        m_contactModels[c]->setState(tw, T);
+        if (wrenches
+            && std::dynamic_pointer_cast<ContactModels::ContinuousContactModel>(m_contactModels[c])
+                   == nullptr)
+        {
+            const blf::Wrench& w = m_contactModels[c]->getContactWrench();
+            for (int i = 0; i < 6; ++i) wrench[6 * c + i] = w[i];
+        }
+    }
+    return !wrenches || m_dContactWrench.upload(wrench);
 }
 
 bool FloatingBaseDynamicalSystem::dynamics(const double& time, StateDerivativeType& stateDerivative)
@@ -314,7 +371,9 @@ bool FloatingBaseDynamicalSystem::dynamics(const double& time, StateDerivativeTy
     blf_fb_state state;
     blf_fb_contacts contacts;
     blf_handle* h = blf::threadHandle();
-    if (h == nullptr || !prepare(where, model, state, contacts)) return false;
+    if (h == nullptr || !prepare(where, model, state, contacts)
+        || !updateContactModels(where, model, state, m_hostContacts))
+        return false;
     const std::size_t n = m_actuatedDoFs;
     if (!m_dOut.resize(18 + 2 * n)) return false;
     double* o = m_dOut.data();
@@ -350,12 +409,34 @@ bool FloatingBaseDynamicalSystem::forwardEulerIntegrate(double initialTime, doub
     blf_fb_contacts contacts;
     blf_handle* h = blf::threadHandle();
     if (h == nullptr || !prepare(where, model, state, contacts)) return false;
-    if (!blf::report(blf_fbd_euler_integrate(h, &model, &state, m_dTau.data(), &contacts,
-                                             m_useMassMatrixRegularizationTerm ? m_dReg.data()
-                                                                               : nullptr,
-                                             1, initialTime, finalTime, dT, nullptr),
-                     where))
-        return false;
+    const double* reg = m_useMassMatrixRegularizationTerm ? m_dReg.data() : nullptr;
+    if (!m_hostContacts)
+    {
+        // every contact a ContinuousContactModel: the whole integration in one launch
+        if (!blf::report(blf_fbd_euler_integrate(h, &model, &state, m_dTau.data(), &contacts, reg,
+                                                 1, initialTime, finalTime, dT, nullptr),
+                         where))
+            return false;
+    } else
+    {
+        // a model the device cannot evaluate: its wrench from the host before every step, as the
+        // reference's dynamics() calls getContactWrench() at each step's start state; one launch
+        // of one step each (the device's schedule, ForwardEuler.tpp:18-49)
+        int32_t iterations = 0;
+        double dT_last = 0.0, t_last = 0.0;
+        if (!blf::report(blf_step_schedule(initialTime, finalTime, dT, &iterations, &dT_last, &t_last),
+                         where))
+            return false;
+        for (int32_t it = 0; it < iterations; ++it)
+        {
+            const double step = it + 1 < iterations ? dT : dT_last;
+            if (!updateContactModels(where, model, state, true)
+                || !blf::report(blf_fbd_euler_integrate(h, &model, &state, m_dTau.data(), &contacts,
+                                                        reg, 1, 0.0, step, step, nullptr),
+                                where))
+                return false;
+        }
+    }
     const std::size_t n = m_actuatedDoFs;
     std::vector<double> host(18 + 2 * n);
     if (!m_dState.download(host.data(), host.size())) return false;

@@ -869,6 +869,111 @@ static void testFloatingBaseDynamics()
     REQUIRE(system->setMassMatrixRegularization(blf::MatrixXd(9, 9)));
 }
 
+// A ContactModel the kernel does not know (BLF_CONTACT_WRENCH): it forwards to a
+// ContinuousContactModel, so the dynamics must equal the device law's, and it counts the
+// setState calls (one per dynamics() and per Euler step, FloatingBaseSystemDynamics.cpp:225).
+class ForwardingContact final : public ContactModels::ContactModel
+{
+    std::shared_ptr<ContactModels::ContinuousContactModel> m_inner;
+
+    void computeContactWrench() final { m_contactWrench = m_inner->getContactWrench(); }
+    void computeAutonomousDynamics() final { m_autonomousDynamics = m_inner->getAutonomousDynamics(); }
+    void computeControlMatrix() final { m_controlMatrix = m_inner->getControlMatrix(); }
+    void computeRegressor() final { m_regressor = m_inner->getRegressor(); }
+    bool initializePrivate(std::weak_ptr<ParametersHandler::IParametersHandler> handler) final
+    {
+        return m_inner->initialize(handler);
+    }
+    void setStatePrivate(const blf::Twist& twist, const blf::Transform& transform) final
+    {
+        ++states;
+        m_inner->setState(twist, transform);
+    }
+    void setNullForceTransformPrivate(const blf::Transform& transform) final
+    {
+        m_inner->setNullForceTransform(transform);
+    }
+
+public:
+    int states{0};
+    ForwardingContact() : m_inner(std::make_shared<ContactModels::ContinuousContactModel>()) {}
+};
+
+static void testFloatingBaseDynamicsAnyContactModel()
+{
+    auto params = std::make_shared<ParametersHandler::StdImplementation>();
+    params->setParameter("length", 0.12);
+    params->setParameter("width", 0.09);
+    params->setParameter("spring_coeff", 3.0e4);
+    params->setParameter("damper_coeff", 300.0);
+    params->setParameter("rho", 0.01);
+    blf::Transform nullT;
+    nullT.position = {{0.01, -0.02, 0.5}};
+    auto continuous = std::make_shared<ContactModels::ContinuousContactModel>();
+    auto forwarding = std::make_shared<ForwardingContact>();
+    auto second = std::make_shared<ContactModels::ContinuousContactModel>();
+    for (ContactModels::ContactModel* c : {static_cast<ContactModels::ContactModel*>(continuous.get()),
+                                           static_cast<ContactModels::ContactModel*>(forwarding.get()),
+                                           static_cast<ContactModels::ContactModel*>(second.get())})
+    {
+        REQUIRE(c->initialize(params));
+        c->setNullForceTransform(nullT);
+    }
+    const blf::Matrix3 R0 = rpy(0.05, -0.1, 0.2);
+    blf::VectorXd tau(3, 0.0), q(3, 0.0), qd(3, 0.0);
+    q[0] = 0.2; q[1] = -0.4; q[2] = 0.3;
+    qd[0] = 0.3; qd[1] = -0.2; qd[2] = 0.5;
+    tau[0] = 1.0; tau[2] = -0.5;
+    const blf::Vector6 nu{{0.1, -0.05, -0.2, 0.3, 0.1, -0.2}};
+    auto device = std::make_shared<FloatingBaseDynamicalSystem>();
+    auto mixed = std::make_shared<FloatingBaseDynamicalSystem>();
+    for (auto& s : {device, mixed})
+    {
+        REQUIRE(s->initalize(params));
+        REQUIRE(s->setRobotModel(chainModel()));
+        REQUIRE(s->setState({nu, qd, blf::Vector3{{0.0, 0.0, 0.85}}, R0, q}));
+    }
+    // the same two ContinuousContactModel wrenches on frame 0: both on the device, or one of them
+    // through the forwarding model (its wrench evaluated on the host at the device's frame state)
+    REQUIRE(device->setControlInput({tau, {ContactWrench(0, continuous), ContactWrench(0, second)}}));
+    REQUIRE(mixed->setControlInput({tau, {ContactWrench(0, forwarding), ContactWrench(0, second)}}));
+    FloatingBaseDynamicalSystem::StateDerivativeType d0, d1;
+    REQUIRE(device->dynamics(0.0, d0));
+    REQUIRE(mixed->dynamics(0.0, d1));
+    REQUIRE(forwarding->states == 1);
+    double scale = 0.0, diff = 0.0;
+    for (int i = 0; i < 6; ++i)
+    {
+        scale = std::max(scale, std::abs(std::get<0>(d0)[i]));
+        diff = std::max(diff, std::abs(std::get<0>(d0)[i] - std::get<0>(d1)[i]));
+    }
+    for (int j = 0; j < 3; ++j) diff = std::max(diff, std::abs(std::get<1>(d0)[j] - std::get<1>(d1)[j]));
+    REQUIRE(scale > 1.0 && diff <= 1e-10 * scale);   // the contacts act (|base acc| >> 0) and agree
+    // dynamics() leaves every contact model in its frame's state (the reference's side effect):
+    // the device-evaluated model and the forwarded one now report the same wrench
+    const blf::Wrench wc = continuous->getContactWrench(), wf = forwarding->getContactWrench();
+    for (int i = 0; i < 6; ++i) REQUIRE(std::abs(wc[i] - wf[i]) <= 1e-9 * (1.0 + std::abs(wc[i])));
+    // ForwardEuler: one host evaluation per step (5 steps), the same trajectory as the device law's
+    ForwardEuler<FloatingBaseDynamicalSystem> e0(0.01), e1(0.01);
+    REQUIRE(e0.setDynamicalSystem(device) && e1.setDynamicalSystem(mixed));
+    REQUIRE(e0.integrate(0.0, 0.05) && e1.integrate(0.0, 0.05));
+    REQUIRE(forwarding->states == 1 + 5);
+    const auto& s0 = e0.getSolution();
+    const auto& s1 = e1.getSolution();
+    double sd = 0.0;
+    for (int i = 0; i < 6; ++i) sd = std::max(sd, std::abs(std::get<0>(s0)[i] - std::get<0>(s1)[i]));
+    for (int i = 0; i < 3; ++i)
+    {
+        sd = std::max(sd, std::abs(std::get<1>(s0)[i] - std::get<1>(s1)[i]));
+        sd = std::max(sd, std::abs(std::get<4>(s0)[i] - std::get<4>(s1)[i]));
+        sd = std::max(sd, std::abs(std::get<2>(s0)[i] - std::get<2>(s1)[i]));
+    }
+    REQUIRE(sd <= 1e-9);
+    // a contact without a model is refused (ContactWrench owns its model, as the reference's)
+    REQUIRE(mixed->setControlInput({tau, {ContactWrench(0, nullptr)}}));
+    REQUIRE_FALSE(mixed->dynamics(0.0, d1));
+}
+
 // ---- fixed joints (blf::reduceFixedJoints): host-only checks of the merge -------------------------
 // Whole-body mass and centre of mass at q = 0 (base at the origin) of a model, by a forward pass.
 static std::array<double, 4> massAndCom(const blf::RobotModel& m)
@@ -1078,6 +1183,7 @@ int main(int argc, char** argv)
         {"FloatingBaseSystemKinematics", true, testFloatingBaseKinematics},
         {"IntegratorTest: floating base kinematics (literal)", true, testIntegratorKinematicsLiteral},
         {"FloatingBaseDynamicalSystem", true, testFloatingBaseDynamics},
+        {"FloatingBaseDynamicalSystem, any ContactModel", true, testFloatingBaseDynamicsAnyContactModel},
         {"Fixed joints (model merge)", false, testFixedJoints},
         {"Fixed / prismatic joints (device)", true, testFixedJointsDevice},
     };

@@ -427,15 +427,38 @@ typedef struct blf_fb_state {
     double* joint_pos;  /* [B][n]  */
 } blf_fb_state;
 
-/* Contacts of the control input (the reference's std::vector<ContactWrench>): a
- * ContinuousContactModel on each listed frame, updated with the frame's world transform and
- * mixed velocity before its wrench is mapped through the frame Jacobian. */
+/* Contacts of the control input (the reference's std::vector<ContactWrench>, each a frame index
+ * and a std::weak_ptr<ContactModel>; FloatingBaseSystemDynamics.cpp:198-228 maps every contact's
+ * getContactWrench() through the frame Jacobian).  Each contact follows one of two laws:
+ *   BLF_CONTACT_CONTINUOUS  a ContinuousContactModel (params, null_pose), updated on the device
+ *                           with the frame's world transform and mixed velocity at every
+ *                           evaluation, as the reference's setState + getContactWrench;
+ *   BLF_CONTACT_WRENCH      any other ContactModel: the caller evaluates it (its setState from
+ *                           blf_fb_frame_state, then getContactWrench) and passes the wrench,
+ *                           (force, torque) in the mixed representation at the frame; held
+ *                           constant over one blf_fbd_euler_integrate call (the C++ adapter
+ *                           integrates step by step when a contact has this law).
+ * law == NULL: every contact BLF_CONTACT_CONTINUOUS; any law value other than BLF_CONTACT_WRENCH
+ * is taken as continuous.  params and null_pose are required for every contact (ignored for
+ * BLF_CONTACT_WRENCH ones), wrench whenever law is given. */
+#define BLF_CONTACT_CONTINUOUS 0
+#define BLF_CONTACT_WRENCH     1
 typedef struct blf_fb_contacts {
     int32_t ncontacts;            /* 0..BLF_FBD_MAX_CONTACTS                                  */
     const int32_t* frame;         /* [C] frame indices                                       */
     const double* params;         /* [C][4] (length, width, spring_coeff, damper_coeff)      */
     const double* null_pose;      /* [B][C][12] null-force transforms                        */
+    const int32_t* law;           /* [C] BLF_CONTACT_* or NULL (all continuous)              */
+    const double* wrench;         /* [B][C][6] wrenches of the BLF_CONTACT_WRENCH contacts   */
 } blf_fb_contacts;
+
+/* The world transform pose [B][K][12] = (p, R row-major) and the mixed velocity twist [B][K][6]
+ * = (v, w) of K frames of every system (either output may be NULL): what the reference hands a
+ * contact model through kinDyn getWorldTransform / getFrameVel (FloatingBaseSystemDynamics.cpp:
+ * 225-226) before it asks for the wrench, for the caller's BLF_CONTACT_WRENCH models.            */
+blf_status blf_fb_frame_state(blf_handle* handle, const blf_fb_model* model,
+                              const blf_fb_state* state, int32_t nframes, const int32_t* frames,
+                              int64_t batch, double* pose, double* twist, void* stream);
 
 /* FloatingBaseDynamicalSystem::dynamics for a batch:
  *   nu_dot = LLT(M [+ mass_reg]) \ (-h + sum_c J_c^T w_c + [0; tau]),  dp = v_B,

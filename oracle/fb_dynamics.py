@@ -133,11 +133,17 @@ def frame_state(model, K, f):
     return pf, Rf, vel, J
 
 
+CONTACT_WRENCH = 1   # blf_fb_contacts.law: the caller's wrench instead of the continuous law
+
+
 def dynamics(model, state, i, contacts=(), contact_params=None, null_poses=None, rho=0.01,
-             reg=None, gravity=G):
+             reg=None, gravity=G, laws=None, wrenches=None):
     """FloatingBaseDynamicalSystem::dynamics for system i of a state batch.  contacts: frame
-    indices; contact_params [C][4] (L, W, k, b); null_poses [C][12].  Returns (base_acc[6],
-    joint_acc[n], dpos[3], drot[3,3], djoint[n])."""
+    indices; contact_params [C][4] (L, W, k, b); null_poses [C][12]; laws [C] (None: every
+    contact a ContinuousContactModel) with wrenches [C][6], the (force, torque) a CONTACT_WRENCH
+    contact's model returns (mapped through J_c^T like any ContactModel's wrench,
+    FloatingBaseSystemDynamics.cpp:198-228).  Returns (base_acc[6], joint_acc[n], dpos[3],
+    drot[3,3], djoint[n])."""
     s = {k: v[i] for k, v in state.items()}
     K = kinematics(model, s["base_pos"], s["base_rot"], s["joint_pos"], s["base_vel"], s["joint_vel"])
     M, h = mass_and_bias(model, K, gravity)
@@ -145,7 +151,10 @@ def dynamics(model, state, i, contacts=(), contact_params=None, null_poses=None,
     for c, f in enumerate(contacts):
         pf, Rf, vel, J = frame_state(model, K, f)
         pose = np.concatenate([pf, Rf.reshape(-1)])
-        wrench = O.contact_eval(contact_params[c], vel, pose, null_poses[c])[0]
+        if laws is not None and laws[c] == CONTACT_WRENCH:
+            wrench = np.asarray(wrenches[c], dtype=np.float64)
+        else:
+            wrench = O.contact_eval(contact_params[c], vel, pose, null_poses[c])[0]
         known = known + J.T @ wrench
     known[6:] += s["joint_torque"]
     A = M + (reg if reg is not None else 0.0)

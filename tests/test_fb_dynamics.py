@@ -180,3 +180,33 @@ def test_fixed_joints_reject_inconsistent_models():
     short = dict(MODEL, link_mass=np.asarray(MODEL["link_mass"])[:-1])
     with pytest.raises(ValueError, match="link_mass"):
         robot.reduce_fixed_joints(short, FIXED)
+
+
+def test_given_wrench_law_is_the_jacobian_transpose_map():
+    """A BLF_CONTACT_WRENCH contact (any ContactModel's wrench, FloatingBaseSystemDynamics.cpp:
+    198-228): nu_dot(w) - nu_dot(0) = M^-1 J_c^T w, and the continuous model's own wrench given
+    this way reproduces the continuous law."""
+    st = robot.random_states(MODEL, 2, seed=17)
+    frames = np.array([0, 1], dtype=np.int32)
+    params = np.array([[0.12, 0.09, 3.0e4, 300.0]] * 2)
+    null = np.zeros((2, 12))
+    null[:, 3:] = np.eye(3).reshape(-1)
+    w = np.array([[10.0, -5.0, 200.0, 1.0, -2.0, 0.5], [-3.0, 4.0, 150.0, 0.2, 0.1, -0.3]])
+    kw = dict(contacts=frames, contact_params=params, null_poses=null)
+    laws = np.array([F.CONTACT_WRENCH, F.CONTACT_WRENCH])
+    a1 = F.dynamics(MODEL, st, 0, laws=laws, wrenches=w, **kw)
+    a0 = F.dynamics(MODEL, st, 0, laws=laws, wrenches=np.zeros((2, 6)), **kw)
+    s = {k: v[0] for k, v in st.items()}
+    K = F.kinematics(MODEL, s["base_pos"], s["base_rot"], s["joint_pos"], s["base_vel"], s["joint_vel"])
+    M, _ = F.mass_and_bias(MODEL, K)
+    rhs = sum(F.frame_state(MODEL, K, f)[3].T @ w[c] for c, f in enumerate(frames))
+    d = np.linalg.solve(M, rhs)
+    got = np.concatenate([a1[0] - a0[0], a1[1] - a0[1]])
+    np.testing.assert_allclose(got, d, rtol=1e-9, atol=1e-9 * np.abs(d).max())
+    cont = F.dynamics(MODEL, st, 0, **kw)
+    wc = []
+    for c, f in enumerate(frames):
+        pf, Rf, vel, _ = F.frame_state(MODEL, K, f)
+        wc.append(O.contact_eval(params[c], vel, np.concatenate([pf, Rf.reshape(-1)]), null[c])[0])
+    given = F.dynamics(MODEL, st, 0, laws=laws, wrenches=np.array(wc), **kw)
+    np.testing.assert_array_equal(given[1], cont[1])

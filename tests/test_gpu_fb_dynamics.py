@@ -220,3 +220,113 @@ def test_fbd_prismatic_joints_vs_oracle(handle, HWkind):
                                 contact_params=host["params"], null_poses=host["null_pose"][i])
         for k in native.FB_STATE_KEYS:
             assert rel_err(got[k][i], ref[k]) < TOL, k
+
+
+# ---- contact laws (blf_fb_contacts.law): any ContactModel through its wrench --------------------
+def test_fb_frame_state_vs_oracle(handle):
+    """blf_fb_frame_state: world transform and mixed twist of the sole frames, the state the
+    reference hands each contact model (FloatingBaseSystemDynamics.cpp:225-226)."""
+    B = 24
+    st = robot.random_states(MODEL, B, seed=31)
+    dm = handle.fb_model(MODEL)
+    frames = np.array([1, 0, 1], dtype=np.int32)
+    pose, twist = handle.fb_frame_state(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS},
+                                        _d(frames, torch.int32))
+    pose, twist = pose.cpu().numpy(), twist.cpu().numpy()
+    for i in range(0, B, 5):
+        K = F.kinematics(MODEL, st["base_pos"][i], st["base_rot"][i], st["joint_pos"][i],
+                         st["base_vel"][i], st["joint_vel"][i])
+        for c, f in enumerate(frames):
+            pf, Rf, vel, _ = F.frame_state(MODEL, K, f)
+            np.testing.assert_allclose(pose[i, c], np.concatenate([pf, Rf.reshape(-1)]), rtol=0, atol=1e-12)
+            np.testing.assert_allclose(twist[i, c], vel, rtol=0, atol=1e-12 * max(1.0, np.abs(vel).max()))
+
+
+def _mixed_contacts(B, seed):
+    """Contact 0 a ContinuousContactModel, contact 1 BLF_CONTACT_WRENCH with a random wrench."""
+    host, dev = contacts_for(B, seed=seed)
+    rng = np.random.default_rng(seed + 100)
+    wrench = rng.normal(size=(B, 2, 6)) * np.array([40.0, 40.0, 300.0, 5.0, 5.0, 2.0])
+    law = np.array([native.CONTACT_CONTINUOUS, native.CONTACT_WRENCH], dtype=np.int32)
+    host = dict(host, law=law, wrench=wrench)
+    dev = dict(dev, law=_d(law, torch.int32), wrench=_d(wrench))
+    return host, dev
+
+
+@pytest.mark.parametrize("HWkind", ["two_per_wave", "one_per_wave"])
+def test_fbd_mixed_contact_laws_vs_oracle(handle, HWkind):
+    """A continuous contact and a given-wrench contact (any other ContactModel, evaluated by the
+    caller) in one launch: dynamics and a short Euler integration against the numpy oracle."""
+    model = MODEL if HWkind == "two_per_wave" else robot.with_joint_types(MODEL, prismatic=PRISMATIC)
+    if HWkind == "one_per_wave":   # NV > 32: one system per wavefront
+        model = dict(model)
+        extra = 4
+        torso = model["names"].index("torso_pitch")
+        model["n"] = model["n"] + extra
+        model["parent"] = np.concatenate([model["parent"], np.full(extra, torso)]).astype(np.int32)
+        model["joint_origin"] = np.concatenate([model["joint_origin"], np.tile([[0.0, 0.01, 0.05]], (extra, 1))])
+        model["joint_rot"] = np.concatenate([model["joint_rot"], np.tile(np.eye(3), (extra, 1, 1))])
+        model["joint_axis"] = np.concatenate([model["joint_axis"], np.tile([[0.0, 0.0, 1.0]], (extra, 1))])
+        model["link_mass"] = np.concatenate([model["link_mass"], np.full(extra, 0.3)])
+        model["link_com"] = np.concatenate([model["link_com"], np.zeros((extra, 3))])
+        model["link_inertia"] = np.concatenate([model["link_inertia"], np.tile(np.eye(3) * 1e-3, (extra, 1, 1))])
+        model["joint_type"] = np.concatenate([model["joint_type"], np.zeros(extra, dtype=np.int32)])
+        model["names"] = list(model["names"]) + [f"extra{i}" for i in range(extra)]
+    B = 21
+    st = robot.random_states(model, B, seed=12)
+    host, dev = _mixed_contacts(B, seed=4)
+    dm = handle.fb_model(model)
+    out = handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS}, _d(st["joint_torque"]),
+                              contacts=dev)
+    out = {k: v.cpu().numpy() for k, v in out.items()}
+    dst = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    handle.fbd_euler_integrate(dm, dst, _d(st["joint_torque"]), 0.0, 0.003, 0.001, contacts=dev)
+    got = {k: v.cpu().numpy() for k, v in dst.items()}
+    for i in range(0, B, 4):
+        kw = dict(contacts=host["frame"], contact_params=host["params"], null_poses=host["null_pose"][i],
+                  laws=host["law"], wrenches=host["wrench"][i])
+        ba, ja, dp, dR, dq = F.dynamics(model, st, i, **kw)
+        assert rel_err(out["base_vel"][i], ba) < TOL
+        assert rel_err(out["joint_vel"][i], ja) < TOL
+        # the given wrench matters: the continuous law in its place gives other accelerations
+        alt = F.dynamics(model, st, i, **dict(kw, laws=None))[1]
+        assert rel_err(alt, ja) > 1e-6
+        ref = F.euler_integrate(model, st, i, 0.0, 0.003, 0.001, **kw)
+        for k in native.FB_STATE_KEYS:
+            assert rel_err(got[k][i], ref[k]) < TOL, (i, k)
+
+
+def test_fbd_given_wrench_of_the_continuous_model_equals_the_continuous_law(handle):
+    """The C++ adapter's path for a ContactModel the kernel does not know: frame state on the
+    device, the model's wrench at that state, BLF_CONTACT_WRENCH.  With the ContinuousContactModel
+    itself evaluated that way (blf_contact_model_eval) the dynamics equal the in-kernel law."""
+    B = 32
+    st = robot.random_states(MODEL, B, seed=8)
+    host, dev = contacts_for(B, seed=6)
+    dm = handle.fb_model(MODEL)
+    dst = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    tau = _d(st["joint_torque"])
+    pose, twist = handle.fb_frame_state(dm, dst, dev["frame"])
+    C = 2
+    prm = dev["params"].repeat(B, 1).contiguous()
+    w = handle.contact_model_eval(prm, twist.reshape(B * C, 6).contiguous(), pose.reshape(B * C, 12).contiguous(),
+                                  dev["null_pose"].reshape(B * C, 12).contiguous(), outputs=("wrench",))["wrench"]
+    law = _d(np.array([native.CONTACT_WRENCH] * C, dtype=np.int32), torch.int32)
+    given = dict(dev, law=law, wrench=w.reshape(B, C, 6).contiguous())
+    a = handle.fbd_dynamics(dm, dst, tau, contacts=dev)
+    b = handle.fbd_dynamics(dm, dst, tau, contacts=given)
+    for k in ("base_vel", "joint_vel"):
+        x, y = a[k].cpu().numpy(), b[k].cpu().numpy()
+        assert np.abs(x - y).max() <= 1e-12 * max(1.0, np.abs(x).max()), k
+
+
+def test_fbd_contact_law_without_wrench_is_refused(handle):
+    B = 2
+    st = robot.random_states(MODEL, B, seed=1)
+    host, dev = contacts_for(B)
+    dm = handle.fb_model(MODEL)
+    bad = dict(dev, law=_d(np.array([0, 1], dtype=np.int32), torch.int32), wrench=None)
+    with pytest.raises(native.BlfError) as e:
+        handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS}, _d(st["joint_torque"]),
+                            contacts=bad)
+    assert e.value.code == 1
