@@ -546,7 +546,10 @@ __global__ __launch_bounds__(256) void quintic_fit_kernel(const double* __restri
 
 // one lane per (spline, query); the workgroup's [256][3][D] output slab is staged in LDS and
 // written with coalesced 16-B stores (slab.h)
-constexpr int kEvalBlock = 256;
+#ifndef BLF_Q_BLOCK   // queries per workgroup (A/B builds)
+#define BLF_Q_BLOCK 256
+#endif
+constexpr int kEvalBlock = BLF_Q_BLOCK;
 #ifndef BLF_Q_STAGE
 #define BLF_Q_STAGE 512
 #endif
@@ -563,7 +566,7 @@ __global__ __launch_bounds__(kEvalBlock) void quintic_eval_kernel(const double* 
                                                                   int32_t Q, double* __restrict__ pva,
                                                                   int32_t* __restrict__ idx)
 {
-    __shared__ double s_out[kEvalBlock * 9];
+    __shared__ __attribute__((aligned(16))) double s_out[kEvalBlock * 9];
     __shared__ __attribute__((aligned(16))) double s_spl[kEvalStage];   // the splines' knots + coefficients
     const int K = K1 - 1;
     const int W = 3 * D, SW = odd_stride(W);
@@ -711,8 +714,10 @@ blf_status launch_quintic_eval(const double* kt, const double* coeffs, int32_t K
 {
     const int64_t n = S * Q;
     if (n == 0) return BLF_OK;
-    auto kern = (((uintptr_t)coeffs & 15) == 0) ? quintic_eval_kernel<true> : quintic_eval_kernel<false>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(n, kEvalBlock)), dim3(kEvalBlock), 0, s, kt,
+    const bool vec = ((uintptr_t)coeffs & 15) == 0;
+    const int64_t ntiles = ceil_div(n, kEvalBlock);
+    auto kern = vec ? quintic_eval_kernel<true> : quintic_eval_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(kEvalBlock), 0, s, kt,
                        coeffs, K1, D, S, tq, Q, pva, idx);
     return check_hip(hipGetLastError(), "quintic_eval_kernel launch");
 }

@@ -146,6 +146,27 @@ __device__ __forceinline__ void slab_store(double* __restrict__ g, int64_t GS,
     if (GS == W && ((uintptr_t)g & 15) == 0) {
         double2* g2 = reinterpret_cast<double2*>(g);
         const int n2 = n >> 1;
+        if (SW == W && ((uintptr_t)s & 15) == 0) {
+            // unpadded rows (odd W): the LDS slab is the global slab, 16-B LDS reads with no row
+            // arithmetic (the quintic evaluation's 9-double rows: two float row divisions, two
+            // address computations and two 8-B LDS reads per 16-B store before)
+            const double2* s2 = reinterpret_cast<const double2*>(s);
+            for (int base = 0; base < n2; base += U * NT) {
+                double2 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = base + u * NT + t;
+                    if (j < n2) v[u] = s2[j];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = base + u * NT + t;
+                    if (j < n2) st_stream(g2 + j, v[u]);
+                }
+            }
+            if ((n & 1) && t == 0) g[n - 1] = s[n - 1];
+            return;
+        }
         for (int base = 0; base < n2; base += U * NT) {
             double2 v[U];
 #pragma unroll

@@ -73,6 +73,16 @@ def main():
     report("quintic_eval_kernel", S * (Q * (8 + 72 + 4) + 3 * 8 + 2 * 3 * 6 * 8), ms, S * Q,
            "queries")
     del kt, kp, co, tq
+    # what the memory system gives a plain stream on this box: torch's write-only fill and copy
+    # of 3 GiB (reference lines for the write-dominated kernels above, not library kernels)
+    big = torch.empty(3 * 2 ** 27, dtype=torch.float64, device=dev)
+    ms = timed(lambda: big.fill_(1.0))
+    report("ref:torch_fill", big.numel() * 8, ms, big.numel(), "doubles")
+    half = big[: big.numel() // 2]
+    other = big[big.numel() // 2:]
+    ms = timed(lambda: other.copy_(half))
+    report("ref:torch_copy", half.numel() * 16, ms, half.numel(), "doubles")
+    del big, half, other
     # contact_model_eval: all four outputs
     C = 4 * 1024 * 1024
     prm = torch.tensor([0.12, 0.09, 2000.0, 100.0], dtype=torch.float64, device=dev)
