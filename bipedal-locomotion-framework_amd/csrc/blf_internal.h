@@ -118,7 +118,7 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
                             const blf_fb_contacts* ct, const double* reg, int64_t batch,
                             int32_t nsteps, double dT, double dT_last, hipStream_t s,
                             const blf_joint_impedance* impedance = nullptr);
-size_t fbd_lds_bytes(int n, int C);
+size_t fbd_lds_bytes(int n, int C, bool aba = false);   // aba: the articulated-body layout
 blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const double* omega0,
                          int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s);
 blf_status launch_fb_frame_state(const blf_fb_model* md, const blf_fb_state* st, int32_t K,

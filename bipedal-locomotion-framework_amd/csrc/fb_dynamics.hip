@@ -121,6 +121,13 @@ constexpr bool kPrefixLds = BLF_FBD_PREFIX_LDS && BLF_FBD_CSUB;   // (the base's
 constexpr bool kSubst = BLF_FBD_SUBST && BLF_FBD_CHOLB > 1;        // (the pivots: the block factorization)
 constexpr int kLinkRec = 40 + kPad;   // record stride (40 doubles of data)
 constexpr int kR = 0, kP = 9, kW = 12, kV = 15, kAl = 18, kA = 21, kSI = 24, kSF = 34;
+// The articulated-body layout (Smem aba): 27-double records.  Step 3 writes a link's spatial
+// inertia / force over the first 16 doubles of its own record once it has read the kinematics
+// (no other lane reads that record afterwards: the contacts, which do, run before step 3), and
+// fbd_aba keeps joint j's slot (articulated inertia 21 | bias 6, later da 6) in link j + 1's record
+// after reading that link's spatial terms.
+constexpr int kLinkRecA = 27;
+constexpr int kSIa = 0, kSFa = 10;
 constexpr int kComp = 16;             // subtree sum: spatial inertia 10 | spatial force 6
 constexpr int kCompS = kComp + kPad;  // its stride
 constexpr int kCs = 16 + kPad;        // contact scratch: point 3 | wrench 6 | link 1 | spatial wrench 6
@@ -133,11 +140,17 @@ struct Smem {
     double* base;
     int o_link, o_jrot, o_jz, o_jo, o_comp, o_sax, o_rhs, o_cscr, o_st, o_tq, o_anc, o_cst, o_imp;
     int ms;   // row stride of L (odd: the per-lane row accesses do not conflict)
+    int lrec;   // link record stride: kLinkRec, or kLinkRecA for the articulated-body solve
     size_t total;
-    __host__ __device__ Smem(double* b, int n, int C) : base(b)
+    // aba: the layout of the articulated-body solve (fbd_aba): records of kLinkRecA doubles that
+    // later hold the spatial terms (kSIa / kSFa) and the joint slots, no subtree-sum / pivot-column
+    // or column-axis arrays -- 9.3 KB per 30-DoF system instead of 19.2 KB, so two wavefronts of two
+    // systems fit per SIMD
+    __host__ __device__ Smem(double* b, int n, int C, bool aba = false) : base(b)
     {
         const int L = n + 1, NV = n + 6;
         ms = NV | 1;
+        lrec = aba ? kLinkRecA : kLinkRec;
         size_t o = 0;
         auto take = [&](size_t k) {
             const int at = (int)o;
@@ -145,18 +158,17 @@ struct Smem {
             return at;
         };
         // link records; after the mass matrix is assembled the same space holds L (NV rows)
-        const size_t lk = (size_t)kLinkRec * L, lm = (size_t)NV * ms;
+        const size_t lk = (size_t)lrec * L, lm = aba ? 0 : (size_t)NV * ms;
         o_link = take(lk > lm ? lk : lm);
         o_jrot = take(BLF_FBD_KINJUMP ? 0 : kJrot * (size_t)n);   // E_j Rot(a_j, s_j) (9) | E_j a_j (3): levels only
         o_jz = take(3 * (size_t)n);
         o_jo = take(3 * (size_t)n);
         // subtree sums [j] (joint j's subtree) and [n] (every link); later the pivot-column
         // buffers of the factorization (two sets of up to 4 columns, 8 NV)
-        // (the articulated-body solve's per-joint slots, 27 n, use the same space)
-        const size_t cp = (size_t)kCompS * (n + 1) > (size_t)27 * n ? (size_t)kCompS * (n + 1) : (size_t)28 * n;
+        const size_t cp = (size_t)kCompS * (n + 1);
         const size_t cb = 8 * (size_t)(NV > 32 ? NV : 32);   // (BLF_FBD_COLFIX: 2 CB NVMAX)
-        o_comp = take(cp > cb ? cp : cb);
-        o_sax = take(kSax * (size_t)NV);
+        o_comp = take(aba ? 0 : cp > cb ? cp : cb);
+        o_sax = take(aba ? 0 : kSax * (size_t)NV);
         o_rhs = take((size_t)NV);
         o_cscr = take((size_t)kCs * (C > 0 ? C : 1));
         o_st = take(18 + 2 * (size_t)n + (size_t)NV + 9);   // Euler state (6 + n + 3 + 9 + n) + acc + dR
@@ -421,7 +433,7 @@ __device__ __forceinline__ void fbd_kinematics_levels(const Model& m, const Smem
             // the parent link's record and this joint's rotation into registers first (the child
             // record's stores could otherwise alias them and delay the loads)
             double pr[24], Ej[12];
-            const double* prs = S.link() + kLinkRec * P;
+            const double* prs = S.link() + S.lrec * P;
 #pragma unroll
             for (int i = 0; i < 24; ++i) pr[i] = prs[i];
 #pragma unroll
@@ -451,7 +463,7 @@ __device__ __forceinline__ void fbd_kinematics_levels(const Model& m, const Smem
             cross3(pr + kW, zs, t2);           // w_P x z sd
             cross3(pr + kAl, r, t3);           // al_P x r
             cross3(pr + kW, t1, t4);           // w_P x (w_P x r)
-            double* cr = S.link() + kLinkRec * (j + 1);
+            double* cr = S.link() + S.lrec * (j + 1);
 #pragma unroll
             for (int i = 0; i < 9; ++i) cr[kR + i] = cR[i];
 #pragma unroll
@@ -579,7 +591,7 @@ __device__ __forceinline__ void fbd_kinematics_jump(const Model& m, const Smem& 
     };
     int ptr = jl ? T.P : 0;
     if (jl && ptr == 0) compose(Rb, pb);
-    double* own = S.link() + kLinkRec * (lane + 1);
+    double* own = S.link() + S.lrec * (lane + 1);
     if (jl) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) own[kR + i] = R[i];
@@ -592,7 +604,7 @@ __device__ __forceinline__ void fbd_kinematics_jump(const Model& m, const Smem& 
         const bool act = jl && ptr > 0;
         const int pn = H.shfl(ptr, act ? ptr - 1 : 0);
         if (act) {
-            const double* x = S.link() + kLinkRec * ptr;
+            const double* x = S.link() + S.lrec * ptr;
             double RX[9], pX[3];
 #pragma unroll
             for (int i = 0; i < 9; ++i) RX[i] = x[kR + i];
@@ -642,7 +654,7 @@ __device__ __forceinline__ void fbd_kinematics_jump(const Model& m, const Smem& 
         const bool act = jl && ptr > 0;
         const int pn = H.shfl(ptr, act ? ptr - 1 : 0);
         if (act) {
-            const double* e = S.link() + kLinkRec * ptr;
+            const double* e = S.link() + S.lrec * ptr;
             double sX[6], xX[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
@@ -733,7 +745,6 @@ __host__ __device__ constexpr int s6(int i, int j)
 {
     return i <= j ? i * 6 - i * (i - 1) / 2 + (j - i) : j * 6 - j * (j - 1) / 2 + (i - j);
 }
-constexpr int kAbaSlot = 27 + (1 - kPad);   // Ia (21) | pa (6), odd stride (27); later da (6)
 
 // the spatial inertia about the origin (m, h, Ibar xx xy xz yy yz zz) as a 6 x 6 on (w; u)
 __device__ __forceinline__ void spatial6(const double* si, double (&I)[21])
@@ -749,11 +760,14 @@ __device__ __forceinline__ void spatial6(const double* si, double (&I)[21])
 }
 
 template <int HW, bool PRI>
-__device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const double* tau, const Topo& T, int lane)
+__device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const double* tau, const double* bp,
+                                        const Topo& T, int lane)
 {
     const int n = m.n;
     const bool jl = lane < n;
-    double* slot = S.comp();   // [n][kAbaSlot]; the subtree sums / pivot columns are not used here
+    // joint j's slot: link j + 1's record (Smem aba), written after that link's spatial terms are read
+    double* const rec = S.link();
+    const int lr = S.lrec;
     bool ok = true;
     // this lane's joint axis s = (w; u) and torque
     double sv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -774,13 +788,13 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
     // inward sweep, deepest joints first
     for (int lev = T.maxdepth; lev >= 0; --lev) {
         if (jl && T.depth == lev) {
-            const double* k = S.link() + kLinkRec * (lane + 1);
+            const double* k = rec + lr * (lane + 1);
             double IA[21], pA[6];
-            spatial6(k + kSI, IA);
+            spatial6(k + kSIa, IA);
 #pragma unroll
-            for (int a = 0; a < 6; ++a) pA[a] = k[kSF + a];
+            for (int a = 0; a < 6; ++a) pA[a] = k[kSFa + a];
             for (unsigned long long b = T.cmask; b; b &= b - 1) {
-                const double* c = slot + kAbaSlot * __builtin_ctzll(b);
+                const double* c = rec + lr * (__builtin_ctzll(b) + 1);
 #pragma unroll
                 for (int e = 0; e < 21; ++e) IA[e] = IA[e] + c[e];
 #pragma unroll
@@ -802,7 +816,7 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
             ok = ok && D > 0.0;
             iD = 1.0 / D;
             uD = (tq - sp) * iD;
-            double* o = slot + kAbaSlot * lane;
+            double* o = rec + lr * (lane + 1);
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 const double Ua = U[a] * iD;
@@ -817,12 +831,12 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
     double da[6];
     {
         double IA[21], pA[6];
-        const double* k = S.link();
-        spatial6(k + kSI, IA);
+        const double* k = rec;
+        spatial6(k + kSIa, IA);
 #pragma unroll
-        for (int a = 0; a < 6; ++a) pA[a] = k[kSF + a];
+        for (int a = 0; a < 6; ++a) pA[a] = k[kSFa + a];
         for (unsigned long long b = T.bmask; b; b &= b - 1) {
-            const double* c = slot + kAbaSlot * __builtin_ctzll(b);
+            const double* c = rec + lr * (__builtin_ctzll(b) + 1);
 #pragma unroll
             for (int e = 0; e < 21; ++e) IA[e] = IA[e] + c[e];
 #pragma unroll
@@ -866,21 +880,22 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
     for (int lev = 0; lev <= T.maxdepth; ++lev) {
         if (jl && T.depth == lev) {
             double dp[6];
-            const double* src = slot + kAbaSlot * (T.P > 0 ? T.P - 1 : 0);
+            const double* src = rec + lr * T.P;   // the parent joint's slot (T.P = 0: the base, unused)
 #pragma unroll
             for (int a = 0; a < 6; ++a) dp[a] = T.P > 0 ? src[a] : da[a];
             double Ud = 0.0;
 #pragma unroll
             for (int a = 0; a < 6; ++a) Ud = fma(U[a], dp[a], Ud);
             qdd = fma(-Ud, iD, uD);
-            double* o = slot + kAbaSlot * lane;
+            double* o = rec + lr * (lane + 1);
 #pragma unroll
             for (int a = 0; a < 6; ++a) o[a] = fma(sv[a], qdd, dp[a]);
         }
         wave_sync();
     }
-    // nu_dot: base (linear: da_0's u - p_B x w; angular: w), then the joints
-    const double* pB = S.link() + kP;
+    // nu_dot: base (linear: da_0's u - p_B x w; angular: w), then the joints (p_B from the state:
+    // the base record's position now holds its spatial force)
+    const double* pB = bp;
     if (lane < 6) {
         const double w[3] = {da[0], da[1], da[2]};
         double pw[3];
@@ -948,7 +963,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
     //    instead of in every component group of the subtree sums
     auto link_step = [&]() {
     for (int l = lane; l < L; l += HW) {
-        double* k = S.link() + kLinkRec * l;
+        double* k = S.link() + S.lrec * l;
         const double* R = k + kR;
         const double* cl = m.com + 3 * l;
         const double* Ic = m.inertia + 9 * l;
@@ -981,7 +996,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         for (int a = 0; a < 3; ++a) tq[a] = Ia[a] + t1[a];
         cross3(c, f, cf);
         const double cc = dot3(c, c);
-        double* si = k + kSI;
+        double* si = k + (ABA ? kSIa : kSI);   // (ABA: over the record's kinematics, read above)
         si[0] = ms;
         si[1] = ms * c[0]; si[2] = ms * c[1]; si[3] = ms * c[2];
         si[4] = Iw[0] + ms * (cc - c[0] * c[0]);
@@ -1006,7 +1021,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
                 for (int a = 0; a < 6; ++a) sfv[a] = hit ? sfv[a] - w[a] : sfv[a];
             }
         }
-        double* sf = k + kSF;
+        double* sf = k + (ABA ? kSFa : kSF);
         for (int a = 0; a < 6; ++a) sf[a] = sfv[a];
     }
     };
@@ -1027,7 +1042,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             fp = m.fpose + 12 * f;
         }
         double pose[12], tw[6];
-        frame_state(S.link() + kLinkRec * l, fp, pose, tw);
+        frame_state(S.link() + S.lrec * l, fp, pose, tw);
         double* sc = S.cscr() + kCs * c;
         if (given_wrench(ct, c)) {   // any ContactModel, evaluated by the caller
             const double* gw = ct.wrench + (sys * ct.C + c) * 6;
@@ -1062,9 +1077,10 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
         wave_sync();
         FSTAMP_ADD(2, f_t2b);
     }
+    static_assert(!ABA || BLF_FBD_CSUB, "the ABA layout needs the contacts before step 3");
     if constexpr (ABA) {   // steps 5-9 replaced by the articulated-body solve (no regularisation)
         FSTAMP(f_t4a);
-        const bool ok = fbd_aba<HW, PRI>(m, S, tau, T, lane);
+        const bool ok = fbd_aba<HW, PRI>(m, S, tau, bp, T, lane);
         FSTAMP_ADD(7, f_t4a);
         FSTAMP_ADD(9, f_t0);
         return ok;
@@ -1084,7 +1100,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             double bo[G];   // the base link's own terms (every lane reads them: no branch)
 #pragma unroll
             for (int q = 0; q < G; ++q) {
-                v[q] = jl ? S.link()[kLinkRec * (lane + 1) + kSI + g + q] : 0.0;
+                v[q] = jl ? S.link()[S.lrec * (lane + 1) + kSI + g + q] : 0.0;
                 bo[q] = kPrefixLds ? 0.0 : S.link()[kSI + g + q];
             }
             if constexpr (!BLF_FBD_CSUB)
@@ -1160,7 +1176,7 @@ __device__ __forceinline__ bool fbd_eval(const Model& m, const Smem& S, const do
             const unsigned long long ch = lev >= 0 ? T.cmask : T.bmask;
             double acc[kComp];
 #pragma unroll
-            for (int p = 0; p < kComp; ++p) acc[p] = S.link()[kLinkRec * l + kSI + p];
+            for (int p = 0; p < kComp; ++p) acc[p] = S.link()[S.lrec * l + kSI + p];
             if constexpr (!BLF_FBD_CSUB)
             for (int c = 0; c < ct.C; ++c) {
                 const double* sc = S.cscr() + kCs * c;
@@ -1496,7 +1512,7 @@ __global__ __launch_bounds__(64) void fbd_dynamics_kernel(Model m, blf_fb_state 
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const Half<HW> H;
     const int n = m.n, NV = n + 6;
-    const Smem S(smem + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
+    const Smem S(smem + H.half * Smem(nullptr, n, ct.C, ABA).total, n, ct.C, ABA);
     // system of this half; a missing second system of the last wavefront recomputes the last one
     // and writes nothing
     const int64_t q0 = (int64_t)blockIdx.x * (kWave / HW) + H.half;
@@ -1558,7 +1574,7 @@ __global__ __launch_bounds__(64, HW == 32 ? 1 : 2) void fbd_euler_kernel(Model m
     constexpr bool kLM = BLF_FBD_LDSMODEL && HW == 32;
     constexpr bool kCS = BLF_FBD_CSTAGE && !kLM && HW == 32;   // (LLVM's allocator crashes on the HW = 64 form)
     constexpr int kMB = kLM ? fbd_model_block<NVMAX>() : 0;
-    const Smem S(smem + kMB + H.half * Smem(nullptr, n, ct.C).total, n, ct.C);
+    const Smem S(smem + kMB + H.half * Smem(nullptr, n, ct.C, ABA).total, n, ct.C, ABA);
     const int lane = H.hl;
     if constexpr (kLM) {
         constexpr int J = NVMAX - 6, Lk = NVMAX - 5;
@@ -1701,7 +1717,7 @@ __global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, co
     wave_sync();
     double a[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // m c (3), m cdot (3), m
     if (lane < L) {
-        const double* k = S.link() + kLinkRec * lane;
+        const double* k = S.link() + S.lrec * lane;
         const double* R = k + kR;
         const double* cl = m.com + 3 * lane;
         double rc[3], t[3];
@@ -1759,7 +1775,7 @@ __global__ __launch_bounds__(64) void fb_frame_state_kernel(Model m, blf_fb_stat
     for (int c = lane; c < K; c += kWave) {
         const int f = frames[c];
         double p[12], tw[6];
-        frame_state(S.link() + kLinkRec * m.flink[f], m.fpose + 12 * f, p, tw);
+        frame_state(S.link() + S.lrec * m.flink[f], m.fpose + 12 * f, p, tw);
         if (pose)
             for (int a = 0; a < 12; ++a) pose[(q * K + c) * 12 + a] = p[a];
         if (twist)
@@ -1826,7 +1842,7 @@ Contacts to_contacts(const blf_fb_contacts* c)
 
 }  // namespace
 
-size_t fbd_lds_bytes(int n, int C) { return sizeof(double) * Smem(nullptr, n, C).total; }
+size_t fbd_lds_bytes(int n, int C, bool aba) { return sizeof(double) * Smem(nullptr, n, C, aba).total; }
 
 // The articulated-body solve (fbd_aba) unless the model carries a mass-matrix regularisation,
 // which needs M itself; BLF_FBD_ABA=0 keeps the factorization for every model (A/B only).
@@ -1845,8 +1861,8 @@ blf_status launch_fbd_dynamics(const blf_fb_model* md, const blf_fb_state* st, c
 {
     if (batch == 0) return BLF_OK;
     const Contacts c = to_contacts(ct);
-    const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     const bool pri = md->joint_type != nullptr, aba = use_aba(reg);
+    const size_t lds = fbd_lds_bytes(md->ndof, c.C, aba);
 #define FBD_DYN(NV, HW) (pri ? (aba ? fbd_dynamics_kernel<NV, HW, true, true> : fbd_dynamics_kernel<NV, HW, true, false>) \
                              : (aba ? fbd_dynamics_kernel<NV, HW, false, true> : fbd_dynamics_kernel<NV, HW, false, false>))
     if (md->ndof + 6 <= 32)   // two systems per wavefront
@@ -1867,10 +1883,10 @@ blf_status launch_fbd_euler(const blf_fb_model* md, const blf_fb_state* st, cons
     if (batch == 0) return BLF_OK;
     const size_t mb32 = BLF_FBD_LDSMODEL ? sizeof(double) * fbd_model_block<32>() : 0;
     const Contacts c = to_contacts(ct);
-    const size_t lds = fbd_lds_bytes(md->ndof, c.C);
     Impedance imp{nullptr, nullptr, nullptr};
     if (impedance) imp = Impedance{impedance->kp, impedance->kd, impedance->q_ref};
     const bool pri = md->joint_type != nullptr, aba = use_aba(reg);
+    const size_t lds = fbd_lds_bytes(md->ndof, c.C, aba);
 #define FBD_EUL(NV, HW) (pri ? (aba ? fbd_euler_kernel<NV, HW, true, true> : fbd_euler_kernel<NV, HW, true, false>) \
                              : (aba ? fbd_euler_kernel<NV, HW, false, true> : fbd_euler_kernel<NV, HW, false, false>))
     if (md->ndof + 6 <= 32)   // two systems per wavefront
