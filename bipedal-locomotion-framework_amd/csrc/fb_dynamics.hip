@@ -786,6 +786,7 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
 #pragma unroll
     for (int a = 0; a < 6; ++a) U[a] = 0.0;
     // inward sweep, deepest joints first
+    FSTAMP(a_in);
     for (int lev = T.maxdepth; lev >= 0; --lev) {
         if (jl && T.depth == lev) {
             const double* k = rec + lr * (lane + 1);
@@ -827,7 +828,9 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
         }
         wave_sync();
     }
+    FSTAMP_ADD(4, a_in);
     // the base: IA_0 da_0 = -pA_0 (every lane, from the base's children's slots)
+    FSTAMP(a_base);
     double da[6];
     {
         double IA[21], pA[6];
@@ -875,7 +878,9 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
             da[i] = t;
         }
     }
+    FSTAMP_ADD(5, a_base);
     // outward sweep: qdd_j and the joint's child link's da, shallowest first
+    FSTAMP(a_out);
     double qdd = 0.0;
     for (int lev = 0; lev <= T.maxdepth; ++lev) {
         if (jl && T.depth == lev) {
@@ -907,6 +912,7 @@ __device__ __forceinline__ bool fbd_aba(const Model& m, const Smem& S, const dou
     }
     if (jl) S.rhs()[6 + lane] = qdd;
     wave_sync();
+    FSTAMP_ADD(6, a_out);
     const Half<HW> H;
     return H.ballot(!ok) == 0ull;
 }
@@ -1698,7 +1704,7 @@ __global__ __launch_bounds__(64) void fb_dcm_kernel(Model m, blf_fb_state st, co
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int n = m.n, L = n + 1;
-    const Smem S(smem, n, 0);
+    const Smem S(smem, n, 0, true);   // kinematics only: the compact (articulated-body) layout
     const int64_t q = blockIdx.x;
     const int lane = threadIdx.x;
     double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n
@@ -1755,7 +1761,7 @@ __global__ __launch_bounds__(64) void fb_frame_state_kernel(Model m, blf_fb_stat
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int n = m.n;
-    const Smem S(smem, n, 0);
+    const Smem S(smem, n, 0, true);   // kinematics only: the compact (articulated-body) layout
     const int64_t q = blockIdx.x;
     const int lane = threadIdx.x;
     double* loc = S.st();   // bv 6 | jv n | bp 3 | bR 9 | jp n
@@ -1903,7 +1909,7 @@ blf_status launch_fb_dcm(const blf_fb_model* md, const blf_fb_state* st, const d
                          int64_t ostride, int64_t batch, double* com, double* xi, hipStream_t s)
 {
     if (batch == 0) return BLF_OK;
-    const size_t lds = fbd_lds_bytes(md->ndof, 0);
+    const size_t lds = fbd_lds_bytes(md->ndof, 0, true);
     hipLaunchKernelGGL((md->joint_type ? fb_dcm_kernel<true> : fb_dcm_kernel<false>), dim3((unsigned)batch),
                        dim3(kWave), lds, s, to_model(md), *st,
                        omega0, ostride, com, xi);
@@ -1915,7 +1921,7 @@ blf_status launch_fb_frame_state(const blf_fb_model* md, const blf_fb_state* st,
                                  hipStream_t s)
 {
     if (batch == 0 || K == 0) return BLF_OK;
-    const size_t lds = fbd_lds_bytes(md->ndof, 0);
+    const size_t lds = fbd_lds_bytes(md->ndof, 0, true);
     hipLaunchKernelGGL((md->joint_type ? fb_frame_state_kernel<true> : fb_frame_state_kernel<false>),
                        dim3((unsigned)batch), dim3(kWave), lds, s, to_model(md), *st, (int)K, frames,
                        pose, twist);

@@ -11,8 +11,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "bipedal-locomotion-framework_amd"))
 from blf import native, robot  # noqa: E402
 
+# the articulated-body solve (the default without mass_reg) stamps slots 4-7 as its inward sweep,
+# base solve, outward sweep and the whole solve; the factorization path as named in brackets
 PHASES = ["joint rot + depth", "forward kinematics", "per-link spatial", "contacts",
-          "subtree sums", "columns + rhs", "mass matrix", "cholesky", "substitution", "total"]
+          "ABA inward (subtree sums)", "ABA base (columns + rhs)", "ABA outward (mass matrix)",
+          "ABA whole (cholesky)", "(substitution)", "total"]
 
 
 def main():
