@@ -76,7 +76,10 @@ def load_urdf(source, frames=(), base=None, considered_joints=None):
     frames            link names to expose as frames (frame_link / frame_pose), in this order
     base              the floating base link (default: the tree's root)
     considered_joints joint names kept as degrees of freedom (default: every moving joint); the
-                      other joints are locked at q = 0, as iDynTree's reduced model loader does
+                      other joints are locked at q = 0, as iDynTree's reduced model loader does,
+                      and the degrees of freedom follow the list's order, as iDynTree orders them
+                      (the list must name every joint after its parent's: the kernels need
+                      parent[j] <= j; otherwise ValueError).  Without it: depth-first preorder.
     """
     text = source if isinstance(source, str) and source.lstrip().startswith("<") else open(source).read()
     root = ET.fromstring(text)
@@ -168,4 +171,37 @@ def load_urdf(source, frames=(), base=None, considered_joints=None):
         model["joint_type"] = joint_type
     if fixed:
         model = robot.reduce_fixed_joints(model, fixed)
+    if considered_joints is not None:
+        wanted = [c for c in dict.fromkeys(considered_joints) if c in model["names"][1:]]
+        if wanted != list(model["names"][1:]):
+            model = reorder_joints(model, [model["names"].index(c) - 1 for c in wanted])
     return model
+
+
+def reorder_joints(model, perm):
+    """The model with its joints in the order perm (perm[k] = the joint placed at k, with its child
+    link): every joint / link array permuted, parents and frame links re-indexed.  ValueError when
+    a joint would precede its parent's joint (the kernels need parent[j] <= j)."""
+    n = model["n"]
+    perm = [int(o) for o in perm]
+    if sorted(perm) != list(range(n)):
+        raise ValueError("reorder_joints: perm must list every joint once")
+    new_link = np.zeros(n + 1, dtype=np.int64)   # old link -> new link
+    for k, o in enumerate(perm):
+        new_link[o + 1] = k + 1
+    parent = np.array([new_link[model["parent"][o]] for o in perm], dtype=np.int32)
+    late = [model["names"][perm[k] + 1] for k in range(n) if parent[k] > k]
+    if late:
+        raise ValueError(f"load_urdf: considered_joints lists {late} before their parent joints; "
+                         "list every joint after its parent's (the kernels need parent[j] <= j)")
+    out = dict(model)
+    out["parent"] = parent
+    for key in ("joint_origin", "joint_rot", "joint_axis", "joint_type"):
+        if key in model:
+            out[key] = np.ascontiguousarray(np.asarray(model[key])[perm])
+    links = [0] + [o + 1 for o in perm]
+    for key in ("link_mass", "link_com", "link_inertia"):
+        out[key] = np.ascontiguousarray(np.asarray(model[key])[links])
+    out["frame_link"] = np.asarray([new_link[l] for l in model["frame_link"]], dtype=np.int32)
+    out["names"] = [model["names"][0]] + [model["names"][o + 1] for o in perm]
+    return out

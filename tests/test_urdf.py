@@ -130,3 +130,34 @@ def test_urdf_errors(bad, msg):
         urdf.load_urdf(to_urdf(MODEL, extra=bad))
     with pytest.raises(ValueError, match="not a link"):
         urdf.load_urdf(to_urdf(MODEL), frames=("nope",))
+
+
+def test_urdf_considered_joints_order():
+    """The degrees of freedom follow considered_joints' order (iDynTree's reduced loader), here the
+    right leg's chain before the left's: the rigid-body terms are the depth-first model's with q,
+    qdot, tau and M permuted the same way; a list that names a joint before its parent's is
+    refused."""
+    names = MODEL["names"][1:]
+    left = [nm for nm in names if nm.startswith("l_")]
+    right = [nm for nm in names if nm.startswith("r_")]
+    rest = [nm for nm in names if nm not in left and nm not in right]
+    order = rest + right + left
+    m = urdf.load_urdf(to_urdf(MODEL), considered_joints=order)
+    assert m["names"][1:] == order
+    n = MODEL["n"]
+    perm = [names.index(nm) for nm in order]
+    assert all(0 <= m["parent"][j] <= j for j in range(n))
+    st = robot.random_states(MODEL, 1, seed=5)
+    K = F.kinematics(MODEL, st["base_pos"][0], st["base_rot"][0], st["joint_pos"][0], st["base_vel"][0],
+                     st["joint_vel"][0])
+    M0, h0 = F.mass_and_bias(MODEL, K)
+    Kp = F.kinematics(m, st["base_pos"][0], st["base_rot"][0], st["joint_pos"][0][perm], st["base_vel"][0],
+                      st["joint_vel"][0][perm])
+    M1, h1 = F.mass_and_bias(m, Kp)
+    rows = list(range(6)) + [6 + j for j in perm]
+    np.testing.assert_allclose(M1, M0[np.ix_(rows, rows)], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(h1, h0[rows], rtol=0, atol=1e-11)
+    child_first = [nm for nm in order if nm != "l_knee"] + ["l_knee"]
+    child_first.insert(child_first.index([nm for nm in left if nm != "l_knee"][0]), "l_knee")
+    with pytest.raises(ValueError, match="before their parent"):
+        urdf.load_urdf(to_urdf(MODEL), considered_joints=child_first)
