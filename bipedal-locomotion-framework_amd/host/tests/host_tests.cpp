@@ -969,6 +969,19 @@ static void testFloatingBaseDynamicsAnyContactModel()
         sd = std::max(sd, std::abs(std::get<2>(s0)[i] - std::get<2>(s1)[i]));
     }
     REQUIRE(sd <= 1e-9);
+    // a final time dT does not divide: the reference's schedule (ceil((T - t0) / dT) steps, the
+    // last one with the stale time, FixedStepIntegrator.tpp:48-64) in the step-by-step path too
+    ForwardEuler<FloatingBaseDynamicalSystem> f0(0.01), f1(0.01);
+    REQUIRE(f0.setDynamicalSystem(device) && f1.setDynamicalSystem(mixed));
+    const int before = forwarding->states;
+    REQUIRE(f0.integrate(0.05, 0.095) && f1.integrate(0.05, 0.095));
+    REQUIRE(forwarding->states == before + 5);   // ceil(0.045 / 0.01) steps, one evaluation each
+    const auto& u0 = f0.getSolution();
+    const auto& u1 = f1.getSolution();
+    double ud = 0.0;
+    for (int i = 0; i < 6; ++i) ud = std::max(ud, std::abs(std::get<0>(u0)[i] - std::get<0>(u1)[i]));
+    for (int i = 0; i < 3; ++i) ud = std::max(ud, std::abs(std::get<2>(u0)[i] - std::get<2>(u1)[i]));
+    REQUIRE(ud <= 1e-9);
     // a contact without a model is refused (ContactWrench owns its model, as the reference's)
     REQUIRE(mixed->setControlInput({tau, {ContactWrench(0, nullptr)}}));
     REQUIRE_FALSE(mixed->dynamics(0.0, d1));

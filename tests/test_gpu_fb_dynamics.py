@@ -330,3 +330,22 @@ def test_fbd_contact_law_without_wrench_is_refused(handle):
         handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS}, _d(st["joint_torque"]),
                             contacts=bad)
     assert e.value.code == 1
+
+
+def test_fb_frame_state_argument_errors(handle):
+    """blf_fb_frame_state refuses null frames / outputs and negative sizes with
+    BLF_ERR_INVALID_ARGUMENT (no device access)."""
+    import ctypes
+    B = 2
+    st = robot.random_states(MODEL, B, seed=1)
+    dm = handle.fb_model(MODEL)
+    fs = handle._fb_state({k: _d(st[k]) for k in native.FB_STATE_KEYS}, B, MODEL["n"])
+    out = _d(np.zeros((B, 1, 12)))
+    L = native.lib()
+    frames = _d(np.array([0], dtype=np.int32), torch.int32)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    for args in ((1, None, B, vp(out), None), (1, vp(frames), B, None, None), (-1, vp(frames), B, vp(out), None),
+                 (1, vp(frames), -1, vp(out), None)):
+        rc = L.blf_fb_frame_state(handle._h, ctypes.byref(dm.c), ctypes.byref(fs), args[0], args[1], args[2],
+                                  args[3], args[4], None)
+        assert rc == 1, args
