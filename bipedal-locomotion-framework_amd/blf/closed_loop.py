@@ -70,13 +70,22 @@ CONTACT_PARAMS = (0.12, 0.09, 2.0e6, 2.0e4)
 MAX_ITER = 100
 
 
+class _nullcontext:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class ClosedLoop:
     """A batch of robots, each closed around its own plan (problems.make_batch with the phase
     table), on one device.  `states` is a host dict (robot.standing_states), `plan` the host
     problem dict with a horizon of at least horizon + the number of periods to run."""
 
     def __init__(self, h, model, plan, states, horizon=100, dT=0.001, law=None,
-                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None, max_iter=MAX_ITER):
+                 contact_params=CONTACT_PARAMS, tol_polish=1e-4, stream=None, max_iter=MAX_ITER,
+                 cold_after_handover=None):
         import torch
         self.h, self.N, self.dT, self.stream = h, horizon, dT, stream
         dev = torch.device("cuda", h.device)
@@ -109,6 +118,15 @@ class ClosedLoop:
         self.prev = None
         self.s = 0
         self.expand_path = False   # True: blf_dcm_phase_expand + blf_dcm_mpc_solve (A/B)
+        # a robot whose last window needed the interior point method is planned cold: such windows
+        # recur on the robot's next periods, and from a cold start the windows the warm kernel hands
+        # over need 4.6 interior point iterations on average instead of 16.1 (DESIGN.md section 11,
+        # tools/c5_handover_starts.py) -- stage 2 is on each group's critical path
+        if cold_after_handover is None:   # BLF_C5_COLD_AFTER_HANDOVER=0: off (A/B)
+            import os
+            cold_after_handover = os.environ.get("BLF_C5_COLD_AFTER_HANDOVER", "1") != "0"
+        self.cold_after_handover = cold_after_handover
+        self.warm_status = torch.empty((self.B,), dtype=torch.int32, device=dev)
 
     def period(self):
         """One control period (stream-ordered; nothing synchronises).  Returns the plan."""
@@ -120,8 +138,14 @@ class ClosedLoop:
         warm = None
         if self.prev is not None:
             # a robot whose previous window was not solved (status != 0) is planned cold
+            status = self.prev["status"]
+            if self.cold_after_handover:   # status != 0 or iters > 0: start cold
+                import torch
+                with torch.cuda.stream(self.stream) if self.stream is not None else _nullcontext():
+                    torch.bitwise_or(status, (self.prev["iters"] > 0).to(torch.int32), out=self.warm_status)
+                status = self.warm_status
             warm = dict(vrp=self.prev["vrp"], lam=self.prev["lam"], shift=1, floor=1e-3,
-                        status=self.prev["status"])
+                        status=status)
         if N <= 128 and not self.expand_path:   # the window read from the phase table
             out = h.dcm_mpc_solve_phased(self.table, s, self.xi, self.omega[:, s:s + N],
                                          self.params, warm=warm, out=self.bufs[s % 2],

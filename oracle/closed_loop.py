@@ -92,7 +92,7 @@ class OracleLoop:
     """blf.closed_loop.ClosedLoop restated on the CPU (same inputs, same sequence)."""
 
     def __init__(self, model, plan, states, null_pose, law, contact_params, horizon=100, dT=0.001,
-                 tol_polish=1e-4, compiled=False, threads=8):
+                 tol_polish=1e-4, compiled=False, threads=8, cold_after_handover=True):
         """compiled: the rigid-body maps (centre of mass, the impedance-driven Euler steps) run the
         C restatement (blf_oracle_fbd.c) on `threads` threads instead of numpy (bench.py's
         configs[4] CPU baseline); the QP is the C oracle either way."""
@@ -114,6 +114,7 @@ class OracleLoop:
         self.params = O.default_params(horizon, tol_polish=tol_polish, max_iter=100)   # blf/closed_loop.py MAX_ITER
         self.prev = None
         self.s = 0
+        self.cold_after_handover = cold_after_handover
 
     def period(self):
         s, N = self.s, self.N
@@ -127,6 +128,9 @@ class OracleLoop:
         w.update(xi_init=xi, omega=omega)
         pv, pl, ps = ((None, None, None) if self.prev is None else
                       (self.prev["vrp"], self.prev["lam"], self.prev["status"]))
+        if ps is not None and self.cold_after_handover:
+            # blf/closed_loop.py: a robot whose last window needed the interior point method starts cold
+            ps = (ps | (self.prev["iters"] > 0)).astype(np.int32)
         pol = np.zeros(xi.shape[0], np.int32)
         # the window's QP and its warm start, kept for tests/golden/make_c5_windows.py
         self.last_window = dict(w, vrp_ws=pv, lam_ws=pl, prev_status=ps)
@@ -146,7 +150,7 @@ class OracleLoop:
                                            null_poses=self.null[i])
             for k in self.state:
                 self.state[k][i] = si[k]
-        self.prev = dict(vrp=vrp, lam=lam, status=st)
+        self.prev = dict(vrp=vrp, lam=lam, status=st, iters=it)
         self.s = s + 1
         return dict(status=st, xi=xo, vrp=vrp, iters=it, lam=lam, polished=pol, com=com,
                     xi_init=xi, q_ref=q_ref)

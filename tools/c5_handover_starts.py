@@ -43,7 +43,8 @@ def main():
                 keep[k].append(w[k][i].cpu().numpy())
             keep["vrp_ws"].append(prev["vrp"][i].cpu().numpy())
             keep["lam_ws"].append(prev["lam"][i].cpu().numpy())
-            keep["prev_status"].append(int(prev["status"][i]))
+            # the status the warm solve was given (the loop's cold-after-hand-over rule applied)
+            keep["prev_status"].append(int((loop.warm_status if loop.cold_after_handover else prev["status"])[i]))
             keep["period"].append(s)
             keep["iters"].append(int(it[i]))
     cap = {k: np.asarray(v) for k, v in keep.items()}
