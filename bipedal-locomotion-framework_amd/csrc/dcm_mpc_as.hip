@@ -121,6 +121,9 @@ struct LdsRows<float, MF> {
 #ifndef BLF_AS_OVERLAP
 #define BLF_AS_OVERLAP 1
 #endif
+#ifndef BLF_AS_KEEPIN
+#define BLF_AS_KEEPIN 1
+#endif
 
 // One facet row (normal, offset) in the scalar type of the pass.
 template <class T>
@@ -1236,6 +1239,9 @@ __device__ __forceinline__ void cold_solve(
                                 smem + 2 * (size_t)M * S, S, NH};
 
     AKnotT<float> F[KPL];
+    // BLF_AS_KEEPIN: the knots' fp64 inputs kept from phase A's loads for phase B (instead of
+    // reading them from global memory again after the float search)
+    KnotIn kin[KPL];
     int cand[KPL];         // the float search's next candidate sets (phase B's guess when uncertified)
     bool cert32 = false;   // the float search certified its point
     int npass32 = 0;       // its passes
@@ -1251,8 +1257,10 @@ __device__ __forceinline__ void cold_solve(
         Fj.rr0 = Fj.rr1 = Fj.xr0 = Fj.xr1 = 0.0f;
         Fj.rh0 = Fj.rh1 = Fj.d0 = Fj.d1 = Fj.qx0 = Fj.qx1 = 0.0f;
         Fj.P00 = Fj.P01 = Fj.P11 = Fj.h00 = Fj.h01 = Fj.h11 = 0.0f;
+        kin[j] = KnotIn{0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (k < N) {
             const KnotIn in = knot_in<PH>(p, k, N, omega, xi_ref, vrp_ref, nfacets, ps, sPh);
+            if (BLF_AS_KEEPIN) kin[j] = in;
             Fj.m = in.m < 0 ? 0 : in.m > M ? M : in.m;
             Fj.w = float(in.w);
             Fj.be = Pf.dt * Fj.w;
@@ -1304,7 +1312,7 @@ __device__ __forceinline__ void cold_solve(
         Kj.P00 = Kj.P01 = Kj.P11 = Kj.h00 = Kj.h01 = Kj.h11 = 0.0;
         Kj.rr0 = Kj.rr1 = Kj.xr0 = Kj.xr1 = 0.0;
         if (k < N) {
-            const KnotIn in = knot_in<PH>(p, k, N, omega, xi_ref, vrp_ref, nfacets, ps, sPh);
+            const KnotIn in = BLF_AS_KEEPIN ? kin[j] : knot_in<PH>(p, k, N, omega, xi_ref, vrp_ref, nfacets, ps, sPh);
             Kj.m = in.m;
             Kj.w = in.w;
             Kj.rr0 = in.rr0;
