@@ -41,7 +41,10 @@ constexpr float kSearchTolD = 1e-4f;
 constexpr double kGuessSlack = 1e-5;
 // The fp32 search hands over to the fp64 passes after a failed pass that changed the candidate
 // sets of at most N / kHandoverDiv knots (oracle ORC_HANDOVER_DIV).
-constexpr int kHandoverDiv = 16;
+#ifndef BLF_HANDOVER_DIV   // (A/B builds; the oracle's ORC_HANDOVER_DIV must match)
+#define BLF_HANDOVER_DIV 16
+#endif
+constexpr int kHandoverDiv = BLF_HANDOVER_DIV;
 // The fp64 certificate's dual tolerance grows with the knot's costate force once
 // |beta nu| > 1 / kTolDualRel: tol_d max(1, kTolDualRel max |beta nu|) (oracle ORC_TOL_DUAL_REL).
 // A planned walk keeps |beta nu| below ~2, so only the QPs of uncapturable DCM states (|beta nu|

@@ -555,7 +555,9 @@ static int ctz(int x) { int n = 0; while (!(x & 1)) { ++n; x >>= 1; } return n; 
 /* as_passes (float): returns 1 when a pass certifies.  A failed pass that changed the candidate
  * sets of at most N / ORC_HANDOVER_DIV knots ends the search (the kernel's handover): its next
  * candidate sets go to the fp64 passes (orc_dcm_mpc_solve_warm) instead of another float pass. */
+#ifndef ORC_HANDOVER_DIV
 #define ORC_HANDOVER_DIV 16   /* kernel kHandoverDiv */
+#endif
 static int passes32(s32* s)
 {
     const int N = s->N;
