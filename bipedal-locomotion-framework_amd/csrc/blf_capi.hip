@@ -185,8 +185,7 @@ blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m, con
                                    double final_time, double dT, void* stream)
 {
     BLF_REQUIRE(handle != nullptr, "blf_lti_euler_integrate: null handle");
-    BLF_REQUIRE(n >= 1 && n <= BLF_LTI_MAX_DIM && m >= 1 && m <= BLF_LTI_MAX_DIM,
-                "blf_lti_euler_integrate: n=%d m=%d outside [1, %d]", n, m, BLF_LTI_MAX_DIM);
+    BLF_REQUIRE(n >= 1 && m >= 1, "blf_lti_euler_integrate: n=%d m=%d, both must be >= 1", n, m);
     BLF_REQUIRE(batch >= 0, "blf_lti_euler_integrate: negative batch");
     BLF_REQUIRE(batch == 0 || (A && Bm && u && x), "blf_lti_euler_integrate: null buffer");
     int iterations = 0;
@@ -202,8 +201,7 @@ blf_status blf_lti_dynamics(blf_handle* handle, int32_t n, int32_t m, const doub
                             const double* x, double* dx, int64_t batch, void* stream)
 {
     BLF_REQUIRE(handle != nullptr, "blf_lti_dynamics: null handle");
-    BLF_REQUIRE(n >= 1 && n <= BLF_LTI_MAX_DIM && m >= 1 && m <= BLF_LTI_MAX_DIM,
-                "blf_lti_dynamics: n=%d m=%d outside [1, %d]", n, m, BLF_LTI_MAX_DIM);
+    BLF_REQUIRE(n >= 1 && m >= 1, "blf_lti_dynamics: n=%d m=%d, both must be >= 1", n, m);
     BLF_REQUIRE(batch >= 0, "blf_lti_dynamics: negative batch");
     BLF_REQUIRE(batch == 0 || (A && Bm && u && x && dx), "blf_lti_dynamics: null buffer");
     return launch_lti_dynamics(n, m, A, Bm, shared_matrices, u, x, dx, batch, (hipStream_t)stream);

@@ -1,7 +1,7 @@
 // euler_rollout.hip — ForwardEuler<LinearTimeInvariantSystem> on the device.
 //
 //  * lti_euler_kernel: FixedStepIntegrator::integrate(t0, T) for a batch of small LTI systems
-//    (n, m <= 8; lti_euler_wg_kernel up to BLF_LTI_MAX_DIM)
+//    (n, m <= 8; lti_euler_wg_kernel up to 512; lti_euler_big_kernel any size)
 //    (reference: src/System/include/BipedalLocomotion/System/FixedStepIntegrator.tpp:21-72,
 //    ForwardEuler.tpp:18-49, src/System/src/LinearTimeInvariantSystem.cpp:71).  The step
 //    schedule (count and the stale-time last step) is computed once on the host (blf_capi.hip)
@@ -72,11 +72,12 @@ __global__ __launch_bounds__(256) void lti_euler_kernel(int n, int m, const doub
         if (r < n) x[q * n + r] = xr[r];
 }
 
-// Systems with n or m above kNmax (up to BLF_LTI_MAX_DIM): one 64-lane workgroup per system, x and
+// Systems with n or m above kNmax (up to kLtiWgMax): one 64-lane workgroup per system, x and
 // B u in LDS, thread t owning rows t, t + 64, ...; each row's sums run left to right exactly as in
 // lti_euler_kernel and the oracle, so the results are the same bits.  A and B are read from
 // global memory (L2; one copy for every system when shared).
-constexpr int kLtiRowsPerLane = (BLF_LTI_MAX_DIM + 63) / 64;
+constexpr int kLtiWgMax = 512;   // lti_euler_wg_kernel's limit; above it, lti_euler_big_kernel
+constexpr int kLtiRowsPerLane = (kLtiWgMax + 63) / 64;
 
 __global__ __launch_bounds__(64) void lti_euler_wg_kernel(int n, int m, const double* __restrict__ A,
                                                           const double* __restrict__ Bm, int shared,
@@ -143,6 +144,71 @@ __global__ __launch_bounds__(256) void lti_dynamics_kernel(int n, int m,
         for (int c = 1; c < m; ++c) bu = bu + Bq[r * m + c] * u[q * m + c];
         dx[q * n + r] = ax + bu;
     }
+}
+
+// Systems above kLtiWgMax (any size, round 5): one 256-thread workgroup per system, the state
+// updated in place in x and B u / dx in a global scratch ([batch][n] each), thread t owning rows
+// t, t + 256, ...  Each row's sums run left to right as in the kernels above and the oracle (the
+// same bits).  A row of A is read once per step; the x it is dotted with stays in L1/L2.  The
+// barriers order the reads of step i before the writes of x (__syncthreads is the workgroup-scope
+// fence for global memory too).
+__global__ __launch_bounds__(256) void lti_euler_big_kernel(int n, int m, const double* __restrict__ A,
+                                                            const double* __restrict__ Bm, int shared,
+                                                            const double* __restrict__ u, double* x,
+                                                            double* scratch, int32_t nsteps,
+                                                            double dT, double dT_last)
+{
+    const int64_t q = blockIdx.x;
+    const int t = threadIdx.x;
+    const int64_t nn = n;
+    const double* Aq = shared ? A : A + q * nn * nn;
+    const double* Bq = shared ? Bm : Bm + q * nn * m;
+    const double* uq = u + q * m;
+    double* xq = x + q * nn;
+    double* bs = scratch + 2 * q * nn;
+    double* dxs = bs + nn;
+    for (int r = t; r < n; r += 256) {
+        const double* Br = Bq + (int64_t)r * m;
+        double acc = Br[0] * uq[0];
+        for (int c = 1; c < m; ++c) acc = acc + Br[c] * uq[c];
+        bs[r] = acc;
+    }
+    for (int32_t i = 0; i < nsteps; ++i) {
+        const double h = (i == nsteps - 1) ? dT_last : dT;
+        for (int r = t; r < n; r += 256) {
+            const double* Ar = Aq + (int64_t)r * nn;
+            double acc = Ar[0] * xq[0];
+            for (int c = 1; c < n; ++c) acc = acc + Ar[c] * xq[c];
+            dxs[r] = acc + bs[r];
+        }
+        __syncthreads();
+        for (int r = t; r < n; r += 256) xq[r] = xq[r] + dxs[r] * h;
+        __syncthreads();
+    }
+}
+
+// dx = A x + B u for systems above kLtiWgMax: one thread per row, rblocks row blocks per system.
+__global__ __launch_bounds__(256) void lti_dynamics_rows_kernel(int n, int m,
+                                                                const double* __restrict__ A,
+                                                                const double* __restrict__ Bm,
+                                                                int shared,
+                                                                const double* __restrict__ u,
+                                                                const double* __restrict__ x,
+                                                                double* __restrict__ dx, int rblocks)
+{
+    const int64_t q = blockIdx.x / rblocks;
+    const int r = (int)(blockIdx.x % rblocks) * 256 + threadIdx.x;
+    if (r >= n) return;
+    const int64_t nn = n;
+    const double* Ar = (shared ? A : A + q * nn * nn) + (int64_t)r * nn;
+    const double* Br = (shared ? Bm : Bm + q * nn * m) + (int64_t)r * m;
+    const double* xq = x + q * nn;
+    const double* uq = u + q * m;
+    double ax = Ar[0] * xq[0];
+    for (int c = 1; c < n; ++c) ax = ax + Ar[c] * xq[c];
+    double bu = Br[0] * uq[0];
+    for (int c = 1; c < m; ++c) bu = bu + Br[c] * uq[c];
+    dx[q * nn + r] = ax + bu;
 }
 
 // 64 problems per workgroup (one wave), knots staged in chunks of KC.  The chunk's omega and
@@ -392,10 +458,22 @@ blf_status launch_lti_euler(int n, int m, const double* A, const double* Bm, int
         if (batch > 0x7fffffffLL)
             return set_error(BLF_ERR_UNSUPPORTED, "lti_euler: %lld systems of size %d too many",
                              (long long)batch, n);
-        hipLaunchKernelGGL(lti_euler_wg_kernel, dim3((unsigned)batch), dim3(64),
-                           2 * sizeof(double) * (size_t)n, s, n, m, A, Bm, shared, u, x, nsteps, dT,
-                           dT_last);
-        return check_hip(hipGetLastError(), "lti_euler_wg_kernel launch");
+        if (n <= kLtiWgMax && m <= kLtiWgMax) {
+            hipLaunchKernelGGL(lti_euler_wg_kernel, dim3((unsigned)batch), dim3(64),
+                               2 * sizeof(double) * (size_t)n, s, n, m, A, Bm, shared, u, x, nsteps,
+                               dT, dT_last);
+            return check_hip(hipGetLastError(), "lti_euler_wg_kernel launch");
+        }
+        // B u and dx scratch, stream-ordered: allocated, used and released on s.
+        double* scratch = nullptr;
+        const size_t bytes = 2 * sizeof(double) * (size_t)n * (size_t)batch;
+        blf_status st = check_hip(hipMallocAsync((void**)&scratch, bytes, s), "lti_euler scratch");
+        if (st != BLF_OK) return st;
+        hipLaunchKernelGGL(lti_euler_big_kernel, dim3((unsigned)batch), dim3(256), 0, s, n, m, A, Bm,
+                           shared, u, x, scratch, nsteps, dT, dT_last);
+        st = check_hip(hipGetLastError(), "lti_euler_big_kernel launch");
+        const blf_status fr = check_hip(hipFreeAsync(scratch, s), "lti_euler scratch free");
+        return st != BLF_OK ? st : fr;
     }
     const int64_t blocks = ceil_div(batch, 256);
     hipLaunchKernelGGL(lti_euler_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, m, A, Bm,
@@ -408,6 +486,15 @@ blf_status launch_lti_dynamics(int n, int m, const double* A, const double* Bm, 
                                hipStream_t s)
 {
     if (batch == 0) return BLF_OK;
+    if (n > kLtiWgMax || m > kLtiWgMax) {
+        const int64_t rblocks = ceil_div(n, 256);
+        if (batch * rblocks > 0x7fffffffLL)
+            return set_error(BLF_ERR_UNSUPPORTED, "lti_dynamics: %lld systems of size %d too many",
+                             (long long)batch, n);
+        hipLaunchKernelGGL(lti_dynamics_rows_kernel, dim3((unsigned)(batch * rblocks)), dim3(256), 0,
+                           s, n, m, A, Bm, shared, u, x, dx, (int)rblocks);
+        return check_hip(hipGetLastError(), "lti_dynamics_rows_kernel launch");
+    }
     hipLaunchKernelGGL(lti_dynamics_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256), 0, s,
                        n, m, A, Bm, shared, u, x, dx, batch);
     return check_hip(hipGetLastError(), "lti_dynamics_kernel launch");

@@ -3,7 +3,7 @@
  * Drop-in for src/System/include/BipedalLocomotion/System/LinearTimeInvariantSystem.h:35-69
  * (src/System/src/LinearTimeInvariantSystem.cpp:13-74): dx = A x + B u.  The matrices, state and
  * input are mirrored to device memory; dynamics() runs blf_lti_dynamics and ForwardEuler runs
- * blf_lti_euler_integrate (n, m <= BLF_LTI_MAX_DIM = 512).
+ * blf_lti_euler_integrate (any n, m >= 1).
  */
 #ifndef BLF_BIPEDAL_LOCOMOTION_SYSTEM_LTI_H
 #define BLF_BIPEDAL_LOCOMOTION_SYSTEM_LTI_H

@@ -25,18 +25,19 @@ bool LinearTimeInvariantSystem::setSystemMatrices(const blf::MatrixXd& A, const 
                   << std::endl;
         return false;
     }
-    if (A.rows() < 1 || A.rows() > BLF_LTI_MAX_DIM || B.cols() < 1 || B.cols() > BLF_LTI_MAX_DIM)
-    {
-        std::cerr << "[LinearTimeInvariantSystem::setSystemMatrices] The device integrator "
-                     "supports 1 <= n, m <= " << BLF_LTI_MAX_DIM << "."
-                  << std::endl;
-        return false;
-    }
     m_A = A;
     m_B = B;
-    if (!m_dA.upload(m_A.data(), m_A.rows() * m_A.cols()) ||
-        !m_dB.upload(m_B.data(), m_B.rows() * m_B.cols()))
-        return false;
+    // Any size, as the reference.  An input-free system (B with no columns) runs with one zero
+    // column and a zero input: Eigen's B u is then a zero vector too, so dx = A x + 0 either way.
+    // An empty system (n = 0) has nothing on the device.
+    const std::size_t n = m_A.rows();
+    if (n > 0)
+    {
+        const blf::VectorXd zero(n, 0.0);
+        if (!m_dA.upload(m_A.data(), n * n) ||
+            !(m_B.cols() > 0 ? m_dB.upload(m_B.data(), n * m_B.cols()) : m_dB.upload(zero.data(), n)))
+            return false;
+    }
     m_isInitialized = true;
     return true;
 }
@@ -72,15 +73,19 @@ bool LinearTimeInvariantSystem::dynamics(const double& time, StateDerivativeType
     const blf::VectorXd& x = std::get<0>(m_state);
     const blf::VectorXd& u = std::get<0>(m_controlInput);
     const int n = static_cast<int>(m_A.rows()), m = static_cast<int>(m_B.cols());
-    blf_handle* h = blf::threadHandle();
-    if (h == nullptr) return false;
-    if (!m_dx.upload(x.data(), n) || !m_du.upload(u.data(), m) || !m_ddx.resize(n)) return false;
-    if (!blf::report(blf_lti_dynamics(h, n, m, m_dA.data(), m_dB.data(), 1, m_du.data(),
-                                      m_dx.data(), m_ddx.data(), 1, nullptr),
-                     "LinearTimeInvariantSystem::dynamics"))
-        return false;
     blf::VectorXd& dx = std::get<0>(stateDerivative);
     dx.resize(n);
+    if (n == 0) return true;
+    blf_handle* h = blf::threadHandle();
+    if (h == nullptr) return false;
+    const double zero = 0.0;
+    if (!m_dx.upload(x.data(), n) || !m_du.upload(m > 0 ? u.data() : &zero, m > 0 ? m : 1) ||
+        !m_ddx.resize(n))
+        return false;
+    if (!blf::report(blf_lti_dynamics(h, n, m > 0 ? m : 1, m_dA.data(), m_dB.data(), 1,
+                                      m_du.data(), m_dx.data(), m_ddx.data(), 1, nullptr),
+                     "LinearTimeInvariantSystem::dynamics"))
+        return false;
     return m_ddx.download(dx.data(), n);
 }
 
@@ -90,10 +95,19 @@ bool LinearTimeInvariantSystem::forwardEulerIntegrate(double initialTime, double
     blf::VectorXd& x = std::get<0>(m_state);
     const blf::VectorXd& u = std::get<0>(m_controlInput);
     const int n = static_cast<int>(m_A.rows()), m = static_cast<int>(m_B.cols());
+    if (n == 0)   // nothing to integrate; the schedule's argument checks still apply
+    {
+        int32_t it = 0;
+        double dTl = 0.0, tl = 0.0;
+        return blf::report(blf_step_schedule(initialTime, finalTime, dT, &it, &dTl, &tl),
+                           "FixedStepIntegrator::integrate");
+    }
     blf_handle* h = blf::threadHandle();
     if (h == nullptr) return false;
-    if (!m_dx.upload(x.data(), n) || !m_du.upload(u.data(), m)) return false;
-    if (!blf::report(blf_lti_euler_integrate(h, n, m, m_dA.data(), m_dB.data(), 1, m_du.data(),
+    const double zero = 0.0;
+    if (!m_dx.upload(x.data(), n) || !m_du.upload(m > 0 ? u.data() : &zero, m > 0 ? m : 1))
+        return false;
+    if (!blf::report(blf_lti_euler_integrate(h, n, m > 0 ? m : 1, m_dA.data(), m_dB.data(), 1, m_du.data(),
                                              m_dx.data(), 1, initialTime, finalTime, dT, nullptr),
                      "FixedStepIntegrator::integrate"))
         return false;

@@ -246,6 +246,228 @@ static void testIntegratorLTI()
     REQUIRE_FALSE(bad.integrate(0.0, 1.0));
 }
 
+// ---- ForwardEuler over a host-side DynamicalSystem subclass (ForwardEuler.tpp:18-49) ----------
+// The reference's IntegratorTest system written as a user's CPU system: dx = A x + B u with the
+// device kernel's summation order, so its trajectory is bit for bit blf_lti_euler_integrate's.
+class HostLinearSystem
+    : public DynamicalSystem<std::tuple<blf::VectorXd>, std::tuple<blf::VectorXd>,
+                             std::tuple<blf::VectorXd>>
+{
+public:
+    int calls = 0;
+    bool dynamics(const double& time, StateDerivativeType& stateDerivative) final
+    {
+        (void)time;
+        ++calls;
+        const auto& x = std::get<0>(m_state);
+        const auto& u = std::get<0>(m_controlInput);
+        auto& dx = std::get<0>(stateDerivative);
+        dx.resize(2);
+        const double A[2][2] = {{0, 1}, {-2, -2}}, B[2] = {0, 2};
+        for (int r = 0; r < 2; ++r)
+        {
+            double ax = 0.0;
+            for (int c = 0; c < 2; ++c) ax = ax + A[r][c] * x[c];
+            dx[r] = ax + B[r] * u[0];
+        }
+        return true;
+    }
+};
+
+// A time-varying system with a two-element state (vector + scalar): the scalar uses `+=`, the
+// vector the entry-wise path; the time argument of every step is recorded.
+class HostClock
+    : public DynamicalSystem<std::tuple<blf::VectorXd, double>, std::tuple<blf::VectorXd, double>,
+                             std::tuple<double>>
+{
+public:
+    std::vector<double> times;
+    bool failAt = false;
+    bool dynamics(const double& time, StateDerivativeType& stateDerivative) final
+    {
+        times.push_back(time);
+        if (failAt && times.size() == 3) return false;
+        auto& [dv, ds] = stateDerivative;
+        dv = blf::VectorXd{std::cos(time), std::get<0>(m_controlInput)};
+        ds = std::get<1>(m_state) * -0.5;
+        return true;
+    }
+};
+
+static void testIntegratorHostSystem()
+{
+    // IntegratorTest.cpp:27-75 on the host-side system: the analytic solution at 1e-3.
+    constexpr double dT = 0.0001, tolerance = 1e-3, simulationTime = 2;
+    auto system = std::make_shared<HostLinearSystem>();
+    system->setControlInput({blf::VectorXd{1.0}});
+    system->setState({blf::VectorXd{0.0, 0.0}});
+    ForwardEuler<HostLinearSystem> integrator(dT);
+    REQUIRE(integrator.setDynamicalSystem(system));
+    bool ok = true;
+    for (int i = 0; i < simulationTime / dT; i++)
+    {
+        const auto& [x] = integrator.getSolution();
+        const double t = dT * i;
+        const double e0 = 1 - std::exp(-t) * (std::cos(t) + std::sin(t));
+        const double e1 = 2 * std::exp(-t) * std::sin(t);
+        const double dn = std::hypot(x(0) - e0, x(1) - e1);
+        ok = ok && dn <= tolerance * std::min(std::hypot(x(0), x(1)), std::hypot(e0, e1));
+        ok = ok && integrator.integrate(0, dT);
+        if (!ok) break;
+    }
+    REQUIRE(ok);
+    REQUIRE(system->calls == int(simulationTime / dT));
+
+    // The schedule, literally FixedStepIntegrator.tpp:48-64: ceil((T - t0)/dT) steps, the last at
+    // the stale time with the remainder step.
+    auto clock = std::make_shared<HostClock>();
+    clock->setState({blf::VectorXd{0.0, 1.0}, 2.0});
+    clock->setControlInput({0.25});
+    ForwardEuler<HostClock> euler(0.3);
+    REQUIRE(euler.setDynamicalSystem(clock));
+    REQUIRE(euler.integrate(0.1, 1.0));
+    const int iters = int(std::ceil((1.0 - 0.1) / 0.3));
+    double v0 = 0.0, v1 = 1.0, s = 2.0, cur = 0.1;
+    std::vector<double> expect;
+    for (std::size_t i = 0; i < std::size_t(iters - 1); i++)
+    {
+        cur = 0.1 + 0.3 * i;
+        expect.push_back(cur);
+        const double d0 = std::cos(cur), d1 = 0.25, ds = s * -0.5;
+        v0 = v0 + d0 * 0.3, v1 = v1 + d1 * 0.3, s += ds * 0.3;
+    }
+    const double last = 1.0 - cur;
+    expect.push_back(cur);
+    {
+        const double d0 = std::cos(cur), d1 = 0.25, ds = s * -0.5;
+        v0 = v0 + d0 * last, v1 = v1 + d1 * last, s += ds * last;
+    }
+    REQUIRE(clock->times == expect);
+    const auto& [v, sc] = euler.getSolution();
+    REQUIRE(v(0) == v0);
+    REQUIRE(v(1) == v1);
+    REQUIRE(sc == s);
+
+    // Errors: the reference's argument checks, a failing dynamics() mid-schedule, a derivative of
+    // the wrong size.
+    REQUIRE_FALSE(euler.integrate(1.0, 0.5));
+    REQUIRE_FALSE(euler.integrate(1.0, 1.0));
+    clock->times.clear();
+    clock->failAt = true;
+    REQUIRE_FALSE(euler.integrate(0.0, 1.0));
+    REQUIRE(clock->times.size() == 3);
+    ForwardEuler<HostClock> negative(-0.1);
+    REQUIRE(negative.setDynamicalSystem(clock));
+    REQUIRE_FALSE(negative.integrate(0.0, 1.0));
+    auto wrong = std::make_shared<HostLinearSystem>();
+    wrong->setControlInput({blf::VectorXd{1.0}});
+    wrong->setState({blf::VectorXd{0.0, 0.0, 0.0}});
+    ForwardEuler<HostLinearSystem> mismatch(0.1);
+    REQUIRE(mismatch.setDynamicalSystem(wrong));
+    REQUIRE_FALSE(mismatch.integrate(0.0, 0.3));
+}
+
+// LinearTimeInvariantSystem of any size (LinearTimeInvariantSystem.cpp:13-38 takes any): a 600-state
+// system against the host-side loop (same sums, same bits), an input-free system (B with no
+// columns) and an empty one (device).
+class HostLti
+    : public DynamicalSystem<std::tuple<blf::VectorXd>, std::tuple<blf::VectorXd>,
+                             std::tuple<blf::VectorXd>>
+{
+public:
+    blf::MatrixXd A, B;
+    bool dynamics(const double&, StateDerivativeType& stateDerivative) final
+    {
+        const auto& x = std::get<0>(m_state);
+        const auto& u = std::get<0>(m_controlInput);
+        auto& dx = std::get<0>(stateDerivative);
+        dx.resize(A.rows());
+        for (std::size_t r = 0; r < A.rows(); ++r)
+        {
+            double ax = A(r, 0) * x[0];
+            for (std::size_t c = 1; c < A.cols(); ++c) ax = ax + A(r, c) * x[c];
+            double bu = B.cols() ? B(r, 0) * u[0] : 0.0;
+            for (std::size_t c = 1; c < B.cols(); ++c) bu = bu + B(r, c) * u[c];
+            dx[r] = ax + bu;
+        }
+        return true;
+    }
+};
+
+static void testIntegratorLTIAnySize()
+{
+    std::mt19937_64 rng(11);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    for (const auto& [n, m] : {std::pair<int, int>{600, 3}, std::pair<int, int>{70, 0}})
+    {
+        blf::MatrixXd A(n, n), B(n, m);
+        for (int r = 0; r < n; ++r)
+        {
+            for (int c = 0; c < n; ++c) A(r, c) = U(rng) / n;
+            for (int c = 0; c < m; ++c) B(r, c) = U(rng);
+        }
+        blf::VectorXd x0(n), u(m);
+        for (int r = 0; r < n; ++r) x0[r] = U(rng);
+        for (int c = 0; c < m; ++c) u[c] = U(rng);
+        auto dev = std::make_shared<LinearTimeInvariantSystem>();
+        auto host = std::make_shared<HostLti>();
+        host->A = A, host->B = B;
+        REQUIRE(dev->setSystemMatrices(A, B));
+        dev->setState({x0}), host->setState({x0});
+        dev->setControlInput({u}), host->setControlInput({u});
+        ForwardEuler<LinearTimeInvariantSystem> di(0.01);
+        ForwardEuler<HostLti> hi(0.01);
+        REQUIRE(di.setDynamicalSystem(dev));
+        REQUIRE(hi.setDynamicalSystem(host));
+        REQUIRE(di.integrate(0.0, 0.045));
+        REQUIRE(hi.integrate(0.0, 0.045));
+        const auto& [xd] = di.getSolution();
+        const auto& [xh] = hi.getSolution();
+        bool same = xd.size() == std::size_t(n);
+        for (int r = 0; same && r < n; ++r) same = xd[r] == xh[r];
+        REQUIRE(same);
+        std::tuple<blf::VectorXd> dd, dh;
+        REQUIRE(dev->dynamics(0.0, dd));
+        REQUIRE(host->dynamics(0.0, dh));
+        same = std::get<0>(dd).size() == std::size_t(n);
+        for (int r = 0; same && r < n; ++r) same = std::get<0>(dd)[r] == std::get<0>(dh)[r];
+        REQUIRE(same);
+    }
+    auto empty = std::make_shared<LinearTimeInvariantSystem>();
+    REQUIRE(empty->setSystemMatrices(blf::MatrixXd(0, 0), blf::MatrixXd(0, 0)));
+    empty->setState({blf::VectorXd{}});
+    empty->setControlInput({blf::VectorXd{}});
+    ForwardEuler<LinearTimeInvariantSystem> ei(0.1);
+    REQUIRE(ei.setDynamicalSystem(empty));
+    REQUIRE(ei.integrate(0.0, 1.0));
+    REQUIRE_FALSE(ei.integrate(1.0, 0.0));
+    std::tuple<blf::VectorXd> de;
+    REQUIRE(empty->dynamics(0.0, de));
+    REQUIRE(std::get<0>(de).size() == 0);
+}
+
+// The host-side system and the device LTI integrator give the same bits (device).
+static void testIntegratorHostSystemMatchesDevice()
+{
+    auto host = std::make_shared<HostLinearSystem>();
+    auto dev = std::make_shared<LinearTimeInvariantSystem>();
+    REQUIRE(dev->setSystemMatrices(blf::MatrixXd(2, 2, {0, 1, -2, -2}), blf::MatrixXd(2, 1, {0, 2})));
+    host->setControlInput({blf::VectorXd{1.0}});
+    dev->setControlInput({blf::VectorXd{1.0}});
+    host->setState({blf::VectorXd{0.3, -0.2}});
+    dev->setState({blf::VectorXd{0.3, -0.2}});
+    ForwardEuler<HostLinearSystem> hi(0.001);
+    ForwardEuler<LinearTimeInvariantSystem> di(0.001);
+    REQUIRE(hi.setDynamicalSystem(host));
+    REQUIRE(di.setDynamicalSystem(dev));
+    REQUIRE(hi.integrate(0.0, 0.9995));
+    REQUIRE(di.integrate(0.0, 0.9995));
+    const auto& [xh] = hi.getSolution();
+    const auto& [xd] = di.getSolution();
+    REQUIRE(xh(0) == xd(0));
+    REQUIRE(xh(1) == xd(1));
+}
+
 // ---- ConvexHullHelper (device, 2-D) -----------------------------------------------------------
 static void testConvexHull()
 {
@@ -1187,6 +1409,9 @@ int main(int argc, char** argv)
         {"VariablesHandler", false, testVariablesHandler},
         {"ParametersHandler (config.ini)", false, testParametersHandler},
         {"Integrator - Linear system", true, testIntegratorLTI},
+        {"Integrator - host-side system", false, testIntegratorHostSystem},
+        {"Integrator - host-side system == device LTI", true, testIntegratorHostSystemMatchesDevice},
+        {"Integrator - LTI of any size", true, testIntegratorLTIAnySize},
         {"Convex Hull helper (2-D)", true, testConvexHull},
         {"Convex Hull helper (3-D, ConvexHullHelperTest.cpp)", true, testConvexHull3},
         {"QuinticSpline", true, testQuinticSpline},

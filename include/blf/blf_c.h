@@ -110,10 +110,10 @@ blf_status blf_step_schedule(double initial_time, double final_time, double dT,
  *   advances by (T - currentTime) with the stale currentTime = t0 + dT*(iters-2) (0 if iters<2).
  * A: [B][n][n] row-major, Bm: [B][n][m] (or a single shared matrix when `shared_matrices` != 0),
  * u: [B][m] (held constant, as setControlInput does), x: [B][n] updated in place.
- * 1 <= n, m <= BLF_LTI_MAX_DIM (n, m <= 8: one lane per system, registers; larger: one
- * workgroup per system, state in LDS — the same arithmetic order, so the same bits).  Arithmetic order (no FMA contraction): dx_r = (sum_c A_rc x_c) + (sum_c B_rc u_c),
+ * n, m >= 1, any size (n, m <= 8: one lane per system, registers; up to 512: one 64-lane
+ * workgroup per system, state in LDS; larger: one 256-thread workgroup per system, state in x and
+ * a stream-ordered scratch — the same arithmetic order everywhere, so the same bits).  Arithmetic order (no FMA contraction): dx_r = (sum_c A_rc x_c) + (sum_c B_rc u_c),
  * each sum left to right; x_r = x_r + dx_r * dT_i.                                            */
-#define BLF_LTI_MAX_DIM 512
 blf_status blf_lti_euler_integrate(blf_handle* handle, int32_t n, int32_t m,
                                    const double* A, const double* Bm, int32_t shared_matrices,
                                    const double* u, double* x, int64_t batch,

@@ -15,18 +15,17 @@
 /* ------------------------------------------------------------------------------------------ */
 /* ForwardEuler<LinearTimeInvariantSystem>::integrate — FixedStepIntegrator.tpp:21-72          */
 /* ------------------------------------------------------------------------------------------ */
-#define ORC_LTI_MAX_DIM 512   /* BLF_LTI_MAX_DIM */
-
 static void lti_step(int n, int m, const double* A, const double* B, const double* u, double* x,
-                     double dT)
+                     double dT, double* dx)
 {
     /* LinearTimeInvariantSystem.cpp:71  dx = A x + B u ;  ForwardEuler.tpp:36-38  x += dx*dT */
-    double dx[ORC_LTI_MAX_DIM];
     for (int r = 0; r < n; ++r) {
-        double ax = A[r * n + 0] * x[0];
-        for (int c = 1; c < n; ++c) ax = ax + A[r * n + c] * x[c];
-        double bu = B[r * m + 0] * u[0];
-        for (int c = 1; c < m; ++c) bu = bu + B[r * m + c] * u[c];
+        const double* Ar = A + (int64_t)r * n;
+        const double* Br = B + (int64_t)r * m;
+        double ax = Ar[0] * x[0];
+        for (int c = 1; c < n; ++c) ax = ax + Ar[c] * x[c];
+        double bu = Br[0] * u[0];
+        for (int c = 1; c < m; ++c) bu = bu + Br[c] * u[c];
         dx[r] = ax + bu;
     }
     for (int r = 0; r < n; ++r) x[r] = x[r] + dx[r] * dT;
@@ -35,22 +34,25 @@ static void lti_step(int n, int m, const double* A, const double* B, const doubl
 int orc_lti_euler_integrate(int n, int m, const double* A, const double* B, const double* u,
                             double* x, double t0, double t1, double dT, int64_t* nsteps_out)
 {
-    if (n < 1 || n > ORC_LTI_MAX_DIM || m < 1 || m > ORC_LTI_MAX_DIM) return 1;
+    if (n < 1 || m < 1) return 1;                 /* any size (the C ABI's n, m >= 1)          */
     if (t0 > t1 || !(dT > 0)) return 4;           /* FixedStepIntegrator.tpp:28-46            */
     if (t0 == t1) return 5;                       /* reference: size_t(i) < -1 -> never ends   */
     double q = ceil((t1 - t0) / dT);
     if (!(q < 2.0e9)) return 3;
+    double* dx = (double*)malloc(sizeof(double) * (size_t)n);
+    if (!dx) return 2;
     int iterations = (int)q;                      /* FixedStepIntegrator.tpp:48               */
     double currentTime = t0;
     int64_t steps = 0;
     for (int64_t i = 0; i < (int64_t)iterations - 1; ++i) {   /* :51-61                      */
         currentTime = t0 + dT * (double)i;
-        lti_step(n, m, A, B, u, x, dT);
+        lti_step(n, m, A, B, u, x, dT, dx);
         ++steps;
     }
     double last = t1 - currentTime;               /* :63-70 stale currentTime                 */
-    lti_step(n, m, A, B, u, x, last);
+    lti_step(n, m, A, B, u, x, last, dx);
     ++steps;
+    free(dx);
     if (nsteps_out) *nsteps_out = steps;
     return 0;
 }

@@ -85,13 +85,47 @@ def test_lti_integrator_large_systems(handle, oracle, n, m, shared):
         np.testing.assert_allclose(dx[i], Ai @ x0[i] + Bi @ u[i], rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("n,m,shared,B", [(513, 1, True, 3), (600, 700, False, 2), (9, 600, True, 4),
+                                          (1100, 2, True, 1)])
+def test_lti_integrator_any_size(handle, oracle, n, m, shared, B):
+    """Above 512 (lti_euler_big_kernel, lti_dynamics_rows_kernel; the reference takes any size,
+    LinearTimeInvariantSystem.cpp:13-38): bit-identical to the oracle's left-to-right sums."""
+    rng = np.random.default_rng(n + 7 * m)
+    A = rng.uniform(-1, 1, (n, n) if shared else (B, n, n)) / n
+    Bm = rng.uniform(-1, 1, (n, m) if shared else (B, n, m)) / m
+    u = rng.uniform(-1, 1, (B, m))
+    x0 = rng.uniform(-1, 1, (B, n))
+    x = _d(x0)
+    handle.lti_euler_integrate(_d(A), _d(Bm), _d(u), x, 0.0, 0.045, 0.01, shared=shared)
+    xg = x.cpu().numpy()
+    for i in range(B):
+        st, xo, steps = oracle.lti_euler_integrate(A if shared else A[i], Bm if shared else Bm[i], u[i],
+                                                   x0[i], 0.0, 0.045, 0.01)
+        assert st == 0 and steps == 5
+        np.testing.assert_array_equal(xg[i], xo)
+    dx = handle.lti_dynamics(_d(A), _d(Bm), _d(u), _d(x0), shared=shared).cpu().numpy()
+    for i in range(B):
+        Ai, Bi = (A, Bm) if shared else (A[i], Bm[i])
+        ax = np.zeros(n); bu = np.zeros(n)
+        ax[:] = Ai[:, 0] * x0[i, 0]
+        for c in range(1, n):
+            ax = ax + Ai[:, c] * x0[i, c]
+        bu[:] = Bi[:, 0] * u[i, 0]
+        for c in range(1, m):
+            bu = bu + Bi[:, c] * u[i, c]
+        np.testing.assert_array_equal(dx[i], ax + bu)   # the same left-to-right sums, bit for bit
+
+
 def test_lti_integrator_size_limit(handle):
-    n = 513
-    x = _d(np.zeros((1, n)))
-    with pytest.raises(native.BlfError) as e:
-        handle.lti_euler_integrate(_d(np.eye(n)), _d(np.ones((n, 1))), _d(np.ones((1, 1))), x, 0.0, 1.0,
-                                   0.1, shared=True)
-    assert e.value.code == 1
+    """Empty systems are refused by the C ABI (the adapter handles n = 0 and m = 0 itself)."""
+    A = _d(np.eye(1)); x = _d(np.zeros((1, 1)))
+    for n, m in [(0, 1), (1, 0)]:
+        rc = native.lib().blf_lti_euler_integrate(handle._h, n, m, A.data_ptr(), A.data_ptr(), 1,
+                                                  A.data_ptr(), x.data_ptr(), 1, 0.0, 1.0, 0.1, None)
+        assert rc == 1
+        rc = native.lib().blf_lti_dynamics(handle._h, n, m, A.data_ptr(), A.data_ptr(), 1, A.data_ptr(),
+                                           x.data_ptr(), x.data_ptr(), 1, None)
+        assert rc == 1
 
 
 def test_lti_integrator_errors(handle):

@@ -49,8 +49,9 @@ def test_integrator_step_schedule_quirks():
 
 
 def test_integrator_lti_large_system_is_euler():
-    """n, m above 8 (up to BLF_LTI_MAX_DIM = 512): the same step, pinned against a plain numpy
-    Euler loop of the reference's schedule (to rounding) and the size limit."""
+    """n, m above 8 (any size, as LinearTimeInvariantSystem.cpp:13-38): the same step, pinned
+    against a plain numpy Euler loop of the reference's schedule (to rounding); empty sizes are
+    refused."""
     rng = np.random.default_rng(5)
     n, m = 40, 7
     A = rng.uniform(-1, 1, (n, n)) / n
@@ -63,7 +64,17 @@ def test_integrator_lti_large_system_is_euler():
     for h in [0.01] * 9 + [0.093 - 0.08]:   # the stale last step of FixedStepIntegrator.tpp:63-70
         xr = xr + (A @ xr + B @ u) * h
     np.testing.assert_allclose(x, xr, rtol=1e-12, atol=1e-13)
-    assert O.lti_euler_integrate(np.eye(513), np.ones((513, 1)), [1.0], np.zeros(513), 0.0, 1.0, 0.1)[0] == 1
+    n = 700
+    A = rng.uniform(-1, 1, (n, n)) / n
+    B = rng.uniform(-1, 1, (n, 2))
+    x0 = rng.uniform(-1, 1, n)
+    st, x, steps = O.lti_euler_integrate(A, B, [0.5, -0.25], x0, 0.0, 0.025, 0.01)
+    assert st == 0 and steps == 3
+    xr = x0.copy()
+    for h in [0.01, 0.01, 0.025 - 0.01]:
+        xr = xr + (A @ xr + B @ np.array([0.5, -0.25])) * h
+    np.testing.assert_allclose(x, xr, rtol=1e-12, atol=1e-13)
+    assert O.lti_euler_integrate(np.zeros((0, 0)), np.zeros((0, 1)), [1.0], np.zeros(0), 0.0, 1.0, 0.1)[0] == 1
 
 
 def test_dcm_rollout_is_the_lti_step():
