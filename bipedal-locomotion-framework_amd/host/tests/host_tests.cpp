@@ -34,6 +34,7 @@
 #include <BipedalLocomotion/System/ForwardEuler.h>
 #include <BipedalLocomotion/System/LinearTimeInvariantSystem.h>
 #include <BipedalLocomotion/System/VariablesHandler.h>
+#include <blf/urdf.h>
 
 using namespace BipedalLocomotion;
 using namespace BipedalLocomotion::Planners;
@@ -1396,9 +1397,70 @@ static void testParametersHandler()
     REQUIRE(cfg->isEmpty());
 }
 
+// `blf_host_tests urdf <file> [frames] [considered] [base]` (comma-separated lists; "-" for none,
+// "*" for "every moving joint"): the C++ loader's model as JSON, for
+// tests/test_host_cpp.py::test_cpp_urdf_loader_matches_python.
+static std::vector<std::string> splitList(const std::string& s)
+{
+    std::vector<std::string> out;
+    if (s == "-" || s.empty()) return out;
+    std::size_t b = 0;
+    for (;;)
+    {
+        const std::size_t e = s.find(',', b);
+        out.push_back(s.substr(b, e == std::string::npos ? std::string::npos : e - b));
+        if (e == std::string::npos) return out;
+        b = e + 1;
+    }
+}
+
+static int dumpUrdf(int argc, char** argv)
+{
+    if (argc < 3) return 2;
+    blf::UrdfOptions opt;
+    if (argc > 3) opt.frames = splitList(argv[3]);
+    if (argc > 4 && std::string(argv[4]) != "*")
+    {
+        opt.hasConsideredJoints = true;
+        opt.consideredJoints = splitList(argv[4]);
+    }
+    if (argc > 5 && std::string(argv[5]) != "-") opt.base = argv[5];
+    blf::RobotModel m;
+    std::vector<std::string> names;
+    std::string err;
+    if (!blf::loadUrdf(argv[2], opt, m, &names, &err))
+    {
+        std::printf("{\"error\": \"%s\"}\n", err.c_str());
+        return 1;
+    }
+    auto arr = [](const char* key, const auto& v, bool last = false) {
+        std::printf("\"%s\": [", key);
+        for (std::size_t i = 0; i < v.size(); ++i)
+            std::printf(i ? ", %.17g" : "%.17g", static_cast<double>(v[i]));
+        std::printf(last ? "]" : "], ");
+    };
+    std::printf("{\"n\": %d, ", m.ndof);
+    std::printf("\"names\": [");
+    for (std::size_t i = 0; i < names.size(); ++i) std::printf(i ? ", \"%s\"" : "\"%s\"", names[i].c_str());
+    std::printf("], ");
+    arr("parent", m.parent);
+    arr("joint_origin", m.jointOrigin);
+    arr("joint_rot", m.jointRotation);
+    arr("joint_axis", m.jointAxis);
+    arr("joint_type", m.jointType);
+    arr("link_mass", m.linkMass);
+    arr("link_com", m.linkCom);
+    arr("link_inertia", m.linkInertia);
+    arr("frame_link", m.frameLink);
+    arr("frame_pose", m.framePose, true);
+    std::printf("}\n");
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     const std::string which = argc > 1 ? argv[1] : "all";
+    if (which == "urdf") return dumpUrdf(argc, argv);
     if (const char* g = std::getenv("BLF_GOLDEN_DIR")) g_golden = g;
     const bool cpu = which == "cpu" || which == "all";
     const bool gpu = which == "gpu" || which == "all";

@@ -161,3 +161,91 @@ def test_urdf_considered_joints_order():
     child_first.insert(child_first.index([nm for nm in left if nm != "l_knee"][0]), "l_knee")
     with pytest.raises(ValueError, match="before their parent"):
         urdf.load_urdf(to_urdf(MODEL), considered_joints=child_first)
+
+
+# ---- the C++ adapter's loader (host/src/UrdfLoader.cpp) against this one ------------------------
+import json
+import os
+import subprocess
+
+_PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bipedal-locomotion-framework_amd")
+_BIN = os.path.join(_PKG, "lib", "blf_host_tests")
+
+
+def _cpp_load(tmp_path, text, frames=(), considered=None, base=None):
+    if not os.path.exists(_BIN):
+        subprocess.check_call(["make", "-s", "-j8", "-C", _PKG])
+    path = tmp_path / "robot.urdf"
+    path.write_text(text)
+    args = [_BIN, "urdf", str(path), ",".join(frames) or "-",
+            "*" if considered is None else (",".join(considered) or "-"), base or "-"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=60)
+    out = json.loads(r.stdout)
+    assert (r.returncode == 0) == ("error" not in out), r.stdout + r.stderr
+    return out
+
+
+def _reversed_joints(text):
+    lines = text.split("\n")
+    joints = [ln for ln in lines if ln.lstrip().startswith("<joint")]
+    rest = [ln for ln in lines if not ln.lstrip().startswith("<joint") and ln != "</robot>"]
+    return "\n".join(rest + joints[::-1] + ["</robot>"])
+
+
+_ORDER = ([nm for nm in MODEL["names"][1:] if not nm.startswith(("l_", "r_"))]
+          + [nm for nm in MODEL["names"][1:] if nm.startswith("r_")]
+          + [nm for nm in MODEL["names"][1:] if nm.startswith("l_")])
+_CASES = {
+    "plain": (to_urdf(MODEL), {}),
+    "soles": (to_urdf(MODEL, soles=True), dict(frames=("l_sole", "r_sole"))),
+    "types": (to_urdf(MODEL, types={"neck_pitch": "continuous", "torso_roll": "prismatic"}), {}),
+    "locked": (to_urdf(MODEL, soles=True), dict(frames=("r_sole",), considered_joints=[
+        nm for nm in MODEL["names"][1:] if nm not in ("l_elbow", "r_elbow", "neck_pitch")])),
+    "order": (to_urdf(MODEL), dict(considered_joints=_ORDER)),
+    "document order": (_reversed_joints(to_urdf(MODEL)), {}),
+    "xml features": (to_urdf(MODEL).replace('<?xml version="1.0"?>', '<?xml version="1.0"?>\n<!DOCTYPE robot>\n'
+                                              '<!-- a comment with <tags> -->').replace(
+        '<robot name="humanoid24">', "<robot name='humanoid&amp;24'>\n<material name=\"grey\"><color rgba=\"0.5 0.5 0.5 1\"/></material>"), {}),
+}
+
+
+@pytest.mark.parametrize("case", list(_CASES))
+def test_cpp_urdf_loader_matches_python(tmp_path, case):
+    """blf::loadUrdf (the C++ adapter's setRobotModel input) gives the Python loader's model: the
+    same DoF names and order, parents, frames and types bit for bit, the floating-point arrays to
+    1e-15 (the 3 x 3 products may round differently)."""
+    text, kw = _CASES[case]
+    py = urdf.load_urdf(text, **kw)
+    cpp = _cpp_load(tmp_path, text, frames=kw.get("frames", ()), considered=kw.get("considered_joints"))
+    n = py["n"]
+    assert cpp["n"] == n and cpp["names"] == py["names"][1:]
+    np.testing.assert_array_equal(cpp["parent"], py["parent"])
+    np.testing.assert_array_equal(cpp["joint_type"], py.get("joint_type", np.zeros(n, dtype=np.int32)))
+    np.testing.assert_array_equal(cpp["frame_link"], py["frame_link"])
+    for k in ("joint_origin", "joint_rot", "joint_axis", "link_mass", "link_com", "link_inertia", "frame_pose"):
+        np.testing.assert_allclose(np.reshape(cpp[k], np.shape(py[k])), py[k], rtol=0, atol=1e-15, err_msg=k)
+
+
+@pytest.mark.parametrize("bad", [
+    '<joint name="x" type="floating"><parent link="base"/><child link="extra"/></joint><link name="extra"/>',
+    '<link name="orphan"/>',
+    '<joint name="y" type="revolute"><parent link="base"/><child link="l_hip_yaw_link"/></joint>',
+    '<link name="base"/>',
+    '<joint name="z" type="revolute"><parent link="base"/><child link="nowhere"/></joint>',
+    '<link name="bad"><inertial><mass value="-1"/></inertial></link><joint name="w" type="fixed">'
+    '<parent link="base"/><child link="bad"/></joint>',
+])
+def test_cpp_urdf_loader_refuses(tmp_path, bad):
+    """Both loaders refuse the same malformed models."""
+    text = to_urdf(MODEL, extra=bad)
+    with pytest.raises(ValueError):
+        urdf.load_urdf(text)
+    assert "error" in _cpp_load(tmp_path, text)
+    assert "error" in _cpp_load(tmp_path, to_urdf(MODEL), frames=("nope",))
+    assert "error" in _cpp_load(tmp_path, to_urdf(MODEL), considered=["no_such_joint"])
+    assert "error" in _cpp_load(tmp_path, "<robot><link name='a'></robot>")   # malformed XML
+    child_first = [nm for nm in _ORDER if nm != "l_knee"]
+    child_first.insert(child_first.index("l_hip_pitch") if "l_hip_pitch" in child_first else 0, "l_knee")
+    with pytest.raises(ValueError):
+        urdf.load_urdf(to_urdf(MODEL), considered_joints=child_first)
+    assert "before their parent" in _cpp_load(tmp_path, to_urdf(MODEL), considered=child_first)["error"]
