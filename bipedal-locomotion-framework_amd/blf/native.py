@@ -22,7 +22,7 @@ QP_SOLVED, QP_MAX_ITER, QP_NUMERICAL, QP_BAD_FACETS = 0, 1, 2, 3
 EXPORTED = ["blf_create", "blf_destroy", "blf_last_error", "blf_version", "blf_set_qp_launch_mode",
             "blf_step_schedule",
             "blf_lti_euler_integrate", "blf_lti_dynamics", "blf_dcm_euler_rollout", "blf_hull2d_hrep",
-            "blf_hull2d_contains", "blf_hull3d_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
+            "blf_hull2d_contains", "blf_hull3d_hrep", "blf_hullnd_hrep", "blf_halfspace_contains", "blf_quintic_fit", "blf_quintic_eval",
             "blf_dcm_mpc_default_params", "blf_dcm_mpc_solve", "blf_dcm_mpc_solve_warm",
             "blf_dcm_phase_expand", "blf_dcm_mpc_solve_phased",
             "blf_dcm_mpc_flops_per_iter",
@@ -154,6 +154,7 @@ def lib():
         L.blf_hull2d_hrep.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
         L.blf_hull2d_contains.argtypes = [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp]
         L.blf_hull3d_hrep.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
+        L.blf_hullnd_hrep.argtypes = [_vp, _i32, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
         L.blf_halfspace_contains.argtypes = [_vp, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp]
         L.blf_quintic_fit.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp]
         L.blf_quintic_eval.argtypes = [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _i32, _vp, _vp, _vp]
@@ -377,6 +378,22 @@ class Handle:
         _check(lib().blf_hull2d_hrep(
             self._h, _ptr(pts, torch.float64, (B, P, 2), "pts"), _ptr(npts, torch.int32, (B,), "npts"),
             P, max_facets, B, _ptr(A, torch.float64, (B, max_facets, 2), "A"),
+            _ptr(b, torch.float64, (B, max_facets), "b"), _ptr(nf, torch.int32, (B,), "nfacets"),
+            _stream(stream)))
+        return A, b, nf
+
+    def hullnd_hrep(self, pts, npts, max_facets=64, out=None, stream=None):
+        """blf_hullnd_hrep: pts [B, P, dim], npts [B] -> A [B, max_facets, dim], b, nfacets."""
+        torch = _torch()
+        B, P, D = pts.shape
+        if out is None:
+            out = (torch.empty((B, max_facets, D), dtype=torch.float64, device=pts.device),
+                   torch.empty((B, max_facets), dtype=torch.float64, device=pts.device),
+                   torch.empty((B,), dtype=torch.int32, device=pts.device))
+        A, b, nf = out
+        _check(lib().blf_hullnd_hrep(
+            self._h, D, _ptr(pts, torch.float64, (B, P, D), "pts"), _ptr(npts, torch.int32, (B,), "npts"),
+            P, max_facets, B, _ptr(A, torch.float64, (B, max_facets, D), "A"),
             _ptr(b, torch.float64, (B, max_facets), "b"), _ptr(nf, torch.int32, (B,), "nfacets"),
             _stream(stream)))
         return A, b, nf

@@ -261,6 +261,28 @@ blf_status blf_hull3d_hrep(blf_handle* handle, const double* pts, const int32_t*
                          (hipStream_t)stream);
 }
 
+blf_status blf_hullnd_hrep(blf_handle* handle, int32_t dim, const double* pts, const int32_t* npts,
+                           int32_t max_points, int32_t max_facets, int64_t batch, double* A,
+                           double* b, int32_t* nfacets, void* stream)
+{
+    BLF_REQUIRE(handle != nullptr, "blf_hullnd_hrep: null handle");
+    BLF_REQUIRE(dim >= 1 && dim <= BLF_HULLND_MAX_DIM, "blf_hullnd_hrep: dim %d outside [1, %d]", dim,
+                BLF_HULLND_MAX_DIM);
+    BLF_REQUIRE(max_points >= 1 && max_points <= BLF_HULLND_MAX_POINTS,
+                "blf_hullnd_hrep: max_points %d outside [1, %d]", max_points, BLF_HULLND_MAX_POINTS);
+    BLF_REQUIRE(max_facets >= 1 && max_facets <= BLF_HULLND_MAX_FACETS,
+                "blf_hullnd_hrep: max_facets %d outside [1, %d]", max_facets, BLF_HULLND_MAX_FACETS);
+    BLF_REQUIRE(batch >= 0, "blf_hullnd_hrep: negative batch");
+    BLF_REQUIRE(batch == 0 || (pts && npts && A && b && nfacets), "blf_hullnd_hrep: null buffer");
+    int64_t subsets = 1;   // C(max_points, dim)
+    for (int k = 1; k <= dim; ++k) subsets = subsets * (max_points - dim + k) / k;
+    if (subsets > BLF_HULLND_MAX_SUBSETS)
+        return set_error(BLF_ERR_UNSUPPORTED, "blf_hullnd_hrep: C(%d, %d) = %lld subsets above %d",
+                         max_points, dim, (long long)subsets, BLF_HULLND_MAX_SUBSETS);
+    return launch_hullnd(dim, pts, npts, max_points, max_facets, batch, A, b, nfacets,
+                         (hipStream_t)stream);
+}
+
 blf_status blf_halfspace_contains(blf_handle* handle, const double* A, const double* b,
                                   const int32_t* nfacets, int32_t dim, int32_t max_facets,
                                   const double* query, int64_t batch, int32_t* inside, void* stream)

@@ -60,6 +60,9 @@ blf_status launch_dcm_rollout(const double* xi0, const double* omega, const doub
                               hipStream_t s);
 blf_status launch_hull2d(const double* pts, const int32_t* npts, int32_t P, int32_t M,
                          int64_t batch, double* A, double* b, int32_t* nf, hipStream_t s);
+blf_status launch_hullnd(int32_t D, const double* pts, const int32_t* npts, int32_t P, int32_t M,
+                         int64_t batch, double* A, double* b, int32_t* nf, hipStream_t s);
+size_t hullnd_lds_bytes(int D, int P, int M);
 blf_status launch_hull3d(const double* pts, const int32_t* npts, int32_t P, int32_t M,
                          int64_t batch, double* A, double* b, int32_t* nf, hipStream_t s);
 blf_status launch_halfspace_contains(const double* A, const double* b, const int32_t* nf,

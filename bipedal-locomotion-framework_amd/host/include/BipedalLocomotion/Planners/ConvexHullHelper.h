@@ -3,13 +3,13 @@
  * Drop-in for src/Planners/include/BipedalLocomotion/Planners/ConvexHullHelper.h:32-81
  * (src/Planners/src/ConvexHullHelper.cpp:35-117).
  * buildConvexHull runs blf_hull2d_hrep on the device for 2 x p points (the planners' support
- * polygons) and blf_hull3d_hrep for 3 x p points (p <= 16; the reference's own test,
- * ConvexHullHelperTest.cpp:15-63, is 3-D); getA()/getB() return the H-representation A x <= b
- * (unit outward normals; 2-D: merged collinear facets, counter-clockwise; 3-D: one row per
- * distinct supporting plane, where Qhull "Qt" may give a split face twice — Qhull's facet order is
+ * polygons, p <= 16), blf_hull3d_hrep for 3 x p points (p <= 16; the reference's own test,
+ * ConvexHullHelperTest.cpp:15-63, is 3-D) and blf_hullnd_hrep for any other n x p (1 <= n <= 8,
+ * p <= 32); getA()/getB() return the H-representation A x <= b (unit outward normals; 2-D:
+ * merged collinear facets, counter-clockwise; otherwise one row per distinct supporting
+ * hyperplane, where Qhull "Qt" may give a split facet once per simplex — Qhull's facet order is
  * internal to Qhull, so only the SET of planes is comparable).  doesPointBelongToConvexHull runs
- * blf_hull2d_contains / blf_halfspace_contains (strict `>` rejects, no tolerance).  Other row
- * counts are rejected with false.  After a failed buildConvexHull (where Qhull would have thrown),
+ * blf_hull2d_contains / blf_halfspace_contains (strict `>` rejects, no tolerance).  After a failed buildConvexHull (where Qhull would have thrown),
  * doesPointBelongToConvexHull returns false for every point instead of testing an empty H-rep.
  */
 #ifndef BLF_BIPEDAL_LOCOMOTION_PLANNERS_CONVEX_HULL_HELPER_H
@@ -33,10 +33,10 @@ class ConvexHullHelper
     blf::DeviceBuffer<double> m_dPts, m_dA, m_dB, m_dQ;
     blf::DeviceBuffer<int32_t> m_dN, m_dInside;
     bool m_valid{false};   // the last buildConvexHull succeeded (a failed build rejects every point)
-    bool buildConvexHull3(const blf::MatrixXd& points);
+    bool buildConvexHullN(const blf::MatrixXd& points);
 
 public:
-    /** points: 2 x p or 3 x p (one point per column).  Any matrix type with rows(), cols(), (i, j). */
+    /** points: n x p (one point per column).  Any matrix type with rows(), cols(), (i, j). */
     template <class Mat> bool buildConvexHull(const Mat& points)
     {
         return buildConvexHull(blf::MatrixXd::from(points));

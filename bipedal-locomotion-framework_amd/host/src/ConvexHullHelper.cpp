@@ -8,49 +8,59 @@
 
 using namespace BipedalLocomotion::Planners;
 
-// 3 x p points: blf_hull3d_hrep (the distinct supporting planes; ConvexHullHelperTest.cpp:15-63).
-bool ConvexHullHelper::buildConvexHull3(const blf::MatrixXd& points)
+// 3 x p points (p <= 16): blf_hull3d_hrep (the distinct supporting planes;
+// ConvexHullHelperTest.cpp:15-63).  Any other n x p (n = 1 or n >= 4, or more points than the
+// 2-D / 3-D kernels take): blf_hullnd_hrep, the same rule in any dimension.
+bool ConvexHullHelper::buildConvexHullN(const blf::MatrixXd& points)
 {
-    const std::size_t p = points.cols();
-    if (p < 4 || p > BLF_HULL_MAX_POINTS)
+    const std::size_t p = points.cols(), dim = points.rows();
+    const bool three = dim == 3 && p <= BLF_HULL_MAX_POINTS;
+    if (dim < 1 || dim > BLF_HULLND_MAX_DIM)
     {
-        std::cerr << "[ConvexHullHelper::buildConvexHull] Between 4 and " << BLF_HULL_MAX_POINTS
-                  << " points are supported in 3-D." << std::endl;
+        std::cerr << "[ConvexHullHelper::buildConvexHull] Point sets of 1 to " << BLF_HULLND_MAX_DIM
+                  << " dimensions are supported." << std::endl;
+        return false;
+    }
+    if (p < dim + 1 || p > BLF_HULLND_MAX_POINTS)
+    {
+        std::cerr << "[ConvexHullHelper::buildConvexHull] Between " << dim + 1 << " and "
+                  << BLF_HULLND_MAX_POINTS << " points are supported in " << dim << "-D." << std::endl;
         return false;
     }
     blf_handle* h = blf::threadHandle();
     if (h == nullptr) return false;
-    std::vector<double> pts(3 * p);
+    std::vector<double> pts(dim * p);
     for (std::size_t j = 0; j < p; ++j)
-        for (std::size_t c = 0; c < 3; ++c) pts[3 * j + c] = points(c, j);
+        for (std::size_t c = 0; c < dim; ++c) pts[dim * j + c] = points(c, j);
     const int32_t n = static_cast<int32_t>(p);
-    const int32_t M = BLF_HULL3D_MAX_FACETS;
-    if (!m_dPts.upload(pts) || !m_dN.upload(&n, 1) || !m_dA.resize(3 * M) || !m_dB.resize(M) ||
+    const int32_t M = three ? BLF_HULL3D_MAX_FACETS : BLF_HULLND_MAX_FACETS;
+    if (!m_dPts.upload(pts) || !m_dN.upload(&n, 1) || !m_dA.resize(dim * M) || !m_dB.resize(M) ||
         !m_dInside.resize(1))
         return false;
-    if (!blf::report(blf_hull3d_hrep(h, m_dPts.data(), m_dN.data(), n, M, 1, m_dA.data(),
-                                     m_dB.data(), m_dInside.data(), nullptr),
-                     "ConvexHullHelper::buildConvexHull"))
-        return false;
+    const blf_status st = three ? blf_hull3d_hrep(h, m_dPts.data(), m_dN.data(), n, M, 1, m_dA.data(),
+                                                  m_dB.data(), m_dInside.data(), nullptr)
+                                : blf_hullnd_hrep(h, static_cast<int32_t>(dim), m_dPts.data(), m_dN.data(),
+                                                  n, M, 1, m_dA.data(), m_dB.data(), m_dInside.data(),
+                                                  nullptr);
+    if (!blf::report(st, "ConvexHullHelper::buildConvexHull")) return false;
     int32_t nf = -1;
-    std::vector<double> A(3 * M), b(M);
+    std::vector<double> A(dim * M), b(M);
     if (!m_dInside.download(&nf, 1) || !m_dA.download(A.data(), A.size()) ||
         !m_dB.download(b.data(), b.size()))
         return false;
     if (nf < 0)
     {
-        std::cerr << "[ConvexHullHelper::buildConvexHull] Degenerate point set (fewer than four "
-                     "points not in one plane)."
-                  << std::endl;
-        m_A.resize(0, 3);
+        std::cerr << "[ConvexHullHelper::buildConvexHull] Degenerate point set (fewer than "
+                  << dim + 1 << " points spanning " << dim << " dimensions)." << std::endl;
+        m_A.resize(0, dim);
         m_b.resize(0);
         return false;
     }
-    m_A.resize(static_cast<std::size_t>(nf), 3);
+    m_A.resize(static_cast<std::size_t>(nf), dim);
     m_b.resize(static_cast<std::size_t>(nf));
     for (int i = 0; i < nf; ++i)
     {
-        for (int c = 0; c < 3; ++c) m_A(i, c) = A[3 * i + c];
+        for (std::size_t c = 0; c < dim; ++c) m_A(i, c) = A[dim * i + c];
         m_b(i) = b[i];
     }
     return true;
@@ -59,19 +69,13 @@ bool ConvexHullHelper::buildConvexHull3(const blf::MatrixXd& points)
 bool ConvexHullHelper::buildConvexHull(const blf::MatrixXd& points)
 {
     m_valid = false;
-    if (points.rows() == 3) return m_valid = buildConvexHull3(points);
-    if (points.rows() != 2)
-    {
-        std::cerr << "[ConvexHullHelper::buildConvexHull] Only 2-D and 3-D point sets are "
-                     "supported by the device hull."
-                  << std::endl;
-        return false;
-    }
+    if (points.rows() != 2 || points.cols() > BLF_HULL_MAX_POINTS)
+        return m_valid = buildConvexHullN(points);
     const std::size_t p = points.cols();
-    if (p < 3 || p > BLF_HULL_MAX_POINTS)
+    if (p < 3)
     {
-        std::cerr << "[ConvexHullHelper::buildConvexHull] Between 3 and " << BLF_HULL_MAX_POINTS
-                  << " points are supported." << std::endl;
+        std::cerr << "[ConvexHullHelper::buildConvexHull] Between 3 and " << BLF_HULLND_MAX_POINTS
+                  << " points are supported in 2-D." << std::endl;
         return false;
     }
     blf_handle* h = blf::threadHandle();

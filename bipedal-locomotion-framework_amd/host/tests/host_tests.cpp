@@ -247,6 +247,50 @@ static void testIntegratorLTI()
     REQUIRE_FALSE(bad.integrate(0.0, 1.0));
 }
 
+// ---- ConvexHullHelper on n x p points (device, blf_hullnd_hrep) ---------------------------------
+static void testConvexHullN()
+{
+    ConvexHullHelper helper;
+    // the 4-D unit hypercube: 16 points, 8 facets x_c <= 1, -x_c <= 0
+    blf::MatrixXd cube(4, 16);
+    for (int j = 0; j < 16; ++j)
+        for (int c = 0; c < 4; ++c) cube(c, j) = (j >> c) & 1;
+    REQUIRE(helper.buildConvexHull(cube));
+    REQUIRE(helper.getA().rows() == 8 && helper.getA().cols() == 4);
+    int unitRows = 0;
+    for (std::size_t i = 0; i < helper.getA().rows(); ++i)
+    {
+        int nz = 0, which = -1;
+        for (int c = 0; c < 4; ++c)
+            if (std::abs(helper.getA()(i, c)) > 1e-12) ++nz, which = c;
+        const double a = helper.getA()(i, which);
+        unitRows += nz == 1 && std::abs(std::abs(a) - 1.0) < 1e-12
+                    && std::abs(helper.getB()(i) - (a > 0 ? 1.0 : 0.0)) < 1e-12;
+    }
+    REQUIRE(unitRows == 8);
+    REQUIRE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.5, 0.5, 0.5, 0.5}));
+    REQUIRE(helper.doesPointBelongToConvexHull(blf::VectorXd{1.0, 0.0, 1.0, 0.0}));
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.5, 0.5, 0.5, 1.01}));
+    // 1-D: an interval
+    blf::MatrixXd line(1, 3, {0.3, -0.2, 0.9});
+    REQUIRE(helper.buildConvexHull(line));
+    REQUIRE(helper.getA().rows() == 2);
+    REQUIRE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.0}));
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{1.0}));
+    // 2-D with more points than the polygon kernel takes (20 on a circle)
+    blf::MatrixXd ring(2, 20);
+    for (int j = 0; j < 20; ++j) ring(0, j) = std::cos(0.1 * M_PI * j), ring(1, j) = std::sin(0.1 * M_PI * j);
+    REQUIRE(helper.buildConvexHull(ring));
+    REQUIRE(helper.getA().rows() == 20);
+    // a flat 4-D set, too few points, too many dimensions
+    blf::MatrixXd flat = cube;
+    for (int j = 0; j < 16; ++j) flat(3, j) = 0.5;
+    REQUIRE_FALSE(helper.buildConvexHull(flat));
+    REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.5, 0.5, 0.5, 0.5}));
+    REQUIRE_FALSE(helper.buildConvexHull(blf::MatrixXd(4, 4)));
+    REQUIRE_FALSE(helper.buildConvexHull(blf::MatrixXd(9, 12)));
+}
+
 // ---- ForwardEuler over a host-side DynamicalSystem subclass (ForwardEuler.tpp:18-49) ----------
 // The reference's IntegratorTest system written as a user's CPU system: dx = A x + B u with the
 // device kernel's summation order, so its trajectory is bit for bit blf_lti_euler_integrate's.
@@ -1476,6 +1520,7 @@ int main(int argc, char** argv)
         {"Integrator - LTI of any size", true, testIntegratorLTIAnySize},
         {"Convex Hull helper (2-D)", true, testConvexHull},
         {"Convex Hull helper (3-D, ConvexHullHelperTest.cpp)", true, testConvexHull3},
+        {"Convex Hull helper (n-D)", true, testConvexHullN},
         {"QuinticSpline", true, testQuinticSpline},
         {"TimeVaryingDCMPlanner advance", true, testPlanner},
         {"TimeVaryingDCMPlanner three contacts", true, testPlannerThreeContacts},

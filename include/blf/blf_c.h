@@ -18,6 +18,7 @@
  *                             A = omega_k I, B = -omega_k I (LinearTimeInvariantSystem.cpp:13-38, :71)
  *   blf_hull2d_hrep           Planners/src/ConvexHullHelper.cpp:35-99 (buildConvexHull/getA/getB)
  *   blf_hull2d_contains       Planners/src/ConvexHullHelper.cpp:101-117 (doesPointBelongToConvexHull)
+ *   blf_hullnd_hrep           ConvexHullHelper.cpp:35-99 on n x p points, any n
  *   blf_hull3d_hrep           ConvexHullHelper.cpp:35-99 on 3 x p points (Planners/tests/
  *                             ConvexHullHelperTest.cpp:15-63 is 3-D)
  *   blf_halfspace_contains    ConvexHullHelper.cpp:101-117 in any dimension
@@ -165,6 +166,23 @@ blf_status blf_hull2d_contains(blf_handle* handle, const double* A, const double
 blf_status blf_hull3d_hrep(blf_handle* handle, const double* pts, const int32_t* npts,
                            int32_t max_points, int32_t max_facets, int64_t batch,
                            double* A, double* b, int32_t* nfacets, void* stream);
+
+/* n-D H-representation (ConvexHullHelper on n x p points, any n: ConvexHullHelper.cpp:35-99 hands
+ * the matrix to Qhull).  pts: [B][P][dim] (1 <= dim <= BLF_HULLND_MAX_DIM, P <=
+ * BLF_HULLND_MAX_POINTS, C(P, dim) <= BLF_HULLND_MAX_SUBSETS), npts: [B].  Output padded to
+ * max_facets rows (<= BLF_HULLND_MAX_FACETS): A: [B][max_facets][dim] unit outward normals,
+ * b: [B][max_facets] (inside: A x <= b), nfacets: [B].  The rows are the distinct supporting
+ * hyperplanes through dim of the points (a facet Qhull "Qt" splits into simplices is one row;
+ * compare as sets), b = the largest n . p over the points; dim = 1: the rows +1 / -1.
+ * nfacets = -1 for fewer than dim + 1 points, a set spanning fewer than dim dimensions, or more
+ * than max_facets planes.  One wavefront per set.  Rule and order: oracle orc_hullnd_hrep. */
+#define BLF_HULLND_MAX_DIM 8
+#define BLF_HULLND_MAX_POINTS 32
+#define BLF_HULLND_MAX_FACETS 1024
+#define BLF_HULLND_MAX_SUBSETS (1 << 20)
+blf_status blf_hullnd_hrep(blf_handle* handle, int32_t dim, const double* pts, const int32_t* npts,
+                           int32_t max_points, int32_t max_facets, int64_t batch, double* A,
+                           double* b, int32_t* nfacets, void* stream);
 
 /* doesPointBelongToConvexHull in `dim` dimensions: A: [B][max_facets][dim], b: [B][max_facets],
  * query: [B][dim]; inside[q] = 1 iff no row i < nfacets has (A p)_i > b_i (sum in column order

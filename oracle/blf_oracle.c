@@ -340,6 +340,139 @@ int orc_hull3d_hrep(const double* pts, int npts, int max_facets, double* A, doub
     return count;
 }
 
+/* ConvexHullHelper::buildConvexHull on dim x p points, any dim (ConvexHullHelper.cpp:35-99; the
+ * reference hands the n x p matrix to Qhull).  Every dim-subset of the points in lexicographic
+ * order spans a candidate hyperplane; its normal is the null vector of the (dim-1) x dim matrix of
+ * differences p_j - p_i0 (Gaussian elimination with full pivoting, first maximum in row-major
+ * order, then back substitution with the last permuted column free), normalised; a plane with
+ * every point on one side (tolerance tol) is a supporting plane, oriented outward, with b = the
+ * largest n . p over the points; planes equal to a stored one (1e-9 on the normal, btol on b) are
+ * dropped -- the rule of orc_hull3d_hrep in any dimension.  dim = 1: the rows +1 / -1 at the
+ * largest / smallest coordinate.  Returns the row count, or -1 for fewer than dim + 1 points, a
+ * set that spans less than dim dimensions, more than max_facets planes, or dim outside
+ * [1, ORC_HULLND_MAX_DIM]. */
+#define ORC_HULLND_MAX_DIM 8
+static int64_t orc_binom(int a, int b)
+{
+    if (b < 0 || a < b) return 0;
+    int64_t r = 1;
+    for (int k = 1; k <= b; ++k) r = r * (a - b + k) / k;
+    return r;
+}
+
+int orc_hullnd_hrep(int dim, const double* pts, int npts, int max_facets, double* A, double* b)
+{
+    for (int e = 0; e < dim * max_facets; ++e) A[e] = 0.0;
+    for (int e = 0; e < max_facets; ++e) b[e] = 0.0;
+    if (dim < 1 || dim > ORC_HULLND_MAX_DIM || npts < dim + 1) return -1;
+    double scale = 0.0;
+    for (int e = 0; e < dim * npts; ++e) {
+        const double a = fabs(pts[e]);
+        if (a > scale) scale = a;
+    }
+    const double tol = 1e-12 * (1.0 + scale);
+    const double btol = 1e-9 * (1.0 + scale);
+    if (dim == 1) {
+        double mn = pts[0], mx = pts[0];
+        for (int l = 1; l < npts; ++l) {
+            if (pts[l] < mn) mn = pts[l];
+            if (pts[l] > mx) mx = pts[l];
+        }
+        if (!(mx - mn > tol) || max_facets < 2) return -1;
+        A[0] = 1.0, b[0] = mx, A[1] = -1.0, b[1] = -mn;
+        return 2;
+    }
+    const int R = dim - 1;
+    int idx[ORC_HULLND_MAX_DIM];
+    for (int i = 0; i < dim; ++i) idx[i] = i;
+    const int64_t total = orc_binom(npts, dim);
+    int count = 0, overflow = 0;
+    for (int64_t t = 0; t < total; ++t) {
+        if (t > 0) {   /* next combination in lexicographic order */
+            int i = dim - 1;
+            while (idx[i] == npts - dim + i) --i;
+            ++idx[i];
+            for (int k = i + 1; k < dim; ++k) idx[k] = idx[k - 1] + 1;
+        }
+        const double* p0 = pts + (int64_t)idx[0] * dim;
+        double W[ORC_HULLND_MAX_DIM - 1][ORC_HULLND_MAX_DIM];
+        int perm[ORC_HULLND_MAX_DIM];
+        for (int r = 0; r < R; ++r)
+            for (int c = 0; c < dim; ++c) W[r][c] = pts[(int64_t)idx[r + 1] * dim + c] - p0[c];
+        for (int c = 0; c < dim; ++c) perm[c] = c;
+        int ok = 1;
+        for (int k = 0; k < R && ok; ++k) {
+            double best = -1.0;
+            int pr = k, pc = k;
+            for (int r = k; r < R; ++r)
+                for (int c = k; c < dim; ++c) {
+                    const double a = fabs(W[r][c]);
+                    if (a > best) best = a, pr = r, pc = c;
+                }
+            if (!(best > tol)) { ok = 0; break; }
+            for (int c = 0; c < dim; ++c) { const double x = W[k][c]; W[k][c] = W[pr][c]; W[pr][c] = x; }
+            for (int r = 0; r < R; ++r) { const double x = W[r][k]; W[r][k] = W[r][pc]; W[r][pc] = x; }
+            { const int x = perm[k]; perm[k] = perm[pc]; perm[pc] = x; }
+            for (int r = k + 1; r < R; ++r) {
+                const double f = W[r][k] / W[k][k];
+                for (int c = k + 1; c < dim; ++c) W[r][c] = W[r][c] - f * W[k][c];
+            }
+        }
+        if (!ok) continue;
+        double x[ORC_HULLND_MAX_DIM], nrm[ORC_HULLND_MAX_DIM];
+        x[dim - 1] = 1.0;
+        for (int k = R - 1; k >= 0; --k) {
+            double sum = W[k][dim - 1];
+            for (int c = k + 1; c < R; ++c) sum = sum + W[k][c] * x[c];
+            x[k] = -sum / W[k][k];
+        }
+        for (int c = 0; c < dim; ++c) nrm[perm[c]] = x[c];
+        double len = nrm[0] * nrm[0];
+        for (int c = 1; c < dim; ++c) len = len + nrm[c] * nrm[c];
+        len = sqrt(len);
+        if (!(len > 0.0)) continue;
+        for (int c = 0; c < dim; ++c) nrm[c] = nrm[c] / len;
+        int pos = 0, neg = 0;
+        for (int l = 0; l < npts; ++l) {
+            const double* q = pts + (int64_t)l * dim;
+            double d = nrm[0] * (q[0] - p0[0]);
+            for (int c = 1; c < dim; ++c) d = d + nrm[c] * (q[c] - p0[c]);
+            if (d > tol) pos = 1;
+            if (d < -tol) neg = 1;
+        }
+        if ((pos && neg) || !(pos || neg)) continue;
+        if (pos)
+            for (int c = 0; c < dim; ++c) nrm[c] = -nrm[c];
+        double bm = -INFINITY;
+        for (int l = 0; l < npts; ++l) {
+            const double* q = pts + (int64_t)l * dim;
+            double v = nrm[0] * q[0];
+            for (int c = 1; c < dim; ++c) v = v + nrm[c] * q[c];
+            if (v > bm) bm = v;
+        }
+        int dup = 0;
+        for (int e = 0; e < count && e < max_facets && !dup; ++e) {
+            int same = fabs(b[e] - bm) <= btol;
+            for (int c = 0; c < dim; ++c) same = same && fabs(A[e * dim + c] - nrm[c]) <= 1e-9;
+            dup = same;
+        }
+        if (dup) continue;
+        if (count < max_facets) {
+            for (int c = 0; c < dim; ++c) A[count * dim + c] = nrm[c];
+            b[count] = bm;
+        } else {
+            overflow = 1;
+        }
+        ++count;
+    }
+    if (overflow || count < dim + 1) {
+        for (int e = 0; e < dim * max_facets; ++e) A[e] = 0.0;
+        for (int e = 0; e < max_facets; ++e) b[e] = 0.0;
+        return -1;
+    }
+    return count;
+}
+
 /* doesPointBelongToConvexHull in any dimension (ConvexHullHelper.cpp:101-117): strict `>` rejects. */
 int orc_halfspace_contains(const double* A, const double* b, int nfacets, int dim, const double* p)
 {

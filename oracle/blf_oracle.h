@@ -24,6 +24,7 @@
  *   orc_hull3d_hrep          ConvexHullHelper.cpp:35-99 on 3 x p points (the reference test's case,
  *                            ConvexHullHelperTest.cpp:15-63); checked as plane sets against scipy's
  *                            Qhull (tests/golden/hull3d.json)
+ *   orc_hullnd_hrep          ConvexHullHelper.cpp:35-99 on n x p points, any n (dim-subset planes)
  *   orc_halfspace_contains   ConvexHullHelper.cpp:101-117 in any dimension
  *   orc_quintic_*            ABSENT in the reference: parity unpinned against the
  *                            reference; pinned by boundary-condition identities + sympy fixtures
@@ -72,6 +73,7 @@ void orc_hull2d_force_andrew(int on);
 int orc_hull2d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);
 int orc_hull2d_contains(const double* A, const double* b, int nfacets, const double* p);
 int orc_hull3d_hrep(const double* pts, int npts, int max_facets, double* A, double* b);
+int orc_hullnd_hrep(int dim, const double* pts, int npts, int max_facets, double* A, double* b);
 int orc_halfspace_contains(const double* A, const double* b, int nfacets, int dim, const double* p);
 
 void orc_quintic_fit(const double* knots_t, const double* knots_pva, int nknots, int dim,

@@ -60,6 +60,7 @@ def lib():
         L.orc_hull2d_hrep.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.orc_hull3d_hrep.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.orc_halfspace_contains.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_hullnd_hrep.argtypes = [ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.orc_hull2d_contains.restype = ctypes.c_int
         L.orc_hull2d_contains.argtypes = [_dp, _dp, ctypes.c_int, _dp]
         L.orc_quintic_fit.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, _dp]
@@ -187,6 +188,16 @@ def hull3d_hrep(pts, max_facets=64):
     A = np.zeros((max_facets, 3))
     b = np.zeros(max_facets)
     m = lib().orc_hull3d_hrep(_d(pts), pts.shape[0], max_facets, _d(A), _d(b))
+    return A, b, m
+
+
+def hullnd_hrep(pts, max_facets=64):
+    """orc_hullnd_hrep: pts [p, dim] -> (A [max_facets, dim], b [max_facets], nfacets or -1)."""
+    pts = _f64(pts)
+    p, dim = pts.shape
+    A = np.zeros((max_facets, dim))
+    b = np.zeros(max_facets)
+    m = lib().orc_hullnd_hrep(dim, _d(pts), p, max_facets, _d(A), _d(b))
     return A, b, m
 
 
