@@ -75,11 +75,10 @@ __global__ __launch_bounds__(64) void hullnd_kernel(const double* __restrict__ p
             int x = 0;
 #pragma unroll
             for (int i = 0; i < D; ++i) {
-                for (;;) {
+                for (; x < n - 1; ++x) {   // bounded: every wave leaves the loop
                     const int64_t c = hull_binom(n - x - 1, D - i - 1);
                     if (rr < c) break;
                     rr -= c;
-                    ++x;
                 }
                 idx[i] = x++;
             }
@@ -275,18 +274,26 @@ blf_status launch_hullnd(int32_t D, const double* pts, const int32_t* npts, int3
     if (batch > 0x7fffffffLL)
         return set_error(BLF_ERR_UNSUPPORTED, "hullnd: %lld point sets too many", (long long)batch);
     const size_t lds = hullnd_lds_bytes(D, P, M);
+    using Kern = void (*)(const double*, const int32_t*, int32_t, int32_t, double*, double*, int32_t*);
+    Kern kern = nullptr;
     switch (D) {
-#define BLF_HULLND_CASE(d)                                                                          \
-    case d:                                                                                         \
-        hipLaunchKernelGGL(hullnd_kernel<d>, dim3((unsigned)batch), dim3(64), lds, s, pts, npts, P, \
-                           M, A, b, nf);                                                            \
-        break;
-        BLF_HULLND_CASE(2) BLF_HULLND_CASE(3) BLF_HULLND_CASE(4) BLF_HULLND_CASE(5)
-        BLF_HULLND_CASE(6) BLF_HULLND_CASE(7) BLF_HULLND_CASE(8)
-#undef BLF_HULLND_CASE
+    case 2: kern = hullnd_kernel<2>; break;
+    case 3: kern = hullnd_kernel<3>; break;
+    case 4: kern = hullnd_kernel<4>; break;
+    case 5: kern = hullnd_kernel<5>; break;
+    case 6: kern = hullnd_kernel<6>; break;
+    case 7: kern = hullnd_kernel<7>; break;
+    case 8: kern = hullnd_kernel<8>; break;
     default:
         return set_error(BLF_ERR_INVALID_ARGUMENT, "hullnd: dim %d outside [1, %d]", D, BLF_HULLND_MAX_DIM);
     }
+    if (lds > 65536) {   // above the default dynamic LDS limit (up to 80 KB at P = 32, M = 1024, D = 8)
+        const blf_status st = check_hip(
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            "hullnd_kernel LDS attribute");
+        if (st != BLF_OK) return st;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(64), lds, s, pts, npts, P, M, A, b, nf);
     return check_hip(hipGetLastError(), "hullnd_kernel launch");
 }
 
