@@ -90,7 +90,7 @@ def test_gpu_hullnd_bitwise(handle, dim):
 @pytest.mark.gpu
 def test_gpu_hullnd_matches_qhull_and_contains(handle):
     """Every golden set through the device, as sets of planes against Qhull; the points pass
-    blf_halfspace_contains, points pushed outside fail."""
+    blf_halfspace_contains, a point pushed past each facet fails."""
     import torch
     for g in _golden():
         P = np.asarray(g["points"])
@@ -100,8 +100,8 @@ def test_gpu_hullnd_matches_qhull_and_contains(handle):
                                       torch.tensor([len(P)], dtype=torch.int32).cuda(), max_facets=1024)
         A, b, m = A.cpu().numpy()[0], b.cpu().numpy()[0], int(nf[0])
         assert _same_planes(A, b, m, g["planes"]), g["name"]
-        c = P.mean(axis=0)
-        q = np.concatenate([P, c + 3.0 * (P - c)])
+        out = np.array([P[np.argmax(P @ A[i])] + 0.1 * A[i] for i in range(m)])   # past facet i
+        q = np.concatenate([P, out])
         inside = handle.halfspace_contains(torch.from_numpy(np.repeat(A[None], len(q), 0)).cuda(),
                                            torch.from_numpy(np.repeat(b[None], len(q), 0)).cuda(),
                                            torch.full((len(q),), m, dtype=torch.int32).cuda(),
