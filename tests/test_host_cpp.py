@@ -28,7 +28,8 @@ def _run(which):
 
 def test_host_bookkeeping_tests():
     out = _run("cpu")
-    for name in ("ContactList", "ContactPhaseList", "VariablesHandler", "ParametersHandler"):
+    for name in ("ContactList", "ContactPhaseList", "VariablesHandler", "ParametersHandler",
+                 "Integrator - host-side system"):
         assert any(line.startswith(name) and line.rstrip().endswith("ok") for line in out.splitlines())
 
 
@@ -38,5 +39,7 @@ def test_host_device_tests():
     for name in ("Integrator - Linear system", "Convex Hull helper (2-D)",
                  "Convex Hull helper (3-D, ConvexHullHelperTest.cpp)", "QuinticSpline",
                  "TimeVaryingDCMPlanner advance", "Continuous Contact",
-                 "FloatingBaseSystemKinematics", "FloatingBaseDynamicalSystem"):
+                 "FloatingBaseSystemKinematics", "FloatingBaseDynamicalSystem",
+                 "Integrator - host-side system == device LTI", "Integrator - LTI of any size",
+                 "Convex Hull helper (n-D)"):
         assert any(line.startswith(name) and line.rstrip().endswith("ok") for line in out.splitlines()), out
