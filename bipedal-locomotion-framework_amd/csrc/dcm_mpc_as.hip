@@ -1139,7 +1139,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
                                                  double xi00, double xi01, double* xi_out, double* vrp_out,
                                                  int32_t* status_out, int32_t* iters_out, int32_t* polished_out,
                                                  double* lam_out, int32_t* list, int list_slot,
-                                                 int32_t* passes_out, int npass)
+                                                 int32_t* passes_out, int npass, int pend = kPending)
 {
     const bool done = certified || status != 0;
 #pragma unroll
@@ -1165,7 +1165,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
     if (lane == 0) {
         xi_out[2 * p * (N + 1)] = xi00;
         xi_out[2 * p * (N + 1) + 1] = xi01;
-        status_out[p] = done ? status : kPending;
+        status_out[p] = done ? status : pend;
         if (passes_out) passes_out[p] = npass;
         if (done) {
             iters_out[p] = 0;
@@ -1193,7 +1193,7 @@ __device__ __forceinline__ void cold_solve(
     const double* __restrict__ Ain, const double* __restrict__ bin,
     const int32_t* __restrict__ nfacets, double* __restrict__ xi_out, double* __restrict__ vrp_out,
     int32_t* __restrict__ status_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out,
-    double* __restrict__ lam_out, const PhaseSrc& ps)
+    double* __restrict__ lam_out, const PhaseSrc& ps, int pend = kPending)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = P.N, M = P.M;
@@ -1380,7 +1380,7 @@ __device__ __forceinline__ void cold_solve(
     AS_STAMP_ADD(14, t_b);
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
                                   status_out, iters_out, polished_out, lam_out, P.list, P.list_slot,
-                                  P.passes_out, npass);
+                                  P.passes_out, npass, pend);
     if (PH && !certified && status == 0) ph_write_window<KPL>(ps, sPh, omega, A2d, Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(0, t_start);
 #ifdef BLF_STAMPS
@@ -1431,6 +1431,9 @@ __global__ __launch_bounds__(kWave, BLF_AS_MINWAVES) void dcm_mpc_cold_fused_ker
                                     lam_out);
 }
 
+#ifndef BLF_WARM_RETRY
+#define BLF_WARM_RETRY 1
+#endif
 // ---- the warm-start kernel ("Warm start") ----
 // One wavefront per QP, fp64 facet rows in LDS.  From the shifted previous solution (xi rolled
 // out from its VRPs), guess = the facets the rollout violates plus those whose previous multiplier
@@ -1447,14 +1450,12 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     PhaseSrc ps)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int N = P.N, M = P.M;
     // a problem whose previous solve failed (prev_status != 0) is not warm-started from it: it is
     // solved exactly as a cold launch solves it (the IPM's stage 2 treats it as cold too)
-    if (P.ws_status != nullptr && P.ws_status[blockIdx.x] != 0) {
-        cold_solve<KPL, LAMOUT, PH, TR, MF>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
-                                             status_out, iters_out, polished_out, lam_out, ps);
-        return;
-    }
+    int pend = kPending;
+    if (P.ws_status != nullptr && P.ws_status[blockIdx.x] != 0) goto cold;
+    {
+    const int N = P.N, M = P.M;
     assume_pad<KPL, TR>(N);
     const int NH = (N + KPL - 1) / KPL;   // lanes holding knots
     const int S = KPL * NH;               // LDS row stride: facet i of slot j, lane l at i S + j NH + l
@@ -1591,6 +1592,15 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
         certified = as_passes<KPL, TR, double>(K, Pd, R, NH, N, lane, xi00, xi01, pk, pl, 10, 4, -1, npass);
         AS_STAMP_ADD(14, t_b);
     }
+#if BLF_WARM_RETRY
+    // the warm passes did not certify: the QP is solved again from a cold start (fp32 search,
+    // fp64 passes), and if that hands it over, stage 2 starts it cold (kPendingCold)
+    if (!certified && status == 0) {
+        pend = kPendingCold;
+        __syncthreads();   // the LDS is the cold solve's
+        goto cold;
+    }
+#endif
     AS_STAMP(t_out);
 
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
@@ -1608,6 +1618,11 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
         g_as_timeline[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
     }
 #endif
+    return;
+    }
+cold:
+    cold_solve<KPL, LAMOUT, PH, TR, MF>(P, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, xi_out, vrp_out,
+                                         status_out, iters_out, polished_out, lam_out, ps, pend);
 }
 
 // Batches up to this size take the fused kernel (N <= 64, cold, per-knot input): they fill at

@@ -812,12 +812,14 @@ __device__ __forceinline__ void ipm_solve(
     const bool own = k < N;
     const bool last = k == N - 1;
     // after the active-set kernel (dcm_mpc_as.hip): only the QPs it handed over
-    if (P.stage2 && status_out[p] != kPending) return;
+    const int st0 = P.stage2 ? status_out[p] : 0;
+    if (P.stage2 && st0 != kPending && st0 != kPendingCold) return;
     // solved here alone (no active-set kernel before): no active-set kernel passes
     if (!P.stage2 && P.passes_out != nullptr && threadIdx.x == 0) P.passes_out[p] = 0;
     // a separate instantiation each way; in the warm one, a problem whose previous solve failed
     // (KParams::ws_status) starts cold, as the cold instantiation would start it
-    const bool warm = WARM && !(P.ws_status != nullptr && P.ws_status[p] != 0);
+    // (and one the warm kernel re-solved cold and still handed over, kPendingCold)
+    const bool warm = WARM && !(P.ws_status != nullptr && P.ws_status[p] != 0) && st0 != kPendingCold;
     const bool ws = warm && k + P.ws_shift < N;           // this knot starts from the warm start
     STAMP(t_start);
 

@@ -10,6 +10,7 @@ namespace qp {
 
 constexpr int kGuessPasses = 8;   // active-set start: drop/add passes (oracle: ORC_GUESS_PASSES)
 constexpr int kPending = -1;      // status of a QP the active-set kernel hands to the IPM kernel
+constexpr int kPendingCold = -2;  // handed over by the warm kernel after its cold re-solve: stage 2 starts cold
 
 struct KParams {
     int N, M, max_iter;

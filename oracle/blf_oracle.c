@@ -1987,6 +1987,9 @@ int orc_dcm_mpc_solve(const orc_dcm_params* prm, const double* xi_init, const do
                                   xi, vrp, NULL, iters_out, NULL, NULL);
 }
 
+#ifndef ORC_WARM_RETRY
+#define ORC_WARM_RETRY 1   /* BLF_WARM_RETRY */
+#endif
 int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, const double* omega,
                            const double* xi_ref, const double* vrp_ref, const double* Ain,
                            const double* bin, const int32_t* nfacets, const orc_dcm_warm* warm,
@@ -2156,6 +2159,14 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
         if (as_kernel) as_passes = w->npass;   /* the warm kernel's passes */
         free(gm);
         if (okg) { polished = 1; status = 0; it = 0; goto done; }
+        if (ORC_WARM_RETRY && warm && as_kernel) {
+            /* the warm kernel's cold re-solve (csrc/dcm_mpc_as.hip, BLF_WARM_RETRY): a QP its warm
+             * passes do not certify is solved again from a cold start (fp32 search, fp64 passes),
+             * and the interior point method, if it still needs it, starts cold (kPendingCold) */
+            free(mem);
+            return orc_dcm_mpc_solve_warm(prm, xi_init, omega, xi_ref, vrp_ref, Ain, bin, nfacets, NULL, xi,
+                                          vrp, lam_out, iters_out, polished_out, passes_out);
+        }
     }
     /* the interior point method's own start (only when the active-set start did not certify):
      * the start point was restored exactly */
