@@ -269,7 +269,10 @@ typedef struct blf_dcm_mpc_solution {
  * previous status is not BLF_QP_OK (e.g. BLF_QP_MAX_ITER) is not warm-started from that iterate:
  * it is solved exactly as the cold start (warm == NULL) solves it, so one failed window does not
  * poison the next (Advanceable::advance, System/include/BipedalLocomotion/System/Advanceable.h:24-46,
- * is called again after a failure with the planner's previous state).                           */
+ * is called again after a failure with the planner's previous state).  A warm-started problem
+ * (horizon <= 128, the active-set kernels' range) whose warm passes do not certify is solved
+ * again from the cold start as well, the interior point method included (round 5; oracle
+ * orc_dcm_mpc_solve_warm, ORC_WARM_RETRY): the same result as a cold solve of it.               */
 typedef struct blf_dcm_mpc_warm_start {
     const double* vrp;       /* [B][N][2]  VRPs of the previous solve (must not alias the output) */
     const double* lambda;    /* [B][N][M]  its multipliers (blf_dcm_mpc_solve_warm's lambda_out)  */
