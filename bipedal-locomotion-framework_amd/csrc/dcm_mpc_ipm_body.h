@@ -367,7 +367,7 @@ __device__ __forceinline__ void residuals(KN& K, bool facets, const KParams& P, 
         const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
         for (int i = 0; i < KN::kMF; ++i) {
-            if (i >= mm) break;
+            if (KN::kMF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
             if (i < km) {
                 const double2 a = A2[i * N + kx];
                 const double gr = FD2(a.x, K.r0, a.y, K.r1);
@@ -952,7 +952,7 @@ __device__ __forceinline__ void ipm_solve(
             double al0 = 0.0, al1 = 0.0;   // A^T lam
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
-                if (i >= mmax) break;
+                if (MF <= kMaxFacets && i >= mmax) break;
                 if (i < K.m) {
                     const double2 a = L.A2[i * N + k];
                     const double gr = FD2(a.x, K.r0, a.y, K.r1);
@@ -1056,13 +1056,13 @@ __device__ __forceinline__ void ipm_solve(
                     if (!guess) {
 #pragma unroll
                         for (int i = 0; i < MF; ++i) {
-                            if (i >= mm) break;
+                            if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                             if (i < km) lmx = keepmax(lmx, K.lam[i]);
                         }
                     }
 #pragma unroll
                     for (int i = 0; i < MF; ++i) {
-                        if (i >= mm) break;
+                        if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                         const bool base = guess ? ((gk >> i) & 1) != 0
                                                 : (K.lam[i] > K.s[i] && K.lam[i] >= kLamRel * lmx);
                         if (i < km && ((base && !((dm >> i) & 1)) || ((am >> i) & 1))) {
@@ -1245,7 +1245,7 @@ __device__ __forceinline__ void ipm_solve(
                         const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                         for (int i = 0; i < MF; ++i) {
-                            if (i >= mm) break;
+                            if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                             if (i < km) {
                                 const double2 a = L.A2[i * N + kx];
                                 const double vi = FD2(a.x, K.r0, a.y, K.r1) - L.BI[i * N + kx].x;
@@ -1319,7 +1319,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < MF; ++i) {
-                    if (i >= mm) break;
+                    if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
                         const double is = 1.0 / K.s[i];
@@ -1340,7 +1340,7 @@ __device__ __forceinline__ void ipm_solve(
                 // kept in an 8-entry register array across the pair loop (which spilled)
 #pragma unroll
                 for (int i = 1; i < MF; ++i) {
-                    if (i >= mm) break;
+                    if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                     if (i < km) {
                         const int ki = opaque(k);
                         const double2 ai = L.A2[i * N + ki];
@@ -1373,7 +1373,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < MF; ++i) {
-                    if (i >= mm) break;
+                    if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                     if (i < km) {
                         double ds, dl;
                         const double is = L.BI[i * N + kx].y;
@@ -1408,7 +1408,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < MF; ++i) {
-                    if (i >= mm) break;
+                    if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
                         const double bi = L.BI[i * N + kx].x;
@@ -1434,7 +1434,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < MF; ++i) {
-                    if (i >= mm) break;
+                    if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                     if (i < km) {
                         const double2 a = L.A2[i * N + kx];
                         const double bi = L.BI[i * N + kx].x;
@@ -1460,7 +1460,7 @@ __device__ __forceinline__ void ipm_solve(
                 const int km = opaque(K.m), mm = opaque_s(mmax);
 #pragma unroll
                 for (int i = 0; i < MF; ++i) {
-                    if (i >= mm) break;
+                    if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
                     if (i < km) {
                         const double2 fa = L.A2[i * N + kx];
                         const double ds = (-facet_rp(K, fa, L.BI[i * N + kx].x, i)) - FD2(fa.x, dr0, fa.y, dr1);
@@ -1500,7 +1500,11 @@ __device__ __forceinline__ void ipm_solve(
             double* lo = lam_out + st * M;
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
-                if (i >= M) break;
+                if constexpr (MF <= kMaxFacets) {
+                    if (i >= M) break;
+                } else {
+                    if (i >= M) continue;
+                }
                 lo[i] = i < K.m ? K.lam[i] : 0.0;
             }
         }
