@@ -53,6 +53,12 @@ Handle::~Handle()
 
 blf_status Handle::stage2_list(hipStream_t s, int64_t batch, Stage2List* out)
 {
+    // the list's slot toggles on the host between solves and may need a stream synchronisation to
+    // grow: a captured graph would freeze one toggle and fail the synchronisation, so a solve under
+    // stream capture is refused (the solve itself is capture-safe; its bookkeeping is not)
+    hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap_st) == hipSuccess && cap_st != hipStreamCaptureStatusNone)
+        return set_error(BLF_ERR_UNSUPPORTED, "DCM-MPC solve under stream capture (the stage-2 list is host-sequenced)");
     std::lock_guard<std::mutex> lock(mu);
     List& l = lists[s];
     if (l.cap < batch) {
@@ -74,7 +80,7 @@ blf_status Handle::stage2_list(hipStream_t s, int64_t batch, Stage2List* out)
         l.cap = cap;
         l.slot = 0;
     }
-    *out = Stage2List{l.buf, &l.slot};
+    *out = Stage2List{l.buf, &l.slot, l.cap};
     return BLF_OK;
 }
 
@@ -166,7 +172,7 @@ blf_status blf_step_schedule(double initial_time, double final_time, double dT, 
 #endif
 // The sources' hash (Makefile SRC_HASH) makes the loaded library traceable to the tree it was
 // built from (blf/native.py build_provenance).
-const char* blf_version(void) { return "blf-mi355x 0.1.0 (gfx950, fp64, -ffp-contract=off) src " BLF_SRC_HASH; }
+const char* blf_version(void) { return "blf-mi355x 0.2.0 (abi 2, gfx950, fp64, -ffp-contract=off) src " BLF_SRC_HASH; }
 
 
 blf_status blf_set_qp_launch_mode(int32_t fuse_stage2, int32_t single_kernel)

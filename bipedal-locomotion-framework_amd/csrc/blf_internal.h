@@ -29,6 +29,7 @@ blf_status check_hip(hipError_t e, const char* what);
 struct Stage2List {
     int32_t* buf;
     int* slot;
+    int64_t cap;   // entries after the two count slots
 };
 
 struct Handle {

@@ -744,6 +744,9 @@ __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const R
     const T nu1 = FD3(K.P01, dx0, K.P11, dx1, s1);
     const T rh0 = P.Rw0 * (K.r0 - K.rr0);
     const T rh1 = P.Rw1 * (K.r1 - K.rr1);
+    // the costates of the new point (K.rh is free after the solve): the refinement's nu (as_refine)
+    K.rh0 = nu0;
+    K.rh1 = nu1;
     const T g0 = fma(K.be, nu0, -rh0);
     const T g1 = fma(K.be, nu1, -rh1);
     const Row<T> a = normal<T>(R, pi1, cx);
@@ -791,6 +794,70 @@ __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const R
         viol = true;
         K.add |= vm;
         K.drop &= ~vm;
+    }
+}
+
+// r_k back onto its active line after a fp64 step (c = 1; oracle project_line): the step moves r
+// along the line in exact arithmetic, but its rounding scales with the step's terms (costates up to
+// 1e10 on the pushed-robot windows), and a drift of 1e-10 off the line failed the certificate's
+// primal check pass after pass.  One quotient per knot, the result selected by the case.
+template <class T, class RS>
+__device__ __forceinline__ void as_project(AKnotT<T>& K, const RS& R, int col, int pk)
+{
+    const int pc = pk & 3, pi1 = (pk >> 2) & 15;
+    const Row<T> a = row<T>(R, pi1, opaque(col));
+    const T aa = FD2(a.x, a.x, a.y, a.y);
+    const T t = (FD2(a.x, K.r0, a.y, K.r1) - a.b) / aa;
+    const T p0 = fma(-t, a.x, K.r0);
+    const T p1 = fma(-t, a.y, K.r1);
+    K.r0 = pc == 1 ? p0 : K.r0;
+    K.r1 = pc == 1 ? p1 : K.r1;
+}
+
+// The refinement of a certified fp64 optimum (oracle dcm_polish, refine_rhs; dcm_qp_common.h): the
+// stationarity residuals at (xi, r, nu) in double-double drive one more Newton step with the
+// certified pass's factorization (K.P, K.h).  K.rh holds the certificate's costates nu_k.
+template <int KPL, int TR, class RS>
+__device__ __forceinline__ void as_refine(AKnot (&K)[KPL], const PT<double>& P, const RS& R, int N, int lane,
+                                          double xi00, double xi01, const int (&pk)[KPL])
+{
+    constexpr int L = KPL - 1;
+    double xk[KPL][2];
+    as_xi_prev<KPL, double>(K, lane, xi00, xi01, xk);
+    // the next knot's costate and omega: the lane's next slot, or the next lane's first
+    double nn0[KPL], nn1[KPL], wn[KPL];
+    if constexpr (KPL == 2) {
+        nn0[0] = K[1].rh0;
+        nn1[0] = K[1].rh1;
+        wn[0] = K[1].w;
+    }
+    nn0[L] = dpp1<kNextWrap>(K[0].rh0);
+    nn1[L] = dpp1<kNextWrap>(K[0].rh1);
+    wn[L] = dpp1<kNextWrap>(K[0].w);
+    double g[KPL][2], dr[KPL][2], dx[KPL][2], vn[KPL][2];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const int k = KPL * lane + j;
+        g[j][0] = g[j][1] = 0.0;
+        if (k < N) {
+            const bool last = k == N - 1;
+            const Row<double> a = normal<double>(R, (pk[j] >> 2) & 15, opaque(R.col(j, lane)));
+            refine_rhs(xk[j][0], xk[j][1], K[j].x0, K[j].x1, K[j].r0, K[j].r1, K[j].rr0, K[j].rr1, K[j].xr0,
+                       K[j].xr1, K[j].w, wn[j], K[j].rh0, K[j].rh1, nn0[j], nn1[j], last, P.dt,
+                       last ? P.Pw0 : P.Qw0, last ? P.Pw1 : P.Qw1, P.Rw0, P.Rw1, pk[j] & 3, a.x, a.y, K[j].d0,
+                       K[j].d1, K[j].qx0, K[j].qx1, g[j][0], g[j][1]);
+        }
+    }
+    as_solve<KPL, TR, double>(K, g, N, lane, dr, dx, vn);
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        if (KPL * lane + j < N) {
+            K[j].r0 = K[j].r0 + dr[j][0];
+            K[j].r1 = K[j].r1 + dr[j][1];
+            K[j].x0 = K[j].x0 + dx[j][0];
+            K[j].x1 = K[j].x1 + dx[j][1];
+            as_project<double>(K[j], R, R.col(j, lane), pk[j]);
+        }
     }
 }
 
@@ -906,6 +973,7 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
                     K[j].r1 = K[j].r1 + dr[j][1];
                     K[j].x0 = K[j].x0 + dx[j][0];
                     K[j].x1 = K[j].x1 + dx[j][1];
+                    if constexpr (sizeof(T) == 8) as_project<T>(K[j], R, R.col(j, lane), opaque(pk[j]));
                     as_certify<T>(K[j], P, R, R.col(j, lane), opaque(pk[j]), dx[j][0], dx[j][1], vn[j][0], vn[j][1],
                                   pl[j][0], pl[j][1], okp, neg, viol);
                 }
@@ -936,6 +1004,13 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
         }
     }
     npass = pass < kGuessPasses ? pass + 1 : kGuessPasses;   // the passes run (wave-uniform)
+    if constexpr (sizeof(T) == 8) {
+        // the refinement where the largest multiplier exceeds kRefineLam (oracle ORC_REFINE_LAM)
+        bool big = false;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) big = big || pl[j][0] > kRefineLam || pl[j][1] > kRefineLam;
+        if (certified && __ballot(big) != 0) as_refine<KPL, TR>(K, P, R, N, lane0, xi00, xi01, pk);
+    }
     return certified;
 }
 
@@ -1138,7 +1213,7 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
                                                  bool certified, int status, int64_t p, int N, int M, int lane,
                                                  double xi00, double xi01, double* xi_out, double* vrp_out,
                                                  int32_t* status_out, int32_t* iters_out, int32_t* polished_out,
-                                                 double* lam_out, int32_t* list, int list_slot,
+                                                 double* lam_out, int32_t* list, int list_slot, int list_cap,
                                                  int32_t* passes_out, int npass, int pend = kPending)
 {
     const bool done = certified || status != 0;
@@ -1173,7 +1248,9 @@ __device__ __forceinline__ void as_write_outputs(const AKnot (&K)[KPL], const in
         } else if (list != nullptr) {
             // stage 2's work list: its kernel loops over the listed QPs only, so a batch with none
             // pending costs one tiny launch (order is irrelevant: each QP is solved on its own)
-            list[2 + atomicAdd(&list[list_slot], 1)] = (int32_t)p;
+            // (bounded by the list's capacity: stage 2 reads at most list_cap entries)
+            const int at = atomicAdd(&list[list_slot], 1);
+            if (at < list_cap) list[2 + at] = (int32_t)p;
         }
     }
 }
@@ -1379,7 +1456,7 @@ __device__ __forceinline__ void cold_solve(
     }
     AS_STAMP_ADD(14, t_b);
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
-                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot,
+                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot, P.list_cap,
                                   P.passes_out, npass, pend);
     if (PH && !certified && status == 0) ph_write_window<KPL>(ps, sPh, omega, A2d, Bv, p, N, M, S, NH, lane);
     AS_STAMP_ADD(0, t_start);
@@ -1604,7 +1681,7 @@ __global__ __launch_bounds__(kWave, 2) void dcm_mpc_warm_kernel(
     AS_STAMP(t_out);
 
     as_write_outputs<KPL, LAMOUT>(K, pk, pl, certified, status, p, N, M, lane, xi00, xi01, xi_out, vrp_out,
-                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot,
+                                  status_out, iters_out, polished_out, lam_out, P.list, P.list_slot, P.list_cap,
                                   P.passes_out, npass);
     if (PH && !certified && status == 0)
         ph_write_window<KPL>(ps, sPh, omega, reinterpret_cast<const double*>(A2), Bv, p, N, M, S, NH, lane);

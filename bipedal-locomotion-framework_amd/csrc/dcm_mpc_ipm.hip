@@ -60,7 +60,8 @@ __global__ __launch_bounds__(NT, (NT <= 256 ? BLF_MIN_WAVES : 1)) void dcm_mpc_i
     int32_t* __restrict__ iters_out, int32_t* __restrict__ polished_out, double* __restrict__ lam_out)
 {
     const int32_t* idx = P.list + 2;
-    const int count = __builtin_amdgcn_readfirstlane(P.list[P.list_slot]);
+    const int listed = __builtin_amdgcn_readfirstlane(P.list[P.list_slot]);
+    const int count = listed < P.list_cap ? listed : P.list_cap;
     if (blockIdx.x == 0 && threadIdx.x == 0) P.list[P.list_slot ^ 1] = 0;
     for (int i = (int)blockIdx.x; i < count; i += (int)gridDim.x) {
         ipm_solve<NT, WARM, LAMOUT, MF>(P, __builtin_amdgcn_readfirstlane(idx[i]), xi_init, omega, xi_ref, vrp_ref,
@@ -141,6 +142,7 @@ KParams make_kparams(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_warm_start
     kp.stage2 = 0;
     kp.list = nullptr;
     kp.list_slot = 0;
+    kp.list_cap = 0;
     kp.passes_out = nullptr;
     kp.f_dt = (float)kp.dt;
     kp.f_Qw0 = (float)kp.Qw0; kp.f_Qw1 = (float)kp.Qw1;
@@ -176,18 +178,31 @@ blf_status launch_ipm(const KParams& kp, const blf_dcm_mpc_problem* pb, const bl
 // (Handle::stage2_list: [0], [1] two count slots, [2..] the QPs).  The active-set kernel appends
 // to slot *slot, which is 0 when it starts; the IPM kernel's list instantiation loops over what it
 // finds there with kListGrid workgroups and zeroes the other slot, and *slot flips to that one
-// for the stream's next solve.
+// for the stream's next solve -- only once that launch is enqueued (finish_stage2).  When a launch
+// fails after the active-set kernel may have appended, both count slots are zeroed on the stream,
+// so the stream's next solve does not append on top of a stale count.
 static void set_pend(KParams& kp, const Stage2List& l)
 {
     kp.list = l.buf;
     kp.list_slot = *l.slot;
+    kp.list_cap = (int)l.cap;
 }
 static void set_stage2(KParams& kp, const Stage2List& l)
 {
     kp.stage2 = 1;
     kp.list = l.buf;
     kp.list_slot = *l.slot;
-    *l.slot ^= 1;
+    kp.list_cap = (int)l.cap;
+}
+static blf_status finish_stage2(blf_status st, const Stage2List& l, hipStream_t s)
+{
+    if (st == BLF_OK) {
+        *l.slot ^= 1;
+        return st;
+    }
+    (void)hipMemsetAsync(l.buf, 0, sizeof(int32_t) * 2, s);
+    *l.slot = 0;
+    return st;
 }
 
 blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_problem* pb,
@@ -210,8 +225,10 @@ blf_status launch_dcm_mpc(const blf_dcm_mpc_params* prm, const blf_dcm_mpc_probl
         set_pend(kp, l);
         const blf_status st = launch_dcm_mpc_as(kp, pb, warm, batch, sol, lam_out, s, nullptr, &stage2_done);
         kp.list = nullptr;
-        if (st != BLF_OK || stage2_done) return st;
+        if (st != BLF_OK) return finish_stage2(st, l, s);
+        if (stage2_done) return st;
         set_stage2(kp, l);
+        return finish_stage2(launch_ipm(kp, pb, warm, batch, sol, lam_out, s), l, s);
     }
     return launch_ipm(kp, pb, warm, batch, sol, lam_out, s);
 }
@@ -255,10 +272,10 @@ blf_status launch_dcm_mpc_phased(const blf_dcm_mpc_params* prm, const blf_phase_
     set_pend(kp, l);
     const blf_status st = launch_dcm_mpc_as(kp, &pin, warm, batch, sol, lam_out, s, &ps);
     kp.list = nullptr;
-    if (st != BLF_OK) return st;
+    if (st != BLF_OK) return finish_stage2(st, l, s);
     set_stage2(kp, l);
     const blf_dcm_mpc_problem pw{xi_init, win->omega, win->xi_ref, win->vrp_ref, win->A, win->b, win->nfacets};
-    return launch_ipm(kp, &pw, warm, batch, sol, lam_out, s);
+    return finish_stage2(launch_ipm(kp, &pw, warm, batch, sol, lam_out, s), l, s);
 }
 
 }  // namespace blf

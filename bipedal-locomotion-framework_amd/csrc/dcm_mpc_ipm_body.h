@@ -39,6 +39,8 @@ __device__ unsigned long long g_blf_stamps[16];
 constexpr int kBP = 4;    // P_{64w} (3): the first knot's P, read by lane 63 of wavefront w-1
 constexpr int kBV = 8;    // v_{64w} (2): backward-scan value at the first knot of wavefront w
 constexpr int kBX = 10;   // x_{64w+64} (2): forward-scan value past the last knot of wavefront w
+constexpr int kBN = 0;    // (nu_{64w}, omega_{64w}) (3): the refinement's next-knot costate, read by
+                          // lane 63 of wavefront w-1
 constexpr int kBnd = 16;
 struct Lds {
     double2 *A2, *BI;   // facet rows: normal (a_x, a_y); (b, 1/s), 1/s later the multiplier step
@@ -339,6 +341,18 @@ template <class KN>
 __device__ __forceinline__ double facet_rp(const KN& K, double2 a, double bi, int i)
 {
     return (FD2(a.x, K.r0, a.y, K.r1) + K.s[i]) - bi;
+}
+
+// r back onto its active line after a polish step (c = 1; oracle project_line): the step moves r
+// along the line in exact arithmetic, but its rounding scales with the step's terms (costates up
+// to 1e10 on the pushed-robot windows), and a drift of 1e-10 off the line failed the certificate.
+template <class KN>
+__device__ __forceinline__ void project_line(KN& K, double2 a, double bi)
+{
+    const double aa = FD2(a.x, a.x, a.y, a.y);
+    const double t = (FD2(a.x, K.r0, a.y, K.r1) - bi) / aa;
+    K.r0 = fma(-t, a.x, K.r0);
+    K.r1 = fma(-t, a.y, K.r1);
 }
 
 // The affine slack / multiplier step of facet i for the VRP step (dra0, dra1) (oracle affine_step).
@@ -1011,6 +1025,7 @@ __device__ __forceinline__ void ipm_solve(
         // the interior point method starts from the saturated LQ start (sat_start) when an
         // active-set start failed: the kernel's own (guess), or the active-set kernel's (stage 2)
         bool sat_pending = P.tol_polish > 0.0 && P.stage2;
+        double last_a = 1.0;   // the previous IPM step length (the stalled-step polish, kStallStep)
         for (it = 0; status == 0; ++it) {
             if (BLF_SAT_ON && sat_pending) {
                 sat_pending = false;
@@ -1036,7 +1051,10 @@ __device__ __forceinline__ void ipm_solve(
                 break;
             }
             STAMP_ADD(4, t_r);
-            if (guess || (P.tol_polish > 0.0 && mu <= P.tol_polish)) {
+            // the polish at mu <= tol_polish, and after a stalled step once mu <= kStallMu (oracle
+            // ORC_STALL_STEP: the pushed-robot windows stall at mu ~1e-3 with steps of 1e-8..1e-100
+            // while lam > s already names the optimal active set)
+            if (guess || (P.tol_polish > 0.0 && (mu <= P.tol_polish || (last_a < kStallStep && mu <= kStallMu)))) {
                 // ---- active-set polish (oracle dcm_polish, DESIGN.md 4 "Polish"): one Newton
                 //      step of the QP with the guessed active facets as equalities, certified
                 //      (primal, stationarity, multiplier signs) or undone; a failed pass is
@@ -1053,18 +1071,30 @@ __device__ __forceinline__ void ipm_solve(
                     const int dm = opaque(drop), am = opaque(add), gk = opaque(gm);
                     int cm = 0;   // the pass's active-set candidates (bit i: facet i)
                     double lmx = 0.0;   // the knot's largest multiplier (the IPM guess's scale)
+                    int jm = 0;         // its facet (the first of equal ones)
                     if (!guess) {
 #pragma unroll
                         for (int i = 0; i < MF; ++i) {
                             if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
-                            if (i < km) lmx = keepmax(lmx, K.lam[i]);
+                            if (i < km) {
+                                if (K.lam[i] > lmx) jm = i;
+                                lmx = keepmax(lmx, K.lam[i]);
+                            }
                         }
                     }
+                    const double2 amx = L.A2[jm * N + kx];
 #pragma unroll
                     for (int i = 0; i < MF; ++i) {
                         if (MF <= kMaxFacets && i >= mm) break;   // 16 slots: no early exit, so the loop unrolls fully
-                        const bool base = guess ? ((gk >> i) & 1) != 0
-                                                : (K.lam[i] > K.s[i] && K.lam[i] >= kLamRel * lmx);
+                        // faint (oracle cand_bit): below kLamRel of the knot's largest multiplier and
+                        // within kLamRelCross of parallel to its facet
+                        bool faint = false;
+                        if (!guess && i < km) {
+                            const double2 ai = L.A2[i * N + kx];
+                            const double cr = fabs(fma(ai.x, amx.y, -(ai.y * amx.x)));
+                            faint = K.lam[i] < kLamRel * lmx && cr < kLamRelCross;
+                        }
+                        const bool base = guess ? ((gk >> i) & 1) != 0 : (K.lam[i] > K.s[i] && !faint);
                         if (i < km && ((base && !((dm >> i) & 1)) || ((am >> i) & 1))) {
                             if (pc == 0) pi1 = i;
                             else if (pc == 1) pi2 = i;
@@ -1149,16 +1179,23 @@ __device__ __forceinline__ void ipm_solve(
                     solve<NW>(K, K.rh0, K.rh1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1,
                               dxk0, dxk1);
                     STAMP_ADD(15, t_ps);
+                    // K.rh and K.d are free after the solve: the refinement's nu_k (below) and the step
+                    // of xi_{64 wv} (lane 0: the refinement's xi_k)
+                    K.d0 = dxk0;
+                    K.d1 = dxk1;
                     if (own) {
                         K.r0 = K.r0 + dr0;
                         K.r1 = K.r1 + dr1;
                         K.x0 = K.x0 + dx0;
                         K.x1 = K.x1 + dx1;
                         const int kx = opaque(k);
+                        if (pc == 1) project_line(K, L.A2[pi1 * N + kx], L.BI[pi1 * N + kx].x);
                         const double s0 = K.qx0 + vn0;
                         const double s1 = K.qx1 + vn1;
                         const double nu0 = FD3(K.P00, dx0, K.P01, dx1, s0);
                         const double nu1 = FD3(K.P01, dx0, K.P11, dx1, s1);
+                        K.rh0 = nu0;
+                        K.rh1 = nu1;
                         const double rh0 = P.Rw0 * (K.r0 - rref[0]);
                         const double rh1 = P.Rw1 * (K.r1 - rref[1]);
                         const double g0 = fma(K.be, nu0, -rh0);
@@ -1268,6 +1305,45 @@ __device__ __forceinline__ void ipm_solve(
 #pragma unroll
                         for (int i = 0; i < MF; ++i)
                             K.lam[i] = (pc >= 1 && i == pi1) ? pl1 : (pc == 2 && i == pi2) ? pl2 : 0.0;
+                    }
+                    // the refinement where the largest multiplier exceeds kRefineLam (oracle
+                    // dcm_polish, refine_rhs): the certificate's costates, the same factorization
+                    const double lq = R.keepmax(own ? keepmax(keepmax(0.0, pl1), pl2) : 0.0);
+                    if (lq > kRefineLam) {
+                        // xi_{64 wv} after the polish step (the previous wavefront's last lane did the same)
+                        const double xr0 = wv > 0 ? xb0 + K.d0 : xb0, xr1 = wv > 0 ? xb1 + K.d1 : xb1;
+                        const double nu0 = K.rh0, nu1 = K.rh1;
+                        double xk0r, xk1r;
+                        xi_prev(K, lane, xr0, xr1, xk0r, xk1r);
+                        // the next knot's costate and omega: the next lane's, across a wavefront from LDS
+                        if (lane == 0 && wv > 0) {
+                            bnd[kBnd * wv + kBN] = nu0;
+                            bnd[kBnd * wv + kBN + 1] = nu1;
+                            bnd[kBnd * wv + kBN + 2] = K.w;
+                        }
+                        if constexpr (NW > 1) __syncthreads();
+                        double nn0 = dpp1<kNextWrap>(nu0), nn1 = dpp1<kNextWrap>(nu1), wn = dpp1<kNextWrap>(K.w);
+                        if (NW > 1 && lane == kWave - 1 && wv < nwa - 1) {
+                            nn0 = bnd[kBnd * (wv + 1) + kBN];
+                            nn1 = bnd[kBnd * (wv + 1) + kBN + 1];
+                            wn = bnd[kBnd * (wv + 1) + kBN + 2];
+                        }
+                        double g0 = 0.0, g1 = 0.0;
+                        if (own) {
+                            const double2 a = L.A2[pi1 * N + opaque(k)];
+                            refine_rhs(xk0r, xk1r, K.x0, K.x1, K.r0, K.r1, rref[0], rref[1], xref[0], xref[1], K.w, wn,
+                                       nu0, nu1, nn0, nn1, last, P.dt, last ? P.Pw0 : P.Qw0, last ? P.Pw1 : P.Qw1,
+                                       P.Rw0, P.Rw1, pc, a.x, a.y, K.d0, K.d1, K.qx0, K.qx1, g0, g1);
+                        }
+                        double dr0, dr1, dx0, dx1, vn0, vn1, ek0, ek1;
+                        solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1, ek0, ek1);
+                        if (own) {
+                            K.r0 = K.r0 + dr0;
+                            K.r1 = K.r1 + dr1;
+                            K.x0 = K.x0 + dx0;
+                            K.x1 = K.x1 + dx1;
+                            if (pc == 1) project_line(K, L.A2[pi1 * N + opaque(k)], L.BI[pi1 * N + opaque(k)].x);
+                        }
                     }
                     polished = 1;
                     break;   // solved: the certified optimum
@@ -1479,6 +1555,7 @@ __device__ __forceinline__ void ipm_solve(
             }
             dres = dres * (1.0 - a);
             pres = pres * (1.0 - a);
+            last_a = a;
             // sum (s + a ds)(lam + a dl) = U0 + a T1 + a^2 T2, T1 = -sum rc = -(U0 + U2 - ntot sigma mu)
             if (ntot > 0) {
                 const double nt = (double)ntot;

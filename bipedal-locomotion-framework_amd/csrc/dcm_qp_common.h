@@ -26,6 +26,7 @@ struct KParams {
                          // the problems the active-set kernel handed over.  The active-set
                          // kernels append to it; stage 2's small grid loops over it.
     int list_slot;       // 0 or 1
+    int list_cap;        // entries the list holds (appends beyond it are dropped; stage 2 reads at most this many)
     int32_t* passes_out; // [B] or nullptr: the active-set kernels' passes per QP (float + fp64);
                          // the IPM kernel writes 0 for the problems it solves alone
     // The active-set kernel's fp32 search (cold starts): the parameters rounded to float, and the
@@ -56,6 +57,109 @@ constexpr double kTolDualRel = 1e-3;
 // largest violation (oracle ORC_ADD_REL).
 constexpr double kLamRel = 1e-8;
 constexpr double kAddRel = 1e-2;
+// Round 6 (oracle ORC_LAM_REL_CROSS, ORC_STALL_STEP / ORC_STALL_MU, ORC_REFINE_LAM; DESIGN.md 4,
+// item 11): the kLamRel rule only drops a facet within |a_i x a_max| < kLamRelCross of parallel to
+// the knot's largest multiplier's facet; the IPM polish also runs after a step shorter than
+// kStallStep once mu <= kStallMu; a certified optimum whose largest multiplier exceeds kRefineLam
+// takes one refinement step with double-double residuals (refine_rhs below).
+constexpr double kLamRelCross = 0.3;
+constexpr double kStallStep = 0.2;
+constexpr double kStallMu = 1.0;
+constexpr double kRefineLam = 1e4;
+
+// ---- double-double arithmetic of the refinement (exact TwoSum / TwoProd by fma; the oracle's
+//      dd_* restate these operation for operation) ----
+struct DD {
+    double hi, lo;
+};
+__device__ __forceinline__ DD dd_two_sum(double a, double b)
+{
+    const double s = a + b;
+    const double bb = s - a;
+    return {s, (a - (s - bb)) + (b - bb)};
+}
+__device__ __forceinline__ DD dd_fast(double a, double b)
+{
+    const double s = a + b;
+    return {s, b - (s - a)};
+}
+__device__ __forceinline__ DD dd_prod(double a, double b)
+{
+    const double p = a * b;
+    return {p, fma(a, b, -p)};
+}
+__device__ __forceinline__ DD dd_add(DD x, DD y)
+{
+    const DD s = dd_two_sum(x.hi, y.hi);
+    return dd_fast(s.hi, s.lo + (x.lo + y.lo));
+}
+__device__ __forceinline__ DD dd_add_d(DD x, double y)
+{
+    const DD s = dd_two_sum(x.hi, y);
+    return dd_fast(s.hi, s.lo + x.lo);
+}
+__device__ __forceinline__ DD dd_mul_d(DD x, double y)
+{
+    const DD p = dd_prod(x.hi, y);
+    return dd_fast(p.hi, fma(x.lo, y, p.lo));
+}
+__device__ __forceinline__ DD dd_neg(DD x)
+{
+    return {-x.hi, -x.lo};
+}
+
+// The refinement's right-hand side of one knot k (oracle refine_rhs): with the certified costates
+// nu_k (of xi_{k+1}) and nu_{k+1},
+//   d_k  = xi_k + dt (om_k xi_k - om_k r_k) - xi_{k+1},
+//   qx_k = W (xi_{k+1} - xi_ref_{k+1}) - nu_k + (1 + dt om_{k+1}) nu_{k+1}   (no last term at N - 1),
+//   g_k  = R (r_k - r_ref_k) - dt om_k nu_k, onto the active line's tangent (c = 1), 0 at a vertex,
+// each in double-double, rounded once.  The stationarity residuals of the certified point are
+// small, so the Newton step they drive (the same factorization) is small and accurate: it brings
+// the multiplier-1e6..1e9 windows from ~1e-14 x lambda_max to ~1e-11 m (tests/test_c5_windows.py).
+// One component j of d_k and qx_k.
+__device__ __forceinline__ void refine_comp(double xk, double xn, double r, double xr, double om, double omn,
+                                            double nu, double nun, bool last, double dt, double Wq, double& d,
+                                            double& q)
+{
+    DD e = dd_add(dd_prod(om, xk), dd_neg(dd_prod(om, r)));
+    e = dd_mul_d(e, dt);
+    e = dd_add_d(e, xk);
+    e = dd_add_d(e, -xn);
+    d = e.hi;
+    DD s = dd_mul_d(dd_two_sum(xn, -xr), Wq);
+    s = dd_add_d(s, -nu);
+    if (!last) {
+        s = dd_add(s, dd_mul_d(dd_prod(dt, omn), nun));
+        s = dd_add_d(s, nun);
+    }
+    q = s.hi;
+}
+
+__device__ __forceinline__ void refine_rhs(double xk0, double xk1, double xn0, double xn1, double r0, double r1,
+                                           double rr0, double rr1, double xr0, double xr1, double om, double omn,
+                                           double nu0, double nu1, double nun0, double nun1, bool last, double dt,
+                                           double Wq0, double Wq1, double Rw0, double Rw1, int c, double ax,
+                                           double ay, double& d0, double& d1, double& q0, double& q1, double& g0,
+                                           double& g1)
+{
+    refine_comp(xk0, xn0, r0, xr0, om, omn, nu0, nun0, last, dt, Wq0, d0, q0);
+    refine_comp(xk1, xn1, r1, xr1, om, omn, nu1, nun1, last, dt, Wq1, d1, q1);
+    const DD bk = dd_prod(dt, om);
+    const DD e0 = dd_add(dd_mul_d(dd_two_sum(r0, -rr0), Rw0), dd_neg(dd_mul_d(bk, nu0)));
+    const DD e1 = dd_add(dd_mul_d(dd_two_sum(r1, -rr1), Rw1), dd_neg(dd_mul_d(bk, nu1)));
+    if (c == 0) {
+        g0 = e0.hi;
+        g1 = e1.hi;
+    } else if (c == 1) {   // t = (-a_y, a_x): g <- t (t . g) / |a|^2
+        const DD tg = dd_add(dd_mul_d(e0, -ay), dd_mul_d(e1, ax));
+        const double tau = tg.hi / fma(ax, ax, ay * ay);   // FD2(ax, ax, ay, ay)
+        g0 = -(ay * tau);
+        g1 = ax * tau;
+    } else {
+        g0 = 0.0;
+        g1 = 0.0;
+    }
+}
 
 // v_readlane of a double (lane l uniform)
 __device__ __forceinline__ double readlane_f64(double v, int l)

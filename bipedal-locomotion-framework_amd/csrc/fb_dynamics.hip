@@ -1781,7 +1781,12 @@ __global__ __launch_bounds__(64) void fb_frame_state_kernel(Model m, blf_fb_stat
     for (int c = lane; c < K; c += kWave) {
         const int f = frames[c];
         double p[12], tw[6];
-        frame_state(S.link() + S.lrec * m.flink[f], m.fpose + 12 * f, p, tw);
+        if (f >= 0 && f < m.F) {
+            frame_state(S.link() + S.lrec * m.flink[f], m.fpose + 12 * f, p, tw);
+        } else {   // a frame index outside [0, nframes): NaN, never an out-of-bounds read
+            for (int a = 0; a < 12; ++a) p[a] = __builtin_nan("");
+            for (int a = 0; a < 6; ++a) tw[a] = __builtin_nan("");
+        }
         if (pose)
             for (int a = 0; a < 12; ++a) pose[(q * K + c) * 12 + a] = p[a];
         if (twist)

@@ -215,6 +215,7 @@ __global__ __launch_bounds__(64) void hullnd_kernel(const double* __restrict__ p
         count += __builtin_popcountll(live);
         overflow = overflow || count > M;
         __syncthreads();
+        if (overflow) break;   // the result is -1 already (count is wave-uniform)
     }
     if (overflow || count < D + 1) {
         if (lane == 0) nfout[s] = -1;

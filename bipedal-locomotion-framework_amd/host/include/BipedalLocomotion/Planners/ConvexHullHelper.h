@@ -5,7 +5,9 @@
  * buildConvexHull runs blf_hull2d_hrep on the device for 2 x p points (the planners' support
  * polygons, p <= 16), blf_hull3d_hrep for 3 x p points (p <= 16; the reference's own test,
  * ConvexHullHelperTest.cpp:15-63, is 3-D) and blf_hullnd_hrep for any other n x p (1 <= n <= 8,
- * p <= 32); getA()/getB() return the H-representation A x <= b (unit outward normals; 2-D:
+ * p <= 32; n = 1 is an extension -- the reference hands every matrix to Qhull, which refuses one
+ * dimension, so its buildConvexHull fails there, while this one returns the rows +1 / -1 of the
+ * interval); getA()/getB() return the H-representation A x <= b (unit outward normals; 2-D:
  * merged collinear facets, counter-clockwise; otherwise one row per distinct supporting
  * hyperplane, where Qhull "Qt" may give a split facet once per simplex — Qhull's facet order is
  * internal to Qhull, so only the SET of planes is comparable).  doesPointBelongToConvexHull runs

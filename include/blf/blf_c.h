@@ -86,7 +86,13 @@ blf_status blf_create(blf_handle** handle, int32_t device);
 blf_status blf_destroy(blf_handle* handle);
 /* Human-readable description of the last error on this thread (never NULL). */
 const char* blf_last_error(void);
-/* Version string of the library (build id). */
+/* Version string of the library: "blf-mi355x <version> (abi <n>, ...) src <hash>".  ABI 2 (0.2.0)
+ * added the optional pointer fields blf_dcm_mpc_solution.passes and blf_fb_contacts.law / .wrench:
+ * a caller built against an older header must zero-initialise these structs (`= {0}`), since the
+ * library reads every field as a device pointer or NULL.  Solves that use a stream's stage-2 list
+ * (blf_dcm_mpc_solve*) are refused with BLF_ERR_UNSUPPORTED while that stream is being captured
+ * into a graph: the list's slot is sequenced on the host. */
+#define BLF_ABI_VERSION 2
 const char* blf_version(void);
 /* QP kernel routing for A/B and parity tests (no reference counterpart; the defaults are the
  * product's).  fuse_stage2 = 0: small cold batches with N <= 64 run the IPM's stage 2 as its own
@@ -476,7 +482,9 @@ typedef struct blf_fb_contacts {
 /* The world transform pose [B][K][12] = (p, R row-major) and the mixed velocity twist [B][K][6]
  * = (v, w) of K frames of every system (either output may be NULL): what the reference hands a
  * contact model through kinDyn getWorldTransform / getFrameVel (FloatingBaseSystemDynamics.cpp:
- * 225-226) before it asks for the wrench, for the caller's BLF_CONTACT_WRENCH models.            */
+ * 225-226) before it asks for the wrench, for the caller's BLF_CONTACT_WRENCH models.  A frame
+ * index outside [0, model->nframes) yields NaN pose and twist for that frame (no read past the
+ * model).                                                                                        */
 blf_status blf_fb_frame_state(blf_handle* handle, const blf_fb_model* model,
                               const blf_fb_state* state, int32_t nframes, const int32_t* frames,
                               int64_t batch, double* pose, double* twist, void* stream);

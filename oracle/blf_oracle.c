@@ -614,8 +614,15 @@ double orc_wave_tree_sum(const double* c, int n)
 #endif
 #define ORC_TOL_DUAL_REL 1e-3   /* the certificate's relative dual tolerance (kernel kTolDualRel) */
 #define ORC_LAM_REL 1e-8        /* the IPM polish's guess: lam_i >= this x the knot's largest (kernel kLamRel) */
+#define ORC_LAM_REL_CROSS 0.3   /* ... among facets this close to parallel to the largest one's (kernel kLamRelCross) */
 #define ORC_ADD_REL 1e-2        /* the IPM polish adds facets violated by >= this x the largest (kernel kAddRel) */
 #define ORC_GUESS_SLACK 1e-5  /* the fp64 passes' guess after the fp32 search (kernel: kGuessSlack) */
+/* round 6: the IPM polish also runs after a stalled step (a < ORC_STALL_STEP) once mu <= ORC_STALL_MU
+ * (kernel kStallStep / kStallMu), and a certified optimum whose largest multiplier exceeds
+ * ORC_REFINE_LAM takes one refinement step with double-double residuals (kernel kRefineLam) */
+#define ORC_STALL_STEP 0.2
+#define ORC_STALL_MU 1.0
+#define ORC_REFINE_LAM 1e4
 #define WV 64
 
 /* Fused forms, used in exactly the places the kernel uses them (csrc/dcm_mpc_ipm.hip):
@@ -1558,25 +1565,146 @@ static void affine_step(const dcm_ws* w, int k, int i, double* ds, double* dl)
  * and 1 is returned.  Rejected: xi, vrp are restored, 0 is returned. */
 /* Facet i of knot k is in a polish pass's active set: guessed (the active-set start's guess bits,
  * or an IPM iterate's lam_i > s_i) and not dropped, or added. */
-/* An IPM iterate's guess: lam_i > s_i, and lam_i at least ORC_LAM_REL (1e-8) of the knot's
- * largest multiplier.  The second condition only matters where multipliers reach ~1e7 (the
+/* An IPM iterate's guess: lam_i > s_i, and not faint: lam_i below ORC_LAM_REL (1e-8) of the knot's
+ * largest multiplier while facet i is within |a_i x a_max| < ORC_LAM_REL_CROSS (0.3, 17 degrees) of
+ * parallel to that multiplier's facet.  The rule only matters where multipliers reach ~1e7 (the
  * uncapturable-state windows, tests/golden/c5_hard_windows.npz): on an edge that meets a nearly
  * parallel neighbour (support polygons of slightly rotated feet, facets 0.1 degree apart) the
  * neighbour's slack is ~1e-5 while its multiplier is ~0.1, rounding-level against the edge's
- * 1e6, and lam > s alone would put the knot on their ill-conditioned vertex. */
+ * 1e6, and lam > s alone would put the knot on their ill-conditioned vertex.  Round 6: only near
+ * parallel facets are faint — on the pushed-robot windows (tests/golden/c5_pushed_windows.npz) a
+ * well-conditioned vertex's second multiplier is below 1e-8 of the first (1e8 against 0.5) and
+ * excluding it made every pass of the polish fail. */
 static int cand_bit(const dcm_ws* w, const int* guess, const int* drop, const int* add, int k, int i)
 {
     double lmx = 0.0;
-    for (int j = 0; j < w->nf[k]; ++j) lmx = keepmax(lmx, w->lam[k * MF + j]);
-    const int base = guess ? ((guess[k] >> i) & 1)
-                           : (w->lam[k * MF + i] > w->s[k * MF + i] && w->lam[k * MF + i] >= ORC_LAM_REL * lmx);
+    int jm = 0;   /* the knot's largest multiplier (the first of equal ones) */
+    for (int j = 0; j < w->nf[k]; ++j) {
+        if (w->lam[k * MF + j] > lmx) jm = j;
+        lmx = keepmax(lmx, w->lam[k * MF + j]);
+    }
+    const double* ai = w->A + (k * w->M + i) * 2;
+    const double* am = w->A + (k * w->M + jm) * 2;
+    const double cr = fabs(fma(ai[0], am[1], -(ai[1] * am[0])));
+    const int faint = w->lam[k * MF + i] < ORC_LAM_REL * lmx && cr < ORC_LAM_REL_CROSS;
+    const int base = guess ? ((guess[k] >> i) & 1) : (w->lam[k * MF + i] > w->s[k * MF + i] && !faint);
     return (base && !((drop[k] >> i) & 1)) || ((add[k] >> i) & 1);
+}
+
+/* ---- the refinement of a certified optimum (round 6; the kernels' refine_rhs, dcm_qp_common.h).
+ * Where the multipliers reach 1e6-1e9 (uncapturable DCM states, tests/golden/c5_*_windows.npz)
+ * the costates are ~1e8-1e10 and a fp64 solve determines the VRPs only to ~1e-14 x the largest
+ * multiplier: the step's own right-hand side (q_k = Q (xi - xi_ref), the costate scan) rounds at
+ * that scale.  The refinement takes ONE more Newton step of the same equality-constrained QP with
+ * the same factorization, written in the Lagrangian-shifted form: with the certified costates nu
+ * (nu_k = the costate of xi_{k+1}),
+ *   d_k  = xi_k + dt (om_k xi_k - om_k r_k) - xi_{k+1}                    (the Euler defect)
+ *   qx_k = W_k (xi_{k+1} - xi_ref_{k+1}) - nu_k + (1 + dt om_{k+1}) nu_{k+1}   (0 past knot N - 1)
+ *   g_k  = R (r_k - r_ref_k) - dt om_k nu_k, projected onto the active line (c = 1), 0 at a vertex
+ * — the stationarity residuals at (xi, r, nu), which are small, so the step's costates are small
+ * and its rounding is small.  Each is evaluated in double-double (exact TwoSum / TwoProd by fma,
+ * the exact alpha_k = 1 + dt om_k and beta_k = dt om_k) and rounded once.  Measured: every window of
+ * the three c5 fixtures from <= 5.7e-4 to <= 1.6e-11 m against the extended-precision solve
+ * (tests/test_c5_windows.py). */
+typedef struct { double hi, lo; } ddv;
+static ddv dd_two_sum(double a, double b)
+{
+    const double s = a + b;
+    const double bb = s - a;
+    ddv r = { s, (a - (s - bb)) + (b - bb) };
+    return r;
+}
+static ddv dd_fast(double a, double b)
+{
+    const double s = a + b;
+    ddv r = { s, b - (s - a) };
+    return r;
+}
+static ddv dd_prod(double a, double b)
+{
+    const double p = a * b;
+    ddv r = { p, fma(a, b, -p) };
+    return r;
+}
+static ddv dd_add(ddv x, ddv y)
+{
+    const ddv s = dd_two_sum(x.hi, y.hi);
+    return dd_fast(s.hi, s.lo + (x.lo + y.lo));
+}
+static ddv dd_add_d(ddv x, double y)
+{
+    const ddv s = dd_two_sum(x.hi, y);
+    return dd_fast(s.hi, s.lo + x.lo);
+}
+static ddv dd_mul_d(ddv x, double y)
+{
+    const ddv p = dd_prod(x.hi, y);
+    return dd_fast(p.hi, fma(x.lo, y, p.lo));
+}
+static ddv dd_neg(ddv x)
+{
+    ddv r = { -x.hi, -x.lo };
+    return r;
+}
+
+/* The refinement's right-hand side of knot k (active count c, active row a = facet pi1). */
+static void refine_rhs(const dcm_ws* w, int k, int c, const double* a, const double* nu, double* d,
+                       double* qx, double* g)
+{
+    const int N = w->N;
+    const double om = w->omega[k];
+    const int last = k == N - 1;
+    for (int j = 0; j < 2; ++j) {
+        const double xk = w->xi[2 * k + j], xn = w->xi[2 * (k + 1) + j], r = w->vrp[2 * k + j];
+        ddv e = dd_add(dd_prod(om, xk), dd_neg(dd_prod(om, r)));
+        e = dd_mul_d(e, w->dt);
+        e = dd_add_d(e, xk);
+        e = dd_add_d(e, -xn);
+        d[j] = e.hi;
+        const double Wq = last ? (j ? w->Pw1 : w->Pw0) : (j ? w->Qw1 : w->Qw0);
+        ddv q = dd_mul_d(dd_two_sum(xn, -w->xi_ref[2 * (k + 1) + j]), Wq);
+        q = dd_add_d(q, -nu[2 * k + j]);
+        if (!last) {
+            q = dd_add(q, dd_mul_d(dd_prod(w->dt, w->omega[k + 1]), nu[2 * (k + 1) + j]));
+            q = dd_add_d(q, nu[2 * (k + 1) + j]);
+        }
+        qx[j] = q.hi;
+    }
+    const ddv bk = dd_prod(w->dt, om);
+    const ddv g0 = dd_add(dd_mul_d(dd_two_sum(w->vrp[2 * k], -w->vrp_ref[2 * k]), w->Rw0), dd_neg(dd_mul_d(bk, nu[2 * k])));
+    const ddv g1 = dd_add(dd_mul_d(dd_two_sum(w->vrp[2 * k + 1], -w->vrp_ref[2 * k + 1]), w->Rw1),
+                          dd_neg(dd_mul_d(bk, nu[2 * k + 1])));
+    if (c == 0) {
+        g[0] = g0.hi;
+        g[1] = g1.hi;
+    } else if (c == 1) {   /* t = (-a_y, a_x): g <- t (t . g) / |a|^2 */
+        const ddv tg = dd_add(dd_mul_d(g0, -a[1]), dd_mul_d(g1, a[0]));
+        const double tau = tg.hi / FD2(a[0], a[0], a[1], a[1]);
+        g[0] = -(a[1] * tau);
+        g[1] = a[0] * tau;
+    } else {
+        g[0] = 0.0;
+        g[1] = 0.0;
+    }
+}
+
+/* r_k back onto its active line after a step (c = 1): the step moves r along the line in exact
+ * arithmetic, but its rounding scales with the step's terms (costates up to 1e10 on the pushed-robot
+ * windows, tests/golden/c5_pushed_windows.npz), and a drift of 1e-10 off the line failed the
+ * certificate's primal check there pass after pass (round 6; the kernels' project_line). */
+static void project_line(dcm_ws* w, int k, const double* a, double b)
+{
+    const double aa = FD2(a[0], a[0], a[1], a[1]);
+    const double t = (FD2(a[0], w->vrp[2 * k], a[1], w->vrp[2 * k + 1]) - b) / aa;
+    w->vrp[2 * k] = fma(-t, a[0], w->vrp[2 * k]);
+    w->vrp[2 * k + 1] = fma(-t, a[1], w->vrp[2 * k + 1]);
 }
 
 static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, int max_pass)
 {
     const int N = w->N, M = w->M;
     int ok = 1;
+    double* nuv = (double*)malloc(sizeof(double) * 2 * (size_t)N);   /* [N][2] the certified costates */
     int* pc = (int*)malloc(sizeof(int) * 4 * (size_t)N);
     int* pi1 = pc + N;
     int* pi2 = pc + 2 * N;
@@ -1705,6 +1833,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
         w->vrp[2 * k + 1] = w->vrp[2 * k + 1] + w->dr[2 * k + 1];
         w->xi[2 * (k + 1)] = w->xi[2 * (k + 1)] + w->x[2 * (k + 1)];
         w->xi[2 * (k + 1) + 1] = w->xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
+        if (pc[k] == 1) project_line(w, k, w->A + (k * M + pi1[k]) * 2, w->b[k * M + pi1[k]]);
     }
     /* 6. certificate: primal feasibility, stationarity, dual feasibility (knot-parallel).  The
      *    costates of the new point are the value-function gradients of the Riccati solve,
@@ -1717,6 +1846,8 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
         const double s1 = w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1];
         const double nu0 = FD3(P00, dx0, P01, dx1, s0);
         const double nu1 = FD3(P01, dx0, P11, dx1, s1);
+        nuv[2 * k] = nu0;
+        nuv[2 * k + 1] = nu1;
         const double rh0 = w->Rw0 * (w->vrp[2 * k] - w->vrp_ref[2 * k]);
         const double rh1 = w->Rw1 * (w->vrp[2 * k + 1] - w->vrp_ref[2 * k + 1]);
         const double g0 = fma(w->be[k], nu0, -rh0);
@@ -1796,7 +1927,23 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
     if (!ok) {
         memcpy(w->vrp, bak, sizeof(double) * 2 * N);
         memcpy(w->xi, bak + 2 * N, sizeof(double) * (2 * (size_t)N + 2));
-    } else {   /* the multipliers of the certified optimum: lam of the active facets, 0 elsewhere */
+    } else {
+        /* the refinement step (refine_rhs) where the largest multiplier exceeds ORC_REFINE_LAM */
+        double lmx = 0.0;
+        for (int k = 0; k < 2 * N; ++k) lmx = keepmax(lmx, lm[k]);
+        if (lmx > ORC_REFINE_LAM) {
+            for (int k = 0; k < N; ++k)
+                refine_rhs(w, k, pc[k], w->A + (k * M + pi1[k]) * 2, nuv, w->d + 2 * k, w->qx + 2 * k, w->g + 2 * k);
+            dcm_solve(w);
+            for (int k = 0; k < N; ++k) {
+                w->vrp[2 * k] = w->vrp[2 * k] + w->dr[2 * k];
+                w->vrp[2 * k + 1] = w->vrp[2 * k + 1] + w->dr[2 * k + 1];
+                w->xi[2 * (k + 1)] = w->xi[2 * (k + 1)] + w->x[2 * (k + 1)];
+                w->xi[2 * (k + 1) + 1] = w->xi[2 * (k + 1) + 1] + w->x[2 * (k + 1) + 1];
+                if (pc[k] == 1) project_line(w, k, w->A + (k * M + pi1[k]) * 2, w->b[k * M + pi1[k]]);
+            }
+        }
+        /* the multipliers of the certified optimum: lam of the active facets, 0 elsewhere */
         for (int k = 0; k < N; ++k)
             for (int i = 0; i < w->nf[k]; ++i)
                 w->lam[k * MF + i] = (pc[k] >= 1 && i == pi1[k]) ? lm[2 * k]
@@ -1805,6 +1952,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
     free(pc);
     free(bak);
     free(add);
+    free(nuv);
     return ok;
 }
 
@@ -2227,10 +2375,15 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
      * start computes them, and each step updates them from sums gathered with the step-length
      * maxima (mu: the exact quadratic in the step length; pres, dres: the linear residuals of an
      * exact Newton step contract by (1 - a)) */
+    double last_a = 1.0;   /* the previous step length (the stalled-step polish) */
     for (it = 0;; ++it) {
         if (it > 0) dcm_residuals(w, 1);   /* the iterate's gradient, defects, Q (xi - xi_ref) */
         if (!(mu == mu) || !(pres == pres) || !(dres == dres) || isinf(mu)) { status = 2; break; }
-        if (prm->tol_polish > 0.0 && mu <= prm->tol_polish) {
+        /* the polish at mu <= tol_polish, and (round 6) after a stalled step once mu <= ORC_STALL_MU:
+         * on the pushed-robot windows (tests/golden/c5_pushed_windows.npz, multipliers up to 1e9)
+         * the iterates stall at mu ~1e-3 with steps of 1e-8..1e-100 while lam > s already names the
+         * optimal active set */
+        if (prm->tol_polish > 0.0 && (mu <= prm->tol_polish || (last_a < ORC_STALL_STEP && mu <= ORC_STALL_MU))) {
             if (dcm_polish(w, prm->tol_primal, prm->tol_dual, NULL, ORC_GUESS_PASSES)) { polished = 1; status = 0; break; }
             dcm_residuals(w, 1);   /* the iterate's gradient and defects again (the polish reused them) */
         }
@@ -2341,6 +2494,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
 #endif
         dres = dres * (1.0 - a);
         pres = pres * (1.0 - a);
+        last_a = a;
         /* sum (s + a ds)(lam + a dl) = U0 + a T1 + a^2 T2 with T1 = sum (s dl + lam ds) = -sum rc
          * = -(U0 + U2 - ntot sigma mu) for the corrector step */
         if (ntot > 0) {

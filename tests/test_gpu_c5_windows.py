@@ -1,7 +1,8 @@
 """The config-5 windows of uncapturable DCM states on the device (tests/test_c5_windows.py has the
 oracle's certificates): the warm solve the closed loop runs and a cold solve of every window of
-tests/golden/c5_failed_windows_r03.npz (the 68 windows that ended at the iteration cap in round 3)
-and c5_hard_windows.npz (the 128 that need the most interior point iterations now), through the C
+tests/golden/c5_failed_windows_r03.npz (the 68 windows that ended at the iteration cap in round 3),
+c5_hard_windows.npz (the 128 that need the most interior point iterations) and c5_pushed_windows.npz
+(the 100 pushed-robot windows the round-5 solver ended unsolved; round 6), through the C
 ABI, against the oracle bit for bit (status, iterations, xi, VRPs, multipliers), every one
 certified (status 0, polished)."""
 import os
@@ -22,7 +23,7 @@ def _load(name):
     return {k: d[k] for k in KEYS}, d
 
 
-@pytest.mark.parametrize("name", ["c5_failed_windows_r03.npz", "c5_hard_windows.npz"])
+@pytest.mark.parametrize("name", ["c5_failed_windows_r03.npz", "c5_hard_windows.npz", "c5_pushed_windows.npz"])
 def test_c5_windows_warm_bitwise(handle, oracle, name):
     prob, d = _load(name)
     B, N = prob["omega"].shape
@@ -44,7 +45,7 @@ def test_c5_windows_warm_bitwise(handle, oracle, name):
     assert out["polished"].cpu().numpy().all()
 
 
-@pytest.mark.parametrize("name", ["c5_failed_windows_r03.npz", "c5_hard_windows.npz"])
+@pytest.mark.parametrize("name", ["c5_failed_windows_r03.npz", "c5_hard_windows.npz", "c5_pushed_windows.npz"])
 def test_c5_windows_cold_bitwise(handle, oracle, name):
     prob, _ = _load(name)
     dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in prob.items()}
@@ -63,7 +64,8 @@ def test_c5_device_window_r05_bitwise(handle, oracle):
     robot 13356 at period 22 of rank 0's shard, tools/capture_c5_failures.py) whose warm start
     needed 92 interior point iterations -- past the default cap of 50.  The warm kernel's passes do
     not certify it, so it is solved again from a cold start (BLF_WARM_RETRY) and stage 2 starts cold
-    (kPendingCold): 31 iterations.  Device and oracle bit for bit, certified."""
+    (kPendingCold): 31 iterations in round 5, 22 with the round-6 polish rules.  Device and oracle
+    bit for bit, certified."""
     prob, d = _load("c5_device_windows_r05.npz")
     B, N = prob["omega"].shape
     dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in prob.items()}
@@ -76,7 +78,7 @@ def test_c5_device_window_r05_bitwise(handle, oracle):
         prob, vrp_ws=d["vrp_ws"], lam_ws=d["lam_ws"], shift=1, floor=1e-3,
         params=oracle.default_params(N, tol_polish=1e-4, max_iter=100), prev_status=d["prev_status"],
         threads=1, device_batch=16384)
-    assert (st == 0).all() and (it == 31).all()
+    assert (st == 0).all() and (it == 22).all()
     for k, ref in (("status", st), ("iters", it), ("xi", xi), ("vrp", vrp), ("lam", lam)):
         np.testing.assert_array_equal(out[k].cpu().numpy(), ref, err_msg=k)
     assert out["polished"].cpu().numpy().all()
