@@ -93,6 +93,50 @@ def valu_issue(kernel_ms):
             "source": path}
 
 
+FP64_PEAK_TFLOPS = 78.6   # MI355X vector fp64 (MI355X_MICROARCH.md)
+
+
+def fbd_sq_summary():
+    """The newest committed SQ summary of fbd_euler_kernel (profiles/*_fbd_euler_sq.json, written by
+    tools/sq_summary.py from tools/gpu_sq.sh's passes with SQ_EXTRA=1) recorded on the library this
+    process loaded; (None, None) without a match."""
+    import glob
+    import re
+    from blf import native
+    lib_hash = native.build_provenance().get("lib_src_hash")
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_fbd_euler_sq.json")),
+                   key=lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))])
+    for path in reversed(files):
+        with open(path) as f:
+            s = json.load(f)
+        if lib_hash and (s.get("build") or {}).get("lib_src_hash") == lib_hash:
+            return s, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def fbd_roofline(kernel_ms, robots_per_launch):
+    """configs[4]'s dominant kernel, fbd_euler_kernel (one control period of the dynamics of a group
+    of robots per launch): fp64 FLOP/s against the vector fp64 peak.  flops per launch = the executed
+    fp64 lanes of the hash-matched SQ pass, 64 x (2 FMA + MUL + ADD) wave-instructions (FMA counted
+    twice; transcendental and conversion instructions not counted); kernel_ms = the launches' mean
+    duration from HIP events on their own streams in the timed region."""
+    s, path = fbd_sq_summary()
+    med = s["median_per_dispatch"] if s else None
+    flops = None
+    if med and "SQ_INSTS_VALU_FMA_F64" in med:
+        flops = 64.0 * (2.0 * med["SQ_INSTS_VALU_FMA_F64"] + med["SQ_INSTS_VALU_MUL_F64"]
+                        + med["SQ_INSTS_VALU_ADD_F64"])
+    achieved = flops / (kernel_ms * 1e-3) / 1e12 if flops else None
+    wc = med.get("SQ_WAVE_CYCLES") if med else None
+    return {"bound": "fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS if achieved else None, "traffic": None,
+            "kernel": "fbd_euler_kernel (one period: 19 ForwardEuler steps of the 30-DoF dynamics)",
+            "kernel_ms": kernel_ms, "robots_per_launch": robots_per_launch,
+            "fp64_flops_per_launch": flops,
+            "wait_inst_lds_frac": (med["SQ_WAIT_INST_LDS"] / wc) if med and wc and "SQ_WAIT_INST_LDS" in med else None,
+            "traffic_source": path}
+
+
 def cpu_baseline(host, N, seconds, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -503,6 +547,9 @@ def closed_loop(args):
     for _ in range(args.warmup):
         for lp in loops:
             lp.period()
+    if not on_cpu:   # the dynamics kernel's launches timed on their own streams (roofline below)
+        for lp in loops:
+            lp.dyn_events = []
     sync()
     if world > 1:
         dist.barrier()
@@ -567,6 +614,10 @@ def closed_loop(args):
                            "stream_groups": len(loops)}}
         if on_cpu:
             line["device"] = "CPU rehearsal (BLF_C5_ORACLE=1: oracle/closed_loop.py on every rank)"
+        else:
+            ev = [e for lp in loops for e in lp.dyn_events]
+            kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+            line["roofline"] = fbd_roofline(kernel_ms, B // len(loops))
         if not args.no_cpu:
             line["cpu_baseline"] = closed_loop_cpu(args, model, N)
         emit(line)

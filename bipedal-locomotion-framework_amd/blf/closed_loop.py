@@ -127,6 +127,7 @@ class ClosedLoop:
             cold_after_handover = os.environ.get("BLF_C5_COLD_AFTER_HANDOVER", "1") != "0"
         self.cold_after_handover = cold_after_handover
         self.warm_status = torch.empty((self.B,), dtype=torch.int32, device=dev)
+        self.dyn_events = None   # a list: period() appends (start, end) events of its dynamics launch
 
     def period(self):
         """One control period (stream-ordered; nothing synchronises).  Returns the plan."""
@@ -161,8 +162,17 @@ class ClosedLoop:
         # advances exactly one knot dt per period, in step with the plan (period_final_time); the
         # dynamics are time-invariant, and a fixed interval keeps the step count the same in every
         # period
+        ev = self.dyn_events
+        if ev is not None:   # bench.py: HIP events around the dynamics launch, on this loop's stream
+            import torch
+            st = self.stream if self.stream is not None else torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
         h.fbd_euler_integrate_impedance(self.dm, self.state, self.imp, self.q_ref, 0.0, self.T,
                                         self.dT, contacts=self.contacts, stream=self.stream)
+        if ev is not None:
+            e1.record(st)
+            ev.append((e0, e1))
         self.prev = out
         self.s = s + 1
         return out

@@ -124,6 +124,14 @@ struct LdsRows<float, MF> {
 #ifndef BLF_AS_KEEPIN
 #define BLF_AS_KEEPIN 1
 #endif
+// A/B builds only (the oracle restates the product, 1 / 1): the anti-cycling rule of the fp64
+// passes and the refinement of multiplier-1e4+ optima
+#ifndef BLF_AS_ANTICYCLE
+#define BLF_AS_ANTICYCLE 1
+#endif
+#ifndef BLF_AS_REFINE
+#define BLF_AS_REFINE 1
+#endif
 
 // One facet row (normal, offset) in the scalar type of the pass.
 template <class T>
@@ -734,7 +742,7 @@ __device__ __forceinline__ void as_pass_h(AKnotT<T>& K, const PT<T>& P, const RS
 template <class T, class RS>
 __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const RS& R, int col, int pk,
                                            T dx0, T dx1, T vn0, T vn1, T& l1o, T& l2o, bool& okp, bool& neg,
-                                           bool& viol)
+                                           bool& viol, bool bland, int& ndrop, int& nadd)
 {
     const int cx = opaque(col);
     const int pc = pk & 3, pi1 = (pk >> 2) & 15, pi2 = (pk >> 6) & 15;
@@ -770,8 +778,8 @@ __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const R
     const int dm = (n1 ? 1 << pi1 : 0) | (n2 ? 1 << pi2 : 0);
     if (bad || dm) okp = false;
     if (dm) neg = true;
-    K.drop |= dm;
-    K.add &= ~dm;
+    // Bland mode (the anti-cycling rule): the new sets go to ndrop / nadd, applied by as_passes
+    int dr = K.drop | dm, ad = K.add & ~dm;
     // primal feasibility of every facet, rows read four at a time
     const int km = opaque(K.m);
     int vm = 0;
@@ -792,8 +800,14 @@ __device__ __forceinline__ void as_certify(AKnotT<T>& K, const PT<T>& P, const R
     if (vm) {
         okp = false;
         viol = true;
-        K.add |= vm;
-        K.drop &= ~vm;
+        ad |= vm;
+        dr &= ~vm;
+    }
+    ndrop = dr;
+    nadd = ad;
+    if (!bland) {
+        K.drop = dr;
+        K.add = ad;
     }
 }
 
@@ -822,6 +836,7 @@ __device__ __forceinline__ void as_refine(AKnot (&K)[KPL], const PT<double>& P, 
                                           double xi00, double xi01, const int (&pk)[KPL])
 {
     constexpr int L = KPL - 1;
+    for (int rs = 0; rs < kRefineSteps; ++rs) {
     double xk[KPL][2];
     as_xi_prev<KPL, double>(K, lane, xi00, xi01, xk);
     // the next knot's costate and omega: the lane's next slot, or the next lane's first
@@ -852,12 +867,16 @@ __device__ __forceinline__ void as_refine(AKnot (&K)[KPL], const PT<double>& P, 
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
         if (KPL * lane + j < N) {
+            // the refined point's costates: nu + the step's own (Lagrangian-shifted) costate
+            K[j].rh0 = K[j].rh0 + FD3(K[j].P00, dx[j][0], K[j].P01, dx[j][1], K[j].qx0 + vn[j][0]);
+            K[j].rh1 = K[j].rh1 + FD3(K[j].P01, dx[j][0], K[j].P11, dx[j][1], K[j].qx1 + vn[j][1]);
             K[j].r0 = K[j].r0 + dr[j][0];
             K[j].r1 = K[j].r1 + dr[j][1];
             K[j].x0 = K[j].x0 + dx[j][0];
             K[j].x1 = K[j].x1 + dx[j][1];
             as_project<double>(K[j], R, R.col(j, lane), pk[j]);
         }
+    }
     }
 }
 
@@ -916,8 +935,13 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
     as_xi_prev<KPL, T>(K, lane, xi00, xi01, xk);
     bool certified = false;
     const int lane0 = lane;
+    // the fp64 passes: up to kAsPasses, the last ones under the anti-cycling rule (oracle
+    // dcm_polish anti_cycle: Bland's rule from pass kGuessPasses on); the fp32 search: kGuessPasses
+    constexpr bool kAnti = sizeof(T) == 8 && BLF_AS_ANTICYCLE;
+    constexpr int kMaxPass = kAnti ? kAsPasses : kGuessPasses;
     int pass = 0;
-    for (; pass < kGuessPasses; ++pass) {
+    for (; pass < kMaxPass; ++pass) {
+        const bool bland = kAnti && pass >= kGuessPasses;   // Bland's rule from pass 8 on
         // BLF_AS_OPQLANE: the lane index opaque per pass, so its masks are recomputed inside the
         // pass instead of hoisted out of the loop into SGPRs (which spill)
         int lane = lane0;
@@ -954,6 +978,7 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
         AS_STAMP_ADD(sb + 2, t_h);
         // the Newton step, then the certificate (costates of the new point from the solve)
         bool neg = false, viol = false;
+        int ndr[KPL], nad[KPL];   // the certificate's new drop / add sets (Bland mode: applied below)
         {
             T g[KPL][2], dr[KPL][2], dx[KPL][2], vn[KPL][2];
 #pragma unroll
@@ -968,6 +993,8 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
 #pragma unroll
             for (int j = 0; j < KPL; ++j) {
                 pl[j][0] = pl[j][1] = T(0);
+                ndr[j] = K[j].drop;
+                nad[j] = K[j].add;
                 if (KPL * lane + j < N) {
                     K[j].r0 = K[j].r0 + dr[j][0];
                     K[j].r1 = K[j].r1 + dr[j][1];
@@ -975,7 +1002,7 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
                     K[j].x1 = K[j].x1 + dx[j][1];
                     if constexpr (sizeof(T) == 8) as_project<T>(K[j], R, R.col(j, lane), opaque(pk[j]));
                     as_certify<T>(K[j], P, R, R.col(j, lane), opaque(pk[j]), dx[j][0], dx[j][1], vn[j][0], vn[j][1],
-                                  pl[j][0], pl[j][1], okp, neg, viol);
+                                  pl[j][0], pl[j][1], okp, neg, viol, kAnti && bland, ndr[j], nad[j]);
                 }
             }
             AS_STAMP_ADD(sb + 4, t_c);
@@ -985,6 +1012,29 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
             certified = true;
             AS_STAMP_ADD(sb + 5, t_o);
             break;
+        }
+        if constexpr (kAnti) {
+            if (bland) {   // Bland: one change, at the lowest knot the certificate changed
+                bool ch[KPL];
+#pragma unroll
+                for (int j = 0; j < KPL; ++j) ch[j] = ndr[j] != K[j].drop || nad[j] != K[j].add;
+                bool any = false;
+#pragma unroll
+                for (int j = 0; j < KPL; ++j) any = any || ch[j];
+                const unsigned long long bl = __ballot(any);
+                const int ls = bl ? __builtin_ctzll(bl) : -1;
+                bool first = true;   // the lane's lowest changed slot is the one kept (lane ls only)
+#pragma unroll
+                for (int j = 0; j < KPL; ++j) {
+                    const bool star = lane == ls && ch[j] && first;
+                    if (ch[j]) first = false;
+                    const int sd = K[j].drop, sa = K[j].add;
+                    const int dn = ndr[j] & ~sd, an = nad[j] & ~sa;
+                    const int bt = dn ? (dn & -dn) : (an & -an);
+                    K[j].drop = star ? (dn ? (sd | bt) : (sd & ~bt)) : sd;
+                    K[j].add = star ? (dn ? (sa & ~bt) : (sa | bt)) : sa;
+                }
+            }
         }
         const bool more = __ballot(neg || viol) != 0;
 #pragma unroll
@@ -1003,13 +1053,14 @@ __device__ __forceinline__ bool as_passes(AKnotT<T> (&K)[KPL], const PT<T>& P, c
             if (ch <= handover) break;
         }
     }
-    npass = pass < kGuessPasses ? pass + 1 : kGuessPasses;   // the passes run (wave-uniform)
+    npass = pass < kMaxPass ? pass + 1 : kMaxPass;   // the passes run (wave-uniform)
     if constexpr (sizeof(T) == 8) {
         // the refinement where the largest multiplier exceeds kRefineLam (oracle ORC_REFINE_LAM)
         bool big = false;
 #pragma unroll
         for (int j = 0; j < KPL; ++j) big = big || pl[j][0] > kRefineLam || pl[j][1] > kRefineLam;
-        if (certified && __ballot(big) != 0) as_refine<KPL, TR>(K, P, R, N, lane0, xi00, xi01, pk);
+        if (BLF_AS_REFINE && certified && __ballot(big) != 0)
+            as_refine<KPL, TR>(K, P, R, N, lane0, xi00, xi01, pk);
     }
     return certified;
 }

@@ -1311,38 +1311,49 @@ __device__ __forceinline__ void ipm_solve(
                     const double lq = R.keepmax(own ? keepmax(keepmax(0.0, pl1), pl2) : 0.0);
                     if (lq > kRefineLam) {
                         // xi_{64 wv} after the polish step (the previous wavefront's last lane did the same)
-                        const double xr0 = wv > 0 ? xb0 + K.d0 : xb0, xr1 = wv > 0 ? xb1 + K.d1 : xb1;
-                        const double nu0 = K.rh0, nu1 = K.rh1;
-                        double xk0r, xk1r;
-                        xi_prev(K, lane, xr0, xr1, xk0r, xk1r);
-                        // the next knot's costate and omega: the next lane's, across a wavefront from LDS
-                        if (lane == 0 && wv > 0) {
-                            bnd[kBnd * wv + kBN] = nu0;
-                            bnd[kBnd * wv + kBN + 1] = nu1;
-                            bnd[kBnd * wv + kBN + 2] = K.w;
-                        }
-                        if constexpr (NW > 1) __syncthreads();
-                        double nn0 = dpp1<kNextWrap>(nu0), nn1 = dpp1<kNextWrap>(nu1), wn = dpp1<kNextWrap>(K.w);
-                        if (NW > 1 && lane == kWave - 1 && wv < nwa - 1) {
-                            nn0 = bnd[kBnd * (wv + 1) + kBN];
-                            nn1 = bnd[kBnd * (wv + 1) + kBN + 1];
-                            wn = bnd[kBnd * (wv + 1) + kBN + 2];
-                        }
-                        double g0 = 0.0, g1 = 0.0;
-                        if (own) {
-                            const double2 a = L.A2[pi1 * N + opaque(k)];
-                            refine_rhs(xk0r, xk1r, K.x0, K.x1, K.r0, K.r1, rref[0], rref[1], xref[0], xref[1], K.w, wn,
-                                       nu0, nu1, nn0, nn1, last, P.dt, last ? P.Pw0 : P.Qw0, last ? P.Pw1 : P.Qw1,
-                                       P.Rw0, P.Rw1, pc, a.x, a.y, K.d0, K.d1, K.qx0, K.qx1, g0, g1);
-                        }
-                        double dr0, dr1, dx0, dx1, vn0, vn1, ek0, ek1;
-                        solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1, ek0, ek1);
-                        if (own) {
-                            K.r0 = K.r0 + dr0;
-                            K.r1 = K.r1 + dr1;
-                            K.x0 = K.x0 + dx0;
-                            K.x1 = K.x1 + dx1;
-                            if (pc == 1) project_line(K, L.A2[pi1 * N + opaque(k)], L.BI[pi1 * N + opaque(k)].x);
+                        double xr0 = wv > 0 ? xb0 + K.d0 : xb0, xr1 = wv > 0 ? xb1 + K.d1 : xb1;
+                        for (int rs = 0; rs < kRefineSteps; ++rs) {
+                            const double nu0 = K.rh0, nu1 = K.rh1;
+                            double xk0r, xk1r;
+                            xi_prev(K, lane, xr0, xr1, xk0r, xk1r);
+                            // the next knot's costate and omega: the next lane's, across a wavefront from LDS
+                            if (lane == 0 && wv > 0) {
+                                bnd[kBnd * wv + kBN] = nu0;
+                                bnd[kBnd * wv + kBN + 1] = nu1;
+                                bnd[kBnd * wv + kBN + 2] = K.w;
+                            }
+                            if constexpr (NW > 1) __syncthreads();
+                            double nn0 = dpp1<kNextWrap>(nu0), nn1 = dpp1<kNextWrap>(nu1), wn = dpp1<kNextWrap>(K.w);
+                            if (NW > 1 && lane == kWave - 1 && wv < nwa - 1) {
+                                nn0 = bnd[kBnd * (wv + 1) + kBN];
+                                nn1 = bnd[kBnd * (wv + 1) + kBN + 1];
+                                wn = bnd[kBnd * (wv + 1) + kBN + 2];
+                            }
+                            double g0 = 0.0, g1 = 0.0;
+                            if (own) {
+                                const double2 a = L.A2[pi1 * N + opaque(k)];
+                                refine_rhs(xk0r, xk1r, K.x0, K.x1, K.r0, K.r1, rref[0], rref[1], xref[0], xref[1], K.w,
+                                           wn, nu0, nu1, nn0, nn1, last, P.dt, last ? P.Pw0 : P.Qw0,
+                                           last ? P.Pw1 : P.Qw1, P.Rw0, P.Rw1, pc, a.x, a.y, K.d0, K.d1, K.qx0,
+                                           K.qx1, g0, g1);
+                            }
+                            double dr0, dr1, dx0, dx1, vn0, vn1, ek0, ek1;
+                            solve<NW>(K, g0, g1, bnd, nwa, wv, lane, own, dr0, dr1, dx0, dx1, vn0, vn1, ek0, ek1);
+                            if (own) {
+                                // the refined point's costates: nu + the step's own (Lagrangian-shifted) costate
+                                K.rh0 = nu0 + FD3(K.P00, dx0, K.P01, dx1, K.qx0 + vn0);
+                                K.rh1 = nu1 + FD3(K.P01, dx0, K.P11, dx1, K.qx1 + vn1);
+                                K.r0 = K.r0 + dr0;
+                                K.r1 = K.r1 + dr1;
+                                K.x0 = K.x0 + dx0;
+                                K.x1 = K.x1 + dx1;
+                                if (pc == 1) project_line(K, L.A2[pi1 * N + opaque(k)], L.BI[pi1 * N + opaque(k)].x);
+                            }
+                            if (wv > 0) {   // the same update as the previous wavefront's last lane
+                                xr0 = xr0 + ek0;
+                                xr1 = xr1 + ek1;
+                            }
+                            if constexpr (NW > 1) __syncthreads();   // bnd's kBN slots are rewritten next step
                         }
                     }
                     polished = 1;

@@ -9,6 +9,9 @@ namespace blf {
 namespace qp {
 
 constexpr int kGuessPasses = 8;   // active-set start: drop/add passes (oracle: ORC_GUESS_PASSES)
+constexpr int kAsPasses = 12;     // the active-set kernels' fp64 passes, anti-cycling (oracle: ORC_AS_PASSES)
+
+
 constexpr int kPending = -1;      // status of a QP the active-set kernel hands to the IPM kernel
 constexpr int kPendingCold = -2;  // handed over by the warm kernel after its cold re-solve: stage 2 starts cold
 
@@ -66,6 +69,7 @@ constexpr double kLamRelCross = 0.3;
 constexpr double kStallStep = 0.2;
 constexpr double kStallMu = 1.0;
 constexpr double kRefineLam = 1e4;
+constexpr int kRefineSteps = 2;   // oracle ORC_REFINE_STEPS
 
 // ---- double-double arithmetic of the refinement (exact TwoSum / TwoProd by fma; the oracle's
 //      dd_* restate these operation for operation) ----

@@ -623,6 +623,10 @@ double orc_wave_tree_sum(const double* c, int n)
 #define ORC_STALL_STEP 0.2
 #define ORC_STALL_MU 1.0
 #define ORC_REFINE_LAM 1e4
+#define ORC_REFINE_STEPS 2   /* refinement steps (kernel kRefineSteps) */
+/* round 6: the active-set kernels' fp64 passes (the cold kernel's phase B and the warm kernel) run
+ * up to ORC_AS_PASSES drop/add passes under the anti-cycling rule of dcm_polish (kernel kAsPasses) */
+#define ORC_AS_PASSES 12
 #define WV 64
 
 /* Fused forms, used in exactly the places the kernel uses them (csrc/dcm_mpc_ipm.hip):
@@ -1595,7 +1599,7 @@ static int cand_bit(const dcm_ws* w, const int* guess, const int* drop, const in
  * Where the multipliers reach 1e6-1e9 (uncapturable DCM states, tests/golden/c5_*_windows.npz)
  * the costates are ~1e8-1e10 and a fp64 solve determines the VRPs only to ~1e-14 x the largest
  * multiplier: the step's own right-hand side (q_k = Q (xi - xi_ref), the costate scan) rounds at
- * that scale.  The refinement takes ONE more Newton step of the same equality-constrained QP with
+ * that scale.  The refinement takes ORC_REFINE_STEPS (2) more Newton steps of the same equality-constrained QP with
  * the same factorization, written in the Lagrangian-shifted form: with the certified costates nu
  * (nu_k = the costate of xi_{k+1}),
  *   d_k  = xi_k + dt (om_k xi_k - om_k r_k) - xi_{k+1}                    (the Euler defect)
@@ -1700,7 +1704,18 @@ static void project_line(dcm_ws* w, int k, const double* a, double b)
     w->vrp[2 * k + 1] = fma(-t, a[1], w->vrp[2 * k + 1]);
 }
 
-static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, int max_pass)
+/* The anti-cycling rule of the active-set kernels' fp64 passes (anti_cycle = 1; round 6).  The
+ * drop/add moves change every knot at once, and on degenerate vertices of three-contact polygons
+ * they cycle: e.g. knot 0 on the vertex of facets 1 and 2 with multipliers -150 / 150, facet 1
+ * dropped, then facet 2, then both added back (bench.py --workload mc: 3 of 4096 cold windows
+ * went to the interior point method after 8 passes, 0.45 of the window's 0.57 ms).  From pass
+ * ORC_GUESS_PASSES (8) on, up to ORC_AS_PASSES (12), every pass changes ONE facet: at the lowest
+ * knot whose sets the certificate changed, the lowest-index facet it dropped (negative
+ * multiplier), else the lowest-index facet it added (violated) -- Bland's rule, which cannot
+ * cycle the way the simultaneous moves do.  (A hash of the passes' candidate sets that switched
+ * on repetition certified the same windows, cost the kernel's pass loop 1.5 % on configs[1]
+ * and is not kept.) */
+static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, int max_pass, int anti_cycle)
 {
     const int N = w->N, M = w->M;
     int ok = 1;
@@ -1721,9 +1736,14 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
      * (Until round 3 the IPM's polish ran at most three passes: pass 1 only dropping, pass 2 only
      * adding; the uncapturable-state windows of tests/golden/c5_hard_windows.npz need the
      * alternating moves of the active-set start there too.) */
+    int* sdr = (int*)malloc(sizeof(int) * 2 * (size_t)N);   /* drop / add before the certificate */
+    int* sad = sdr + N;
     for (int pass = 0; pass < max_pass; ++pass) {
     ++w->npass;
     ok = 1;
+    const int bland = anti_cycle && pass >= ORC_GUESS_PASSES;   /* Bland's rule from pass 8 on */
+    memcpy(sdr, drop, sizeof(int) * N);
+    memcpy(sad, add, sizeof(int) * N);
     int neg = 0, viol = 0;
     double vmax = 0.0;   /* the pass's largest violation (the IPM polish's add threshold) */
     /* 1. active sets, projection onto the active lines, E_k (knot-parallel) */
@@ -1919,6 +1939,19 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
             }
         }
     }
+    if (bland && !ok) {   /* Bland: one change, at the lowest knot the certificate changed */
+        int ks = -1;
+        for (int k = 0; k < N && ks < 0; ++k)
+            if (drop[k] != sdr[k] || add[k] != sad[k]) ks = k;
+        for (int k = 0; k < N; ++k)
+            if (k != ks) { drop[k] = sdr[k]; add[k] = sad[k]; }
+        if (ks >= 0) {
+            const int dn = drop[ks] & ~sdr[ks], an = add[ks] & ~sad[ks];
+            const int bt = dn ? (dn & -dn) : (an & -an);
+            drop[ks] = dn ? (sdr[ks] | bt) : (sdr[ks] & ~bt);
+            add[ks] = dn ? (sad[ks] & ~bt) : (sad[ks] | bt);
+        }
+    }
     if (ok) break;
     if (!(neg || viol)) break;
     memcpy(w->vrp, bak, sizeof(double) * 2 * N);   /* pass 1 starts from the same iterate */
@@ -1931,11 +1964,16 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
         /* the refinement step (refine_rhs) where the largest multiplier exceeds ORC_REFINE_LAM */
         double lmx = 0.0;
         for (int k = 0; k < 2 * N; ++k) lmx = keepmax(lmx, lm[k]);
-        if (lmx > ORC_REFINE_LAM) {
+        for (int rs = 0; rs < ORC_REFINE_STEPS && lmx > ORC_REFINE_LAM; ++rs) {
             for (int k = 0; k < N; ++k)
                 refine_rhs(w, k, pc[k], w->A + (k * M + pi1[k]) * 2, nuv, w->d + 2 * k, w->qx + 2 * k, w->g + 2 * k);
             dcm_solve(w);
             for (int k = 0; k < N; ++k) {
+                /* the costates of the refined point: nu + the step's own (Lagrangian-shifted) costate */
+                const double P00 = w->Pn[3 * k], P01 = w->Pn[3 * k + 1], P11 = w->Pn[3 * k + 2];
+                const double dx0 = w->x[2 * (k + 1)], dx1 = w->x[2 * (k + 1) + 1];
+                nuv[2 * k] = nuv[2 * k] + FD3(P00, dx0, P01, dx1, w->qx[2 * k] + w->v[2 * (k + 1)]);
+                nuv[2 * k + 1] = nuv[2 * k + 1] + FD3(P01, dx0, P11, dx1, w->qx[2 * k + 1] + w->v[2 * (k + 1) + 1]);
                 w->vrp[2 * k] = w->vrp[2 * k] + w->dr[2 * k];
                 w->vrp[2 * k + 1] = w->vrp[2 * k + 1] + w->dr[2 * k + 1];
                 w->xi[2 * (k + 1)] = w->xi[2 * (k + 1)] + w->x[2 * (k + 1)];
@@ -1953,6 +1991,7 @@ static int dcm_polish(dcm_ws* w, double tol_p, double tol_dd, const int* guess, 
     free(bak);
     free(add);
     free(nuv);
+    free(sdr);
     return ok;
 }
 
@@ -2254,7 +2293,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
             }
             g32[k] = gk;
         }
-        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, g32, ORC_GUESS_PASSES);
+        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, g32, ORC_AS_PASSES, 1);
         as_passes = np32 + w->npass;
         free(r32);
         free(g32);
@@ -2303,7 +2342,8 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
                 if (ws && warm->lambda[(k + warm->shift) * M + i] > warm->floor) gm[k] |= 1 << i;
             }
         }
-        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, ORC_GUESS_PASSES);
+        const int okg = dcm_polish(w, prm->tol_primal, prm->tol_dual, gm, as_kernel ? ORC_AS_PASSES : ORC_GUESS_PASSES,
+                                   as_kernel);
         if (as_kernel) as_passes = w->npass;   /* the warm kernel's passes */
         free(gm);
         if (okg) { polished = 1; status = 0; it = 0; goto done; }
@@ -2384,7 +2424,7 @@ int orc_dcm_mpc_solve_warm(const orc_dcm_params* prm, const double* xi_init, con
          * the iterates stall at mu ~1e-3 with steps of 1e-8..1e-100 while lam > s already names the
          * optimal active set */
         if (prm->tol_polish > 0.0 && (mu <= prm->tol_polish || (last_a < ORC_STALL_STEP && mu <= ORC_STALL_MU))) {
-            if (dcm_polish(w, prm->tol_primal, prm->tol_dual, NULL, ORC_GUESS_PASSES)) { polished = 1; status = 0; break; }
+            if (dcm_polish(w, prm->tol_primal, prm->tol_dual, NULL, ORC_GUESS_PASSES, 0)) { polished = 1; status = 0; break; }
             dcm_residuals(w, 1);   /* the iterate's gradient and defects again (the polish reused them) */
         }
         if (mu <= prm->tol_mu && pres <= prm->tol_primal && dres <= prm->tol_dual) { status = 0; break; }

@@ -337,3 +337,23 @@ def test_dcm_mpc_active_set_kernel_and_single_kernel(handle, oracle, horizon, fo
     assert (res["0"]["status"] == 0).all()
     assert np.abs(res["0"]["xi"] - res["1"]["xi"]).max() <= 1e-12
     assert np.abs(res["0"]["vrp"] - res["1"]["vrp"]).max() <= 1e-12
+
+
+def test_bench_batch_bitwise(handle, oracle):
+    """The bench's own configs[1] launch (bench.py: 4096 QPs, horizon 100, 6-footstep plans of seed
+    P.SEED, support polygons assembled on the device): every one of the 4096 solves bit for bit
+    against the oracle evaluated for that launch size, all certified, passes included."""
+    B = 4096
+    prob = P.make_batch(B, horizon=100, n_footsteps=6, seed=P.SEED)
+    dev = _gpu_problem(handle, prob)
+    host = dict(prob)
+    for k in ("A", "b", "nfacets"):
+        host[k] = dev[k].cpu().numpy()
+    out = handle.dcm_mpc_solve(dev)
+    torch.cuda.synchronize()
+    pol, pas = np.zeros(B, np.int32), np.zeros(B, np.int32)
+    st, xi, vrp, it, _ = oracle.dcm_mpc_solve_batch_warm(host, threads=8, polished=pol, passes=pas,
+                                                         device_batch=B)
+    assert (st == 0).all() and pol.all()
+    for k, ref in (("status", st), ("iters", it), ("polished", pol), ("passes", pas), ("xi", xi), ("vrp", vrp)):
+        np.testing.assert_array_equal(out[k].cpu().numpy(), ref, err_msg=k)
