@@ -357,3 +357,47 @@ def test_bench_batch_bitwise(handle, oracle):
     assert (st == 0).all() and pol.all()
     for k, ref in (("status", st), ("iters", it), ("polished", pol), ("passes", pas), ("xi", xi), ("vrp", vrp)):
         np.testing.assert_array_equal(out[k].cpu().numpy(), ref, err_msg=k)
+
+
+def _handover_batch(oracle, B, horizon, seed):
+    """Half the QPs with duplicated facet rows (the polish refuses them: stage 2 solves them)."""
+    prob = oracle.assemble_constraints(P.make_batch(B, horizon=horizon, n_footsteps=4, seed=seed))
+    for q in range(0, B, 2):
+        for k in range(horizon):
+            m = prob["nfacets"][q, k]
+            c = min(2, 8 - m)
+            prob["A"][q, k, m:m + c] = prob["A"][q, k, 0]
+            prob["b"][q, k, m:m + c] = prob["b"][q, k, 0]
+            prob["nfacets"][q, k] = m + c
+    return prob
+
+
+def test_stage2_list_across_launch_kinds(handle, oracle):
+    """The stream's stage-2 list (Handle::stage2_list) through a sequence of solves that take
+    every route over it: the cold kernel + IPM list kernel, the fused small-batch kernel (list
+    untouched), the warm kernel + IPM list kernel, with fuse_stage2 on and off.  Each solve hands
+    QPs over; each equals the oracle bit for bit, so no solve sees a stale count or entry."""
+    big = _handover_batch(oracle, 96, 100, 91)
+    small = _handover_batch(oracle, 8, 40, 92)
+    dbig, dsmall = _to_dev(big), _to_dev(small)
+
+    def check(out, host, **kw):
+        torch.cuda.synchronize()
+        pol = np.zeros(host["xi_init"].shape[0], np.int32)
+        st, xi, vrp, it, lam = oracle.dcm_mpc_solve_batch_warm(host, threads=8, polished=pol, **kw)
+        assert not pol.all()   # QPs were handed over
+        for k, ref in (("status", st), ("iters", it), ("polished", pol), ("xi", xi), ("vrp", vrp), ("lam", lam)):
+            np.testing.assert_array_equal(out[k].cpu().numpy(), ref, err_msg=k)
+        return out
+
+    try:
+        for fuse in (1, 1, 0, 1):
+            native.set_qp_launch_mode(fuse_stage2=fuse)
+            cold = check(handle.dcm_mpc_solve(dbig, lambda_out=True), big)
+            check(handle.dcm_mpc_solve(dsmall, lambda_out=True), small)
+            v, l = cold["vrp"].cpu().numpy().copy(), cold["lam"].cpu().numpy().copy()
+            warm = dict(vrp=cold["vrp"], lam=cold["lam"], shift=1, floor=1e-3)
+            check(handle.dcm_mpc_solve(dbig, warm=warm, lambda_out=True), big, vrp_ws=v, lam_ws=l, shift=1,
+                  floor=1e-3)
+    finally:
+        native.set_qp_launch_mode(fuse_stage2=1)
