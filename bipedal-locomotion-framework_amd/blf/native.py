@@ -759,7 +759,11 @@ class Handle:
                     link_inertia=f64(model["link_inertia"]), frame_link=i32(model["frame_link"]),
                     frame_pose=f64(model["frame_pose"]))
         if model.get("joint_type") is not None:   # absent: every joint revolute (NULL)
-            dm.t["joint_type"] = i32(model["joint_type"])
+            jt = torch.as_tensor(model["joint_type"], dtype=torch.int32)
+            if not ((jt == 0) | (jt == 1)).all():
+                raise ValueError("joint_type: every entry must be 0 (revolute) or 1 (prismatic); merge fixed "
+                                 "joints first (blf.robot.reduce_fixed_joints)")
+            dm.t["joint_type"] = i32(jt)
         c = FbModel()
         c.ndof = int(model["n"])
         c.nframes = int(len(model["frame_link"]))

@@ -397,6 +397,8 @@ __device__ __forceinline__ void fbd_kinematics_levels(const Model& m, const Smem
         const double* E = m.jrot + 9 * j;
         double sn = 0.0, cs = 1.0;   // a prismatic joint does not rotate: E Rot(a, 0) = E exactly
         if (!(PRI && m.jtype[j] == BLF_JOINT_PRISMATIC)) sincos(jp[j], &sn, &cs);
+        if (PRI && m.jtype[j] != BLF_JOINT_PRISMATIC && m.jtype[j] != BLF_JOINT_REVOLUTE)
+            sn = cs = __builtin_nan("");   // an unknown joint type: the robot's outputs are NaN
         const double c1 = 1.0 - cs;
         const double K[9] = {0.0, -a[2], a[1], a[2], 0.0, -a[0], -a[1], a[0], 0.0};
         double Rr[9];
@@ -551,6 +553,8 @@ __device__ __forceinline__ void fbd_kinematics_jump(const Model& m, const Smem& 
         ax[0] = a[0]; ax[1] = a[1]; ax[2] = a[2];
         double sn = 0.0, cs = 1.0;
         if (jl && !pri) sincos(jp[j], &sn, &cs);
+        if (PRI && jl && m.jtype[j] != BLF_JOINT_PRISMATIC && m.jtype[j] != BLF_JOINT_REVOLUTE)
+            sn = cs = __builtin_nan("");   // an unknown joint type: the robot's outputs are NaN
         const double c1 = 1.0 - cs;
         const double K[9] = {0.0, -a[2], a[1], a[2], 0.0, -a[0], -a[1], a[0], 0.0};
         double Rr[9];

@@ -435,8 +435,10 @@ typedef struct blf_fb_model {
     double rho;                   /* Baumgarte parameter of the base rotation rate           */
     const int32_t* joint_type;    /* [n] or NULL (every joint revolute): BLF_JOINT_REVOLUTE /
                                      BLF_JOINT_PRISMATIC (the child link slides along the axis
-                                     by q; URDF "prismatic"); any other value is taken as
-                                     revolute.  Fixed joints carry no DoF: merge
+                                     by q; URDF "prismatic"); any other value makes every
+                                     output of every robot NaN (the wrappers refuse it up
+                                     front: the C++ adapter's setRobotModel returns false,
+                                     blf.native raises).  Fixed joints carry no DoF: merge
                                      them into their parent link first (the C++ adapter's
                                      blf::reduceFixedJoints)                                  */
 } blf_fb_model;

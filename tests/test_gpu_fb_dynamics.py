@@ -222,6 +222,31 @@ def test_fbd_prismatic_joints_vs_oracle(handle, HWkind):
             assert rel_err(got[k][i], ref[k]) < TOL, k
 
 
+def test_fbd_unknown_joint_type(handle):
+    """An unknown blf_fb_model.joint_type is never taken as revolute.  The Python wrapper refuses it
+    (ValueError); through the C ABI (the device array overwritten in place) every output of every
+    robot is NaN, in the dynamics and in the Euler integration."""
+    model = robot.with_joint_types(MODEL, prismatic=PRISMATIC)
+    bad = dict(model)
+    bad["joint_type"] = np.array(model["joint_type"]).copy()
+    bad["joint_type"][3] = 7
+    with pytest.raises(ValueError):
+        handle.fb_model(bad)
+    B = 8
+    st = robot.random_states(model, B, seed=19)
+    host, dev = contacts_for(B, seed=4)
+    dm = handle.fb_model(model)
+    dm.t["joint_type"][3] = 7   # what a C caller could pass
+    out = handle.fbd_dynamics(dm, {k: _d(st[k]) for k in native.FB_STATE_KEYS}, _d(st["joint_torque"]),
+                              contacts=dev)
+    for k in ("base_vel", "joint_vel"):   # the accelerations (the rest of the derivative is the state's)
+        assert torch.isnan(out[k]).all(), k
+    dst = {k: _d(st[k]) for k in native.FB_STATE_KEYS}
+    handle.fbd_euler_integrate(dm, dst, _d(st["joint_torque"]), 0.0, 0.002, 0.001, contacts=dev)
+    for k in ("base_vel", "joint_vel", "base_pos", "base_rot"):
+        assert torch.isnan(dst[k]).all(), k
+
+
 # ---- contact laws (blf_fb_contacts.law): any ContactModel through its wrench --------------------
 def test_fb_frame_state_vs_oracle(handle):
     """blf_fb_frame_state: world transform and mixed twist of the sole frames, the state the
