@@ -1,7 +1,7 @@
 #!/bin/bash
 # Diagnostics: build the working copy of one kernel source (VSRC, default dcm_mpc_ipm; plus extra
 # hipcc flags) into lib/libblf_<name>.so next to the product library, for A/B runs with
-# tools/ab_multi.sh.
+# tools/sessions/ab_multi.sh.
 #   [VSRC=dcm_mpc_as] tools/build_variant.sh <name> [hipcc flags...]
 set -eu
 cd "$(dirname "$0")/../bipedal-locomotion-framework_amd"
