@@ -2,11 +2,63 @@
  * @file ConvexHullHelper.cpp
  * Single-polygon calls into the batched device kernels (batch = 1).
  */
+#include <algorithm>
+#include <cmath>
 #include <iostream>
+#include <utility>
+#include <vector>
 
 #include <BipedalLocomotion/Planners/ConvexHullHelper.h>
 
 using namespace BipedalLocomotion::Planners;
+
+namespace
+{
+// The vertices of one face of a 3-D hull: the input points on the plane a.x = b (within tol),
+// projected onto the plane, then the corners of their planar hull (Andrew's monotone chain,
+// collinear points dropped: Qhull counts them as coplanar points, not vertices).
+int faceVertexCount(const std::vector<double>& pts, std::size_t p, const double* a, double b, double tol)
+{
+    // an orthonormal basis (u, v) of the plane
+    double u[3];
+    if (std::abs(a[0]) < 0.9) { u[0] = 0.0; u[1] = a[2]; u[2] = -a[1]; }
+    else { u[0] = -a[2]; u[1] = 0.0; u[2] = a[0]; }
+    const double nu = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    for (double& x : u) x /= nu;
+    const double v[3] = {a[1] * u[2] - a[2] * u[1], a[2] * u[0] - a[0] * u[2], a[0] * u[1] - a[1] * u[0]};
+    std::vector<std::pair<double, double>> q;
+    for (std::size_t j = 0; j < p; ++j)
+    {
+        const double* x = &pts[3 * j];
+        if (std::abs(a[0] * x[0] + a[1] * x[1] + a[2] * x[2] - b) > tol) continue;
+        q.emplace_back(u[0] * x[0] + u[1] * x[1] + u[2] * x[2], v[0] * x[0] + v[1] * x[1] + v[2] * x[2]);
+    }
+    std::sort(q.begin(), q.end());
+    q.erase(std::unique(q.begin(), q.end(),
+                        [tol](const auto& l, const auto& r) {
+                            return std::abs(l.first - r.first) <= tol && std::abs(l.second - r.second) <= tol;
+                        }),
+            q.end());
+    if (q.size() < 3) return static_cast<int>(q.size());
+    auto turn = [](const auto& o, const auto& a1, const auto& b1) {
+        return (a1.first - o.first) * (b1.second - o.second) - (a1.second - o.second) * (b1.first - o.first);
+    };
+    const double eps = tol * tol;
+    std::vector<std::pair<double, double>> h(2 * q.size());
+    std::size_t k = 0;
+    for (std::size_t i = 0; i < q.size(); ++i)   // lower chain
+    {
+        while (k >= 2 && turn(h[k - 2], h[k - 1], q[i]) <= eps) --k;
+        h[k++] = q[i];
+    }
+    for (std::size_t i = q.size() - 1, t = k + 1; i-- > 0;)   // upper chain
+    {
+        while (k >= t && turn(h[k - 2], h[k - 1], q[i]) <= eps) --k;
+        h[k++] = q[i];
+    }
+    return static_cast<int>(k - 1);
+}
+}  // namespace
 
 // 3 x p points (p <= 16): blf_hull3d_hrep (the distinct supporting planes;
 // ConvexHullHelperTest.cpp:15-63).  Any other n x p (n = 1 or n >= 4, or more points than the
@@ -56,13 +108,30 @@ bool ConvexHullHelper::buildConvexHullN(const blf::MatrixXd& points)
         m_b.resize(0);
         return false;
     }
-    m_A.resize(static_cast<std::size_t>(nf), dim);
-    m_b.resize(static_cast<std::size_t>(nf));
-    for (int i = 0; i < nf; ++i)
+    // Rows as the reference's getA() has them in 3-D: Qhull's "Qt" output is one facet per
+    // triangle, so a face with k vertices is k - 2 rows with the same plane
+    // (ConvexHullHelper.cpp:60-86 of the reference: A is sized to facetList.count()).  The device
+    // returns each distinct plane once.  In 4-D and above the count of a facet's simplices depends
+    // on Qhull's triangulation, and each plane stays one row.
+    std::vector<int> copies(static_cast<std::size_t>(nf), 1);
+    if (dim == 3)
     {
-        for (std::size_t c = 0; c < dim; ++c) m_A(i, c) = A[dim * i + c];
-        m_b(i) = b[i];
+        double scale = 1.0;
+        for (const double x : pts) scale = std::max(scale, std::abs(x));
+        for (int i = 0; i < nf; ++i)
+            copies[i] = std::max(1, faceVertexCount(pts, p, &A[3 * i], b[i], 1e-9 * scale) - 2);
     }
+    std::size_t rows = 0;
+    for (const int c : copies) rows += static_cast<std::size_t>(c);
+    m_A.resize(rows, dim);
+    m_b.resize(rows);
+    std::size_t r = 0;
+    for (int i = 0; i < nf; ++i)
+        for (int k = 0; k < copies[i]; ++k, ++r)
+        {
+            for (std::size_t c = 0; c < dim; ++c) m_A(r, c) = A[dim * i + c];
+            m_b(r) = b[i];
+        }
     return true;
 }
 

@@ -554,8 +554,9 @@ static void testConvexHull3()
         REQUIRE(helper.doesPointBelongToConvexHull(blf::VectorXd{p(0, col), p(1, col), p(2, col)}));
     // p = [0 0 0] does not belong to the convex hull
     REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.0, 0.0, 0.0}));
-    // the Qhull fixture's 10 distinct planes (tests/golden/hull3d.json), unit normals
-    REQUIRE(helper.getA().rows() == 10 && helper.getA().cols() == 3);
+    // Qhull's 12 facets (tests/golden/hull3d.json): 10 distinct planes, the two quadrilateral
+    // faces (z = 0.3, z = 0.24) as two triangles each; unit normals
+    REQUIRE(helper.getA().rows() == 12 && helper.getA().cols() == 3);
     for (std::size_t i = 0; i < helper.getA().rows(); ++i)
     {
         const double n2 = helper.getA()(i, 0) * helper.getA()(i, 0) +
@@ -564,6 +565,26 @@ static void testConvexHull3()
         REQUIRE(std::abs(n2 - 1.0) < 1e-12);
     }
     REQUIRE_FALSE(helper.doesPointBelongToConvexHull(blf::VectorXd{0.7, 0.6}));   // wrong size
+    // the unit cube: 6 square faces, Qhull's 12 triangles; a tetrahedron: 4; a cube with face
+    // centres and edge midpoints (coplanar points, not vertices): still 12
+    {
+        blf::MatrixXd cube(3, 8);
+        for (int j = 0; j < 8; ++j) { cube(0, j) = j & 1; cube(1, j) = (j >> 1) & 1; cube(2, j) = (j >> 2) & 1; }
+        REQUIRE(helper.buildConvexHull(cube));
+        REQUIRE(helper.getA().rows() == 12);
+        const blf::MatrixXd tet(3, 4, {0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1});
+        REQUIRE(helper.buildConvexHull(tet));
+        REQUIRE(helper.getA().rows() == 4);
+        blf::MatrixXd dense(3, 16);
+        for (int j = 0; j < 8; ++j) { dense(0, j) = j & 1; dense(1, j) = (j >> 1) & 1; dense(2, j) = (j >> 2) & 1; }
+        const double extra[8][3] = {{0.5, 0.5, 0.0}, {0.5, 0.5, 1.0}, {0.5, 0.0, 0.5}, {0.5, 1.0, 0.5},
+                                    {0.0, 0.5, 0.5}, {1.0, 0.5, 0.5}, {0.5, 0.0, 0.0}, {1.0, 1.0, 0.5}};
+        for (int j = 0; j < 8; ++j)
+            for (int r = 0; r < 3; ++r) dense(r, 8 + j) = extra[j][r];
+        REQUIRE(helper.buildConvexHull(dense));
+        REQUIRE(helper.getA().rows() == 12);
+        REQUIRE(helper.buildConvexHull(p));   // back to the reference test's hull
+    }
     // a flat set has no 3-D hull
     blf::MatrixXd flat(3, 4);
     for (int j = 0; j < 4; ++j) { flat(0, j) = j & 1; flat(1, j) = j >> 1; flat(2, j) = 0.5; }
